@@ -1,0 +1,163 @@
+/*
+ * pint_amd.h — C-ABI of libpint_hip.so, the MI355X (gfx950) implementation of PINT's
+ * fit-and-residual hot path.
+ *
+ * The reference (Jackson-D-Taylor/PINT, pure Python) has no FFI; every entry point below
+ * replaces a Python call on the hot path, cited as reference file:line.  Plain pointers
+ * and sizes only: caller-owned host buffers, library-owned device buffers, int status
+ * codes (0 = ok) and pint_last_error() for a message.  One context per host thread; each
+ * context owns one HIP stream on one device.
+ *
+ * Data model (see DESIGN.md "Data layout in HBM"):
+ *   - a *pulsar* is a packed SoA TOA set (N rows + 1 TZR row) plus a ModelSpec
+ *     (structure: which components, column map, table offsets);
+ *   - an *instance* is one parameter table (doubles, every parameter a double-double
+ *     hi/lo pair, in the reference's par-file units) bound to a pulsar.  A batch of
+ *     instances (grid points, PTA pulsars, downhill trial states) is evaluated by one
+ *     launch sequence.
+ */
+#ifndef PINT_AMD_H
+#define PINT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------------- */
+#define PINT_OK 0
+#define PINT_E_INVALID 1      /* bad argument / shape / unsupported model feature    */
+#define PINT_E_HIP 2          /* HIP runtime error                                    */
+#define PINT_E_NOT_PD 3       /* normal matrix not positive definite (LinAlgError)    */
+#define PINT_E_KEPLER 4       /* Kepler iteration did not converge / ECC outside [0,1)*/
+#define PINT_E_PARAM 5        /* invalid model parameter region (InvalidModelParameters)*/
+
+/* ---- limits -------------------------------------------------------------------- */
+#define PINT_MAX_COLS 320     /* design-matrix columns incl. Offset                   */
+#define PINT_MAX_F 16
+#define PINT_MAX_DMK 10
+#define PINT_MAX_FD 10
+#define PINT_MAX_JUMP 64
+
+/* ---- per-TOA packed input (reference TOAs.table columns
+ *      toa.py:2320 tdbld, :2385-2439 posvels, freq, error, mjd_float, pulse_number) ---- */
+typedef struct {
+    int32_t n;                      /* TOAs, excluding the TZR row                      */
+    const double *tdb_hi, *tdb_lo;  /* n+1: exact double-double split of longdouble tdbld (days) */
+    const double *freq_mhz;         /* n+1                                              */
+    const double *sigma_s;          /* n: scaled TOA uncertainty (s), noise_model.py:159 */
+    const double *pos_km;           /* (n+1)*3 ssb_obs_pos (row-major xyz)              */
+    const double *vel_kms;          /* (n+1)*3 ssb_obs_vel                              */
+    const double *sun_km;           /* (n+1)*3 obs_sun_pos                              */
+    const double *pulse_number;     /* n (NaN-free when track_mode=pulse numbers)       */
+    const double *delta_pn;         /* n+1 delta_pulse_number                           */
+    const uint32_t *flags;          /* n+1 bit0: barycentric obs, bit1: all ssb_obs_pos != 0 */
+    const uint64_t *jump_mask;      /* n+1 bit k: JUMP k selects this TOA               */
+    const int32_t *dmx_a, *dmx_b;   /* n+1 DMX bin indices (-1 none; two allow overlap) */
+} pint_toas_t;
+
+/* ---- model structure ------------------------------------------------------------ */
+/* column kinds for the design matrix (timing_model.py:2073 designmatrix)              */
+enum {
+    PINT_COL_OFFSET = 0, PINT_COL_F = 1, PINT_COL_LON = 2, PINT_COL_LAT = 3,
+    PINT_COL_PMLON = 4, PINT_COL_PMLAT = 5, PINT_COL_PX = 6, PINT_COL_DM = 7,
+    PINT_COL_DMX = 8, PINT_COL_FD = 9, PINT_COL_JUMP = 10, PINT_COL_BIN = 11
+};
+/* binary parameter ids (stand_alone_psr_binaries/binary_generic.py, ELL1_model.py, DD_model.py) */
+enum {
+    PINT_B_PB = 0, PINT_B_PBDOT, PINT_B_XPBDOT, PINT_B_A1, PINT_B_A1DOT, PINT_B_ECC,
+    PINT_B_EDOT, PINT_B_T0, PINT_B_OM, PINT_B_OMDOT, PINT_B_M2, PINT_B_SINI, PINT_B_GAMMA,
+    PINT_B_DR, PINT_B_DTH, PINT_B_A0, PINT_B_B0, PINT_B_TASC, PINT_B_EPS1, PINT_B_EPS2,
+    PINT_B_EPS1DOT, PINT_B_EPS2DOT, PINT_B_NPAR
+};
+
+typedef struct {
+    int32_t nf;             /* spin terms F0..F{nf-1}                                   */
+    int32_t astrometry;     /* 0 none, 1 equatorial (RAJ/DECJ), 2 ecliptic (ELONG/ELAT) */
+    int32_t shapiro;        /* SolarSystemShapiro present (sun only)                    */
+    int32_t ndm;            /* DispersionDM taylor terms (0 = component absent)         */
+    int32_t ndmx;           /* DMX bins                                                 */
+    int32_t binary;         /* 0 none, 1 ELL1, 2 DD                                     */
+    int32_t nfd;            /* FD terms                                                 */
+    int32_t njump;          /* phase JUMPs                                              */
+    int32_t track_pn;       /* 1: use_pulse_numbers, 0: nearest  (residuals.py:133-149) */
+    int32_t subtract_mean;  /* residuals.py:124                                         */
+    int32_t weighted_mean;
+    int32_t ncol;           /* design-matrix columns incl. Offset                      */
+    int32_t nred;           /* PLRedNoise modes (2*nred Fourier columns), 0 = none     */
+    int32_t tstride;        /* doubles per instance parameter table                    */
+    /* table offsets (doubles; each parameter is a dd pair at [off], [off+1]); -1 absent */
+    int32_t o_F, o_PEPOCH, o_lon, o_lat, o_pmlon, o_pmlat, o_px, o_POSEPOCH;
+    int32_t o_DM, o_DMEPOCH, o_DMX, o_FD, o_JUMP, o_bin[PINT_B_NPAR];
+    double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
+    double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
+    double red_t0;          /* unused reserve                                           */
+    int32_t col_kind[PINT_MAX_COLS];
+    int32_t col_index[PINT_MAX_COLS];
+    int32_t col_toff[PINT_MAX_COLS];  /* table offset of the column's parameter (-1: Offset) */
+} pint_spec_t;
+
+/* ---- context -------------------------------------------------------------------- */
+typedef struct pint_ctx pint_ctx;
+
+/* One context per host thread; it owns one HIP stream on `device`. */
+pint_ctx *pint_ctx_create(int device);
+void pint_ctx_destroy(pint_ctx *ctx);
+const char *pint_last_error(pint_ctx *ctx);
+int pint_device_count(void);
+
+/* Upload one pulsar (packed TOAs + model structure); returns its id >= 0, or -status.
+ * Replaces the TOAs.table hand-off of get_model_and_toas (model_builder.py:859) and the
+ * param-independent noise bases: red_freq[nred] are the PLRedNoise Fourier frequencies
+ * (noise_model.py:847 get_rednoise_freqs), red_phi[2*nred] their weights
+ * (noise_model.py:780 get_noise_weights).  The library copies everything it needs. */
+int pint_add_pulsar(pint_ctx *ctx, const pint_toas_t *toas, const pint_spec_t *spec,
+                    const double *red_freq, const double *red_phi);
+
+/* Bind `ninst` instances (grid points, PTA pulsars, trial states): inst_psr[k] is a
+ * pulsar id; `tables` concatenates each instance's parameter table (spec.tstride doubles,
+ * dd pairs in par-file units).  Replaces the parameter state of a TimingModel
+ * (parameter.py values) for a whole batch. */
+int pint_set_instances(pint_ctx *ctx, int ninst, const int32_t *inst_psr, const double *tables);
+int pint_get_tables(pint_ctx *ctx, double *tables_out);
+int pint_set_tables(pint_ctx *ctx, const double *tables);
+
+/* Evaluate delay (timing_model.py:1515), phase (:1548, incl. the TZR phase) and, when
+ * want_M, the design matrix (:2073) plus the red-noise basis columns; then residuals
+ * (residuals.py:314 calc_phase_resids, :483 calc_time_resids) and the WLS chi2 (:638)
+ * for every instance. */
+int pint_eval(pint_ctx *ctx, int want_M);
+
+/* Copy results to caller buffers (any pointer may be NULL).  Residual rows are n_i per
+ * instance, eval rows n_i+1 (last = TZR TOA), design matrices n_i x K_i column-major
+ * with K_i = ncol + 2*nred. */
+int pint_read_resids(pint_ctx *ctx, double *time_resid, double *phase_resid, double *chi2_wls);
+int pint_read_eval(pint_ctx *ctx, double *phase_hi, double *phase_lo, double *ftaylor, double *delay);
+int pint_read_designmatrix(pint_ctx *ctx, double *M);
+
+/* One normal-equations step for every instance on the state of the last pint_eval(1):
+ * mode 0 = WLS (fitter.py:1965 WLSFitter / :1282 WLSState.step), mode 1 = GLS
+ * (:2104 GLSFitter / :1425 GLSState.step, rank-reduced, full_cov=False).  The GLS mode
+ * also factors the Woodbury Sigma used by pint_chi2_gls. */
+int pint_fit_step(pint_ctx *ctx, int mode);
+/* dpars/errs: (K_i+1) per instance (par units, [0] = Offset); cov: (K_i+1)^2 per instance
+ * (row-major K_i x K_i at the front); chi2_lin: linearised post-step chi2. */
+int pint_read_step(pint_ctx *ctx, double *dpars, double *errs, double *cov, double *chi2_lin);
+
+/* tables += lambda[k] * dpars (double-double add): fitter.py:957 take_step_model and
+ * :2073-2080 the longdouble parameter update. */
+int pint_apply_step(pint_ctx *ctx, const double *lambda_);
+
+/* GLS chi2 (Woodbury, residuals.py:567 _calc_gls_chi2 + utils.py:3074 woodbury_dot) of
+ * the current residuals, per instance. */
+int pint_chi2_gls(pint_ctx *ctx, double *chi2);
+
+/* Device time (ms, HIP events) of the last eval / resid / gram / solve launches. */
+int pint_last_timing(pint_ctx *ctx, double *ms4);
+int pint_sync(pint_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,90 @@
+"""ctypes binding of libpint_hip.so (the C-ABI declared in include/pint_amd.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is visible, every
+compute call raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "libpint_hip.so")
+
+MAX_COLS = 320
+B_NPAR = 22
+
+COL_OFFSET, COL_F, COL_LON, COL_LAT, COL_PMLON, COL_PMLAT, COL_PX, COL_DM, COL_DMX, COL_FD, COL_JUMP, COL_BIN = range(12)
+
+PINT_OK, PINT_E_INVALID, PINT_E_HIP, PINT_E_NOT_PD, PINT_E_KEPLER, PINT_E_PARAM = range(6)
+
+dptr = C.POINTER(C.c_double)
+
+
+class ToasT(C.Structure):
+    _fields_ = [("n", C.c_int32), ("tdb_hi", dptr), ("tdb_lo", dptr), ("freq_mhz", dptr), ("sigma_s", dptr),
+                ("pos_km", dptr), ("vel_kms", dptr), ("sun_km", dptr), ("pulse_number", dptr), ("delta_pn", dptr),
+                ("flags", C.POINTER(C.c_uint32)), ("jump_mask", C.POINTER(C.c_uint64)),
+                ("dmx_a", C.POINTER(C.c_int32)), ("dmx_b", C.POINTER(C.c_int32))]
+
+
+class SpecT(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("nf", "astrometry", "shapiro", "ndm", "ndmx", "binary", "nfd", "njump",
+                                          "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
+                                          "o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px",
+                                          "o_POSEPOCH", "o_DM", "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP")] + [
+        ("o_bin", C.c_int32 * B_NPAR), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
+        ("col_kind", C.c_int32 * MAX_COLS), ("col_index", C.c_int32 * MAX_COLS), ("col_toff", C.c_int32 * MAX_COLS)]
+
+
+class PintError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[pint_hip status {code}] {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libpint_hip.so (build with ``python -c 'import __graft_entry__ as g; g.build()'``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIBPATH):
+        raise RuntimeError(f"HIP extension missing: {LIBPATH} (run __graft_entry__.build())")
+    L = C.CDLL(LIBPATH)
+    vp = C.c_void_p
+    L.pint_ctx_create.restype = vp
+    L.pint_ctx_create.argtypes = [C.c_int]
+    L.pint_ctx_destroy.argtypes = [vp]
+    L.pint_last_error.restype = C.c_char_p
+    L.pint_last_error.argtypes = [vp]
+    L.pint_device_count.restype = C.c_int
+    L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
+    L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
+    for fn in ("pint_get_tables", "pint_set_tables", "pint_read_designmatrix", "pint_chi2_gls", "pint_last_timing"):
+        getattr(L, fn).argtypes = [vp, dptr]
+    L.pint_eval.argtypes = [vp, C.c_int]
+    L.pint_fit_step.argtypes = [vp, C.c_int]
+    L.pint_read_resids.argtypes = [vp, dptr, dptr, dptr]
+    L.pint_read_eval.argtypes = [vp, dptr, dptr, dptr, dptr]
+    L.pint_read_step.argtypes = [vp, dptr, dptr, dptr, dptr]
+    L.pint_apply_step.argtypes = [vp, dptr]
+    L.pint_sync.argtypes = [vp]
+    _lib = L
+    return L
+
+
+EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_device_count", "pint_add_pulsar",
+            "pint_set_instances", "pint_get_tables", "pint_set_tables", "pint_eval", "pint_read_resids",
+            "pint_read_eval", "pint_read_designmatrix", "pint_fit_step", "pint_read_step", "pint_apply_step",
+            "pint_chi2_gls", "pint_last_timing", "pint_sync"]
+
+
+def ptr(a: np.ndarray, ct=C.c_double):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ct))

@@ -1,0 +1,734 @@
+// physics.hpp — per-TOA timing-model evaluation for gfx950: delays, pulse phase (dd) and
+// every design-matrix column, restated from the reference formulas (cited per function).
+// One thread evaluates one TOA; parameters are wave-uniform (scalar loads).
+#pragma once
+#include "dd.hpp"
+#include "../../include/pint_amd.h"
+
+namespace pint {
+
+// ---- constants (values as the reference's astropy/erfa constants; see
+//      tests/golden/... constants and pint/__init__.py:67-102) ----------------------------
+constexpr double C_KMS = 299792.458;              // c, km/s
+constexpr double AU_KM = 149597870.7;             // astropy au
+constexpr double KPC_KM = 3.0856775814913674e16;  // 1 kpc in km
+constexpr double TSUN = 4.92549094830932e-06;     // GM_sun/c^3 (s), pint/__init__.py:80
+constexpr double DMCONST = 4149.377593360996;     // 1/2.41e-4 MHz^2 s cm^3/pc, :68
+constexpr double DAYSEC = 86400.0;
+constexpr double DJY = 365.25;
+constexpr double ERFA_DC = 173.1446326742403;     // c in AU/day (erfa DC)
+constexpr double DR2AS = 206264.80624709636;
+constexpr double MAS_RAD = 4.84813681109536e-09;
+constexpr double HA_RAD = 0.2617993877991494;
+constexpr double DEG_RAD = 0.017453292519943295;
+constexpr double MASYR_RADS = 1.5362818500441604e-16;  // (mas/yr) in rad/s
+constexpr double YR_S = 31557600.0;
+constexpr double TWO_PI = 6.283185307179586;
+constexpr double PI_D = 3.141592653589793;
+
+PD double pval(const double* P, int o) { return P[o] + P[o + 1]; }
+PD dd pdd(const double* P, int o) { return dd_make(P[o], P[o + 1]); }
+
+// ------------------------------------------------------------------------------------
+// erfa pmsafe/starpm/starpv restated (SOFA published algorithm; pyerfa 2.0.0 is the
+// reference's third-party call at astrometry.py:513 and astropy apply_space_motion).
+// Returns the unit vector toward the star at epoch offset dt_days (TDB days).
+// ------------------------------------------------------------------------------------
+PD void starpm_dir(double ra, double dec, double pmr, double pmd, double px, double dt_days,
+                   double out[3]) {
+    // pmsafe: override parallax (PXMIN 5e-7 arcsec, F = 326)
+    double a1[3] = {cos(ra) * cos(dec), sin(ra) * cos(dec), sin(dec)};
+    double ra2 = ra + pmr, dec2 = dec + pmd;
+    double b1[3] = {cos(ra2) * cos(dec2), sin(ra2) * cos(dec2), sin(dec2)};
+    double cx = a1[1] * b1[2] - a1[2] * b1[1];
+    double cy = a1[2] * b1[0] - a1[0] * b1[2];
+    double cz = a1[0] * b1[1] - a1[1] * b1[0];
+    double ss = sqrt(cx * cx + cy * cy + cz * cz);
+    double cs = a1[0] * b1[0] + a1[1] * b1[1] + a1[2] * b1[2];
+    double pm = (ss != 0.0 || cs != 0.0) ? atan2(ss, cs) : 0.0;
+    double px1a = px;
+    pm *= 326.0;
+    if (px1a < pm) px1a = pm;
+    if (px1a < 5e-7) px1a = 5e-7;
+    // starpv (rv = 0)
+    double w = px1a >= 1e-7 ? px1a : 1e-7;
+    double r = DR2AS / w;
+    double rad = pmr / DJY, decd = pmd / DJY;
+    double st = sin(ra), ct = cos(ra), sp = sin(dec), cp = cos(dec);
+    double rcp = r * cp;
+    double x = rcp * ct, y = rcp * st;
+    double rpd = r * decd;
+    double ww = rpd * sp;  // - cp*rd with rd = 0
+    double p[3] = {x, y, r * sp};
+    double v[3] = {-y * rad - ww * ct, x * rad - ww * st, rpd * cp};
+    double vm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (vm / ERFA_DC > 0.5) { v[0] = v[1] = v[2] = 0.0; }
+    double pm_ = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+    double xu[3] = {p[0] / pm_, p[1] / pm_, p[2] / pm_};
+    double vsr = xu[0] * v[0] + xu[1] * v[1] + xu[2] * v[2];
+    double usr[3] = {vsr * xu[0], vsr * xu[1], vsr * xu[2]};
+    double ust[3] = {v[0] - usr[0], v[1] - usr[1], v[2] - usr[2]};
+    double vst = sqrt(ust[0] * ust[0] + ust[1] * ust[1] + ust[2] * ust[2]);
+    double betsr = vsr / ERFA_DC, betst = vst / ERFA_DC;
+    double bett = betst, betr = betsr, d = 1.0, del = 0.0, od = 0.0, odel = 0.0, odd = 0.0, oddel = 0.0;
+    for (int i = 0; i < 100; i++) {
+        d = 1.0 + betr;
+        double w2 = betr * betr + bett * bett;
+        del = -w2 / (sqrt(1.0 - w2) + 1.0);
+        betr = d * betsr + del;
+        bett = d * betst;
+        if (i > 0) {
+            double dd_ = fabs(d - od), ddel = fabs(del - odel);
+            if (i > 1 && dd_ >= odd && ddel >= oddel) break;
+            odd = dd_;
+            oddel = ddel;
+        }
+        od = d;
+        odel = del;
+    }
+    double wr = (betsr != 0.0) ? d + del / betsr : 1.0;
+    double v1[3] = {wr * usr[0] + d * ust[0], wr * usr[1] + d * ust[1], wr * usr[2] + d * ust[2]};
+    // starpm
+    double tl1 = pm_ / ERFA_DC;
+    double q[3] = {p[0] + (dt_days + tl1) * v1[0], p[1] + (dt_days + tl1) * v1[1],
+                   p[2] + (dt_days + tl1) * v1[2]};
+    double r2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2];
+    double rdv = q[0] * v1[0] + q[1] * v1[1] + q[2] * v1[2];
+    double v2 = v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2];
+    double c2mv2 = ERFA_DC * ERFA_DC - v2;
+    double tl2 = (-rdv + sqrt(rdv * rdv + c2mv2 * r2)) / c2mv2;
+    double s = dt_days + (tl1 - tl2);
+    double p2[3] = {p[0] + s * v1[0], p[1] + s * v1[1], p[2] + s * v1[2]};
+    // pvstar -> (ra, dec) -> xyz_from_radec (astrometry.py:530)
+    double th = atan2(p2[1], p2[0]);
+    double ph = atan2(p2[2], sqrt(p2[0] * p2[0] + p2[1] * p2[1]));
+    out[0] = cos(th) * cos(ph);
+    out[1] = sin(th) * cos(ph);
+    out[2] = sin(ph);
+}
+
+// Ecliptic -> ICRS rotation (pulsar_ecliptic.py:70: rotation_matrix(obl, "x") is ICRS->ECL)
+PD void ecl_to_icrs(double obl, const double e[3], double o[3]) {
+    double c = cos(obl), s = sin(obl);
+    o[0] = e[0];
+    o[1] = c * e[1] - s * e[2];
+    o[2] = s * e[1] + c * e[2];
+}
+PD void icrs_to_ecl(double obl, const double e[3], double o[3]) {
+    double c = cos(obl), s = sin(obl);
+    o[0] = e[0];
+    o[1] = c * e[1] + s * e[2];
+    o[2] = -s * e[1] + c * e[2];
+}
+
+// Unit vector SSB->pulsar (ICRS) at TDB epoch `epoch_mjd` (astrometry.py:469-528
+// AstrometryEquatorial.ssb_to_psb_xyz_ICRS; :71 base path + SkyCoord apply_space_motion for
+// ecliptic models, sky_coordinate.py apply_space_motion -> erfa.pmsafe, 1-kpc dummy distance
+// utils.py:2171).
+PD void psr_dir_icrs(const pint_spec_t& S, const double* P, double epoch_mjd, double L[3]) {
+    double lon = pval(P, S.o_lon), lat = pval(P, S.o_lat);
+    double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
+    double pmb = S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0;
+    double posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
+    if (S.astrometry == 1) {
+        double ra = lon * HA_RAD, dec = lat * DEG_RAD;
+        if (pml == 0.0 && pmb == 0.0) {
+            L[0] = cos(ra) * cos(dec);
+            L[1] = sin(ra) * cos(dec);
+            L[2] = sin(dec);
+            return;
+        }
+        double px_as = (S.o_px >= 0 ? pval(P, S.o_px) : 0.0) * 1e-3;
+        double pmr = pml * MAS_RAD / cos(dec);
+        double pmd = pmb * MAS_RAD;
+        starpm_dir(ra, dec, pmr, pmd, px_as, epoch_mjd - posep, L);
+        return;
+    }
+    // ecliptic
+    double l = lon * DEG_RAD, b = lat * DEG_RAD;
+    double ue[3] = {cos(l) * cos(b), sin(l) * cos(b), sin(b)};
+    if (pml == 0.0 && pmb == 0.0) {
+        ecl_to_icrs(S.obliquity, ue, L);
+        return;
+    }
+    // tangential velocity (rad/yr at unit distance) in ecliptic, rotated to ICRS
+    double el[3] = {-sin(l), cos(l), 0.0};
+    double eb[3] = {-sin(b) * cos(l), -sin(b) * sin(l), cos(b)};
+    double ve[3];
+    for (int k = 0; k < 3; k++) ve[k] = pml * MAS_RAD * el[k] + pmb * MAS_RAD * eb[k];
+    double u[3], v[3];
+    ecl_to_icrs(S.obliquity, ue, u);
+    ecl_to_icrs(S.obliquity, ve, v);
+    double ra = atan2(u[1], u[0]);
+    double dec = atan2(u[2], sqrt(u[0] * u[0] + u[1] * u[1]));
+    double era[3] = {-sin(ra), cos(ra), 0.0};
+    double edec[3] = {-sin(dec) * cos(ra), -sin(dec) * sin(ra), cos(dec)};
+    double pmra_c = v[0] * era[0] + v[1] * era[1] + v[2] * era[2];
+    double pmdec = v[0] * edec[0] + v[1] * edec[1] + v[2] * edec[2];
+    starpm_dir(ra, dec, pmra_c / cos(dec), pmdec, 1e-3 /* 1 kpc dummy */, epoch_mjd - posep, L);
+}
+
+// ------------------------------------------------------------------------------------
+// Binary models.  Base quantities are computed once per TOA; d_delay/d(param) per column.
+// All derivatives are per SI unit of the parameter (s, rad, rad/s, ...), converted to the
+// par-file unit by bin_unit_factor().
+// ------------------------------------------------------------------------------------
+struct BinState {
+    // common
+    double tt0;      // s (ttasc for ELL1)
+    double orbits_frac, Phi;  // frac(orbits), orbital phase (rad)
+    double floor_orbits;
+    double PBs, PBDOT, XPBDOT, pb;  // PB (s), pbprime (s)
+    double a1, A1DOT, ecc, EDOT;
+    double TM2, SINI, GAMMA, DR, DTH, A0, B0;
+    // ELL1
+    double eps1, eps2, EPS1DOT, EPS2DOT, nhat;
+    double R0, R1, R2;  // d_delayR_da1 and Phi derivatives (ELL1_model.py:221-315)
+    double Dre, Drep, Drepp;
+    // DD
+    double E, sinE, cosE, nu, k, omega, OMDOT_rs, er, eTheta, alpha, beta;
+    double delay;
+    int status;
+};
+
+PD double bin_unit_factor(int pid) {
+    switch (pid) {
+        case PINT_B_PB: case PINT_B_T0: case PINT_B_TASC: return DAYSEC;
+        case PINT_B_OM: return DEG_RAD;
+        case PINT_B_OMDOT: return DEG_RAD / YR_S;
+        default: return 1.0;
+    }
+}
+
+PD double binp(const pint_spec_t& S, const double* P, int pid, double dflt = 0.0) {
+    int o = S.o_bin[pid];
+    return o >= 0 ? pval(P, o) : dflt;
+}
+
+// orbits (binary_orbits.py:98 OrbitPB.orbits) in dd; returns frac and floor
+PD void orbit_phase(dd tt0, double PBs_hi, double PBs_lo, double pbdot_sum, BinState& B) {
+    dd x = dd_div(tt0, dd_make(PBs_hi, PBs_lo));
+    double xd = dd_to_d(x);
+    dd orb = dd_add_d(x, -0.5 * pbdot_sum * xd * xd);
+    dd fl = dd_floor(orb);
+    B.floor_orbits = dd_to_d(fl);
+    B.orbits_frac = dd_to_d(dd_sub(orb, fl));
+    B.Phi = B.orbits_frac * TWO_PI;  // orbit_phase(): (orbits - floor)*2pi (binary_orbits.py:25)
+}
+
+// ---- ELL1 (ELL1_model.py) ---------------------------------------------------------
+PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_delay, BinState& B) {
+    dd tasc = pdd(P, S.o_bin[PINT_B_TASC]);
+    // ttasc = (t - TASC) in s with t = tdbld*day - acc_delay (pulsar_binary.py:398, ELL1_model.py:42)
+    dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, tasc), DAYSEC), -acc_delay);
+    B.tt0 = dd_to_d(tt);
+    dd PB = pdd(P, S.o_bin[PINT_B_PB]);
+    dd PBs = dd_mul_d(PB, DAYSEC);
+    B.PBs = dd_to_d(PBs);
+    B.PBDOT = binp(S, P, PINT_B_PBDOT);
+    B.XPBDOT = binp(S, P, PINT_B_XPBDOT);
+    orbit_phase(tt, PBs.hi, PBs.lo, B.PBDOT + B.XPBDOT, B);
+    B.pb = B.PBs + B.PBDOT * B.tt0;  // pbprime (binary_orbits.py:107)
+    B.A1DOT = binp(S, P, PINT_B_A1DOT);
+    B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
+    B.EPS1DOT = binp(S, P, PINT_B_EPS1DOT);
+    B.EPS2DOT = binp(S, P, PINT_B_EPS2DOT);
+    B.eps1 = binp(S, P, PINT_B_EPS1) + B.tt0 * B.EPS1DOT;
+    B.eps2 = binp(S, P, PINT_B_EPS2) + B.tt0 * B.EPS2DOT;
+    B.TM2 = binp(S, P, PINT_B_M2) * TSUN;
+    B.SINI = binp(S, P, PINT_B_SINI);
+    double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2;
+    double s1 = sin(Phi), c1 = cos(Phi), s2 = sin(2 * Phi), c2 = cos(2 * Phi);
+    double s3 = sin(3 * Phi), c3 = cos(3 * Phi), s4 = sin(4 * Phi), c4 = cos(4 * Phi);
+    double e1s = e1 * e1, e2s = e2 * e2;
+    // d_delayR_da1 (ELL1_model.py:221-253)
+    B.R0 = s1 + 0.5 * (e2 * s2 - e1 * c2) -
+           (1.0 / 8) * (5 * e2s * s1 - 3 * e2s * s3 - 2 * e2 * e1 * c1 + 6 * e2 * e1 * c3 + 3 * e1s * s1 + 3 * e1s * s3) -
+           (1.0 / 12) * (5 * e2s * e2 * s2 + 3 * e1s * e2 * s2 - 6 * e1 * e2s * c2 - 4 * e1s * e1 * c2 -
+                         4 * e2s * e2 * s4 + 12 * e1s * e2 * s4 + 12 * e1 * e2s * c4 - 4 * e1s * e1 * c4);
+    // d_d_delayR_dPhi_da1 (:255-284)
+    B.R1 = c1 + e1 * s2 + e2 * c2 -
+           (1.0 / 8) * (5 * e2s * c1 - 9 * e2s * c3 + 2 * e1 * e2 * s1 - 18 * e1 * e2 * s3 + 3 * e1s * c1 + 9 * e1s * c3) -
+           (1.0 / 12) * (10 * e2s * e2 * c2 + 6 * e1s * e2 * c2 + 12 * e1 * e2s * s2 + 8 * e1s * e1 * s2 -
+                         16 * e2s * e2 * c4 + 48 * e1s * e2 * c4 - 48 * e1 * e2s * s4 + 16 * e1s * e1 * s4);
+    // d_dd_delayR_dPhi_da1 (:286-315)
+    B.R2 = -s1 + 2 * e1 * c2 - 2 * e2 * s2 -
+           (1.0 / 8) * (-5 * e2s * s1 + 27 * e2s * s3 + 2 * e1 * e2 * c1 - 54 * e1 * e2 * c3 - 3 * e1s * s1 - 27 * e1s * s3) -
+           (1.0 / 12) * (-20 * e2s * e2 * s2 - 12 * e1s * e2 * s2 + 24 * e1 * e2s * c2 + 16 * e1s * e1 * c2 +
+                         64 * e2s * e2 * s4 - 192 * e1s * e2 * s4 - 192 * e1 * e2s * c4 + 64 * e1s * e1 * c4);
+    B.Dre = B.a1 * B.R0;  // delayR (:317)
+    B.Drep = B.a1 * B.R1;  // Drep (:398)
+    B.Drepp = B.a1 * B.R2;  // Drepp (:478)
+    B.nhat = TWO_PI / B.pb;
+    double nD = B.nhat * B.Drep;
+    double delayI = B.Dre * (1 - nD + nD * nD + 0.5 * B.nhat * B.nhat * B.Dre * B.Drepp);  // :141-166
+    double delayS = -2 * B.TM2 * log(1 - B.SINI * s1);                                   // :599-603
+    B.delay = delayI + delayS;
+    B.status = 0;
+}
+
+// d(ELL1 delay)/d(par) per SI unit (ELL1_model.py:637 d_ELL1delay_d_par -> :174, :325, :406,
+// :483, :605).  prtl_der() seeds follow binary_generic.py:267 semantics incl. zero entries.
+PD double ell1_deriv(const BinState& B, int pid) {
+    double d_a1 = 0, d_Phi = 0, d_e1 = 0, d_e2 = 0, d_pb = 0, d_TM2 = 0, d_SINI = 0;
+    double tt0 = B.tt0, PBs = B.PBs;
+    switch (pid) {
+        case PINT_B_A1: d_a1 = 1; break;
+        case PINT_B_A1DOT: d_a1 = tt0; break;
+        case PINT_B_EPS1: d_e1 = 1; break;
+        case PINT_B_EPS1DOT: d_e1 = tt0; break;
+        case PINT_B_EPS2: d_e2 = 1; break;
+        case PINT_B_EPS2DOT: d_e2 = tt0; break;
+        case PINT_B_TASC:
+            d_e1 = -B.EPS1DOT;
+            d_e2 = -B.EPS2DOT;
+            // d_Phi_d_TASC uses pb()=pbprime and pbdot() (ELL1_model.py:108)
+            d_Phi = (B.PBDOT * tt0 / B.pb - 1.0) * TWO_PI / B.pb;
+            break;
+        case PINT_B_PB:
+            d_Phi = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs));
+            d_pb = 1;
+            break;
+        case PINT_B_PBDOT:
+            d_Phi = -PI_D * tt0 * tt0 / (PBs * PBs);
+            d_pb = tt0;
+            break;
+        case PINT_B_XPBDOT: d_Phi = -PI_D * tt0 * tt0 / (PBs * PBs); break;
+        case PINT_B_M2: d_TM2 = TSUN; break;
+        case PINT_B_SINI: d_SINI = 1; break;
+        default: return 0.0;
+    }
+    double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2, a1 = B.a1;
+    double s1 = sin(Phi), c1 = cos(Phi), s2 = sin(2 * Phi), c2 = cos(2 * Phi);
+    double s3 = sin(3 * Phi), c3 = cos(3 * Phi), s4 = sin(4 * Phi), c4 = cos(4 * Phi);
+    double e1s = e1 * e1, e2s = e2 * e2;
+    double nhat = B.nhat, Dre = B.Dre, Drep = B.Drep, Drepp = B.Drepp;
+    double d_nhat = -TWO_PI / (B.pb * B.pb) * d_pb;
+    // d_Dre_d_par (:325-394)
+    double dDre_de1 = a1 * (-0.5 * c2 - (1.0 / 8) * (-2 * e2 * c1 + 6 * e2 * c3 + 6 * e1 * s1 + 6 * e1 * s3) -
+                            (1.0 / 12) * (6 * e1 * e2 * s2 - 6 * e2s * c2 - 12 * e1s * c2 + 24 * e1 * e2 * s4 +
+                                          12 * e2s * c4 - 12 * e1s * c4));
+    double dDre_de2 = a1 * (0.5 * s2 - (1.0 / 8) * (-2 * e1 * c1 + 6 * e1 * c3 + 10 * e2 * s1 - 6 * e2 * s3) -
+                            (1.0 / 12) * (15 * e2s * s2 + 3 * e1s * s2 - 12 * e1 * e2 * c2 - 12 * e2s * s4 +
+                                          12 * e1s * s4 + 24 * e1 * e2 * c4));
+    double dDre = d_a1 * B.R0 + Drep * d_Phi + dDre_de1 * d_e1 + dDre_de2 * d_e2;
+    // d_Drep_d_par (:406-476)
+    double dDrep_de1 = a1 * (s2 - (1.0 / 8) * (6 * e1 * c1 + 18 * e1 * c3 + 2 * e2 * s1 - 18 * e2 * s3) -
+                             (1.0 / 12) * (12 * e1 * e2 * c2 + 12 * e2s * s2 + 16 * e1s * s2 + 96 * e1 * e2 * c4 -
+                                           48 * e2s * s4 + 48 * e1s * s4));
+    double dDrep_de2 = a1 * (c2 - (1.0 / 8) * (2 * e1 * s1 - 18 * e1 * s3 + 10 * e2 * c1 - 18 * e2 * c3) -
+                             (1.0 / 12) * (30 * e2s * c2 + 6 * e1s * c2 + 24 * e1 * e2 * s2 - 48 * e2s * c4 +
+                                           48 * e1s * c4 - 96 * e1 * e2 * s4));
+    double dDrep = d_a1 * B.R1 + Drepp * d_Phi + dDrep_de1 * d_e1 + dDrep_de2 * d_e2;
+    // d_Drepp_d_par (:483-597)
+    double dDrepp_dPhi =
+        a1 * (-c1 - 4.0 * (e1 * s2 + e2 * c2) -
+              (1.0 / 8) * (-5 * e2s * c1 + 81 * e2s * c3 - 2 * e1 * e2 * s1 + 162 * e1 * e2 * s3 - 3 * e1s * c1 - 81 * e1s * c3) -
+              (1.0 / 12) * (-40 * e2s * e2 * c2 - 24 * e1s * e2 * c2 - 48 * e1 * e2s * s2 - 32 * e1s * e1 * s2 +
+                            256 * e2s * e2 * c4 - 768 * e1s * e2 * c4 + 768 * e1 * e2s * s4 - 256 * e1s * e1 * s4));
+    double dDrepp_de1 = a1 * (2.0 * c2 - (1.0 / 8) * (-6 * e1 * s1 - 54 * e1 * s3 + 2 * e2 * c1 - 54 * e2 * c3) -
+                              (1.0 / 12) * (-24 * e1 * e2 * s2 + 24 * e2s * c2 + 48 * e1s * c2 - 384 * e1 * e2 * s4 -
+                                            192 * e2s * c4 + 192 * e1s * c4));
+    double dDrepp_de2 = a1 * (-2.0 * s2 - (1.0 / 8) * (2 * e1 * c1 - 54 * e1 * c3 - 10 * e2 * s1 + 54 * e2 * s3) -
+                              (1.0 / 12) * (-60 * e2s * s2 - 12 * e1s * s2 + 48 * e1 * e2 * c2 + 192 * e2s * s4 -
+                                            192 * e1s * s4 - 384 * e1 * e2 * c4));
+    double dDrepp = d_a1 * B.R2 + dDrepp_dPhi * d_Phi + dDrepp_de1 * d_e1 + dDrepp_de2 * d_e2;
+    // d_delayI_d_par (:174-219)
+    double nD = nhat * Drep;
+    double dI_dDre = (1 - nD + nD * nD + 0.5 * nhat * nhat * Dre * Drepp) + Dre * 0.5 * nhat * nhat * Drepp;
+    double dI_dDrep = -Dre * nhat + 2 * nD * nhat * Dre;
+    double dI_dDrepp = 0.5 * (nhat * Dre) * (nhat * Dre);
+    double dI_dnhat = Dre * (-Drep + 2 * nD * Drep + nhat * Dre * Drepp);
+    double dI = dI_dDre * dDre + dI_dDrep * dDrep + dI_dDrepp * dDrepp + dI_dnhat * d_nhat;
+    // d_delayS_d_par (:605-631) -- note the reference's d_delayS_d_Phi omits cos(Phi) (:620)
+    double lg = 1 - B.SINI * s1;
+    double dS = -2 * log(lg) * d_TM2 + (-2 * B.TM2 / lg * (-s1)) * d_SINI + (-2 * B.TM2 / lg * (-B.SINI)) * d_Phi;
+    return dI + dS;
+}
+
+// ---- DD (DD_model.py, binary_generic.py) ------------------------------------------
+PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_delay, BinState& B) {
+    dd T0 = pdd(P, S.o_bin[PINT_B_T0]);
+    dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, T0), DAYSEC), -acc_delay);  // get_tt0 (binary_generic.py:372)
+    B.tt0 = dd_to_d(tt);
+    dd PB = pdd(P, S.o_bin[PINT_B_PB]);
+    dd PBs = dd_mul_d(PB, DAYSEC);
+    B.PBs = dd_to_d(PBs);
+    B.PBDOT = binp(S, P, PINT_B_PBDOT);
+    B.XPBDOT = binp(S, P, PINT_B_XPBDOT);
+    orbit_phase(tt, PBs.hi, PBs.lo, B.PBDOT + B.XPBDOT, B);
+    B.pb = B.PBs + B.PBDOT * B.tt0;
+    B.A1DOT = binp(S, P, PINT_B_A1DOT);
+    B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
+    B.EDOT = binp(S, P, PINT_B_EDOT);
+    B.ecc = binp(S, P, PINT_B_ECC) + B.tt0 * B.EDOT;
+    B.TM2 = binp(S, P, PINT_B_M2) * TSUN;
+    B.SINI = binp(S, P, PINT_B_SINI);
+    B.GAMMA = binp(S, P, PINT_B_GAMMA);
+    B.DR = binp(S, P, PINT_B_DR);
+    B.DTH = binp(S, P, PINT_B_DTH);
+    B.A0 = binp(S, P, PINT_B_A0);
+    B.B0 = binp(S, P, PINT_B_B0);
+    B.status = 0;
+    double e = B.ecc, M = B.Phi;
+    if (!(e >= 0.0 && e < 1.0)) { B.status = PINT_E_KEPLER; B.delay = 0; return; }
+    // compute_eccentric_anomaly (binary_generic.py:337-370): Newton from E0 = M, tol 5e-15
+    double U = M;
+    int it = 0;
+    double kU = U - e * sin(U) - M;
+    while (fabs(kU) > 5e-15 && it < 64) {
+        U = U - kU / (1 - e * cos(U));
+        kU = U - e * sin(U) - M;
+        it++;
+    }
+    if (fabs(kU) > 5e-15) B.status = PINT_E_KEPLER;
+    B.E = U;
+    B.sinE = sin(U);
+    B.cosE = cos(U);
+    // nu (binary_generic.py:538-549), unwrapped: 2*pi*orbits + nu - M = 2*pi*floor(orbits) + nu
+    double nu = 2 * atan(sqrt((1.0 + e) / (1.0 - e)) * tan(U / 2.0));
+    if (nu < 0) nu += TWO_PI;
+    B.nu = TWO_PI * B.floor_orbits + nu;
+    B.OMDOT_rs = binp(S, P, PINT_B_OMDOT) * (DEG_RAD / YR_S);
+    B.k = B.OMDOT_rs / (TWO_PI / B.pb);              // DD_model.py:76 k
+    B.omega = binp(S, P, PINT_B_OM) * DEG_RAD + B.nu * B.k;  // :86
+    B.er = e * (1 + B.DR);
+    B.eTheta = e * (1 + B.DTH);
+    double sw = sin(B.omega), cw = cos(B.omega);
+    B.alpha = B.a1 * sw;                                    // :223
+    B.beta = B.a1 * sqrt(1 - B.eTheta * B.eTheta) * cw;     // :275
+    double sE = B.sinE, cE = B.cosE;
+    double delayR = B.alpha * (cE - B.er) + B.beta * sE;    // :423
+    B.Dre = delayR + B.GAMMA * sE;                          // :434 + delayE :786
+    B.Drep = -B.alpha * sE + (B.beta + B.GAMMA) * cE;       // :470
+    B.Drepp = -B.alpha * cE - (B.beta + B.GAMMA) * sE;      // :520
+    B.nhat = TWO_PI / B.pb / (1 - e * cE);                  // :562
+    double nH = B.nhat;
+    double delayI = B.Dre * (1 - nH * B.Drep + (nH * B.Drep) * (nH * B.Drep) + 0.5 * nH * nH * B.Dre * B.Drepp -
+                             0.5 * e * sE / (1 - e * cE) * nH * nH * B.Dre * B.Drep);  // :602-646
+    double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + sqrt(1 - e * e) * cw * sE);
+    double delayS = -2 * B.TM2 * log(logNum);               // :700-720
+    double oPn = B.omega + B.nu;
+    double delayA = B.A0 * (sin(oPn) + e * sw) + B.B0 * (cos(oPn) + e * cw);  // :794-806
+    B.delay = delayI + delayS + delayA;
+}
+
+PD double ddm_deriv(const BinState& B, int pid) {
+    const double e = B.ecc, sE = B.sinE, cE = B.cosE, tt0 = B.tt0, PBs = B.PBs;
+    const double omeE = 1 - e * cE;
+    // ---- seeds (binary_generic.py / binary_orbits.py / DD_model.py) ----
+    bool orbit_par = (pid == PINT_B_PB || pid == PINT_B_PBDOT || pid == PINT_B_XPBDOT || pid == PINT_B_T0);
+    double d_ecc = 0, d_a1 = 0, d_M = 0, d_pb = 0;
+    switch (pid) {
+        case PINT_B_T0: d_ecc = -B.EDOT; d_a1 = -B.A1DOT;
+            d_M = ((B.PBDOT - B.XPBDOT) * tt0 / PBs - 1.0) * TWO_PI / PBs;  // binary_orbits.py:114
+            d_pb = -B.PBDOT; break;
+        case PINT_B_ECC: d_ecc = 1; break;
+        case PINT_B_EDOT: d_ecc = tt0; break;
+        case PINT_B_A1: d_a1 = 1; break;
+        case PINT_B_A1DOT: d_a1 = tt0; break;
+        case PINT_B_PB: d_M = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs));
+            d_pb = 1; break;
+        case PINT_B_PBDOT: d_M = -PI_D * tt0 * tt0 / (PBs * PBs); d_pb = tt0; break;
+        case PINT_B_XPBDOT: d_M = -PI_D * tt0 * tt0 / (PBs * PBs); break;
+        default: break;
+    }
+    // E (binary_generic.py:397-448)
+    double d_E_d_ECC = sE / (1.0 - e * cE);
+    double d_E = 0;
+    if (pid == PINT_B_T0) d_E = (d_M - B.EDOT * sE) / (1.0 - cE * e);
+    else if (pid == PINT_B_ECC) d_E = d_E_d_ECC;
+    else if (pid == PINT_B_EDOT) d_E = tt0 * d_E_d_ECC;
+    else if (orbit_par) d_E = d_M / (1.0 - cE * e);
+    // nu (binary_generic.py:451-624)
+    double snu = sin(B.nu), cnu = cos(B.nu);
+    double d_nu_d_E = (1 + e * cnu) / (1 - e * cE) * (sE / snu);
+    double d_nu_d_ecc = sE * sE / ((e * cE - 1) * (e * cE - 1)) / snu;
+    double d_nu = 0;
+    if (pid == PINT_B_T0) d_nu = d_nu_d_ecc * (-B.EDOT) + d_nu_d_E * d_E;
+    else if (pid == PINT_B_ECC) d_nu = d_nu_d_ecc + d_nu_d_E * d_E_d_ECC;
+    else if (pid == PINT_B_EDOT) d_nu = tt0 * (d_nu_d_ecc + d_nu_d_E * d_E_d_ECC);
+    else if (orbit_par) d_nu = d_nu_d_E * d_E;
+    // omega (DD_model.py:88-133)
+    double d_omega;
+    if (pid == PINT_B_OM) d_omega = 1;
+    else if (pid == PINT_B_OMDOT) d_omega = B.pb / TWO_PI * B.nu;
+    else if (orbit_par) d_omega = d_nu * B.k + d_pb * B.nu * B.OMDOT_rs / TWO_PI;
+    else d_omega = B.k * d_nu;
+    // er / eTheta (DD_model.py:149-205): d_ecc_d_par only for T0/ECC/EDOT; DR/DTH -> ecc
+    double d_er = (pid == PINT_B_DR) ? e : d_ecc;
+    double d_eTh = (pid == PINT_B_DTH) ? e : d_ecc;
+    double sw = sin(B.omega), cw = cos(B.omega);
+    double eTh = B.eTheta, sq = sqrt(1 - eTh * eTh);
+    // alpha (DD_model.py:225-246)
+    double d_alpha = d_a1 * sw + B.a1 * cw * d_omega;
+    // beta (DD_model.py:277-407): specific d_beta_d_X methods take precedence in prtl_der
+    double d_beta;
+    switch (pid) {
+        case PINT_B_A1: d_beta = sq * cw; break;
+        case PINT_B_A1DOT: d_beta = tt0 * sq * cw; break;
+        case PINT_B_T0: d_beta = -B.A1DOT * sq * cw; break;
+        case PINT_B_ECC: case PINT_B_EDOT: {
+            double f = (pid == PINT_B_EDOT) ? tt0 : 1.0;
+            d_beta = B.a1 * ((-eTh) / sq * cw * f - sq * sw * d_omega);
+        } break;
+        case PINT_B_DTH: d_beta = B.a1 * (-eTh) / sq * cw; break;
+        default:
+            d_beta = sq * cw * d_a1 + (-B.a1 * sq * sw) * d_omega + (B.a1 * (-eTh) / sq * cw) * d_eTh;
+    }
+    double d_gamma = (pid == PINT_B_GAMMA) ? 1.0 : 0.0;
+    double alpha = B.alpha, beta = B.beta, G = B.GAMMA;
+    // Dre, Drep, Drepp (DD_model.py:437-550)
+    double dDre = alpha * (-d_er - d_E * sE) + (cE - B.er) * d_alpha + (d_beta + d_gamma) * sE + (beta + G) * cE * d_E;
+    double dDrep = -sE * d_alpha - (alpha * cE + (beta + G) * sE) * d_E + cE * (d_beta + d_gamma);
+    double dDrepp = -cE * d_alpha + (alpha * sE - (beta + G) * cE) * d_E - sE * (d_beta + d_gamma);
+    // nhat (DD_model.py:564-590): uses prtl_der("PB") (1 only for PB)
+    double dPB = (pid == PINT_B_PB) ? 1.0 : 0.0;
+    double d_nhat = -TWO_PI / B.pb / omeE * (dPB / B.pb - (cE * d_ecc - e * sE * d_E) / omeE);
+    // delayI (DD_model.py:648-698)
+    double Dre = B.Dre, Drep = B.Drep, Drepp = B.Drepp, nH = B.nhat;
+    double x = -0.5 * e * sE / omeE;
+    double dx = -sE / (2 * omeE * omeE) * d_ecc + e * (e - cE) / (2 * omeE * omeE) * d_E;
+    double dI_dDre = 1 + (Drep * nH) * (Drep * nH) + Dre * Drepp * nH * nH + Drep * nH * (2 * Dre * nH * x - 1);
+    double dI_dDrep = Dre * nH * (2 * Drep * nH + Dre * nH * x - 1);
+    double dI_dDrepp = (Dre * nH) * (Dre * nH) / 2;
+    double dI_dnhat = Dre * (-Drep + 2 * Drep * Drep * nH + nH * Dre * Drepp + 2 * x * nH * Dre * Drep);
+    double dI_dx = (Dre * nH) * (Dre * nH) * Drep;
+    double dI = dDre * dI_dDre + dDrep * dI_dDrep + dDrepp * dI_dDrepp + dx * dI_dx + d_nhat * dI_dnhat;
+    // delayS (DD_model.py:722-784)
+    double sq1 = sqrt(1 - e * e);
+    double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + sq1 * cw * sE);
+    double d_TM2 = (pid == PINT_B_M2) ? TSUN : 0.0;
+    double d_SINI = (pid == PINT_B_SINI) ? 1.0 : 0.0;
+    double TM2 = B.TM2;
+    double dS = d_TM2 * (-2 * log(logNum)) +
+                d_ecc * (-2 * TM2 / logNum * (-cE - B.SINI * (-e * cw * sE / sq1 - sw))) +
+                d_E * (-2 * TM2 / logNum * (e * sE - B.SINI * (sq1 * cE * cw - sE * sw))) +
+                d_omega * (2 * TM2 / logNum * B.SINI * ((cE - e) * cw - sq1 * sE * sw)) +
+                d_SINI * (-2 * TM2 / logNum * (-sq1 * cw * sE - (cE - e) * sw));
+    // delayA (DD_model.py:808-848)
+    double oPn = B.omega + B.nu;
+    double dA;
+    if (pid == PINT_B_A0) dA = e * sw + sin(oPn);
+    else if (pid == PINT_B_B0) dA = e * cw + cos(oPn);
+    else
+        dA = d_omega * (B.A0 * (cos(oPn) + e * cw) - B.B0 * (sin(oPn) + e * sw)) +
+             d_nu * (B.A0 * cos(oPn) - B.B0 * sin(oPn)) + d_ecc * (B.A0 * sw + B.B0 * cw);
+    return dI + dS + dA;
+}
+
+// ------------------------------------------------------------------------------------
+// Per-TOA evaluation
+// ------------------------------------------------------------------------------------
+struct ToaRow {
+    dd tdb;
+    double freq;
+    double pos[3], vel[3], sun[3];
+    uint32_t flags;
+    uint64_t jmask;
+    int dmx_a, dmx_b;
+};
+
+struct EvalOut {
+    dd phase;        // spindown + jump phase (cycles)
+    double delay;    // total delay (s)
+    double fdt;      // spin frequency at dt incl. delay (for d_phase_d_delay)
+    double ftaylor;  // spin frequency at dt without delay (residuals.py:295-310)
+    int status;
+};
+
+// taylor_horner (utils.py:419) with coefficients [0, F0, F1, ...] in dd
+PD dd spin_phase(const pint_spec_t& S, const double* P, dd dt) {
+    int m = S.nf;
+    dd r = pdd(P, S.o_F + 2 * (m - 1));
+    for (int j = m - 1; j >= 1; j--) {
+        r = dd_add(dd_div_d(dd_mul(r, dt), (double)(j + 1)), pdd(P, S.o_F + 2 * (j - 1)));
+    }
+    return dd_mul(r, dt);
+}
+// taylor_horner_deriv(dt, [0, F0, ...], 1) in double
+PD double spin_freq(const pint_spec_t& S, const double* P, double dt) {
+    int m = S.nf;
+    double r = pval(P, S.o_F + 2 * (m - 1));
+    for (int j = m - 1; j >= 1; j--) r = r * dt / (double)j + pval(P, S.o_F + 2 * (j - 1));
+    return r;
+}
+
+// Evaluate one TOA.  If M != nullptr, writes the design-matrix row (column-major, leading
+// dimension ld) for columns 0..ncol-1 (timing_model.py:2164-2173).
+PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut& o, double* M,
+                 long ld) {
+    o.status = 0;
+    double delay = 0.0;
+    // ---- astrometry: solar_system_geometric_delay (astrometry.py:155-184) ----
+    double L[3] = {0, 0, 1};
+    double tdb_f = dd_to_d(t.tdb);
+    bool has_pos = (t.flags & 2u) != 0;
+    bool is_bary = (t.flags & 1u) != 0;
+    double rr = 0.0, re_dot_L = 0.0;
+    double px_mas = S.o_px >= 0 ? pval(P, S.o_px) : 0.0;
+    if (S.astrometry) {
+        psr_dir_icrs(S, P, tdb_f, L);
+        rr = t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1] + t.pos[2] * t.pos[2];
+        re_dot_L = t.pos[0] * L[0] + t.pos[1] * L[1] + t.pos[2] * L[2];
+        if (has_pos) {
+            double d = -re_dot_L / C_KMS;
+            if (px_mas != 0.0) {
+                double Lkm = KPC_KM / px_mas;
+                d += (0.5 * (rr / Lkm) * (1.0 - re_dot_L * re_dot_L / rr)) / C_KMS;
+            }
+            delay += d;
+        }
+    }
+    // ---- solar system Shapiro (solar_system_shapiro.py:59-124), sun only ----
+    if (S.shapiro && !is_bary) {
+        double r = sqrt(t.sun[0] * t.sun[0] + t.sun[1] * t.sun[1] + t.sun[2] * t.sun[2]);
+        double rct = t.sun[0] * L[0] + t.sun[1] * L[1] + t.sun[2] * L[2];
+        delay += -2.0 * TSUN * log((r - rct) / AU_KM);
+    }
+    // ---- barycentric radio frequency (astrometry.py:359-364) ----
+    double bfreq = t.freq;
+    if (S.astrometry) {
+        double vdl = t.vel[0] * L[0] + t.vel[1] * L[1] + t.vel[2] * L[2];
+        bfreq = t.freq * (1.0 - vdl / C_KMS);
+    }
+    double inv_f2 = 1.0 / (bfreq * bfreq);
+    // ---- DispersionDM (dispersion_model.py:217-234) ----
+    double dt_yr_dm = 0.0;
+    if (S.ndm > 0) {
+        bool any = false;
+        for (int k = 1; k < S.ndm; k++) any |= (pval(P, S.o_DM + 2 * k) != 0.0);
+        if (S.o_DMEPOCH >= 0) {
+            dd dtd = dd_sub(t.tdb, pdd(P, S.o_DMEPOCH));
+            dt_yr_dm = dd_to_d(dtd) / DJY;
+        }
+        double x = any ? dt_yr_dm : 0.0;
+        double dm = pval(P, S.o_DM + 2 * (S.ndm - 1));
+        for (int k = S.ndm - 1; k >= 1; k--) dm = dm * x / (double)k + pval(P, S.o_DM + 2 * (k - 1));
+        delay += dm * DMCONST * inv_f2;
+    }
+    // ---- DMX (dispersion_model.py:659-678) ----
+    if (S.ndmx > 0) {
+        double dmx = 0.0;
+        if (t.dmx_a >= 0) dmx += pval(P, S.o_DMX + 2 * t.dmx_a);
+        if (t.dmx_b >= 0) dmx += pval(P, S.o_DMX + 2 * t.dmx_b);
+        delay += dmx * DMCONST * inv_f2;
+    }
+    // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
+    BinState B;
+    B.status = 0;
+    if (S.binary == 1) {
+        ell1_setup(S, P, t.tdb, delay, B);
+        delay += B.delay;
+    } else if (S.binary == 2) {
+        ddm_setup(S, P, t.tdb, delay, B);
+        delay += B.delay;
+        if (B.status) o.status = B.status;
+    }
+    // ---- FD (frequency_dependent.py:70-101) ----
+    double logf = log(bfreq / 1000.0);
+    if (!isfinite(logf)) logf = 0.0;
+    if (S.nfd > 0) {
+        double fd = 0.0;
+        for (int k = S.nfd; k >= 1; k--) fd = fd * logf + pval(P, S.o_FD + 2 * (k - 1));
+        fd *= logf;
+        delay += fd;
+    }
+    o.delay = delay;
+    // ---- spindown phase (spindown.py:124-155) + jumps (jump.py:119-136) ----
+    dd dt0 = dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_PEPOCH)), DAYSEC);
+    dd dt = dd_add_d(dt0, -delay);
+    dd ph = spin_phase(S, P, dt);
+    if (S.njump > 0 && t.jmask) {
+        dd F0 = pdd(P, S.o_F);
+        for (int k = 0; k < S.njump; k++)
+            if ((t.jmask >> k) & 1ull) ph = dd_add(ph, dd_mul(dd_make(pval(P, S.o_JUMP + 2 * k)), F0));
+    }
+    o.phase = ph;
+    double dtd = dd_to_d(dt);
+    o.fdt = spin_freq(S, P, dtd);
+    o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
+    if (!M) return;
+    // ---- design matrix row (timing_model.py:2073-2175) ----
+    double F0 = pval(P, S.o_F);
+    double chain = o.fdt / F0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+    // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities)
+    double r_m = 0, edec = 0, era = 0;
+    double plon = 0, plat = 0;
+    if (S.astrometry) {
+        double r_km = sqrt(rr);
+        r_m = r_km;  // keep km; divide by c in km/s
+        double xy = sqrt(t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1]);
+        edec = atan2(t.pos[2], xy);
+        era = atan2(t.pos[1], t.pos[0]);
+        if (S.astrometry == 2) {
+            // earth ecliptic lon/lat via ICRS->PulsarEcliptic (astrometry.py:1034-1055)
+            double ue[3] = {cos(era) * cos(edec), sin(era) * cos(edec), sin(edec)}, ee[3];
+            icrs_to_ecl(S.obliquity, ue, ee);
+            era = atan2(ee[1], ee[0]);
+            edec = atan2(ee[2], sqrt(ee[0] * ee[0] + ee[1] * ee[1]));
+            plon = pval(P, S.o_lon) * DEG_RAD;
+        } else {
+            plon = pval(P, S.o_lon) * HA_RAD;
+        }
+        plat = pval(P, S.o_lat) * DEG_RAD;
+    }
+    double te_s = 0.0;
+    if (S.o_POSEPOCH >= 0) te_s = dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC));
+    for (int c = 0; c < S.ncol; c++) {
+        int kind = S.col_kind[c], idx = S.col_index[c];
+        double v = 0.0;
+        switch (kind) {
+            case PINT_COL_OFFSET: v = 1.0 / F0; break;
+            case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): dt^(k+1)/(k+1)!
+                double r = 1.0;
+                for (int j = 1; j <= idx + 1; j++) r = r * dtd / (double)j;
+                v = -r / F0;
+            } break;
+            case PINT_COL_JUMP: v = ((t.jmask >> idx) & 1ull) ? -1.0 : 0.0; break;  // jump.py:138
+            case PINT_COL_LON: {  // d_delay_astrometry_d_RAJ / _ELONG
+                double g = cos(edec) * cos(plat) * sin(plon - era);
+                double dd_ = r_m * g / C_KMS;
+                v = chain * dd_ * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
+            } break;
+            case PINT_COL_LAT: {
+                double g = cos(edec) * sin(plat) * cos(plon - era) - sin(edec) * cos(plat);
+                v = chain * (r_m * g / C_KMS) * DEG_RAD;
+            } break;
+            case PINT_COL_PMLON: {
+                double g = cos(edec) * sin(plon - era);
+                v = chain * (r_m * g * te_s / C_KMS) * MASYR_RADS;
+            } break;
+            case PINT_COL_PMLAT: {
+                double g = cos(edec) * sin(plat) * cos(plon - era) - cos(plat) * sin(edec);
+                v = chain * (r_m * g * te_s / C_KMS) * MASYR_RADS;
+            } break;
+            case PINT_COL_PX: {  // astrometry.py:219-249
+                double pxr2 = rr - re_dot_L * re_dot_L;
+                v = chain * 0.5 * (pxr2 / (AU_KM * C_KMS)) * MAS_RAD;
+            } break;
+            case PINT_COL_DM: {  // d_dm_d_DMs (dispersion_model.py:253) * DMconst / bfreq^2
+                double r = 1.0;
+                for (int j = 1; j <= idx; j++) r = r * dt_yr_dm / (double)j;
+                v = chain * DMCONST * r * inv_f2;
+            } break;
+            case PINT_COL_DMX: {  // d_dm_d_DMX (:684)
+                double sel = (t.dmx_a == idx || t.dmx_b == idx) ? 1.0 : 0.0;
+                v = chain * DMCONST * sel * inv_f2;
+            } break;
+            case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103)
+                double r = 1.0;
+                for (int j = 0; j < idx + 1; j++) r *= logf;
+                v = chain * r;
+            } break;
+            case PINT_COL_BIN: {
+                double d = (S.binary == 1) ? ell1_deriv(B, idx) : ddm_deriv(B, idx);
+                v = chain * d * bin_unit_factor(idx);
+            } break;
+            default: v = 0.0;
+        }
+        M[(long)c * ld] = v;
+    }
+}
+
+}  // namespace pint

@@ -1,0 +1,905 @@
+// pint_hip.hip — gfx950 kernels and the C-ABI of libpint_hip.so.
+//
+// Launch sequence per fit iteration (all instances of a batch in each launch):
+//   k_eval      one thread per TOA row: delays, dd phase, design-matrix row, red-noise
+//               Fourier columns (HBM-streaming; timing_model.py:1515/1548/2073)
+//   k_resid     one workgroup per instance: TZR subtraction, track mode, weighted mean,
+//               time residuals, WLS chi2 (residuals.py:314-667) — wave-shuffle reductions
+//   k_gram      FP64 MFMA (v_mfma_f64_16x16x4f64) Gram [T|r]^T W [T|r] over TOA chunks
+//               staged in LDS, split over N (fitter.py:2187-2192, :1425-1470)
+//   k_solve     one workgroup per instance: normalisation, Cholesky in LDS, xhat, inverse
+//               (covariance), Woodbury Sigma factor for the GLS chi2 (utils.py:3074)
+//   k_apply     parameter update in double-double (fitter.py:957, :2073-2080)
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+#include "physics.hpp"
+
+using namespace pint;
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------
+// device-side descriptors
+// ---------------------------------------------------------------------------------
+struct PsrDev {
+    const double *tdb_hi, *tdb_lo, *freq, *sigma, *pos, *vel, *sun, *pn, *dpn;
+    const uint32_t* flags;
+    const uint64_t* jmask;
+    const int32_t *dmx_a, *dmx_b;
+    const pint_spec_t* spec;
+    const double* red_freq;  // nred
+    const double* red_phi;   // 2*nred
+    int n;
+    int K;   // ncol + 2*nred
+    int Kp;  // padded K+1 (residual column) to 16
+    int pad;
+};
+
+struct InstDev {
+    int psr;
+    int n;
+    int K;
+    int Kp;
+    long toff;   // table offset (doubles)
+    long roff;   // eval-row offset (n+1 rows)
+    long moff;   // design-matrix offset (n*K)
+    long goff;   // Gram offset (Kp*Kp per split)
+    long soff;   // solve outputs offset (K*K)
+    long coff;   // per-instance K vectors offset
+};
+
+#define HIPCHK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);               \
+            return PINT_E_HIP;                                                       \
+        }                                                                            \
+    } while (0)
+
+// ---------------------------------------------------------------------------------
+// wave / block reductions (64-wide waves)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int NW>
+__device__ double block_sum(double v, double* sh) {
+    v = wave_sum(v);
+    int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) t += sh[i];
+    return t;
+}
+
+// ---------------------------------------------------------------------------------
+// k_eval: one thread per TOA row (row n = TZR TOA)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
+                                              const double* __restrict__ tables, double* __restrict__ ph_hi,
+                                              double* __restrict__ ph_lo, double* __restrict__ ftay,
+                                              double* __restrict__ delay_out, double* __restrict__ Mout, int want_M,
+                                              int* __restrict__ status) {
+    int b = blockIdx.x;
+    int ii = blk_inst[b];
+    const InstDev I = insts[ii];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    int r = blk_row0[b] + threadIdx.x;
+    int n = I.n;
+    if (r > n) return;
+    const double* P = tables + I.toff;
+    ToaRow t;
+    t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
+    t.freq = Pd.freq[r];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        t.pos[k] = Pd.pos[3 * r + k];
+        t.vel[k] = Pd.vel[3 * r + k];
+        t.sun[k] = Pd.sun[3 * r + k];
+    }
+    t.flags = Pd.flags[r];
+    t.jmask = Pd.jmask[r];
+    t.dmx_a = Pd.dmx_a[r];
+    t.dmx_b = Pd.dmx_b[r];
+    EvalOut o;
+    double* Mrow = (want_M && r < n) ? (Mout + I.moff + r) : nullptr;
+    eval_toa(S, P, t, o, Mrow, n);
+    if (o.status) atomicOr(status, 1 << o.status);
+    ph_hi[I.roff + r] = o.phase.hi;
+    ph_lo[I.roff + r] = o.phase.lo;
+    ftay[I.roff + r] = o.ftaylor;
+    delay_out[I.roff + r] = o.delay;
+    if (Mrow && S.nred > 0) {
+        // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
+        // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.
+        dd ts = dd_mul_d(t.tdb, DAYSEC);
+        for (int k = 0; k < S.nred; k++) {
+            dd x = dd_mul_d(ts, Pd.red_freq[k]);
+            double fr = dd_to_d(dd_sub(x, dd_floor(x)));
+            double s, c;
+            sincos(TWO_PI * fr, &s, &c);
+            Mrow[(long)(S.ncol + 2 * k) * n] = s;
+            Mrow[(long)(S.ncol + 2 * k + 1) * n] = c;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_resid: one workgroup (256) per instance — residuals.py:314-425, :483-538, :638-667
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                               const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
+                                               const double* __restrict__ ftay, double* __restrict__ rtime,
+                                               double* __restrict__ rphase, double* __restrict__ chi2) {
+    __shared__ double sh[8];
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    int n = I.n;
+    long ro = I.roff;
+    long oo = I.roff - blockIdx.x;  // output rows: n per instance (roff counts n+1)
+    dd tz = dd_make(ph_hi[ro + n], ph_lo[ro + n]);
+    dd d0 = dd_make(0.0);
+    if (!S.track_pn && S.subtract_mean) {
+        d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
+    }
+    double sw = 0.0, swx = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        dd d = dd_add_d(dd_sub(dd_make(ph_hi[ro + i], ph_lo[ro + i]), tz), Pd.dpn[i]);
+        double full;
+        if (S.track_pn) {
+            full = dd_to_d(dd_add_d(d, -Pd.pn[i]));
+        } else {
+            dd x = dd_sub(d, d0);
+            full = dd_to_d(dd_sub(x, dd_round_half_up(x)));
+        }
+        rphase[oo + i] = full;
+        double w = S.weighted_mean ? 1.0 / (Pd.sigma[i] * Pd.sigma[i]) : 1.0;
+        sw += w;
+        swx += w * full;
+    }
+    double mean = 0.0;
+    if (S.subtract_mean) {
+        double a = block_sum<4>(swx, sh);
+        double bsum = block_sum<4>(sw, sh);
+        mean = a / bsum;
+    }
+    double c2 = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        double p = rphase[oo + i] - mean;
+        rphase[oo + i] = p;
+        double rt = p / ftay[ro + i];
+        rtime[oo + i] = rt;
+        double z = rt / Pd.sigma[i];
+        c2 += z * z;
+    }
+    c2 = block_sum<4>(c2, sh);
+    if (threadIdx.x == 0) chi2[blockIdx.x] = c2;
+}
+
+// ---------------------------------------------------------------------------------
+// k_gram: FP64 MFMA Gram of [T | r] with weights w = 1/sigma^2, one workgroup computes
+// the whole (upper-triangular tiles of the) Kp x Kp Gram for one N-split of one instance.
+// Also accumulates the unweighted column sums of squares (normalize_designmatrix).
+// ---------------------------------------------------------------------------------
+constexpr int GCH = 16;       // TOAs per LDS chunk (multiple of 4)
+constexpr int GMAXKP = 256;   // max padded columns
+constexpr int GWAVES = 8;
+constexpr int GMAXT = 17;     // ceil(136 / 8) upper tiles per wave at Kp=256
+
+__global__ __launch_bounds__(512) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              const double* __restrict__ M, const double* __restrict__ rtime,
+                                              int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
+    extern __shared__ double lds[];
+    const int inst = blockIdx.y, split = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const int n = I.n, K = I.K, Kp = I.Kp;
+    const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
+    double* Ts = lds;                  // [GCH][stride]
+    double* Ws = lds + GCH * stride;   // weighted copy
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + (I.roff - inst);
+    long per = (n + nsplit - 1) / nsplit;
+    per = (per + GCH - 1) / GCH * GCH;
+    long i0 = split * per, i1 = i0 + per;
+    if (i1 > n) i1 = n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nt = Kp / 16;
+    const int ntiles = nt * (nt + 1) / 2;
+    double4_t acc[GMAXT];
+#pragma unroll
+    for (int t = 0; t < GMAXT; t++) acc[t] = (double4_t){0, 0, 0, 0};
+    // per-thread column-sum-of-squares accumulators: thread handles columns c = tid/GCH + 32*j
+    double csq[GMAXKP / 32];
+#pragma unroll
+    for (int j = 0; j < GMAXKP / 32; j++) csq[j] = 0.0;
+    for (long c0 = i0; c0 < i1; c0 += GCH) {
+        __syncthreads();
+        // stage: element e -> (row i = e % GCH, col c = e / GCH): 16 consecutive TOAs per column
+        const int ii = tid % GCH;
+        const long toa = c0 + ii;
+        const bool ok = toa < i1;
+        const double w = ok ? 1.0 / (Pd.sigma[toa] * Pd.sigma[toa]) : 0.0;
+#pragma unroll
+        for (int j = 0; j < GMAXKP / 32; j++) {
+            int c = tid / GCH + 32 * j;
+            if (c < Kp) {
+                double v = 0.0;
+                if (ok) {
+                    if (c < K) v = Mi[(long)c * n + toa];
+                    else if (c == K) v = ri[toa];
+                }
+                Ts[ii * stride + c] = v;
+                Ws[ii * stride + c] = w * v;
+                if (c < K) csq[j] += v * v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < GMAXT; t++) {
+            int tt = wave + t * GWAVES;
+            if (tt < ntiles) {
+                // decode upper-triangular tile index tt -> (ti <= tj)
+                int ti = 0, rem = tt;
+                while (rem >= nt - ti) { rem -= nt - ti; ti++; }
+                int tj = ti + rem;
+#pragma unroll
+                for (int kk = 0; kk < GCH / 4; kk++) {
+                    int row = kk * 4 + (lane >> 4);
+                    double a = Ts[row * stride + ti * 16 + (lane & 15)];
+                    double bb = Ws[row * stride + tj * 16 + (lane & 15)];
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // write partial tiles: D[row=(lane>>4)+4*r][col=lane&15]
+    double* G = Gpart + I.goff + (long)split * Kp * Kp;
+#pragma unroll
+    for (int t = 0; t < GMAXT; t++) {
+        int tt = wave + t * GWAVES;
+        if (tt < ntiles) {
+            int ti = 0, rem = tt;
+            while (rem >= nt - ti) { rem -= nt - ti; ti++; }
+            int tj = ti + rem;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int row = ti * 16 + (lane >> 4) + 4 * q;
+                int col = tj * 16 + (lane & 15);
+                G[(long)row * Kp + col] = acc[t][q];
+            }
+        }
+    }
+    // column sums of squares: reduce over the GCH lanes sharing a column
+#pragma unroll
+    for (int j = 0; j < GMAXKP / 32; j++) {
+        double v = csq[j];
+        for (int o = GCH / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        int c = tid / GCH + 32 * j;
+        if ((tid % GCH) == 0 && c < K) colsq[(I.coff + c) * nsplit + split] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_solve: one workgroup per instance.  Normalised normal matrix in LDS (packed lower
+// triangle), Cholesky, xhat, inverse.  mode 0: WLS (fitter.py:1282-1359: whitened-column
+// normalisation, no prior); mode 1: GLS (fitter.py:2164-2202 / 1425-1507: unweighted
+// column norms, phiinv/norm^2 on the noise columns).  Also factors the Woodbury Sigma
+// (residuals.py:567-589: U=[F, 1], Phi=[phi, 1e40]) for k_woodbury.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+__device__ int chol_packed(double* A, int K, double* sh, int* flag) {
+    // in-place lower Cholesky of packed lower-triangular A (K x K); returns 0 if PD
+    for (int k = 0; k < K; k++) {
+        if (threadIdx.x == 0) {
+            double d = A[tri(k, k)];
+            if (!(d > 0.0)) *flag = 1;
+            A[tri(k, k)] = sqrt(d);
+        }
+        __syncthreads();
+        if (*flag) return 1;
+        double lkk = A[tri(k, k)];
+        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) A[tri(i, k)] /= lkk;
+        __syncthreads();
+        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) {
+            double lik = A[tri(i, k)];
+            for (int j = k + 1; j <= i; j++) A[tri(i, j)] -= lik * A[tri(j, k)];
+        }
+        __syncthreads();
+    }
+    return 0;
+}
+
+// solve L L^T x = b in place (x in shared vec)
+__device__ void chol_solve_packed(const double* L, int K, double* x) {
+    for (int k = 0; k < K; k++) {
+        __syncthreads();
+        double xk = x[k] / L[tri(k, k)];
+        __syncthreads();
+        if (threadIdx.x == 0) x[k] = xk;
+        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) x[i] -= L[tri(i, k)] * xk;
+    }
+    for (int k = K - 1; k >= 0; k--) {
+        __syncthreads();
+        double xk = x[k] / L[tri(k, k)];
+        __syncthreads();
+        if (threadIdx.x == 0) x[k] = xk;
+        for (int i = threadIdx.x; i < k; i += blockDim.x) x[i] -= L[tri(k, i)] * xk;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_solve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                               const double* __restrict__ tables, const double* __restrict__ Gpart,
+                                               const double* __restrict__ colsq, int nsplit, int mode,
+                                               double* __restrict__ work, double* __restrict__ dpars,
+                                               double* __restrict__ errs, double* __restrict__ cov,
+                                               double* __restrict__ chi2lin, double* __restrict__ sigL,
+                                               int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int flag;
+    __shared__ double sh[8];
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int K = I.K, Kp = I.Kp, ncol = S.ncol;
+    const double* P = tables + I.toff;
+    double* A = lds;                        // packed lower, K(K+1)/2
+    double* x = lds + K * (K + 1) / 2;      // K
+    double* nrm = x + K;                    // K
+    const double* Gp = Gpart + I.goff;
+    auto G = [&](int i, int j) {  // full symmetric accessor, sums splits
+        if (i > j) { int t = i; i = j; j = t; }
+        double s = 0.0;
+        for (int q = 0; q < nsplit; q++) s += Gp[(long)q * Kp * Kp + (long)i * Kp + j];
+        return s;
+    };
+    if (threadIdx.x == 0) flag = 0;
+    // norms (normalize_designmatrix, utils.py:2879: zero norm -> 1)
+    for (int j = threadIdx.x; j < K; j += blockDim.x) {
+        double v;
+        if (mode == 0) v = G(j, j);
+        else {
+            v = 0.0;
+            for (int q = 0; q < nsplit; q++) v += colsq[(I.coff + j) * nsplit + q];
+        }
+        v = sqrt(v);
+        nrm[j] = (v == 0.0) ? 1.0 : v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < K * (K + 1) / 2; e += blockDim.x) {
+        int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+        while (i * (i + 1) / 2 > e) i--;
+        while ((i + 1) * (i + 2) / 2 <= e) i++;
+        int j = e - i * (i + 1) / 2;
+        double v = G(i, j) / (nrm[i] * nrm[j]);
+        if (i == j && mode == 1 && i >= ncol) v += 1.0 / Pd.red_phi[i - ncol] / (nrm[i] * nrm[i]);
+        A[e] = v;
+    }
+    for (int j = threadIdx.x; j < K; j += blockDim.x) x[j] = G(j, K) / nrm[j];
+    __syncthreads();
+    double rwr = G(K, K);
+    int bad = chol_packed(A, K, sh, &flag);
+    if (bad) {
+        if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        return;
+    }
+    chol_solve_packed(A, K, x);
+    // xhat -> dpars, linearised chi2 = rWr - b.xhat (normal equations)
+    double bx = 0.0;
+    for (int j = threadIdx.x; j < K; j += blockDim.x) bx += (G(j, K) / nrm[j]) * x[j];
+    bx = block_sum<4>(bx, sh);
+    if (threadIdx.x == 0) chi2lin[inst] = rwr - bx;
+    for (int j = threadIdx.x; j < K; j += blockDim.x) dpars[I.coff + j] = x[j] / nrm[j];
+    // inverse: Linv columns (one thread per column), stored full lower in work (K*K)
+    double* Li = work + I.soff;
+    for (int c = threadIdx.x; c < K; c += blockDim.x) {
+        for (int i = 0; i < c; i++) Li[(long)i * K + c] = 0.0;
+        Li[(long)c * K + c] = 1.0 / A[tri(c, c)];
+        for (int i = c + 1; i < K; i++) {
+            double s = 0.0;
+            for (int m = c; m < i; m++) s += A[tri(i, m)] * Li[(long)m * K + c];
+            Li[(long)i * K + c] = -s / A[tri(i, i)];
+        }
+    }
+    __syncthreads();
+    // cov_n = Linv^T Linv ; cov = cov_n / (n n^T), only the ncol x ncol timing block is
+    // returned in full, errs for all K
+    double* C = cov + (long)I.soff;
+    for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
+        int i = e / K, j = e % K;
+        if (j < i) continue;
+        if (i >= ncol && i != j) continue;
+        double s = 0.0;
+        for (int m = j; m < K; m++) s += Li[(long)m * K + i] * Li[(long)m * K + j];
+        double v = s / (nrm[i] * nrm[j]);
+        C[(long)i * K + j] = v;
+        C[(long)j * K + i] = v;
+        if (i == j) errs[I.coff + i] = sqrt(s) / nrm[i];
+    }
+    // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column);
+    // factor into sigL (packed lower) for k_woodbury (GLS pulsars only).
+    if (S.nred > 0) {
+        __syncthreads();
+        int R = 2 * S.nred, Kn = R + 1;
+        double F0 = pval(P, S.o_F);
+        double* L = sigL + I.coff * 0 + (long)inst * 0;  // placeholder replaced below
+        L = sigL + (long)I.soff;  // reuse soff region sizing (K*K >= Kn*(Kn+1)/2)
+        for (int e = threadIdx.x; e < Kn * (Kn + 1) / 2; e += blockDim.x) {
+            int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (i * (i + 1) / 2 > e) i--;
+            while ((i + 1) * (i + 2) / 2 <= e) i++;
+            int j = e - i * (i + 1) / 2;
+            int ci = (i < R) ? ncol + i : 0, cj = (j < R) ? ncol + j : 0;
+            double si = (i < R) ? 1.0 : F0, sj = (j < R) ? 1.0 : F0;
+            double v = G(ci, cj) * si * sj;
+            if (i == j) v += (i < R) ? 1.0 / Pd.red_phi[i] : 1e-40;
+            L[e] = v;
+        }
+        __syncthreads();
+        // factor in global memory (Kn small)
+        if (threadIdx.x == 0) flag = 0;
+        __syncthreads();
+        if (chol_packed(L, Kn, sh, &flag)) {
+            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        }
+    }
+}
+
+// Woodbury GLS chi2 of the current residuals (utils.py:3074-3126 woodbury_dot):
+// chi2 = r^T N^-1 r - d^T Sigma^-1 d, d = U^T N^-1 r, U = [F, 1].
+__global__ __launch_bounds__(256) void k_woodbury(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                  const double* __restrict__ M, const double* __restrict__ rtime,
+                                                  const double* __restrict__ sigL, double* __restrict__ chi2) {
+    extern __shared__ double lds[];
+    __shared__ double sh[8];
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int n = I.n;
+    const double* ri = rtime + (I.roff - inst);
+    const double* Mi = M + I.moff;
+    int R = 2 * S.nred, Kn = R + 1;
+    double* d = lds;  // Kn
+    double rwr = 0.0, rw1 = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        double w = 1.0 / (Pd.sigma[i] * Pd.sigma[i]);
+        rwr += ri[i] * ri[i] * w;
+        rw1 += ri[i] * w;
+    }
+    rwr = block_sum<4>(rwr, sh);
+    rw1 = block_sum<4>(rw1, sh);
+    for (int j = 0; j < R; j++) {
+        const double* col = Mi + (long)(S.ncol + j) * n;
+        double s = 0.0;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) s += col[i] * ri[i] / (Pd.sigma[i] * Pd.sigma[i]);
+        s = block_sum<4>(s, sh);
+        if (threadIdx.x == 0) d[j] = s;
+    }
+    if (threadIdx.x == 0) d[R] = rw1;
+    __syncthreads();
+    const double* L = sigL + I.soff;
+    if (threadIdx.x == 0) {
+        double q = 0.0;
+        for (int k = 0; k < Kn; k++) {
+            double s = d[k];
+            for (int m = 0; m < k; m++) s -= L[tri(k, m)] * d[m];
+            d[k] = s / L[tri(k, k)];
+            q += d[k] * d[k];
+        }
+        chi2[inst] = rwr - q;
+    }
+}
+
+// tables += lambda * dpars on every timing column (skips Offset), double-double add
+__global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, double* __restrict__ tables,
+                        const double* __restrict__ dpars, const double* __restrict__ lam) {
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const pint_spec_t& S = *psrs[I.psr].spec;
+    double* P = tables + I.toff;
+    for (int c = threadIdx.x; c < S.ncol; c += blockDim.x) {
+        int o = S.col_toff[c];
+        if (o < 0) continue;
+        dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam[inst] * dpars[I.coff + c]);
+        P[o] = v.hi;
+        P[o + 1] = v.lo;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------
+struct PsrHost {
+    PsrDev dev;
+    pint_spec_t spec;
+    std::vector<void*> bufs;
+    int n, K;
+};
+
+struct pint_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<PsrHost> psrs;
+    PsrDev* d_psrs = nullptr;
+    int npsr_dev = 0;
+    // instances
+    int ninst = 0;
+    std::vector<InstDev> inst;
+    InstDev* d_inst = nullptr;
+    int* d_blk_inst = nullptr;
+    int* d_blk_row0 = nullptr;
+    int nblk = 0;
+    long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0;
+    int nsplit = 1;
+    double *d_tables = nullptr, *d_phhi = nullptr, *d_phlo = nullptr, *d_ftay = nullptr, *d_delay = nullptr;
+    double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
+    double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
+    double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
+    int* d_status = nullptr;
+    int maxK = 0;
+    hipEvent_t ev[8];
+    float ms_eval = 0, ms_gram = 0, ms_solve = 0, ms_resid = 0;
+};
+
+static void dfree(void*& p) {
+    if (p) hipFree(p);
+    p = nullptr;
+}
+
+template <typename T>
+static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const T*& dst) {
+    void* p = nullptr;
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = sizeof(T);
+    HIPCHK(hipMalloc(&p, bytes));
+    if (src && count) HIPCHK(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(p, 0, bytes));
+    ph.bufs.push_back(p);
+    dst = (const T*)p;
+    return 0;
+}
+
+extern "C" {
+
+int pint_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+pint_ctx* pint_ctx_create(int device) {
+    pint_ctx* ctx = new pint_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        ctx->err = "hipSetDevice failed";
+        return ctx;
+    }
+    hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 8; i++) hipEventCreate(&ctx->ev[i]);
+    hipMalloc(&ctx->d_status, sizeof(int));
+    return ctx;
+}
+
+const char* pint_last_error(pint_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+static void free_instances(pint_ctx* ctx) {
+    void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
+                   (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
+                   (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
+                   (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
+                   (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
+                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g};
+    for (auto p : ps) dfree(*p);
+    ctx->ninst = 0;
+}
+
+void pint_ctx_destroy(pint_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    free_instances(ctx);
+    for (auto& p : ctx->psrs) {
+        for (auto b : p.bufs) hipFree(b);
+    }
+    if (ctx->d_psrs) hipFree(ctx->d_psrs);
+    if (ctx->d_status) hipFree(ctx->d_status);
+    for (int i = 0; i < 8; i++) hipEventDestroy(ctx->ev[i]);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec, const double* red_freq,
+                    const double* red_phi) {
+    if (!ctx || !t || !spec) return -PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    int n = t->n;
+    if (n <= 0) { ctx->err = "pulsar has no TOAs"; return -PINT_E_INVALID; }
+    if (spec->nf < 1 || spec->o_F < 0 || spec->o_PEPOCH < 0) { ctx->err = "Spindown F0/PEPOCH required"; return -PINT_E_INVALID; }
+    if (spec->ncol < 1 || spec->ncol > PINT_MAX_COLS) { ctx->err = "bad column count"; return -PINT_E_INVALID; }
+    int K = spec->ncol + 2 * spec->nred;
+    int Kp = (K + 1 + 15) / 16 * 16;
+    if (Kp > GMAXKP) { ctx->err = "design matrix too wide for k_gram (K+1 > 256)"; return -PINT_E_INVALID; }
+    if (spec->njump > PINT_MAX_JUMP) { ctx->err = "too many JUMPs"; return -PINT_E_INVALID; }
+    PsrHost ph;
+    ph.spec = *spec;
+    ph.n = n;
+    ph.K = K;
+    PsrDev& d = ph.dev;
+    memset(&d, 0, sizeof(d));
+    int rc = 0;
+    rc |= upload(ctx, ph, t->tdb_hi, n + 1, d.tdb_hi);
+    rc |= upload(ctx, ph, t->tdb_lo, n + 1, d.tdb_lo);
+    rc |= upload(ctx, ph, t->freq_mhz, n + 1, d.freq);
+    rc |= upload(ctx, ph, t->sigma_s, n, d.sigma);
+    rc |= upload(ctx, ph, t->pos_km, 3 * (n + 1), d.pos);
+    rc |= upload(ctx, ph, t->vel_kms, 3 * (n + 1), d.vel);
+    rc |= upload(ctx, ph, t->sun_km, 3 * (n + 1), d.sun);
+    rc |= upload(ctx, ph, t->pulse_number, n, d.pn);
+    rc |= upload(ctx, ph, t->delta_pn, n + 1, d.dpn);
+    rc |= upload(ctx, ph, t->flags, n + 1, d.flags);
+    rc |= upload(ctx, ph, t->jump_mask, n + 1, d.jmask);
+    rc |= upload(ctx, ph, t->dmx_a, n + 1, d.dmx_a);
+    rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
+    rc |= upload(ctx, ph, red_freq, (size_t)spec->nred, d.red_freq);
+    rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
+    const pint_spec_t* sp = nullptr;
+    rc |= upload(ctx, ph, spec, 1, sp);
+    if (rc) return -PINT_E_HIP;
+    d.spec = sp;
+    d.n = n;
+    d.K = K;
+    d.Kp = Kp;
+    ctx->psrs.push_back(ph);
+    // refresh device descriptor array
+    if (ctx->d_psrs) hipFree(ctx->d_psrs);
+    std::vector<PsrDev> all;
+    for (auto& p : ctx->psrs) all.push_back(p.dev);
+    HIPCHK(hipMalloc(&ctx->d_psrs, sizeof(PsrDev) * all.size()));
+    HIPCHK(hipMemcpy(ctx->d_psrs, all.data(), sizeof(PsrDev) * all.size(), hipMemcpyHostToDevice));
+    return (int)ctx->psrs.size() - 1;
+}
+
+int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
+    if (!ctx || ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    free_instances(ctx);
+    ctx->inst.resize(ninst);
+    long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0;
+    std::vector<int> bi, br;
+    int maxK = 0, maxN = 0;
+    for (int k = 0; k < ninst; k++) {
+        int p = inst_psr[k];
+        if (p < 0 || p >= (int)ctx->psrs.size()) { ctx->err = "bad pulsar id"; return PINT_E_INVALID; }
+        if (ctx->psrs[p].n > maxN) maxN = ctx->psrs[p].n;
+    }
+    // N-split for the Gram so the launch fills the 256 CUs
+    int nsplit = (256 + ninst - 1) / ninst;
+    int maxsplit = (maxN + 255) / 256;
+    if (nsplit > maxsplit) nsplit = maxsplit;
+    if (nsplit < 1) nsplit = 1;
+    ctx->nsplit = nsplit;
+    for (int k = 0; k < ninst; k++) {
+        int p = inst_psr[k];
+        PsrHost& ph = ctx->psrs[p];
+        InstDev& I = ctx->inst[k];
+        I.psr = p;
+        I.n = ph.n;
+        I.K = ph.K;
+        I.Kp = ph.dev.Kp;
+        I.toff = toff;
+        I.roff = roff;
+        I.moff = moff;
+        I.goff = goff;
+        I.soff = soff;
+        I.coff = coff;
+        toff += ph.spec.tstride;
+        for (int r0 = 0; r0 <= ph.n; r0 += 256) {
+            bi.push_back(k);
+            br.push_back(r0);
+        }
+        roff += ph.n + 1;
+        moff += (long)ph.n * ph.K;
+        goff += (long)nsplit * I.Kp * I.Kp;
+        soff += (long)(ph.K + 1) * (ph.K + 1);
+        coff += ph.K + 1;
+        out += ph.n;
+        if (ph.K > maxK) maxK = ph.K;
+    }
+    ctx->ninst = ninst;
+    ctx->tot_table = toff;
+    ctx->tot_rows = roff;
+    ctx->tot_m = moff;
+    ctx->tot_g = goff;
+    ctx->tot_s = soff;
+    ctx->tot_c = coff;
+    ctx->tot_out = out;
+    ctx->maxK = maxK;
+    ctx->nblk = (int)bi.size();
+    HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
+    HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&ctx->d_blk_inst, sizeof(int) * bi.size()));
+    HIPCHK(hipMalloc(&ctx->d_blk_row0, sizeof(int) * br.size()));
+    HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_blk_row0, br.data(), sizeof(int) * br.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&ctx->d_tables, sizeof(double) * toff));
+    HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&ctx->d_phhi, sizeof(double) * roff));
+    HIPCHK(hipMalloc(&ctx->d_phlo, sizeof(double) * roff));
+    HIPCHK(hipMalloc(&ctx->d_ftay, sizeof(double) * roff));
+    HIPCHK(hipMalloc(&ctx->d_delay, sizeof(double) * roff));
+    HIPCHK(hipMalloc(&ctx->d_M, sizeof(double) * (moff > 0 ? moff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_rt, sizeof(double) * out));
+    HIPCHK(hipMalloc(&ctx->d_rp, sizeof(double) * out));
+    HIPCHK(hipMalloc(&ctx->d_chi2, sizeof(double) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_chi2g, sizeof(double) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_chi2lin, sizeof(double) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_G, sizeof(double) * goff));
+    HIPCHK(hipMalloc(&ctx->d_colsq, sizeof(double) * coff * nsplit));
+    HIPCHK(hipMalloc(&ctx->d_work, sizeof(double) * soff));
+    HIPCHK(hipMalloc(&ctx->d_cov, sizeof(double) * soff));
+    HIPCHK(hipMalloc(&ctx->d_sigL, sizeof(double) * soff));
+    HIPCHK(hipMalloc(&ctx->d_dpars, sizeof(double) * coff));
+    HIPCHK(hipMalloc(&ctx->d_errs, sizeof(double) * coff));
+    HIPCHK(hipMalloc(&ctx->d_lam, sizeof(double) * ninst));
+    HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * soff, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_get_tables(pint_ctx* ctx, double* out) {
+    HIPCHK(hipMemcpyAsync(out, ctx->d_tables, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_set_tables(pint_ctx* ctx, const double* tables) {
+    HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+static int check_status(pint_ctx* ctx) {
+    int st = 0;
+    HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
+    if (st & (1 << PINT_E_NOT_PD)) { ctx->err = "normal matrix not positive definite"; return PINT_E_NOT_PD; }
+    if (st) { ctx->err = "device status " + std::to_string(st); return PINT_E_PARAM; }
+    return PINT_OK;
+}
+
+// Evaluate phases/delays (+ design matrix) and residuals for every instance.
+int pint_eval(pint_ctx* ctx, int want_M) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
+    hipEventRecord(ctx->ev[0], ctx->stream);
+    hipLaunchKernelGGL(k_eval, dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_blk_inst,
+                       ctx->d_blk_row0, ctx->d_tables, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
+                       want_M, ctx->d_status);
+    HIPCHK(hipGetLastError());
+    hipEventRecord(ctx->ev[1], ctx->stream);
+    hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
+                       ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
+    HIPCHK(hipGetLastError());
+    hipEventRecord(ctx->ev[2], ctx->stream);
+    int rc = check_status(ctx);
+    hipEventElapsedTime(&ctx->ms_eval, ctx->ev[0], ctx->ev[1]);
+    hipEventElapsedTime(&ctx->ms_resid, ctx->ev[1], ctx->ev[2]);
+    return rc;
+}
+
+int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, double* chi2) {
+    if (time_resid) HIPCHK(hipMemcpyAsync(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
+    if (phase_resid) HIPCHK(hipMemcpyAsync(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
+    if (chi2) HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_read_eval(pint_ctx* ctx, double* ph_hi, double* ph_lo, double* ftaylor, double* delay) {
+    size_t b = sizeof(double) * ctx->tot_rows;
+    if (ph_hi) HIPCHK(hipMemcpyAsync(ph_hi, ctx->d_phhi, b, hipMemcpyDeviceToHost, ctx->stream));
+    if (ph_lo) HIPCHK(hipMemcpyAsync(ph_lo, ctx->d_phlo, b, hipMemcpyDeviceToHost, ctx->stream));
+    if (ftaylor) HIPCHK(hipMemcpyAsync(ftaylor, ctx->d_ftay, b, hipMemcpyDeviceToHost, ctx->stream));
+    if (delay) HIPCHK(hipMemcpyAsync(delay, ctx->d_delay, b, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_read_designmatrix(pint_ctx* ctx, double* M) {
+    HIPCHK(hipMemcpyAsync(M, ctx->d_M, sizeof(double) * ctx->tot_m, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+// Gram + solve for every instance; requires pint_eval(want_M=1) on the current state.
+int pint_fit_step(pint_ctx* ctx, int mode) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
+    int maxKp = 16;
+    for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
+    int stride = maxKp + ((maxKp & 31) == 0 ? 16 : 0);
+    size_t lds_g = sizeof(double) * 2 * GCH * stride;
+    hipEventRecord(ctx->ev[3], ctx->stream);
+    hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(512), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                       ctx->d_M, ctx->d_rt, ctx->nsplit, ctx->d_G, ctx->d_colsq);
+    HIPCHK(hipGetLastError());
+    hipEventRecord(ctx->ev[4], ctx->stream);
+    int K = ctx->maxK;
+    size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 2 * K + 8);
+    if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
+    hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(256), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                       ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_work, ctx->d_dpars,
+                       ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+    HIPCHK(hipGetLastError());
+    hipEventRecord(ctx->ev[5], ctx->stream);
+    int rc = check_status(ctx);
+    hipEventElapsedTime(&ctx->ms_gram, ctx->ev[3], ctx->ev[4]);
+    hipEventElapsedTime(&ctx->ms_solve, ctx->ev[4], ctx->ev[5]);
+    return rc;
+}
+
+int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, double* chi2lin) {
+    if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
+    if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
+    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_s, hipMemcpyDeviceToHost, ctx->stream));
+    if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
+    HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
+                       ctx->d_dpars, ctx->d_lam);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+// Woodbury GLS chi2 of the current residuals; requires a previous pint_fit_step(mode=1)
+// (Sigma factor) and the red-noise columns of the last design matrix.
+int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
+    int R = 0;
+    for (auto& p : ctx->psrs) R = 2 * p.spec.nred > R ? 2 * p.spec.nred : R;
+    hipLaunchKernelGGL(k_woodbury, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
+                       ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_sigL, ctx->d_chi2g);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_last_timing(pint_ctx* ctx, double* ms) {
+    ms[0] = ctx->ms_eval;
+    ms[1] = ctx->ms_resid;
+    ms[2] = ctx->ms_gram;
+    ms[3] = ctx->ms_solve;
+    return PINT_OK;
+}
+
+int pint_sync(pint_ctx* ctx) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,453 @@
+"""GPU engine: packs (TimingModel, TOAs) into the C-ABI structures and drives the HIP
+launch sequence through ctypes.  One ``Session`` = one pint_ctx (one HIP stream on one
+device) holding any number of pulsars and a batch of parameter-table instances.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from .noise import red_noise_freqs_weights, scaled_sigma_us
+from .parameter import LD
+from .timing_model import BIN_IDS, OBLIQUITY, TimingModel
+
+UNITS = {  # design-matrix column units as the reference prints them (per par unit / F0)
+    "RAJ": "1 / (hourangle Hz)", "DECJ": "1 / (deg Hz)", "ELONG": "1 / (deg Hz)", "ELAT": "1 / (deg Hz)",
+}
+
+
+def split_ld(v) -> tuple:
+    v = LD(v)
+    hi = float(v)
+    lo = float(v - LD(hi))
+    return hi, lo
+
+
+@dataclass
+class PulsarLayout:
+    """Host record of one uploaded pulsar: table layout, columns, sizes."""
+    model: TimingModel
+    toas: object
+    n: int
+    offsets: Dict[str, int]
+    tstride: int
+    columns: List[str]
+    spec: L.SpecT
+    nred: int
+    K: int
+    red_freq: Optional[np.ndarray] = None
+    red_phi: Optional[np.ndarray] = None
+    sigma_us: Optional[np.ndarray] = None
+    psr_id: int = -1
+    track_mode: str = "nearest"
+    keep: list = field(default_factory=list)
+
+
+def _track_mode(model, toas, track_mode):
+    """residuals.py:133-149 auto-selection."""
+    if track_mode is not None:
+        return track_mode
+    tr = model["TRACK"].value if "TRACK" in model else None
+    if tr == "-2":
+        return "use_pulse_numbers"
+    if tr == "0":
+        return "nearest"
+    pn = toas.get_pulse_numbers()
+    if pn is not None and not np.any(np.isnan(pn)):
+        return "use_pulse_numbers"
+    return "nearest"
+
+
+def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, use_weighted_mean=True,
+                 use_gls_basis=True) -> PulsarLayout:
+    model.validate()
+    spec = L.SpecT()
+    offs: Dict[str, int] = {}
+    pos = 0
+
+    def place(name):
+        nonlocal pos
+        offs[name] = pos
+        pos += 2
+        return offs[name]
+
+    for s in ("o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px", "o_POSEPOCH", "o_DM",
+              "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP"):
+        setattr(spec, s, -1)
+    for i in range(L.B_NPAR):
+        spec.o_bin[i] = -1
+    F = model.spin_terms()
+    spec.nf = len(F)
+    spec.o_F = pos
+    for n in F:
+        place(n)
+    spec.o_PEPOCH = place("PEPOCH")
+    ak = model.astrometry_kind
+    spec.astrometry = ak
+    if ak:
+        names = ["RAJ", "DECJ", "PMRA", "PMDEC"] if ak == 1 else ["ELONG", "ELAT", "PMELONG", "PMELAT"]
+        spec.o_lon, spec.o_lat, spec.o_pmlon, spec.o_pmlat = [place(n) for n in names]
+        spec.o_px = place("PX")
+        if model.POSEPOCH.value is not None:
+            spec.o_POSEPOCH = place("POSEPOCH")
+        spec.shapiro = 1 if "SolarSystemShapiro" in model.components else 0
+        if ak == 2:
+            spec.obliquity = OBLIQUITY[str(model.ECL.value or "IERS2010")]
+    dms = model.dm_terms()
+    spec.ndm = len(dms)
+    if dms:
+        spec.o_DM = pos
+        for n in dms:
+            place(n)
+        if model.DMEPOCH.value is not None:
+            spec.o_DMEPOCH = place("DMEPOCH")
+    dmx = model.dmx_params()
+    spec.ndmx = len(dmx)
+    if dmx:
+        spec.o_DMX = pos
+        for n in dmx:
+            place(n)
+    fds = model.fd_terms()
+    spec.nfd = len(fds)
+    if fds:
+        spec.o_FD = pos
+        for n in fds:
+            place(n)
+    jumps = model.mask_params("JUMP")
+    spec.njump = len(jumps)
+    if len(jumps) > 64:
+        raise NotImplementedError("more than 64 JUMPs")
+    if jumps:
+        spec.o_JUMP = pos
+        for n in jumps:
+            place(n)
+    spec.binary = {None: 0, "ELL1": 1, "DD": 2}[model.binary]
+    if model.binary:
+        for n, pid in BIN_IDS.items():
+            if n in model:
+                spec.o_bin[pid] = place(n)
+        need = ["PB", "A1", "TASC" if model.binary == "ELL1" else "T0"]
+        for n in need:
+            if n not in model or model[n].value is None:
+                raise ValueError(f"binary parameter {n} missing")
+    tstride = pos
+    spec.tstride = tstride
+    # ---- columns: Offset + free params in params order (timing_model.py:2141-2173)
+    cols = ["Offset"]
+    kinds, idxs, toffs = [L.COL_OFFSET], [0], [-1]
+    noise_like = {"EFAC", "EQUAD", "ECORR", "TNEQ"}
+    for n in model.free_params:
+        p = model[n]
+        base = "".join(ch for ch in n if not ch.isdigit())
+        if p.kind == "mask" and base in noise_like:
+            continue
+        if n in ("TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX"):
+            continue
+        if n in F:
+            k, i = L.COL_F, F.index(n)
+        elif n in ("RAJ", "ELONG"):
+            k, i = L.COL_LON, 0
+        elif n in ("DECJ", "ELAT"):
+            k, i = L.COL_LAT, 0
+        elif n in ("PMRA", "PMELONG"):
+            k, i = L.COL_PMLON, 0
+        elif n in ("PMDEC", "PMELAT"):
+            k, i = L.COL_PMLAT, 0
+        elif n == "PX":
+            k, i = L.COL_PX, 0
+        elif n in dms:
+            k, i = L.COL_DM, dms.index(n)
+        elif n in dmx:
+            k, i = L.COL_DMX, dmx.index(n)
+        elif n in fds:
+            k, i = L.COL_FD, fds.index(n)
+        elif n in jumps:
+            k, i = L.COL_JUMP, jumps.index(n)
+        elif model.binary and n in BIN_IDS and n in offs:
+            k, i = L.COL_BIN, BIN_IDS[n]
+        else:
+            raise ValueError(f"Cannot compute the design matrix because parameter {n} is unfittable "
+                             f"(timing_model.py:2118-2131)")
+        if n not in offs:
+            raise ValueError(f"parameter {n} has no table slot")
+        cols.append(n)
+        kinds.append(k)
+        idxs.append(i)
+        toffs.append(offs[n])
+    if len(cols) > L.MAX_COLS:
+        raise NotImplementedError("too many design-matrix columns")
+    spec.ncol = len(cols)
+    for j in range(len(cols)):
+        spec.col_kind[j] = kinds[j]
+        spec.col_index[j] = idxs[j]
+        spec.col_toff[j] = toffs[j]
+    tm = _track_mode(model, toas, track_mode)
+    spec.track_pn = 1 if tm == "use_pulse_numbers" else 0
+    has_phoff = "PhaseOffset" in model.components
+    spec.subtract_mean = 1 if (subtract_mean and not has_phoff) else 0
+    spec.weighted_mean = 1 if use_weighted_mean else 0
+    nred = 0
+    rf = rp = None
+    if use_gls_basis and "PLRedNoise" in model.components:
+        rf, rp = red_noise_freqs_weights(model, toas)
+        nred = len(rf)
+    if model.mask_params("ECORR") and use_gls_basis:
+        eps_n = 0
+        from .noise import ecorr_epochs
+        t = np.asarray(toas.tdbld * LD(86400))
+        for name in model.mask_params("ECORR"):
+            p = model[name]
+            eps_n += len(ecorr_epochs(t[toas.select_mask(p.key, p.key_value)]))
+        if eps_n > 0:
+            raise NotImplementedError("ECORR epochs with >= 2 TOAs: Schur-complement GLS lands next round")
+    spec.nred = nred
+    lay = PulsarLayout(model=model, toas=toas, n=toas.ntoas, offsets=offs, tstride=tstride, columns=cols,
+                       spec=spec, nred=nred, K=len(cols) + 2 * nred, red_freq=rf, red_phi=rp, track_mode=tm)
+    return lay
+
+
+def pack_table(lay: PulsarLayout, model: Optional[TimingModel] = None) -> np.ndarray:
+    model = model or lay.model
+    tab = np.zeros(lay.tstride)
+    for n, o in lay.offsets.items():
+        v = model[n].value
+        if v is None:
+            v = 0.0
+        tab[o], tab[o + 1] = split_ld(v)
+    return tab
+
+
+def unpack_table(lay: PulsarLayout, tab: np.ndarray, model: TimingModel):
+    """Write device table values back into a model (longdouble where the reference keeps it)."""
+    for n, o in lay.offsets.items():
+        p = model[n]
+        if p.value is None and tab[o] == 0.0 and tab[o + 1] == 0.0:
+            continue
+        v = LD(tab[o]) + LD(tab[o + 1])
+        p.value = v if (p.long_double or p.kind == "mjd") else float(v)
+
+
+def pack_toas(lay: PulsarLayout):
+    """Per-TOA boundary arrays (n+1 rows; the last is the TZR TOA) + masks."""
+    model, toas = lay.model, lay.toas
+    n = toas.ntoas
+    A = toas.arrays
+    tz = toas.tzr if "AbsPhase" in model.components else None
+    if tz is None:
+        tz = make_tzr_row(model, toas)
+
+    def cat(name, default=0.0, width=None):
+        a = np.asarray(A[name], dtype=np.float64)
+        b = np.asarray(tz.get(name, np.full((1,) + a.shape[1:], default)), dtype=np.float64).reshape((1,) + a.shape[1:])
+        return np.ascontiguousarray(np.concatenate([a, b]))
+
+    tdb_hi, tdb_lo = cat("tdb_hi"), cat("tdb_lo")
+    freq = cat("freq_mhz", np.inf)
+    pos, vel, sun = cat("ssb_obs_pos_km"), cat("ssb_obs_vel_kms"), cat("obs_sun_pos_km")
+    dpn = cat("delta_pulse_number")
+    is_bary = np.concatenate([np.asarray(A["is_bary"]), np.asarray(tz.get("is_bary", [0])).reshape(1)]).astype(bool)
+    allpos = np.all(pos != 0, axis=1)
+    flags = (is_bary.astype(np.uint32) | (allpos.astype(np.uint32) << 1)).astype(np.uint32)
+    sigma = scaled_sigma_us(model, toas)
+    lay.sigma_us = sigma
+    sigma_s = np.ascontiguousarray(sigma * 1e-6)
+    pn = toas.get_pulse_numbers()
+    pn = np.ascontiguousarray(pn if pn is not None else np.zeros(n), dtype=np.float64)
+    jm = np.zeros(n + 1, dtype=np.uint64)
+    for k, name in enumerate(model.mask_params("JUMP")):
+        p = model[name]
+        idx = toas.select_mask(p.key, p.key_value)
+        jm[idx] |= np.uint64(1) << np.uint64(k)
+        if len(toas.select_mask(p.key, p.key_value, tzr=True)) if toas.tzr else False:
+            jm[n] |= np.uint64(1) << np.uint64(k)
+    da = np.full(n + 1, -1, dtype=np.int32)
+    db = np.full(n + 1, -1, dtype=np.int32)
+    mjdf = np.concatenate([np.asarray(A["mjd_float"], dtype=np.float64),
+                           np.asarray(tz.get("mjd_float", [0.0]), dtype=np.float64).reshape(1)])
+    for j, name in enumerate(model.dmx_params()):
+        tag = name.split("_")[1]
+        r1 = float(model["DMXR1_" + tag].value)
+        r2 = float(model["DMXR2_" + tag].value)
+        sel = np.where((mjdf >= r1) & (mjdf <= r2))[0]  # toa_select.py:101 inclusive
+        for i in sel:
+            if da[i] < 0:
+                da[i] = j
+            elif db[i] < 0:
+                db[i] = j
+            else:
+                raise NotImplementedError("more than two overlapping DMX bins on one TOA")
+    keep = [tdb_hi, tdb_lo, freq, sigma_s, pos, vel, sun, pn, dpn, flags, jm, da, db]
+    t = L.ToasT(n, L.ptr(tdb_hi), L.ptr(tdb_lo), L.ptr(freq), L.ptr(sigma_s), L.ptr(pos), L.ptr(vel), L.ptr(sun),
+                L.ptr(pn), L.ptr(dpn), L.ptr(flags, C.c_uint32), L.ptr(jm, C.c_uint64), L.ptr(da, C.c_int32),
+                L.ptr(db, C.c_int32))
+    return t, keep
+
+
+def make_tzr_row(model, toas) -> dict:
+    """No TZRMJD in the model: the reference adds AbsPhase with TZRMJD = first TOA after
+    PEPOCH at the barycenter, infinite frequency (timing_model.py:1584, absolute_phase.py:129)."""
+    mjds = toas.get_mjds()
+    pe = float(model.PEPOCH.value)
+    later = mjds[mjds > pe]
+    tz = later.min() if len(later) else mjds[mjds <= pe].max()
+    hi, lo = split_ld(LD(tz))
+    return {"tdb_hi": np.array([hi]), "tdb_lo": np.array([lo]), "freq_mhz": np.array([np.inf]),
+            "ssb_obs_pos_km": np.zeros((1, 3)), "ssb_obs_vel_kms": np.zeros((1, 3)),
+            "obs_sun_pos_km": np.zeros((1, 3)), "mjd_float": np.array([tz]), "is_bary": np.array([1]),
+            "delta_pulse_number": np.zeros(1), "flags": {}}
+
+
+class Session:
+    """A pint_ctx with uploaded pulsars and a batch of instances."""
+
+    def __init__(self, device: Optional[int] = None):
+        self.L = L.lib()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.L.pint_device_count() <= 0:
+            raise RuntimeError("no HIP device visible: the pint_amd compute path needs an MI355X GPU")
+        self.ctx = self.L.pint_ctx_create(device)
+        if not self.ctx:
+            raise RuntimeError("pint_ctx_create failed")
+        err = self.L.pint_last_error(self.ctx)
+        if err:
+            raise RuntimeError(err.decode())
+        self.layouts: List[PulsarLayout] = []
+        self.inst_psr: List[int] = []
+        self.inst_layout: List[PulsarLayout] = []
+
+    def close(self):
+        if self.ctx:
+            self.L.pint_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise L.PintError(rc, self.L.pint_last_error(self.ctx).decode())
+
+    def add(self, lay: PulsarLayout) -> PulsarLayout:
+        t, keep = pack_toas(lay)
+        rf = np.ascontiguousarray(lay.red_freq if lay.red_freq is not None else np.zeros(1))
+        rp = np.ascontiguousarray(lay.red_phi if lay.red_phi is not None else np.zeros(1))
+        pid = self.L.pint_add_pulsar(self.ctx, C.byref(t), C.byref(lay.spec), L.ptr(rf), L.ptr(rp))
+        if pid < 0:
+            self._check(-pid)
+        lay.psr_id = pid
+        self.layouts.append(lay)
+        return lay
+
+    def set_instances(self, insts: Sequence[tuple]):
+        """insts: sequence of (layout, table ndarray)."""
+        ids = np.array([lay.psr_id for lay, _ in insts], dtype=np.int32)
+        tabs = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64) for _, t in insts]))
+        self._check(self.L.pint_set_instances(self.ctx, len(insts), L.ptr(ids, C.c_int32), L.ptr(tabs)))
+        self.inst_layout = [lay for lay, _ in insts]
+        self.ntab = len(tabs)
+
+    # -- launches -------------------------------------------------------------------
+    def eval(self, want_M=False):
+        self._check(self.L.pint_eval(self.ctx, 1 if want_M else 0))
+
+    def fit_step(self, mode):
+        self._check(self.L.pint_fit_step(self.ctx, int(mode)))
+
+    def apply_step(self, lam):
+        lam = np.ascontiguousarray(np.broadcast_to(np.asarray(lam, dtype=np.float64), (len(self.inst_layout),)))
+        self._check(self.L.pint_apply_step(self.ctx, L.ptr(lam)))
+
+    def set_tables(self, tabs):
+        tabs = np.ascontiguousarray(tabs, dtype=np.float64)
+        self._check(self.L.pint_set_tables(self.ctx, L.ptr(tabs)))
+
+    # -- reads ----------------------------------------------------------------------
+    def _split(self, flat, sizes):
+        out, o = [], 0
+        for s in sizes:
+            out.append(flat[o:o + s])
+            o += s
+        return out
+
+    def read_resids(self):
+        n = [l.n for l in self.inst_layout]
+        tr = np.empty(sum(n))
+        pr = np.empty(sum(n))
+        c2 = np.empty(len(n))
+        self._check(self.L.pint_read_resids(self.ctx, L.ptr(tr), L.ptr(pr), L.ptr(c2)))
+        return self._split(tr, n), self._split(pr, n), c2
+
+    def read_eval(self):
+        rows = [l.n + 1 for l in self.inst_layout]
+        a = [np.empty(sum(rows)) for _ in range(4)]
+        self._check(self.L.pint_read_eval(self.ctx, *[L.ptr(x) for x in a]))
+        return [self._split(x, rows) for x in a]
+
+    def read_designmatrix(self):
+        sizes = [l.n * l.K for l in self.inst_layout]
+        M = np.empty(sum(sizes))
+        self._check(self.L.pint_read_designmatrix(self.ctx, L.ptr(M)))
+        return [m.reshape(l.K, l.n).T for m, l in zip(self._split(M, sizes), self.inst_layout)]
+
+    def read_step(self):
+        kk = [l.K + 1 for l in self.inst_layout]
+        dp = np.empty(sum(kk))
+        er = np.empty(sum(kk))
+        cov = np.empty(sum(k * k for k in kk))
+        cl = np.empty(len(kk))
+        self._check(self.L.pint_read_step(self.ctx, L.ptr(dp), L.ptr(er), L.ptr(cov), L.ptr(cl)))
+        covs = []
+        o = 0
+        for l in self.inst_layout:
+            k = l.K + 1
+            covs.append(cov[o:o + (l.K * l.K)].reshape(l.K, l.K))
+            o += k * k
+        return self._split(dp, kk), self._split(er, kk), covs, cl
+
+    def read_tables(self):
+        t = np.empty(self.ntab)
+        self._check(self.L.pint_get_tables(self.ctx, L.ptr(t)))
+        return self._split(t, [l.tstride for l in self.inst_layout])
+
+    def chi2_gls(self):
+        c = np.empty(len(self.inst_layout))
+        self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
+        return c
+
+    def timing(self):
+        ms = np.zeros(4)
+        self.L.pint_last_timing(self.ctx, L.ptr(ms))
+        return ms
+
+
+# -- convenience single-model evaluations (used by TimingModel methods) ----------------
+def _single(model, toas, **kw):
+    s = Session()
+    lay = s.add(build_layout(model, toas, **kw))
+    s.set_instances([(lay, pack_table(lay))])
+    return s, lay
+
+
+def evaluate_delay_phase(model, toas):
+    s, lay = _single(model, toas)
+    s.eval(False)
+    hi, lo, ft, dl = [x[0] for x in s.read_eval()]
+    s.close()
+    return {"delay": dl[:-1], "phase_hi": hi, "phase_lo": lo, "tzr_delay": dl[-1], "phase": (hi, lo)}
+
+
+def evaluate_designmatrix(model, toas):
+    s, lay = _single(model, toas, use_gls_basis=False)
+    s.eval(True)
+    M = s.read_designmatrix()[0]
+    s.close()
+    return M[:, :len(lay.columns)].copy(), list(lay.columns), [UNITS.get(c, "") for c in lay.columns]

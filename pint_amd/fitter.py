@@ -1,0 +1,307 @@
+"""Fitters (host mirror of reference fitter.py): WLSFitter (:1940), GLSFitter (:2090),
+DownhillWLSFitter (:1379), DownhillGLSFitter (:1527), Fitter.auto (:252).
+
+The numerical work -- design matrix, residuals, Gram on FP64 MFMA, Cholesky, step,
+covariance, Woodbury chi2, parameter update in double-double -- runs on the GPU; the host
+only sequences launches and applies the reference's control flow (downhill lambda halving
+and convergence rules, exceptions).  ``BatchFit`` drives many independent fits (grid
+points, PTA pulsars) through one launch sequence per iteration.
+"""
+from __future__ import annotations
+
+import copy
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .engine import Session, build_layout, pack_table, unpack_table
+
+
+class ConvergenceFailure(ValueError):
+    pass
+
+
+class MaxiterReached(ConvergenceFailure):
+    pass
+
+
+class StepProblem(ConvergenceFailure):
+    pass
+
+
+class CorrelatedErrors(ValueError):
+    def __init__(self, model):
+        super().__init__(f"Model has correlated errors and requires a GLS-based fitter: {model}")
+
+
+class InvalidModelParameters(ValueError):
+    pass
+
+
+class DegeneracyWarning(UserWarning):
+    pass
+
+
+class CovarianceMatrix:
+    def __init__(self, matrix, labels):
+        self.matrix = np.asarray(matrix)
+        self.labels = list(labels)
+
+    def get_label_matrix(self, labels):
+        idx = [self.labels.index(l) for l in labels]
+        return self.matrix[np.ix_(idx, idx)]
+
+
+class FitResult:
+    """Per-instance fit outcome of a BatchFit."""
+
+    def __init__(self):
+        self.chi2 = np.nan
+        self.errors = None
+        self.cov = None
+        self.converged = False
+        self.status = "ok"
+        self.noise_coeffs = None
+
+
+class BatchFit:
+    """Run the same fitter on many (model, toas) instances at once.
+
+    mode: 'wls' | 'gls'; downhill: reference DownhillFitter control flow per instance.
+    Each instance's model is updated in place at the end (like fitter.model).
+    """
+
+    def __init__(self, items: Sequence[tuple], mode: str = "wls", session: Optional[Session] = None,
+                 layouts=None):
+        self.items = list(items)
+        self.mode = mode
+        self.gls = mode == "gls"
+        self.s = session or Session()
+        if layouts is None:
+            layouts = []
+            cache = {}
+            for model, toas in self.items:
+                key = (id(toas), tuple(model.free_params), model.name)
+                if key in cache:
+                    layouts.append(cache[key])
+                    continue
+                lay = self.s.add(build_layout(model, toas, use_gls_basis=self.gls))
+                cache[key] = lay
+                layouts.append(lay)
+        self.layouts = layouts
+        self.tables = [pack_table(l, m) for l, (m, _) in zip(self.layouts, self.items)]
+        self.s.set_instances(list(zip(self.layouts, self.tables)))
+        self.ninst = len(self.items)
+        self.use_gls_chi2 = [self.gls and l.nred > 0 for l in self.layouts]
+
+    # -- helpers ------------------------------------------------------------------------
+    def _chi2_now(self):
+        tr, pr, c2 = self.s.read_resids()
+        if any(self.use_gls_chi2):
+            cg = self.s.chi2_gls()
+            c2 = np.where(self.use_gls_chi2, cg, c2)
+        return c2, tr
+
+    def _step(self):
+        self.s.eval(want_M=True)
+        self.s.fit_step(1 if self.gls else 0)
+
+    def _finish(self, results):
+        tabs = self.s.read_tables()
+        for (m, _), lay, t in zip(self.items, self.layouts, tabs):
+            unpack_table(lay, t, m)
+        return results
+
+    def _errors_into(self, results):
+        dp, er, cov, _ = self.s.read_step()
+        for k, (res, lay) in enumerate(zip(results, self.layouts)):
+            nc = len(lay.columns)
+            res.errors = er[k][:nc].copy()
+            res.cov = cov[k][:nc, :nc].copy()
+            res.noise_coeffs = dp[k][nc:lay.K].copy()
+            res.labels = list(lay.columns)
+            m = self.items[k][0]
+            for j, name in enumerate(lay.columns[1:], start=1):
+                m[name].uncertainty = float(res.errors[j])
+
+    # -- plain WLS/GLS (fitter.py:1965-2087, :2104-2289) -------------------------------
+    def fit_plain(self, maxiter=1):
+        results = [FitResult() for _ in range(self.ninst)]
+        for _ in range(maxiter):
+            self._step()
+            self._errors_into(results)
+            self.s.apply_step(np.ones(self.ninst))
+        self.s.eval(want_M=False)
+        c2, _ = self._chi2_now()
+        for r, c in zip(results, c2):
+            r.chi2 = float(c)
+            r.converged = True
+        self.resid_time = self.s.read_resids()[0]
+        return self._finish(results)
+
+    # -- downhill (fitter.py:999-1105) ---------------------------------------------------
+    def fit_downhill(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3):
+        n = self.ninst
+        results = [FitResult() for _ in range(n)]
+        self._step()                                     # step of the initial state
+        cur_tab = np.concatenate(self.s.read_tables())
+        sizes = [l.tstride for l in self.layouts]
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        self.s.eval(want_M=False)
+        cur_chi2, _ = self._chi2_now()
+        best_chi2 = cur_chi2.copy()
+        best_tab = cur_tab.copy()
+        active = np.ones(n, dtype=bool)
+        converged = np.zeros(n, dtype=bool)
+        exc = np.zeros(n, dtype=bool)
+        for it in range(maxiter):
+            if not active.any():
+                break
+            lam = np.ones(n)
+            decided = ~active
+            dec = np.zeros(n)
+            while not decided.all():
+                self.s.set_tables(cur_tab)
+                self.s.apply_step(np.where(decided, 0.0, lam))
+                try:
+                    self.s.eval(want_M=False)
+                    new_chi2, _ = self._chi2_now()
+                except Exception:
+                    new_chi2 = np.full(n, np.nan)
+                new_tab = np.concatenate(self.s.read_tables())
+                for k in np.where(~decided)[0]:
+                    c = new_chi2[k]
+                    d = cur_chi2[k] - c
+                    ok = np.isfinite(c)
+                    if ok and c < best_chi2[k]:
+                        best_chi2[k] = c
+                        best_tab[offs[k]:offs[k + 1]] = new_tab[offs[k]:offs[k + 1]]
+                    if (not ok) or d < -max_chi2_increase:
+                        lam[k] /= 2
+                        if lam[k] < min_lambda:
+                            exc[k] = True
+                            decided[k] = True
+                            dec[k] = 0.0
+                        continue
+                    cur_tab[offs[k]:offs[k + 1]] = new_tab[offs[k]:offs[k + 1]]
+                    cur_chi2[k] = c
+                    dec[k] = d
+                    decided[k] = True
+            for k in np.where(active)[0]:
+                if exc[k]:
+                    active[k] = False
+                elif -max_chi2_increase <= dec[k] < required_chi2_decrease and lam[k] == 1:
+                    converged[k] = True
+                    active[k] = False
+            if active.any() and it < maxiter - 1:
+                self.s.set_tables(cur_tab)
+                self._step()  # step at the new current states (inactive ones are ignored)
+        # best state -> model, residuals; covariance from a step at the best state
+        self.s.set_tables(best_tab)
+        self._step()
+        self._errors_into(results)
+        self.s.eval(want_M=False)
+        c2, _ = self._chi2_now()
+        self.resid_time = self.s.read_resids()[0]
+        for k, r in enumerate(results):
+            r.chi2 = float(c2[k])
+            r.converged = bool(converged[k])
+            r.status = "StepProblem" if exc[k] else ("converged" if converged[k] else "MaxiterReached")
+        return self._finish(results)
+
+    def close(self):
+        self.s.close()
+
+
+# ----------------------------------------------------------------------------------
+# single-model fitters (reference API)
+# ----------------------------------------------------------------------------------
+class Fitter:
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        self.toas = toas
+        self.model_init = model
+        self.track_mode = track_mode
+        self.model = copy.deepcopy(model)
+        self.resids_init = residuals
+        self.resids = None
+        self.converged = False
+        self.method = None
+
+    @classmethod
+    def auto(cls, toas, model, downhill=True, track_mode=None, residuals=None, **kwargs):
+        """fitter.py:252 Fitter.auto (narrowband only)."""
+        if model.has_correlated_errors:
+            return (DownhillGLSFitter if downhill else GLSFitter)(toas, model, track_mode=track_mode)
+        return (DownhillWLSFitter if downhill else WLSFitter)(toas, model, track_mode=track_mode)
+
+    def make_resids(self, model):
+        from .residuals import Residuals
+        return Residuals(self.toas, model, track_mode=self.track_mode)
+
+    def update_resids(self):
+        self.resids = self.make_resids(self.model)
+
+    def get_designmatrix(self):
+        return self.model.designmatrix(self.toas)
+
+    def _run(self, mode, plain=True, **kw):
+        bf = BatchFit([(self.model, self.toas)], mode=mode)
+        try:
+            res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
+        finally:
+            bf.close()
+        self.fitresult = res
+        self.errors = res.errors
+        self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
+        self.converged = res.converged
+        self.update_resids()
+        return res
+
+    def set_params(self, d):
+        for k, v in d.items():
+            self.model[k].value = v
+
+
+class WLSFitter(Fitter):
+    def fit_toas(self, maxiter=1, threshold=None, debug=False):
+        if self.model.has_correlated_errors:
+            pass  # the reference WLSFitter ignores correlated noise
+        res = self._run("wls", plain=True, maxiter=maxiter)
+        return res.chi2
+
+
+class GLSFitter(Fitter):
+    def fit_toas(self, maxiter=1, threshold=0, full_cov=False, debug=False):
+        if full_cov:
+            raise NotImplementedError("full_cov=True (dense N x N covariance) is outside the GPU path")
+        res = self._run("gls", plain=True, maxiter=maxiter)
+        return res.chi2
+
+
+class DownhillFitter(Fitter):
+    mode = "wls"
+
+    def fit_toas(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,
+                 debug=False, **kw):
+        # fitter.py:1168-1175: no free noise params -> required_chi2_decrease passed as
+        # both max_chi2_increase and min_lambda
+        res = self._run(self.mode, plain=False, maxiter=maxiter, required_chi2_decrease=required_chi2_decrease,
+                        max_chi2_increase=required_chi2_decrease, min_lambda=required_chi2_decrease)
+        if res.status == "StepProblem":
+            raise StepProblem("Unable to improve chi2 even with very small steps")
+        if not res.converged:
+            raise MaxiterReached(f"Convergence not detected after {maxiter} steps.")
+        return self.converged
+
+
+class DownhillWLSFitter(DownhillFitter):
+    mode = "wls"
+
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        if model.has_correlated_errors:
+            raise CorrelatedErrors(model)
+        super().__init__(toas, model, track_mode, residuals)
+
+
+class DownhillGLSFitter(DownhillFitter):
+    mode = "gls"

@@ -1,0 +1,91 @@
+"""Noise-model host preparation: scaled TOA uncertainties, PLRedNoise frequencies/weights,
+ECORR epochs.  These are parameter-independent during a timing fit (noise parameters are
+not fitted on this path) and are computed once per (model, TOAs) at upload, like the
+DMX/JUMP index tables.  Reference: noise_model.py:159-177 (scale_toa_sigma), :761-789
+(PLRedNoise weights), :808-880 (ECORR epochs, Fourier basis), :883 (powerlaw).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def scaled_sigma_us(model, toas) -> np.ndarray:
+    """ScaleToaError.scale_toa_sigma (noise_model.py:159): EQUADs in quadrature, then EFACs."""
+    sigma = np.array(toas.get_errors(), dtype=np.float64, copy=True)
+    for name in model.mask_params("EQUAD"):
+        p = model[name]
+        if p.value is None:
+            continue
+        idx = toas.select_mask(p.key, p.key_value)
+        if len(idx):
+            sigma[idx] = np.hypot(sigma[idx], float(p.value))
+    for name in model.mask_params("EFAC"):
+        p = model[name]
+        idx = toas.select_mask(p.key, p.key_value)
+        if len(idx):
+            sigma[idx] *= float(p.value)
+    return sigma
+
+
+def red_noise_freqs_weights(model, toas):
+    """(f_k [nmodes], phi [2 nmodes]) — get_rednoise_freqs (noise_model.py:847) with
+    T = max(t) - min(t) of t = tdbld*86400 in longdouble, powerlaw(f) * f[0] (:780-789)."""
+    amp, gam, nf = model.red_noise_params()
+    t = toas.tdbld * np.longdouble(86400)
+    T = t.max() - t.min()
+    f = np.linspace(1 / T, nf / T, nf)
+    ff = np.zeros(2 * nf)
+    ff[::2] = f
+    ff[1::2] = f
+    fyr = 1 / 3.16e7
+    phi = amp ** 2 / 12.0 / np.pi ** 2 * fyr ** (gam - 3) * ff ** (-gam)
+    return np.asarray(ff[::2], dtype=np.float64), phi * ff[0]
+
+
+def fourier_basis(model, toas) -> np.ndarray:
+    """Host copy of the red-noise basis for API/parity use (noise_model.py:861).  The device
+    generates the same columns inside k_eval."""
+    f, _ = red_noise_freqs_weights(model, toas)
+    t = toas.tdbld * np.longdouble(86400)
+    F = np.zeros((toas.ntoas, 2 * len(f)))
+    F[:, ::2] = np.sin(2 * np.pi * t[:, None] * f)
+    F[:, 1::2] = np.cos(2 * np.pi * t[:, None] * f)
+    return F
+
+
+def ecorr_epochs(t_sec: np.ndarray, dt: float = 1.0, nmin: int = 2):
+    """get_ecorr_epochs (noise_model.py:808): 1-s buckets on sorted times, >= nmin TOAs."""
+    if len(t_sec) == 0:
+        return []
+    isort = np.argsort(t_sec)
+    ref = [t_sec[isort[0]]]
+    buckets = [[isort[0]]]
+    for i in isort[1:]:
+        if t_sec[i] - ref[-1] < dt:
+            buckets[-1].append(i)
+        else:
+            ref.append(t_sec[i])
+            buckets.append([i])
+    return [b for b in buckets if len(b) >= nmin]
+
+
+def noise_basis(model, toas):
+    """(U, weights) in the reference's component order (timing_model.py:1704-1716)."""
+    mats, wts = [], []
+    if "EcorrNoise" in model.components or model.mask_params("ECORR"):
+        t = np.asarray(toas.tdbld * np.longdouble(86400))
+        for name in model.mask_params("ECORR"):
+            p = model[name]
+            idx = toas.select_mask(p.key, p.key_value)
+            eps = ecorr_epochs(t[idx])
+            U = np.zeros((toas.ntoas, len(eps)))
+            for j, b in enumerate(eps):
+                U[idx[b], j] = 1.0
+            mats.append(U)
+            wts.append(np.full(len(eps), (float(p.value) * 1e-6) ** 2))
+    if "PLRedNoise" in model.components:
+        mats.append(fourier_basis(model, toas))
+        wts.append(red_noise_freqs_weights(model, toas)[1])
+    if not mats:
+        return None, None
+    return np.hstack(mats), np.concatenate(wts)

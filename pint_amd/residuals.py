@@ -1,0 +1,86 @@
+"""Residuals (host mirror of reference residuals.py:40-906, TOA residuals only).
+
+All arithmetic runs on the GPU (k_eval + k_resid + k_gram/k_solve/k_woodbury); this class
+holds the results.  Values are plain float64 arrays in seconds / cycles (the reference
+returns astropy Quantities with the same numbers).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import Session, build_layout, pack_table
+
+
+class Residuals:
+    def __init__(self, toas=None, model=None, residual_type="toa", unit="s", subtract_mean=True,
+                 use_weighted_mean=True, track_mode=None, use_abs_phase=True, _session=None):
+        if residual_type != "toa":
+            raise NotImplementedError("only TOA residuals are on this hot path (wideband is out of scope)")
+        self.toas = toas
+        self.model = model
+        self.subtract_mean = subtract_mean and "PhaseOffset" not in model.components
+        self.use_weighted_mean = use_weighted_mean
+        self.use_abs_phase = use_abs_phase
+        self._chi2 = None
+        self.noise_resids = {}
+        self._track_mode_arg = track_mode
+        self.phase_resids = None
+        self.time_resids = None
+        if toas is not None and model is not None:
+            self.update()
+
+    def update(self):
+        s = Session()
+        try:
+            lay = s.add(build_layout(self.model, self.toas, track_mode=self._track_mode_arg,
+                                     subtract_mean=self.subtract_mean, use_weighted_mean=self.use_weighted_mean))
+            self.track_mode = lay.track_mode
+            s.set_instances([(lay, pack_table(lay))])
+            corr = self.model.has_correlated_errors and lay.nred > 0
+            s.eval(want_M=corr)
+            tr, pr, c2 = s.read_resids()
+            self.time_resids = tr[0]
+            self.phase_resids = pr[0]
+            self._sigma_us = lay.sigma_us
+            if corr:
+                s.fit_step(1)
+                self._chi2 = float(s.chi2_gls()[0])
+            else:
+                self._chi2 = float(c2[0])
+        finally:
+            s.close()
+
+    @property
+    def resids(self):
+        return self.time_resids
+
+    @property
+    def resids_value(self):
+        return self.time_resids
+
+    @property
+    def chi2(self) -> float:
+        return self._chi2
+
+    def calc_chi2(self, lognorm=False):
+        if lognorm:
+            raise NotImplementedError("lnlikelihood normalisation lands with §8(f) item 3")
+        return self._chi2
+
+    @property
+    def dof(self) -> int:
+        return self.toas.ntoas - (len(self.model.free_params) + 1)
+
+    @property
+    def reduced_chi2(self) -> float:
+        return self.chi2 / self.dof
+
+    def get_data_error(self, scaled=True):
+        return self._sigma_us if scaled else self.toas.get_errors()
+
+    def rms_weighted(self):
+        """Weighted RMS in microseconds (residuals.py:252 via utils.py:2002)."""
+        w = 1.0 / (self._sigma_us * 1e-6) ** 2
+        r = self.time_resids
+        m = (w * r).sum() / w.sum()
+        return float(np.sqrt((w * (r - m) ** 2).sum() / w.sum()) * 1e6)
