@@ -59,7 +59,7 @@ POSEPOCH 54800
 F0 {F0:.15f} 1
 F1 {F1:.6e} 1
 PEPOCH 54800
-DM {DM:.6f} 1
+DM {DM:.6f}
 DM1 0.0001 1
 DM2 0.00001 1
 DMEPOCH 54800

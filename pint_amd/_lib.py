@@ -74,6 +74,7 @@ def lib():
     L.pint_read_step.argtypes = [vp, dptr, dptr, dptr, dptr]
     L.pint_apply_step.argtypes = [vp, dptr]
     L.pint_sync.argtypes = [vp]
+    L.pint_debug_read.argtypes = [vp, C.c_int, dptr]
     _lib = L
     return L
 
@@ -81,7 +82,7 @@ def lib():
 EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_device_count", "pint_add_pulsar",
             "pint_set_instances", "pint_get_tables", "pint_set_tables", "pint_eval", "pint_read_resids",
             "pint_read_eval", "pint_read_designmatrix", "pint_fit_step", "pint_read_step", "pint_apply_step",
-            "pint_chi2_gls", "pint_last_timing", "pint_sync"]
+            "pint_chi2_gls", "pint_last_timing", "pint_sync", "pint_debug_read"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -9,6 +9,10 @@
 #include <math.h>
 
 #define PD __host__ __device__ __forceinline__
+// Error-free transformations must not be contracted: hipcc's device default is
+// -ffp-contract=fast, which would fuse the product inside two_prod with a later add
+// (after inlining) and destroy the exact error term.  Every dd routine opts out.
+#define DD_NOCONTRACT _Pragma("clang fp contract(off)")
 
 struct dd {
     double hi, lo;
@@ -17,22 +21,26 @@ struct dd {
 PD dd dd_make(double h, double l = 0.0) { dd r; r.hi = h; r.lo = l; return r; }
 
 PD dd two_sum(double a, double b) {
+    DD_NOCONTRACT
     double s = a + b;
     double bb = s - a;
     double e = (a - (s - bb)) + (b - bb);
     return dd_make(s, e);
 }
 PD dd quick_two_sum(double a, double b) {
+    DD_NOCONTRACT
     double s = a + b;
     double e = b - (s - a);
     return dd_make(s, e);
 }
 PD dd two_prod(double a, double b) {
+    DD_NOCONTRACT
     double p = a * b;
     double e = fma(a, b, -p);
     return dd_make(p, e);
 }
 PD dd dd_add(dd a, dd b) {
+    DD_NOCONTRACT
     dd s = two_sum(a.hi, b.hi);
     dd t = two_sum(a.lo, b.lo);
     s.lo += t.hi;
@@ -43,21 +51,25 @@ PD dd dd_add(dd a, dd b) {
 PD dd dd_neg(dd a) { return dd_make(-a.hi, -a.lo); }
 PD dd dd_sub(dd a, dd b) { return dd_add(a, dd_neg(b)); }
 PD dd dd_add_d(dd a, double b) {
+    DD_NOCONTRACT
     dd s = two_sum(a.hi, b);
     s.lo += a.lo;
     return quick_two_sum(s.hi, s.lo);
 }
 PD dd dd_mul(dd a, dd b) {
+    DD_NOCONTRACT
     dd p = two_prod(a.hi, b.hi);
     p.lo += a.hi * b.lo + a.lo * b.hi;
     return quick_two_sum(p.hi, p.lo);
 }
 PD dd dd_mul_d(dd a, double b) {
+    DD_NOCONTRACT
     dd p = two_prod(a.hi, b);
     p.lo += a.lo * b;
     return quick_two_sum(p.hi, p.lo);
 }
 PD dd dd_div_d(dd a, double b) {
+    DD_NOCONTRACT
     double q1 = a.hi / b;
     dd p = two_prod(q1, b);
     dd r = dd_sub(a, p);
@@ -69,6 +81,7 @@ PD dd dd_div_d(dd a, double b) {
     return dd_add_d(q, q3);
 }
 PD dd dd_div(dd a, dd b) {
+    DD_NOCONTRACT
     double q1 = a.hi / b.hi;
     dd r = dd_sub(a, dd_mul_d(b, q1));
     double q2 = r.hi / b.hi;
@@ -80,6 +93,7 @@ PD dd dd_div(dd a, dd b) {
 PD double dd_to_d(dd a) { return a.hi + a.lo; }
 // floor of a dd value, as a dd (exact integer)
 PD dd dd_floor(dd a) {
+    DD_NOCONTRACT
     double fh = floor(a.hi);
     if (fh == a.hi) {
         double fl = floor(a.lo);

@@ -897,6 +897,16 @@ int pint_last_timing(pint_ctx* ctx, double* ms) {
     return PINT_OK;
 }
 
+// debug/introspection: which 0 = Gram partials (sum over splits done by caller),
+// 1 = column sums of squares, 2 = Woodbury Sigma factor, 3 = L^-1 work
+int pint_debug_read(pint_ctx* ctx, int which, double* out) {
+    size_t n = which == 0 ? ctx->tot_g : which == 1 ? ctx->tot_c * ctx->nsplit : ctx->tot_s;
+    double* src = which == 0 ? ctx->d_G : which == 1 ? ctx->d_colsq : which == 2 ? ctx->d_sigL : ctx->d_work;
+    HIPCHK(hipMemcpyAsync(out, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return ctx->nsplit;
+}
+
 int pint_sync(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
