@@ -1,0 +1,219 @@
+"""Benchmark: GLS fits/s on the synthetic 68-pulsar x 10k-TOA PTA (BASELINE.json metric),
+plus chi2-grid points/s, on N MI355X GPUs of one node.
+
+One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar of the
+PTA, batched in one launch sequence per GPU: design matrix + residuals (k_eval/k_resid),
+Gram on FP64 MFMA (k_gram), Cholesky/solve/covariance (k_solve), double-double parameter
+update (k_apply), post-fit residuals and Woodbury chi2 (k_woodbury), with the fit outputs
+(steps, errors, covariances, chi2) copied back to the host.  Pulsars are sharded over
+ranks (no data-path collective; strong scaling of the fixed 68-pulsar PTA); each rank
+reports its time, the max over ranks is the step time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MI355X_HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+MI355X_FP64_MFMA_PEAK_TFLOPS = 78.6  # vendor FP64 matrix peak
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--npsr", type=int, default=68)
+    ap.add_argument("--ntoas", type=int, default=10000)
+    ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    from pint_amd.engine import Session, build_layout, pack_table
+    from pint_amd.simulation import make_pta
+
+    # ---- workload: this rank's shard of the PTA (pulsar i uses seed i) ----
+    mine = [i for i in range(args.npsr) if i % world == rank]
+    t0 = time.time()
+    from pint_amd import simulation as sim
+    from pint_amd.timing_model import get_model
+    specs = []
+    for i in mine:
+        kind = "ELL1" if i % 6 in (1, 4) else ("DD" if i % 6 == 2 else "")
+        m = get_model(sim.pta_par(i, kind))
+        specs.append(dict(model=m, start=53000, end=56652, ntoas=args.ntoas, freq=[800, 1200, 1600, 2000],
+                          obs="geocenter", error_us=0.5, add_noise=True, add_correlated_noise=True, seed=i))
+    toas = sim.make_fake_toas_batch(specs)
+    items = [(sp["model"], t) for sp, t in zip(specs, toas)]
+    log(f"[rank {rank}] generated {len(items)} pulsars x {args.ntoas} TOAs in {time.time()-t0:.1f}s")
+
+    s = Session(device=local)
+    lays = [s.add(build_layout(m, t)) for m, t in items]
+    tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
+    s.set_instances(list(zip(lays, tabs0)))
+    flat0 = np.concatenate(tabs0)
+    nin = len(lays)
+    ones = np.ones(nin)
+
+    def step():
+        s.set_tables(flat0)
+        s.eval(want_M=True)
+        s.fit_step(1)
+        ms1 = s.timing()
+        s.read_step()
+        s.apply_step(ones)
+        s.eval(want_M=False)
+        c2 = s.chi2_gls()
+        return ms1, c2
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    kt = np.zeros(4)
+    for _ in range(args.steps):
+        ms1, c2 = step()
+        kt += ms1
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kt /= args.steps
+    ms_step = dt / args.steps * 1e3
+    fits_per_s = args.npsr / (dt / args.steps)
+
+    # ---- roofline for the dominant kernel (per-launch, HIP events in the library) ----
+    n_tot = sum(l.n for l in lays)
+    K = np.array([l.K + 1 for l in lays])
+    N = np.array([l.n for l in lays])
+    gram_flops = float(np.sum(N * K * (K + 1)))       # symmetric Gram: K(K+1)/2 entries x 2N flops
+    eval_bytes = float(np.sum(N * (120 + 8 * (K - 1))))  # packed TOA row read + M row written
+    names = ["k_eval", "k_resid", "k_gram", "k_solve"]
+    dom = int(np.argmax(kt))
+    if names[dom] == "k_gram":
+        ach = gram_flops / (kt[2] * 1e-3) / 1e12
+        roof = {"kernel": "k_gram", "bound": "mfma", "achieved": round(ach, 3),
+                "peak": MI355X_FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MI355X_FP64_MFMA_PEAK_TFLOPS, 4),
+                "traffic": None}
+    elif names[dom] == "k_eval":
+        ach = eval_bytes / (kt[0] * 1e-3) / 1e9
+        roof = {"kernel": "k_eval", "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4), "traffic": None}
+    else:
+        roof = {"kernel": names[dom], "bound": "latency", "achieved": None, "peak": None, "unit": None,
+                "frac": None, "traffic": None}
+    roof["kernel_ms"] = {n: round(float(v), 4) for n, v in zip(names, kt)}
+    roof["gram_tflops"] = round(gram_flops / (kt[2] * 1e-3) / 1e12, 3) if kt[2] > 0 else None
+    roof["eval_gbs"] = round(eval_bytes / (kt[0] * 1e-3) / 1e9, 1) if kt[0] > 0 else None
+
+    # ---- chi2-grid leg (C4 shape: 256x256 (F0,F1) WLS grid of the NGC6440E fixture) ----
+    grid = None
+    if args.grid > 0:
+        grid = grid_leg(args.grid, rank, world, dist, barrier)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(items[:1])
+
+    if rank == 0:
+        out = {"metric": "GLS fits/sec, 68-PSR x 10k-TOA synthetic PTA (whole node)", "value": round(fits_per_s, 3),
+               "unit": "fits/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": None, "dtype": "f64+dd", "data": "synthetic (make_fake_toas-style, GPU-zeroed)",
+               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1",
+                          "npsr": args.npsr, "ntoas": args.ntoas, "K_cols_max": int(K.max() - 1),
+                          "parallelism": f"pulsar-sharded x{world}"},
+               "roofline": roof, "grid": grid, "cpu_baseline": cpu}
+        print(json.dumps(out))
+    s.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def grid_leg(side, rank, world, dist, barrier):
+    """chi2 over a side x side (F0, F1) grid, WLSFitter per point (gridutils.py:166 parallel
+    semantics), points sharded over ranks; timed over one full grid."""
+    import copy
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import load
+    from pint_amd import WLSFitter
+    from pint_amd.gridutils import grid_chisq
+    model, toas, _, _ = load("ngc6440e")
+    f = WLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+    s0, s1 = f.model.F0.uncertainty, f.model.F1.uncertainty
+    g0 = F0 + np.linspace(-3, 3, side) * np.longdouble(s0)
+    g1 = F1 + np.linspace(-3, 3, side) * np.longdouble(s1)
+    grid_chisq(f, ("F0", "F1"), (g0[:4], g1[:4]))  # warm-up
+    barrier()
+    t0 = time.perf_counter()
+    chi2, _ = grid_chisq(f, ("F0", "F1"), (g0, g1))
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
+            "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 3),
+            "chi2_min": float(np.nanmin(chi2))}
+
+
+def cpu_baseline(items):
+    """The oracle (numpy longdouble restatement, oracle/pint_oracle.py) timed on this host
+    on a bounded sample: GLS fits of one 10k-TOA PTA pulsar, scaled to fits/s."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pint_oracle as O
+    except Exception as e:  # oracle missing: report, never fall back
+        return {"value": None, "error": repr(e)}
+    model, toas = items[0]
+    t0 = time.perf_counter()
+    nfit = 0
+    while True:
+        O.gls_fit_from_product_inputs(model, toas)
+        nfit += 1
+        if time.perf_counter() - t0 > 10.0 or nfit >= 5:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(nfit / dt, 4), "unit": "fits/s", "cores": 1, "kind": "port",
+            "sample": f"{nfit} GLS fit(s) of one {toas.ntoas}-TOA PTA pulsar (K={len(model.free_params)+1}"
+                      f"+red noise), numpy longdouble oracle, 1 thread"}
+
+
+if __name__ == "__main__":
+    main()
