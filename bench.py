@@ -84,16 +84,18 @@ def main():
     nin = len(lays)
     ones = np.ones(nin)
 
+    s.set_lazy(True)
+
     def step():
         s.set_tables(flat0)
         s.eval(want_M=True)
         s.fit_step(1)
-        ms1 = s.timing()
-        s.read_step()
+        s.read_step()          # steps, errors, timing covariance -> host (fit outputs)
         s.apply_step(ones)
         s.eval(want_M=False)
-        c2 = s.chi2_gls()
-        return ms1, c2
+        c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
+        s.check()              # device status + HIP-event kernel timings
+        return s.timing(), c2
 
     for _ in range(args.warmup):
         step()

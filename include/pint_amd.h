@@ -141,8 +141,9 @@ int pint_read_designmatrix(pint_ctx *ctx, double *M);
  * (:2104 GLSFitter / :1425 GLSState.step, rank-reduced, full_cov=False).  The GLS mode
  * also factors the Woodbury Sigma used by pint_chi2_gls. */
 int pint_fit_step(pint_ctx *ctx, int mode);
-/* dpars/errs: (K_i+1) per instance (par units, [0] = Offset); cov: (K_i+1)^2 per instance
- * (row-major K_i x K_i at the front); chi2_lin: linearised post-step chi2. */
+/* dpars/errs: (K_i+1) per instance (par units, [0] = Offset; noise coefficients after the
+ * ncol timing columns); cov: ncol_i x ncol_i per instance (timing-parameter covariance,
+ * fitter.py:2240 parameter_covariance_matrix); chi2_lin: linearised post-step chi2. */
 int pint_read_step(pint_ctx *ctx, double *dpars, double *errs, double *cov, double *chi2_lin);
 
 /* tables += lambda[k] * dpars (double-double add): fitter.py:957 take_step_model and
@@ -152,6 +153,13 @@ int pint_apply_step(pint_ctx *ctx, const double *lambda_);
 /* GLS chi2 (Woodbury, residuals.py:567 _calc_gls_chi2 + utils.py:3074 woodbury_dot) of
  * the current residuals, per instance. */
 int pint_chi2_gls(pint_ctx *ctx, double *chi2);
+
+/* Lazy mode (1): launches return without synchronising or checking the device status;
+ * pint_check() synchronises and returns the accumulated status. */
+int pint_set_lazy(pint_ctx *ctx, int lazy);
+int pint_check(pint_ctx *ctx);
+/* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor. */
+int pint_debug_read(pint_ctx *ctx, int which, double *out);
 
 /* Device time (ms, HIP events) of the last eval / resid / gram / solve launches. */
 int pint_last_timing(pint_ctx *ctx, double *ms4);

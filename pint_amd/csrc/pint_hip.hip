@@ -49,6 +49,7 @@ struct InstDev {
     long goff;   // Gram offset (Kp*Kp per split)
     long soff;   // solve outputs offset (K*K)
     long coff;   // per-instance K vectors offset
+    long cvoff;  // compact timing covariance offset (ncol*ncol)
 };
 
 #define HIPCHK(x)                                                                    \
@@ -293,83 +294,110 @@ __global__ __launch_bounds__(512) void k_gram(const PsrDev* __restrict__ psrs, c
 }
 
 // ---------------------------------------------------------------------------------
-// k_solve: one workgroup per instance.  Normalised normal matrix in LDS (packed lower
-// triangle), Cholesky, xhat, inverse.  mode 0: WLS (fitter.py:1282-1359: whitened-column
-// normalisation, no prior); mode 1: GLS (fitter.py:2164-2202 / 1425-1507: unweighted
-// column norms, phiinv/norm^2 on the noise columns).  Also factors the Woodbury Sigma
-// (residuals.py:567-589: U=[F, 1], Phi=[phi, 1e40]) for k_woodbury.
+// k_solve: one 1024-thread workgroup per instance, everything in LDS (packed lower
+// triangle, K <= 199).  mode 0: WLS (fitter.py:1282-1359: whitened-column normalisation,
+// timing columns only); mode 1: GLS (fitter.py:2164-2202 / 1425-1507: unweighted column
+// norms, phiinv/norm^2 on the noise columns).
+//   left-looking Cholesky (row groups of 16 lanes, shuffle-reduced dot products)
+//   -> in-place triangular inverse L^-1 -> xhat = L^-T (L^-1 b) -> cov = L^-T L^-1
+// The reference solves the same normal equations with cho_factor/cho_solve (GLSFitter)
+// or an SVD (GLSState / WLS on the N x P matrix); for a positive-definite normal matrix
+// these give the same solution (SURVEY.md §7 "Linear algebra").
+// Also factors the Woodbury Sigma (residuals.py:567-589: U = [F, 1], Phi = [phi, 1e40])
+// for k_woodbury.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+constexpr int SOLVE_T = 1024;
+constexpr int RG = 16;             // lanes per row group
+constexpr int NGRP = SOLVE_T / RG;  // 64 row groups
 
-__device__ int chol_packed(double* A, int K, double* sh, int* flag) {
-    // in-place lower Cholesky of packed lower-triangular A (K x K); returns 0 if PD
-    for (int k = 0; k < K; k++) {
-        if (threadIdx.x == 0) {
-            double d = A[tri(k, k)];
-            if (!(d > 0.0)) *flag = 1;
-            A[tri(k, k)] = sqrt(d);
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+__device__ __forceinline__ double grp_sum(double v) {
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 1, 64);
+    return v;
+}
+
+// Left-looking Cholesky of packed-lower A in LDS; strict lower part is overwritten by L,
+// the diagonal of L goes to D (A's diagonal is left untouched).  Returns 1 if not PD.
+__device__ int chol_lds(double* A, double* D, int K, double* tmp) {
+    const int g = threadIdx.x / RG, l = threadIdx.x % RG;
+    for (int j = 0; j < K; j++) {
+        for (int i = j + g; i < K; i += NGRP) {
+            double sacc = 0.0;
+            for (int k = l; k < j; k += RG) sacc += A[tri(i, k)] * A[tri(j, k)];
+            sacc = grp_sum(sacc);
+            if (l == 0) tmp[i] = sacc;
         }
         __syncthreads();
-        if (*flag) return 1;
-        double lkk = A[tri(k, k)];
-        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) A[tri(i, k)] /= lkk;
-        __syncthreads();
-        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) {
-            double lik = A[tri(i, k)];
-            for (int j = k + 1; j <= i; j++) A[tri(i, j)] -= lik * A[tri(j, k)];
-        }
+        double djj = A[tri(j, j)] - tmp[j];
+        if (!(djj > 0.0)) return 1;  // uniform: every thread reads the same LDS values
+        double ljj = sqrt(djj);
+        for (int i = j + 1 + threadIdx.x; i < K; i += blockDim.x) A[tri(i, j)] = (A[tri(i, j)] - tmp[i]) / ljj;
+        if (threadIdx.x == 0) D[j] = ljj;
         __syncthreads();
     }
     return 0;
 }
 
-// solve L L^T x = b in place (x in shared vec)
-__device__ void chol_solve_packed(const double* L, int K, double* x) {
-    for (int k = 0; k < K; k++) {
+// In-place inverse of the Cholesky factor (strict lower in A, diagonal in D):
+// afterwards A's strict lower part holds L^-1 and D holds 1/diag(L).
+__device__ void trinv_lds(double* A, double* D, int K, double* tmp) {
+    const int g = threadIdx.x / RG, l = threadIdx.x % RG;
+    for (int j = K - 1; j >= 0; j--) {
+        double dj = D[j];
+        for (int i = j + 1 + g; i < K; i += NGRP) {
+            // sum_{k=j+1..i} Linv[i][k] * L[k][j]; Linv[i][i] = D[i] (already inverted)
+            double sacc = 0.0;
+            for (int k = j + 1 + l; k <= i; k += RG) {
+                double li = (k == i) ? D[i] : A[tri(i, k)];
+                sacc += li * A[tri(k, j)];
+            }
+            sacc = grp_sum(sacc);
+            if (l == 0) tmp[i] = -sacc / dj;
+        }
         __syncthreads();
-        double xk = x[k] / L[tri(k, k)];
+        for (int i = j + 1 + threadIdx.x; i < K; i += blockDim.x) A[tri(i, j)] = tmp[i];
+        if (threadIdx.x == 0) D[j] = 1.0 / dj;
         __syncthreads();
-        if (threadIdx.x == 0) x[k] = xk;
-        for (int i = k + 1 + threadIdx.x; i < K; i += blockDim.x) x[i] -= L[tri(i, k)] * xk;
     }
-    for (int k = K - 1; k >= 0; k--) {
-        __syncthreads();
-        double xk = x[k] / L[tri(k, k)];
-        __syncthreads();
-        if (threadIdx.x == 0) x[k] = xk;
-        for (int i = threadIdx.x; i < k; i += blockDim.x) x[i] -= L[tri(k, i)] * xk;
-    }
-    __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_solve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                               const double* __restrict__ tables, const double* __restrict__ Gpart,
-                                               const double* __restrict__ colsq, int nsplit, int mode,
-                                               double* __restrict__ work, double* __restrict__ dpars,
-                                               double* __restrict__ errs, double* __restrict__ cov,
-                                               double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                               int* __restrict__ status) {
+__device__ __forceinline__ double linv(const double* A, const double* D, int i, int j) {
+    return i == j ? D[i] : A[tri(i, j)];
+}
+
+__global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ tables, const double* __restrict__ Gpart,
+                                                   const double* __restrict__ colsq, int nsplit, int mode,
+                                                   double* __restrict__ work, double* __restrict__ dpars,
+                                                   double* __restrict__ errs, double* __restrict__ cov,
+                                                   double* __restrict__ chi2lin, double* __restrict__ sigL,
+                                                   int* __restrict__ status) {
     extern __shared__ double lds[];
-    __shared__ int flag;
-    __shared__ double sh[8];
+    __shared__ double sh[SOLVE_T / 64];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
-    const int K = I.K, Kp = I.Kp, ncol = S.ncol;
+    const int Kfull = I.K, Kp = I.Kp, ncol = S.ncol;
+    const int K = (mode == 0) ? ncol : Kfull;  // WLS ignores the noise basis (fitter.py:1965)
     const double* P = tables + I.toff;
-    double* A = lds;                        // packed lower, K(K+1)/2
-    double* x = lds + K * (K + 1) / 2;      // K
-    double* nrm = x + K;                    // K
+    double* A = lds;                        // packed lower K(K+1)/2
+    double* D = A + K * (K + 1) / 2;        // K
+    double* tmp = D + K;                    // K
+    double* bv = tmp + K;                   // K
+    double* yv = bv + K;                    // K
+    double* nrm = yv + K;                   // K
     const double* Gp = Gpart + I.goff;
-    auto G = [&](int i, int j) {  // full symmetric accessor, sums splits
+    auto G = [&](int i, int j) {  // symmetric accessor summing the N-split partials
         if (i > j) { int t = i; i = j; j = t; }
-        double s = 0.0;
-        for (int q = 0; q < nsplit; q++) s += Gp[(long)q * Kp * Kp + (long)i * Kp + j];
-        return s;
+        double sacc = 0.0;
+        for (int q = 0; q < nsplit; q++) sacc += Gp[(long)q * Kp * Kp + (long)i * Kp + j];
+        return sacc;
     };
-    if (threadIdx.x == 0) flag = 0;
-    // norms (normalize_designmatrix, utils.py:2879: zero norm -> 1)
+    // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
     for (int j = threadIdx.x; j < K; j += blockDim.x) {
         double v;
         if (mode == 0) v = G(j, j);
@@ -390,55 +418,68 @@ __global__ __launch_bounds__(256) void k_solve(const PsrDev* __restrict__ psrs, 
         if (i == j && mode == 1 && i >= ncol) v += 1.0 / Pd.red_phi[i - ncol] / (nrm[i] * nrm[i]);
         A[e] = v;
     }
-    for (int j = threadIdx.x; j < K; j += blockDim.x) x[j] = G(j, K) / nrm[j];
+    for (int j = threadIdx.x; j < K; j += blockDim.x) bv[j] = G(j, Kfull) / nrm[j];
+    double rwr = G(Kfull, Kfull);
     __syncthreads();
-    double rwr = G(K, K);
-    int bad = chol_packed(A, K, sh, &flag);
-    if (bad) {
+    if (chol_lds(A, D, K, tmp)) {
         if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         return;
     }
-    chol_solve_packed(A, K, x);
-    // xhat -> dpars, linearised chi2 = rWr - b.xhat (normal equations)
-    double bx = 0.0;
-    for (int j = threadIdx.x; j < K; j += blockDim.x) bx += (G(j, K) / nrm[j]) * x[j];
-    bx = block_sum<4>(bx, sh);
-    if (threadIdx.x == 0) chi2lin[inst] = rwr - bx;
-    for (int j = threadIdx.x; j < K; j += blockDim.x) dpars[I.coff + j] = x[j] / nrm[j];
-    // inverse: Linv columns (one thread per column), stored full lower in work (K*K)
-    double* Li = work + I.soff;
-    for (int c = threadIdx.x; c < K; c += blockDim.x) {
-        for (int i = 0; i < c; i++) Li[(long)i * K + c] = 0.0;
-        Li[(long)c * K + c] = 1.0 / A[tri(c, c)];
-        for (int i = c + 1; i < K; i++) {
-            double s = 0.0;
-            for (int m = c; m < i; m++) s += A[tri(i, m)] * Li[(long)m * K + c];
-            Li[(long)i * K + c] = -s / A[tri(i, i)];
-        }
+    trinv_lds(A, D, K, tmp);
+    // y = L^-1 b ; xhat = L^-T y   (row-group dot products)
+    const int g = threadIdx.x / RG, l = threadIdx.x % RG;
+    for (int m = g; m < K; m += NGRP) {
+        double sacc = 0.0;
+        for (int k = l; k <= m; k += RG) sacc += linv(A, D, m, k) * bv[k];
+        sacc = grp_sum(sacc);
+        if (l == 0) yv[m] = sacc;
     }
     __syncthreads();
-    // cov_n = Linv^T Linv ; cov = cov_n / (n n^T), only the ncol x ncol timing block is
-    // returned in full, errs for all K
-    double* C = cov + (long)I.soff;
-    for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
-        int i = e / K, j = e % K;
-        if (j < i) continue;
-        if (i >= ncol && i != j) continue;
-        double s = 0.0;
-        for (int m = j; m < K; m++) s += Li[(long)m * K + i] * Li[(long)m * K + j];
-        double v = s / (nrm[i] * nrm[j]);
-        C[(long)i * K + j] = v;
-        C[(long)j * K + i] = v;
-        if (i == j) errs[I.coff + i] = sqrt(s) / nrm[i];
+    for (int i = g; i < K; i += NGRP) {
+        double sacc = 0.0;
+        for (int m = i + l; m < K; m += RG) sacc += linv(A, D, m, i) * yv[m];
+        sacc = grp_sum(sacc);
+        if (l == 0) tmp[i] = sacc;  // xhat (normalised)
     }
-    // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column);
-    // factor into sigL (packed lower) for k_woodbury (GLS pulsars only).
-    if (S.nred > 0) {
+    __syncthreads();
+    double bx = 0.0;
+    for (int j = threadIdx.x; j < K; j += blockDim.x) {
+        bx += bv[j] * tmp[j];
+        dpars[I.coff + j] = tmp[j] / nrm[j];
+    }
+    bx = block_sum<SOLVE_T / 64>(bx, sh);
+    if (threadIdx.x == 0) chi2lin[inst] = rwr - bx;
+    // cov = L^-T L^-1 / (n n^T): timing block (ncol x ncol, compact), errs for all K
+    double* C = cov + (long)I.cvoff;
+    const int npair = ncol * (ncol + 1) / 2 + (K - ncol);
+    for (int e = threadIdx.x; e < npair; e += blockDim.x) {
+        int i, j;
+        if (e < ncol * (ncol + 1) / 2) {
+            j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (j * (j + 1) / 2 > e) j--;
+            while ((j + 1) * (j + 2) / 2 <= e) j++;
+            i = e - j * (j + 1) / 2;  // i <= j
+        } else {
+            i = j = ncol + (e - ncol * (ncol + 1) / 2);
+        }
+        double sacc = 0.0;
+        for (int m = j; m < K; m++) sacc += linv(A, D, m, i) * linv(A, D, m, j);
+        double v = sacc / (nrm[i] * nrm[j]);
+        if (j < ncol) {
+            C[(long)i * ncol + j] = v;
+            C[(long)j * ncol + i] = v;
+        }
+        if (i == j) errs[I.coff + i] = sqrt(sacc) / nrm[i];
+    }
+    // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column):
+    // factor in LDS, store L (diag in place) packed to sigL for k_woodbury.
+    if (mode == 1 && S.nred > 0) {
         __syncthreads();
-        int R = 2 * S.nred, Kn = R + 1;
-        double F0 = pval(P, S.o_F);
-        double* L = sigL + I.coff * 0 + (long)inst * 0;  // placeholder replaced below
-        L = sigL + (long)I.soff;  // reuse soff region sizing (K*K >= Kn*(Kn+1)/2)
+        const int R = 2 * S.nred, Kn = R + 1;
+        const double F0 = pval(P, S.o_F);
+        double* Sg = lds;
+        double* Dg = Sg + Kn * (Kn + 1) / 2;
+        double* tg = Dg + Kn;
         for (int e = threadIdx.x; e < Kn * (Kn + 1) / 2; e += blockDim.x) {
             int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
             while (i * (i + 1) / 2 > e) i--;
@@ -448,15 +489,17 @@ __global__ __launch_bounds__(256) void k_solve(const PsrDev* __restrict__ psrs, 
             double si = (i < R) ? 1.0 : F0, sj = (j < R) ? 1.0 : F0;
             double v = G(ci, cj) * si * sj;
             if (i == j) v += (i < R) ? 1.0 / Pd.red_phi[i] : 1e-40;
-            L[e] = v;
+            Sg[e] = v;
         }
         __syncthreads();
-        // factor in global memory (Kn small)
-        if (threadIdx.x == 0) flag = 0;
-        __syncthreads();
-        if (chol_packed(L, Kn, sh, &flag)) {
+        if (chol_lds(Sg, Dg, Kn, tg)) {
             if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+            return;
         }
+        double* L = sigL + (long)I.soff;
+        for (int e = threadIdx.x; e < Kn * (Kn + 1) / 2; e += blockDim.x) L[e] = Sg[e];
+        __syncthreads();
+        for (int i = threadIdx.x; i < Kn; i += blockDim.x) L[tri(i, i)] = Dg[i];
     }
 }
 
@@ -546,7 +589,8 @@ struct pint_ctx {
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
-    long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0;
+    long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
+    int lazy = 0;
     int nsplit = 1;
     double *d_tables = nullptr, *d_phhi = nullptr, *d_phlo = nullptr, *d_ftay = nullptr, *d_delay = nullptr;
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
@@ -681,7 +725,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     hipSetDevice(ctx->device);
     free_instances(ctx);
     ctx->inst.resize(ninst);
-    long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0;
+    long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0;
     std::vector<int> bi, br;
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
@@ -709,6 +753,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.goff = goff;
         I.soff = soff;
         I.coff = coff;
+        I.cvoff = cvoff;
+        cvoff += (long)ph.spec.ncol * ph.spec.ncol;
         toff += ph.spec.tstride;
         for (int r0 = 0; r0 <= ph.n; r0 += 256) {
             bi.push_back(k);
@@ -730,6 +776,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->tot_s = soff;
     ctx->tot_c = coff;
     ctx->tot_out = out;
+    ctx->tot_cv = cvoff;
     ctx->maxK = maxK;
     ctx->nblk = (int)bi.size();
     HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
@@ -753,12 +800,12 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(hipMalloc(&ctx->d_G, sizeof(double) * goff));
     HIPCHK(hipMalloc(&ctx->d_colsq, sizeof(double) * coff * nsplit));
     HIPCHK(hipMalloc(&ctx->d_work, sizeof(double) * soff));
-    HIPCHK(hipMalloc(&ctx->d_cov, sizeof(double) * soff));
+    HIPCHK(hipMalloc(&ctx->d_cov, sizeof(double) * (cvoff > 0 ? cvoff : 1)));
     HIPCHK(hipMalloc(&ctx->d_sigL, sizeof(double) * soff));
     HIPCHK(hipMalloc(&ctx->d_dpars, sizeof(double) * coff));
     HIPCHK(hipMalloc(&ctx->d_errs, sizeof(double) * coff));
     HIPCHK(hipMalloc(&ctx->d_lam, sizeof(double) * ninst));
-    HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * soff, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * (cvoff > 0 ? cvoff : 1), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -800,6 +847,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                        ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
     HIPCHK(hipGetLastError());
     hipEventRecord(ctx->ev[2], ctx->stream);
+    if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
     hipEventElapsedTime(&ctx->ms_eval, ctx->ev[0], ctx->ev[1]);
     hipEventElapsedTime(&ctx->ms_resid, ctx->ev[1], ctx->ev[2]);
@@ -845,13 +893,14 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     HIPCHK(hipGetLastError());
     hipEventRecord(ctx->ev[4], ctx->stream);
     int K = ctx->maxK;
-    size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 2 * K + 8);
+    size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
     if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
-    hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(256), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
+    hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_work, ctx->d_dpars,
                        ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
     HIPCHK(hipGetLastError());
     hipEventRecord(ctx->ev[5], ctx->stream);
+    if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
     hipEventElapsedTime(&ctx->ms_gram, ctx->ev[3], ctx->ev[4]);
     hipEventElapsedTime(&ctx->ms_solve, ctx->ev[4], ctx->ev[5]);
@@ -861,7 +910,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
 int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, double* chi2lin) {
     if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
     if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
-    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_s, hipMemcpyDeviceToHost, ctx->stream));
+    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, hipMemcpyDeviceToHost, ctx->stream));
     if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -872,7 +921,7 @@ int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
     hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
                        ctx->d_dpars, ctx->d_lam);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
@@ -887,6 +936,22 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
+}
+
+// Lazy mode: launches return without synchronising; pint_check() syncs, reads the device
+// status word and the event timings.
+int pint_set_lazy(pint_ctx* ctx, int lazy) {
+    ctx->lazy = lazy;
+    return PINT_OK;
+}
+
+int pint_check(pint_ctx* ctx) {
+    int rc = check_status(ctx);
+    hipEventElapsedTime(&ctx->ms_eval, ctx->ev[0], ctx->ev[1]);
+    hipEventElapsedTime(&ctx->ms_resid, ctx->ev[1], ctx->ev[2]);
+    hipEventElapsedTime(&ctx->ms_gram, ctx->ev[3], ctx->ev[4]);
+    hipEventElapsedTime(&ctx->ms_solve, ctx->ev[4], ctx->ev[5]);
+    return rc;
 }
 
 int pint_last_timing(pint_ctx* ctx, double* ms) {

@@ -398,19 +398,26 @@ class Session:
         self._check(self.L.pint_read_designmatrix(self.ctx, L.ptr(M)))
         return [m.reshape(l.K, l.n).T for m, l in zip(self._split(M, sizes), self.inst_layout)]
 
-    def read_step(self):
+    def set_lazy(self, lazy=True):
+        self._check(self.L.pint_set_lazy(self.ctx, 1 if lazy else 0))
+
+    def check(self):
+        self._check(self.L.pint_check(self.ctx))
+
+    def read_step(self, want_cov=True):
         kk = [l.K + 1 for l in self.inst_layout]
         dp = np.empty(sum(kk))
         er = np.empty(sum(kk))
-        cov = np.empty(sum(k * k for k in kk))
+        nc = [len(l.columns) for l in self.inst_layout]
+        cov = np.empty(max(1, sum(c * c for c in nc))) if want_cov else None
         cl = np.empty(len(kk))
         self._check(self.L.pint_read_step(self.ctx, L.ptr(dp), L.ptr(er), L.ptr(cov), L.ptr(cl)))
         covs = []
-        o = 0
-        for l in self.inst_layout:
-            k = l.K + 1
-            covs.append(cov[o:o + (l.K * l.K)].reshape(l.K, l.K))
-            o += k * k
+        if want_cov:
+            o = 0
+            for c in nc:
+                covs.append(cov[o:o + c * c].reshape(c, c))
+                o += c * c
         return self._split(dp, kk), self._split(er, kk), covs, cl
 
     def read_tables(self):

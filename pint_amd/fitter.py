@@ -71,9 +71,11 @@ class BatchFit:
     Each instance's model is updated in place at the end (like fitter.model).
     """
 
-    def __init__(self, items: Sequence[tuple], mode: str = "wls", session: Optional[Session] = None,
-                 layouts=None):
-        self.items = list(items)
+    def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
+                 layouts=None, tables=None):
+        """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
+        are bare parameter tables of already-uploaded pulsars, e.g. grid points)."""
+        self.items = list(items) if items is not None else None
         self.mode = mode
         self.gls = mode == "gls"
         self.s = session or Session()
@@ -89,9 +91,11 @@ class BatchFit:
                 cache[key] = lay
                 layouts.append(lay)
         self.layouts = layouts
-        self.tables = [pack_table(l, m) for l, (m, _) in zip(self.layouts, self.items)]
+        if tables is None:
+            tables = [pack_table(l, m) for l, (m, _) in zip(self.layouts, self.items)]
+        self.tables = tables
         self.s.set_instances(list(zip(self.layouts, self.tables)))
-        self.ninst = len(self.items)
+        self.ninst = len(self.layouts)
         self.use_gls_chi2 = [self.gls and l.nred > 0 for l in self.layouts]
 
     # -- helpers ------------------------------------------------------------------------
@@ -108,8 +112,10 @@ class BatchFit:
 
     def _finish(self, results):
         tabs = self.s.read_tables()
-        for (m, _), lay, t in zip(self.items, self.layouts, tabs):
-            unpack_table(lay, t, m)
+        self.final_tables = tabs
+        if self.items is not None:
+            for (m, _), lay, t in zip(self.items, self.layouts, tabs):
+                unpack_table(lay, t, m)
         return results
 
     def _errors_into(self, results):
@@ -117,12 +123,13 @@ class BatchFit:
         for k, (res, lay) in enumerate(zip(results, self.layouts)):
             nc = len(lay.columns)
             res.errors = er[k][:nc].copy()
-            res.cov = cov[k][:nc, :nc].copy()
+            res.cov = cov[k].copy()
             res.noise_coeffs = dp[k][nc:lay.K].copy()
             res.labels = list(lay.columns)
-            m = self.items[k][0]
-            for j, name in enumerate(lay.columns[1:], start=1):
-                m[name].uncertainty = float(res.errors[j])
+            if self.items is not None:
+                m = self.items[k][0]
+                for j, name in enumerate(lay.columns[1:], start=1):
+                    m[name].uncertainty = float(res.errors[j])
 
     # -- plain WLS/GLS (fitter.py:1965-2087, :2104-2289) -------------------------------
     def fit_plain(self, maxiter=1):

@@ -43,7 +43,10 @@ def _dist():
 def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
                executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
     """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
-    Returns (chi2 array of meshgrid shape, dict of extra parameter arrays)."""
+    Returns (chi2 array of meshgrid shape, dict of extra parameter arrays).  `executor`,
+    `ncpu`, `chunksize` are accepted for API compatibility: the points run as one GPU batch
+    per rank instead of a process pool."""
+    from .engine import Session, build_layout, pack_table, split_ld
     mode, down = _fit_kind(ftr)
     out, flat = grid_points(parvalues)
     shape = out[0].shape
@@ -55,46 +58,46 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     base = copy.deepcopy(ftr.model)
     for p in parnames:
         base[p].frozen = True
-    items = []
-    for i in range(lo, hi):
-        m = copy.deepcopy(base)
-        for p, vals in zip(parnames, flat):
-            m[p].value = LD(vals[i]) if (m[p].long_double or m[p].kind == "mjd") else float(vals[i])
-        items.append((m, ftr.toas))
     chi2 = np.full(hi - lo, np.nan)
     extra = {e: np.full(hi - lo, np.nan) for e in extraparnames}
-    if items:
-        bf = BatchFit(items, mode=mode, layouts=_shared_layouts(items, mode))
+    if hi > lo:
+        s = Session()
         try:
+            lay = s.add(build_layout(base, ftr.toas, use_gls_basis=(mode == "gls")))
+            t0 = pack_table(lay, base)
+            tabs = np.tile(t0, (hi - lo, 1))
+            for p, vals in zip(parnames, flat):
+                v = np.asarray(vals[lo:hi], dtype=np.longdouble)
+                h = v.astype(np.float64)
+                l = (v - h.astype(np.longdouble)).astype(np.float64)
+                o = lay.offsets[p]
+                tabs[:, o] = h
+                tabs[:, o + 1] = l
+            bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (hi - lo), tables=list(tabs))
             if down:
-                kw = dict(maxiter=fitargs.get("maxiter", 10))
                 rq = fitargs.get("required_chi2_decrease", 1e-2)
-                res = bf.fit_downhill(required_chi2_decrease=rq, max_chi2_increase=rq, min_lambda=rq, **kw)
+                res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
+                                      max_chi2_increase=rq, min_lambda=rq)
             else:
                 res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1))
-        finally:
-            bf.close()
-        for k, r in enumerate(res):
-            # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
-            chi2[k] = np.nan if (down and r.status == "MaxiterReached") else r.chi2
+            for k, r in enumerate(res):
+                # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
+                chi2[k] = np.nan if (down and r.status == "MaxiterReached") else r.chi2
             for e in extraparnames:
-                extra[e][k] = float(items[k][0][e].value)
+                o = lay.offsets[e]
+                extra[e][:] = [float(np.longdouble(t[o]) + np.longdouble(t[o + 1])) for t in bf.final_tables]
+        finally:
+            s.close()
     if dist and world > 1:
         import torch
+        use_cuda = dist.get_backend() == "nccl"
         buf = torch.full((per,), float("nan"), dtype=torch.float64)
         buf[: hi - lo] = torch.from_numpy(chi2)
-        gathered = [torch.empty_like(buf) for _ in range(world)]
-        dev_buf = buf.cuda() if torch.cuda.is_available() and dist.get_backend() == "nccl" else buf
-        gl = [g.to(dev_buf.device) for g in gathered]
-        dist.all_gather(gl, dev_buf)
+        if use_cuda:
+            buf = buf.cuda()
+        gl = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(gl, buf)
         chi2_all = torch.cat([g.cpu() for g in gl]).numpy()[:npts]
     else:
         chi2_all = chi2
-    extraout = {e: extra[e] for e in extraparnames}
-    return chi2_all.reshape(shape), extraout
-
-
-def _shared_layouts(items, mode):
-    """All grid points share one uploaded pulsar (same TOAs and structure)."""
-    from .engine import build_layout
-    return None
+    return chi2_all.reshape(shape), {e: extra[e] for e in extraparnames}
