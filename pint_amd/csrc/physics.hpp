@@ -556,6 +556,7 @@ PD double spin_freq(const pint_spec_t& S, const double* P, double dt) {
 
 // Evaluate one TOA.  If M != nullptr, writes the design-matrix row (column-major, leading
 // dimension ld) for columns 0..ncol-1 (timing_model.py:2164-2173).
+template <int BIN>
 PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut& o, double* M,
                  long ld) {
     o.status = 0;
@@ -617,10 +618,10 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
     BinState B;
     B.status = 0;
-    if (S.binary == 1) {
+    if (BIN == 1) {
         ell1_setup(S, P, t.tdb, delay, B);
         delay += B.delay;
-    } else if (S.binary == 2) {
+    } else if (BIN == 2) {
         ddm_setup(S, P, t.tdb, delay, B);
         delay += B.delay;
         if (B.status) o.status = B.status;
@@ -722,7 +723,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut
                 v = chain * r;
             } break;
             case PINT_COL_BIN: {
-                double d = (S.binary == 1) ? ell1_deriv(B, idx) : ddm_deriv(B, idx);
+                double d = 0.0;
+                if (BIN == 1) d = ell1_deriv(B, idx);
+                if (BIN == 2) d = ddm_deriv(B, idx);
                 v = chain * d * bin_unit_factor(idx);
             } break;
             default: v = 0.0;

@@ -85,11 +85,12 @@ __device__ double block_sum(double v, double* sh) {
 // ---------------------------------------------------------------------------------
 // k_eval: one thread per TOA row (row n = TZR TOA)
 // ---------------------------------------------------------------------------------
+template <int WANT_M, int BIN>
 __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
                                               const double* __restrict__ tables, double* __restrict__ ph_hi,
                                               double* __restrict__ ph_lo, double* __restrict__ ftay,
-                                              double* __restrict__ delay_out, double* __restrict__ Mout, int want_M,
+                                              double* __restrict__ delay_out, double* __restrict__ Mout,
                                               int* __restrict__ status) {
     int b = blockIdx.x;
     int ii = blk_inst[b];
@@ -114,24 +115,24 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
     t.dmx_a = Pd.dmx_a[r];
     t.dmx_b = Pd.dmx_b[r];
     EvalOut o;
-    double* Mrow = (want_M && r < n) ? (Mout + I.moff + r) : nullptr;
-    eval_toa(S, P, t, o, Mrow, n);
+    double* Mrow = (WANT_M && r < n) ? (Mout + I.moff + r) : nullptr;
+    eval_toa<BIN>(S, P, t, o, Mrow, n);
     if (o.status) atomicOr(status, 1 << o.status);
     ph_hi[I.roff + r] = o.phase.hi;
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
     delay_out[I.roff + r] = o.delay;
-    if (Mrow && S.nred > 0) {
+    if (WANT_M && Mrow && S.nred > 0) {
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
         // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.
         dd ts = dd_mul_d(t.tdb, DAYSEC);
         for (int k = 0; k < S.nred; k++) {
             dd x = dd_mul_d(ts, Pd.red_freq[k]);
             double fr = dd_to_d(dd_sub(x, dd_floor(x)));
-            double s, c;
-            sincos(TWO_PI * fr, &s, &c);
-            Mrow[(long)(S.ncol + 2 * k) * n] = s;
-            Mrow[(long)(S.ncol + 2 * k + 1) * n] = c;
+            double sn, cs;
+            sincos(TWO_PI * fr, &sn, &cs);
+            Mrow[(long)(S.ncol + 2 * k) * n] = sn;
+            Mrow[(long)(S.ncol + 2 * k + 1) * n] = cs;
         }
     }
 }
@@ -196,12 +197,41 @@ __global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, 
 // ---------------------------------------------------------------------------------
 constexpr int GCH = 16;       // TOAs per LDS chunk (multiple of 4)
 constexpr int GMAXKP = 256;   // max padded columns
-constexpr int GWAVES = 8;
-constexpr int GMAXT = 17;     // ceil(136 / 8) upper tiles per wave at Kp=256
+constexpr int GWAVES = 16;
+constexpr int GTHREADS = GWAVES * 64;
+constexpr int GMAXT = 9;      // ceil(136 / 16) upper tiles per wave at Kp=256
+constexpr int GMAXQ = GCH * GMAXKP / GTHREADS;  // staged elements per thread per chunk (16)
 
-__global__ __launch_bounds__(512) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                              const double* __restrict__ M, const double* __restrict__ rtime,
-                                              int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
+// Stage the next chunk into registers (coalesced: 32 consecutive TOAs of one column per
+// 32 lanes), so the global loads of chunk c+1 overlap the MFMAs of chunk c.
+struct GramStage {
+    double v[GMAXQ];
+    double w;
+};
+
+__device__ __forceinline__ void gram_load(GramStage& st, const double* __restrict__ Mi, const double* __restrict__ ri,
+                                          const double* __restrict__ sigma, long c0, long i1, int n, int K, int Kp) {
+    const int tid = threadIdx.x;
+    const int ii = tid % GCH;
+    const long toa = c0 + ii;
+    const bool ok = toa < i1;
+    double sg = ok ? sigma[toa] : 1.0;
+    st.w = ok ? 1.0 / (sg * sg) : 0.0;
+#pragma unroll
+    for (int q = 0; q < GMAXQ; q++) {
+        int c = tid / GCH + (GTHREADS / GCH) * q;
+        double v = 0.0;
+        if (ok && c < Kp) {
+            if (c < K) v = Mi[(long)c * n + toa];
+            else if (c == K) v = ri[toa];
+        }
+        st.v[q] = v;
+    }
+}
+
+__global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ M, const double* __restrict__ rtime,
+                                                   int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
     extern __shared__ double lds[];
     const int inst = blockIdx.y, split = blockIdx.x;
     const InstDev I = insts[inst];
@@ -219,79 +249,85 @@ __global__ __launch_bounds__(512) void k_gram(const PsrDev* __restrict__ psrs, c
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nt = Kp / 16;
     const int ntiles = nt * (nt + 1) / 2;
+    // this wave's tiles: a contiguous run of the row-major upper-triangular tile list, so
+    // consecutive tiles share the A row-block
+    const int t_lo = (ntiles * wave) / GWAVES, t_hi = (ntiles * (wave + 1)) / GWAVES;
+    int ti0 = 0, tj0 = 0;
+    {
+        int rem = t_lo;
+        while (rem >= nt - ti0) { rem -= nt - ti0; ti0++; }
+        tj0 = ti0 + rem;
+    }
     double4_t acc[GMAXT];
 #pragma unroll
     for (int t = 0; t < GMAXT; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    // per-thread column-sum-of-squares accumulators: thread handles columns c = tid/GCH + 32*j
-    double csq[GMAXKP / 32];
-#pragma unroll
-    for (int j = 0; j < GMAXKP / 32; j++) csq[j] = 0.0;
+    double csq = 0.0;  // thread tid < K owns column tid
+    GramStage st;
+    if (i0 < i1) gram_load(st, Mi, ri, Pd.sigma, i0, i1, n, K, Kp);
     for (long c0 = i0; c0 < i1; c0 += GCH) {
-        __syncthreads();
-        // stage: element e -> (row i = e % GCH, col c = e / GCH): 16 consecutive TOAs per column
-        const int ii = tid % GCH;
-        const long toa = c0 + ii;
-        const bool ok = toa < i1;
-        const double w = ok ? 1.0 / (Pd.sigma[toa] * Pd.sigma[toa]) : 0.0;
+        __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
+        {
+            const int ii = tid % GCH;
 #pragma unroll
-        for (int j = 0; j < GMAXKP / 32; j++) {
-            int c = tid / GCH + 32 * j;
-            if (c < Kp) {
-                double v = 0.0;
-                if (ok) {
-                    if (c < K) v = Mi[(long)c * n + toa];
-                    else if (c == K) v = ri[toa];
+            for (int q = 0; q < GMAXQ; q++) {
+                int c = tid / GCH + (GTHREADS / GCH) * q;
+                if (c < Kp) {
+                    double v = st.v[q];
+                    Ts[ii * stride + c] = v;
+                    Ws[ii * stride + c] = st.w * v;
                 }
-                Ts[ii * stride + c] = v;
-                Ws[ii * stride + c] = w * v;
-                if (c < K) csq[j] += v * v;
             }
         }
         __syncthreads();
+        if (c0 + GCH < i1) gram_load(st, Mi, ri, Pd.sigma, c0 + GCH, i1, n, K, Kp);  // prefetch next
+        if (tid < K) {
+#pragma unroll 8
+            for (int r = 0; r < GCH; r++) {
+                double v = Ts[r * stride + tid];
+                csq += v * v;
+            }
+        }
 #pragma unroll
-        for (int t = 0; t < GMAXT; t++) {
-            int tt = wave + t * GWAVES;
-            if (tt < ntiles) {
-                // decode upper-triangular tile index tt -> (ti <= tj)
-                int ti = 0, rem = tt;
-                while (rem >= nt - ti) { rem -= nt - ti; ti++; }
-                int tj = ti + rem;
+        for (int kk = 0; kk < GCH / 4; kk++) {
+            const int row = kk * 4 + (lane >> 4);
+            const double* Tr = Ts + row * stride + (lane & 15);
+            const double* Wr = Ws + row * stride + (lane & 15);
+            int ti = ti0, tj = tj0, cur_i = -1;
+            double a = 0.0;
 #pragma unroll
-                for (int kk = 0; kk < GCH / 4; kk++) {
-                    int row = kk * 4 + (lane >> 4);
-                    double a = Ts[row * stride + ti * 16 + (lane & 15)];
-                    double bb = Ws[row * stride + tj * 16 + (lane & 15)];
+            for (int t = 0; t < GMAXT; t++) {
+                if (t_lo + t < t_hi) {
+                    if (ti != cur_i) {
+                        cur_i = ti;
+                        a = Tr[ti * 16];
+                    }
+                    double bb = Wr[tj * 16];
                     acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[t], 0, 0, 0);
+                    if (++tj == nt) { ti++; tj = ti; }
                 }
             }
         }
     }
     // write partial tiles: D[row=(lane>>4)+4*r][col=lane&15]
     double* G = Gpart + I.goff + (long)split * Kp * Kp;
+    {
+        int ti = ti0, tj = tj0;
 #pragma unroll
-    for (int t = 0; t < GMAXT; t++) {
-        int tt = wave + t * GWAVES;
-        if (tt < ntiles) {
-            int ti = 0, rem = tt;
-            while (rem >= nt - ti) { rem -= nt - ti; ti++; }
-            int tj = ti + rem;
+        for (int t = 0; t < GMAXT; t++) {
+            if (t_lo + t < t_hi) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                int row = ti * 16 + (lane >> 4) + 4 * q;
-                int col = tj * 16 + (lane & 15);
-                G[(long)row * Kp + col] = acc[t][q];
+                for (int q = 0; q < 4; q++) {
+                    int row = ti * 16 + (lane >> 4) + 4 * q;
+                    int col = tj * 16 + (lane & 15);
+                    G[(long)row * Kp + col] = acc[t][q];
+                }
+                if (++tj == nt) { ti++; tj = ti; }
             }
         }
     }
-    // column sums of squares: reduce over the GCH lanes sharing a column
-#pragma unroll
-    for (int j = 0; j < GMAXKP / 32; j++) {
-        double v = csq[j];
-        for (int o = GCH / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        int c = tid / GCH + 32 * j;
-        if ((tid % GCH) == 0 && c < K) colsq[(I.coff + c) * nsplit + split] = v;
-    }
+    if (tid < K) colsq[(I.coff + tid) * nsplit + split] = csq;
 }
+
 
 // ---------------------------------------------------------------------------------
 // k_solve: one 1024-thread workgroup per instance, everything in LDS (packed lower
@@ -589,6 +625,7 @@ struct pint_ctx {
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
+    int blk_off[4] = {0, 0, 0, 0};  // block ranges per binary type (0 none, 1 ELL1, 2 DD)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
     int lazy = 0;
     int nsplit = 1;
@@ -726,7 +763,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     free_instances(ctx);
     ctx->inst.resize(ninst);
     long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0;
-    std::vector<int> bi, br;
+    std::vector<int> bti[3], btr[3];
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
@@ -734,8 +771,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         if (ctx->psrs[p].n > maxN) maxN = ctx->psrs[p].n;
     }
     // N-split for the Gram so the launch fills the 256 CUs
-    int nsplit = (256 + ninst - 1) / ninst;
-    int maxsplit = (maxN + 255) / 256;
+    int nsplit = (1024 + ninst - 1) / ninst;
+    int maxsplit = (maxN + 4 * GCH - 1) / (4 * GCH);
     if (nsplit > maxsplit) nsplit = maxsplit;
     if (nsplit < 1) nsplit = 1;
     ctx->nsplit = nsplit;
@@ -756,9 +793,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.cvoff = cvoff;
         cvoff += (long)ph.spec.ncol * ph.spec.ncol;
         toff += ph.spec.tstride;
+        int bt = ph.spec.binary;
         for (int r0 = 0; r0 <= ph.n; r0 += 256) {
-            bi.push_back(k);
-            br.push_back(r0);
+            bti[bt].push_back(k);
+            btr[bt].push_back(r0);
         }
         roff += ph.n + 1;
         moff += (long)ph.n * ph.K;
@@ -778,6 +816,13 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->tot_out = out;
     ctx->tot_cv = cvoff;
     ctx->maxK = maxK;
+    std::vector<int> bi, br;
+    for (int t = 0; t < 3; t++) {
+        ctx->blk_off[t] = (int)bi.size();
+        bi.insert(bi.end(), bti[t].begin(), bti[t].end());
+        br.insert(br.end(), btr[t].begin(), btr[t].end());
+    }
+    ctx->blk_off[3] = (int)bi.size();
     ctx->nblk = (int)bi.size();
     HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
@@ -838,10 +883,22 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     hipSetDevice(ctx->device);
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     hipEventRecord(ctx->ev[0], ctx->stream);
-    hipLaunchKernelGGL(k_eval, dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_blk_inst,
-                       ctx->d_blk_row0, ctx->d_tables, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
-                       want_M, ctx->d_status);
-    HIPCHK(hipGetLastError());
+    for (int t = 0; t < 3; t++) {
+        int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
+        if (nb == 0) continue;
+        const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
+        const int* br = ctx->d_blk_row0 + ctx->blk_off[t];
+#define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
+        hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
+                           ctx->d_tables, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, ctx->d_status)
+        if (want_M) {
+            if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
+        } else {
+            if (t == 0) PINT_EVAL_LAUNCH(0, 0); else if (t == 1) PINT_EVAL_LAUNCH(0, 1); else PINT_EVAL_LAUNCH(0, 2);
+        }
+#undef PINT_EVAL_LAUNCH
+        HIPCHK(hipGetLastError());
+    }
     hipEventRecord(ctx->ev[1], ctx->stream);
     hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
                        ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
@@ -888,7 +945,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     int stride = maxKp + ((maxKp & 31) == 0 ? 16 : 0);
     size_t lds_g = sizeof(double) * 2 * GCH * stride;
     hipEventRecord(ctx->ev[3], ctx->stream);
-    hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(512), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
+    hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(GTHREADS), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->d_M, ctx->d_rt, ctx->nsplit, ctx->d_G, ctx->d_colsq);
     HIPCHK(hipGetLastError());
     hipEventRecord(ctx->ev[4], ctx->stream);
