@@ -154,6 +154,14 @@ int pint_apply_step(pint_ctx *ctx, const double *lambda_);
  * the current residuals, per instance. */
 int pint_chi2_gls(pint_ctx *ctx, double *chi2);
 
+/* ECORR epochs of pulsar `psr` (replaces EcorrNoise.ecorr_basis_weight_pair,
+ * noise_model.py:385-427 + get_ecorr_epochs :808): nep epochs, TOA index lists in CSR form
+ * (ep_ptr[nep+1], ep_idx[ep_ptr[nep]]) and the prior variance phi_e = ECORR^2 in s^2.
+ * The quantisation block is eliminated by a Schur complement on the device (its normal
+ * matrix block is diagonal), so it adds no Gram columns.  Call before pint_set_instances. */
+int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const int32_t *ep_idx,
+                   const double *ep_phi);
+
 /* Lazy mode (1): launches return without synchronising or checking the device status;
  * pint_check() synchronises and returns the accumulated status. */
 int pint_set_lazy(pint_ctx *ctx, int lazy);

@@ -32,10 +32,13 @@ struct PsrDev {
     const pint_spec_t* spec;
     const double* red_freq;  // nred
     const double* red_phi;   // 2*nred
+    const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
+    const int32_t* ep_idx;
+    const double* ep_phi;    // nep prior variances (s^2)
     int n;
     int K;   // ncol + 2*nred
     int Kp;  // padded K+1 (residual column) to 16
-    int pad;
+    int nep; // ECORR epochs (eliminated by Schur complement)
 };
 
 struct InstDev {
@@ -50,6 +53,8 @@ struct InstDev {
     long soff;   // solve outputs offset (K*K)
     long coff;   // per-instance K vectors offset
     long cvoff;  // compact timing covariance offset (ncol*ncol)
+    long eoff;   // ECORR epoch sums offset (nep*Kp) and per-epoch scalars (eoff/Kp)
+    long epoff;  // per-epoch scalar offset (nep)
 };
 
 #define HIPCHK(x)                                                                    \
@@ -210,42 +215,94 @@ struct GramStage {
 };
 
 __device__ __forceinline__ void gram_load(GramStage& st, const double* __restrict__ Mi, const double* __restrict__ ri,
-                                          const double* __restrict__ sigma, long c0, long i1, int n, int K, int Kp) {
+                                          const double* __restrict__ sigma, const double* __restrict__ Ei,
+                                          const double* __restrict__ eDi, long c0, long i1, int n, int K, int Kp) {
     const int tid = threadIdx.x;
     const int ii = tid % GCH;
     const long toa = c0 + ii;
     const bool ok = toa < i1;
-    double sg = ok ? sigma[toa] : 1.0;
-    st.w = ok ? 1.0 / (sg * sg) : 0.0;
+    const bool real = toa < n;
+    double w;
+    if (!ok) w = 0.0;
+    else if (real) { double sg = sigma[toa]; w = 1.0 / (sg * sg); }
+    else w = -1.0 / eDi[toa - n];  // ECORR Schur row: -s_e s_e^T / D_e
+    st.w = w;
 #pragma unroll
     for (int q = 0; q < GMAXQ; q++) {
         int c = tid / GCH + (GTHREADS / GCH) * q;
         double v = 0.0;
         if (ok && c < Kp) {
-            if (c < K) v = Mi[(long)c * n + toa];
+            if (!real) v = Ei[(toa - n) * Kp + c];
+            else if (c < K) v = Mi[(long)c * n + toa];
             else if (c == K) v = ri[toa];
         }
         st.v[q] = v;
     }
 }
 
+// ECORR epoch sums (one wave per epoch, lanes over columns): s_e = sum_{i in e} w_i [T|r]_i,
+// W_e = sum w_i, D_e = W_e + 1/phi_e.  The quantisation-matrix block of the GLS normal
+// matrix is diagonal (disjoint epochs), so eliminating it is the rank-nep update
+// G' = G - sum_e s_e s_e^T / D_e, folded into k_gram as nep extra rows of weight -1/D_e.
+__global__ __launch_bounds__(256) void k_ecorr(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                               const double* __restrict__ M, const double* __restrict__ rtime,
+                                               double* __restrict__ esum, double* __restrict__ eD,
+                                               double* __restrict__ eW) {
+    const int inst = blockIdx.y;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (e >= Pd.nep) return;
+    const int n = I.n, K = I.K, Kp = I.Kp;
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + (I.roff - inst);
+    const int a = Pd.ep_ptr[e], b = Pd.ep_ptr[e + 1];
+    double* out = esum + I.eoff + (long)e * Kp;
+    for (int c = lane; c < Kp; c += 64) {
+        double acc = 0.0;
+        if (c <= K) {
+            const double* col = (c < K) ? Mi + (long)c * n : ri;
+            for (int k = a; k < b; k++) {
+                int i = Pd.ep_idx[k];
+                double sg = Pd.sigma[i];
+                acc += col[i] / (sg * sg);
+            }
+        }
+        out[c] = acc;
+    }
+    if (lane == 0) {
+        double W = 0.0;
+        for (int k = a; k < b; k++) {
+            double sg = Pd.sigma[Pd.ep_idx[k]];
+            W += 1.0 / (sg * sg);
+        }
+        eW[I.epoff + e] = W;
+        eD[I.epoff + e] = W + 1.0 / Pd.ep_phi[e];
+    }
+}
+
 __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ M, const double* __restrict__ rtime,
-                                                   int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
+                                                   const double* __restrict__ esum, const double* __restrict__ eD,
+                                                   int nsplit, int mode, double* __restrict__ Gpart,
+                                                   double* __restrict__ colsq) {
     extern __shared__ double lds[];
     const int inst = blockIdx.y, split = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const int n = I.n, K = I.K, Kp = I.Kp;
+    const long nrow = n + (mode == 1 ? Pd.nep : 0);  // + ECORR Schur rows (GLS only)
+    const double* Ei = esum + I.eoff;
+    const double* eDi = eD + I.epoff;
     const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
     double* Ts = lds;                  // [GCH][stride]
     double* Ws = lds + GCH * stride;   // weighted copy
     const double* Mi = M + I.moff;
     const double* ri = rtime + (I.roff - inst);
-    long per = (n + nsplit - 1) / nsplit;
+    long per = (nrow + nsplit - 1) / nsplit;
     per = (per + GCH - 1) / GCH * GCH;
     long i0 = split * per, i1 = i0 + per;
-    if (i1 > n) i1 = n;
+    if (i1 > nrow) i1 = nrow;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nt = Kp / 16;
     const int ntiles = nt * (nt + 1) / 2;
@@ -263,7 +320,7 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
     for (int t = 0; t < GMAXT; t++) acc[t] = (double4_t){0, 0, 0, 0};
     double csq = 0.0;  // thread tid < K owns column tid
     GramStage st;
-    if (i0 < i1) gram_load(st, Mi, ri, Pd.sigma, i0, i1, n, K, Kp);
+    if (i0 < i1) gram_load(st, Mi, ri, Pd.sigma, Ei, eDi, i0, i1, n, K, Kp);
     for (long c0 = i0; c0 < i1; c0 += GCH) {
         __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
         {
@@ -279,12 +336,19 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
             }
         }
         __syncthreads();
-        if (c0 + GCH < i1) gram_load(st, Mi, ri, Pd.sigma, c0 + GCH, i1, n, K, Kp);  // prefetch next
+        if (c0 + GCH < i1) gram_load(st, Mi, ri, Pd.sigma, Ei, eDi, c0 + GCH, i1, n, K, Kp);  // prefetch next
         if (tid < K) {
+            if (c0 + GCH <= n) {
 #pragma unroll 8
-            for (int r = 0; r < GCH; r++) {
-                double v = Ts[r * stride + tid];
-                csq += v * v;
+                for (int r = 0; r < GCH; r++) {
+                    double v = Ts[r * stride + tid];
+                    csq += v * v;
+                }
+            } else {
+                for (int r = 0; r < (int)(n - c0); r++) {  // unweighted norms: real rows only
+                    double v = Ts[r * stride + tid];
+                    csq += v * v;
+                }
             }
         }
 #pragma unroll
@@ -509,7 +573,7 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
     }
     // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column):
     // factor in LDS, store L (diag in place) packed to sigL for k_woodbury.
-    if (mode == 1 && S.nred > 0) {
+    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
         __syncthreads();
         const int R = 2 * S.nred, Kn = R + 1;
         const double F0 = pval(P, S.o_F);
@@ -540,10 +604,15 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
 }
 
 // Woodbury GLS chi2 of the current residuals (utils.py:3074-3126 woodbury_dot):
-// chi2 = r^T N^-1 r - d^T Sigma^-1 d, d = U^T N^-1 r, U = [F, 1].
+// chi2 = r^T N^-1 r - d^T Sigma^-1 d, d = U^T N^-1 r, U = [F, ECORR, 1].  The ECORR block
+// is eliminated: with c_e = sum_{i in e} w_i r_i, r^T N^-1 r -= sum c_e^2 / D_e and
+// d_j -= sum_e B_je c_e / D_e (B from k_ecorr's epoch sums); Sigma' (Schur-reduced) was
+// factored by k_solve from the reduced Gram.
 __global__ __launch_bounds__(256) void k_woodbury(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                   const double* __restrict__ M, const double* __restrict__ rtime,
-                                                  const double* __restrict__ sigL, double* __restrict__ chi2) {
+                                                  const double* __restrict__ sigL, const double* __restrict__ esum,
+                                                  const double* __restrict__ eD, const double* __restrict__ eW,
+                                                  double* __restrict__ ecs, double* __restrict__ chi2) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
     const int inst = blockIdx.x;
@@ -561,12 +630,29 @@ __global__ __launch_bounds__(256) void k_woodbury(const PsrDev* __restrict__ psr
         rwr += ri[i] * ri[i] * w;
         rw1 += ri[i] * w;
     }
+    // ECORR epochs: c_e / D_e of the current residuals
+    const int nep = Pd.nep;
+    const double* Ei = esum + I.eoff;
+    double* ce = ecs + I.epoff;
+    for (int e = threadIdx.x; e < nep; e += blockDim.x) {
+        double c = 0.0;
+        for (int k = Pd.ep_ptr[e]; k < Pd.ep_ptr[e + 1]; k++) {
+            int i = Pd.ep_idx[k];
+            c += ri[i] / (Pd.sigma[i] * Pd.sigma[i]);
+        }
+        double De = eD[I.epoff + e];
+        rwr -= c * c / De;
+        rw1 -= eW[I.epoff + e] * c / De;
+        ce[e] = c / De;
+    }
+    __syncthreads();
     rwr = block_sum<4>(rwr, sh);
     rw1 = block_sum<4>(rw1, sh);
     for (int j = 0; j < R; j++) {
         const double* col = Mi + (long)(S.ncol + j) * n;
         double s = 0.0;
         for (int i = threadIdx.x; i < n; i += blockDim.x) s += col[i] * ri[i] / (Pd.sigma[i] * Pd.sigma[i]);
+        for (int e = threadIdx.x; e < nep; e += blockDim.x) s -= Ei[(long)e * I.Kp + S.ncol + j] * ce[e];
         s = block_sum<4>(s, sh);
         if (threadIdx.x == 0) d[j] = s;
     }
@@ -633,6 +719,9 @@ struct pint_ctx {
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
     double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
+    double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr;
+    long tot_e = 0, tot_ep = 0;
+    int max_nep = 0;
     int* d_status = nullptr;
     int maxK = 0;
     hipEvent_t ev[8];
@@ -654,6 +743,16 @@ static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const 
     else HIPCHK(hipMemset(p, 0, bytes));
     ph.bufs.push_back(p);
     dst = (const T*)p;
+    return 0;
+}
+
+static int refresh_psrs(pint_ctx* ctx) {
+    if (ctx->d_psrs) hipFree(ctx->d_psrs);
+    ctx->d_psrs = nullptr;
+    std::vector<PsrDev> all;
+    for (auto& p : ctx->psrs) all.push_back(p.dev);
+    HIPCHK(hipMalloc(&ctx->d_psrs, sizeof(PsrDev) * all.size()));
+    HIPCHK(hipMemcpy(ctx->d_psrs, all.data(), sizeof(PsrDev) * all.size(), hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -686,7 +785,8 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
-                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g};
+                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
+                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs};
     for (auto p : ps) dfree(*p);
     ctx->ninst = 0;
 }
@@ -748,13 +848,30 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     d.K = K;
     d.Kp = Kp;
     ctx->psrs.push_back(ph);
-    // refresh device descriptor array
-    if (ctx->d_psrs) hipFree(ctx->d_psrs);
-    std::vector<PsrDev> all;
-    for (auto& p : ctx->psrs) all.push_back(p.dev);
-    HIPCHK(hipMalloc(&ctx->d_psrs, sizeof(PsrDev) * all.size()));
-    HIPCHK(hipMemcpy(ctx->d_psrs, all.data(), sizeof(PsrDev) * all.size(), hipMemcpyHostToDevice));
+    if (refresh_psrs(ctx)) return -PINT_E_HIP;
     return (int)ctx->psrs.size() - 1;
+}
+
+int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const int32_t* ep_idx,
+                   const double* ep_phi) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || nep < 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    PsrHost& ph = ctx->psrs[psr];
+    if (nep == 0) { ph.dev.nep = 0; return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK; }
+    if (!ep_ptr || !ep_idx || !ep_phi || ep_ptr[0] != 0) { ctx->err = "bad ECORR epoch lists"; return PINT_E_INVALID; }
+    for (int e = 0; e < nep; e++) {
+        if (ep_ptr[e + 1] < ep_ptr[e] || !(ep_phi[e] > 0.0)) { ctx->err = "bad ECORR epoch"; return PINT_E_INVALID; }
+    }
+    for (int k = 0; k < ep_ptr[nep]; k++) {
+        if (ep_idx[k] < 0 || ep_idx[k] >= ph.n) { ctx->err = "ECORR TOA index out of range"; return PINT_E_INVALID; }
+    }
+    int rc = 0;
+    rc |= upload(ctx, ph, ep_ptr, (size_t)nep + 1, ph.dev.ep_ptr);
+    rc |= upload(ctx, ph, ep_idx, (size_t)ep_ptr[nep], ph.dev.ep_idx);
+    rc |= upload(ctx, ph, ep_phi, (size_t)nep, ph.dev.ep_phi);
+    if (rc) return PINT_E_HIP;
+    ph.dev.nep = nep;
+    return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
 }
 
 int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
@@ -762,7 +879,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     hipSetDevice(ctx->device);
     free_instances(ctx);
     ctx->inst.resize(ninst);
-    long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0;
+    long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0, eoff = 0, epoff = 0;
+    int max_nep = 0;
     std::vector<int> bti[3], btr[3];
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
@@ -791,6 +909,11 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.soff = soff;
         I.coff = coff;
         I.cvoff = cvoff;
+        I.eoff = eoff;
+        I.epoff = epoff;
+        eoff += (long)ph.dev.nep * I.Kp;
+        epoff += ph.dev.nep;
+        if (ph.dev.nep > max_nep) max_nep = ph.dev.nep;
         cvoff += (long)ph.spec.ncol * ph.spec.ncol;
         toff += ph.spec.tstride;
         int bt = ph.spec.binary;
@@ -816,6 +939,9 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->tot_out = out;
     ctx->tot_cv = cvoff;
     ctx->maxK = maxK;
+    ctx->tot_e = eoff;
+    ctx->tot_ep = epoff;
+    ctx->max_nep = max_nep;
     std::vector<int> bi, br;
     for (int t = 0; t < 3; t++) {
         ctx->blk_off[t] = (int)bi.size();
@@ -850,6 +976,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(hipMalloc(&ctx->d_dpars, sizeof(double) * coff));
     HIPCHK(hipMalloc(&ctx->d_errs, sizeof(double) * coff));
     HIPCHK(hipMalloc(&ctx->d_lam, sizeof(double) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * (cvoff > 0 ? cvoff : 1), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -945,8 +1075,13 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     int stride = maxKp + ((maxKp & 31) == 0 ? 16 : 0);
     size_t lds_g = sizeof(double) * 2 * GCH * stride;
     hipEventRecord(ctx->ev[3], ctx->stream);
+    if (mode == 1 && ctx->max_nep > 0) {
+        hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
+        HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(GTHREADS), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->d_M, ctx->d_rt, ctx->nsplit, ctx->d_G, ctx->d_colsq);
+                       ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->nsplit, mode, ctx->d_G, ctx->d_colsq);
     HIPCHK(hipGetLastError());
     hipEventRecord(ctx->ev[4], ctx->stream);
     int K = ctx->maxK;
@@ -988,7 +1123,8 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     int R = 0;
     for (auto& p : ctx->psrs) R = 2 * p.spec.nred > R ? 2 * p.spec.nred : R;
     hipLaunchKernelGGL(k_woodbury, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
-                       ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_sigL, ctx->d_chi2g);
+                       ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_ecs,
+                       ctx->d_chi2g);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

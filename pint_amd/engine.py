@@ -46,6 +46,11 @@ class PulsarLayout:
     psr_id: int = -1
     track_mode: str = "nearest"
     keep: list = field(default_factory=list)
+    # ECORR epochs (noise_model.py:385-427): CSR TOA lists + prior variances (s^2)
+    nep: int = 0
+    ep_ptr: Optional[np.ndarray] = None
+    ep_idx: Optional[np.ndarray] = None
+    ep_phi: Optional[np.ndarray] = None
 
 
 def _track_mode(model, toas, track_mode):
@@ -196,18 +201,24 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
     if use_gls_basis and "PLRedNoise" in model.components:
         rf, rp = red_noise_freqs_weights(model, toas)
         nred = len(rf)
+    ep_lists, ep_phi = [], []
     if model.mask_params("ECORR") and use_gls_basis:
-        eps_n = 0
         from .noise import ecorr_epochs
         t = np.asarray(toas.tdbld * LD(86400))
         for name in model.mask_params("ECORR"):
             p = model[name]
-            eps_n += len(ecorr_epochs(t[toas.select_mask(p.key, p.key_value)]))
-        if eps_n > 0:
-            raise NotImplementedError("ECORR epochs with >= 2 TOAs: Schur-complement GLS lands next round")
+            idx = toas.select_mask(p.key, p.key_value)
+            for b in ecorr_epochs(t[idx]):
+                ep_lists.append(np.sort(idx[b]))
+                ep_phi.append((float(p.value) * 1e-6) ** 2)
     spec.nred = nred
     lay = PulsarLayout(model=model, toas=toas, n=toas.ntoas, offsets=offs, tstride=tstride, columns=cols,
                        spec=spec, nred=nred, K=len(cols) + 2 * nred, red_freq=rf, red_phi=rp, track_mode=tm)
+    if ep_lists:
+        lay.nep = len(ep_lists)
+        lay.ep_ptr = np.concatenate([[0], np.cumsum([len(e) for e in ep_lists])]).astype(np.int32)
+        lay.ep_idx = np.concatenate(ep_lists).astype(np.int32)
+        lay.ep_phi = np.asarray(ep_phi, dtype=np.float64)
     return lay
 
 
@@ -344,6 +355,9 @@ class Session:
         if pid < 0:
             self._check(-pid)
         lay.psr_id = pid
+        if lay.nep > 0:
+            self._check(self.L.pint_set_ecorr(self.ctx, pid, lay.nep, L.ptr(lay.ep_ptr, C.c_int32),
+                                              L.ptr(lay.ep_idx, C.c_int32), L.ptr(lay.ep_phi)))
         self.layouts.append(lay)
         return lay
 

@@ -96,7 +96,7 @@ class BatchFit:
         self.tables = tables
         self.s.set_instances(list(zip(self.layouts, self.tables)))
         self.ninst = len(self.layouts)
-        self.use_gls_chi2 = [self.gls and l.nred > 0 for l in self.layouts]
+        self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in self.layouts]
 
     # -- helpers ------------------------------------------------------------------------
     def _chi2_now(self):

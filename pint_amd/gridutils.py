@@ -40,6 +40,28 @@ def _dist():
     return None
 
 
+def shard_range(npts: int, rank: int, world: int):
+    """Contiguous block [lo, hi) of the flattened meshgrid owned by `rank`."""
+    per = (npts + world - 1) // world
+    return per, rank * per, min(npts, (rank + 1) * per)
+
+
+def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
+    """All-gather every rank's chi2 block (NaN-padded to `per`) -> the full flat array.
+    Over RCCL when the process group is nccl, gloo on CPU."""
+    if dist is None or dist.get_world_size() == 1:
+        return local
+    import torch
+    world = dist.get_world_size()
+    buf = torch.full((per,), float("nan"), dtype=torch.float64)
+    buf[: len(local)] = torch.from_numpy(np.ascontiguousarray(local, dtype=np.float64))
+    if dist.get_backend() == "nccl":
+        buf = buf.cuda()
+    gl = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(gl, buf)
+    return torch.cat([g.cpu() for g in gl]).numpy()[:npts]
+
+
 def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
                executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
     """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
@@ -53,8 +75,7 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     npts = flat[0].size
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
-    per = (npts + world - 1) // world
-    lo, hi = rank * per, min(npts, (rank + 1) * per)
+    per, lo, hi = shard_range(npts, rank, world)
     base = copy.deepcopy(ftr.model)
     for p in parnames:
         base[p].frozen = True
@@ -88,16 +109,5 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
                 extra[e][:] = [float(np.longdouble(t[o]) + np.longdouble(t[o + 1])) for t in bf.final_tables]
         finally:
             s.close()
-    if dist and world > 1:
-        import torch
-        use_cuda = dist.get_backend() == "nccl"
-        buf = torch.full((per,), float("nan"), dtype=torch.float64)
-        buf[: hi - lo] = torch.from_numpy(chi2)
-        if use_cuda:
-            buf = buf.cuda()
-        gl = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(gl, buf)
-        chi2_all = torch.cat([g.cpu() for g in gl]).numpy()[:npts]
-    else:
-        chi2_all = chi2
+    chi2_all = gather_blocks(chi2, per, npts, dist)
     return chi2_all.reshape(shape), {e: extra[e] for e in extraparnames}

@@ -70,8 +70,12 @@ def ecorr_epochs(t_sec: np.ndarray, dt: float = 1.0, nmin: int = 2):
 
 
 def noise_basis(model, toas):
-    """(U, weights) in the reference's component order (timing_model.py:1704-1716)."""
+    """(U, weights) in the reference's NoiseComponent_list order (timing_model.py:1133,
+    :1690): PLRedNoise before EcorrNoise (pinned by the B1855 fixture's noise_dims)."""
     mats, wts = [], []
+    if "PLRedNoise" in model.components:
+        mats.append(fourier_basis(model, toas))
+        wts.append(red_noise_freqs_weights(model, toas)[1])
     if "EcorrNoise" in model.components or model.mask_params("ECORR"):
         t = np.asarray(toas.tdbld * np.longdouble(86400))
         for name in model.mask_params("ECORR"):
@@ -83,9 +87,6 @@ def noise_basis(model, toas):
                 U[idx[b], j] = 1.0
             mats.append(U)
             wts.append(np.full(len(eps), (float(p.value) * 1e-6) ** 2))
-    if "PLRedNoise" in model.components:
-        mats.append(fourier_basis(model, toas))
-        wts.append(red_noise_freqs_weights(model, toas)[1])
     if not mats:
         return None, None
     return np.hstack(mats), np.concatenate(wts)

@@ -36,7 +36,7 @@ class Residuals:
                                      subtract_mean=self.subtract_mean, use_weighted_mean=self.use_weighted_mean))
             self.track_mode = lay.track_mode
             s.set_instances([(lay, pack_table(lay))])
-            corr = self.model.has_correlated_errors and lay.nred > 0
+            corr = self.model.has_correlated_errors and (lay.nred > 0 or lay.nep > 0)
             s.eval(want_M=corr)
             tr, pr, c2 = s.read_resids()
             self.time_resids = tr[0]

@@ -75,7 +75,8 @@ class TimingModel:
         astro = [n for n, p in self._params.items() if p.component.startswith("Astrometry")]
         spin = [n for n, p in self._params.items() if p.component == "Spindown"]
         rest = []
-        for comp in DELAY_ORDER + ["Binary", "AbsPhase", "PhaseJump"] + NOISE:
+        order = [("Binary" if c.startswith("Binary") else c) for c in DELAY_ORDER]
+        for comp in dict.fromkeys(order + ["AbsPhase", "PhaseJump"] + NOISE):
             if comp.startswith("Astrometry"):
                 continue
             rest += [n for n, p in self._params.items() if p.component == comp]

@@ -1,0 +1,264 @@
+"""GPU parity tests: the HIP path (libpint_hip.so through the C-ABI) against the golden
+vectors captured from the reference and against the CPU oracle on seeded inputs.
+
+Bars: residuals <= 1 ns (we hold ~10-50 ps: the reference's own
+longdouble rounding), design matrix 1e-9 relative per column, fitted parameters <= 1e-3
+sigma, chi2 1e-9 relative stage-wise (the end-to-end chi2 floor is documented in
+tests/test_oracle_golden.py::test_gls_fit)."""
+import copy
+
+import numpy as np
+import pytest
+
+from golden_util import load, ref_value
+
+import pint_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd"]
+GLS_NAMES = ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855"]
+
+
+@pytest.fixture(scope="module", params=NAMES)
+def fx(request):
+    return (request.param,) + load(request.param)
+
+
+def test_native_library_loaded():
+    import pint_amd._lib as L
+    lib = L.lib()
+    assert lib.pint_device_count() >= 1
+
+
+def test_delays(fx):
+    from pint_amd.engine import evaluate_delay_phase
+    name, model, toas, z, meta = fx
+    dp = evaluate_delay_phase(model, toas)
+    assert np.max(np.abs(dp["delay"] - z["delay_total"])) < 5e-12
+    assert abs(dp["tzr_delay"] - z["tzr_delay"][0]) < 5e-12
+
+
+def test_residuals(fx):
+    from pint_amd import Residuals
+    name, model, toas, z, meta = fx
+    r = Residuals(toas, model)
+    assert r.track_mode == meta["res_track_mode"]
+    assert np.max(np.abs(r.time_resids - z["res_time"])) < 1e-10       # bar 1 ns
+    assert np.sqrt(np.mean((r.time_resids - z["res_time"]) ** 2)) < 3e-11
+    if "noise_U_ncols" not in z or int(z["noise_U_ncols"][0]) == 0:
+        assert abs(r.chi2 / meta["res_chi2"] - 1) < 1e-7
+
+
+def test_designmatrix(fx):
+    name, model, toas, z, meta = fx
+    M, params, units = model.designmatrix(toas)
+    assert params == meta["dm_params"]
+    ref = z["dm_M"]
+    if "dm_rows" in z:
+        M = M[z["dm_rows"]]
+    scale = np.max(np.abs(ref), axis=0)
+    scale[scale == 0] = 1
+    err = np.max(np.abs(M - ref) / scale, axis=0)
+    bad = {params[j]: err[j] for j in np.where(err > 1e-9)[0]}
+    assert not bad, bad
+
+
+def test_designmatrix_vs_oracle_all_rows(fx):
+    name, model, toas, z, meta = fx
+    M, params, _ = model.designmatrix(toas)
+    Mo, no = O.designmatrix(O.from_product_model(model), O.toas_from_product(toas))
+    assert params == no
+    scale = np.max(np.abs(Mo), axis=0)
+    scale[scale == 0] = 1
+    assert np.max(np.abs(M - Mo) / scale) < 1e-9
+
+
+def test_wls_fit_ngc():
+    from pint_amd import WLSFitter
+    model, toas, z, meta = load("ngc6440e")
+    f = WLSFitter(toas, model)
+    c2 = f.fit_toas(maxiter=1)
+    assert abs(c2 / meta["wls_chi2"] - 1) < 1e-7
+    for p in meta["wls_params"]:
+        s = meta["wls_errors"][p]
+        d = float((np.longdouble(f.model[p].value) - ref_value(meta, "wls_params", p)) / np.longdouble(s))
+        assert abs(d) < 1e-3, (p, d)
+        assert abs(f.model[p].uncertainty / s - 1) < 1e-6, p
+    cov = f.parameter_covariance_matrix.matrix
+    assert np.allclose(cov, z["wls_cov"], rtol=1e-6, atol=0)
+    assert np.max(np.abs(f.resids.time_resids - z["wls_post_resid"])) < 1e-10
+
+
+@pytest.mark.parametrize("name", GLS_NAMES)
+def test_gls_fit(name):
+    from pint_amd import GLSFitter
+    model, toas, z, meta = load(name)
+    f = GLSFitter(toas, model)
+    c2 = f.fit_toas(maxiter=1)
+    worst = 0.0
+    for p in meta["gls_params"]:
+        s = meta["gls_errors"][p]
+        d = float((np.longdouble(f.model[p].value) - ref_value(meta, "gls_params", p)) / np.longdouble(s))
+        worst = max(worst, abs(d))
+        # FP64 normal-equation solves agree to ~cond*eps: J0740's normalised normal matrix
+        # has cond 7e12 (B1855 with the dense ECORR block 1e16, 3e11 after elimination),
+        # so its weakest-determined errors agree with the reference's LAPACK to ~1e-3
+        etol = {"j0740": 5e-3, "b1855": 1e-4}.get(name, 1e-5)
+        assert abs(f.model[p].uncertainty / s - 1) < etol, (p, f.model[p].uncertainty / s - 1)
+    assert worst < 1e-3, worst
+    assert abs(c2 / meta["gls_chi2"] - 1) < 5e-6
+    assert np.max(np.abs(f.resids.time_resids - z["gls_post_resid"])) < 2e-10
+
+
+@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd"])
+def test_downhill_gls(name):
+    from pint_amd import DownhillGLSFitter
+    from pint_amd.fitter import MaxiterReached, StepProblem
+    model, toas, z, meta = load(name)
+    f = DownhillGLSFitter(toas, model)
+    try:
+        f.fit_toas(maxiter=10)
+        status = "converged"
+    except (MaxiterReached, StepProblem) as e:
+        status = type(e).__name__
+    assert status == meta["down_status"]
+    assert abs(f.resids.chi2 / meta["down_chi2"] - 1) < 5e-6
+    for p in meta["down_params"]:
+        s = meta["down_errors"][p]
+        d = float((np.longdouble(f.model[p].value) - ref_value(meta, "down_params", p)) / np.longdouble(s))
+        assert abs(d) < 5e-2, (p, d)  # see test_oracle_golden.test_downhill_gls
+
+
+def test_downhill_wls_ngc():
+    from pint_amd import DownhillWLSFitter
+    model, toas, z, meta = load("ngc6440e")
+    f = DownhillWLSFitter(toas, model)
+    f.fit_toas(maxiter=10)
+    assert f.converged == meta["dwls_converged"]
+    assert abs(f.resids.chi2 / meta["dwls_chi2"] - 1) < 1e-7
+    for p in meta["dwls_params"]:
+        s = meta["dwls_errors"][p]
+        d = float((np.longdouble(f.model[p].value) - ref_value(meta, "dwls_params", p)) / np.longdouble(s))
+        assert abs(d) < 1e-3, (p, d)
+
+
+def test_grid_chisq_ngc():
+    from pint_amd import WLSFitter
+    from pint_amd.gridutils import grid_chisq
+    model, toas, z, meta = load("ngc6440e")
+    f = WLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    g0 = z["grid_F0_hi"].astype(np.longdouble) + z["grid_F0_lo"]
+    g1 = z["grid_F1_hi"].astype(np.longdouble) + z["grid_F1_lo"]
+    c2, _ = grid_chisq(f, ("F0", "F1"), (g0, g1))
+    assert c2.shape == z["grid_chi2_parallel"].shape
+    assert np.allclose(c2, z["grid_chi2_parallel"], rtol=1e-7, atol=0)
+
+
+# ---- seeded perturbations against the oracle --------------------------------------------
+@pytest.mark.parametrize("name,seed", [("pta_ell1", 1), ("pta_dd", 2), ("j0740", 3), ("b1855", 4), ("pta_iso", 5)])
+def test_perturbed_vs_oracle(name, seed):
+    """Move every free parameter by a few sigma (seeded) and compare the GPU residuals,
+    design matrix and one GLS step with the oracle at the same inputs."""
+    from pint_amd import Residuals
+    from pint_amd.engine import evaluate_designmatrix
+    model, toas, z, meta = load(name)
+    rng = np.random.default_rng(seed)
+    for p in model.free_params:
+        s = model[p].uncertainty or 0.0
+        if s > 0:
+            model[p].value = np.longdouble(model[p].value) + np.longdouble(rng.normal() * 3 * s)
+    om, ot = O.from_product_model(model), O.toas_from_product(toas)
+    ro = O.residuals(om, ot)
+    r = Residuals(toas, model, track_mode="nearest")
+    ro = O.residuals(om, ot, track_mode="nearest")
+    assert np.max(np.abs(r.time_resids - ro["time"])) < 1e-10
+    M, params, _ = evaluate_designmatrix(model, toas)
+    Mo, _ = O.designmatrix(om, ot)
+    scale = np.max(np.abs(Mo), axis=0)
+    scale[scale == 0] = 1
+    assert np.max(np.abs(M - Mo) / scale) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["pta_dd", "b1855"])
+def test_gls_step_vs_oracle(name):
+    from pint_amd.fitter import BatchFit
+    model, toas, z, meta = load(name)
+    bf = BatchFit([(model, toas)], mode="gls")
+    bf._step()
+    dp, er, cov, _ = bf.s.read_step()
+    st = O.gls_step(O.from_product_model(model), O.toas_from_product(toas))
+    ncol = len(st["names"])
+    e = st["errs"]
+    assert np.max(np.abs(er[0][:ncol] / e - 1)) < 1e-4
+    assert np.max(np.abs((dp[0][:ncol] - st["dpars"]) / e)) < 1e-3
+    bf.close()
+
+
+# ---- batching invariance / full-size properties ---------------------------------------------
+def test_batch_invariance():
+    """The same pulsar fitted alone and as instance k of a 37-instance batch (mixed with other
+    pulsars, different N-splits) gives the same result to rounding."""
+    from pint_amd.fitter import BatchFit
+    a = load("pta_dd")
+    b = load("pta_ell1")
+    single = BatchFit([(copy.deepcopy(a[0]), a[1])], mode="gls")
+    r1 = single.fit_plain(1)
+    items = []
+    for k in range(37):
+        src = a if k % 3 == 1 else b
+        items.append((copy.deepcopy(src[0]), src[1]))
+    batch = BatchFit(items, mode="gls")
+    rs = batch.fit_plain(1)
+    for k in range(37):
+        if k % 3 == 1:
+            assert abs(rs[k].chi2 / r1[0].chi2 - 1) < 1e-10
+            assert np.allclose(rs[k].errors, r1[0].errors, rtol=1e-9)
+    single.close()
+    batch.close()
+
+
+def test_simulate_and_fit_recovers_truth():
+    """Full-size (10k TOAs) property test: fake TOAs from a DD model with white noise, perturb
+    the model by a few sigma, one GLS fit comes back to the truth within 5 sigma and gives
+    reduced chi2 ~ 1."""
+    from pint_amd import GLSFitter, simulation as sim
+    from pint_amd.timing_model import get_model
+    truth = get_model(sim.pta_par(2, "DD"))
+    toas = sim.make_fake_toas_batch([dict(model=truth, start=53000, end=56652, ntoas=10000,
+                                          freq=[800, 1200, 1600, 2000], obs="geocenter", error_us=0.5,
+                                          add_noise=True, add_correlated_noise=False, seed=7)])[0]
+    model = copy.deepcopy(truth)
+    f0 = GLSFitter(toas, copy.deepcopy(truth))
+    f0.fit_toas(maxiter=1)
+    errs = {p: f0.model[p].uncertainty for p in truth.free_params}
+    rng = np.random.default_rng(11)
+    for p in truth.free_params:
+        model[p].value = np.longdouble(model[p].value) + np.longdouble(2 * rng.normal() * errs[p])
+    f = GLSFitter(toas, model)
+    c2 = f.fit_toas(maxiter=3)
+    for p in truth.free_params:
+        d = float((np.longdouble(f.model[p].value) - np.longdouble(truth[p].value)) / np.longdouble(errs[p]))
+        assert abs(d) < 5, (p, d)
+    dof = toas.ntoas - len(truth.free_params) - 1
+    assert 0.9 < c2 / dof < 1.1
+
+
+# ---- edge cases -----------------------------------------------------------------------------
+@pytest.mark.parametrize("nsub", [7, 16, 17, 33, 61])
+def test_ragged_subsets_vs_oracle(nsub):
+    """TOA counts that are not multiples of the Gram chunk (16) or wave size (64)."""
+    from pint_amd import WLSFitter
+    model, toas, z, meta = load("ngc6440e")
+    sub = toas[np.arange(nsub)]
+    m = copy.deepcopy(model)
+    if nsub < 8:
+        m.free_params = ["F0", "F1"]
+    f = WLSFitter(sub, m)
+    c2 = f.fit_toas(maxiter=1)
+    om = O.from_product_model(m)
+    om2, st, c2o = O.fit_once(om, O.toas_from_product(sub), gls=False)
+    assert abs(c2 - c2o) <= 1e-7 * max(1.0, c2o)
+    for j, p in enumerate(st["names"][1:], start=1):
+        assert abs(f.model[p].uncertainty / st["errs"][j] - 1) < 1e-7, p
