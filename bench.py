@@ -101,7 +101,7 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    kt = np.zeros(4)
+    kt = np.zeros(6)
     for _ in range(args.steps):
         ms1, c2 = step()
         kt += ms1
@@ -116,29 +116,47 @@ def main():
     ms_step = dt / args.steps * 1e3
     fits_per_s = args.npsr / (dt / args.steps)
 
-    # ---- roofline for the dominant kernel (per-launch, HIP events in the library) ----
-    n_tot = sum(l.n for l in lays)
-    K = np.array([l.K + 1 for l in lays])
+    # ---- roofline: algorithmic work per launch (DESIGN.md "Kernels") / HIP-event time ----
+    K = np.array([l.K for l in lays])                # timing + red-noise columns
+    P = np.array([len(l.columns) for l in lays])     # timing columns
     N = np.array([l.n for l in lays])
-    gram_flops = float(np.sum(N * K * (K + 1)))       # symmetric Gram: K(K+1)/2 entries x 2N flops
-    eval_bytes = float(np.sum(N * (120 + 8 * (K - 1))))  # packed TOA row read + M row written
-    names = ["k_eval", "k_resid", "k_gram", "k_solve"]
-    dom = int(np.argmax(kt))
-    if names[dom] == "k_gram":
-        ach = gram_flops / (kt[2] * 1e-3) / 1e12
-        roof = {"kernel": "k_gram", "bound": "mfma", "achieved": round(ach, 3),
-                "peak": MI355X_FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MI355X_FP64_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None}
-    elif names[dom] == "k_eval":
-        ach = eval_bytes / (kt[0] * 1e-3) / 1e9
-        roof = {"kernel": "k_eval", "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4), "traffic": None}
+    R = K - P
+    flops = {
+        "k_gram": float(np.sum(N * (K + 1) * (K + 2))),          # symmetric [T|r]^T W [T|r]
+        "k_solve": float(np.sum(K.astype(float) ** 3)),          # chol K^3/3 + inverse/cov 2K^3/3
+        "k_woodbury": float(np.sum(2 * N * (R + 2))),            # F^T W r, r^T W r, 1^T W r
+    }
+    nbytes = {
+        "k_eval_M": float(np.sum(N * (120 + 8 * P))),            # SURVEY.md §8(d) B_dm
+        "k_eval": float(np.sum(N * (120 + 8))),                  # B_res
+        "k_resid": float(np.sum(N * (8 * 4 + 8 * 2))),          # phase hi/lo, ftaylor, sigma in; resid out
+    }
+    names = ["k_eval", "k_resid", "k_gram", "k_solve", "k_eval_M", "k_woodbury"]
+    kms = {n: float(v) for n, v in zip(names, kt)}
+    dom = max(kms, key=kms.get)
+    peaks = load_peaks()
+    if dom in flops and dom != "k_woodbury":
+        ach = flops[dom] / (kms[dom] * 1e-3) / 1e12
+        pk = MI355X_FP64_MFMA_PEAK_TFLOPS
+        roof = {"kernel": dom, "bound": "mfma" if dom == "k_gram" else "fp64", "achieved": round(ach, 3),
+                "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4)}
     else:
-        roof = {"kernel": names[dom], "bound": "latency", "achieved": None, "peak": None, "unit": None,
-                "frac": None, "traffic": None}
-    roof["kernel_ms"] = {n: round(float(v), 4) for n, v in zip(names, kt)}
-    roof["gram_tflops"] = round(gram_flops / (kt[2] * 1e-3) / 1e12, 3) if kt[2] > 0 else None
-    roof["eval_gbs"] = round(eval_bytes / (kt[0] * 1e-3) / 1e9, 1) if kt[0] > 0 else None
+        b = nbytes.get(dom, flops.get(dom, 0.0) * 4)
+        ach = b / (kms[dom] * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4)}
+    roof["traffic"] = pmc_traffic(dom, args)
+    roof["kernel_ms"] = {n: round(v, 4) for n, v in kms.items()}
+    roof["per_kernel"] = {}
+    for n in names:
+        if kms[n] <= 0:
+            continue
+        if n in flops:
+            roof["per_kernel"][n] = {"TFLOP/s": round(flops[n] / (kms[n] * 1e-3) / 1e12, 3)}
+        if n in nbytes:
+            roof["per_kernel"][n] = {"GB/s": round(nbytes[n] / (kms[n] * 1e-3) / 1e9, 1)}
+    if peaks:
+        roof["measured_peaks"] = peaks
 
     # ---- chi2-grid leg (C4 shape: 256x256 (F0,F1) WLS grid of the NGC6440E fixture) ----
     grid = None
@@ -162,6 +180,29 @@ def main():
     s.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def load_peaks():
+    """Peaks measured on an MI355X by bench/peaks.hip (committed under profiles/)."""
+    f = os.path.join(ROOT, "profiles", "peaks_r01.json")
+    if os.path.exists(f):
+        with open(f) as fh:
+            return json.load(fh)
+    return None
+
+
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    same bench command (FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md, + WRITE_SIZE)."""
+    f = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        d = json.load(fh)
+    if d.get("workload") != f"pta{args.npsr}x{args.ntoas}":
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes")
 
 
 def grid_leg(side, rank, world, dist, barrier):

@@ -169,8 +169,10 @@ int pint_check(pint_ctx *ctx);
 /* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor. */
 int pint_debug_read(pint_ctx *ctx, int which, double *out);
 
-/* Device time (ms, HIP events) of the last eval / resid / gram / solve launches. */
-int pint_last_timing(pint_ctx *ctx, double *ms4);
+/* Device time (ms, HIP events on the library's stream) of the last launches, 6 values:
+ * [0] eval (no design matrix), [1] resid, [2] ecorr+gram, [3] solve, [4] eval with design
+ * matrix, [5] Woodbury chi2. */
+int pint_last_timing(pint_ctx *ctx, double *ms6);
 int pint_sync(pint_ctx *ctx);
 
 #ifdef __cplusplus

@@ -608,32 +608,77 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
 // is eliminated: with c_e = sum_{i in e} w_i r_i, r^T N^-1 r -= sum c_e^2 / D_e and
 // d_j -= sum_e B_je c_e / D_e (B from k_ecorr's epoch sums); Sigma' (Schur-reduced) was
 // factored by k_solve from the reduced Gram.
-__global__ __launch_bounds__(256) void k_woodbury(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                  const double* __restrict__ M, const double* __restrict__ rtime,
-                                                  const double* __restrict__ sigL, const double* __restrict__ esum,
-                                                  const double* __restrict__ eD, const double* __restrict__ eW,
-                                                  double* __restrict__ ecs, double* __restrict__ chi2) {
+//   k_wdot    grid (nsplit, ninst): per-split partial dot products F_j^T W r, r^T W r,
+//             1^T W r; one wave per column (coalesced column reads, shuffle reduction)
+//   k_wsolve  one workgroup per instance: split sums, ECORR correction, forward
+//             substitution with Sigma's Cholesky factor, chi2
+__global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              const double* __restrict__ M, const double* __restrict__ rtime,
+                                              int nsplit, int stride, double* __restrict__ wpart) {
+    const int inst = blockIdx.y, split = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int n = I.n, R = 2 * S.nred;
+    const double* ri = rtime + (I.roff - inst);
+    const double* Mi = M + I.moff;
+    long per = (n + nsplit - 1) / nsplit;
+    long i0 = split * per, i1 = i0 + per;
+    if (i1 > n) i1 = n;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* out = wpart + ((long)inst * nsplit + split) * stride;
+    for (int j = wave; j < R + 2; j += 4) {
+        double acc = 0.0;
+        if (j < R) {
+            const double* col = Mi + (long)(S.ncol + j) * n;
+            for (long i = i0 + lane; i < i1; i += 64) {
+                double sg = Pd.sigma[i];
+                acc += col[i] * ri[i] / (sg * sg);
+            }
+        } else if (j == R) {  // r^T W r
+            for (long i = i0 + lane; i < i1; i += 64) {
+                double sg = Pd.sigma[i];
+                acc += ri[i] * ri[i] / (sg * sg);
+            }
+        } else {  // 1^T W r
+            for (long i = i0 + lane; i < i1; i += 64) {
+                double sg = Pd.sigma[i];
+                acc += ri[i] / (sg * sg);
+            }
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) out[j] = acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                const double* __restrict__ rtime, const double* __restrict__ sigL,
+                                                const double* __restrict__ esum, const double* __restrict__ eD,
+                                                const double* __restrict__ eW, const double* __restrict__ wpart,
+                                                int nsplit, int stride, double* __restrict__ ecs,
+                                                double* __restrict__ chi2) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
-    const int n = I.n;
+    const int R = 2 * S.nred, Kn = R + 1;
     const double* ri = rtime + (I.roff - inst);
-    const double* Mi = M + I.moff;
-    int R = 2 * S.nred, Kn = R + 1;
     double* d = lds;  // Kn
+    const double* wp = wpart + (long)inst * nsplit * stride;
     double rwr = 0.0, rw1 = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        double w = 1.0 / (Pd.sigma[i] * Pd.sigma[i]);
-        rwr += ri[i] * ri[i] * w;
-        rw1 += ri[i] * w;
+    if (threadIdx.x == 0) {
+        for (int q = 0; q < nsplit; q++) {
+            rwr += wp[(long)q * stride + R];
+            rw1 += wp[(long)q * stride + R + 1];
+        }
     }
     // ECORR epochs: c_e / D_e of the current residuals
     const int nep = Pd.nep;
     const double* Ei = esum + I.eoff;
     double* ce = ecs + I.epoff;
+    double erwr = 0.0, erw1 = 0.0;
     for (int e = threadIdx.x; e < nep; e += blockDim.x) {
         double c = 0.0;
         for (int k = Pd.ep_ptr[e]; k < Pd.ep_ptr[e + 1]; k++) {
@@ -641,34 +686,34 @@ __global__ __launch_bounds__(256) void k_woodbury(const PsrDev* __restrict__ psr
             c += ri[i] / (Pd.sigma[i] * Pd.sigma[i]);
         }
         double De = eD[I.epoff + e];
-        rwr -= c * c / De;
-        rw1 -= eW[I.epoff + e] * c / De;
+        erwr += c * c / De;
+        erw1 += eW[I.epoff + e] * c / De;
         ce[e] = c / De;
     }
-    __syncthreads();
-    rwr = block_sum<4>(rwr, sh);
-    rw1 = block_sum<4>(rw1, sh);
-    for (int j = 0; j < R; j++) {
-        const double* col = Mi + (long)(S.ncol + j) * n;
-        double s = 0.0;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) s += col[i] * ri[i] / (Pd.sigma[i] * Pd.sigma[i]);
-        for (int e = threadIdx.x; e < nep; e += blockDim.x) s -= Ei[(long)e * I.Kp + S.ncol + j] * ce[e];
-        s = block_sum<4>(s, sh);
-        if (threadIdx.x == 0) d[j] = s;
+    erwr = block_sum<4>(erwr, sh);
+    erw1 = block_sum<4>(erw1, sh);
+    __syncthreads();  // ce visible
+    for (int j = threadIdx.x; j < R; j += blockDim.x) {
+        double v = 0.0;
+        for (int q = 0; q < nsplit; q++) v += wp[(long)q * stride + j];
+        for (int e = 0; e < nep; e++) v -= Ei[(long)e * I.Kp + S.ncol + j] * ce[e];
+        d[j] = v;
     }
-    if (threadIdx.x == 0) d[R] = rw1;
+    if (threadIdx.x == 0) d[R] = rw1 - erw1;
     __syncthreads();
+    // forward substitution L y = d (column-oriented, one barrier per column)
     const double* L = sigL + I.soff;
-    if (threadIdx.x == 0) {
-        double q = 0.0;
-        for (int k = 0; k < Kn; k++) {
-            double s = d[k];
-            for (int m = 0; m < k; m++) s -= L[tri(k, m)] * d[m];
-            d[k] = s / L[tri(k, k)];
-            q += d[k] * d[k];
-        }
-        chi2[inst] = rwr - q;
+    for (int k = 0; k < Kn; k++) {
+        double yk = d[k] / L[tri(k, k)];
+        __syncthreads();
+        if (threadIdx.x == 0) d[k] = yk;
+        for (int i = k + 1 + threadIdx.x; i < Kn; i += blockDim.x) d[i] -= L[tri(i, k)] * yk;
+        __syncthreads();
     }
+    double q = 0.0;
+    for (int k = threadIdx.x; k < Kn; k += blockDim.x) q += d[k] * d[k];
+    q = block_sum<4>(q, sh);
+    if (threadIdx.x == 0) chi2[inst] = (rwr - erwr) - q;
 }
 
 // tables += lambda * dpars on every timing column (skips Offset), double-double add
@@ -719,13 +764,17 @@ struct pint_ctx {
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
     double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
-    double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr;
+    double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
+    size_t wpart_cap = 0;
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
     int* d_status = nullptr;
     int maxK = 0;
-    hipEvent_t ev[8];
-    float ms_eval = 0, ms_gram = 0, ms_solve = 0, ms_resid = 0;
+    // HIP event pairs: 0/1 eval, 2/3 eval with design matrix, 4/5 resid, 6/7 ecorr+gram,
+    // 7/8 solve, 10/11 Woodbury chi2
+    hipEvent_t ev[12];
+    bool rec[12] = {false};
+    float ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
 static void dfree(void*& p) {
@@ -772,7 +821,7 @@ pint_ctx* pint_ctx_create(int device) {
         return ctx;
     }
     hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    for (int i = 0; i < 8; i++) hipEventCreate(&ctx->ev[i]);
+    for (int i = 0; i < 12; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
     return ctx;
 }
@@ -786,9 +835,10 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
-                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs};
+                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart};
     for (auto p : ps) dfree(*p);
     ctx->ninst = 0;
+    ctx->wpart_cap = 0;
 }
 
 void pint_ctx_destroy(pint_ctx* ctx) {
@@ -801,7 +851,7 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     }
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
     if (ctx->d_status) hipFree(ctx->d_status);
-    for (int i = 0; i < 8; i++) hipEventDestroy(ctx->ev[i]);
+    for (int i = 0; i < 12; i++) hipEventDestroy(ctx->ev[i]);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -997,6 +1047,21 @@ int pint_set_tables(pint_ctx* ctx, const double* tables) {
     return PINT_OK;
 }
 
+static void record(pint_ctx* ctx, int i) {
+    hipEventRecord(ctx->ev[i], ctx->stream);
+    ctx->rec[i] = true;
+}
+
+static void update_timings(pint_ctx* ctx) {
+    const int pairs[6][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}};
+    for (int k = 0; k < 6; k++) {
+        float t = 0.0f;
+        if (ctx->rec[pairs[k][0]] && ctx->rec[pairs[k][1]] &&
+            hipEventElapsedTime(&t, ctx->ev[pairs[k][0]], ctx->ev[pairs[k][1]]) == hipSuccess)
+            ctx->ms[k] = t;
+    }
+}
+
 static int check_status(pint_ctx* ctx) {
     int st = 0;
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -1012,7 +1077,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
-    hipEventRecord(ctx->ev[0], ctx->stream);
+    record(ctx, want_M ? 2 : 0);
     for (int t = 0; t < 3; t++) {
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
@@ -1029,15 +1094,15 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #undef PINT_EVAL_LAUNCH
         HIPCHK(hipGetLastError());
     }
-    hipEventRecord(ctx->ev[1], ctx->stream);
+    record(ctx, want_M ? 3 : 1);
+    record(ctx, 4);
     hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
                        ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
     HIPCHK(hipGetLastError());
-    hipEventRecord(ctx->ev[2], ctx->stream);
+    record(ctx, 5);
     if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
-    hipEventElapsedTime(&ctx->ms_eval, ctx->ev[0], ctx->ev[1]);
-    hipEventElapsedTime(&ctx->ms_resid, ctx->ev[1], ctx->ev[2]);
+    update_timings(ctx);
     return rc;
 }
 
@@ -1074,7 +1139,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
     int stride = maxKp + ((maxKp & 31) == 0 ? 16 : 0);
     size_t lds_g = sizeof(double) * 2 * GCH * stride;
-    hipEventRecord(ctx->ev[3], ctx->stream);
+    record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
@@ -1083,7 +1148,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(GTHREADS), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->nsplit, mode, ctx->d_G, ctx->d_colsq);
     HIPCHK(hipGetLastError());
-    hipEventRecord(ctx->ev[4], ctx->stream);
+    record(ctx, 7);
     int K = ctx->maxK;
     size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
     if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
@@ -1091,11 +1156,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                        ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_work, ctx->d_dpars,
                        ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
     HIPCHK(hipGetLastError());
-    hipEventRecord(ctx->ev[5], ctx->stream);
+    record(ctx, 8);
     if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
-    hipEventElapsedTime(&ctx->ms_gram, ctx->ev[3], ctx->ev[4]);
-    hipEventElapsedTime(&ctx->ms_solve, ctx->ev[4], ctx->ev[5]);
+    update_timings(ctx);
     return rc;
 }
 
@@ -1121,11 +1185,24 @@ int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
 // (Sigma factor) and the red-noise columns of the last design matrix.
 int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     int R = 0;
-    for (auto& p : ctx->psrs) R = 2 * p.spec.nred > R ? 2 * p.spec.nred : R;
-    hipLaunchKernelGGL(k_woodbury, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
-                       ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_ecs,
-                       ctx->d_chi2g);
+    for (auto& I : ctx->inst) R = 2 * ctx->psrs[I.psr].spec.nred > R ? 2 * ctx->psrs[I.psr].spec.nred : R;
+    int stride = R + 2;
+    int nsw = ctx->nsplit;  // same N-split as the Gram (fills the CUs)
+    size_t need = (size_t)ctx->ninst * nsw * stride;
+    if (need > ctx->wpart_cap) {
+        dfree((void*&)ctx->d_wpart);
+        HIPCHK(hipMalloc(&ctx->d_wpart, sizeof(double) * need));
+        ctx->wpart_cap = need;
+    }
+    record(ctx, 10);
+    hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
+                       ctx->d_rt, nsw, stride, ctx->d_wpart);
     HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
+                       ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
+                       stride, ctx->d_ecs, ctx->d_chi2g);
+    HIPCHK(hipGetLastError());
+    record(ctx, 11);
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -1140,18 +1217,13 @@ int pint_set_lazy(pint_ctx* ctx, int lazy) {
 
 int pint_check(pint_ctx* ctx) {
     int rc = check_status(ctx);
-    hipEventElapsedTime(&ctx->ms_eval, ctx->ev[0], ctx->ev[1]);
-    hipEventElapsedTime(&ctx->ms_resid, ctx->ev[1], ctx->ev[2]);
-    hipEventElapsedTime(&ctx->ms_gram, ctx->ev[3], ctx->ev[4]);
-    hipEventElapsedTime(&ctx->ms_solve, ctx->ev[4], ctx->ev[5]);
+    update_timings(ctx);
     return rc;
 }
 
 int pint_last_timing(pint_ctx* ctx, double* ms) {
-    ms[0] = ctx->ms_eval;
-    ms[1] = ctx->ms_resid;
-    ms[2] = ctx->ms_gram;
-    ms[3] = ctx->ms_solve;
+    update_timings(ctx);
+    for (int k = 0; k < 6; k++) ms[k] = ctx->ms[k];
     return PINT_OK;
 }
 

@@ -445,7 +445,7 @@ class Session:
         return c
 
     def timing(self):
-        ms = np.zeros(4)
+        ms = np.zeros(6)
         self.L.pint_last_timing(self.ctx, L.ptr(ms))
         return ms
 

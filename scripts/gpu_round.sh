@@ -26,7 +26,7 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
-        -o run -- python3 bench.py --steps 5 --warmup 1 --grid 64 --cpu-baseline 0 \
+        -o run -- python3 bench.py --steps 10 --warmup 2 --grid 64 --cpu-baseline 0 \
         > gpurun_out/prof.log 2>&1
     step pmc 0 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch \
         -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --cpu-baseline 0 \
@@ -34,5 +34,9 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step pmc2 0 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write \
         -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --cpu-baseline 0 \
         > gpurun_out/pmc_write.log 2>&1
+fi
+if [ "$MODE" = all ] || [ "$MODE" = peaks ]; then
+    step peaks 0 timeout -k 10 120 ./build/peaks > gpurun_out/peaks.json
+    cat gpurun_out/peaks.json
 fi
 echo done
