@@ -196,6 +196,7 @@ PD double bin_unit_factor(int pid) {
         case PINT_B_PB: case PINT_B_T0: case PINT_B_TASC: return DAYSEC;
         case PINT_B_OM: return DEG_RAD;
         case PINT_B_OMDOT: return DEG_RAD / YR_S;
+        case PINT_B_EPS1DOT: case PINT_B_EPS2DOT: return 1e-12;  // units 1e-12/s (binary_ell1.py:142)
         default: return 1.0;
     }
 }
@@ -231,8 +232,8 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
     B.pb = B.PBs + B.PBDOT * B.tt0;  // pbprime (binary_orbits.py:107)
     B.A1DOT = binp(S, P, PINT_B_A1DOT);
     B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
-    B.EPS1DOT = binp(S, P, PINT_B_EPS1DOT);
-    B.EPS2DOT = binp(S, P, PINT_B_EPS2DOT);
+    B.EPS1DOT = binp(S, P, PINT_B_EPS1DOT) * 1e-12;  // par units 1e-12/s -> 1/s
+    B.EPS2DOT = binp(S, P, PINT_B_EPS2DOT) * 1e-12;
     B.eps1 = binp(S, P, PINT_B_EPS1) + B.tt0 * B.EPS1DOT;
     B.eps2 = binp(S, P, PINT_B_EPS2) + B.tt0 * B.EPS2DOT;
     B.TM2 = binp(S, P, PINT_B_M2) * TSUN;

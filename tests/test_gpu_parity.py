@@ -181,6 +181,30 @@ def test_perturbed_vs_oracle(name, seed):
     assert np.max(np.abs(M - Mo) / scale) < 1e-9
 
 
+@pytest.mark.parametrize("extra", [{"EPS1DOT": 0.7, "EPS2DOT": -0.4, "A1DOT": 2e-14, "PBDOT": 3e-13},
+                                   {"EPS1DOT": -2.0}])
+def test_ell1_rates_vs_oracle(extra):
+    """ELL1 time derivatives (EPS1DOT/EPS2DOT in 1e-12/s, A1DOT, PBDOT) set and free: GPU
+    residuals and design matrix vs the oracle (no reference fixture has them non-zero)."""
+    from pint_amd import Residuals
+    from pint_amd.engine import evaluate_designmatrix
+    model, toas, z, meta = load("pta_ell1")
+    for k, v in extra.items():
+        model[k].value = np.longdouble(v)
+    model.free_params = model.free_params + [k for k in extra if k not in model.free_params]
+    om, ot = O.from_product_model(model), O.toas_from_product(toas)
+    r = Residuals(toas, model, track_mode="nearest")
+    ro = O.residuals(om, ot, track_mode="nearest")
+    assert np.max(np.abs(r.time_resids - ro["time"])) < 1e-10
+    M, params, _ = evaluate_designmatrix(model, toas)
+    Mo, no = O.designmatrix(om, ot)
+    assert params == no
+    scale = np.max(np.abs(Mo), axis=0)
+    scale[scale == 0] = 1
+    err = np.max(np.abs(M - Mo) / scale, axis=0)
+    assert np.max(err) < 1e-9, {p: e for p, e in zip(params, err) if e > 1e-9}
+
+
 @pytest.mark.parametrize("name", ["pta_dd", "b1855"])
 def test_gls_step_vs_oracle(name):
     from pint_amd.fitter import BatchFit
