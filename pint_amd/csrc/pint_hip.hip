@@ -25,7 +25,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // device-side descriptors
 // ---------------------------------------------------------------------------------
 struct PsrDev {
-    const double *tdb_hi, *tdb_lo, *freq, *sigma, *pos, *vel, *sun, *pn, *dpn;
+    const double *tdb_hi, *tdb_lo, *freq, *sigma, *isig, *pos, *vel, *sun, *pn, *dpn;
     const uint32_t* flags;
     const uint64_t* jmask;
     const int32_t *dmx_a, *dmx_b;
@@ -55,6 +55,13 @@ struct InstDev {
     long cvoff;  // compact timing covariance offset (ncol*ncol)
     long eoff;   // ECORR epoch sums offset (nep*Kp) and per-epoch scalars (eoff/Kp)
     long epoff;  // per-epoch scalar offset (nep)
+    long ooff;   // residual output offset (n per instance)
+    int self;    // index of this instance in the batch
+    int pad_;
+};
+
+struct KpGroup {  // instances sharing k_gram's tiles-per-wave T (launched together)
+    int T, first, count, maxKp;
 };
 
 #define HIPCHK(x)                                                                    \
@@ -200,45 +207,12 @@ __global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, 
 // the whole (upper-triangular tiles of the) Kp x Kp Gram for one N-split of one instance.
 // Also accumulates the unweighted column sums of squares (normalize_designmatrix).
 // ---------------------------------------------------------------------------------
-constexpr int GCH = 16;       // TOAs per LDS chunk (multiple of 4)
+constexpr int GCH = 32;       // TOA rows per LDS chunk (multiple of 4)
 constexpr int GMAXKP = 256;   // max padded columns
 constexpr int GWAVES = 16;
 constexpr int GTHREADS = GWAVES * 64;
-constexpr int GMAXT = 9;      // ceil(136 / 16) upper tiles per wave at Kp=256
-constexpr int GMAXQ = GCH * GMAXKP / GTHREADS;  // staged elements per thread per chunk (16)
-
-// Stage the next chunk into registers (coalesced: 32 consecutive TOAs of one column per
-// 32 lanes), so the global loads of chunk c+1 overlap the MFMAs of chunk c.
-struct GramStage {
-    double v[GMAXQ];
-    double w;
-};
-
-__device__ __forceinline__ void gram_load(GramStage& st, const double* __restrict__ Mi, const double* __restrict__ ri,
-                                          const double* __restrict__ sigma, const double* __restrict__ Ei,
-                                          const double* __restrict__ eDi, long c0, long i1, int n, int K, int Kp) {
-    const int tid = threadIdx.x;
-    const int ii = tid % GCH;
-    const long toa = c0 + ii;
-    const bool ok = toa < i1;
-    const bool real = toa < n;
-    double w;
-    if (!ok) w = 0.0;
-    else if (real) { double sg = sigma[toa]; w = 1.0 / (sg * sg); }
-    else w = -1.0 / eDi[toa - n];  // ECORR Schur row: -s_e s_e^T / D_e
-    st.w = w;
-#pragma unroll
-    for (int q = 0; q < GMAXQ; q++) {
-        int c = tid / GCH + (GTHREADS / GCH) * q;
-        double v = 0.0;
-        if (ok && c < Kp) {
-            if (!real) v = Ei[(toa - n) * Kp + c];
-            else if (c < K) v = Mi[(long)c * n + toa];
-            else if (c == K) v = ri[toa];
-        }
-        st.v[q] = v;
-    }
-}
+constexpr int GMAXT_ALL = 9;  // max upper 16x16 tiles per wave = ceil(136 / 16) at Kp = 256
+constexpr int GMAXQ = GCH * GMAXKP / GTHREADS;  // staged elements per thread per chunk (8)
 
 // ECORR epoch sums (one wave per epoch, lanes over columns): s_e = sum_{i in e} w_i [T|r]_i,
 // W_e = sum w_i, D_e = W_e + 1/phi_e.  The quantisation-matrix block of the GLS normal
@@ -281,117 +255,177 @@ __global__ __launch_bounds__(256) void k_ecorr(const PsrDev* __restrict__ psrs, 
     }
 }
 
+// k_gram: FP64 MFMA Gram of the whitened rows [T | r] / sigma, one 16-wave workgroup per
+// (N-split, instance).  The row-major list of upper 16x16 tiles is cut into 16 contiguous
+// runs of T or T-1 tiles (T = ceil(ntiles/16), a template parameter so the first T-1
+// tiles are unconditional and the operand reads can be hoisted).  Chunks of GCH rows are
+// staged global -> registers (prefetched one chunk ahead, branch-free clamped loads) ->
+// LDS; every wave then issues GCH/4 x T v_mfma_f64_16x16x4f64 with operands from LDS.
+// VIRT: the ECORR Schur rows s_e / sqrt(D_e) of k_ecorr, stored negated in the extra
+// partial slot, so the sum over partials is G - sum_e s_e s_e^T / D_e.
+// Also accumulates the unweighted column sums of squares (normalize_designmatrix).
+template <int T, bool VIRT>
 __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ M, const double* __restrict__ rtime,
                                                    const double* __restrict__ esum, const double* __restrict__ eD,
-                                                   int nsplit, int mode, double* __restrict__ Gpart,
-                                                   double* __restrict__ colsq) {
+                                                   int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
     extern __shared__ double lds[];
-    const int inst = blockIdx.y, split = blockIdx.x;
-    const InstDev I = insts[inst];
+    const InstDev I = insts[blockIdx.y];
+    const int split = VIRT ? nsplit : blockIdx.x;
     const PsrDev& Pd = psrs[I.psr];
     const int n = I.n, K = I.K, Kp = I.Kp;
-    const long nrow = n + (mode == 1 ? Pd.nep : 0);  // + ECORR Schur rows (GLS only)
+    const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
+    double* Ts = lds;                    // [GCH][stride] whitened rows
+    double* Sg = lds + GCH * stride;     // [GCH] sigma of the staged rows (colsq)
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + I.ooff;
     const double* Ei = esum + I.eoff;
     const double* eDi = eD + I.epoff;
-    const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
-    double* Ts = lds;                  // [GCH][stride]
-    double* Ws = lds + GCH * stride;   // weighted copy
-    const double* Mi = M + I.moff;
-    const double* ri = rtime + (I.roff - inst);
-    long per = (nrow + nsplit - 1) / nsplit;
-    per = (per + GCH - 1) / GCH * GCH;
-    long i0 = split * per, i1 = i0 + per;
-    if (i1 > nrow) i1 = nrow;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    long i0, i1;
+    if (VIRT) {
+        i0 = 0;
+        i1 = Pd.nep;
+    } else {
+        long per = (n + nsplit - 1) / nsplit;
+        per = (per + GCH - 1) / GCH * GCH;
+        i0 = split * per;
+        i1 = i0 + per;
+        if (i1 > n) i1 = n;
+    }
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = Kp / 16;
     const int ntiles = nt * (nt + 1) / 2;
-    // this wave's tiles: a contiguous run of the row-major upper-triangular tile list, so
-    // consecutive tiles share the A row-block
     const int t_lo = (ntiles * wave) / GWAVES, t_hi = (ntiles * (wave + 1)) / GWAVES;
-    int ti0 = 0, tj0 = 0;
+    const bool full = (t_hi - t_lo) == T;  // else T-1 tiles
+    int tI[T], tJ[T];
     {
-        int rem = t_lo;
-        while (rem >= nt - ti0) { rem -= nt - ti0; ti0++; }
-        tj0 = ti0 + rem;
-    }
-    double4_t acc[GMAXT];
+        int ti = 0, rem = t_lo;
+        while (rem >= nt - ti) { rem -= nt - ti; ti++; }
+        int tj = ti + rem;
 #pragma unroll
-    for (int t = 0; t < GMAXT; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    double csq = 0.0;  // thread tid < K owns column tid
-    GramStage st;
-    if (i0 < i1) gram_load(st, Mi, ri, Pd.sigma, Ei, eDi, i0, i1, n, K, Kp);
-    for (long c0 = i0; c0 < i1; c0 += GCH) {
-        __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
-        {
-            const int ii = tid % GCH;
-#pragma unroll
-            for (int q = 0; q < GMAXQ; q++) {
-                int c = tid / GCH + (GTHREADS / GCH) * q;
-                if (c < Kp) {
-                    double v = st.v[q];
-                    Ts[ii * stride + c] = v;
-                    Ws[ii * stride + c] = st.w * v;
-                }
-            }
-        }
-        __syncthreads();
-        if (c0 + GCH < i1) gram_load(st, Mi, ri, Pd.sigma, Ei, eDi, c0 + GCH, i1, n, K, Kp);  // prefetch next
-        if (tid < K) {
-            if (c0 + GCH <= n) {
-#pragma unroll 8
-                for (int r = 0; r < GCH; r++) {
-                    double v = Ts[r * stride + tid];
-                    csq += v * v;
-                }
-            } else {
-                for (int r = 0; r < (int)(n - c0); r++) {  // unweighted norms: real rows only
-                    double v = Ts[r * stride + tid];
-                    csq += v * v;
-                }
-            }
-        }
-#pragma unroll
-        for (int kk = 0; kk < GCH / 4; kk++) {
-            const int row = kk * 4 + (lane >> 4);
-            const double* Tr = Ts + row * stride + (lane & 15);
-            const double* Wr = Ws + row * stride + (lane & 15);
-            int ti = ti0, tj = tj0, cur_i = -1;
-            double a = 0.0;
-#pragma unroll
-            for (int t = 0; t < GMAXT; t++) {
-                if (t_lo + t < t_hi) {
-                    if (ti != cur_i) {
-                        cur_i = ti;
-                        a = Tr[ti * 16];
-                    }
-                    double bb = Wr[tj * 16];
-                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[t], 0, 0, 0);
-                    if (++tj == nt) { ti++; tj = ti; }
-                }
-            }
-        }
-    }
-    // write partial tiles: D[row=(lane>>4)+4*r][col=lane&15]
-    double* G = Gpart + I.goff + (long)split * Kp * Kp;
-    {
-        int ti = ti0, tj = tj0;
-#pragma unroll
-        for (int t = 0; t < GMAXT; t++) {
-            if (t_lo + t < t_hi) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    int row = ti * 16 + (lane >> 4) + 4 * q;
-                    int col = tj * 16 + (lane & 15);
-                    G[(long)row * Kp + col] = acc[t][q];
-                }
+        for (int t = 0; t < T; t++) {
+            tI[t] = ti;
+            tJ[t] = tj;
+            if (t + 2 < T || (t + 1 < T && full)) {
                 if (++tj == nt) { ti++; tj = ti; }
             }
         }
     }
-    if (tid < K) colsq[(I.coff + tid) * nsplit + split] = csq;
+    double4_t acc[T];
+#pragma unroll
+    for (int t = 0; t < T; t++) acc[t] = (double4_t){0, 0, 0, 0};
+    double csq = 0.0;  // thread tid < K owns column tid
+    // staging: thread -> (row ii = tid % GCH, columns c_base + 32 q)
+    const int ii = tid % GCH, c_base = tid / GCH;
+    const int nq = (Kp + (GTHREADS / GCH) - 1) / (GTHREADS / GCH);  // uniform
+    // the prefetch only issues loads (raw values into registers, clamped addresses, no
+    // arithmetic on the results), so the waits land at the LDS store of the next chunk
+    double st[GMAXQ];
+    double sg_next = 1.0, w_next = 0.0, r_next = 0.0;
+    bool ok_next = false;
+    auto load = [&](long c0) {
+        long row = c0 + ii;
+        ok_next = row < i1;
+        if (!ok_next) row = i1 - 1;  // clamped, valid address; zero weight at the store
+        if (VIRT) {
+            w_next = eDi[row];
+        } else {
+            sg_next = Pd.sigma[row];
+            w_next = Pd.isig[row];
+            r_next = ri[row];
+        }
+#pragma unroll
+        for (int q = 0; q < GMAXQ; q++) {
+            if (q < nq) {
+                const int c = c_base + (GTHREADS / GCH) * q;
+                if (VIRT) st[q] = Ei[row * Kp + (c < Kp ? c : Kp - 1)];
+                else st[q] = Mi[(long)(c < K ? c : K - 1) * n + row];
+            }
+        }
+    };
+    if (i0 < i1) load(i0);
+    for (long c0 = i0; c0 < i1; c0 += GCH) {
+        __syncthreads();  // previous chunk's MFMAs are done with the LDS tile
+        {
+            double iw = VIRT ? 1.0 / sqrt(w_next) : w_next;
+            iw = ok_next ? iw : 0.0;
+#pragma unroll
+            for (int q = 0; q < GMAXQ; q++) {
+                const int c = c_base + (GTHREADS / GCH) * q;
+                if (q < nq && c < Kp) {
+                    double v = st[q];
+                    if (!VIRT) v = c < K ? v : (c == K ? r_next : 0.0);
+                    Ts[ii * stride + c] = v * iw;
+                }
+            }
+        }
+        if (!VIRT && c_base == 0) Sg[ii] = sg_next;
+        __syncthreads();
+        if (c0 + GCH < i1) load(c0 + GCH);  // prefetch next chunk (overlaps the MFMAs)
+        if (!VIRT && tid < K) {
+            const int nr = (i1 - c0 < GCH) ? (int)(i1 - c0) : GCH;
+            for (int r = 0; r < nr; r++) {
+                double v = Ts[r * stride + tid] * Sg[r];
+                csq += v * v;
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < GCH / 4; kk++) {
+            const double* Tr = Ts + (kk * 4 + (lane >> 4)) * stride + (lane & 15);
+            double a[T], b[T];
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                a[t] = Tr[tI[t] * 16];
+                b[t] = Tr[tJ[t] * 16];
+            }
+#pragma unroll
+            for (int t = 0; t < T - 1; t++) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
+            if (full) acc[T - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T - 1], b[T - 1], acc[T - 1], 0, 0, 0);
+        }
+    }
+    // write partial tiles: D[row=(lane>>4)+4*r][col=lane&15]
+    double* G = Gpart + I.goff + (long)split * Kp * Kp;
+    const double sgn = VIRT ? -1.0 : 1.0;
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        if (t < T - 1 || full) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int row = tI[t] * 16 + (lane >> 4) + 4 * q;
+                int col = tJ[t] * 16 + (lane & 15);
+                G[(long)row * Kp + col] = sgn * acc[t][q];
+            }
+        }
+    }
+    if (!VIRT && tid < K) colsq[(I.coff + tid) * nsplit + split] = csq;
 }
 
+
+// Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
+// triangle only, in a fixed order (deterministic), and the column sums of squares.
+__global__ __launch_bounds__(256) void k_greduce(const InstDev* __restrict__ insts, int nsplit, int nparts,
+                                                 double* __restrict__ Gpart, double* __restrict__ colsq) {
+    const InstDev I = insts[blockIdx.y];
+    const int Kp = I.Kp;
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long KK = (long)Kp * Kp;
+    if (e < KK) {
+        const int i = (int)(e / Kp), j = (int)(e % Kp);
+        if (i <= j) {
+            double* G = Gpart + I.goff;
+            double sacc = G[e];
+            for (int q = 1; q < nparts; q++) sacc += G[(long)q * KK + e];
+            G[e] = sacc;
+        }
+    }
+    if (e < I.K) {
+        double* cs = colsq + (I.coff + e) * nsplit;
+        double v = cs[0];
+        for (int q = 1; q < nsplit; q++) v += cs[q];
+        cs[0] = v;
+    }
+}
 
 // ---------------------------------------------------------------------------------
 // k_solve: one 1024-thread workgroup per instance, everything in LDS (packed lower
@@ -470,7 +504,7 @@ __device__ __forceinline__ double linv(const double* A, const double* D, int i, 
 
 __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ tables, const double* __restrict__ Gpart,
-                                                   const double* __restrict__ colsq, int nsplit, int mode,
+                                                   const double* __restrict__ colsq, int nsplit, int nparts, int mode,
                                                    double* __restrict__ work, double* __restrict__ dpars,
                                                    double* __restrict__ errs, double* __restrict__ cov,
                                                    double* __restrict__ chi2lin, double* __restrict__ sigL,
@@ -491,11 +525,9 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
     double* yv = bv + K;                    // K
     double* nrm = yv + K;                   // K
     const double* Gp = Gpart + I.goff;
-    auto G = [&](int i, int j) {  // symmetric accessor summing the N-split partials
+    auto G = [&](int i, int j) {  // symmetric accessor (partials summed into slot 0 by k_greduce)
         if (i > j) { int t = i; i = j; j = t; }
-        double sacc = 0.0;
-        for (int q = 0; q < nsplit; q++) sacc += Gp[(long)q * Kp * Kp + (long)i * Kp + j];
-        return sacc;
+        return Gp[(long)i * Kp + j];
     };
     // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
     for (int j = threadIdx.x; j < K; j += blockDim.x) {
@@ -503,7 +535,7 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
         if (mode == 0) v = G(j, j);
         else {
             v = 0.0;
-            for (int q = 0; q < nsplit; q++) v += colsq[(I.coff + j) * nsplit + q];
+            v = colsq[(I.coff + j) * nsplit];
         }
         v = sqrt(v);
         nrm[j] = (v == 0.0) ? 1.0 : v;
@@ -753,6 +785,8 @@ struct pint_ctx {
     int ninst = 0;
     std::vector<InstDev> inst;
     InstDev* d_inst = nullptr;
+    InstDev* d_inst_sorted = nullptr;   // instances grouped by k_gram T
+    std::vector<KpGroup> kp_groups;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
@@ -829,7 +863,7 @@ pint_ctx* pint_ctx_create(int device) {
 const char* pint_last_error(pint_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static void free_instances(pint_ctx* ctx) {
-    void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
+    void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
@@ -879,6 +913,14 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->tdb_lo, n + 1, d.tdb_lo);
     rc |= upload(ctx, ph, t->freq_mhz, n + 1, d.freq);
     rc |= upload(ctx, ph, t->sigma_s, n, d.sigma);
+    {
+        std::vector<double> is(n);
+        for (int i = 0; i < n; i++) {
+            if (!(t->sigma_s[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; return -PINT_E_INVALID; }
+            is[i] = 1.0 / t->sigma_s[i];
+        }
+        rc |= upload(ctx, ph, is.data(), n, d.isig);
+    }
     rc |= upload(ctx, ph, t->pos_km, 3 * (n + 1), d.pos);
     rc |= upload(ctx, ph, t->vel_kms, 3 * (n + 1), d.vel);
     rc |= upload(ctx, ph, t->sun_km, 3 * (n + 1), d.sun);
@@ -939,10 +981,30 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         if (ctx->psrs[p].n > maxN) maxN = ctx->psrs[p].n;
     }
     // N-split for the Gram so the launch fills the 256 CUs
-    int nsplit = (1024 + ninst - 1) / ninst;
+    // choose the split count that minimises (workgroup rounds) / nsplit, i.e. the k_gram
+    // makespan with one 1024-thread workgroup resident per CU, with >= 4 chunks per split
+    int ncu = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
+            ncu = prop.multiProcessorCount;
+    }
     int maxsplit = (maxN + 4 * GCH - 1) / (4 * GCH);
-    if (nsplit > maxsplit) nsplit = maxsplit;
-    if (nsplit < 1) nsplit = 1;
+    if (maxsplit < 1) maxsplit = 1;
+    // (smallest split count within 3% of the best makespan: each split adds a partial
+    // Gram that k_greduce must sum)
+    double best = 1e30;
+    for (int ns = 1; ns <= maxsplit && ns <= 4096; ns++) {
+        long blocks = (long)ninst * ns;
+        double cost = (double)((blocks + ncu - 1) / ncu) / ns;
+        if (cost < best) best = cost;
+    }
+    int nsplit = 1;
+    for (int ns = 1; ns <= maxsplit && ns <= 4096; ns++) {
+        long blocks = (long)ninst * ns;
+        double cost = (double)((blocks + ncu - 1) / ncu) / ns;
+        if (cost <= best * 1.03) { nsplit = ns; break; }
+    }
     ctx->nsplit = nsplit;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
@@ -961,6 +1023,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.cvoff = cvoff;
         I.eoff = eoff;
         I.epoff = epoff;
+        I.ooff = out;
+        I.self = k;
         eoff += (long)ph.dev.nep * I.Kp;
         epoff += ph.dev.nep;
         if (ph.dev.nep > max_nep) max_nep = ph.dev.nep;
@@ -973,7 +1037,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         }
         roff += ph.n + 1;
         moff += (long)ph.n * ph.K;
-        goff += (long)nsplit * I.Kp * I.Kp;
+        goff += (long)(nsplit + 1) * I.Kp * I.Kp;  // + ECORR Schur partial
         soff += (long)(ph.K + 1) * (ph.K + 1);
         coff += ph.K + 1;
         out += ph.n;
@@ -1002,6 +1066,23 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->nblk = (int)bi.size();
     HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+    {
+        std::vector<InstDev> sorted;
+        ctx->kp_groups.clear();
+        for (int T = 1; T <= GMAXT_ALL; T++) {
+            KpGroup g{T, (int)sorted.size(), 0, 16};
+            for (auto& I : ctx->inst) {
+                int nt = I.Kp / 16, tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
+                if (tT != T) continue;
+                sorted.push_back(I);
+                g.count++;
+                if (I.Kp > g.maxKp) g.maxKp = I.Kp;
+            }
+            if (g.count) ctx->kp_groups.push_back(g);
+        }
+        HIPCHK(hipMalloc(&ctx->d_inst_sorted, sizeof(InstDev) * ninst));
+        HIPCHK(hipMemcpy(ctx->d_inst_sorted, sorted.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMalloc(&ctx->d_blk_inst, sizeof(int) * bi.size()));
     HIPCHK(hipMalloc(&ctx->d_blk_row0, sizeof(int) * br.size()));
     HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
@@ -1135,25 +1216,58 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
-    int maxKp = 16;
-    for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
-    int stride = maxKp + ((maxKp & 31) == 0 ? 16 : 0);
-    size_t lds_g = sizeof(double) * 2 * GCH * stride;
+    const int nparts = ctx->nsplit + ((mode == 1 && ctx->max_nep > 0) ? 1 : 0);
     record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_gram, dim3(ctx->nsplit, ctx->ninst), dim3(GTHREADS), lds_g, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->nsplit, mode, ctx->d_G, ctx->d_colsq);
+    {
+        // every instance of the batch uses the tile split of the widest one (maxKp); narrower
+        // instances have fewer tiles: T must cover the widest, and per-instance tile counts
+        // are recomputed in-kernel from their own Kp, so a launch is per distinct Kp group.
+        for (int g = 0; g < (int)ctx->kp_groups.size(); g++) {
+            const KpGroup& kg = ctx->kp_groups[g];
+            const int T = kg.T;
+            const int sstride = kg.maxKp + 16;
+            size_t lds = sizeof(double) * (GCH * sstride + GCH);
+            const InstDev* di = ctx->d_inst_sorted + kg.first;
+            for (int virt = 0; virt < 2; virt++) {
+                if (virt && !(mode == 1 && ctx->max_nep > 0)) break;
+                dim3 grid(virt ? 1 : ctx->nsplit, kg.count);
+#define PINT_GRAM_CASE(TT)                                                                                         \
+                case TT:                                                                                           \
+                    if (virt) hipLaunchKernelGGL((k_gram<TT, true>), grid, dim3(GTHREADS), lds, ctx->stream,       \
+                                                 ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD,    \
+                                                 ctx->nsplit, ctx->d_G, ctx->d_colsq);                             \
+                    else hipLaunchKernelGGL((k_gram<TT, false>), grid, dim3(GTHREADS), lds, ctx->stream,          \
+                                            ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD,          \
+                                            ctx->nsplit, ctx->d_G, ctx->d_colsq);                                  \
+                    break;
+                switch (T) {
+                    PINT_GRAM_CASE(1) PINT_GRAM_CASE(2) PINT_GRAM_CASE(3) PINT_GRAM_CASE(4) PINT_GRAM_CASE(5)
+                    PINT_GRAM_CASE(6) PINT_GRAM_CASE(7) PINT_GRAM_CASE(8) PINT_GRAM_CASE(9)
+                    default: ctx->err = "Kp out of range"; return PINT_E_INVALID;
+                }
+#undef PINT_GRAM_CASE
+            }
+        }
+    }
     HIPCHK(hipGetLastError());
+    if (nparts > 1) {
+        int maxKp = 16;
+        for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
+        hipLaunchKernelGGL(k_greduce, dim3((maxKp * maxKp + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream,
+                           ctx->d_inst, ctx->nsplit, nparts, ctx->d_G, ctx->d_colsq);
+        HIPCHK(hipGetLastError());
+    }
     record(ctx, 7);
     int K = ctx->maxK;
     size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
     if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
     hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_work, ctx->d_dpars,
+                       ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, ctx->d_work, ctx->d_dpars,
                        ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
     HIPCHK(hipGetLastError());
     record(ctx, 8);

@@ -8,10 +8,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {  # step <name> <allowed-nonzero> <cmd...>
     local name=$1 ok=$2; shift 2
-    echo "== $name: $*" | tee -a gpurun_out/steps.log
+    echo "== $name: $*" >> gpurun_out/steps.log
     "$@"
     local rc=$?
-    echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+    echo "== $name rc=$rc" >> gpurun_out/steps.log
     if [ $rc -ne 0 ] && [ "$rc" != "$ok" ]; then exit $rc; fi
 }
 MODE=${1:-all}
@@ -39,4 +39,5 @@ if [ "$MODE" = all ] || [ "$MODE" = peaks ]; then
     step peaks 0 timeout -k 10 120 ./build/peaks > gpurun_out/peaks.json
     cat gpurun_out/peaks.json
 fi
+cat gpurun_out/steps.log
 echo done
