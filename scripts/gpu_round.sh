@@ -16,7 +16,7 @@ step() {  # step <name> <allowed-nonzero> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-    step pytest 1 timeout -k 10 1200 python -m pytest tests -m gpu -q -rf -p no:cacheprovider \
+    step pytest 1 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread \
         > gpurun_out/pytest_gpu.log 2>&1
     tail -30 gpurun_out/pytest_gpu.log
 fi

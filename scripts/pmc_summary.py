@@ -23,7 +23,7 @@ def load(path, counter):
             key = "k_eval_M" if m.group(1) == "1" else "k_eval"
             key += f"<{m.group(2)}>"
         else:
-            key = name.split("(")[0].strip()
+            key = re.sub(r"<.*", "", name.split("(")[0].replace("void ", "").strip())
         per[key].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
