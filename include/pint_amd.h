@@ -166,7 +166,13 @@ int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const
  * pint_check() synchronises and returns the accumulated status. */
 int pint_set_lazy(pint_ctx *ctx, int lazy);
 int pint_check(pint_ctx *ctx);
-/* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor. */
+/* Engine options (no reference counterpart): PINT_OPT_BLOCKED_SOLVE = 1 (default) solves
+ * the normal equations with the blocked FP64-MFMA kernel, 0 with the column-by-column
+ * LDS kernel (used by the tests to cross-check the two). */
+#define PINT_OPT_BLOCKED_SOLVE 1
+int pint_set_option(pint_ctx *ctx, int key, int value);
+/* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor
+ * (L^-1, packed lower). */
 int pint_debug_read(pint_ctx *ctx, int which, double *out);
 
 /* Device time (ms, HIP events on the library's stream) of the last launches, 6 values:

@@ -628,10 +628,309 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
             if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
             return;
         }
+        trinv_lds(Sg, Dg, Kn, tg);  // k_wsolve applies L^-1 as a matrix-vector product
         double* L = sigL + (long)I.soff;
         for (int e = threadIdx.x; e < Kn * (Kn + 1) / 2; e += blockDim.x) L[e] = Sg[e];
         __syncthreads();
         for (int i = threadIdx.x; i < Kn; i += blockDim.x) L[tri(i, i)] = Dg[i];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_solve_blk: the same solve, blocked on 16x16 tiles so the work runs on FP64 MFMA and
+// the sequential depth is nb = ceil(K/16) block steps instead of K column steps.
+//
+// LDS holds the lower block triangle of the (padded) normal matrix, each 16x16 block
+// column-major with an XOR swizzle (element (r,c) at c*16 + (r ^ (c & 14))), so both the
+// plain and the transposed MFMA operand reads, and the accumulator stores, hit distinct
+// bank pairs within each half-wave.  Padding rows/columns (K..16*nb-1) are identity.
+//   Cholesky, right-looking: wave 0 factors the diagonal block in registers (readlane
+//     broadcasts) and overwrites it with L_kk^-1; the panel L_ik = A_ik L_kk^-T and the
+//     trailing update A_ij -= L_ik L_jk^T are v_mfma_f64_16x16x4f64 block products
+//     spread over the waves;
+//   X = L^-1 in place, block row by block row: X_ij = -L_ii^-1 sum_{k=j}^{i-1} L_ik X_kj;
+//   covariance C = X^T X (timing block, straight from the accumulators to HBM), errors
+//     from the column norms of X, xhat = X^T (X b).
+// The Woodbury Sigma of the GLS chi2 is factored by the same routine; its X = L^-1 goes
+// to sigL (packed lower incl. diagonal) for k_wsolve.
+// ---------------------------------------------------------------------------------
+constexpr int BS_MAXNB = 12;  // 78 blocks x 2 KiB + 2 vectors fit the 160 KiB LDS
+
+__device__ __forceinline__ int swz(int r, int c) { return (c << 4) + (r ^ (c & 14)); }
+__device__ __forceinline__ int lblk(int I, int J) { return ((I * (I + 1)) / 2 + J) << 8; }
+
+__device__ __forceinline__ double rdlane(double v, int l) {  // v_readlane of a double, l uniform
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// acc(D) += opX(X) opY(Y)^T; X, Y swizzled LDS blocks, TX/TY = read transposed.
+// D[(lane>>4)+4q][lane&15] is acc[q].
+template <bool TX, bool TY>
+__device__ __forceinline__ void bmma(double4_t& acc, const double* X, const double* Y, int lane, bool neg) {
+    const int m = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int c = 4 * q + kq;
+        double a = TX ? X[swz(c, m)] : X[swz(m, c)];
+        double b = TY ? Y[swz(c, m)] : Y[swz(m, c)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -a : a, b, acc, 0, 0, 0);
+    }
+}
+// acc += X Dp, with Dp an accumulator (D layout) used directly as the B operand
+__device__ __forceinline__ void bmma_reg(double4_t& acc, const double* X, const double4_t& Dp, int lane) {
+    const int m = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[swz(m, 4 * q + kq)], Dp[q], acc, 0, 0, 0);
+}
+__device__ __forceinline__ double4_t bload(const double* Z, int lane) {
+    double4_t v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = Z[swz((lane >> 4) + 4 * q, lane & 15)];
+    return v;
+}
+__device__ __forceinline__ void bstore(double* Z, const double4_t& v, int lane, double s) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) Z[swz((lane >> 4) + 4 * q, lane & 15)] = s * v[q];
+}
+
+// One wave: Cholesky of the (full, symmetric) 16x16 block in registers (lane r holds row
+// r), then its inverse column by column (lane c solves L x = e_c); the block is
+// overwritten by L^-1 (zeros above the diagonal).  Returns false if not positive definite.
+__device__ bool diag_factor(double* Akk, int lane) {
+    const int r = lane & 15;
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = Akk[swz(r, c)];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const double djj = rdlane(a[j], j);
+        ok = ok && (djj > 0.0);
+        const double ljj = sqrt(djj);
+        const double il = 1.0 / ljj;
+        a[j] = (r == j) ? ljj : (r > j ? a[j] * il : 0.0);
+#pragma unroll
+        for (int c = j + 1; c < 16; c++) a[c] -= a[j] * rdlane(a[j], c);
+    }
+    double x[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        double s = (r == t) ? 1.0 : 0.0;
+#pragma unroll
+        for (int u = 0; u < t; u++) s -= rdlane(a[u], t) * x[u];
+        x[t] = s / rdlane(a[t], t);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+    }
+    return ok;
+}
+
+__device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+1)/2 + j, j <= i
+    int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+    while (ii * (ii + 1) / 2 > p) ii--;
+    while ((ii + 1) * (ii + 2) / 2 <= p) ii++;
+    i = ii;
+    j = p - ii * (ii + 1) / 2;
+}
+
+// Blocked Cholesky + in-place inverse of the nb x nb block lower matrix A in LDS:
+// afterwards A holds X = L^-1.  Needs NW >= nb - 1.  Returns false (uniformly) if A is
+// not positive definite.
+template <int NW>
+__device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
+    for (int k = 0; k < nb; k++) {
+        if (wave == 0) {
+            bool ok = diag_factor(A + lblk(k, k), lane);
+            if (!ok && lane == 0) *sflag = 1;
+        }
+        __syncthreads();
+        if (*sflag) return false;
+        const double* Lkk = A + lblk(k, k);
+        for (int i = k + 1 + wave; i < nb; i += NW) {  // panel: L_ik = A_ik L_kk^-T
+            double* Aik = A + lblk(i, k);
+            double4_t acc = {0, 0, 0, 0};
+            bmma<false, false>(acc, Aik, Lkk, lane, false);
+            bstore(Aik, acc, lane, 1.0);
+        }
+        __syncthreads();
+        const int m = nb - k - 1;
+        if (m == 0) break;
+        for (int p = wave; p < m * (m + 1) / 2; p += NW) {  // trailing: A_ij -= L_ik L_jk^T
+            int ii, jj;
+            tri_decode(p, ii, jj);
+            double* Aij = A + lblk(k + 1 + ii, k + 1 + jj);
+            double4_t acc = bload(Aij, lane);
+            bmma<false, false>(acc, A + lblk(k + 1 + ii, k), A + lblk(k + 1 + jj, k), lane, true);
+            bstore(Aij, acc, lane, 1.0);
+        }
+        __syncthreads();
+    }
+    for (int i = 1; i < nb; i++) {  // X = L^-1, block row i (diagonal blocks already hold L_ii^-1)
+        double4_t acc2 = {0, 0, 0, 0};
+        const int j = wave;
+        if (j < i) {
+            double4_t acc = {0, 0, 0, 0};
+            for (int k = j; k < i; k++) bmma<false, true>(acc, A + lblk(i, k), A + lblk(k, j), lane, false);
+            bmma_reg(acc2, A + lblk(i, i), acc, lane);
+        }
+        __syncthreads();
+        if (j < i) bstore(A + lblk(i, j), acc2, lane, -1.0);
+        __syncthreads();
+    }
+    return true;
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                       const double* __restrict__ tables, const double* __restrict__ Gpart,
+                                                       const double* __restrict__ colsq, int nsplit, int mode,
+                                                       double* __restrict__ dpars, double* __restrict__ errs,
+                                                       double* __restrict__ cov, double* __restrict__ chi2lin,
+                                                       double* __restrict__ sigL, int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int sflag;
+    __shared__ double sh[NW];
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int Kfull = I.K, Kp = I.Kp, ncol = S.ncol;
+    const int K = (mode == 0) ? ncol : Kfull;
+    const int nb = (K + 15) >> 4;
+    const int nblk = nb * (nb + 1) / 2;
+    double* A = lds;
+    double* bv = A + nblk * 256;
+    double* yv = bv + nb * 16;
+    const double* Gp = Gpart + I.goff;
+    auto G = [&](int i, int j) {
+        if (i > j) { int t = i; i = j; j = t; }
+        return Gp[(long)i * Kp + j];
+    };
+    // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
+    auto nrmf = [&](int j) {
+        if (j >= K) return 1.0;
+        double v = sqrt(mode == 0 ? G(j, j) : colsq[(I.coff + j) * nsplit]);
+        return v == 0.0 ? 1.0 : v;
+    };
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid == 0) sflag = 0;
+    for (int e = tid; e < nblk * 256; e += NW * 64) {
+        int Ib, Jb;
+        tri_decode(e >> 8, Ib, Jb);
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+        double v;
+        if (gi < K && gj < K) {
+            const double ni = nrmf(gi), nj = nrmf(gj);
+            v = G(gi, gj) / (ni * nj);
+            if (gi == gj && mode == 1 && gi >= ncol) v += 1.0 / Pd.red_phi[gi - ncol] / (ni * ni);
+        } else {
+            v = (gi == gj) ? 1.0 : 0.0;
+        }
+        A[((e >> 8) << 8) + swz(r, c)] = v;
+    }
+    for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) / nrmf(j) : 0.0;
+    const double rwr = G(Kfull, Kfull);
+    __syncthreads();
+    if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag)) {
+        if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        return;
+    }
+    // covariance of the timing block: C = X^T X / (n n^T)
+    {
+        const int nbt = (ncol + 15) >> 4;
+        double* C = cov + (long)I.cvoff;
+        for (int p = wave; p < nbt * (nbt + 1) / 2; p += NW) {
+            int bj, bi;
+            tri_decode(p, bj, bi);  // bi <= bj
+            double4_t acc = {0, 0, 0, 0};
+            for (int k = bj; k < nb; k++) bmma<true, true>(acc, A + lblk(k, bi), A + lblk(k, bj), lane, false);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int row = bi * 16 + (lane >> 4) + 4 * q, col = bj * 16 + (lane & 15);
+                if (row < ncol && col < ncol) {
+                    const double v = acc[q] / (nrmf(row) * nrmf(col));
+                    C[(long)row * ncol + col] = v;
+                    C[(long)col * ncol + row] = v;
+                }
+            }
+        }
+    }
+    // errors (all K columns) and y = X b, 4 lanes per column / row
+    const int g0 = tid >> 2, sub = tid & 3;
+    for (int g = g0; g < nb * 16; g += NW * 16) {
+        const int Jb = g >> 4, cc = g & 15;
+        double se = 0.0, sy = 0.0;
+        for (int rr = g + sub; rr < nb * 16; rr += 4) {
+            const double x = A[lblk(rr >> 4, Jb) + swz(rr & 15, cc)];
+            se += x * x;
+        }
+        for (int c = sub; c <= g; c += 4) sy += A[lblk(Jb, c >> 4) + swz(cc, c & 15)] * bv[c];
+        se += __shfl_xor(se, 1, 64);
+        se += __shfl_xor(se, 2, 64);
+        sy += __shfl_xor(sy, 1, 64);
+        sy += __shfl_xor(sy, 2, 64);
+        if (sub == 0) {
+            if (g < K) errs[I.coff + g] = sqrt(se) / nrmf(g);
+            yv[g] = sy;
+        }
+    }
+    __syncthreads();
+    // xhat = X^T y (normalised) -> dpars; chi2lin = r^T W r - |y|^2
+    double q2 = 0.0;
+    for (int g = g0; g < K; g += NW * 16) {
+        const int Jb = g >> 4, cc = g & 15;
+        double s = 0.0;
+        for (int rr = g + sub; rr < nb * 16; rr += 4) s += A[lblk(rr >> 4, Jb) + swz(rr & 15, cc)] * yv[rr];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if (sub == 0) {
+            dpars[I.coff + g] = s / nrmf(g);
+            q2 += yv[g] * yv[g];
+        }
+    }
+    q2 = block_sum<NW>(q2, sh);
+    if (tid == 0) chi2lin[inst] = rwr - q2;
+    // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column),
+    // Schur-reduced for ECORR through the Gram; X_Sigma = L^-1 -> sigL for k_wsolve
+    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
+        __syncthreads();
+        const int R = 2 * S.nred, Kn = R + 1;
+        const int nbs = (Kn + 15) >> 4;
+        const double F0 = pval(tables + I.toff, S.o_F);
+        for (int e = tid; e < nbs * (nbs + 1) / 2 * 256; e += NW * 64) {
+            int Ib, Jb;
+            tri_decode(e >> 8, Ib, Jb);
+            const int r = e & 15, c = (e >> 4) & 15;
+            const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+            double v;
+            if (gi < Kn && gj < Kn) {
+                const int ci = (gi < R) ? ncol + gi : 0, cj = (gj < R) ? ncol + gj : 0;
+                const double si = (gi < R) ? 1.0 : F0, sj = (gj < R) ? 1.0 : F0;
+                v = G(ci, cj) * si * sj;
+                if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
+            } else {
+                v = (gi == gj) ? 1.0 : 0.0;
+            }
+            A[((e >> 8) << 8) + swz(r, c)] = v;
+        }
+        __syncthreads();
+        if (!blk_cholinv<NW>(A, nbs, wave, lane, &sflag)) {
+            if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+            return;
+        }
+        double* L = sigL + (long)I.soff;
+        for (int e = tid; e < Kn * (Kn + 1) / 2; e += NW * 64) {
+            int i, j;
+            tri_decode(e, i, j);
+            L[e] = A[lblk(i >> 4, j >> 4) + swz(i & 15, j & 15)];
+        }
     }
 }
 
@@ -733,17 +1032,14 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     }
     if (threadIdx.x == 0) d[R] = rw1 - erw1;
     __syncthreads();
-    // forward substitution L y = d (column-oriented, one barrier per column)
-    const double* L = sigL + I.soff;
-    for (int k = 0; k < Kn; k++) {
-        double yk = d[k] / L[tri(k, k)];
-        __syncthreads();
-        if (threadIdx.x == 0) d[k] = yk;
-        for (int i = k + 1 + threadIdx.x; i < Kn; i += blockDim.x) d[i] -= L[tri(i, k)] * yk;
-        __syncthreads();
-    }
+    // y = L^-1 d with the explicit inverse factor from k_solve (row dot products)
+    const double* X = sigL + I.soff;
     double q = 0.0;
-    for (int k = threadIdx.x; k < Kn; k += blockDim.x) q += d[k] * d[k];
+    for (int i = threadIdx.x; i < Kn; i += blockDim.x) {
+        double s = 0.0;
+        for (int j = 0; j <= i; j++) s += X[tri(i, j)] * d[j];
+        q += s * s;
+    }
     q = block_sum<4>(q, sh);
     if (threadIdx.x == 0) chi2[inst] = (rwr - erwr) - q;
 }
@@ -793,6 +1089,7 @@ struct pint_ctx {
     int blk_off[4] = {0, 0, 0, 0};  // block ranges per binary type (0 none, 1 ELL1, 2 DD)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
     int lazy = 0;
+    int blocked_solve = 1;  // k_solve_blk (MFMA, blocked) vs the column-by-column k_solve
     int nsplit = 1;
     double *d_tables = nullptr, *d_phhi = nullptr, *d_phlo = nullptr, *d_ftay = nullptr, *d_delay = nullptr;
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
@@ -1263,12 +1560,32 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
-    int K = ctx->maxK;
-    size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
-    if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
-    hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, ctx->d_work, ctx->d_dpars,
-                       ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+    // blocked MFMA solve when the (padded) normal matrix and the Woodbury Sigma fit the LDS
+    int Ks = 0, Kn = 0;
+    for (auto& I : ctx->inst) {
+        const pint_spec_t& sp = ctx->psrs[I.psr].spec;
+        Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
+        if (mode == 1) Kn = std::max(Kn, 2 * sp.nred + 1);
+    }
+    const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
+    if (nbx <= BS_MAXNB && ctx->blocked_solve) {
+        size_t lds_b = sizeof(double) * ((size_t)nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx);
+        if (nbx <= 5)
+            hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+        else
+            hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+    } else {
+        int K = ctx->maxK;
+        size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
+        if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
+        hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, ctx->d_work, ctx->d_dpars,
+                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+    }
     HIPCHK(hipGetLastError());
     record(ctx, 8);
     if (ctx->lazy) return PINT_OK;
@@ -1327,6 +1644,13 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
 int pint_set_lazy(pint_ctx* ctx, int lazy) {
     ctx->lazy = lazy;
     return PINT_OK;
+}
+
+int pint_set_option(pint_ctx* ctx, int key, int value) {
+    if (!ctx) return PINT_E_INVALID;
+    if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
+    ctx->err = "unknown option";
+    return PINT_E_INVALID;
 }
 
 int pint_check(pint_ctx* ctx) {

@@ -415,6 +415,9 @@ class Session:
     def set_lazy(self, lazy=True):
         self._check(self.L.pint_set_lazy(self.ctx, 1 if lazy else 0))
 
+    def set_blocked_solve(self, on=True):
+        self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))
+
     def check(self):
         self._check(self.L.pint_check(self.ctx))
 
