@@ -32,10 +32,15 @@ PD dd pdd(const double* P, int o) { return dd_make(P[o], P[o + 1]); }
 // ------------------------------------------------------------------------------------
 // erfa pmsafe/starpm/starpv restated (SOFA published algorithm; pyerfa 2.0.0 is the
 // reference's third-party call at astrometry.py:513 and astropy apply_space_motion).
-// Returns the unit vector toward the star at epoch offset dt_days (TDB days).
+// Split in two: pm_setup() is everything that does not depend on the epoch (pmsafe's
+// parallax override, starpv with its relativistic iteration) and runs once per instance
+// (k_prep); pm_dir() is starpm's propagation to one TOA's epoch.
 // ------------------------------------------------------------------------------------
-PD void starpm_dir(double ra, double dec, double pmr, double pmd, double px, double dt_days,
-                   double out[3]) {
+struct PmState {
+    double p[3], v1[3], tl1;
+};
+
+PD void pm_setup(double ra, double dec, double pmr, double pmd, double px, PmState& st) {
     // pmsafe: override parallax (PXMIN 5e-7 arcsec, F = 326)
     double a1[3] = {cos(ra) * cos(dec), sin(ra) * cos(dec), sin(dec)};
     double ra2 = ra + pmr, dec2 = dec + pmd;
@@ -54,13 +59,13 @@ PD void starpm_dir(double ra, double dec, double pmr, double pmd, double px, dou
     double w = px1a >= 1e-7 ? px1a : 1e-7;
     double r = DR2AS / w;
     double rad = pmr / DJY, decd = pmd / DJY;
-    double st = sin(ra), ct = cos(ra), sp = sin(dec), cp = cos(dec);
+    double st_ = sin(ra), ct = cos(ra), sp = sin(dec), cp = cos(dec);
     double rcp = r * cp;
-    double x = rcp * ct, y = rcp * st;
+    double x = rcp * ct, y = rcp * st_;
     double rpd = r * decd;
     double ww = rpd * sp;  // - cp*rd with rd = 0
     double p[3] = {x, y, r * sp};
-    double v[3] = {-y * rad - ww * ct, x * rad - ww * st, rpd * cp};
+    double v[3] = {-y * rad - ww * ct, x * rad - ww * st_, rpd * cp};
     double vm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
     if (vm / ERFA_DC > 0.5) { v[0] = v[1] = v[2] = 0.0; }
     double pm_ = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
@@ -87,11 +92,20 @@ PD void starpm_dir(double ra, double dec, double pmr, double pmd, double px, dou
         odel = del;
     }
     double wr = (betsr != 0.0) ? d + del / betsr : 1.0;
-    double v1[3] = {wr * usr[0] + d * ust[0], wr * usr[1] + d * ust[1], wr * usr[2] + d * ust[2]};
-    // starpm
-    double tl1 = pm_ / ERFA_DC;
-    double q[3] = {p[0] + (dt_days + tl1) * v1[0], p[1] + (dt_days + tl1) * v1[1],
-                   p[2] + (dt_days + tl1) * v1[2]};
+    for (int k = 0; k < 3; k++) {
+        st.p[k] = p[k];
+        st.v1[k] = wr * usr[k] + d * ust[k];
+    }
+    st.tl1 = pm_ / ERFA_DC;
+}
+
+// starpm's propagation to dt_days, then pvstar -> (ra, dec) -> xyz_from_radec
+// (astrometry.py:530), i.e. the unit vector of the propagated position.
+PD void pm_dir(const PmState& st, double dt_days, double out[3]) {
+    const double* p = st.p;
+    const double* v1 = st.v1;
+    const double tl1 = st.tl1;
+    double q[3] = {p[0] + (dt_days + tl1) * v1[0], p[1] + (dt_days + tl1) * v1[1], p[2] + (dt_days + tl1) * v1[2]};
     double r2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2];
     double rdv = q[0] * v1[0] + q[1] * v1[1] + q[2] * v1[2];
     double v2 = v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2];
@@ -99,12 +113,10 @@ PD void starpm_dir(double ra, double dec, double pmr, double pmd, double px, dou
     double tl2 = (-rdv + sqrt(rdv * rdv + c2mv2 * r2)) / c2mv2;
     double s = dt_days + (tl1 - tl2);
     double p2[3] = {p[0] + s * v1[0], p[1] + s * v1[1], p[2] + s * v1[2]};
-    // pvstar -> (ra, dec) -> xyz_from_radec (astrometry.py:530)
-    double th = atan2(p2[1], p2[0]);
-    double ph = atan2(p2[2], sqrt(p2[0] * p2[0] + p2[1] * p2[1]));
-    out[0] = cos(th) * cos(ph);
-    out[1] = sin(th) * cos(ph);
-    out[2] = sin(ph);
+    double in = 1.0 / sqrt(p2[0] * p2[0] + p2[1] * p2[1] + p2[2] * p2[2]);
+    out[0] = p2[0] * in;
+    out[1] = p2[1] * in;
+    out[2] = p2[2] * in;
 }
 
 // Ecliptic -> ICRS rotation (pulsar_ecliptic.py:70: rotation_matrix(obl, "x") is ICRS->ECL)
@@ -121,36 +133,53 @@ PD void icrs_to_ecl(double obl, const double e[3], double o[3]) {
     o[2] = -s * e[1] + c * e[2];
 }
 
-// Unit vector SSB->pulsar (ICRS) at TDB epoch `epoch_mjd` (astrometry.py:469-528
-// AstrometryEquatorial.ssb_to_psb_xyz_ICRS; :71 base path + SkyCoord apply_space_motion for
-// ecliptic models, sky_coordinate.py apply_space_motion -> erfa.pmsafe, 1-kpc dummy distance
-// utils.py:2171).
-PD void psr_dir_icrs(const pint_spec_t& S, const double* P, double epoch_mjd, double L[3]) {
+// Per-instance constants of the astrometry (computed once by k_prep): the pulsar
+// direction without proper motion, or the starpm state, and the position angles used by
+// the design-matrix columns.  astrometry.py:469-528 AstrometryEquatorial.ssb_to_psb_xyz_ICRS;
+// :71 base path + SkyCoord apply_space_motion for ecliptic models (sky_coordinate.py
+// apply_space_motion -> erfa.pmsafe, 1-kpc dummy distance utils.py:2171).
+struct InstConst {
+    PmState pm;
+    double L0[3];
+    double posep;        // POSEPOCH (MJD) or 0
+    double plon, plat;   // rad (RAJ in hourangle, ELONG/ELAT/DECJ in deg -> rad)
+    double cplat, splat;
+    double F0, iF0;
+    int has_pm;
+    int pad_;
+};
+
+PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
+    C.F0 = pval(P, S.o_F);
+    C.iF0 = 1.0 / C.F0;
+    C.has_pm = 0;
+    C.L0[0] = 0.0; C.L0[1] = 0.0; C.L0[2] = 1.0;
+    C.posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
+    C.plon = C.plat = C.cplat = C.splat = 0.0;
+    if (!S.astrometry) return;
     double lon = pval(P, S.o_lon), lat = pval(P, S.o_lat);
     double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
     double pmb = S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0;
-    double posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
+    C.plon = lon * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
+    C.plat = lat * DEG_RAD;
+    C.cplat = cos(C.plat);
+    C.splat = sin(C.plat);
     if (S.astrometry == 1) {
         double ra = lon * HA_RAD, dec = lat * DEG_RAD;
-        if (pml == 0.0 && pmb == 0.0) {
-            L[0] = cos(ra) * cos(dec);
-            L[1] = sin(ra) * cos(dec);
-            L[2] = sin(dec);
-            return;
-        }
+        C.L0[0] = cos(ra) * cos(dec);
+        C.L0[1] = sin(ra) * cos(dec);
+        C.L0[2] = sin(dec);
+        if (pml == 0.0 && pmb == 0.0) return;
         double px_as = (S.o_px >= 0 ? pval(P, S.o_px) : 0.0) * 1e-3;
-        double pmr = pml * MAS_RAD / cos(dec);
-        double pmd = pmb * MAS_RAD;
-        starpm_dir(ra, dec, pmr, pmd, px_as, epoch_mjd - posep, L);
+        pm_setup(ra, dec, pml * MAS_RAD / cos(dec), pmb * MAS_RAD, px_as, C.pm);
+        C.has_pm = 1;
         return;
     }
     // ecliptic
     double l = lon * DEG_RAD, b = lat * DEG_RAD;
     double ue[3] = {cos(l) * cos(b), sin(l) * cos(b), sin(b)};
-    if (pml == 0.0 && pmb == 0.0) {
-        ecl_to_icrs(S.obliquity, ue, L);
-        return;
-    }
+    ecl_to_icrs(S.obliquity, ue, C.L0);
+    if (pml == 0.0 && pmb == 0.0) return;
     // tangential velocity (rad/yr at unit distance) in ecliptic, rotated to ICRS
     double el[3] = {-sin(l), cos(l), 0.0};
     double eb[3] = {-sin(b) * cos(l), -sin(b) * sin(l), cos(b)};
@@ -165,7 +194,19 @@ PD void psr_dir_icrs(const pint_spec_t& S, const double* P, double epoch_mjd, do
     double edec[3] = {-sin(dec) * cos(ra), -sin(dec) * sin(ra), cos(dec)};
     double pmra_c = v[0] * era[0] + v[1] * era[1] + v[2] * era[2];
     double pmdec = v[0] * edec[0] + v[1] * edec[1] + v[2] * edec[2];
-    starpm_dir(ra, dec, pmra_c / cos(dec), pmdec, 1e-3 /* 1 kpc dummy */, epoch_mjd - posep, L);
+    pm_setup(ra, dec, pmra_c / cos(dec), pmdec, 1e-3 /* 1 kpc dummy */, C.pm);
+    C.has_pm = 1;
+}
+
+// Unit vector SSB->pulsar (ICRS) at TDB epoch `epoch_mjd`.
+PD void psr_dir_icrs(const InstConst& C, double epoch_mjd, double L[3]) {
+    if (C.has_pm) {
+        pm_dir(C.pm, epoch_mjd - C.posep, L);
+    } else {
+        L[0] = C.L0[0];
+        L[1] = C.L0[1];
+        L[2] = C.L0[2];
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -187,6 +228,9 @@ struct BinState {
     double Dre, Drep, Drepp;
     // DD
     double E, sinE, cosE, nu, k, omega, OMDOT_rs, er, eTheta, alpha, beta;
+    // trigonometry shared by the delay and every derivative column (computed once)
+    double s1, c1, s2, c2, s3, c3, s4, c4;                   // ELL1: sin/cos(k Phi)
+    double snu, cnu, sw, cw, soPn, coPn, logNum, lgNum, sqTh, sqE;  // DD
     double delay;
     int status;
 };
@@ -241,6 +285,7 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
     double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2;
     double s1 = sin(Phi), c1 = cos(Phi), s2 = sin(2 * Phi), c2 = cos(2 * Phi);
     double s3 = sin(3 * Phi), c3 = cos(3 * Phi), s4 = sin(4 * Phi), c4 = cos(4 * Phi);
+    B.s1 = s1; B.c1 = c1; B.s2 = s2; B.c2 = c2; B.s3 = s3; B.c3 = c3; B.s4 = s4; B.c4 = c4;
     double e1s = e1 * e1, e2s = e2 * e2;
     // d_delayR_da1 (ELL1_model.py:221-253)
     B.R0 = s1 + 0.5 * (e2 * s2 - e1 * c2) -
@@ -269,42 +314,19 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
 }
 
 // d(ELL1 delay)/d(par) per SI unit (ELL1_model.py:637 d_ELL1delay_d_par -> :174, :325, :406,
-// :483, :605).  prtl_der() seeds follow binary_generic.py:267 semantics incl. zero entries.
-PD double ell1_deriv(const BinState& B, int pid) {
-    double d_a1 = 0, d_Phi = 0, d_e1 = 0, d_e2 = 0, d_pb = 0, d_TM2 = 0, d_SINI = 0;
-    double tt0 = B.tt0, PBs = B.PBs;
-    switch (pid) {
-        case PINT_B_A1: d_a1 = 1; break;
-        case PINT_B_A1DOT: d_a1 = tt0; break;
-        case PINT_B_EPS1: d_e1 = 1; break;
-        case PINT_B_EPS1DOT: d_e1 = tt0; break;
-        case PINT_B_EPS2: d_e2 = 1; break;
-        case PINT_B_EPS2DOT: d_e2 = tt0; break;
-        case PINT_B_TASC:
-            d_e1 = -B.EPS1DOT;
-            d_e2 = -B.EPS2DOT;
-            // d_Phi_d_TASC uses pb()=pbprime and pbdot() (ELL1_model.py:108)
-            d_Phi = (B.PBDOT * tt0 / B.pb - 1.0) * TWO_PI / B.pb;
-            break;
-        case PINT_B_PB:
-            d_Phi = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs));
-            d_pb = 1;
-            break;
-        case PINT_B_PBDOT:
-            d_Phi = -PI_D * tt0 * tt0 / (PBs * PBs);
-            d_pb = tt0;
-            break;
-        case PINT_B_XPBDOT: d_Phi = -PI_D * tt0 * tt0 / (PBs * PBs); break;
-        case PINT_B_M2: d_TM2 = TSUN; break;
-        case PINT_B_SINI: d_SINI = 1; break;
-        default: return 0.0;
-    }
-    double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2, a1 = B.a1;
-    double s1 = sin(Phi), c1 = cos(Phi), s2 = sin(2 * Phi), c2 = cos(2 * Phi);
-    double s3 = sin(3 * Phi), c3 = cos(3 * Phi), s4 = sin(4 * Phi), c4 = cos(4 * Phi);
+// :483, :605).  The reference's chain rule is linear in the seeds (d a1, d Phi, d eps1,
+// d eps2, d pb, d TM2, d SINI)/d(par) of prtl_der() (binary_generic.py:267), so the
+// gradient over those seven primitives is formed once per TOA (ell1_grad) and every
+// column is a dot product with its seed vector (ell1_deriv).
+struct Ell1Grad {
+    double a1, Phi, e1, e2, pb, TM2, SINI;
+};
+
+PD void ell1_grad(const BinState& B, Ell1Grad& g) {
+    double e1 = B.eps1, e2 = B.eps2, a1 = B.a1;
+    double s1 = B.s1, c1 = B.c1, s2 = B.s2, c2 = B.c2, s3 = B.s3, c3 = B.c3, s4 = B.s4, c4 = B.c4;
     double e1s = e1 * e1, e2s = e2 * e2;
     double nhat = B.nhat, Dre = B.Dre, Drep = B.Drep, Drepp = B.Drepp;
-    double d_nhat = -TWO_PI / (B.pb * B.pb) * d_pb;
     // d_Dre_d_par (:325-394)
     double dDre_de1 = a1 * (-0.5 * c2 - (1.0 / 8) * (-2 * e2 * c1 + 6 * e2 * c3 + 6 * e1 * s1 + 6 * e1 * s3) -
                             (1.0 / 12) * (6 * e1 * e2 * s2 - 6 * e2s * c2 - 12 * e1s * c2 + 24 * e1 * e2 * s4 +
@@ -312,7 +334,6 @@ PD double ell1_deriv(const BinState& B, int pid) {
     double dDre_de2 = a1 * (0.5 * s2 - (1.0 / 8) * (-2 * e1 * c1 + 6 * e1 * c3 + 10 * e2 * s1 - 6 * e2 * s3) -
                             (1.0 / 12) * (15 * e2s * s2 + 3 * e1s * s2 - 12 * e1 * e2 * c2 - 12 * e2s * s4 +
                                           12 * e1s * s4 + 24 * e1 * e2 * c4));
-    double dDre = d_a1 * B.R0 + Drep * d_Phi + dDre_de1 * d_e1 + dDre_de2 * d_e2;
     // d_Drep_d_par (:406-476)
     double dDrep_de1 = a1 * (s2 - (1.0 / 8) * (6 * e1 * c1 + 18 * e1 * c3 + 2 * e2 * s1 - 18 * e2 * s3) -
                              (1.0 / 12) * (12 * e1 * e2 * c2 + 12 * e2s * s2 + 16 * e1s * s2 + 96 * e1 * e2 * c4 -
@@ -320,7 +341,6 @@ PD double ell1_deriv(const BinState& B, int pid) {
     double dDrep_de2 = a1 * (c2 - (1.0 / 8) * (2 * e1 * s1 - 18 * e1 * s3 + 10 * e2 * c1 - 18 * e2 * c3) -
                              (1.0 / 12) * (30 * e2s * c2 + 6 * e1s * c2 + 24 * e1 * e2 * s2 - 48 * e2s * c4 +
                                            48 * e1s * c4 - 96 * e1 * e2 * s4));
-    double dDrep = d_a1 * B.R1 + Drepp * d_Phi + dDrep_de1 * d_e1 + dDrep_de2 * d_e2;
     // d_Drepp_d_par (:483-597)
     double dDrepp_dPhi =
         a1 * (-c1 - 4.0 * (e1 * s2 + e2 * c2) -
@@ -333,18 +353,43 @@ PD double ell1_deriv(const BinState& B, int pid) {
     double dDrepp_de2 = a1 * (-2.0 * s2 - (1.0 / 8) * (2 * e1 * c1 - 54 * e1 * c3 - 10 * e2 * s1 + 54 * e2 * s3) -
                               (1.0 / 12) * (-60 * e2s * s2 - 12 * e1s * s2 + 48 * e1 * e2 * c2 + 192 * e2s * s4 -
                                             192 * e1s * s4 - 384 * e1 * e2 * c4));
-    double dDrepp = d_a1 * B.R2 + dDrepp_dPhi * d_Phi + dDrepp_de1 * d_e1 + dDrepp_de2 * d_e2;
     // d_delayI_d_par (:174-219)
     double nD = nhat * Drep;
     double dI_dDre = (1 - nD + nD * nD + 0.5 * nhat * nhat * Dre * Drepp) + Dre * 0.5 * nhat * nhat * Drepp;
     double dI_dDrep = -Dre * nhat + 2 * nD * nhat * Dre;
     double dI_dDrepp = 0.5 * (nhat * Dre) * (nhat * Dre);
     double dI_dnhat = Dre * (-Drep + 2 * nD * Drep + nhat * Dre * Drepp);
-    double dI = dI_dDre * dDre + dI_dDrep * dDrep + dI_dDrepp * dDrepp + dI_dnhat * d_nhat;
     // d_delayS_d_par (:605-631) -- note the reference's d_delayS_d_Phi omits cos(Phi) (:620)
     double lg = 1 - B.SINI * s1;
-    double dS = -2 * log(lg) * d_TM2 + (-2 * B.TM2 / lg * (-s1)) * d_SINI + (-2 * B.TM2 / lg * (-B.SINI)) * d_Phi;
-    return dI + dS;
+    g.a1 = dI_dDre * B.R0 + dI_dDrep * B.R1 + dI_dDrepp * B.R2;
+    g.Phi = dI_dDre * Drep + dI_dDrep * Drepp + dI_dDrepp * dDrepp_dPhi + (-2 * B.TM2 / lg * (-B.SINI));
+    g.e1 = dI_dDre * dDre_de1 + dI_dDrep * dDrep_de1 + dI_dDrepp * dDrepp_de1;
+    g.e2 = dI_dDre * dDre_de2 + dI_dDrep * dDrep_de2 + dI_dDrepp * dDrepp_de2;
+    g.pb = dI_dnhat * (-TWO_PI / (B.pb * B.pb));
+    g.TM2 = -2 * log(lg);
+    g.SINI = -2 * B.TM2 / lg * (-s1);
+}
+
+PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
+    double tt0 = B.tt0, PBs = B.PBs;
+    switch (pid) {
+        case PINT_B_A1: return g.a1;
+        case PINT_B_A1DOT: return g.a1 * tt0;
+        case PINT_B_EPS1: return g.e1;
+        case PINT_B_EPS1DOT: return g.e1 * tt0;
+        case PINT_B_EPS2: return g.e2;
+        case PINT_B_EPS2DOT: return g.e2 * tt0;
+        case PINT_B_TASC:
+            // d_Phi_d_TASC uses pb()=pbprime and pbdot() (ELL1_model.py:108)
+            return g.e1 * (-B.EPS1DOT) + g.e2 * (-B.EPS2DOT) + g.Phi * ((B.PBDOT * tt0 / B.pb - 1.0) * TWO_PI / B.pb);
+        case PINT_B_PB:
+            return g.Phi * (TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs))) + g.pb;
+        case PINT_B_PBDOT: return g.Phi * (-PI_D * tt0 * tt0 / (PBs * PBs)) + g.pb * tt0;
+        case PINT_B_XPBDOT: return g.Phi * (-PI_D * tt0 * tt0 / (PBs * PBs));
+        case PINT_B_M2: return g.TM2 * TSUN;
+        case PINT_B_SINI: return g.SINI;
+        default: return 0.0;
+    }
 }
 
 // ---- DD (DD_model.py, binary_generic.py) ------------------------------------------
@@ -396,8 +441,14 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_dela
     B.er = e * (1 + B.DR);
     B.eTheta = e * (1 + B.DTH);
     double sw = sin(B.omega), cw = cos(B.omega);
+    B.sw = sw;
+    B.cw = cw;
+    B.snu = sin(B.nu);
+    B.cnu = cos(B.nu);
+    B.sqTh = sqrt(1 - B.eTheta * B.eTheta);
+    B.sqE = sqrt(1 - e * e);
     B.alpha = B.a1 * sw;                                    // :223
-    B.beta = B.a1 * sqrt(1 - B.eTheta * B.eTheta) * cw;     // :275
+    B.beta = B.a1 * B.sqTh * cw;                            // :275
     double sE = B.sinE, cE = B.cosE;
     double delayR = B.alpha * (cE - B.er) + B.beta * sE;    // :423
     B.Dre = delayR + B.GAMMA * sE;                          // :434 + delayE :786
@@ -407,10 +458,14 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_dela
     double nH = B.nhat;
     double delayI = B.Dre * (1 - nH * B.Drep + (nH * B.Drep) * (nH * B.Drep) + 0.5 * nH * nH * B.Dre * B.Drepp -
                              0.5 * e * sE / (1 - e * cE) * nH * nH * B.Dre * B.Drep);  // :602-646
-    double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + sqrt(1 - e * e) * cw * sE);
-    double delayS = -2 * B.TM2 * log(logNum);               // :700-720
+    double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + B.sqE * cw * sE);
+    B.logNum = logNum;
+    B.lgNum = log(logNum);
+    double delayS = -2 * B.TM2 * B.lgNum;                   // :700-720
     double oPn = B.omega + B.nu;
-    double delayA = B.A0 * (sin(oPn) + e * sw) + B.B0 * (cos(oPn) + e * cw);  // :794-806
+    B.soPn = sin(oPn);
+    B.coPn = cos(oPn);
+    double delayA = B.A0 * (B.soPn + e * sw) + B.B0 * (B.coPn + e * cw);  // :794-806
     B.delay = delayI + delayS + delayA;
 }
 
@@ -442,7 +497,7 @@ PD double ddm_deriv(const BinState& B, int pid) {
     else if (pid == PINT_B_EDOT) d_E = tt0 * d_E_d_ECC;
     else if (orbit_par) d_E = d_M / (1.0 - cE * e);
     // nu (binary_generic.py:451-624)
-    double snu = sin(B.nu), cnu = cos(B.nu);
+    double snu = B.snu, cnu = B.cnu;
     double d_nu_d_E = (1 + e * cnu) / (1 - e * cE) * (sE / snu);
     double d_nu_d_ecc = sE * sE / ((e * cE - 1) * (e * cE - 1)) / snu;
     double d_nu = 0;
@@ -459,8 +514,8 @@ PD double ddm_deriv(const BinState& B, int pid) {
     // er / eTheta (DD_model.py:149-205): d_ecc_d_par only for T0/ECC/EDOT; DR/DTH -> ecc
     double d_er = (pid == PINT_B_DR) ? e : d_ecc;
     double d_eTh = (pid == PINT_B_DTH) ? e : d_ecc;
-    double sw = sin(B.omega), cw = cos(B.omega);
-    double eTh = B.eTheta, sq = sqrt(1 - eTh * eTh);
+    double sw = B.sw, cw = B.cw;
+    double eTh = B.eTheta, sq = B.sqTh;
     // alpha (DD_model.py:225-246)
     double d_alpha = d_a1 * sw + B.a1 * cw * d_omega;
     // beta (DD_model.py:277-407): specific d_beta_d_X methods take precedence in prtl_der
@@ -497,24 +552,24 @@ PD double ddm_deriv(const BinState& B, int pid) {
     double dI_dx = (Dre * nH) * (Dre * nH) * Drep;
     double dI = dDre * dI_dDre + dDrep * dI_dDrep + dDrepp * dI_dDrepp + dx * dI_dx + d_nhat * dI_dnhat;
     // delayS (DD_model.py:722-784)
-    double sq1 = sqrt(1 - e * e);
-    double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + sq1 * cw * sE);
+    double sq1 = B.sqE;
+    double logNum = B.logNum;
     double d_TM2 = (pid == PINT_B_M2) ? TSUN : 0.0;
     double d_SINI = (pid == PINT_B_SINI) ? 1.0 : 0.0;
     double TM2 = B.TM2;
-    double dS = d_TM2 * (-2 * log(logNum)) +
+    double dS = d_TM2 * (-2 * B.lgNum) +
                 d_ecc * (-2 * TM2 / logNum * (-cE - B.SINI * (-e * cw * sE / sq1 - sw))) +
                 d_E * (-2 * TM2 / logNum * (e * sE - B.SINI * (sq1 * cE * cw - sE * sw))) +
                 d_omega * (2 * TM2 / logNum * B.SINI * ((cE - e) * cw - sq1 * sE * sw)) +
                 d_SINI * (-2 * TM2 / logNum * (-sq1 * cw * sE - (cE - e) * sw));
     // delayA (DD_model.py:808-848)
-    double oPn = B.omega + B.nu;
+    const double soPn = B.soPn, coPn = B.coPn;
     double dA;
-    if (pid == PINT_B_A0) dA = e * sw + sin(oPn);
-    else if (pid == PINT_B_B0) dA = e * cw + cos(oPn);
+    if (pid == PINT_B_A0) dA = e * sw + soPn;
+    else if (pid == PINT_B_B0) dA = e * cw + coPn;
     else
-        dA = d_omega * (B.A0 * (cos(oPn) + e * cw) - B.B0 * (sin(oPn) + e * sw)) +
-             d_nu * (B.A0 * cos(oPn) - B.B0 * sin(oPn)) + d_ecc * (B.A0 * sw + B.B0 * cw);
+        dA = d_omega * (B.A0 * (coPn + e * cw) - B.B0 * (soPn + e * sw)) +
+             d_nu * (B.A0 * coPn - B.B0 * soPn) + d_ecc * (B.A0 * sw + B.B0 * cw);
     return dI + dS + dA;
 }
 
@@ -555,11 +610,19 @@ PD double spin_freq(const pint_spec_t& S, const double* P, double dt) {
     return r;
 }
 
-// Evaluate one TOA.  If M != nullptr, writes the design-matrix row (column-major, leading
-// dimension ld) for columns 0..ncol-1 (timing_model.py:2164-2173).
+// Column runs (built by pint_add_pulsar from spec.col_kind/col_index): consecutive
+// design-matrix columns of one kind with consecutive indices, so the row loop walks ~15
+// runs with tight per-kind inner loops instead of a switch per column.
+struct ColRun {
+    int kind, col0, cnt, idx0;
+};
+
+// Evaluate one TOA.  If Mb != nullptr, writes the design-matrix row r (column-major,
+// leading dimension ld, column c at Mb + c*ld) for columns 0..ncol-1
+// (timing_model.py:2164-2173).
 template <int BIN>
-PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut& o, double* M,
-                 long ld) {
+PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalOut& o,
+                 double* Mb, unsigned r, long ld, const ColRun* runs, int nrun) {
     o.status = 0;
     double delay = 0.0;
     // ---- astrometry: solar_system_geometric_delay (astrometry.py:155-184) ----
@@ -570,7 +633,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut
     double rr = 0.0, re_dot_L = 0.0;
     double px_mas = S.o_px >= 0 ? pval(P, S.o_px) : 0.0;
     if (S.astrometry) {
-        psr_dir_icrs(S, P, tdb_f, L);
+        psr_dir_icrs(C, tdb_f, L);
         rr = t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1] + t.pos[2] * t.pos[2];
         re_dot_L = t.pos[0] * L[0] + t.pos[1] * L[1] + t.pos[2] * L[2];
         if (has_pos) {
@@ -584,9 +647,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut
     }
     // ---- solar system Shapiro (solar_system_shapiro.py:59-124), sun only ----
     if (S.shapiro && !is_bary) {
-        double r = sqrt(t.sun[0] * t.sun[0] + t.sun[1] * t.sun[1] + t.sun[2] * t.sun[2]);
+        double rs = sqrt(t.sun[0] * t.sun[0] + t.sun[1] * t.sun[1] + t.sun[2] * t.sun[2]);
         double rct = t.sun[0] * L[0] + t.sun[1] * L[1] + t.sun[2] * L[2];
-        delay += -2.0 * TSUN * log((r - rct) / AU_KM);
+        delay += -2.0 * TSUN * log((rs - rct) / AU_KM);
     }
     // ---- barycentric radio frequency (astrometry.py:359-364) ----
     double bfreq = t.freq;
@@ -650,88 +713,94 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const ToaRow& t, EvalOut
     double dtd = dd_to_d(dt);
     o.fdt = spin_freq(S, P, dtd);
     o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
-    if (!M) return;
+    if (!Mb) return;
     // ---- design matrix row (timing_model.py:2073-2175) ----
-    double F0 = pval(P, S.o_F);
-    double chain = o.fdt / F0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
-    // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities)
-    double r_m = 0, edec = 0, era = 0;
-    double plon = 0, plat = 0;
+    const double F0 = C.F0, iF0 = C.iF0;
+    const double chain = o.fdt * iF0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+    // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities), once per TOA
+    double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
     if (S.astrometry) {
         double r_km = sqrt(rr);
-        r_m = r_km;  // keep km; divide by c in km/s
         double xy = sqrt(t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1]);
-        edec = atan2(t.pos[2], xy);
-        era = atan2(t.pos[1], t.pos[0]);
+        double edec = atan2(t.pos[2], xy);
+        double era = atan2(t.pos[1], t.pos[0]);
         if (S.astrometry == 2) {
             // earth ecliptic lon/lat via ICRS->PulsarEcliptic (astrometry.py:1034-1055)
             double ue[3] = {cos(era) * cos(edec), sin(era) * cos(edec), sin(edec)}, ee[3];
             icrs_to_ecl(S.obliquity, ue, ee);
             era = atan2(ee[1], ee[0]);
             edec = atan2(ee[2], sqrt(ee[0] * ee[0] + ee[1] * ee[1]));
-            plon = pval(P, S.o_lon) * DEG_RAD;
-        } else {
-            plon = pval(P, S.o_lon) * HA_RAD;
         }
-        plat = pval(P, S.o_lat) * DEG_RAD;
+        const double ced = cos(edec), sed = sin(edec);
+        const double sdl = sin(C.plon - era), cdl = cos(C.plon - era);
+        const double te_s = S.o_POSEPOCH >= 0 ? dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC)) : 0.0;
+        const double rc = chain * r_km / C_KMS;
+        // d_delay_astrometry_d_RAJ / _ELONG, _DECJ / _ELAT, PM partials x te (astrometry.py:536-627, 1067-1170)
+        gLON = rc * (ced * C.cplat * sdl) * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
+        gLAT = rc * (ced * C.splat * cdl - sed * C.cplat) * DEG_RAD;
+        gPMLON = rc * (ced * sdl) * te_s * MASYR_RADS;
+        gPMLAT = rc * (ced * C.splat * cdl - C.cplat * sed) * te_s * MASYR_RADS;
+        // d_delay_astrometry_d_PX (astrometry.py:219-249)
+        gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) / (AU_KM * C_KMS)) * MAS_RAD;
     }
-    double te_s = 0.0;
-    if (S.o_POSEPOCH >= 0) te_s = dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC));
-    for (int c = 0; c < S.ncol; c++) {
-        int kind = S.col_kind[c], idx = S.col_index[c];
-        double v = 0.0;
-        switch (kind) {
-            case PINT_COL_OFFSET: v = 1.0 / F0; break;
-            case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): dt^(k+1)/(k+1)!
-                double r = 1.0;
-                for (int j = 1; j <= idx + 1; j++) r = r * dtd / (double)j;
-                v = -r / F0;
+    Ell1Grad eg;
+    if (BIN == 1) ell1_grad(B, eg);
+    const double dmc = chain * DMCONST * inv_f2;
+    for (int u = 0; u < nrun; u++) {
+        const ColRun R = runs[u];
+        double* colp = Mb + (long)R.col0 * ld;
+        switch (R.kind) {
+            case PINT_COL_OFFSET: colp[r] = iF0; break;
+            case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): -dt^(k+1)/(k+1)! / F0
+                double v = 1.0;
+                for (int j = 1; j <= R.idx0; j++) v = v * dtd / (double)j;
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    v = v * dtd / (double)(R.idx0 + j + 1);
+                    colp[r] = -v * iF0;
+                }
             } break;
-            case PINT_COL_JUMP: v = ((t.jmask >> idx) & 1ull) ? -1.0 : 0.0; break;  // jump.py:138
-            case PINT_COL_LON: {  // d_delay_astrometry_d_RAJ / _ELONG
-                double g = cos(edec) * cos(plat) * sin(plon - era);
-                double dd_ = r_m * g / C_KMS;
-                v = chain * dd_ * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
-            } break;
-            case PINT_COL_LAT: {
-                double g = cos(edec) * sin(plat) * cos(plon - era) - sin(edec) * cos(plat);
-                v = chain * (r_m * g / C_KMS) * DEG_RAD;
-            } break;
-            case PINT_COL_PMLON: {
-                double g = cos(edec) * sin(plon - era);
-                v = chain * (r_m * g * te_s / C_KMS) * MASYR_RADS;
-            } break;
-            case PINT_COL_PMLAT: {
-                double g = cos(edec) * sin(plat) * cos(plon - era) - cos(plat) * sin(edec);
-                v = chain * (r_m * g * te_s / C_KMS) * MASYR_RADS;
-            } break;
-            case PINT_COL_PX: {  // astrometry.py:219-249
-                double pxr2 = rr - re_dot_L * re_dot_L;
-                v = chain * 0.5 * (pxr2 / (AU_KM * C_KMS)) * MAS_RAD;
-            } break;
+            case PINT_COL_JUMP:  // jump.py:138
+                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = ((t.jmask >> (R.idx0 + j)) & 1ull) ? -1.0 : 0.0;
+                break;
+            case PINT_COL_LON: colp[r] = gLON; break;
+            case PINT_COL_LAT: colp[r] = gLAT; break;
+            case PINT_COL_PMLON: colp[r] = gPMLON; break;
+            case PINT_COL_PMLAT: colp[r] = gPMLAT; break;
+            case PINT_COL_PX: colp[r] = gPX; break;
             case PINT_COL_DM: {  // d_dm_d_DMs (dispersion_model.py:253) * DMconst / bfreq^2
-                double r = 1.0;
-                for (int j = 1; j <= idx; j++) r = r * dt_yr_dm / (double)j;
-                v = chain * DMCONST * r * inv_f2;
+                double v = 1.0;
+                for (int j = 1; j <= R.idx0; j++) v = v * dt_yr_dm / (double)j;
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    if (j > 0) v = v * dt_yr_dm / (double)(R.idx0 + j);
+                    colp[r] = dmc * v;
+                }
             } break;
-            case PINT_COL_DMX: {  // d_dm_d_DMX (:684)
-                double sel = (t.dmx_a == idx || t.dmx_b == idx) ? 1.0 : 0.0;
-                v = chain * DMCONST * sel * inv_f2;
+            case PINT_COL_DMX:  // d_dm_d_DMX (:684): 1 on the bin's TOAs
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    const int idx = R.idx0 + j;
+                    colp[r] = (t.dmx_a == idx || t.dmx_b == idx) ? dmc : 0.0;
+                }
+                break;
+            case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103): logf^(k+1)
+                double v = 1.0;
+                for (int j = 0; j <= R.idx0; j++) v *= logf;
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    if (j > 0) v *= logf;
+                    colp[r] = chain * v;
+                }
             } break;
-            case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103)
-                double r = 1.0;
-                for (int j = 0; j < idx + 1; j++) r *= logf;
-                v = chain * r;
-            } break;
-            case PINT_COL_BIN: {
-                double d = 0.0;
-                if (BIN == 1) d = ell1_deriv(B, idx);
-                if (BIN == 2) d = ddm_deriv(B, idx);
-                v = chain * d * bin_unit_factor(idx);
-            } break;
-            default: v = 0.0;
+            case PINT_COL_BIN:
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    const int pid = S.col_index[R.col0 + j];
+                    double d = 0.0;
+                    if (BIN == 1) d = ell1_deriv(B, eg, pid);
+                    if (BIN == 2) d = ddm_deriv(B, pid);
+                    colp[r] = chain * d * bin_unit_factor(pid);
+                }
+                break;
+            default:
+                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
         }
-        M[(long)c * ld] = v;
     }
 }
 

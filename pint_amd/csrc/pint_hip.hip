@@ -35,6 +35,8 @@ struct PsrDev {
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
+    const ColRun* runs;      // design-matrix column runs
+    int nrun;
     int n;
     int K;   // ncol + 2*nred
     int Kp;  // padded K+1 (residual column) to 16
@@ -97,21 +99,33 @@ __device__ double block_sum(double v, double* sh) {
 // ---------------------------------------------------------------------------------
 // k_eval: one thread per TOA row (row n = TZR TOA)
 // ---------------------------------------------------------------------------------
+// k_prep: per-instance constants of the evaluation (astrometry/starpm state, 1/F0), one
+// thread per instance, so k_eval's threads only do per-TOA work.
+__global__ void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, int ninst,
+                       const double* __restrict__ tables, InstConst* __restrict__ ic) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ninst) return;
+    const InstDev I = insts[k];
+    InstConst C;
+    inst_setup(*psrs[I.psr].spec, tables + I.toff, C);
+    ic[k] = C;
+}
+
 template <int WANT_M, int BIN>
 __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
-                                              const double* __restrict__ tables, double* __restrict__ ph_hi,
-                                              double* __restrict__ ph_lo, double* __restrict__ ftay,
-                                              double* __restrict__ delay_out, double* __restrict__ Mout,
-                                              int* __restrict__ status) {
+                                              const double* __restrict__ tables, const InstConst* __restrict__ ic,
+                                              double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                              double* __restrict__ ftay, double* __restrict__ delay_out,
+                                              double* __restrict__ Mout, int* __restrict__ status) {
     int b = blockIdx.x;
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
-    int r = blk_row0[b] + threadIdx.x;
-    int n = I.n;
-    if (r > n) return;
+    const unsigned r = (unsigned)(blk_row0[b] + threadIdx.x);
+    const int n = I.n;
+    if (r > (unsigned)n) return;
     const double* P = tables + I.toff;
     ToaRow t;
     t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
@@ -127,24 +141,26 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
     t.dmx_a = Pd.dmx_a[r];
     t.dmx_b = Pd.dmx_b[r];
     EvalOut o;
-    double* Mrow = (WANT_M && r < n) ? (Mout + I.moff + r) : nullptr;
-    eval_toa<BIN>(S, P, t, o, Mrow, n);
+    double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
+    const bool rowM = WANT_M && r < (unsigned)n;
+    eval_toa<BIN>(S, P, ic[ii], t, o, rowM ? Mb : nullptr, r, n, Pd.runs, Pd.nrun);
     if (o.status) atomicOr(status, 1 << o.status);
     ph_hi[I.roff + r] = o.phase.hi;
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
     delay_out[I.roff + r] = o.delay;
-    if (WANT_M && Mrow && S.nred > 0) {
+    if (WANT_M && rowM && S.nred > 0) {
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
         // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.
         dd ts = dd_mul_d(t.tdb, DAYSEC);
-        for (int k = 0; k < S.nred; k++) {
+        double* colp = Mb + (long)S.ncol * n;
+        for (int k = 0; k < S.nred; k++, colp += 2L * n) {
             dd x = dd_mul_d(ts, Pd.red_freq[k]);
             double fr = dd_to_d(dd_sub(x, dd_floor(x)));
             double sn, cs;
             sincos(TWO_PI * fr, &sn, &cs);
-            Mrow[(long)(S.ncol + 2 * k) * n] = sn;
-            Mrow[(long)(S.ncol + 2 * k + 1) * n] = cs;
+            colp[r] = sn;
+            colp[r + n] = cs;
         }
     }
 }
@@ -1096,6 +1112,7 @@ struct pint_ctx {
     double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
     double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
+    InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
     size_t wpart_cap = 0;
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
@@ -1166,7 +1183,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
-                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart};
+                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic};
     for (auto p : ps) dfree(*p);
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
@@ -1229,6 +1246,20 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
     rc |= upload(ctx, ph, red_freq, (size_t)spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
+    {
+        // design-matrix column runs: same kind, consecutive indices (BIN: same kind only)
+        std::vector<ColRun> runs;
+        for (int c = 0; c < spec->ncol; c++) {
+            const int k = spec->col_kind[c], ix = spec->col_index[c];
+            if (!runs.empty()) {
+                ColRun& R = runs.back();
+                if (R.kind == k && (k == PINT_COL_BIN || R.idx0 + R.cnt == ix)) { R.cnt++; continue; }
+            }
+            runs.push_back(ColRun{k, c, 1, ix});
+        }
+        rc |= upload(ctx, ph, runs.data(), runs.size(), d.runs);
+        d.nrun = (int)runs.size();
+    }
     const pint_spec_t* sp = nullptr;
     rc |= upload(ctx, ph, spec, 1, sp);
     if (rc) return -PINT_E_HIP;
@@ -1408,6 +1439,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(hipMalloc(&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(hipMalloc(&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(hipMalloc(&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_ic, sizeof(InstConst) * ninst));
     HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * (cvoff > 0 ? cvoff : 1), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -1456,6 +1488,9 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     hipSetDevice(ctx->device);
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     record(ctx, want_M ? 2 : 0);
+    hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                       ctx->ninst, ctx->d_tables, ctx->d_ic);
+    HIPCHK(hipGetLastError());
     for (int t = 0; t < 3; t++) {
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
@@ -1463,7 +1498,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         const int* br = ctx->d_blk_row0 + ctx->blk_off[t];
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
-                           ctx->d_tables, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, ctx->d_status)
+                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, ctx->d_status)
         if (want_M) {
             if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
         } else {
