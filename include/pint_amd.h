@@ -19,6 +19,7 @@
 #ifndef PINT_AMD_H
 #define PINT_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -163,7 +164,11 @@ int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const
                    const double *ep_phi);
 
 /* Lazy mode (1): launches return without synchronising or checking the device status;
- * pint_check() synchronises and returns the accumulated status. */
+ * pint_check() synchronises and returns the accumulated status.  In lazy mode
+ * pint_set_tables, pint_read_step and pint_chi2_gls only enqueue their copies
+ * (pint_read_step on a second stream, overlapped with the kernels that follow): host
+ * buffers must stay valid, and outputs are complete, after pint_check().  Use pinned
+ * buffers (pint_host_alloc) for the copies to run asynchronously. */
 int pint_set_lazy(pint_ctx *ctx, int lazy);
 int pint_check(pint_ctx *ctx);
 /* Engine options (no reference counterpart): PINT_OPT_BLOCKED_SOLVE = 1 (default) solves
@@ -171,6 +176,9 @@ int pint_check(pint_ctx *ctx);
  * LDS kernel (used by the tests to cross-check the two). */
 #define PINT_OPT_BLOCKED_SOLVE 1
 int pint_set_option(pint_ctx *ctx, int key, int value);
+/* Page-locked host memory for the output buffers (hipHostMalloc); NULL on failure. */
+void *pint_host_alloc(size_t bytes);
+void pint_host_free(void *p);
 /* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor
  * (L^-1, packed lower). */
 int pint_debug_read(pint_ctx *ctx, int which, double *out);

@@ -1089,6 +1089,9 @@ struct PsrHost {
 struct pint_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t cstream = nullptr;   // copy stream: fit outputs -> host, overlapped with compute
+    hipEvent_t ev_solved = nullptr, ev_copied = nullptr;
+    bool copy_pending = false;
     std::string err;
     std::vector<PsrHost> psrs;
     PsrDev* d_psrs = nullptr;
@@ -1169,6 +1172,9 @@ pint_ctx* pint_ctx_create(int device) {
         return ctx;
     }
     hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
+    hipEventCreateWithFlags(&ctx->ev_solved, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_copied, hipEventDisableTiming);
     for (int i = 0; i < 12; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
     return ctx;
@@ -1200,6 +1206,10 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
     if (ctx->d_status) hipFree(ctx->d_status);
     for (int i = 0; i < 12; i++) hipEventDestroy(ctx->ev[i]);
+    if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
+    if (ctx->ev_solved) hipEventDestroy(ctx->ev_solved);
+    if (ctx->ev_copied) hipEventDestroy(ctx->ev_copied);
+    if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1453,7 +1463,7 @@ int pint_get_tables(pint_ctx* ctx, double* out) {
 
 int pint_set_tables(pint_ctx* ctx, const double* tables) {
     HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
@@ -1474,6 +1484,7 @@ static void update_timings(pint_ctx* ctx) {
 
 static int check_status(pint_ctx* ctx) {
     int st = 0;
+    HIPCHK(hipStreamSynchronize(ctx->cstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
@@ -1595,6 +1606,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
+    if (ctx->copy_pending) {  // the previous step's outputs may still be in flight to the host
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
+        ctx->copy_pending = false;
+    }
     // blocked MFMA solve when the (padded) normal matrix and the Woodbury Sigma fit the LDS
     int Ks = 0, Kn = 0;
     for (auto& I : ctx->inst) {
@@ -1623,6 +1638,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     HIPCHK(hipGetLastError());
     record(ctx, 8);
+    HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
     if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
     update_timings(ctx);
@@ -1630,12 +1646,31 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
 }
 
 int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, double* chi2lin) {
-    if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
-    if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
-    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, hipMemcpyDeviceToHost, ctx->stream));
-    if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // lazy: copies run on the copy stream after the solve, overlapped with the kernels that
+    // follow; the caller's buffers (pinned: pint_host_alloc) are valid after pint_check().
+    hipStream_t st = ctx->lazy ? ctx->cstream : ctx->stream;
+    if (ctx->lazy) HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_solved, 0));
+    if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
+    if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
+    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, hipMemcpyDeviceToHost, st));
+    if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, st));
+    if (ctx->lazy) {
+        HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
+        ctx->copy_pending = true;
+        return PINT_OK;
+    }
+    HIPCHK(hipStreamSynchronize(st));
     return PINT_OK;
+}
+
+void* pint_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 8, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void pint_host_free(void* p) {
+    if (p) hipHostFree(p);
 }
 
 int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
@@ -1670,7 +1705,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     HIPCHK(hipGetLastError());
     record(ctx, 11);
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
@@ -1712,6 +1747,7 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
 
 int pint_sync(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->cstream));
     return PINT_OK;
 }
 

@@ -331,11 +331,32 @@ class Session:
         self.layouts: List[PulsarLayout] = []
         self.inst_psr: List[int] = []
         self.inst_layout: List[PulsarLayout] = []
+        self.lazy = False
+        self._pinned: Dict[str, tuple] = {}
 
     def close(self):
         if self.ctx:
             self.L.pint_ctx_destroy(self.ctx)
             self.ctx = None
+        for ptr_, _ in self._pinned.values():
+            self.L.pint_host_free(ptr_)
+        self._pinned = {}
+
+    def _pin(self, name, n):
+        """Page-locked host buffer of n doubles (reused across calls, grown on demand), so
+        device->host copies of the fit outputs can run asynchronously."""
+        n = max(1, int(n))
+        cur = self._pinned.get(name)
+        if cur is not None and cur[1].size >= n:
+            return cur[1][:n]
+        if cur is not None:
+            self.L.pint_host_free(cur[0])
+        p = self.L.pint_host_alloc(8 * n)
+        if not p:
+            raise MemoryError("pint_host_alloc failed")
+        arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_double)), shape=(n,))
+        self._pinned[name] = (p, arr)
+        return arr
 
     def __del__(self):
         try:
@@ -382,6 +403,7 @@ class Session:
 
     def set_tables(self, tabs):
         tabs = np.ascontiguousarray(tabs, dtype=np.float64)
+        self._tab_keep = tabs  # lazy mode: the host buffer must outlive the enqueued copy
         self._check(self.L.pint_set_tables(self.ctx, L.ptr(tabs)))
 
     # -- reads ----------------------------------------------------------------------
@@ -413,7 +435,10 @@ class Session:
         return [m.reshape(l.K, l.n).T for m, l in zip(self._split(M, sizes), self.inst_layout)]
 
     def set_lazy(self, lazy=True):
+        """Lazy mode: launches and output copies are only enqueued; read_step/chi2_gls return
+        pinned buffers that are complete after check()."""
         self._check(self.L.pint_set_lazy(self.ctx, 1 if lazy else 0))
+        self.lazy = bool(lazy)
 
     def set_blocked_solve(self, on=True):
         self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))
@@ -423,12 +448,15 @@ class Session:
 
     def read_step(self, want_cov=True):
         kk = [l.K + 1 for l in self.inst_layout]
-        dp = np.empty(sum(kk))
-        er = np.empty(sum(kk))
         nc = [len(l.columns) for l in self.inst_layout]
-        cov = np.empty(max(1, sum(c * c for c in nc))) if want_cov else None
-        cl = np.empty(len(kk))
+        dp = self._pin("dp", sum(kk))
+        er = self._pin("er", sum(kk))
+        cov = self._pin("cov", sum(c * c for c in nc)) if want_cov else None
+        cl = self._pin("cl", len(kk))
         self._check(self.L.pint_read_step(self.ctx, L.ptr(dp), L.ptr(er), L.ptr(cov), L.ptr(cl)))
+        if not self.lazy:  # synchronous call: hand out private copies of the pinned buffers
+            dp, er, cl = dp.copy(), er.copy(), cl.copy()
+            cov = cov.copy() if want_cov else None
         covs = []
         if want_cov:
             o = 0
@@ -443,9 +471,9 @@ class Session:
         return self._split(t, [l.tstride for l in self.inst_layout])
 
     def chi2_gls(self):
-        c = np.empty(len(self.inst_layout))
+        c = self._pin("chi2g", len(self.inst_layout))
         self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
-        return c
+        return c if self.lazy else c.copy()
 
     def timing(self):
         ms = np.zeros(6)
