@@ -88,7 +88,7 @@ def main():
 
     def step():
         s.set_tables(flat0)
-        s.eval(want_M=True)
+        s.eval(want_M=Session.FIT)
         s.fit_step(1)
         s.read_step()          # steps, errors, timing covariance -> host (fit outputs)
         s.apply_step(ones)
@@ -121,8 +121,13 @@ def main():
     P = np.array([len(l.columns) for l in lays])     # timing columns
     N = np.array([l.n for l in lays])
     R = K - P
+    # the Gram is formed in the fit layout: dense columns on MFMA (symmetric half), the sparse
+    # DMX columns as bin sums (one (Kd+1)-row multiply-add per TOA)
+    fl = [s.fit_layout(l) for l in lays]
+    Kd = np.array([f[1] for f in fl])
+    ndc = np.array([f[2] for f in fl])
     flops = {
-        "k_gram": float(np.sum(N * (K + 1) * (K + 2))),          # symmetric [T|r]^T W [T|r]
+        "k_gram": float(np.sum(N * (Kd + 1) * (Kd + 2) + np.where(ndc > 0, 2 * N * (Kd + 2), 0))),
         "k_solve": float(np.sum(K.astype(float) ** 3)),          # chol K^3/3 + inverse/cov 2K^3/3
         "k_woodbury": float(np.sum(2 * N * (R + 2))),            # F^T W r, r^T W r, 1^T W r
     }

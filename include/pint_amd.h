@@ -128,7 +128,7 @@ int pint_set_tables(pint_ctx *ctx, const double *tables);
  * want_M, the design matrix (:2073) plus the red-noise basis columns; then residuals
  * (residuals.py:314 calc_phase_resids, :483 calc_time_resids) and the WLS chi2 (:638)
  * for every instance. */
-int pint_eval(pint_ctx *ctx, int want_M);
+int pint_eval(pint_ctx *ctx, int want_M);  /* want_M: 0 none, 1 full, 2 fit layout */
 
 /* Copy results to caller buffers (any pointer may be NULL).  Residual rows are n_i per
  * instance, eval rows n_i+1 (last = TZR TOA), design matrices n_i x K_i column-major
@@ -162,6 +162,13 @@ int pint_chi2_gls(pint_ctx *ctx, double *chi2);
  * matrix block is diagonal), so it adds no Gram columns.  Call before pint_set_instances. */
 int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const int32_t *ep_idx,
                    const double *ep_phi);
+
+/* Fit layout of pulsar `psr` (no reference counterpart; for benchmarks/tests):
+ * out4 = {compact, Gram columns excl. residual, sparse DMX columns, padded Gram width}.
+ * compact = 1 when the DMX columns are kept out of M and the dense Gram (>= 8 free DMX
+ * columns, no TOA in two free bins, no ECORR): pint_eval(ctx, 2) then writes the compact
+ * design matrix, and pint_fit_step forms their Gram rows as bin sums. */
+int pint_fit_layout(pint_ctx *ctx, int psr, int32_t *out4);
 
 /* Lazy mode (1): launches return without synchronising or checking the device status;
  * pint_check() synchronises and returns the accumulated status.  In lazy mode

@@ -590,6 +590,7 @@ struct EvalOut {
     double delay;    // total delay (s)
     double fdt;      // spin frequency at dt incl. delay (for d_phase_d_delay)
     double ftaylor;  // spin frequency at dt without delay (residuals.py:295-310)
+    double dmc;      // value of this TOA's DMX design-matrix entries (compact layout)
     int status;
 };
 
@@ -615,15 +616,20 @@ PD double spin_freq(const pint_spec_t& S, const double* P, double dt) {
 // runs with tight per-kind inner loops instead of a switch per column.
 struct ColRun {
     int kind, col0, cnt, idx0;
+    int dcol0;  // column in the compact fit layout (DMX columns are not stored there: -1)
+    int pad_[3];
 };
 
 // Evaluate one TOA.  If Mb != nullptr, writes the design-matrix row r (column-major,
 // leading dimension ld, column c at Mb + c*ld) for columns 0..ncol-1
-// (timing_model.py:2164-2173).
+// (timing_model.py:2164-2173).  compact: the fit layout, where the DMX columns (1 on the
+// bin's TOAs times one per-TOA value, o.dmc) are not stored and the other columns are
+// packed (ColRun.dcol0).
 template <int BIN>
 PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalOut& o,
-                 double* Mb, unsigned r, long ld, const ColRun* runs, int nrun) {
+                 double* Mb, unsigned r, long ld, const ColRun* runs, int nrun, bool compact) {
     o.status = 0;
+    o.dmc = 0.0;
     double delay = 0.0;
     // ---- astrometry: solar_system_geometric_delay (astrometry.py:155-184) ----
     double L[3] = {0, 0, 1};
@@ -746,9 +752,11 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     Ell1Grad eg;
     if (BIN == 1) ell1_grad(B, eg);
     const double dmc = chain * DMCONST * inv_f2;
+    o.dmc = dmc;
     for (int u = 0; u < nrun; u++) {
         const ColRun R = runs[u];
-        double* colp = Mb + (long)R.col0 * ld;
+        if (compact && R.kind == PINT_COL_DMX) continue;
+        double* colp = Mb + (long)(compact ? R.dcol0 : R.col0) * ld;
         switch (R.kind) {
             case PINT_COL_OFFSET: colp[r] = iF0; break;
             case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): -dt^(k+1)/(k+1)! / F0

@@ -37,6 +37,15 @@ struct PsrDev {
     const double* ep_phi;    // nep prior variances (s^2)
     const ColRun* runs;      // design-matrix column runs
     int nrun;
+    // sparse-DMX fit layout: the DMX columns (one nonzero value per TOA, in its bin) are
+    // kept out of M and out of the dense Gram; their Gram rows are bin sums (k_dmx)
+    const int32_t* cmap;     // K+1: compact column (>= 0) or -(a+1) for DMX column a
+    const int32_t* dptr;     // ndc+1: CSR of the TOAs of each DMX column
+    const int32_t* didx;
+    const int32_t* drow;     // n: DMX column of each TOA (-1: none)
+    int dsplit;              // compact layout applies (>= 8 DMX columns, no ECORR, no overlapping bins)
+    int dcontig;             // every DMX column's TOAs are one contiguous row range (k_gram fuses the bin sums)
+    int ndc, Kd, Kpd, red0c; // DMX columns; compact width (excl. residual), padded, first red column
     int n;
     int K;   // ncol + 2*nred
     int Kp;  // padded K+1 (residual column) to 16
@@ -58,9 +67,53 @@ struct InstDev {
     long eoff;   // ECORR epoch sums offset (nep*Kp) and per-epoch scalars (eoff/Kp)
     long epoff;  // per-epoch scalar offset (nep)
     long ooff;   // residual output offset (n per instance)
+    long sdoff;  // DMX cross-sum offset (ndc*Kpd) / per-column sums offset (ndc)
+    long ddoff;
     int self;    // index of this instance in the batch
     int pad_;
 };
+
+// Symmetric view of an instance's Gram [T|r]^T W [T|r] in the original column order:
+// full layout (cmap == nullptr), or the compact layout's dense Gram plus the DMX bin sums.
+struct GramView {
+    const double* Gp;
+    int Kp;
+    const int32_t* cmap;
+    const double* Sd;  // ndc x Kp: sum_{i in bin a} w_i x_i [T|r]_i (compact columns)
+    const double* DD;  // ndc: sum_{i in bin a} w_i x_i^2
+    __device__ __forceinline__ double operator()(int i, int j) const {
+        if (!cmap) {
+            if (i > j) { int t = i; i = j; j = t; }
+            return Gp[(long)i * Kp + j];
+        }
+        int a = cmap[i], b = cmap[j];
+        if (a >= 0 && b >= 0) {
+            if (a > b) { int t = a; a = b; b = t; }
+            return Gp[(long)a * Kp + b];
+        }
+        if (a < 0 && b < 0) return a == b ? DD[-a - 1] : 0.0;
+        if (a < 0) return Sd[(long)(-a - 1) * Kp + b];
+        return Sd[(long)(-b - 1) * Kp + a];
+    }
+};
+
+__device__ __forceinline__ GramView gram_view(const PsrDev& Pd, const InstDev& I, const double* Gpart, bool cmp,
+                                              const double* Sd, const double* DD) {
+    GramView g;
+    g.Gp = Gpart + I.goff;
+    g.Kp = cmp ? Pd.Kpd : I.Kp;
+    g.cmap = cmp ? Pd.cmap : nullptr;
+    g.Sd = Sd + I.sdoff;
+    g.DD = DD + I.ddoff;
+    return g;
+}
+// unweighted column sum of squares (normalize_designmatrix) in the original order
+__device__ __forceinline__ double colsq_of(const PsrDev& Pd, const InstDev& I, const double* colsq, int nsplit,
+                                           bool cmp, const double* DCS, int j) {
+    if (!cmp) return colsq[(I.coff + j) * nsplit];
+    int a = Pd.cmap[j];
+    return a >= 0 ? colsq[(I.coff + a) * nsplit] : DCS[I.ddoff - a - 1];
+}
 
 struct KpGroup {  // instances sharing k_gram's tiles-per-wave T (launched together)
     int T, first, count, maxKp;
@@ -117,7 +170,8 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               const double* __restrict__ tables, const InstConst* __restrict__ ic,
                                               double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                               double* __restrict__ ftay, double* __restrict__ delay_out,
-                                              double* __restrict__ Mout, int* __restrict__ status) {
+                                              double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
+                                              int* __restrict__ status) {
     int b = blockIdx.x;
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
@@ -143,7 +197,9 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
     EvalOut o;
     double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
     const bool rowM = WANT_M && r < (unsigned)n;
-    eval_toa<BIN>(S, P, ic[ii], t, o, rowM ? Mb : nullptr, r, n, Pd.runs, Pd.nrun);
+    const bool cmp = WANT_M && compact && Pd.dsplit;
+    eval_toa<BIN>(S, P, ic[ii], t, o, rowM ? Mb : nullptr, r, n, Pd.runs, Pd.nrun, cmp);
+    if (rowM && cmp) dmxv[I.ooff + r] = o.dmc;
     if (o.status) atomicOr(status, 1 << o.status);
     ph_hi[I.roff + r] = o.phase.hi;
     ph_lo[I.roff + r] = o.phase.lo;
@@ -153,7 +209,7 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
         // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.
         dd ts = dd_mul_d(t.tdb, DAYSEC);
-        double* colp = Mb + (long)S.ncol * n;
+        double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
         for (int k = 0; k < S.nred; k++, colp += 2L * n) {
             dd x = dd_mul_d(ts, Pd.red_freq[k]);
             double fr = dd_to_d(dd_sub(x, dd_floor(x)));
@@ -223,12 +279,19 @@ __global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, 
 // the whole (upper-triangular tiles of the) Kp x Kp Gram for one N-split of one instance.
 // Also accumulates the unweighted column sums of squares (normalize_designmatrix).
 // ---------------------------------------------------------------------------------
-constexpr int GCH = 32;       // TOA rows per LDS chunk (multiple of 4)
+constexpr int GCH = 32;       // TOA rows per LDS chunk at the widest Gram (multiple of 4)
 constexpr int GMAXKP = 256;   // max padded columns
 constexpr int GWAVES = 16;
 constexpr int GTHREADS = GWAVES * 64;
 constexpr int GMAXT_ALL = 9;  // max upper 16x16 tiles per wave = ceil(136 / 16) at Kp = 256
-constexpr int GMAXQ = GCH * GMAXKP / GTHREADS;  // staged elements per thread per chunk (8)
+// rows per chunk for a tiles-per-wave T: narrow Grams (the compact fit layout) stage more
+// rows per chunk so each CU keeps enough bytes in flight; the staging registers per thread
+// (gram_q) stay <= 10 so the 1024-thread workgroup fits 128 VGPRs without spilling.
+__host__ __device__ constexpr int gram_ch(int T) { return T == 1 ? 128 : (T <= 3 ? 64 : 32); }
+__host__ __device__ constexpr int gram_maxkp(int T) {  // widest Kp whose upper tiles need T per wave
+    return T == 1 ? 80 : T == 2 ? 112 : T == 3 ? 144 : T == 4 ? 160 : T == 5 ? 192 : T == 6 ? 208 : T == 7 ? 224 : T == 8 ? 240 : 256;
+}
+__host__ __device__ constexpr int gram_q(int T) { return (gram_maxkp(T) * gram_ch(T) + GTHREADS - 1) / GTHREADS; }
 
 // ECORR epoch sums (one wave per epoch, lanes over columns): s_e = sum_{i in e} w_i [T|r]_i,
 // W_e = sum w_i, D_e = W_e + 1/phi_e.  The quantisation-matrix block of the GLS normal
@@ -274,25 +337,27 @@ __global__ __launch_bounds__(256) void k_ecorr(const PsrDev* __restrict__ psrs, 
 // k_gram: FP64 MFMA Gram of the whitened rows [T | r] / sigma, one 16-wave workgroup per
 // (N-split, instance).  The row-major list of upper 16x16 tiles is cut into 16 contiguous
 // runs of T or T-1 tiles (T = ceil(ntiles/16), a template parameter so the first T-1
-// tiles are unconditional and the operand reads can be hoisted).  Chunks of GCH rows are
+// tiles are unconditional and the operand reads can be hoisted).  Chunks of CH rows are
 // staged global -> registers (prefetched one chunk ahead, branch-free clamped loads) ->
-// LDS; every wave then issues GCH/4 x T v_mfma_f64_16x16x4f64 with operands from LDS.
+// LDS; every wave then issues CH/4 x T v_mfma_f64_16x16x4f64 with operands from LDS.
 // VIRT: the ECORR Schur rows s_e / sqrt(D_e) of k_ecorr, stored negated in the extra
 // partial slot, so the sum over partials is G - sum_e s_e s_e^T / D_e.
 // Also accumulates the unweighted column sums of squares (normalize_designmatrix).
-template <int T, bool VIRT>
+template <int T, int CH, bool VIRT>
 __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ M, const double* __restrict__ rtime,
                                                    const double* __restrict__ esum, const double* __restrict__ eD,
-                                                   int nsplit, double* __restrict__ Gpart, double* __restrict__ colsq) {
+                                                   int nsplit, int compact, double* __restrict__ Gpart,
+                                                   double* __restrict__ colsq) {
     extern __shared__ double lds[];
     const InstDev I = insts[blockIdx.y];
     const int split = VIRT ? nsplit : blockIdx.x;
     const PsrDev& Pd = psrs[I.psr];
-    const int n = I.n, K = I.K, Kp = I.Kp;
+    const bool cmp = compact && Pd.dsplit;
+    const int n = I.n, K = cmp ? Pd.Kd : I.K, Kp = cmp ? Pd.Kpd : I.Kp;
     const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
-    double* Ts = lds;                    // [GCH][stride] whitened rows
-    double* Sg = lds + GCH * stride;     // [GCH] sigma of the staged rows (colsq)
+    double* Ts = lds;                    // [CH][stride] whitened rows
+    double* Sg = lds + CH * stride;      // [CH] sigma of the staged rows (colsq)
     const double* Mi = M + I.moff;
     const double* ri = rtime + I.ooff;
     const double* Ei = esum + I.eoff;
@@ -303,10 +368,11 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
         i1 = Pd.nep;
     } else {
         long per = (n + nsplit - 1) / nsplit;
-        per = (per + GCH - 1) / GCH * GCH;
+        per = (per + 3) / 4 * 4;
         i0 = split * per;
         i1 = i0 + per;
         if (i1 > n) i1 = n;
+        if (i0 > n) i0 = n;
     }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -331,13 +397,18 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
     double4_t acc[T];
 #pragma unroll
     for (int t = 0; t < T; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    double csq = 0.0;  // thread tid < K owns column tid
-    // staging: thread -> (row ii = tid % GCH, columns c_base + 32 q)
-    const int ii = tid % GCH, c_base = tid / GCH;
-    const int nq = (Kp + (GTHREADS / GCH) - 1) / (GTHREADS / GCH);  // uniform
+    // column sums of squares: every thread takes column tid % Kp of rows tid / Kp (mod CG2)
+    // of each chunk; the CG2 partials are summed through LDS at the end of the split
+    const int ccol = tid % Kp, cgrp = tid / Kp, CG2 = GTHREADS / Kp;
+    double csq = 0.0;
+    // staging: thread -> (row ii = tid % CH, columns c_base + (1024/CH) q)
+    constexpr int CG = GTHREADS / CH;
+    const int ii = tid % CH, c_base = tid / CH;
+    const int nq = (Kp + CG - 1) / CG;  // uniform
     // the prefetch only issues loads (raw values into registers, clamped addresses, no
     // arithmetic on the results), so the waits land at the LDS store of the next chunk
-    double st[GMAXQ];
+    constexpr int QN = gram_q(T);
+    double st[QN];
     double sg_next = 1.0, w_next = 0.0, r_next = 0.0;
     bool ok_next = false;
     auto load = [&](long c0) {
@@ -352,42 +423,42 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
             r_next = ri[row];
         }
 #pragma unroll
-        for (int q = 0; q < GMAXQ; q++) {
+        for (int q = 0; q < QN; q++) {
             if (q < nq) {
-                const int c = c_base + (GTHREADS / GCH) * q;
+                const int c = c_base + CG * q;
                 if (VIRT) st[q] = Ei[row * Kp + (c < Kp ? c : Kp - 1)];
                 else st[q] = Mi[(long)(c < K ? c : K - 1) * n + row];
             }
         }
     };
     if (i0 < i1) load(i0);
-    for (long c0 = i0; c0 < i1; c0 += GCH) {
+    for (long c0 = i0; c0 < i1; c0 += CH) {
         __syncthreads();  // previous chunk's MFMAs are done with the LDS tile
         {
             double iw = VIRT ? 1.0 / sqrt(w_next) : w_next;
             iw = ok_next ? iw : 0.0;
 #pragma unroll
-            for (int q = 0; q < GMAXQ; q++) {
-                const int c = c_base + (GTHREADS / GCH) * q;
+            for (int q = 0; q < QN; q++) {
+                const int c = c_base + CG * q;
                 if (q < nq && c < Kp) {
                     double v = st[q];
                     if (!VIRT) v = c < K ? v : (c == K ? r_next : 0.0);
                     Ts[ii * stride + c] = v * iw;
                 }
             }
+            if (!VIRT && c_base == 0) Sg[ii] = sg_next;
         }
-        if (!VIRT && c_base == 0) Sg[ii] = sg_next;
         __syncthreads();
-        if (c0 + GCH < i1) load(c0 + GCH);  // prefetch next chunk (overlaps the MFMAs)
-        if (!VIRT && tid < K) {
-            const int nr = (i1 - c0 < GCH) ? (int)(i1 - c0) : GCH;
-            for (int r = 0; r < nr; r++) {
-                double v = Ts[r * stride + tid] * Sg[r];
-                csq += v * v;
+        if (c0 + CH < i1) load(c0 + CH);  // prefetch next chunk (overlaps the MFMAs)
+        if (!VIRT && cgrp < CG2) {
+            const int nr = (i1 - c0 < CH) ? (int)(i1 - c0) : CH;
+            for (int r = cgrp; r < nr; r += CG2) {
+                const double u = Ts[r * stride + ccol] * Sg[r];
+                csq += u * u;
             }
         }
 #pragma unroll
-        for (int kk = 0; kk < GCH / 4; kk++) {
+        for (int kk = 0; kk < CH / 4; kk++) {
             const double* Tr = Ts + (kk * 4 + (lane >> 4)) * stride + (lane & 15);
             double a[T], b[T];
 #pragma unroll
@@ -414,16 +485,159 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
             }
         }
     }
-    if (!VIRT && tid < K) colsq[(I.coff + tid) * nsplit + split] = csq;
+    if (!VIRT) {
+        __syncthreads();  // done with the LDS tile: reuse it for the colsq partials
+        if (cgrp < CG2) lds[cgrp * Kp + ccol] = csq;
+        __syncthreads();
+        if (tid < K) {
+            double v = 0.0;
+            for (int g = 0; g < CG2; g++) v += lds[g * Kp + tid];
+            colsq[(I.coff + tid) * nsplit + split] = v;
+        }
+    }
 }
 
 
+// k_dmx: Gram rows of the DMX columns in the compact fit layout when a bin's TOAs are not
+// one contiguous row range (otherwise k_gram accumulates them).  A DMX column is x_i on
+// the TOAs of its bin (d_dm_d_DMX, dispersion_model.py:684, times DMconst/f^2 and the
+// phase chain) and 0 elsewhere, so its Gram row is a sum over the bin's TOAs:
+//   Sd[a][c] = sum_{i in bin a} w_i x_i [T|r]_ic (c over the compact columns + residual),
+//   DD[a] = sum w_i x_i^2 (bins do not overlap in this layout), DCS[a] = sum x_i^2.
+// One workgroup per (bin, instance); a wave per column, lanes over the bin's TOAs.
+__global__ __launch_bounds__(256) void k_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                             const double* __restrict__ M, const double* __restrict__ rtime,
+                                             const double* __restrict__ dmxv, double* __restrict__ Sd,
+                                             double* __restrict__ DD, double* __restrict__ DCS) {
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    const int a = blockIdx.x;
+    if (!Pd.dsplit || Pd.dcontig || a >= Pd.ndc) return;  // dcontig: fused into k_gram
+    const int n = I.n, Kd = Pd.Kd, Kpd = Pd.Kpd;
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + I.ooff;
+    const double* xv = dmxv + I.ooff;
+    const int k0 = Pd.dptr[a], k1 = Pd.dptr[a + 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* out = Sd + I.sdoff + (long)a * Kpd;
+    for (int c = wave; c <= Kd; c += 4) {
+        const double* col = c < Kd ? Mi + (long)c * n : ri;
+        double acc = 0.0;
+        for (int k = k0 + lane; k < k1; k += 64) {
+            const int i = Pd.didx[k];
+            const double is = Pd.isig[i];
+            acc += is * is * xv[i] * col[i];
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) out[c] = acc;
+    }
+    if (wave == 0) {
+        double d = 0.0, q = 0.0;
+        for (int k = k0 + lane; k < k1; k += 64) {
+            const int i = Pd.didx[k];
+            const double x = xv[i], is = Pd.isig[i];
+            d += is * is * x * x;
+            q += x * x;
+        }
+        d = wave_sum(d);
+        q = wave_sum(q);
+        if (lane == 0) {
+            DD[I.ddoff + a] = d;
+            DCS[I.ddoff + a] = q;
+        }
+    }
+}
+
+// k_dmx_rows: the same bin sums when every bin is one contiguous row range (time-sorted
+// TOAs).  One workgroup per (bin, instance): 64-row slices of [T|r] are staged through LDS
+// with coalesced column reads (a wave reads 64 consecutive rows of one column), then
+// thread c sums column c down the slice; thread Kd+1 forms DD/DCS.
+constexpr int DMX_RS = 64;
+__global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                  const double* __restrict__ M, const double* __restrict__ rtime,
+                                                  const double* __restrict__ dmxv, double* __restrict__ Sd,
+                                                  double* __restrict__ DD, double* __restrict__ DCS) {
+    extern __shared__ double lds[];
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    const int a = blockIdx.x;
+    if (!Pd.dsplit || !Pd.dcontig || a >= Pd.ndc) return;
+    const int n = I.n, Kd = Pd.Kd, Kpd = Pd.Kpd;
+    const int W = Kd + 2;               // columns + residual + the DD/DCS slot
+    const int str = W | 1;              // odd stride
+    double* Ts = lds;                   // [DMX_RS][str]
+    double* wx = lds + DMX_RS * str;    // [DMX_RS] w_i x_i
+    double* xx = wx + DMX_RS;           // [DMX_RS] x_i
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + I.ooff;
+    const double* xv = dmxv + I.ooff;
+    const int cnt = Pd.dptr[a + 1] - Pd.dptr[a];
+    const int lo = cnt > 0 ? Pd.didx[Pd.dptr[a]] : 0, hi = lo + cnt;
+    const int t = threadIdx.x, row = t & 63, g = t >> 6;
+    // summing threads: column sc = t % W of rows t / W (mod SG)
+    const int sc = t % W, sg = t / W, SG = (256 / W < DMX_RS) ? 256 / W : DMX_RS;
+    double acc = 0.0, qacc = 0.0;
+    for (int r0 = lo; r0 < hi; r0 += DMX_RS) {
+        const int nr = hi - r0 < DMX_RS ? hi - r0 : DMX_RS;
+        const int i = r0 + (row < nr ? row : nr - 1);
+        for (int cb = g; cb <= Kd; cb += 32) {  // 8 independent loads in flight per thread
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int c = cb + 4 * u;
+                v[u] = c < Kd ? Mi[(long)c * n + i] : ri[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int c = cb + 4 * u;
+                if (c <= Kd && row < nr) Ts[row * str + c] = v[u];
+            }
+        }
+        if (g == 0 && row < nr) {
+            const double is = Pd.isig[i], x = xv[i];
+            wx[row] = is * is * x;
+            xx[row] = x;
+        }
+        __syncthreads();
+        if (sg < SG) {
+            for (int r = sg; r < nr; r += SG) {
+                if (sc <= Kd) acc += Ts[r * str + sc] * wx[r];
+                else {
+                    acc += wx[r] * xx[r];
+                    qacc += xx[r] * xx[r];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // sum the SG row-group partials
+    if (sg < SG) {
+        Ts[sg * str + sc] = acc;
+        if (sc == Kd + 1) wx[sg] = qacc;
+    }
+    __syncthreads();
+    if (t < W) {
+        double v = 0.0;
+        for (int q = 0; q < SG; q++) v += Ts[q * str + t];
+        if (t <= Kd) Sd[I.sdoff + (long)a * Kpd + t] = v;
+        else {
+            double qv = 0.0;
+            for (int q = 0; q < SG; q++) qv += wx[q];
+            DD[I.ddoff + a] = v;
+            DCS[I.ddoff + a] = qv;
+        }
+    }
+}
+
 // Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
 // triangle only, in a fixed order (deterministic), and the column sums of squares.
-__global__ __launch_bounds__(256) void k_greduce(const InstDev* __restrict__ insts, int nsplit, int nparts,
-                                                 double* __restrict__ Gpart, double* __restrict__ colsq) {
+__global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                 int nsplit, int nparts, int compact, double* __restrict__ Gpart,
+                                                 double* __restrict__ colsq) {
     const InstDev I = insts[blockIdx.y];
-    const int Kp = I.Kp;
+    const PsrDev& Pd = psrs[I.psr];
+    const bool cmp = compact && Pd.dsplit;
+    const int Kp = cmp ? Pd.Kpd : I.Kp, Kc = cmp ? Pd.Kd : I.K;
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long KK = (long)Kp * Kp;
     if (e < KK) {
@@ -435,7 +649,7 @@ __global__ __launch_bounds__(256) void k_greduce(const InstDev* __restrict__ ins
             G[e] = sacc;
         }
     }
-    if (e < I.K) {
+    if (e < Kc) {
         double* cs = colsq + (I.coff + e) * nsplit;
         double v = cs[0];
         for (int q = 1; q < nsplit; q++) v += cs[q];
@@ -521,6 +735,8 @@ __device__ __forceinline__ double linv(const double* A, const double* D, int i, 
 __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ tables, const double* __restrict__ Gpart,
                                                    const double* __restrict__ colsq, int nsplit, int nparts, int mode,
+                                                   int compact, const double* __restrict__ Sd,
+                                                   const double* __restrict__ DD, const double* __restrict__ DCS,
                                                    double* __restrict__ work, double* __restrict__ dpars,
                                                    double* __restrict__ errs, double* __restrict__ cov,
                                                    double* __restrict__ chi2lin, double* __restrict__ sigL,
@@ -540,18 +756,14 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
     double* bv = tmp + K;                   // K
     double* yv = bv + K;                    // K
     double* nrm = yv + K;                   // K
-    const double* Gp = Gpart + I.goff;
-    auto G = [&](int i, int j) {  // symmetric accessor (partials summed into slot 0 by k_greduce)
-        if (i > j) { int t = i; i = j; j = t; }
-        return Gp[(long)i * Kp + j];
-    };
+    const bool cmp = compact && Pd.dsplit;
+    const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);  // (partials summed into slot 0 by k_greduce)
     // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
     for (int j = threadIdx.x; j < K; j += blockDim.x) {
         double v;
         if (mode == 0) v = G(j, j);
         else {
-            v = 0.0;
-            v = colsq[(I.coff + j) * nsplit];
+            v = colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j);
         }
         v = sqrt(v);
         nrm[j] = (v == 0.0) ? 1.0 : v;
@@ -805,6 +1017,8 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
                                                        const double* __restrict__ colsq, int nsplit, int mode,
+                                                       int compact, const double* __restrict__ Sd,
+                                                       const double* __restrict__ DD, const double* __restrict__ DCS,
                                                        double* __restrict__ dpars, double* __restrict__ errs,
                                                        double* __restrict__ cov, double* __restrict__ chi2lin,
                                                        double* __restrict__ sigL, int* __restrict__ status) {
@@ -822,15 +1036,12 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     double* A = lds;
     double* bv = A + nblk * 256;
     double* yv = bv + nb * 16;
-    const double* Gp = Gpart + I.goff;
-    auto G = [&](int i, int j) {
-        if (i > j) { int t = i; i = j; j = t; }
-        return Gp[(long)i * Kp + j];
-    };
+    const bool cmp = compact && Pd.dsplit;
+    const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);
     // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
     auto nrmf = [&](int j) {
         if (j >= K) return 1.0;
-        double v = sqrt(mode == 0 ? G(j, j) : colsq[(I.coff + j) * nsplit]);
+        double v = sqrt(mode == 0 ? G(j, j) : colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j));
         return v == 0.0 ? 1.0 : v;
     };
     const int tid = threadIdx.x, lane = tid & 63;
@@ -961,7 +1172,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
 //             substitution with Sigma's Cholesky factor, chi2
 __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               const double* __restrict__ M, const double* __restrict__ rtime,
-                                              int nsplit, int stride, double* __restrict__ wpart) {
+                                              int nsplit, int stride, int compact, double* __restrict__ wpart) {
     const int inst = blockIdx.y, split = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -977,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, c
     for (int j = wave; j < R + 2; j += 4) {
         double acc = 0.0;
         if (j < R) {
-            const double* col = Mi + (long)(S.ncol + j) * n;
+            const double* col = Mi + (long)((compact && Pd.dsplit ? Pd.red0c : S.ncol) + j) * n;
             for (long i = i0 + lane; i < i1; i += 64) {
                 double sg = Pd.sigma[i];
                 acc += col[i] * ri[i] / (sg * sg);
@@ -1082,6 +1293,7 @@ __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restri
 struct PsrHost {
     PsrDev dev;
     pint_spec_t spec;
+    std::vector<int> dlo, dhi;  // row range of each DMX column's bin (compact layout)
     std::vector<void*> bufs;
     int n, K;
 };
@@ -1100,8 +1312,9 @@ struct pint_ctx {
     int ninst = 0;
     std::vector<InstDev> inst;
     InstDev* d_inst = nullptr;
-    InstDev* d_inst_sorted = nullptr;   // instances grouped by k_gram T
-    std::vector<KpGroup> kp_groups;
+    InstDev* d_inst_sorted = nullptr;   // instances grouped by k_gram T (full layout)
+    InstDev* d_inst_sorted_c = nullptr; // ... compact layout
+    std::vector<KpGroup> kp_groups, kp_groups_c;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
@@ -1116,6 +1329,9 @@ struct pint_ctx {
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
     double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
     InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
+    double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
+    int max_ndc = 0;
+    int m_compact = 0;  // layout of the design matrix written by the last pint_eval(want_M)
     size_t wpart_cap = 0;
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
@@ -1189,7 +1405,9 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
-                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic};
+                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
+                   (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
+                   (void**)&ctx->d_inst_sorted_c};
     for (auto p : ps) dfree(*p);
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
@@ -1257,15 +1475,67 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, red_freq, (size_t)spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
     {
+        // compact fit layout: DMX columns out of M when there are enough of them and no TOA
+        // lies in two free bins (bins do not overlap), ECORR checked in pint_set_ecorr
+        const int ncol = spec->ncol;
+        std::vector<int> colOfBin(spec->ndmx > 0 ? spec->ndmx : 1, -1);
+        int ndc = 0;
+        for (int c = 0; c < ncol; c++)
+            if (spec->col_kind[c] == PINT_COL_DMX) {
+                const int bin = spec->col_index[c];
+                if (bin >= 0 && bin < spec->ndmx) colOfBin[bin] = ndc;
+                ndc++;
+            }
+        bool ok = ndc >= 8;
+        std::vector<std::vector<int>> lists(ndc);
+        for (int i = 0; ok && i < n; i++) {
+            const int a = t->dmx_a[i] >= 0 && t->dmx_a[i] < spec->ndmx ? colOfBin[t->dmx_a[i]] : -1;
+            const int b = t->dmx_b[i] >= 0 && t->dmx_b[i] < spec->ndmx ? colOfBin[t->dmx_b[i]] : -1;
+            if (a >= 0 && b >= 0) ok = false;
+            else if (a >= 0) lists[a].push_back(i);
+            else if (b >= 0) lists[b].push_back(i);
+        }
+        std::vector<int32_t> cmap(K + 1), dptr(ndc + 1, 0), didx;
+        int kd = 0, ad = 0;
+        for (int c = 0; c < ncol; c++) cmap[c] = (spec->col_kind[c] == PINT_COL_DMX) ? -(++ad) : kd++;
+        const int red0c = kd;
+        for (int c = ncol; c < K; c++) cmap[c] = kd++;
+        cmap[K] = kd;  // residual column
+        for (int a = 0; a < ndc; a++) {
+            dptr[a + 1] = dptr[a] + (int)lists[a].size();
+            didx.insert(didx.end(), lists[a].begin(), lists[a].end());
+        }
+        std::vector<int32_t> drow(n, -1);
+        bool contig = true;
+        for (int a = 0; a < ndc; a++) {
+            for (size_t k = 0; k < lists[a].size(); k++) {
+                drow[lists[a][k]] = a;
+                if (k > 0 && lists[a][k] != lists[a][k - 1] + 1) contig = false;
+            }
+        }
+        rc |= upload(ctx, ph, drow.data(), drow.size(), d.drow);
+        ph.dlo.assign(ndc, 0);
+        ph.dhi.assign(ndc, 0);
+        for (int a = 0; a < ndc; a++)
+            if (!lists[a].empty()) { ph.dlo[a] = lists[a].front(); ph.dhi[a] = lists[a].back() + 1; }
+        d.dcontig = (ok && contig) ? 1 : 0;
+        d.dsplit = ok ? 1 : 0;
+        d.ndc = ndc;
+        d.Kd = kd;
+        d.Kpd = (kd + 1 + 15) / 16 * 16;
+        d.red0c = red0c;
+        rc |= upload(ctx, ph, cmap.data(), cmap.size(), d.cmap);
+        rc |= upload(ctx, ph, dptr.data(), dptr.size(), d.dptr);
+        rc |= upload(ctx, ph, didx.data(), didx.size(), d.didx);
         // design-matrix column runs: same kind, consecutive indices (BIN: same kind only)
         std::vector<ColRun> runs;
-        for (int c = 0; c < spec->ncol; c++) {
+        for (int c = 0; c < ncol; c++) {
             const int k = spec->col_kind[c], ix = spec->col_index[c];
             if (!runs.empty()) {
                 ColRun& R = runs.back();
                 if (R.kind == k && (k == PINT_COL_BIN || R.idx0 + R.cnt == ix)) { R.cnt++; continue; }
             }
-            runs.push_back(ColRun{k, c, 1, ix});
+            runs.push_back(ColRun{k, c, 1, ix, k == PINT_COL_DMX ? -1 : cmap[c], {0, 0, 0}});
         }
         rc |= upload(ctx, ph, runs.data(), runs.size(), d.runs);
         d.nrun = (int)runs.size();
@@ -1280,6 +1550,16 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     ctx->psrs.push_back(ph);
     if (refresh_psrs(ctx)) return -PINT_E_HIP;
     return (int)ctx->psrs.size() - 1;
+}
+
+int pint_fit_layout(pint_ctx* ctx, int psr, int32_t* out4) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !out4) return PINT_E_INVALID;
+    const PsrDev& d = ctx->psrs[psr].dev;
+    out4[0] = d.dsplit;
+    out4[1] = d.dsplit ? d.Kd : d.K;
+    out4[2] = d.dsplit ? d.ndc : 0;
+    out4[3] = d.dsplit ? d.Kpd : d.Kp;
+    return PINT_OK;
 }
 
 int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const int32_t* ep_idx,
@@ -1301,6 +1581,7 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
     rc |= upload(ctx, ph, ep_phi, (size_t)nep, ph.dev.ep_phi);
     if (rc) return PINT_E_HIP;
     ph.dev.nep = nep;
+    ph.dev.dsplit = 0;  // the ECORR Schur rows span every column: keep the full layout
     return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
 }
 
@@ -1310,7 +1591,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     free_instances(ctx);
     ctx->inst.resize(ninst);
     long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0, eoff = 0, epoff = 0;
-    int max_nep = 0;
+    long sdoff = 0, ddoff = 0;
+    int max_nep = 0, max_ndc = 0;
     std::vector<int> bti[3], btr[3];
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
@@ -1362,6 +1644,13 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.eoff = eoff;
         I.epoff = epoff;
         I.ooff = out;
+        I.sdoff = sdoff;
+        I.ddoff = ddoff;
+        if (ph.dev.dsplit) {
+            sdoff += (long)ph.dev.ndc * ph.dev.Kpd;
+            ddoff += ph.dev.ndc;
+            if (ph.dev.ndc > max_ndc) max_ndc = ph.dev.ndc;
+        }
         I.self = k;
         eoff += (long)ph.dev.nep * I.Kp;
         epoff += ph.dev.nep;
@@ -1394,6 +1683,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->tot_e = eoff;
     ctx->tot_ep = epoff;
     ctx->max_nep = max_nep;
+    ctx->max_ndc = max_ndc;
     std::vector<int> bi, br;
     for (int t = 0; t < 3; t++) {
         ctx->blk_off[t] = (int)bi.size();
@@ -1404,22 +1694,26 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->nblk = (int)bi.size();
     HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
-    {
+    for (int lay = 0; lay < 2; lay++) {  // k_gram launch groups: full and compact layouts
         std::vector<InstDev> sorted;
-        ctx->kp_groups.clear();
+        std::vector<KpGroup>& groups = lay ? ctx->kp_groups_c : ctx->kp_groups;
+        groups.clear();
         for (int T = 1; T <= GMAXT_ALL; T++) {
             KpGroup g{T, (int)sorted.size(), 0, 16};
             for (auto& I : ctx->inst) {
-                int nt = I.Kp / 16, tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
+                const PsrDev& pd = ctx->psrs[I.psr].dev;
+                const int kp = (lay && pd.dsplit) ? pd.Kpd : I.Kp;
+                int nt = kp / 16, tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
                 if (tT != T) continue;
                 sorted.push_back(I);
                 g.count++;
-                if (I.Kp > g.maxKp) g.maxKp = I.Kp;
+                if (kp > g.maxKp) g.maxKp = kp;
             }
-            if (g.count) ctx->kp_groups.push_back(g);
+            if (g.count) groups.push_back(g);
         }
-        HIPCHK(hipMalloc(&ctx->d_inst_sorted, sizeof(InstDev) * ninst));
-        HIPCHK(hipMemcpy(ctx->d_inst_sorted, sorted.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+        InstDev*& dst = lay ? ctx->d_inst_sorted_c : ctx->d_inst_sorted;
+        HIPCHK(hipMalloc(&dst, sizeof(InstDev) * ninst));
+        HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMalloc(&ctx->d_blk_inst, sizeof(int) * bi.size()));
     HIPCHK(hipMalloc(&ctx->d_blk_row0, sizeof(int) * br.size()));
@@ -1450,6 +1744,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(hipMalloc(&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(hipMalloc(&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(hipMalloc(&ctx->d_ic, sizeof(InstConst) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_dmxv, sizeof(double) * (out > 0 ? out : 1)));
+    HIPCHK(hipMalloc(&ctx->d_Sd, sizeof(double) * (sdoff > 0 ? sdoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_DD, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
+    HIPCHK(hipMalloc(&ctx->d_DCS, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
     HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * (cvoff > 0 ? cvoff : 1), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -1497,7 +1795,9 @@ static int check_status(pint_ctx* ctx) {
 int pint_eval(pint_ctx* ctx, int want_M) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (want_M < 0 || want_M > 2) return PINT_E_INVALID;
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
+    if (want_M) ctx->m_compact = (want_M == 2) ? 1 : 0;
     record(ctx, want_M ? 2 : 0);
     hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->ninst, ctx->d_tables, ctx->d_ic);
@@ -1509,7 +1809,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         const int* br = ctx->d_blk_row0 + ctx->blk_off[t];
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
-                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, ctx->d_status)
+                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, ctx->d_status)
         if (want_M) {
             if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
         } else {
@@ -1566,27 +1867,47 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
         HIPCHK(hipGetLastError());
     }
+    const int cmp = ctx->m_compact;
+    if (cmp && ctx->max_ndc > 0) {
+        int maxKd = 0;
+        bool any_gather = false;
+        for (auto& I : ctx->inst) {
+            const PsrDev& pd = ctx->psrs[I.psr].dev;
+            if (pd.dsplit) maxKd = std::max(maxKd, pd.Kd);
+            if (pd.dsplit && !pd.dcontig) any_gather = true;
+        }
+        size_t lds = sizeof(double) * (DMX_RS * ((maxKd + 2) | 1) + 2 * DMX_RS);
+        hipLaunchKernelGGL(k_dmx_rows, dim3(ctx->max_ndc, ctx->ninst), dim3(256), lds, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+        HIPCHK(hipGetLastError());
+        if (any_gather) {
+            hipLaunchKernelGGL(k_dmx, dim3(ctx->max_ndc, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+            HIPCHK(hipGetLastError());
+        }
+    }
     {
-        // every instance of the batch uses the tile split of the widest one (maxKp); narrower
-        // instances have fewer tiles: T must cover the widest, and per-instance tile counts
-        // are recomputed in-kernel from their own Kp, so a launch is per distinct Kp group.
-        for (int g = 0; g < (int)ctx->kp_groups.size(); g++) {
-            const KpGroup& kg = ctx->kp_groups[g];
+        // instances are launched in groups of equal tiles-per-wave T (template parameter);
+        // per-instance tile counts are recomputed in-kernel from their own Kp.
+        const std::vector<KpGroup>& groups = cmp ? ctx->kp_groups_c : ctx->kp_groups;
+        for (int g = 0; g < (int)groups.size(); g++) {
+            const KpGroup& kg = groups[g];
             const int T = kg.T;
             const int sstride = kg.maxKp + 16;
-            size_t lds = sizeof(double) * (GCH * sstride + GCH);
-            const InstDev* di = ctx->d_inst_sorted + kg.first;
+            const int CH = gram_ch(T);
+            size_t lds = sizeof(double) * (CH * sstride + CH);
+            const InstDev* di = (cmp ? ctx->d_inst_sorted_c : ctx->d_inst_sorted) + kg.first;
             for (int virt = 0; virt < 2; virt++) {
                 if (virt && !(mode == 1 && ctx->max_nep > 0)) break;
                 dim3 grid(virt ? 1 : ctx->nsplit, kg.count);
 #define PINT_GRAM_CASE(TT)                                                                                         \
                 case TT:                                                                                           \
-                    if (virt) hipLaunchKernelGGL((k_gram<TT, true>), grid, dim3(GTHREADS), lds, ctx->stream,       \
-                                                 ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD,    \
-                                                 ctx->nsplit, ctx->d_G, ctx->d_colsq);                             \
-                    else hipLaunchKernelGGL((k_gram<TT, false>), grid, dim3(GTHREADS), lds, ctx->stream,          \
-                                            ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD,          \
-                                            ctx->nsplit, ctx->d_G, ctx->d_colsq);                                  \
+                    if (virt) hipLaunchKernelGGL((k_gram<TT, gram_ch(TT), true>), grid, dim3(GTHREADS), lds,      \
+                                                 ctx->stream, ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum,  \
+                                                 ctx->d_eD, ctx->nsplit, cmp, ctx->d_G, ctx->d_colsq);            \
+                    else hipLaunchKernelGGL((k_gram<TT, gram_ch(TT), false>), grid, dim3(GTHREADS), lds,         \
+                                            ctx->stream, ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum,       \
+                                            ctx->d_eD, ctx->nsplit, cmp, ctx->d_G, ctx->d_colsq);                 \
                     break;
                 switch (T) {
                     PINT_GRAM_CASE(1) PINT_GRAM_CASE(2) PINT_GRAM_CASE(3) PINT_GRAM_CASE(4) PINT_GRAM_CASE(5)
@@ -1602,7 +1923,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         int maxKp = 16;
         for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
         hipLaunchKernelGGL(k_greduce, dim3((maxKp * maxKp + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream,
-                           ctx->d_inst, ctx->nsplit, nparts, ctx->d_G, ctx->d_colsq);
+                           ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, ctx->d_G, ctx->d_colsq);
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
@@ -1622,18 +1943,21 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         size_t lds_b = sizeof(double) * ((size_t)nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx);
         if (nbx <= 5)
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
+                               ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
                                ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
         else
             hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                               ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
+                               ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
                                ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
     } else {
         int K = ctx->maxK;
         size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
         if (lds_s > 160 * 1024) { ctx->err = "normal matrix too large for LDS solve"; return PINT_E_INVALID; }
         hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, ctx->d_work, ctx->d_dpars,
+                           ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, cmp, ctx->d_Sd, ctx->d_DD,
+                           ctx->d_DCS, ctx->d_work, ctx->d_dpars,
                            ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
     }
     HIPCHK(hipGetLastError());
@@ -1697,7 +2021,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     }
     record(ctx, 10);
     hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
-                       ctx->d_rt, nsw, stride, ctx->d_wpart);
+                       ctx->d_rt, nsw, stride, ctx->m_compact, ctx->d_wpart);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,

@@ -391,8 +391,12 @@ class Session:
         self.ntab = len(tabs)
 
     # -- launches -------------------------------------------------------------------
+    FIT = 2  # want_M for a fit step: compact layout (DMX columns as bin sums)
+
     def eval(self, want_M=False):
-        self._check(self.L.pint_eval(self.ctx, 1 if want_M else 0))
+        """want_M: False (phases/residuals only), True (full design matrix, as
+        TimingModel.designmatrix returns it) or Session.FIT (fit layout for fit_step)."""
+        self._check(self.L.pint_eval(self.ctx, 2 if want_M == self.FIT else (1 if want_M else 0)))
 
     def fit_step(self, mode):
         self._check(self.L.pint_fit_step(self.ctx, int(mode)))
@@ -439,6 +443,12 @@ class Session:
         pinned buffers that are complete after check()."""
         self._check(self.L.pint_set_lazy(self.ctx, 1 if lazy else 0))
         self.lazy = bool(lazy)
+
+    def fit_layout(self, lay):
+        """(compact, Gram columns, sparse DMX columns, padded Gram width) of a pulsar."""
+        out = np.zeros(4, dtype=np.int32)
+        self._check(self.L.pint_fit_layout(self.ctx, lay.psr_id, L.ptr(out, C.c_int32)))
+        return tuple(int(x) for x in out)
 
     def set_blocked_solve(self, on=True):
         self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))

@@ -107,7 +107,7 @@ class BatchFit:
         return c2, tr
 
     def _step(self):
-        self.s.eval(want_M=True)
+        self.s.eval(want_M=Session.FIT)
         self.s.fit_step(1 if self.gls else 0)
 
     def _finish(self, results):

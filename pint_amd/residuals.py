@@ -37,7 +37,7 @@ class Residuals:
             self.track_mode = lay.track_mode
             s.set_instances([(lay, pack_table(lay))])
             corr = self.model.has_correlated_errors and (lay.nred > 0 or lay.nep > 0)
-            s.eval(want_M=corr)
+            s.eval(want_M=Session.FIT if corr else False)
             tr, pr, c2 = s.read_resids()
             self.time_resids = tr[0]
             self.phase_resids = pr[0]

@@ -319,3 +319,30 @@ def test_blocked_solve_matches_column_solve(name):
     assert abs(l1 - l2) <= (1e-7 if name in ("b1855", "j0740") else 1e-9) * abs(l2) + 1e-6
     if gls:
         assert abs(g1 / g2 - 1) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["pta_dd", "pta_ell1", "pta_iso"])
+def test_compact_dmx_layout_matches_full(name):
+    """The fit layout keeps the DMX columns out of M and the dense Gram (their Gram rows are
+    bin sums, k_dmx).  It is the same normal matrix: step, errors, covariance and the
+    Woodbury chi2 agree with the full-layout fit to rounding."""
+    from pint_amd.engine import Session
+    from pint_amd.fitter import BatchFit
+    model, toas, z, meta = load(name)
+    out = []
+    for want in (Session.FIT, True):
+        bf = BatchFit([(copy.deepcopy(model), toas)], mode="gls")
+        if want == Session.FIT:
+            assert bf.s.fit_layout(bf.layouts[0])[0] == 1  # the PTA fixtures have 20 DMX bins
+        bf.s.eval(want_M=want)
+        bf.s.fit_step(1)
+        dp, er, cov, cl = bf.s.read_step()
+        out.append((dp[0], er[0], cov[0], cl[0], bf.s.chi2_gls()[0]))
+        bf.close()
+    (d1, e1, c1, l1, g1), (d2, e2, c2_, l2, g2) = out
+    n = len(e1) - 1
+    assert np.max(np.abs((d1[:n] - d2[:n]) / e2[:n])) < 1e-8
+    assert np.max(np.abs(e1[:n] / e2[:n] - 1)) < 1e-9
+    sc = np.sqrt(np.outer(np.diag(c2_), np.diag(c2_)))
+    assert np.max(np.abs(c1 - c2_) / sc) < 1e-9
+    assert abs(g1 / g2 - 1) < 1e-10
