@@ -222,13 +222,14 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
 }
 
 // ---------------------------------------------------------------------------------
-// k_resid: one workgroup (256) per instance — residuals.py:314-425, :483-538, :638-667
+// k_resid: one 1024-thread workgroup per instance — residuals.py:314-425, :483-538, :638-667
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                               const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
-                                               const double* __restrict__ ftay, double* __restrict__ rtime,
-                                               double* __restrict__ rphase, double* __restrict__ chi2) {
-    __shared__ double sh[8];
+constexpr int RES_T = 1024;
+__global__ __launch_bounds__(RES_T) void k_resid(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                 const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
+                                                 const double* __restrict__ ftay, double* __restrict__ rtime,
+                                                 double* __restrict__ rphase, double* __restrict__ chi2) {
+    __shared__ double sh[RES_T / 64];
     const InstDev I = insts[blockIdx.x];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, 
         d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
     }
     double sw = 0.0, swx = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int i = threadIdx.x; i < n; i += RES_T) {
         dd d = dd_add_d(dd_sub(dd_make(ph_hi[ro + i], ph_lo[ro + i]), tz), Pd.dpn[i]);
         double full;
         if (S.track_pn) {
@@ -251,26 +252,26 @@ __global__ __launch_bounds__(256) void k_resid(const PsrDev* __restrict__ psrs, 
             full = dd_to_d(dd_sub(x, dd_round_half_up(x)));
         }
         rphase[oo + i] = full;
-        double w = S.weighted_mean ? 1.0 / (Pd.sigma[i] * Pd.sigma[i]) : 1.0;
+        double w = S.weighted_mean ? Pd.isig[i] * Pd.isig[i] : 1.0;
         sw += w;
         swx += w * full;
     }
     double mean = 0.0;
     if (S.subtract_mean) {
-        double a = block_sum<4>(swx, sh);
-        double bsum = block_sum<4>(sw, sh);
+        double a = block_sum<RES_T / 64>(swx, sh);
+        double bsum = block_sum<RES_T / 64>(sw, sh);
         mean = a / bsum;
     }
     double c2 = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int i = threadIdx.x; i < n; i += RES_T) {
         double p = rphase[oo + i] - mean;
         rphase[oo + i] = p;
         double rt = p / ftay[ro + i];
         rtime[oo + i] = rt;
-        double z = rt / Pd.sigma[i];
+        double z = rt * Pd.isig[i];
         c2 += z * z;
     }
-    c2 = block_sum<4>(c2, sh);
+    c2 = block_sum<RES_T / 64>(c2, sh);
     if (threadIdx.x == 0) chi2[blockIdx.x] = c2;
 }
 
@@ -1170,6 +1171,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
 //             1^T W r; one wave per column (coalesced column reads, shuffle reduction)
 //   k_wsolve  one workgroup per instance: split sums, ECORR correction, forward
 //             substitution with Sigma's Cholesky factor, chi2
+// one wave per column (coalesced column reads, 4 row-slices in flight per lane), shuffle
+// reduction; columns R and R+1 are r^T W r and 1^T W r
 __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               const double* __restrict__ M, const double* __restrict__ rtime,
                                               int nsplit, int stride, int compact, double* __restrict__ wpart) {
@@ -1179,30 +1182,20 @@ __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, c
     const pint_spec_t& S = *Pd.spec;
     const int n = I.n, R = 2 * S.nred;
     const double* ri = rtime + (I.roff - inst);
-    const double* Mi = M + I.moff;
+    const double* Fb = M + I.moff + (long)(compact && Pd.dsplit ? Pd.red0c : S.ncol) * n;
     long per = (n + nsplit - 1) / nsplit;
     long i0 = split * per, i1 = i0 + per;
     if (i1 > n) i1 = n;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* out = wpart + ((long)inst * nsplit + split) * stride;
     for (int j = wave; j < R + 2; j += 4) {
+        const double* col = Fb + (long)(j < R ? j : 0) * n;
         double acc = 0.0;
-        if (j < R) {
-            const double* col = Mi + (long)((compact && Pd.dsplit ? Pd.red0c : S.ncol) + j) * n;
-            for (long i = i0 + lane; i < i1; i += 64) {
-                double sg = Pd.sigma[i];
-                acc += col[i] * ri[i] / (sg * sg);
-            }
-        } else if (j == R) {  // r^T W r
-            for (long i = i0 + lane; i < i1; i += 64) {
-                double sg = Pd.sigma[i];
-                acc += ri[i] * ri[i] / (sg * sg);
-            }
-        } else {  // 1^T W r
-            for (long i = i0 + lane; i < i1; i += 64) {
-                double sg = Pd.sigma[i];
-                acc += ri[i] / (sg * sg);
-            }
+#pragma unroll 4
+        for (long i = i0 + lane; i < i1; i += 64) {
+            const double is = Pd.isig[i], r = ri[i];
+            const double f = j < R ? col[i] : (j == R ? r : 1.0);
+            acc += f * is * is * r;
         }
         acc = wave_sum(acc);
         if (lane == 0) out[j] = acc;
@@ -1821,7 +1814,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     }
     record(ctx, want_M ? 3 : 1);
     record(ctx, 4);
-    hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
+    hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(RES_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
                        ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
     HIPCHK(hipGetLastError());
     record(ctx, 5);
