@@ -43,6 +43,8 @@ struct PsrDev {
     const int32_t* dptr;     // ndc+1: CSR of the TOAs of each DMX column
     const int32_t* didx;
     const int32_t* drow;     // n: DMX column of each TOA (-1: none)
+    const int32_t* dorig;    // Kd: original column of each compact dense column
+    const int32_t* xorig;    // ndc: original column of each DMX column
     int dsplit;              // compact layout applies (>= 8 DMX columns, no ECORR, no overlapping bins)
     int dcontig;             // every DMX column's TOAs are one contiguous row range (k_gram fuses the bin sums)
     int ndc, Kd, Kpd, red0c; // DMX columns; compact width (excl. residual), padded, first red column
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                               double* __restrict__ ftay, double* __restrict__ delay_out,
                                               double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                              int* __restrict__ status) {
+                                              int write_red, int* __restrict__ status) {
     int b = blockIdx.x;
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
@@ -205,9 +207,11 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
     delay_out[I.roff + r] = o.delay;
-    if (WANT_M && rowM && S.nred > 0) {
+    if (WANT_M && rowM && S.nred > 0 && write_red) {
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
-        // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.
+        // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.  The basis
+        // does not depend on the timing parameters: it is written once per instance and
+        // layout (write_red) and stays resident in M across fit iterations.
         dd ts = dd_mul_d(t.tdb, DAYSEC);
         double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
         for (int k = 0; k < S.nred; k++, colp += 2L * n) {
@@ -741,12 +745,13 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
                                                    double* __restrict__ work, double* __restrict__ dpars,
                                                    double* __restrict__ errs, double* __restrict__ cov,
                                                    double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                   int* __restrict__ status) {
+                                                   int* __restrict__ status, int skip_dsplit) {
     extern __shared__ double lds[];
     __shared__ double sh[SOLVE_T / 64];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
+    if (skip_dsplit && compact && Pd.dsplit) return;  // solved by k_solve_dmx
     const pint_spec_t& S = *Pd.spec;
     const int Kfull = I.K, Kp = I.Kp, ncol = S.ncol;
     const int K = (mode == 0) ? ncol : Kfull;  // WLS ignores the noise basis (fitter.py:1965)
@@ -1014,6 +1019,41 @@ __device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
     return true;
 }
 
+// Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column), from
+// the (ECORR Schur-reduced) Gram; factored with blk_cholinv in the LDS region A and its
+// X = L^-1 stored packed lower (incl. diagonal) to Xout for k_wsolve (residuals.py:567-589).
+template <int NW>
+__device__ bool woodbury_sigma(const GramView& G, const PsrDev& Pd, const pint_spec_t& S, double F0, double* A,
+                               int wave, int lane, int* sflag, double* Xout) {
+    const int ncol = S.ncol, R = 2 * S.nred, Kn = R + 1;
+    const int nbs = (Kn + 15) >> 4;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < nbs * (nbs + 1) / 2 * 256; e += NW * 64) {
+        int Ib, Jb;
+        tri_decode(e >> 8, Ib, Jb);
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+        double v;
+        if (gi < Kn && gj < Kn) {
+            const int ci = (gi < R) ? ncol + gi : 0, cj = (gj < R) ? ncol + gj : 0;
+            const double si = (gi < R) ? 1.0 : F0, sj = (gj < R) ? 1.0 : F0;
+            v = G(ci, cj) * si * sj;
+            if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
+        } else {
+            v = (gi == gj) ? 1.0 : 0.0;
+        }
+        A[((e >> 8) << 8) + swz(r, c)] = v;
+    }
+    __syncthreads();
+    if (!blk_cholinv<NW>(A, nbs, wave, lane, sflag)) return false;
+    for (int e = tid; e < Kn * (Kn + 1) / 2; e += NW * 64) {
+        int i, j;
+        tri_decode(e, i, j);
+        Xout[e] = A[lblk(i >> 4, j >> 4) + swz(i & 15, j & 15)];
+    }
+    return true;
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
@@ -1022,15 +1062,17 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
                                                        const double* __restrict__ DD, const double* __restrict__ DCS,
                                                        double* __restrict__ dpars, double* __restrict__ errs,
                                                        double* __restrict__ cov, double* __restrict__ chi2lin,
-                                                       double* __restrict__ sigL, int* __restrict__ status) {
+                                                       double* __restrict__ sigL, int* __restrict__ status,
+                                                       int skip_dsplit) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
+    if (skip_dsplit && compact && Pd.dsplit) return;  // solved by k_solve_dmx
     const pint_spec_t& S = *Pd.spec;
-    const int Kfull = I.K, Kp = I.Kp, ncol = S.ncol;
+    const int Kfull = I.K, ncol = S.ncol;
     const int K = (mode == 0) ? ncol : Kfull;
     const int nb = (K + 15) >> 4;
     const int nblk = nb * (nb + 1) / 2;
@@ -1125,39 +1167,263 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     }
     q2 = block_sum<NW>(q2, sh);
     if (tid == 0) chi2lin[inst] = rwr - q2;
-    // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column),
-    // Schur-reduced for ECORR through the Gram; X_Sigma = L^-1 -> sigL for k_wsolve
+    // Woodbury Sigma of the GLS chi2 (k_wsolve)
     if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
         __syncthreads();
-        const int R = 2 * S.nred, Kn = R + 1;
-        const int nbs = (Kn + 15) >> 4;
-        const double F0 = pval(tables + I.toff, S.o_F);
-        for (int e = tid; e < nbs * (nbs + 1) / 2 * 256; e += NW * 64) {
-            int Ib, Jb;
-            tri_decode(e >> 8, Ib, Jb);
-            const int r = e & 15, c = (e >> 4) & 15;
-            const int gi = Ib * 16 + r, gj = Jb * 16 + c;
-            double v;
-            if (gi < Kn && gj < Kn) {
-                const int ci = (gi < R) ? ncol + gi : 0, cj = (gj < R) ? ncol + gj : 0;
-                const double si = (gi < R) ? 1.0 : F0, sj = (gj < R) ? 1.0 : F0;
-                v = G(ci, cj) * si * sj;
-                if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
-            } else {
-                v = (gi == gj) ? 1.0 : 0.0;
-            }
-            A[((e >> 8) << 8) + swz(r, c)] = v;
-        }
-        __syncthreads();
-        if (!blk_cholinv<NW>(A, nbs, wave, lane, &sflag)) {
+        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), A, wave, lane, &sflag, sigL + (long)I.soff)) {
             if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
             return;
         }
-        double* L = sigL + (long)I.soff;
-        for (int e = tid; e < Kn * (Kn + 1) / 2; e += NW * 64) {
-            int i, j;
-            tri_decode(e, i, j);
-            L[e] = A[lblk(i >> 4, j >> 4) + swz(i & 15, j & 15)];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_solve_dmx: the normal equations of the compact fit layout with the DMX block
+// eliminated.  In the normalised system A = [A_dd A_dx; A_xd D] the DMX-DMX block D is
+// diagonal (a TOA lies in at most one free bin), so
+//   S = A_dd - A_dx D^-1 A_xd = A_dd - U U^T,  U = A_dx D^-1/2       (rank-ndc update, MFMA)
+//   x_d = S^-1 (b_d - U D^-1/2 b_x),  x_x = D^-1 b_x - D^-1/2 U^T x_d
+//   C_dd = S^-1 = X^T X (X = L_S^-1),  W = X U,
+//   C_xd = -D^-1/2 W^T X,  C_xx = D^-1 + D^-1/2 W^T W D^-1/2.
+// This is the same solution and covariance as the dense solve of A (fitter.py:2196-2202
+// cho_factor/cho_solve); only the Cholesky depth shrinks from ceil(K/16) to ceil(Kd/16).
+// LDS: S (lower blocks) and U (nbd x nbk blocks), then W in place of U.
+// ---------------------------------------------------------------------------------
+constexpr int SD_MAXBLK = 76;  // S + U blocks (2 KiB each) that fit next to the vectors
+
+__device__ __forceinline__ int ublk(int I, int k, int nbk, int nblkS) { return (nblkS + I * nbk + k) << 8; }
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                       const double* __restrict__ tables, const double* __restrict__ Gpart,
+                                                       const double* __restrict__ colsq, int nsplit, int mode,
+                                                       const double* __restrict__ Sd, const double* __restrict__ DD,
+                                                       const double* __restrict__ DCS, double* __restrict__ dpars,
+                                                       double* __restrict__ errs, double* __restrict__ cov,
+                                                       double* __restrict__ chi2lin, double* __restrict__ sigL,
+                                                       int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int sflag;
+    __shared__ double sh[NW];
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.dsplit) return;  // full layout: k_solve_blk / k_solve
+    const pint_spec_t& S = *Pd.spec;
+    const int ncol = S.ncol, ndc = Pd.ndc, Kp = Pd.Kpd, Kres = Pd.Kd;
+    const int Kd = (mode == 0) ? Pd.red0c : Pd.Kd;  // dense columns in the solve (WLS: no noise basis)
+    const int red0 = Pd.red0c;
+    const int nbd = (Kd + 15) >> 4, nbk = (ndc + 15) >> 4;
+    const int nblkS = nbd * (nbd + 1) / 2;
+    double* A = lds;                                  // S blocks, then U/W blocks
+    double* bd = A + (nblkS + nbd * nbk) * 256;       // nbd*16: b_d, then b'_d
+    double* yv = bd + nbd * 16;                       // nbd*16
+    double* bx = yv + nbd * 16;                       // nbk*16: b_x (normalised)
+    double* Dn = bx + nbk * 16;                       // nbk*16: normalised D
+    double* zx = Dn + nbk * 16;                       // nbk*16
+    const double* Gp = Gpart + I.goff;
+    const double* Sdi = Sd + I.sdoff;
+    auto Gd = [&](int i, int j) {  // dense compact Gram (upper storage)
+        if (i > j) { int t = i; i = j; j = t; }
+        return Gp[(long)i * Kp + j];
+    };
+    auto nrm_d = [&](int c) {  // norm of compact dense column c
+        double v = sqrt(mode == 0 ? Gd(c, c) : colsq[(I.coff + c) * nsplit]);
+        return v == 0.0 ? 1.0 : v;
+    };
+    auto nrm_x = [&](int a) {  // norm of DMX column a
+        double v = sqrt(mode == 0 ? DD[I.ddoff + a] : DCS[I.ddoff + a]);
+        return v == 0.0 ? 1.0 : v;
+    };
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid == 0) sflag = 0;
+    // ---- build S = A_dd, U = A_dx D^-1/2, b_d, b_x, D (normalised) ----
+    for (int a = tid; a < nbk * 16; a += NW * 64) {
+        double d = 1.0, b = 0.0;
+        if (a < ndc) {
+            const double na = nrm_x(a);
+            d = DD[I.ddoff + a] / (na * na);
+            b = Sdi[(long)a * Kp + Kres] / na;
+        }
+        Dn[a] = d;
+        bx[a] = b;
+    }
+    for (int e = tid; e < nblkS * 256; e += NW * 64) {
+        int Ib, Jb;
+        tri_decode(e >> 8, Ib, Jb);
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+        double v;
+        if (gi < Kd && gj < Kd) {
+            const double ni = nrm_d(gi), nj = nrm_d(gj);
+            v = Gd(gi, gj) / (ni * nj);
+            if (gi == gj && mode == 1 && gi >= red0) v += 1.0 / Pd.red_phi[gi - red0] / (ni * ni);
+        } else {
+            v = (gi == gj) ? 1.0 : 0.0;
+        }
+        A[((e >> 8) << 8) + swz(r, c)] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < nbd * nbk * 256; e += NW * 64) {
+        const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, a = kb * 16 + c;
+        double v = 0.0;
+        if (gi < Kd && a < ndc) v = Sdi[(long)a * Kp + gi] / (nrm_d(gi) * nrm_x(a)) / sqrt(Dn[a]);
+        A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = v;
+    }
+    for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) / nrm_d(c) : 0.0;
+    const double rwr = Gd(Kres, Kres);
+    __syncthreads();
+    // ---- S -= U U^T (lower blocks), b'_d = b_d - U D^-1/2 b_x ----
+    for (int p = wave; p < nblkS; p += NW) {
+        int Ib, Jb;
+        tri_decode(p, Ib, Jb);
+        double4_t acc = bload(A + lblk(Ib, Jb), lane);
+        for (int k = 0; k < nbk; k++)
+            bmma<false, false>(acc, A + ublk(Ib, k, nbk, nblkS), A + ublk(Jb, k, nbk, nblkS), lane, true);
+        bstore(A + lblk(Ib, Jb), acc, lane, 1.0);
+    }
+    {
+        const int g0 = tid >> 2, sub = tid & 3;
+        double bnew = 0.0;
+        for (int c = g0; c < nbd * 16; c += NW * 16) {
+            double sacc = 0.0;
+            for (int a = sub; a < ndc; a += 4)
+                sacc += A[ublk(c >> 4, a >> 4, nbk, nblkS) + swz(c & 15, a & 15)] * bx[a] / sqrt(Dn[a]);
+            sacc += __shfl_xor(sacc, 1, 64);
+            sacc += __shfl_xor(sacc, 2, 64);
+            bnew = bd[c] - sacc;
+        }
+        __syncthreads();
+        if (sub == 0 && g0 < nbd * 16) bd[g0] = bnew;  // NW*16 >= nbd*16 groups
+    }
+    __syncthreads();
+    if (!blk_cholinv<NW>(A, nbd, wave, lane, &sflag)) {
+        if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        return;
+    }
+    // ---- y = X b'_d ; W = X U (in place, wave per U block column, block rows descending) ----
+    const int g0 = tid >> 2, sub = tid & 3;
+    for (int g = g0; g < nbd * 16; g += NW * 16) {
+        double sy = 0.0;
+        for (int c = sub; c <= g; c += 4) sy += A[lblk(g >> 4, c >> 4) + swz(g & 15, c & 15)] * bd[c];
+        sy += __shfl_xor(sy, 1, 64);
+        sy += __shfl_xor(sy, 2, 64);
+        if (sub == 0) yv[g] = sy;
+    }
+    for (int kb = wave; kb < nbk; kb += NW) {
+        for (int Ib = nbd - 1; Ib >= 0; Ib--) {
+            double4_t acc = {0, 0, 0, 0};
+            for (int Jb = 0; Jb <= Ib; Jb++)
+                bmma<false, true>(acc, A + lblk(Ib, Jb), A + ublk(Jb, kb, nbk, nblkS), lane, false);
+            bstore(A + ublk(Ib, kb, nbk, nblkS), acc, lane, 1.0);
+        }
+    }
+    __syncthreads();
+    // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors; chi2lin ----
+    double bx_dot = 0.0;
+    for (int g = g0; g < Kd; g += NW * 16) {
+        double s1 = 0.0, se = 0.0;
+        for (int rr = g + sub; rr < nbd * 16; rr += 4) {
+            const double x = A[lblk(rr >> 4, g >> 4) + swz(rr & 15, g & 15)];
+            s1 += x * yv[rr];
+            se += x * x;
+        }
+        s1 += __shfl_xor(s1, 1, 64);
+        s1 += __shfl_xor(s1, 2, 64);
+        se += __shfl_xor(se, 1, 64);
+        se += __shfl_xor(se, 2, 64);
+        if (sub == 0) {
+            const int o = Pd.dorig[g];
+            const double nd = nrm_d(g);
+            dpars[I.coff + o] = s1 / nd;
+            errs[I.coff + o] = sqrt(se) / nd;
+            bx_dot += Gd(g, Kres) / nd * s1;  // b_d . x_d
+        }
+    }
+    for (int a = g0; a < ndc; a += NW * 16) {
+        double sz = 0.0, sw = 0.0;
+        for (int rr = sub; rr < nbd * 16; rr += 4) {
+            const double w = A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
+            sz += w * yv[rr];
+            sw += w * w;
+        }
+        sz += __shfl_xor(sz, 1, 64);
+        sz += __shfl_xor(sz, 2, 64);
+        sw += __shfl_xor(sw, 1, 64);
+        sw += __shfl_xor(sw, 2, 64);
+        if (sub == 0) {
+            const double d = Dn[a], na = nrm_x(a);
+            const double xx = bx[a] / d - sz / sqrt(d);
+            const int o = Pd.xorig[a];
+            dpars[I.coff + o] = xx / na;
+            errs[I.coff + o] = sqrt(1.0 / d + sw / d) / na;
+            bx_dot += bx[a] * xx;
+        }
+    }
+    bx_dot = block_sum<NW>(bx_dot, sh);
+    if (tid == 0) chi2lin[inst] = rwr - bx_dot;
+    // ---- covariance of the timing parameters (ncol x ncol, original order) ----
+    {
+        double* C = cov + (long)I.cvoff;
+        const int nbt = (red0 + 15) >> 4;  // dense timing columns: compact 0..red0-1
+        const int nd_pairs = nbt * (nbt + 1) / 2, nx_pairs = nbk * (nbk + 1) / 2, ndx = nbk * nbt;
+        for (int p = wave; p < nd_pairs + nx_pairs + ndx; p += NW) {
+            double4_t acc = {0, 0, 0, 0};
+            int kind, bi, bj;
+            if (p < nd_pairs) {  // C_dd = X^T X
+                kind = 0;
+                tri_decode(p, bj, bi);
+                for (int k = bj; k < nbd; k++) bmma<true, true>(acc, A + lblk(k, bi), A + lblk(k, bj), lane, false);
+            } else if (p < nd_pairs + nx_pairs) {  // (W^T W)_ab
+                kind = 1;
+                tri_decode(p - nd_pairs, bj, bi);
+                for (int k = 0; k < nbd; k++)
+                    bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + ublk(k, bj, nbk, nblkS), lane, false);
+            } else {  // (W^T X)_{a c}: DMX block bi x dense block bj
+                kind = 2;
+                const int q = p - nd_pairs - nx_pairs;
+                bi = q / nbt;
+                bj = q % nbt;
+                for (int k = bj; k < nbd; k++)
+                    bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + lblk(k, bj), lane, false);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int ri = bi * 16 + (lane >> 4) + 4 * q, cj = bj * 16 + (lane & 15);
+                int oi, oj;
+                double v;
+                if (kind == 0) {
+                    if (ri >= red0 || cj >= red0) continue;
+                    oi = Pd.dorig[ri];
+                    oj = Pd.dorig[cj];
+                    v = acc[q] / (nrm_d(ri) * nrm_d(cj));
+                } else if (kind == 1) {
+                    if (ri >= ndc || cj >= ndc) continue;
+                    oi = Pd.xorig[ri];
+                    oj = Pd.xorig[cj];
+                    v = acc[q] / sqrt(Dn[ri] * Dn[cj]) + (ri == cj ? 1.0 / Dn[ri] : 0.0);
+                    v /= nrm_x(ri) * nrm_x(cj);
+                } else {
+                    if (ri >= ndc || cj >= red0) continue;
+                    oi = Pd.xorig[ri];
+                    oj = Pd.dorig[cj];
+                    v = -acc[q] / sqrt(Dn[ri]) / (nrm_x(ri) * nrm_d(cj));
+                }
+                C[(long)oi * ncol + oj] = v;
+                C[(long)oj * ncol + oi] = v;
+            }
+        }
+    }
+    // Woodbury Sigma of the GLS chi2 (k_wsolve)
+    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
+        __syncthreads();
+        const GramView G = gram_view(Pd, I, Gpart, true, Sd, DD);
+        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), A, wave, lane, &sflag, sigL + (long)I.soff)) {
+            if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+            return;
         }
     }
 }
@@ -1325,6 +1591,7 @@ struct pint_ctx {
     double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
     int max_ndc = 0;
     int m_compact = 0;  // layout of the design matrix written by the last pint_eval(want_M)
+    int red_valid[2] = {0, 0};  // red-noise columns of M already written (full, compact layout)
     size_t wpart_cap = 0;
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
@@ -1517,6 +1784,15 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         d.Kd = kd;
         d.Kpd = (kd + 1 + 15) / 16 * 16;
         d.red0c = red0c;
+        {
+            std::vector<int32_t> dorig(kd > 0 ? kd : 1), xorig(ndc > 0 ? ndc : 1);
+            for (int c = 0; c < K; c++) {
+                if (cmap[c] >= 0) dorig[cmap[c]] = c;
+                else xorig[-cmap[c] - 1] = c;
+            }
+            rc |= upload(ctx, ph, dorig.data(), dorig.size(), d.dorig);
+            rc |= upload(ctx, ph, xorig.data(), xorig.size(), d.xorig);
+        }
         rc |= upload(ctx, ph, cmap.data(), cmap.size(), d.cmap);
         rc |= upload(ctx, ph, dptr.data(), dptr.size(), d.dptr);
         rc |= upload(ctx, ph, didx.data(), didx.size(), d.didx);
@@ -1619,6 +1895,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         if (cost <= best * 1.03) { nsplit = ns; break; }
     }
     ctx->nsplit = nsplit;
+    ctx->red_valid[0] = ctx->red_valid[1] = 0;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
         PsrHost& ph = ctx->psrs[p];
@@ -1791,6 +2068,14 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     if (want_M < 0 || want_M > 2) return PINT_E_INVALID;
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     if (want_M) ctx->m_compact = (want_M == 2) ? 1 : 0;
+    // the full and compact layouts place the red-noise columns differently; each is written
+    // once after pint_set_instances (M is reallocated there)
+    int write_red = 0;
+    if (want_M) {
+        write_red = ctx->red_valid[want_M == 2] ? 0 : 1;
+        ctx->red_valid[want_M == 2] = 1;
+        ctx->red_valid[want_M != 2] = 0;  // the other layout's red columns get overwritten
+    }
     record(ctx, want_M ? 2 : 0);
     hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->ninst, ctx->d_tables, ctx->d_ic);
@@ -1803,7 +2088,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, ctx->d_status)
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status)
         if (want_M) {
             if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
         } else {
@@ -1924,26 +2209,55 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
         ctx->copy_pending = false;
     }
-    // blocked MFMA solve when the (padded) normal matrix and the Woodbury Sigma fit the LDS
-    int Ks = 0, Kn = 0;
+    // DMX-eliminated solve for compact-layout instances (k_solve_dmx), when every such
+    // instance fits its LDS budget; the others (and everything in the full layout) go to the
+    // blocked MFMA solve, or the column-by-column one beyond its LDS budget.
+    int Ks = 0, Kn = 0, ndmx_inst = 0;
+    bool dmx_ok = cmp && ctx->blocked_solve;
+    size_t lds_x = 0;
     for (auto& I : ctx->inst) {
-        const pint_spec_t& sp = ctx->psrs[I.psr].spec;
-        Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
-        if (mode == 1) Kn = std::max(Kn, 2 * sp.nred + 1);
+        const PsrHost& ph = ctx->psrs[I.psr];
+        const pint_spec_t& sp = ph.spec;
+        const int kn = mode == 1 ? 2 * sp.nred + 1 : 0;
+        Kn = std::max(Kn, kn);
+        if (cmp && ph.dev.dsplit) {
+            ndmx_inst++;
+            const int kd = mode == 0 ? ph.dev.red0c : ph.dev.Kd;
+            const int nbd = (kd + 15) / 16, nbk = (ph.dev.ndc + 15) / 16, nbs = (kn + 15) / 16;
+            const int blk = nbd * (nbd + 1) / 2 + nbd * nbk;
+            if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB) dmx_ok = false;
+            lds_x = std::max(lds_x, sizeof(double) * ((size_t)std::max(blk, nbs * (nbs + 1) / 2) * 256 +
+                                                      (size_t)(2 * nbd + 3 * nbk) * 16));
+        } else {
+            Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
+        }
+    }
+    if (!dmx_ok) {  // every instance through the general solve
+        for (auto& I : ctx->inst) Ks = std::max(Ks, mode == 0 ? ctx->psrs[I.psr].spec.ncol : I.K);
+        ndmx_inst = 0;
+    }
+    const int skip = ndmx_inst > 0 ? 1 : 0;
+    if (skip) {
+        hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst), dim3(1024), lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
+                           ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+        HIPCHK(hipGetLastError());
     }
     const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
-    if (nbx <= BS_MAXNB && ctx->blocked_solve) {
+    if (skip && Ks == 0) {
+        // every instance went through k_solve_dmx
+    } else if (nbx <= BS_MAXNB && ctx->blocked_solve) {
         size_t lds_b = sizeof(double) * ((size_t)nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx);
         if (nbx <= 5)
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
         else
             hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
     } else {
         int K = ctx->maxK;
         size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
@@ -1951,7 +2265,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, cmp, ctx->d_Sd, ctx->d_DD,
                            ctx->d_DCS, ctx->d_work, ctx->d_dpars,
-                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
     }
     HIPCHK(hipGetLastError());
     record(ctx, 8);

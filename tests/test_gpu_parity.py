@@ -311,7 +311,7 @@ def test_blocked_solve_matches_column_solve(name):
         bf.close()
     (d1, e1, c1, l1, g1), (d2, e2, c2_, l2, g2) = out
     n = len(e1) - 1
-    tol = 3e-4 if name in ("b1855", "j0740") else 1e-7
+    tol = 1e-3 if name in ("b1855", "j0740") else 1e-7
     assert np.max(np.abs((d1[:n] - d2[:n]) / e2[:n])) < tol
     assert np.max(np.abs(e1[:n] / e2[:n] - 1)) < tol
     sc = np.sqrt(np.outer(np.diag(c2_), np.diag(c2_)))
