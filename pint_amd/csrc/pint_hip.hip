@@ -745,7 +745,7 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
                                                    double* __restrict__ work, double* __restrict__ dpars,
                                                    double* __restrict__ errs, double* __restrict__ cov,
                                                    double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                   int* __restrict__ status, int skip_dsplit) {
+                                                   int* __restrict__ status, int skip_dsplit, int do_sigma) {
     extern __shared__ double lds[];
     __shared__ double sh[SOLVE_T / 64];
     const int inst = blockIdx.x;
@@ -838,8 +838,8 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
         if (i == j) errs[I.coff + i] = sqrt(sacc) / nrm[i];
     }
     // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column):
-    // factor in LDS, store L (diag in place) packed to sigL for k_woodbury.
-    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
+    // factor in LDS, store L^-1 (diag in place) packed to sigL for k_wsolve (unless k_sigma does).
+    if (do_sigma && mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
         __syncthreads();
         const int R = 2 * S.nred, Kn = R + 1;
         const double F0 = pval(P, S.o_F);
@@ -888,6 +888,10 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
 // The Woodbury Sigma of the GLS chi2 is factored by the same routine; its X = L^-1 goes
 // to sigL (packed lower incl. diagonal) for k_wsolve.
 // ---------------------------------------------------------------------------------
+// phase timestamps of workgroup 0 (s_memrealtime, 100 MHz), read by pint_debug_read(.., 4, ..)
+__device__ unsigned long long g_ts[32];
+#define TS(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_ts[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
 constexpr int BS_MAXNB = 12;  // 78 blocks x 2 KiB + 2 vectors fit the 160 KiB LDS
 
 __device__ __forceinline__ int swz(int r, int c) { return (c << 4) + (r ^ (c & 14)); }
@@ -931,11 +935,12 @@ __device__ __forceinline__ void bstore(double* Z, const double4_t& v, int lane, 
 }
 
 // One wave: Cholesky of the (full, symmetric) 16x16 block in registers (lane r holds row
-// r), then its inverse column by column (lane c solves L x = e_c); the block is
-// overwritten by L^-1 (zeros above the diagonal).  Returns false if not positive definite.
-__device__ bool diag_factor(double* Akk, int lane) {
+// r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
+// the block is overwritten by L^-1 (zeros above the diagonal).  Returns false if not
+// positive definite.
+__device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
-    double a[16];
+    double a[16], ril[16];
 #pragma unroll
     for (int c = 0; c < 16; c++) a[c] = Akk[swz(r, c)];
     bool ok = true;
@@ -943,9 +948,9 @@ __device__ bool diag_factor(double* Akk, int lane) {
     for (int j = 0; j < 16; j++) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
-        const double ljj = sqrt(djj);
-        const double il = 1.0 / ljj;
-        a[j] = (r == j) ? ljj : (r > j ? a[j] * il : 0.0);
+        const double il = rsqrt(djj);
+        ril[j] = il;
+        a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
 #pragma unroll
         for (int c = j + 1; c < 16; c++) a[c] -= a[j] * rdlane(a[j], c);
     }
@@ -955,7 +960,7 @@ __device__ bool diag_factor(double* Akk, int lane) {
         double s = (r == t) ? 1.0 : 0.0;
 #pragma unroll
         for (int u = 0; u < t; u++) s -= rdlane(a[u], t) * x[u];
-        x[t] = s / rdlane(a[t], t);
+        x[t] = s * ril[t];
     }
     if (lane < 16) {
 #pragma unroll
@@ -976,13 +981,16 @@ __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+
 // afterwards A holds X = L^-1.  Needs NW >= nb - 1.  Returns false (uniformly) if A is
 // not positive definite.
 template <int NW>
-__device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
+__device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
     for (int k = 0; k < nb; k++) {
+        if (k == 0) TS(9);
         if (wave == 0) {
             bool ok = diag_factor(A + lblk(k, k), lane);
             if (!ok && lane == 0) *sflag = 1;
         }
+        if (k == 0) TS(10);
         __syncthreads();
+        if (k == 0) TS(11);
         if (*sflag) return false;
         const double* Lkk = A + lblk(k, k);
         for (int i = k + 1 + wave; i < nb; i += NW) {  // panel: L_ik = A_ik L_kk^-T
@@ -992,6 +1000,7 @@ __device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
             bstore(Aik, acc, lane, 1.0);
         }
         __syncthreads();
+        if (k == 0) TS(12);
         const int m = nb - k - 1;
         if (m == 0) break;
         for (int p = wave; p < m * (m + 1) / 2; p += NW) {  // trailing: A_ij -= L_ik L_jk^T
@@ -1003,7 +1012,9 @@ __device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
             bstore(Aij, acc, lane, 1.0);
         }
         __syncthreads();
+        if (k == 0) TS(13);
     }
+    TS(14);
     for (int i = 1; i < nb; i++) {  // X = L^-1, block row i (diagonal blocks already hold L_ii^-1)
         double4_t acc2 = {0, 0, 0, 0};
         const int j = wave;
@@ -1015,7 +1026,9 @@ __device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
         __syncthreads();
         if (j < i) bstore(A + lblk(i, j), acc2, lane, -1.0);
         __syncthreads();
+        if (i == 1) TS(15);
     }
+    TS(16);
     return true;
 }
 
@@ -1023,7 +1036,7 @@ __device__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
 // the (ECORR Schur-reduced) Gram; factored with blk_cholinv in the LDS region A and its
 // X = L^-1 stored packed lower (incl. diagonal) to Xout for k_wsolve (residuals.py:567-589).
 template <int NW>
-__device__ bool woodbury_sigma(const GramView& G, const PsrDev& Pd, const pint_spec_t& S, double F0, double* A,
+__device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& Pd, const pint_spec_t& S, double F0, double* A,
                                int wave, int lane, int* sflag, double* Xout) {
     const int ncol = S.ncol, R = 2 * S.nred, Kn = R + 1;
     const int nbs = (Kn + 15) >> 4;
@@ -1167,14 +1180,6 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     }
     q2 = block_sum<NW>(q2, sh);
     if (tid == 0) chi2lin[inst] = rwr - q2;
-    // Woodbury Sigma of the GLS chi2 (k_wsolve)
-    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
-        __syncthreads();
-        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), A, wave, lane, &sflag, sigL + (long)I.soff)) {
-            if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
-            return;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1220,35 +1225,44 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     double* yv = bd + nbd * 16;                       // nbd*16
     double* bx = yv + nbd * 16;                       // nbk*16: b_x (normalised)
     double* Dn = bx + nbk * 16;                       // nbk*16: normalised D
-    double* zx = Dn + nbk * 16;                       // nbk*16
+    double* nd = Dn + nbk * 16;                       // nbd*16: dense column norms
+    double* nx = nd + nbd * 16;                       // nbk*16: DMX column norms
     const double* Gp = Gpart + I.goff;
     const double* Sdi = Sd + I.sdoff;
     auto Gd = [&](int i, int j) {  // dense compact Gram (upper storage)
         if (i > j) { int t = i; i = j; j = t; }
         return Gp[(long)i * Kp + j];
     };
-    auto nrm_d = [&](int c) {  // norm of compact dense column c
-        double v = sqrt(mode == 0 ? Gd(c, c) : colsq[(I.coff + c) * nsplit]);
-        return v == 0.0 ? 1.0 : v;
-    };
-    auto nrm_x = [&](int a) {  // norm of DMX column a
-        double v = sqrt(mode == 0 ? DD[I.ddoff + a] : DCS[I.ddoff + a]);
-        return v == 0.0 ? 1.0 : v;
-    };
+    auto nrm_d = [&](int c) { return nd[c]; };  // norms, staged in LDS below
+    auto nrm_x = [&](int a) { return nx[a]; };
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
-    // ---- build S = A_dd, U = A_dx D^-1/2, b_d, b_x, D (normalised) ----
+    TS(0);
+    // ---- column norms (utils.py:2879: zero norm -> 1), b_x, D (normalised) ----
+    for (int c = tid; c < nbd * 16; c += NW * 64) {
+        double v = 1.0;
+        if (c < Kd) {
+            v = sqrt(mode == 0 ? Gd(c, c) : colsq[(I.coff + c) * nsplit]);
+            v = v == 0.0 ? 1.0 : v;
+        }
+        nd[c] = v;
+    }
     for (int a = tid; a < nbk * 16; a += NW * 64) {
-        double d = 1.0, b = 0.0;
+        double d = 1.0, b = 0.0, na = 1.0;
         if (a < ndc) {
-            const double na = nrm_x(a);
-            d = DD[I.ddoff + a] / (na * na);
+            const double dd_ = DD[I.ddoff + a];
+            na = sqrt(mode == 0 ? dd_ : DCS[I.ddoff + a]);
+            na = na == 0.0 ? 1.0 : na;
+            d = dd_ / (na * na);
             b = Sdi[(long)a * Kp + Kres] / na;
         }
+        nx[a] = na;
         Dn[a] = d;
         bx[a] = b;
     }
+    __syncthreads();
+    // ---- build S = A_dd, U = A_dx D^-1/2, b_d ----
     for (int e = tid; e < nblkS * 256; e += NW * 64) {
         int Ib, Jb;
         tri_decode(e >> 8, Ib, Jb);
@@ -1276,6 +1290,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) / nrm_d(c) : 0.0;
     const double rwr = Gd(Kres, Kres);
     __syncthreads();
+    TS(1);
     // ---- S -= U U^T (lower blocks), b'_d = b_d - U D^-1/2 b_x ----
     for (int p = wave; p < nblkS; p += NW) {
         int Ib, Jb;
@@ -1300,10 +1315,12 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         if (sub == 0 && g0 < nbd * 16) bd[g0] = bnew;  // NW*16 >= nbd*16 groups
     }
     __syncthreads();
+    TS(2);
     if (!blk_cholinv<NW>(A, nbd, wave, lane, &sflag)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         return;
     }
+    TS(3);
     // ---- y = X b'_d ; W = X U (in place, wave per U block column, block rows descending) ----
     const int g0 = tid >> 2, sub = tid & 3;
     for (int g = g0; g < nbd * 16; g += NW * 16) {
@@ -1322,6 +1339,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         }
     }
     __syncthreads();
+    TS(4);
     // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors; chi2lin ----
     double bx_dot = 0.0;
     for (int g = g0; g < Kd; g += NW * 16) {
@@ -1365,6 +1383,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     }
     bx_dot = block_sum<NW>(bx_dot, sh);
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
+    TS(5);
     // ---- covariance of the timing parameters (ncol x ncol, original order) ----
     {
         double* C = cov + (long)I.cvoff;
@@ -1417,14 +1436,30 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             }
         }
     }
-    // Woodbury Sigma of the GLS chi2 (k_wsolve)
-    if (mode == 1 && (S.nred > 0 || Pd.nep > 0)) {
-        __syncthreads();
-        const GramView G = gram_view(Pd, I, Gpart, true, Sd, DD);
-        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), A, wave, lane, &sflag, sigL + (long)I.soff)) {
-            if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
-            return;
-        }
+    TS(6);
+}
+
+// k_sigma: the Woodbury Sigma factor of every GLS instance (woodbury_sigma), launched on a
+// side stream right after the Gram so it runs on the CUs the per-instance solve leaves idle.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_sigma(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ tables, const double* __restrict__ Gpart,
+                                                   int compact, const double* __restrict__ Sd,
+                                                   const double* __restrict__ DD, double* __restrict__ sigL,
+                                                   int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int sflag;
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    if (!(S.nred > 0 || Pd.nep > 0)) return;
+    if (threadIdx.x == 0) sflag = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const GramView G = gram_view(Pd, I, Gpart, compact && Pd.dsplit, Sd, DD);
+    if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff)) {
+        if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
     }
 }
 
@@ -1563,6 +1598,9 @@ struct pint_ctx {
     hipStream_t cstream = nullptr;   // copy stream: fit outputs -> host, overlapped with compute
     hipEvent_t ev_solved = nullptr, ev_copied = nullptr;
     bool copy_pending = false;
+    hipStream_t sstream = nullptr;   // side stream: the Woodbury Sigma factor (k_sigma)
+    hipEvent_t ev_gram = nullptr, ev_sigma = nullptr;
+    bool sigma_pending = false;
     std::string err;
     std::vector<PsrHost> psrs;
     PsrDev* d_psrs = nullptr;
@@ -1651,6 +1689,9 @@ pint_ctx* pint_ctx_create(int device) {
     hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
     hipEventCreateWithFlags(&ctx->ev_solved, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_copied, hipEventDisableTiming);
+    hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
+    hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int i = 0; i < 12; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
     return ctx;
@@ -1687,6 +1728,10 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
     if (ctx->ev_solved) hipEventDestroy(ctx->ev_solved);
     if (ctx->ev_copied) hipEventDestroy(ctx->ev_copied);
+    if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
+    if (ctx->ev_gram) hipEventDestroy(ctx->ev_gram);
+    if (ctx->ev_sigma) hipEventDestroy(ctx->ev_sigma);
+    if (ctx->sstream) hipStreamDestroy(ctx->sstream);
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -2053,6 +2098,7 @@ static void update_timings(pint_ctx* ctx) {
 static int check_status(pint_ctx* ctx) {
     int st = 0;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
@@ -2139,6 +2185,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     hipSetDevice(ctx->device);
     HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     const int nparts = ctx->nsplit + ((mode == 1 && ctx->max_nep > 0) ? 1 : 0);
+    if (ctx->sigma_pending) {  // the previous k_sigma reads the Gram buffer this step overwrites
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
+        ctx->sigma_pending = false;
+    }
     record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
@@ -2205,6 +2255,34 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
+    // Woodbury Sigma factor on the side stream, concurrent with the per-instance solve
+    int do_sigma = 0;
+    if (mode == 1) {
+        int kn = 0;
+        bool any = false;
+        for (auto& I : ctx->inst) {
+            const PsrHost& ph = ctx->psrs[I.psr];
+            if (ph.spec.nred > 0 || ph.dev.nep > 0) { any = true; kn = std::max(kn, 2 * ph.spec.nred + 1); }
+        }
+        const int nbs = (kn + 15) / 16;
+        if (any && nbs <= BS_MAXNB && ctx->blocked_solve) {
+            HIPCHK(hipEventRecord(ctx->ev_gram, ctx->stream));
+            HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
+            const size_t lds_s = sizeof(double) * (size_t)nbs * (nbs + 1) / 2 * 256;
+            if (nbs <= 5)
+                hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
+                                   ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
+            else
+                hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
+                                   ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
+                                   ctx->d_status);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
+            ctx->sigma_pending = true;
+        } else if (any) {
+            do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
+        }
+    }
     if (ctx->copy_pending) {  // the previous step's outputs may still be in flight to the host
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
         ctx->copy_pending = false;
@@ -2227,7 +2305,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             const int blk = nbd * (nbd + 1) / 2 + nbd * nbk;
             if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB) dmx_ok = false;
             lds_x = std::max(lds_x, sizeof(double) * ((size_t)std::max(blk, nbs * (nbs + 1) / 2) * 256 +
-                                                      (size_t)(2 * nbd + 3 * nbk) * 16));
+                                                      (size_t)(3 * nbd + 4 * nbk) * 16));
         } else {
             Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
         }
@@ -2265,7 +2343,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, cmp, ctx->d_Sd, ctx->d_DD,
                            ctx->d_DCS, ctx->d_work, ctx->d_dpars,
-                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
+                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, do_sigma);
+    }
+    if (do_sigma && !(nbx > BS_MAXNB || !ctx->blocked_solve)) {
+        // Sigma too large for k_sigma but the main solve went to the blocked kernels
+        ctx->err = "Woodbury Sigma too large for the LDS factorisation";
+        return PINT_E_INVALID;
     }
     HIPCHK(hipGetLastError());
     record(ctx, 8);
@@ -2327,6 +2410,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
         ctx->wpart_cap = need;
     }
     record(ctx, 10);
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
     hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
                        ctx->d_rt, nsw, stride, ctx->m_compact, ctx->d_wpart);
     HIPCHK(hipGetLastError());
@@ -2369,6 +2453,14 @@ int pint_last_timing(pint_ctx* ctx, double* ms) {
 // debug/introspection: which 0 = Gram partials (sum over splits done by caller),
 // 1 = column sums of squares, 2 = Woodbury Sigma factor, 3 = L^-1 work
 int pint_debug_read(pint_ctx* ctx, int which, double* out) {
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
+    if (which == 4) {  // phase timestamps (us) of k_solve_dmx workgroup 0
+        unsigned long long ts[32];
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_ts), sizeof(ts)));
+        for (int i = 0; i < 32; i++) out[i] = (double)(ts[i] - ts[0]) * 0.01;
+        return 32;
+    }
     size_t n = which == 0 ? ctx->tot_g : which == 1 ? ctx->tot_c * ctx->nsplit : ctx->tot_s;
     double* src = which == 0 ? ctx->d_G : which == 1 ? ctx->d_colsq : which == 2 ? ctx->d_sigL : ctx->d_work;
     HIPCHK(hipMemcpyAsync(out, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
@@ -2379,6 +2471,7 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
 int pint_sync(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->cstream));
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
     return PINT_OK;
 }
 
