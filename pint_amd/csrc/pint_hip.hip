@@ -360,9 +360,12 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
     const PsrDev& Pd = psrs[I.psr];
     const bool cmp = compact && Pd.dsplit;
     const int n = I.n, K = cmp ? Pd.Kd : I.K, Kp = cmp ? Pd.Kpd : I.Kp;
-    const int stride = Kp + ((Kp & 31) == 0 ? 16 : 0);  // row stride = 16 mod 32 doubles
-    double* Ts = lds;                    // [CH][stride] whitened rows
-    double* Sg = lds + CH * stride;      // [CH] sigma of the staged rows (colsq)
+    // the staged chunk is column-major, column stride CS = CH + 2 (= 2 mod 32 doubles): the
+    // staging stores (lanes over consecutive rows) and the MFMA operand reads (16 columns x
+    // 4 rows per wave) both hit distinct bank pairs within each half-wave
+    constexpr int CS = CH + 2;
+    double* Ts = lds;                    // [Kp][CS] whitened rows, column-major
+    double* Sg = lds + Kp * CS;          // [CH] sigma of the staged rows (colsq)
     const double* Mi = M + I.moff;
     const double* ri = rtime + I.ooff;
     const double* Ei = esum + I.eoff;
@@ -448,7 +451,7 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
                 if (q < nq && c < Kp) {
                     double v = st[q];
                     if (!VIRT) v = c < K ? v : (c == K ? r_next : 0.0);
-                    Ts[ii * stride + c] = v * iw;
+                    Ts[c * CS + ii] = v * iw;
                 }
             }
             if (!VIRT && c_base == 0) Sg[ii] = sg_next;
@@ -458,18 +461,18 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
         if (!VIRT && cgrp < CG2) {
             const int nr = (i1 - c0 < CH) ? (int)(i1 - c0) : CH;
             for (int r = cgrp; r < nr; r += CG2) {
-                const double u = Ts[r * stride + ccol] * Sg[r];
+                const double u = Ts[ccol * CS + r] * Sg[r];
                 csq += u * u;
             }
         }
 #pragma unroll
         for (int kk = 0; kk < CH / 4; kk++) {
-            const double* Tr = Ts + (kk * 4 + (lane >> 4)) * stride + (lane & 15);
+            const double* Tr = Ts + (lane & 15) * CS + kk * 4 + (lane >> 4);
             double a[T], b[T];
 #pragma unroll
             for (int t = 0; t < T; t++) {
-                a[t] = Tr[tI[t] * 16];
-                b[t] = Tr[tJ[t] * 16];
+                a[t] = Tr[tI[t] * 16 * CS];
+                b[t] = Tr[tJ[t] * 16 * CS];
             }
 #pragma unroll
             for (int t = 0; t < T - 1; t++) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
@@ -2075,6 +2078,7 @@ int pint_get_tables(pint_ctx* ctx, double* out) {
 }
 
 int pint_set_tables(pint_ctx* ctx, const double* tables) {
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -2221,9 +2225,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         for (int g = 0; g < (int)groups.size(); g++) {
             const KpGroup& kg = groups[g];
             const int T = kg.T;
-            const int sstride = kg.maxKp + 16;
             const int CH = gram_ch(T);
-            size_t lds = sizeof(double) * (CH * sstride + CH);
+            size_t lds = sizeof(double) * ((size_t)kg.maxKp * (CH + 2) + CH);
             const InstDev* di = (cmp ? ctx->d_inst_sorted_c : ctx->d_inst_sorted) + kg.first;
             for (int virt = 0; virt < 2; virt++) {
                 if (virt && !(mode == 1 && ctx->max_nep > 0)) break;
@@ -2388,6 +2391,7 @@ void pint_host_free(void* p) {
 }
 
 int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
                        ctx->d_dpars, ctx->d_lam);
