@@ -180,9 +180,17 @@ int pint_set_lazy(pint_ctx *ctx, int lazy);
 int pint_check(pint_ctx *ctx);
 /* Engine options (no reference counterpart): PINT_OPT_BLOCKED_SOLVE = 1 (default) solves
  * the normal equations with the blocked FP64-MFMA kernel, 0 with the column-by-column
- * LDS kernel (used by the tests to cross-check the two). */
+ * LDS kernel (used by the tests to cross-check the two).  PINT_OPT_VGRAM = 1 (default)
+ * generates the PLRedNoise Fourier columns inside the Gram and Woodbury kernels of the
+ * compact fit layout (never stored in M) and fuses the DMX bin sums into the Gram; 0
+ * keeps them in M (the tests cross-check the two).  Takes effect at pint_set_instances. */
 #define PINT_OPT_BLOCKED_SOLVE 1
+#define PINT_OPT_VGRAM 2
 int pint_set_option(pint_ctx *ctx, int key, int value);
+/* Introspection: PINT_QUERY_NVGRAM = 1 returns the number of instances of the current batch
+ * on the generated-Fourier path; negative status on error. */
+#define PINT_QUERY_NVGRAM 1
+int pint_query(pint_ctx *ctx, int key);
 /* Page-locked host memory for the output buffers (hipHostMalloc); NULL on failure. */
 void *pint_host_alloc(size_t bytes);
 void pint_host_free(void *p);

@@ -15,6 +15,8 @@
 #include <vector>
 #include <cstring>
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include "physics.hpp"
 
 using namespace pint;
@@ -32,6 +34,7 @@ struct PsrDev {
     const pint_spec_t* spec;
     const double* red_freq;  // nred
     const double* red_phi;   // 2*nred
+    const double* red_cs;    // n x 2: (cos, sin) of the red-noise fundamental per TOA (k_redbase)
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
@@ -52,6 +55,10 @@ struct PsrDev {
     int K;   // ncol + 2*nred
     int Kp;  // padded K+1 (residual column) to 16
     int nep; // ECORR epochs (eliminated by Schur complement)
+    int vg;  // compact fit layout on the k_gram_v path (DMX slots as MFMA rows, F^T W F from k_trig)
+    int vns; // k_gram_v DMX slots (bins of an N-split are distinct mod vns)
+    int vkp; // k_gram_v LDS width: [T | r | slots | F] padded to 16
+    int pad_;
 };
 
 struct InstDev {
@@ -71,6 +78,7 @@ struct InstDev {
     long ooff;   // residual output offset (n per instance)
     long sdoff;  // DMX cross-sum offset (ndc*Kpd) / per-column sums offset (ndc)
     long ddoff;
+    long vgoff;  // k_gram_v DMX slot partials offset (nsplit * vns * (Kd+3))
     int self;    // index of this instance in the batch
     int pad_;
 };
@@ -156,7 +164,7 @@ __device__ double block_sum(double v, double* sh) {
 // ---------------------------------------------------------------------------------
 // k_prep: per-instance constants of the evaluation (astrometry/starpm state, 1/F0), one
 // thread per instance, so k_eval's threads only do per-TOA work.
-__global__ void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, int ninst,
+__global__ __launch_bounds__(64) void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, int ninst,
                        const double* __restrict__ tables, InstConst* __restrict__ ic) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ninst) return;
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
     delay_out[I.roff + r] = o.delay;
-    if (WANT_M && rowM && S.nred > 0 && write_red) {
+    if (WANT_M && rowM && S.nred > 0 && write_red && !(cmp && Pd.vg)) {  // vg: generated where used
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
         // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.  The basis
         // does not depend on the timing parameters: it is written once per instance and
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(256) void k_dmx(const PsrDev* __restrict__ psrs, co
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const int a = blockIdx.x;
-    if (!Pd.dsplit || Pd.dcontig || a >= Pd.ndc) return;  // dcontig: fused into k_gram
+    if (!Pd.dsplit || Pd.dcontig || Pd.vg || a >= Pd.ndc) return;  // dcontig: k_dmx_rows
     const int n = I.n, Kd = Pd.Kd, Kpd = Pd.Kpd;
     const double* Mi = M + I.moff;
     const double* ri = rtime + I.ooff;
@@ -569,7 +577,7 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const int a = blockIdx.x;
-    if (!Pd.dsplit || !Pd.dcontig || a >= Pd.ndc) return;
+    if (!Pd.dsplit || !Pd.dcontig || Pd.vg || a >= Pd.ndc) return;  // vg: fused into k_gram_v
     const int n = I.n, Kd = Pd.Kd, Kpd = Pd.Kpd;
     const int W = Kd + 2;               // columns + residual + the DD/DCS slot
     const int str = W | 1;              // odd stride
@@ -637,31 +645,406 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Compact fit layout, "vg" path (PsrDev::vg, PINT_OPT_VGRAM).
+// The PLRedNoise basis (noise_model.py:861-880, frequencies :847-858) is a harmonic
+// series: F[:,2h] = sin((h+1) theta_i), F[:,2h+1] = cos((h+1) theta_i), theta_i =
+// 2 pi t_i f_1, t = tdbld * 86400 s, f_k = k f_1.  Hence
+//  - its Gram block F^T W F follows from the weighted trig sums C_m = sum_i w_i cos(m
+//    theta_i), S_m = sum_i w_i sin(m theta_i), m <= 2 nred, by the product-to-sum
+//    identities (k_trig, k_tsum, k_greduce): O(N nred) VALU work instead of O(N nred^2)
+//    MFMA work; harmonics are rotations of the per-TOA fundamental (k_redbase);
+//  - k_gram_v runs the MFMA tiles of the rows [T | r] (compact timing columns and the
+//    residual) against every column [T | r | F] of M: ~ (P+1)/(P+R+1) of the full Gram;
+//  - the DMX bin rows (bins are contiguous row ranges) are per-bin sums over the bin's
+//    rows of the timing columns and of the generated Fourier columns (k_trig), replacing
+//    k_dmx_rows' pass over the whole of M.
+// ---------------------------------------------------------------------------------
+constexpr int VTRIG = 64;   // trig sums per kind: C_m, S_m weighted, U_m, V_m unweighted (m < 64)   // trig sums m = 0..63 (nred <= 31)
+constexpr int VMAXR0 = 48;  // timing columns + residual staged from M (<= 3 row tiles)
+constexpr int VMAXKP = 144; // widest k_gram_v LDS tile [T | r | slots | F] (two buffers of 64 rows)
+constexpr int VCH = 64;     // k_gram_v rows per chunk
+
+// sin/cos of 2 pi frac(x) for a phase x in cycles (double-double argument reduction)
+__device__ __forceinline__ void dd_sincos_cyc(dd x, double* s, double* c) {
+    const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
+    sincos(TWO_PI * fr, s, c);
+}
+
+__device__ __forceinline__ void rot(double& c, double& s, double c1, double s1) {
+    const double cn = c * c1 - s * s1;
+    s = s * c1 + c * s1;
+    c = cn;
+}
+
+// e^{i k theta} from e^{i theta} by binary powering (k >= 0)
+__device__ __forceinline__ void cpow(double c1, double s1, int k, double& c, double& s) {
+    c = 1.0;
+    s = 0.0;
+    double bc = c1, bs = s1;
+    while (k) {
+        if (k & 1) rot(c, s, bc, bs);
+        k >>= 1;
+        if (k) rot(bc, bs, bc, bs);
+    }
+}
+
+// rows [i0, i1) of N-split `split` (k_gram's partition: a multiple of 4 rows per split)
+__device__ __forceinline__ void split_rows(int n, int nsplit, int split, long& i0, long& i1) {
+    long per = (n + nsplit - 1) / nsplit;
+    per = (per + 3) / 4 * 4;
+    i0 = split * per;
+    i1 = i0 + per;
+    if (i1 > n) i1 = n;
+    if (i0 > n) i0 = n;
+}
+
+// LDS column order of k_gram_v -> compact column: timing [0, r0) stay, the residual (LDS
+// column r0) goes to Kd, the Fourier columns (r0, Kd] move down by one, padding stays.
+__device__ __forceinline__ int vg_cidx(int p, int r0, int Kd) {
+    return p < r0 ? p : (p == r0 ? Kd : (p <= Kd ? p - 1 : p));
+}
+
+template <int T>
+__global__ __launch_bounds__(GTHREADS) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                     const double* __restrict__ M, const double* __restrict__ rtime,
+                                                     const double* __restrict__ dmxv, int nsplit,
+                                                     double* __restrict__ Gpart, double* __restrict__ colsq,
+                                                     double* __restrict__ Sdp) {
+    extern __shared__ double lds[];
+    constexpr int CH = VCH;
+    constexpr int CS = CH + 2;                   // column stride (= 2 mod 32 doubles)
+    constexpr int CG = GTHREADS / CH;            // staging threads per row
+    constexpr int QL = (VMAXR0 + CG - 1) / CG;   // timing columns loaded per thread
+    constexpr int QN = (VMAXKP + CG - 1) / CG;   // LDS columns stored per thread
+    const InstDev I = insts[blockIdx.y];
+    const int split = blockIdx.x;
+    const PsrDev& Pd = psrs[I.psr];
+    const int n = I.n, Kd = Pd.Kd, Kp = Pd.Kpd, r0 = Pd.red0c, NS = Pd.vns, Kpv = Pd.vkp;
+    const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
+    const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD, DCS
+    double* Tb[2] = {lds, lds + Kpv * CS};  // double-buffered [Kpv][CS] whitened rows
+    double* Sg = lds + 2 * Kpv * CS;        // [2][CH] sigma
+    long i0, i1;
+    split_rows(n, nsplit, split, i0, i1);
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + I.ooff;
+    const double* xv = dmxv + I.ooff;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nt = Kpv / 16, ntr = f0 / 16;
+    const int ntiles = ntr * nt - ntr * (ntr - 1) / 2;  // row tiles < ntr, upper part
+    const int t_lo = (ntiles * wave) / GWAVES, t_hi = (ntiles * (wave + 1)) / GWAVES;
+    const bool full = (t_hi - t_lo) == T;
+    int tI[T], tJ[T];
+    {
+        int ti = 0, rem = t_lo;
+        while (rem >= nt - ti) { rem -= nt - ti; ti++; }
+        int tj = ti + rem;
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+            tI[t] = ti;
+            tJ[t] = tj;
+            if (t + 2 < T || (t + 1 < T && full)) {
+                if (++tj == nt) { ti++; tj = ti; }
+            }
+        }
+    }
+    double4_t acc[T];
+#pragma unroll
+    for (int t = 0; t < T; t++) acc[t] = (double4_t){0, 0, 0, 0};
+    // column sums of squares of the [T | r | slots] columns (the Fourier ones: k_trig)
+    const int ccol = tid % f0, cgrp = tid / f0, CG2 = GTHREADS / f0;
+    double csq = 0.0;
+    const int ii = tid % CH, cb = tid / CH;
+    // this thread's Fourier columns p = cb + CG q in [f0, Wv): all sines or all cosines (CG
+    // even), harmonics h1, h1 + CG/2, ...: e^{i h theta} of the row's fundamental
+    // (k_redbase) advanced by e^{i (CG/2) theta}
+    int qf = 0;
+    while (qf < QN && cb + CG * qf < f0) qf++;
+    const int pf = cb + CG * qf;
+    const bool fsin = ((pf - f0) & 1) == 0;
+    const int h1 = (pf - f0) / 2 + 1;
+    double st[QL];  // the next chunk's row ii, raw loads (consumed at its store)
+    double sg_n = 1.0, w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
+    int d_n = -1;
+    bool ok_n = false;
+    auto load = [&](long c0) {
+        long row = c0 + ii;
+        ok_n = row < i1;
+        if (!ok_n) row = i1 - 1;
+        sg_n = Pd.sigma[row];
+        w_n = Pd.isig[row];
+        r_n = ri[row];
+        x_n = xv[row];
+        d_n = Pd.drow[row];
+        if (pf < Wv) {
+            c1_n = Pd.red_cs[2 * row];
+            s1_n = Pd.red_cs[2 * row + 1];
+        }
+#pragma unroll
+        for (int q = 0; q < QL; q++) {
+            const int p = cb + CG * q;
+            if (p < r0) st[q] = Mi[(long)p * n + row];
+        }
+    };
+    auto store = [&](double* Ts, double* sg) {
+        const double iw = ok_n ? w_n : 0.0;
+        const int sl = d_n >= 0 ? s0 + d_n % NS : -1;  // LDS column of the row's DMX slot
+        double fc = 1.0, fs = 0.0, c4 = 1.0, s4 = 0.0;
+        if (pf < Wv) {
+            cpow(c1_n, s1_n, h1, fc, fs);
+            cpow(c1_n, s1_n, CG / 2, c4, s4);
+        }
+#pragma unroll
+        for (int q = 0; q < QN; q++) {
+            const int p = cb + CG * q;
+            if (p < Kpv) {
+                double v;
+                if (q < QL && p < r0) v = st[q < QL ? q : 0];
+                else if (p == r0) v = r_n;
+                else if (p < f0) v = p == sl ? x_n : 0.0;
+                else if (p < Wv) {
+                    v = fsin ? fs : fc;
+                    rot(fc, fs, c4, s4);
+                } else v = 0.0;
+                Ts[p * CS + ii] = v * iw;
+            }
+        }
+        if (cb == 0) sg[ii] = sg_n;
+    };
+    const long nch = (i1 - i0 + CH - 1) / CH;
+    if (nch > 0) {
+        load(i0);
+        store(Tb[0], Sg);
+        if (nch > 1) load(i0 + CH);
+    }
+    __syncthreads();
+    for (long k = 0; k < nch; k++) {
+        double* Ts = Tb[k & 1];
+        const double* sg = Sg + (k & 1) * CH;
+        // stage chunk k+1 into the other buffer (its last readers finished before the
+        // barrier that ended iteration k-1), then prefetch chunk k+2
+        if (k + 1 < nch) {
+            store(Tb[(k + 1) & 1], Sg + ((k + 1) & 1) * CH);
+            if (k + 2 < nch) load(i0 + (k + 2) * CH);
+        }
+        const long c0 = i0 + k * CH;
+        const int nr = (i1 - c0 < CH) ? (int)(i1 - c0) : CH;
+        if (cgrp < CG2) {
+            for (int r = cgrp; r < nr; r += CG2) {
+                const double u = Ts[ccol * CS + r] * sg[r];
+                csq += u * u;
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < CH / 4; kk++) {
+            const double* Tr = Ts + (lane & 15) * CS + kk * 4 + (lane >> 4);
+            double a[T], b[T];
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                a[t] = Tr[tI[t] * 16 * CS];
+                b[t] = Tr[tJ[t] * 16 * CS];
+            }
+#pragma unroll
+            for (int t = 0; t < T - 1; t++) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
+            if (full) acc[T - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T - 1], b[T - 1], acc[T - 1], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // partial tiles (upper triangle in LDS order): [T|r] x [T|r|F] -> the Gram partial at
+    // (min, max) of the compact columns; slot rows/columns -> this split's DMX partials
+    double* G = Gpart + I.goff + (long)split * Kp * Kp;
+    double* Sp = Sdp + I.vgoff + (long)split * NS * SW;
+    auto cidx = [&](int p) { return p < r0 ? p : (p == r0 ? Kd : r0 + (p - f0)); };
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        if (t < T - 1 || full) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int pr = tI[t] * 16 + (lane >> 4) + 4 * q;
+                const int pc = tJ[t] * 16 + (lane & 15);
+                const double v = acc[t][q];
+                if (pr > pc || pc >= Wv) continue;
+                const bool rs = pr >= s0, cs = pc >= s0 && pc < f0;  // slot row / slot column
+                if (!rs && !cs) {
+                    int a = cidx(pr), b = cidx(pc);
+                    if (a > b) { const int x = a; a = b; b = x; }
+                    G[(long)a * Kp + b] = v;
+                } else if (!rs) {
+                    Sp[(long)(pc - s0) * SW + cidx(pr)] = v;            // DMX x [T|r]
+                } else if (cs) {
+                    if (pr == pc) Sp[(long)(pr - s0) * SW + Kd + 1] = v;  // DD
+                } else {
+                    Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F
+                }
+            }
+        }
+    }
+    if (cgrp < CG2) lds[cgrp * f0 + ccol] = csq;  // the last barrier freed the LDS tiles
+    __syncthreads();
+    if (tid < f0 && tid != r0) {
+        double v = 0.0;
+        for (int g = 0; g < CG2; g++) v += lds[g * f0 + tid];
+        if (tid >= s0) Sp[(long)(tid - s0) * SW + Kd + 2] = v;  // DCS
+        else colsq[(I.coff + tid) * nsplit + split] = v;
+    }
+}
+
+// k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
+// with the phase t_i f_1 reduced in double-double; computed once at pint_add_pulsar
+// (TOA-only data, like tdb).  Harmonic m is reached by rotations of it.
+__global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __restrict__ tdb_lo, int n, double f1,
+                          double* __restrict__ cs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s, c;
+    dd_sincos_cyc(dd_mul_d(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), f1), &s, &c);
+    cs[2 * i] = c;
+    cs[2 * i + 1] = s;
+}
+
+// k_trig: the trig sums of every vg instance (m <= 2 nred): weighted C_m = sum w cos(m
+// theta), S_m = sum w sin(m theta) for F^T W F, and unweighted U_m, V_m for the Fourier
+// column norms (sum sin^2(h theta) = (N - U_2h)/2).  One 256-thread block per (kind,
+// N-split, half of the m range): wave w accumulates m = 8(4 half + w) .. +7 over the
+// split's rows (harmonics by rotation of the per-TOA fundamental, k_redbase), one partial
+// per block -> TSp (summed by k_tsum).  Runs on the side stream, concurrent with k_gram_v
+// (one wave per SIMD, so it co-resides with k_gram_v's workgroups).
+__global__ __launch_bounds__(256) void k_trig(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              int nsplit, double* __restrict__ TSp) {
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.vg) return;
+    const int x = blockIdx.x % (2 * nsplit), kind = blockIdx.x / (2 * nsplit), nred = Pd.spec->nred;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int m0 = 8 * (4 * (x & 1) + wave);
+    if (nred <= 0 || m0 > 2 * nred) return;
+    long i0, i1;
+    split_rows(I.n, nsplit, x >> 1, i0, i1);
+    double C[8], Sn[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) C[u] = Sn[u] = 0.0;
+    for (long i = i0 + lane; i < i1; i += 64) {
+        const double is = Pd.isig[i], w = kind ? 1.0 : is * is;
+        const double c1 = Pd.red_cs[2 * i], s1 = Pd.red_cs[2 * i + 1];
+        double c, s;
+        cpow(c1, s1, m0, c, s);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            C[u] += w * c;
+            Sn[u] += w * s;
+            rot(c, s, c1, s1);
+        }
+    }
+    double* out = TSp + ((long)I.self * nsplit + (x >> 1)) * (4 * VTRIG) + 2 * VTRIG * kind + m0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const double cv = wave_sum(C[u]), sv = wave_sum(Sn[u]);
+        if (lane == 0) {
+            out[u] = cv;
+            out[VTRIG + u] = sv;
+        }
+    }
+}
+
+// k_tsum: k_trig's per-block trig-sum partials of an instance summed in a fixed order
+__global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              int nsplit, const double* __restrict__ TSp, double* __restrict__ TS) {
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.vg) return;
+    const int m = threadIdx.x, nb = nsplit;
+    const double* p = TSp + (long)I.self * nsplit * (4 * VTRIG) + m;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int x = 0;
+    for (; x + 3 < nb; x += 4) {
+        v0 += p[(long)x * 4 * VTRIG];
+        v1 += p[(long)(x + 1) * 4 * VTRIG];
+        v2 += p[(long)(x + 2) * 4 * VTRIG];
+        v3 += p[(long)(x + 3) * 4 * VTRIG];
+    }
+    for (; x < nb; x++) v0 += p[(long)x * 4 * VTRIG];
+    TS[(long)I.self * 4 * VTRIG + m] = (v0 + v1) + (v2 + v3);
+}
+
 // Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
 // triangle only, in a fixed order (deterministic), and the column sums of squares.
+// vg instances: the Fourier block F^T W F from the trig sums TS (k_trig + k_tsum) by the
+// product-to-sum identities (a, b = harmonics 1..nred), and past block nbg the DMX bin
+// rows Sd, DD, DCS from k_gram_v's slot partials of the N-splits the bin's rows fall in:
+//   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
+//   sin a cos b = (S_a+b + S_a-b)/2     (S_-k = -S_k),
 __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                 int nsplit, int nparts, int compact, double* __restrict__ Gpart,
-                                                 double* __restrict__ colsq) {
+                                                 int nsplit, int nparts, int compact, int nbg,
+                                                 double* __restrict__ Gpart, double* __restrict__ colsq,
+                                                 const double* __restrict__ TS, const double* __restrict__ Sdp,
+                                                 double* __restrict__ Sd, double* __restrict__ DD,
+                                                 double* __restrict__ DCS) {
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const bool cmp = compact && Pd.dsplit;
+    const bool vg = cmp && Pd.vg;
     const int Kp = cmp ? Pd.Kpd : I.Kp, Kc = cmp ? Pd.Kd : I.K;
+    const int r0 = Pd.red0c;
+    if ((int)blockIdx.x >= nbg) {  // DMX bin a of a vg instance: its slot partials
+        const int a = blockIdx.x - nbg;
+        if (!vg || a >= Pd.ndc) return;
+        const int SW = Kc + 3;
+        const int cnt = Pd.dptr[a + 1] - Pd.dptr[a];
+        const long lo = cnt > 0 ? Pd.didx[Pd.dptr[a]] : 0, hi = lo + cnt;
+        long per = (I.n + nsplit - 1) / nsplit;
+        per = (per + 3) / 4 * 4;
+        const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
+        const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
+        for (int c = threadIdx.x; c < SW; c += blockDim.x) {
+            double v = 0.0;
+            for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
+            if (c <= Kc) Sd[I.sdoff + (long)a * Kp + c] = v;
+            else if (c == Kc + 1) DD[I.ddoff + a] = v;
+            else DCS[I.ddoff + a] = v;
+        }
+        return;
+    }
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long KK = (long)Kp * Kp;
     if (e < KK) {
         const int i = (int)(e / Kp), j = (int)(e % Kp);
         if (i <= j) {
             double* G = Gpart + I.goff;
-            double sacc = G[e];
-            for (int q = 1; q < nparts; q++) sacc += G[(long)q * KK + e];
-            G[e] = sacc;
+            if (vg && (j > Kc)) {
+                G[e] = 0.0;  // padding
+            } else if (vg && i >= r0 && j < Kc) {
+                const double* C = TS + (long)I.self * 4 * VTRIG;
+                const double* Sn = C + VTRIG;
+                const int ha = (i - r0) / 2 + 1, sa = (i - r0) & 1;  // 0 sin, 1 cos
+                const int hb = (j - r0) / 2 + 1, sb = (j - r0) & 1;
+                const int dm = ha > hb ? ha - hb : hb - ha, sm = ha + hb;
+                const double sd = ha >= hb ? Sn[ha - hb] : -Sn[hb - ha];  // S_(a-b), signed
+                double v;
+                if (sa == 0 && sb == 0) v = 0.5 * (C[dm] - C[sm]);
+                else if (sa == 1 && sb == 1) v = 0.5 * (C[dm] + C[sm]);
+                else if (sa == 0) v = 0.5 * (Sn[sm] + sd);  // sin a cos b
+                else v = 0.5 * (Sn[sm] - sd);               // cos a sin b
+                G[e] = v;
+            } else {
+                double sacc = G[e];
+                for (int q = 1; q < nparts; q++) sacc += G[(long)q * KK + e];
+                G[e] = sacc;
+            }
         }
     }
     if (e < Kc) {
         double* cs = colsq + (I.coff + e) * nsplit;
-        double v = cs[0];
-        for (int q = 1; q < nsplit; q++) v += cs[q];
-        cs[0] = v;
+        if (vg && e >= r0) {  // Fourier column: sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2
+            const double* U = TS + (long)I.self * 4 * VTRIG + 2 * VTRIG;
+            const int h = (int)(e - r0) / 2 + 1;
+            cs[0] = 0.5 * (U[0] + (((e - r0) & 1) ? U[2 * h] : -U[2 * h]));
+        } else {
+            double v = cs[0];
+            for (int q = 1; q < nsplit; q++) v += cs[q];
+            cs[0] = v;
+        }
     }
 }
 
@@ -1486,12 +1869,59 @@ __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, c
     const pint_spec_t& S = *Pd.spec;
     const int n = I.n, R = 2 * S.nred;
     const double* ri = rtime + (I.roff - inst);
-    const double* Fb = M + I.moff + (long)(compact && Pd.dsplit ? Pd.red0c : S.ncol) * n;
     long per = (n + nsplit - 1) / nsplit;
     long i0 = split * per, i1 = i0 + per;
     if (i1 > n) i1 = n;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* out = wpart + ((long)inst * nsplit + split) * stride;
+    if (compact && Pd.dsplit && Pd.vg) {
+        // Fourier columns generated per row by rotations of the fundamental (k_redbase):
+        // wave w takes harmonics 8w .. 8w+7; wave 0 also accumulates r^T W r and 1^T W r
+        const int h0 = 8 * wave;
+        const bool act = h0 < S.nred;
+        double a[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) a[u] = 0.0;
+        double rr = 0.0, r1 = 0.0;
+        for (long i = i0 + lane; i < i1; i += 64) {
+            const double is = Pd.isig[i], r = ri[i], wr = is * is * r;
+            if (wave == 0) {
+                rr += wr * r;
+                r1 += wr;
+            }
+            if (act) {
+                const double c1 = Pd.red_cs[2 * i], s1 = Pd.red_cs[2 * i + 1];
+                double sn, cs;
+                cpow(c1, s1, h0 + 1, cs, sn);
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    a[2 * u] += sn * wr;
+                    a[2 * u + 1] += cs * wr;
+                    rot(cs, sn, c1, s1);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (h0 + u < S.nred) {
+                const double vs = wave_sum(a[2 * u]), vc = wave_sum(a[2 * u + 1]);
+                if (lane == 0) {
+                    out[2 * (h0 + u)] = vs;
+                    out[2 * (h0 + u) + 1] = vc;
+                }
+            }
+        }
+        if (wave == 0) {
+            rr = wave_sum(rr);
+            r1 = wave_sum(r1);
+            if (lane == 0) {
+                out[R] = rr;
+                out[R + 1] = r1;
+            }
+        }
+        return;
+    }
+    const double* Fb = M + I.moff + (long)(compact && Pd.dsplit ? Pd.red0c : S.ncol) * n;
     for (int j = wave; j < R + 2; j += 4) {
         const double* col = Fb + (long)(j < R ? j : 0) * n;
         double acc = 0.0;
@@ -1614,7 +2044,14 @@ struct pint_ctx {
     InstDev* d_inst = nullptr;
     InstDev* d_inst_sorted = nullptr;   // instances grouped by k_gram T (full layout)
     InstDev* d_inst_sorted_c = nullptr; // ... compact layout
-    std::vector<KpGroup> kp_groups, kp_groups_c;
+    InstDev* d_inst_sorted_v = nullptr; // ... compact layout, generated Fourier basis (k_gram_v)
+    std::vector<KpGroup> kp_groups, kp_groups_c, kp_groups_v;
+    int vgram = 1;       // PINT_OPT_VGRAM
+    int n_vg = 0;        // instances on the k_gram_v path
+    bool any_dmx_rows = false;  // compact instances still on k_dmx_rows / k_dmx
+    double *d_TSp = nullptr, *d_TS = nullptr;  // k_trig per-block trig sums, their totals
+    double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
+    hipEvent_t ev_start = nullptr, ev_trig = nullptr;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
@@ -1692,9 +2129,14 @@ pint_ctx* pint_ctx_create(int device) {
     hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
     hipEventCreateWithFlags(&ctx->ev_solved, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_copied, hipEventDisableTiming);
-    hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
+    // PINT_SERIAL=1 (profiling aid): side-stream kernels run on the main stream, so
+    // rocprof's per-kernel durations are not inflated by concurrent kernels
+    if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
+    else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_trig, hipEventDisableTiming);
     for (int i = 0; i < 12; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
     return ctx;
@@ -1711,7 +2153,8 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
-                   (void**)&ctx->d_inst_sorted_c};
+                   (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
+                   (void**)&ctx->d_TSp, (void**)&ctx->d_TS};
     for (auto p : ps) dfree(*p);
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
@@ -1734,7 +2177,7 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     if (ctx->ev_gram) hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_sigma) hipEventDestroy(ctx->ev_sigma);
-    if (ctx->sstream) hipStreamDestroy(ctx->sstream);
+    if (ctx->sstream && ctx->sstream != ctx->stream) hipStreamDestroy(ctx->sstream);
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1782,6 +2225,13 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
     rc |= upload(ctx, ph, red_freq, (size_t)spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
+    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * n, d.red_cs);
+    if (!rc && spec->nred > 0) {
+        hipLaunchKernelGGL(k_redbase, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, d.tdb_hi, d.tdb_lo, n,
+                           red_freq[0], (double*)d.red_cs);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
     {
         // compact fit layout: DMX columns out of M when there are enough of them and no TOA
         // lies in two free bins (bins do not overlap), ECORR checked in pint_set_ecorr
@@ -1944,6 +2394,43 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     ctx->nsplit = nsplit;
     ctx->red_valid[0] = ctx->red_valid[1] = 0;
+    // vg compact path (k_gram_v + k_trig): contiguous DMX bins, no ECORR, nred <= 31, <= 47
+    // timing columns; the DMX slots fill the [T | r] row tiles (+16 if needed) such that the
+    // bins of every N-split are distinct mod vns; LDS width <= VMAXKP
+    for (auto& ph : ctx->psrs) {
+        PsrDev& d = ph.dev;
+        d.vg = 0;
+        if (!(ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
+              d.red0c + 1 <= VMAXR0))
+            continue;
+        long per = (ph.n + nsplit - 1) / nsplit;
+        per = (per + 3) / 4 * 4;
+        const int wt = d.red0c + 1, R = d.Kd - d.red0c;
+        for (int ntr = (wt + 15) / 16; ntr <= (wt + 15) / 16 + 2; ntr++) {
+            const int ns = 16 * ntr - wt, kpv = (16 * ntr + R + 15) / 16 * 16;
+            if (ns < 1 || kpv > VMAXKP) continue;
+            bool ok = true;
+            for (int sp = 0; ok && sp < nsplit; sp++) {
+                const long i0 = sp * per, i1 = std::min<long>(i0 + per, ph.n);
+                std::vector<char> seen(ns, 0);
+                for (int a = 0; ok && a < d.ndc; a++) {
+                    if (ph.dhi[a] <= ph.dlo[a] || ph.dlo[a] >= i1 || ph.dhi[a] <= i0) continue;
+                    if (seen[a % ns]) ok = false;
+                    seen[a % ns] = 1;
+                }
+            }
+            if (ok) {
+                d.vg = 1;
+                d.vns = ns;
+                d.vkp = kpv;
+                break;
+            }
+        }
+    }
+    if (refresh_psrs(ctx)) return PINT_E_HIP;
+    long vgoff = 0;
+    ctx->n_vg = 0;
+    ctx->any_dmx_rows = false;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
         PsrHost& ph = ctx->psrs[p];
@@ -1964,6 +2451,13 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.ooff = out;
         I.sdoff = sdoff;
         I.ddoff = ddoff;
+        I.vgoff = vgoff;
+        if (ph.dev.vg) {
+            vgoff += (long)nsplit * ph.dev.vns * (ph.dev.Kd + 3);
+            ctx->n_vg++;
+        } else if (ph.dev.dsplit) {
+            ctx->any_dmx_rows = true;
+        }
         if (ph.dev.dsplit) {
             sdoff += (long)ph.dev.ndc * ph.dev.Kpd;
             ddoff += ph.dev.ndc;
@@ -2012,16 +2506,24 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->nblk = (int)bi.size();
     HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
-    for (int lay = 0; lay < 2; lay++) {  // k_gram launch groups: full and compact layouts
+    for (int lay = 0; lay < 3; lay++) {  // k_gram launch groups: full, compact, compact + vg
         std::vector<InstDev> sorted;
-        std::vector<KpGroup>& groups = lay ? ctx->kp_groups_c : ctx->kp_groups;
+        std::vector<KpGroup>& groups = lay == 0 ? ctx->kp_groups : (lay == 1 ? ctx->kp_groups_c : ctx->kp_groups_v);
         groups.clear();
         for (int T = 1; T <= GMAXT_ALL; T++) {
             KpGroup g{T, (int)sorted.size(), 0, 16};
             for (auto& I : ctx->inst) {
                 const PsrDev& pd = ctx->psrs[I.psr].dev;
-                const int kp = (lay && pd.dsplit) ? pd.Kpd : I.Kp;
-                int nt = kp / 16, tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
+                if (lay == 1 && pd.dsplit && pd.vg) continue;
+                if (lay == 2 && !(pd.dsplit && pd.vg)) continue;
+                const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
+                const int nt = kp / 16;
+                int ntl = nt * (nt + 1) / 2;
+                if (lay == 2) {
+                    const int ntr = (pd.red0c + 1 + pd.vns) / 16;
+                    ntl = ntr * nt - ntr * (ntr - 1) / 2;
+                }
+                const int tT = (ntl + GWAVES - 1) / GWAVES;
                 if (tT != T) continue;
                 sorted.push_back(I);
                 g.count++;
@@ -2029,10 +2531,14 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             }
             if (g.count) groups.push_back(g);
         }
-        InstDev*& dst = lay ? ctx->d_inst_sorted_c : ctx->d_inst_sorted;
-        HIPCHK(hipMalloc(&dst, sizeof(InstDev) * ninst));
-        HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+        InstDev*& dst = lay == 0 ? ctx->d_inst_sorted : (lay == 1 ? ctx->d_inst_sorted_c : ctx->d_inst_sorted_v);
+        HIPCHK(hipMalloc(&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
+        if (!sorted.empty())
+            HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * sorted.size(), hipMemcpyHostToDevice));
     }
+    HIPCHK(hipMalloc(&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
+    HIPCHK(hipMalloc(&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
+    HIPCHK(hipMalloc(&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
     HIPCHK(hipMalloc(&ctx->d_blk_inst, sizeof(int) * bi.size()));
     HIPCHK(hipMalloc(&ctx->d_blk_row0, sizeof(int) * br.size()));
     HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
@@ -2200,7 +2706,19 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
     }
     const int cmp = ctx->m_compact;
-    if (cmp && ctx->max_ndc > 0) {
+    const bool vgp = cmp && ctx->n_vg > 0;  // k_gram_v / k_trig path for the vg instances
+    if (vgp) {  // trig sums on the side stream, concurrent with k_gram_v
+        HIPCHK(hipEventRecord(ctx->ev_start, ctx->stream));
+        HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_start, 0));
+        hipLaunchKernelGGL(k_trig, dim3(4 * ctx->nsplit, ctx->ninst), dim3(256), 0, ctx->sstream, ctx->d_psrs,
+                           ctx->d_inst, ctx->nsplit, ctx->d_TSp);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->sstream, ctx->d_psrs, ctx->d_inst,
+                           ctx->nsplit, ctx->d_TSp, ctx->d_TS);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev_trig, ctx->sstream));
+    }
+    if (cmp && ctx->max_ndc > 0 && ctx->any_dmx_rows) {
         int maxKd = 0;
         bool any_gather = false;
         for (auto& I : ctx->inst) {
@@ -2249,12 +2767,30 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             }
         }
     }
+    if (vgp) {
+        for (const KpGroup& kg : ctx->kp_groups_v) {
+            const InstDev* di = ctx->d_inst_sorted_v + kg.first;
+            dim3 grid(ctx->nsplit, kg.count);
+            const size_t lds = sizeof(double) * (2 * (size_t)kg.maxKp * (VCH + 2) + 2 * VCH);
+#define PINT_GRAMV(TT)                                                                                           \
+            hipLaunchKernelGGL((k_gram_v<TT>), grid, dim3(GTHREADS), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,      \
+                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_colsq, ctx->d_Sdp)
+            if (kg.T == 1) PINT_GRAMV(1); else if (kg.T == 2) PINT_GRAMV(2); else PINT_GRAMV(3);
+#undef PINT_GRAMV
+        }
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_trig, 0));
+    }
     HIPCHK(hipGetLastError());
-    if (nparts > 1) {
+    if (nparts > 1 || vgp) {
         int maxKp = 16;
-        for (auto& I : ctx->inst) maxKp = I.Kp > maxKp ? I.Kp : maxKp;
-        hipLaunchKernelGGL(k_greduce, dim3((maxKp * maxKp + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream,
-                           ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, ctx->d_G, ctx->d_colsq);
+        for (auto& I : ctx->inst) {
+            const PsrDev& pd = ctx->psrs[I.psr].dev;
+            maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : I.Kp);
+        }
+        const int nbg = (maxKp * maxKp + 255) / 256;
+        hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? ctx->max_ndc : 0), ctx->ninst), dim3(256), 0, ctx->stream,
+                           ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
+                           ctx->d_Sdp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
@@ -2438,8 +2974,16 @@ int pint_set_lazy(pint_ctx* ctx, int lazy) {
 int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (!ctx) return PINT_E_INVALID;
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
     ctx->err = "unknown option";
     return PINT_E_INVALID;
+}
+
+int pint_query(pint_ctx* ctx, int key) {
+    if (!ctx) return -PINT_E_INVALID;
+    if (key == PINT_QUERY_NVGRAM) return ctx->n_vg;
+    ctx->err = "unknown query";
+    return -PINT_E_INVALID;
 }
 
 int pint_check(pint_ctx* ctx) {

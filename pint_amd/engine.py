@@ -453,6 +453,14 @@ class Session:
     def set_blocked_solve(self, on=True):
         self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))
 
+    def set_vgram(self, on=True):
+        """Generated-Fourier compact fit path (k_gram_v); applies from the next set_instances."""
+        self._check(self.L.pint_set_option(self.ctx, 2, 1 if on else 0))
+
+    def n_vgram(self):
+        """Instances of the current batch on the generated-Fourier compact path."""
+        return int(self.L.pint_query(self.ctx, 1))
+
     def check(self):
         self._check(self.L.pint_check(self.ctx))
 

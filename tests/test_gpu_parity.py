@@ -347,3 +347,55 @@ def test_compact_dmx_layout_matches_full(name):
     sc = np.sqrt(np.outer(np.diag(c2_), np.diag(c2_)))
     assert np.max(np.abs(c1 - c2_) / sc) < 1e-9
     assert abs(g1 / g2 - 1) < 1e-10
+
+
+def _fit_once_paths(items, vgram):
+    from pint_amd.engine import Session
+    from pint_amd.fitter import BatchFit
+    s = Session()
+    s.set_vgram(vgram)
+    bf = BatchFit([(copy.deepcopy(m), t) for m, t in items], mode="gls", session=s)
+    nvg = s.n_vgram()
+    s.eval(want_M=Session.FIT)
+    s.fit_step(1)
+    dp, er, cov, cl = s.read_step()
+    c2 = s.chi2_gls()
+    out = [(dp[k], er[k], cov[k], cl[k], c2[k]) for k in range(len(items))]
+    bf.close()
+    return nvg, out
+
+
+def _assert_same_fit(a, b, tol_step=1e-8, tol_err=1e-9, tol_chi2=1e-10):
+    (d1, e1, c1, l1, g1), (d2, e2, c2_, l2, g2) = a, b
+    n = len(e1) - 1
+    assert np.max(np.abs((d1[:n] - d2[:n]) / e2[:n])) < tol_step
+    assert np.max(np.abs(e1[:n] / e2[:n] - 1)) < tol_err
+    sc = np.sqrt(np.outer(np.diag(c2_), np.diag(c2_)))
+    assert np.max(np.abs(c1 - c2_) / sc) < tol_err
+    assert abs(l1 / l2 - 1) < tol_chi2
+    assert abs(g1 / g2 - 1) < tol_chi2
+
+
+@pytest.mark.parametrize("name", ["pta_dd", "pta_ell1", "pta_iso"])
+def test_generated_fourier_path_matches_stored(name):
+    """k_gram_v (Fourier columns generated in-kernel, F^T W F from trig sums, DMX bin sums
+    fused into the Gram) against the stored-basis compact path (k_gram + k_dmx_rows +
+    M-reading k_wdot): the same normal equations, so the step, errors, covariance and both
+    chi2 agree to rounding."""
+    model, toas, z, meta = load(name)
+    n1, (a,) = _fit_once_paths([(model, toas)], True)
+    n0, (b,) = _fit_once_paths([(model, toas)], False)
+    assert (n1, n0) == (1, 0)
+    _assert_same_fit(a, b)
+
+
+def test_generated_fourier_path_full_size():
+    """Bench-shaped pulsars (10k TOAs, 100 DMX bins, 30 red-noise modes; isolated, ELL1 and
+    DD) batched together: the k_gram_v path against the stored-basis path."""
+    from pint_amd import simulation as sim
+    items = sim.make_pta(npsr=3, ntoas=10000)
+    n1, a = _fit_once_paths(items, True)
+    n0, b = _fit_once_paths(items, False)
+    assert (n1, n0) == (3, 0)
+    for x, y in zip(a, b):
+        _assert_same_fit(x, y)
