@@ -662,8 +662,10 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
 // ---------------------------------------------------------------------------------
 constexpr int VTRIG = 64;   // trig sums per kind: C_m, S_m weighted, U_m, V_m unweighted (m < 64)   // trig sums m = 0..63 (nred <= 31)
 constexpr int VMAXR0 = 48;  // timing columns + residual staged from M (<= 3 row tiles)
-constexpr int VMAXKP = 144; // widest k_gram_v LDS tile [T | r | slots | F] (two buffers of 64 rows)
+constexpr int VMAXKP = 144; // widest k_gram_v LDS tile [T | r | slots | F] (9 column tiles)
 constexpr int VCH = 64;     // k_gram_v rows per chunk
+constexpr int VW = 4;       // k_gram_v waves per workgroup
+constexpr int VTG = 4;      // k_gram_v tiles per round of the cross-wave reduction
 
 // sin/cos of 2 pi frac(x) for a phase x in cycles (double-double argument reduction)
 __device__ __forceinline__ void dd_sincos_cyc(dd x, double* s, double* c) {
@@ -705,26 +707,37 @@ __device__ __forceinline__ int vg_cidx(int p, int r0, int Kd) {
     return p < r0 ? p : (p == r0 ? Kd : (p <= Kd ? p - 1 : p));
 }
 
-template <int T>
-__global__ __launch_bounds__(GTHREADS) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                     const double* __restrict__ M, const double* __restrict__ rtime,
-                                                     const double* __restrict__ dmxv, int nsplit,
-                                                     double* __restrict__ Gpart, double* __restrict__ colsq,
-                                                     double* __restrict__ Sdp) {
+// k_gram_v: one VW-wave workgroup per (N-split, instance).  Chunks of VCH = 64 rows are
+// staged in LDS as the whitened row block [T | r | DMX slots | F] (column-major, stride
+// VCH+2), one row per lane: wave w stages the timing columns w, w + VW, ... and generates
+// its share of the Fourier harmonics from the row's fundamental (k_redbase) by rotation;
+// wave 0 also stages the residual and the row's DMX slot entry (the slot block is zero
+// except one entry per row, so only the previous and the new entry of the row are
+// rewritten).  Each wave then takes 16 rows of the chunk
+// and accumulates ALL the tiles (row tiles < ntr x column tiles >= row tile) of its rows:
+// per 4-row k-step it reads NTR + nt operands and issues up to NT independent
+// v_mfma_f64_16x16x4f64.  The waves' partial tiles are summed through LDS at the end.
+template <int NTR, int NTC>
+__global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ M, const double* __restrict__ rtime,
+                                                    const double* __restrict__ dmxv, int nsplit,
+                                                    double* __restrict__ Gpart, double* __restrict__ Sdp) {
     extern __shared__ double lds[];
+    constexpr int NTH = VW * 64;
     constexpr int CH = VCH;
-    constexpr int CS = CH + 2;                   // column stride (= 2 mod 32 doubles)
-    constexpr int CG = GTHREADS / CH;            // staging threads per row
-    constexpr int QL = (VMAXR0 + CG - 1) / CG;   // timing columns loaded per thread
-    constexpr int QN = (VMAXKP + CG - 1) / CG;   // LDS columns stored per thread
+    constexpr int CS = CH + 2;  // column stride (= 2 mod 32 doubles)
+    constexpr int QL = (VMAXR0 + VW - 1) / VW;  // timing columns staged per lane (bound)
+    constexpr int NT = NTR * NTC - NTR * (NTR - 1) / 2;
+    constexpr int KS = CH / 4 / VW;  // k-steps per wave per chunk
     const InstDev I = insts[blockIdx.y];
     const int split = blockIdx.x;
     const PsrDev& Pd = psrs[I.psr];
     const int n = I.n, Kd = Pd.Kd, Kp = Pd.Kpd, r0 = Pd.red0c, NS = Pd.vns, Kpv = Pd.vkp;
+    const int nred = Pd.spec->nred;
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
-    const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD, DCS
-    double* Tb[2] = {lds, lds + Kpv * CS};  // double-buffered [Kpv][CS] whitened rows
-    double* Sg = lds + 2 * Kpv * CS;        // [2][CH] sigma
+    const int nt = Kpv / 16;                                          // <= NTC; ntr == NTR
+    const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
+    double* Ts = lds;       // [Kpv][CS] whitened rows
     long i0, i1;
     split_rows(n, nsplit, split, i0, i1);
     const double* Mi = M + I.moff;
@@ -732,162 +745,132 @@ __global__ __launch_bounds__(GTHREADS) void k_gram_v(const PsrDev* __restrict__ 
     const double* xv = dmxv + I.ooff;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nt = Kpv / 16, ntr = f0 / 16;
-    const int ntiles = ntr * nt - ntr * (ntr - 1) / 2;  // row tiles < ntr, upper part
-    const int t_lo = (ntiles * wave) / GWAVES, t_hi = (ntiles * (wave + 1)) / GWAVES;
-    const bool full = (t_hi - t_lo) == T;
-    int tI[T], tJ[T];
-    {
-        int ti = 0, rem = t_lo;
-        while (rem >= nt - ti) { rem -= nt - ti; ti++; }
-        int tj = ti + rem;
+    double4_t acc[NT];
 #pragma unroll
-        for (int t = 0; t < T; t++) {
-            tI[t] = ti;
-            tJ[t] = tj;
-            if (t + 2 < T || (t + 1 < T && full)) {
-                if (++tj == nt) { ti++; tj = ti; }
-            }
-        }
-    }
-    double4_t acc[T];
-#pragma unroll
-    for (int t = 0; t < T; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    // column sums of squares of the [T | r | slots] columns (the Fourier ones: k_trig)
-    const int ccol = tid % f0, cgrp = tid / f0, CG2 = GTHREADS / f0;
-    double csq = 0.0;
-    const int ii = tid % CH, cb = tid / CH;
-    // this thread's Fourier columns p = cb + CG q in [f0, Wv): all sines or all cosines (CG
-    // even), harmonics h1, h1 + CG/2, ...: e^{i h theta} of the row's fundamental
-    // (k_redbase) advanced by e^{i (CG/2) theta}
-    int qf = 0;
-    while (qf < QN && cb + CG * qf < f0) qf++;
-    const int pf = cb + CG * qf;
-    const bool fsin = ((pf - f0) & 1) == 0;
-    const int h1 = (pf - f0) / 2 + 1;
-    double st[QL];  // the next chunk's row ii, raw loads (consumed at its store)
-    double sg_n = 1.0, w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
+    for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
+    for (int k = tid; k < Kpv * CS; k += NTH) Ts[k] = 0.0;  // slot and padding columns stay 0
+    // Fourier harmonics of this wave
+    const int hper = (nred + VW - 1) / VW;
+    const int hb = wave * hper, he = std::min(nred, (wave + 1) * hper);
+    int slot_prev = -1;  // wave 0: the LDS slot column of this lane's previous row
+    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
+    double st[QL];
     int d_n = -1;
     bool ok_n = false;
     auto load = [&](long c0) {
-        long row = c0 + ii;
+        long row = c0 + lane;
         ok_n = row < i1;
         if (!ok_n) row = i1 - 1;
-        sg_n = Pd.sigma[row];
         w_n = Pd.isig[row];
-        r_n = ri[row];
-        x_n = xv[row];
-        d_n = Pd.drow[row];
-        if (pf < Wv) {
+        if (wave == 0) {
+            r_n = ri[row];
+            x_n = xv[row];
+            d_n = Pd.drow[row];
+        }
+        if (hb < he) {
             c1_n = Pd.red_cs[2 * row];
             s1_n = Pd.red_cs[2 * row + 1];
         }
 #pragma unroll
         for (int q = 0; q < QL; q++) {
-            const int p = cb + CG * q;
-            if (p < r0) st[q] = Mi[(long)p * n + row];
+            const int c = wave + VW * q;
+            if (c < r0) st[q] = Mi[(long)c * n + row];
         }
     };
-    auto store = [&](double* Ts, double* sg) {
-        const double iw = ok_n ? w_n : 0.0;
-        const int sl = d_n >= 0 ? s0 + d_n % NS : -1;  // LDS column of the row's DMX slot
-        double fc = 1.0, fs = 0.0, c4 = 1.0, s4 = 0.0;
-        if (pf < Wv) {
-            cpow(c1_n, s1_n, h1, fc, fs);
-            cpow(c1_n, s1_n, CG / 2, c4, s4);
-        }
+    if (i0 < i1) load(i0);
+    for (long c0 = i0; c0 < i1; c0 += CH) {
+        __syncthreads();  // the previous chunk's MFMAs are done with the LDS tile
+        {
+            const double iw = ok_n ? w_n : 0.0;
 #pragma unroll
-        for (int q = 0; q < QN; q++) {
-            const int p = cb + CG * q;
-            if (p < Kpv) {
-                double v;
-                if (q < QL && p < r0) v = st[q < QL ? q : 0];
-                else if (p == r0) v = r_n;
-                else if (p < f0) v = p == sl ? x_n : 0.0;
-                else if (p < Wv) {
-                    v = fsin ? fs : fc;
-                    rot(fc, fs, c4, s4);
-                } else v = 0.0;
-                Ts[p * CS + ii] = v * iw;
+            for (int q = 0; q < QL; q++) {
+                const int c = wave + VW * q;
+                if (c < r0) Ts[c * CS + lane] = st[q] * iw;
             }
-        }
-        if (cb == 0) sg[ii] = sg_n;
-    };
-    const long nch = (i1 - i0 + CH - 1) / CH;
-    if (nch > 0) {
-        load(i0);
-        store(Tb[0], Sg);
-        if (nch > 1) load(i0 + CH);
-    }
-    __syncthreads();
-    for (long k = 0; k < nch; k++) {
-        double* Ts = Tb[k & 1];
-        const double* sg = Sg + (k & 1) * CH;
-        // stage chunk k+1 into the other buffer (its last readers finished before the
-        // barrier that ended iteration k-1), then prefetch chunk k+2
-        if (k + 1 < nch) {
-            store(Tb[(k + 1) & 1], Sg + ((k + 1) & 1) * CH);
-            if (k + 2 < nch) load(i0 + (k + 2) * CH);
-        }
-        const long c0 = i0 + k * CH;
-        const int nr = (i1 - c0 < CH) ? (int)(i1 - c0) : CH;
-        if (cgrp < CG2) {
-            for (int r = cgrp; r < nr; r += CG2) {
-                const double u = Ts[ccol * CS + r] * sg[r];
-                csq += u * u;
+            if (wave == 0) {
+                Ts[r0 * CS + lane] = r_n * iw;
+                const int sl = (ok_n && d_n >= 0) ? d_n % NS : -1;
+                if (slot_prev >= 0) Ts[(s0 + slot_prev) * CS + lane] = 0.0;
+                if (sl >= 0) Ts[(s0 + sl) * CS + lane] = x_n * iw;
+                slot_prev = sl;
             }
-        }
-#pragma unroll
-        for (int kk = 0; kk < CH / 4; kk++) {
-            const double* Tr = Ts + (lane & 15) * CS + kk * 4 + (lane >> 4);
-            double a[T], b[T];
-#pragma unroll
-            for (int t = 0; t < T; t++) {
-                a[t] = Tr[tI[t] * 16 * CS];
-                b[t] = Tr[tJ[t] * 16 * CS];
+            if (hb < he) {
+                double c, s;
+                cpow(c1_n, s1_n, hb + 1, c, s);
+                double* dst = Ts + (f0 + 2 * hb) * CS + lane;
+                for (int h = hb; h < he; h++, dst += 2 * CS) {
+                    dst[0] = s * iw;
+                    dst[CS] = c * iw;
+                    rot(c, s, c1_n, s1_n);
+                }
             }
-#pragma unroll
-            for (int t = 0; t < T - 1; t++) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
-            if (full) acc[T - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T - 1], b[T - 1], acc[T - 1], 0, 0, 0);
         }
         __syncthreads();
-    }
-    // partial tiles (upper triangle in LDS order): [T|r] x [T|r|F] -> the Gram partial at
-    // (min, max) of the compact columns; slot rows/columns -> this split's DMX partials
-    double* G = Gpart + I.goff + (long)split * Kp * Kp;
-    double* Sp = Sdp + I.vgoff + (long)split * NS * SW;
-    auto cidx = [&](int p) { return p < r0 ? p : (p == r0 ? Kd : r0 + (p - f0)); };
+        if (c0 + CH < i1) load(c0 + CH);  // prefetch the next chunk (overlaps the MFMAs)
 #pragma unroll
-    for (int t = 0; t < T; t++) {
-        if (t < T - 1 || full) {
+        for (int ks = 0; ks < KS; ks++) {
+            const double* Tr = Ts + (lane & 15) * CS + (wave * KS + ks) * 4 + (lane >> 4);
+            double a[NTR], b[NTC];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int pr = tI[t] * 16 + (lane >> 4) + 4 * q;
-                const int pc = tJ[t] * 16 + (lane & 15);
-                const double v = acc[t][q];
-                if (pr > pc || pc >= Wv) continue;
-                const bool rs = pr >= s0, cs = pc >= s0 && pc < f0;  // slot row / slot column
-                if (!rs && !cs) {
-                    int a = cidx(pr), b = cidx(pc);
-                    if (a > b) { const int x = a; a = b; b = x; }
-                    G[(long)a * Kp + b] = v;
-                } else if (!rs) {
-                    Sp[(long)(pc - s0) * SW + cidx(pr)] = v;            // DMX x [T|r]
-                } else if (cs) {
-                    if (pr == pc) Sp[(long)(pr - s0) * SW + Kd + 1] = v;  // DD
-                } else {
-                    Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F
+            for (int t = 0; t < NTR; t++) a[t] = Tr[t * 16 * CS];
+#pragma unroll
+            for (int t = 0; t < NTC; t++) b[t] = t < nt ? Tr[t * 16 * CS] : 0.0;
+            int k = 0;
+#pragma unroll
+            for (int ti = 0; ti < NTR; ti++) {
+#pragma unroll
+                for (int tj = ti; tj < NTC; tj++, k++) {
+                    if (tj < nt) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
                 }
             }
         }
     }
-    if (cgrp < CG2) lds[cgrp * f0 + ccol] = csq;  // the last barrier freed the LDS tiles
-    __syncthreads();
-    if (tid < f0 && tid != r0) {
-        double v = 0.0;
-        for (int g = 0; g < CG2; g++) v += lds[g * f0 + tid];
-        if (tid >= s0) Sp[(long)(tid - s0) * SW + Kd + 2] = v;  // DCS
-        else colsq[(I.coff + tid) * nsplit + split] = v;
+    // sum the waves' partial tiles through LDS, TG tiles at a time, and store them:
+    // [T|r] x [T|r|F] -> the Gram partial at (min, max) of the compact columns; slot rows /
+    // columns -> this split's DMX partials
+    double* G = Gpart + I.goff + (long)split * Kp * Kp;
+    double* Sp = Sdp + I.vgoff + (long)split * NS * SW;
+    auto cidx = [&](int p) { return p < r0 ? p : (p == r0 ? Kd : r0 + (p - f0)); };
+    constexpr int TG = NT < VTG ? NT : VTG;
+    double* red = lds;  // [VW][TG][256] (the host sizes LDS for it)
+    int k = 0;
+#pragma unroll
+    for (int ti = 0; ti < NTR; ti++) {
+#pragma unroll
+        for (int tj = ti; tj < NTC; tj++, k++) {
+            const int g = k % TG;
+            if (g == 0) __syncthreads();  // the previous group's (or the MFMAs') readers are done
+#pragma unroll
+            for (int q = 0; q < 4; q++) red[((wave * TG + g) * 4 + q) * 64 + lane] = acc[k][q];
+            if (g == TG - 1 || k == NT - 1) {
+                __syncthreads();
+                const int kbase = k - g;
+                for (int e = tid; e < (g + 1) * 256; e += NTH) {
+                    const int gg = e >> 8, q = (e >> 6) & 3, ln = e & 63;
+                    double v = 0.0;
+#pragma unroll
+                    for (int w = 0; w < VW; w++) v += red[((w * TG + gg) * 4 + q) * 64 + ln];
+                    int tt = kbase + gg, r_ = 0;  // tile (r_, r_ + tt) of the row-major list
+                    while (tt >= NTC - r_) { tt -= NTC - r_; r_++; }
+                    const int tJ_ = r_ + tt;
+                    if (tJ_ >= nt) continue;
+                    const int pr = r_ * 16 + (ln >> 4) + 4 * q, pc = tJ_ * 16 + (ln & 15);
+                    if (pr > pc || pc >= Wv) continue;
+                    const bool rs = pr >= s0, cs = pc >= s0 && pc < f0;
+                    if (!rs && !cs) {
+                        int a_ = cidx(pr), b_ = cidx(pc);
+                        if (a_ > b_) { const int x_ = a_; a_ = b_; b_ = x_; }
+                        G[(long)a_ * Kp + b_] = v;
+                    } else if (!rs) {
+                        Sp[(long)(pc - s0) * SW + cidx(pr)] = v;            // DMX x [T|r]
+                    } else if (cs) {
+                        if (pr == pc) Sp[(long)(pr - s0) * SW + Kd + 1] = v;  // DD
+                    } else {
+                        Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -910,14 +893,34 @@ __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __res
 // N-split, half of the m range): wave w accumulates m = 8(4 half + w) .. +7 over the
 // split's rows (harmonics by rotation of the per-TOA fundamental, k_redbase), one partial
 // per block -> TSp (summed by k_tsum).  Runs on the side stream, concurrent with k_gram_v
-// (one wave per SIMD, so it co-resides with k_gram_v's workgroups).
+// (one wave per SIMD, so it co-resides with k_gram_v's workgroups).  Blocks past 4 nsplit:
+// the unweighted sums of squares of the timing columns per N-split (normalize_designmatrix).
 __global__ __launch_bounds__(256) void k_trig(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                              int nsplit, double* __restrict__ TSp) {
+                                              int nsplit, const double* __restrict__ M, double* __restrict__ TSp,
+                                              double* __restrict__ colsq) {
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     if (!Pd.vg) return;
-    const int x = blockIdx.x % (2 * nsplit), kind = blockIdx.x / (2 * nsplit), nred = Pd.spec->nred;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if ((int)blockIdx.x >= 4 * nsplit) {  // unweighted sums of squares of the timing columns
+        const int sp = blockIdx.x - 4 * nsplit;
+        long i0, i1;
+        split_rows(I.n, nsplit, sp, i0, i1);
+        for (int c = wave; c < Pd.red0c; c += 4) {
+            const double* col = M + I.moff + (long)c * I.n;
+            double a0 = 0.0, a1 = 0.0;
+            long i = i0 + lane;
+            for (; i + 64 < i1; i += 128) {
+                a0 += col[i] * col[i];
+                a1 += col[i + 64] * col[i + 64];
+            }
+            if (i < i1) a0 += col[i] * col[i];
+            const double v = wave_sum(a0 + a1);
+            if (lane == 0) colsq[(I.coff + c) * nsplit + sp] = v;
+        }
+        return;
+    }
+    const int x = blockIdx.x % (2 * nsplit), kind = blockIdx.x / (2 * nsplit), nred = Pd.spec->nred;
     const int m0 = 8 * (4 * (x & 1) + wave);
     if (nred <= 0 || m0 > 2 * nred) return;
     long i0, i1;
@@ -979,8 +982,9 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
                                                  int nsplit, int nparts, int compact, int nbg,
                                                  double* __restrict__ Gpart, double* __restrict__ colsq,
                                                  const double* __restrict__ TS, const double* __restrict__ Sdp,
-                                                 double* __restrict__ Sd, double* __restrict__ DD,
-                                                 double* __restrict__ DCS) {
+                                                 const double* __restrict__ dmxv, double* __restrict__ Sd,
+                                                 double* __restrict__ DD, double* __restrict__ DCS) {
+    __shared__ double sh[8];
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const bool cmp = compact && Pd.dsplit;
@@ -997,13 +1001,19 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         per = (per + 3) / 4 * 4;
         const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
         const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
-        for (int c = threadIdx.x; c < SW; c += blockDim.x) {
+        for (int c = threadIdx.x; c <= Kc + 1; c += blockDim.x) {
             double v = 0.0;
             for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
             if (c <= Kc) Sd[I.sdoff + (long)a * Kp + c] = v;
-            else if (c == Kc + 1) DD[I.ddoff + a] = v;
-            else DCS[I.ddoff + a] = v;
+            else DD[I.ddoff + a] = v;
         }
+        double q2 = 0.0;  // DCS = sum x^2 over the bin
+        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            const double xx = dmxv[I.ooff + i];
+            q2 += xx * xx;
+        }
+        q2 = block_sum<4>(q2, sh);
+        if (threadIdx.x == 0) DCS[I.ddoff + a] = q2;
         return;
     }
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2518,12 +2528,11 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 if (lay == 2 && !(pd.dsplit && pd.vg)) continue;
                 const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
                 const int nt = kp / 16;
-                int ntl = nt * (nt + 1) / 2;
-                if (lay == 2) {
+                int tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
+                if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column-tile bound (6 | 9)
                     const int ntr = (pd.red0c + 1 + pd.vns) / 16;
-                    ntl = ntr * nt - ntr * (ntr - 1) / 2;
+                    tT = 2 * (ntr - 1) + (nt <= 6 ? 1 : 2);
                 }
-                const int tT = (ntl + GWAVES - 1) / GWAVES;
                 if (tT != T) continue;
                 sorted.push_back(I);
                 g.count++;
@@ -2535,6 +2544,13 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         HIPCHK(hipMalloc(&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
         if (!sorted.empty())
             HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * sorted.size(), hipMemcpyHostToDevice));
+    }
+    if (getenv("PINT_VERBOSE")) {
+        for (auto& g : ctx->kp_groups_v) fprintf(stderr, "[pint] k_gram_v group key %d: %d instances, max width %d\n", g.T, g.count, g.maxKp);
+        for (size_t k = 0; k < ctx->psrs.size() && k < 4; k++) {
+            const PsrDev& d = ctx->psrs[k].dev;
+            fprintf(stderr, "[pint] psr %zu: vg %d r0 %d Kd %d ns %d kpv %d ndc %d nsplit %d\n", k, d.vg, d.red0c, d.Kd, d.vns, d.vkp, d.ndc, nsplit);
+        }
     }
     HIPCHK(hipMalloc(&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
     HIPCHK(hipMalloc(&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
@@ -2710,8 +2726,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (vgp) {  // trig sums on the side stream, concurrent with k_gram_v
         HIPCHK(hipEventRecord(ctx->ev_start, ctx->stream));
         HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_start, 0));
-        hipLaunchKernelGGL(k_trig, dim3(4 * ctx->nsplit, ctx->ninst), dim3(256), 0, ctx->sstream, ctx->d_psrs,
-                           ctx->d_inst, ctx->nsplit, ctx->d_TSp);
+        hipLaunchKernelGGL(k_trig, dim3(5 * ctx->nsplit, ctx->ninst), dim3(256), 0, ctx->sstream, ctx->d_psrs,
+                           ctx->d_inst, ctx->nsplit, ctx->d_M, ctx->d_TSp, ctx->d_colsq);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->sstream, ctx->d_psrs, ctx->d_inst,
                            ctx->nsplit, ctx->d_TSp, ctx->d_TS);
@@ -2771,11 +2787,18 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         for (const KpGroup& kg : ctx->kp_groups_v) {
             const InstDev* di = ctx->d_inst_sorted_v + kg.first;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * (2 * (size_t)kg.maxKp * (VCH + 2) + 2 * VCH);
-#define PINT_GRAMV(TT)                                                                                           \
-            hipLaunchKernelGGL((k_gram_v<TT>), grid, dim3(GTHREADS), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,      \
-                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_colsq, ctx->d_Sdp)
-            if (kg.T == 1) PINT_GRAMV(1); else if (kg.T == 2) PINT_GRAMV(2); else PINT_GRAMV(3);
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)kg.maxKp * (VCH + 2) + VCH, VW * VTG * 256);
+#define PINT_GRAMV(R_, C_)                                                                                       \
+            hipLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,   \
+                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp)
+            switch (kg.T) {
+                case 1: PINT_GRAMV(1, 6); break;
+                case 2: PINT_GRAMV(1, 9); break;
+                case 3: PINT_GRAMV(2, 6); break;
+                case 4: PINT_GRAMV(2, 9); break;
+                case 5: PINT_GRAMV(3, 6); break;
+                default: PINT_GRAMV(3, 9); break;
+            }
 #undef PINT_GRAMV
         }
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_trig, 0));
@@ -2790,7 +2813,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         const int nbg = (maxKp * maxKp + 255) / 256;
         hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? ctx->max_ndc : 0), ctx->ninst), dim3(256), 0, ctx->stream,
                            ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
-                           ctx->d_Sdp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+                           ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
         HIPCHK(hipGetLastError());
     }
     record(ctx, 7);
