@@ -1,13 +1,13 @@
 """Benchmark: GLS fits/s on the synthetic 68-pulsar x 10k-TOA PTA (BASELINE.json metric),
 plus chi2-grid points/s, on N MI355X GPUs of one node.
 
-One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar of the
-PTA, batched in one launch sequence per GPU: design matrix + residuals (k_eval/k_resid),
-Gram on FP64 MFMA (k_gram), Cholesky/solve/covariance (k_solve), double-double parameter
-update (k_apply), post-fit residuals and Woodbury chi2 (k_woodbury), with the fit outputs
-(steps, errors, covariances, chi2) copied back to the host.  Pulsars are sharded over
-ranks (no data-path collective; strong scaling of the fixed 68-pulsar PTA); each rank
-reports its time, the max over ranks is the step time.
+One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar of a
+68-pulsar PTA, batched in one launch sequence per GPU: design matrix + residuals
+(k_eval/k_resid), Gram on FP64 MFMA (k_gram_v, + trig sums k_trig), Cholesky/solve/
+covariance (k_solve_dmx), double-double parameter update (k_apply), post-fit residuals and
+Woodbury chi2 (k_wdot/k_wsolve), with the fit outputs (steps, errors, covariances, chi2)
+copied back to the host (on a copy stream, overlapped with the kernels).  Weak scaling: rank r fits its own 68-pulsar PTA (pulsar seeds 68r .. 68r+67),
+no data-path collective; the max over ranks is the step time and value = 68 x N / step.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -61,8 +61,8 @@ def main():
     from pint_amd.engine import Session, build_layout, pack_table
     from pint_amd.simulation import make_pta
 
-    # ---- workload: this rank's shard of the PTA (pulsar i uses seed i) ----
-    mine = [i for i in range(args.npsr) if i % world == rank]
+    # ---- workload: this rank's own PTA (weak scaling; pulsar i uses seed i) ----
+    mine = list(range(rank * args.npsr, (rank + 1) * args.npsr))
     t0 = time.time()
     from pint_amd import simulation as sim
     from pint_amd.timing_model import get_model
@@ -90,21 +90,22 @@ def main():
         s.set_tables(flat0)
         s.eval(want_M=Session.FIT)
         s.fit_step(1)
-        s.read_step()          # steps, errors, timing covariance -> host (fit outputs)
+        out = s.read_step()    # steps, errors, timing covariance -> host (fit outputs)
         s.apply_step(ones)
         s.eval(want_M=False)
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
-        s.check()              # device status + HIP-event kernel timings
-        return s.timing(), c2
+        return out, c2
 
     for _ in range(args.warmup):
         step()
+        s.check()
     barrier()
     t0 = time.perf_counter()
-    kt = np.zeros(6)
+    kt = np.zeros(8)
     for _ in range(args.steps):
-        ms1, c2 = step()
-        kt += ms1
+        step()
+        s.check()              # device status + HIP-event kernel timings
+        kt += s.timing()
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -114,43 +115,47 @@ def main():
         dt = float(tt.item())
     kt /= args.steps
     ms_step = dt / args.steps * 1e3
-    fits_per_s = args.npsr / (dt / args.steps)
+    fits_per_s = args.npsr * world / (dt / args.steps)
 
-    # ---- roofline: algorithmic work per launch (DESIGN.md "Kernels") / HIP-event time ----
+    # ---- roofline: work per launch / HIP-event time of that kernel ----
     K = np.array([l.K for l in lays])                # timing + red-noise columns
     P = np.array([len(l.columns) for l in lays])     # timing columns
-    N = np.array([l.n for l in lays])
+    N = np.array([l.n for l in lays]).astype(float)
     R = K - P
-    # the Gram is formed in the fit layout: dense columns on MFMA (symmetric half), the sparse
-    # DMX columns as bin sums (one (Kd+1)-row multiply-add per TOA)
-    fl = [s.fit_layout(l) for l in lays]
-    Kd = np.array([f[1] for f in fl])
-    ndc = np.array([f[2] for f in fl])
+    vl = [s.vgram_layout(l) for l in lays]
+    # k_gram_v: MFMA tiles [T|r|DMX slots] x [T|r|slots|F] of 16x16 + the two trig tiles,
+    # 2048 flops per tile per 4 rows
+    tiles = []
+    for vg, ns, kpv, r0 in vl:
+        ntr, nt = (r0 + 1 + ns) // 16, kpv // 16
+        tiles.append(ntr * nt - ntr * (ntr - 1) // 2 + 2 if vg else 0)
+    tiles = np.array(tiles, dtype=float)
     flops = {
-        "k_gram": float(np.sum(N * (Kd + 1) * (Kd + 2) + np.where(ndc > 0, 2 * N * (Kd + 2), 0))),
-        "k_solve": float(np.sum(K.astype(float) ** 3)),          # chol K^3/3 + inverse/cov 2K^3/3
-        "k_woodbury": float(np.sum(2 * N * (R + 2))),            # F^T W r, r^T W r, 1^T W r
+        "k_gram": float(np.sum(tiles * N * 512.0)),           # FP64 MFMA flops executed
+        "k_solve": float(np.sum(K.astype(float) ** 3)),       # chol K^3/3 + inverse/cov 2K^3/3
     }
+    # the full GLS Gram the reference forms (2 N K^2, SURVEY.md 8(d) F_gram) for reference
+    gram_equiv = float(np.sum(2.0 * N * (K + 1.0) ** 2))
     nbytes = {
-        "k_eval_M": float(np.sum(N * (120 + 8 * P))),            # SURVEY.md §8(d) B_dm
-        "k_eval": float(np.sum(N * (120 + 8))),                  # B_res
-        "k_resid": float(np.sum(N * (8 * 4 + 8 * 2))),          # phase hi/lo, ftaylor, sigma in; resid out
+        "k_eval_M": float(np.sum(N * (120 + 8 * P))),          # SURVEY.md 8(d) B_dm
+        "k_eval": float(np.sum(N * (120 + 8))),                # B_res
+        "k_resid": float(np.sum(N * (8 * 4 + 8 * 2))),        # phase hi/lo, ftaylor, sigma in; resid out
+        "k_woodbury": float(np.sum(N * (8 * 4))),              # r, sigma, fundamental (cos, sin) in
     }
-    names = ["k_eval", "k_resid", "k_gram", "k_solve", "k_eval_M", "k_woodbury"]
+    names = ["k_eval", "k_resid", "gram_span", "k_solve", "k_eval_M", "k_woodbury", "k_gram", "k_greduce"]
     kms = {n: float(v) for n, v in zip(names, kt)}
-    dom = max(kms, key=kms.get)
+    dom = max((n for n in names if n not in ("gram_span", "k_greduce")), key=lambda n: kms[n])
     peaks = load_peaks()
-    if dom in flops and dom != "k_woodbury":
+    if dom in flops:
         ach = flops[dom] / (kms[dom] * 1e-3) / 1e12
         pk = MI355X_FP64_MFMA_PEAK_TFLOPS
-        roof = {"kernel": dom, "bound": "mfma" if dom == "k_gram" else "fp64", "achieved": round(ach, 3),
-                "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4)}
+        roof = {"kernel": "k_gram_v" if dom == "k_gram" else dom, "bound": "mfma" if dom == "k_gram" else "fp64",
+                "achieved": round(ach, 3), "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4)}
     else:
-        b = nbytes.get(dom, flops.get(dom, 0.0) * 4)
-        ach = b / (kms[dom] * 1e-3) / 1e9
+        ach = nbytes[dom] / (kms[dom] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4)}
-    roof["traffic"] = pmc_traffic(dom, args)
+    roof["traffic"] = pmc_traffic(roof["kernel"], args)
     roof["kernel_ms"] = {n: round(v, 4) for n, v in kms.items()}
     roof["per_kernel"] = {}
     for n in names:
@@ -160,6 +165,8 @@ def main():
             roof["per_kernel"][n] = {"TFLOP/s": round(flops[n] / (kms[n] * 1e-3) / 1e12, 3)}
         if n in nbytes:
             roof["per_kernel"][n] = {"GB/s": round(nbytes[n] / (kms[n] * 1e-3) / 1e9, 1)}
+    if kms["k_gram"] > 0:
+        roof["gram_full_equiv_tflops"] = round(gram_equiv / (kms["k_gram"] * 1e-3) / 1e12, 2)
     if peaks:
         roof["measured_peaks"] = peaks
 
@@ -175,11 +182,12 @@ def main():
     if rank == 0:
         out = {"metric": "GLS fits/sec, 68-PSR x 10k-TOA synthetic PTA (whole node)", "value": round(fits_per_s, 3),
                "unit": "fits/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong",
+               "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "f64+dd", "data": "synthetic (make_fake_toas-style, GPU-zeroed)",
-               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1",
-                          "npsr": args.npsr, "ntoas": args.ntoas, "K_cols_max": int(K.max() - 1),
-                          "parallelism": f"pulsar-sharded x{world}"},
+               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1 per GPU",
+                          "npsr": args.npsr, "npsr_total": args.npsr * world, "ntoas": args.ntoas,
+                          "K_cols_max": int(K.max() - 1),
+                          "parallelism": f"one PTA per GPU x{world} (weak)"},
                "roofline": roof, "grid": grid, "cpu_baseline": cpu}
         print(json.dumps(out))
     s.close()

@@ -169,6 +169,9 @@ int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const
  * columns, no TOA in two free bins, no ECORR): pint_eval(ctx, 2) then writes the compact
  * design matrix, and pint_fit_step forms their Gram rows as bin sums. */
 int pint_fit_layout(pint_ctx *ctx, int psr, int32_t *out4);
+/* The k_gram_v layout of a pulsar in the current batch: (on the vg path, DMX slots, LDS
+ * width [T | r | slots | F] padded to 16, timing columns of the compact layout). */
+int pint_vgram_layout(pint_ctx *ctx, int psr, int32_t *out4);
 
 /* Lazy mode (1): launches return without synchronising or checking the device status;
  * pint_check() synchronises and returns the accumulated status.  In lazy mode
@@ -187,6 +190,15 @@ int pint_check(pint_ctx *ctx);
 #define PINT_OPT_BLOCKED_SOLVE 1
 #define PINT_OPT_VGRAM 2
 int pint_set_option(pint_ctx *ctx, int key, int value);
+/* HIP-graph capture of a launch sequence (lazy mode only).  Everything the calls between
+ * pint_capture_begin and pint_capture_end enqueue (kernels, the copies to and from the
+ * caller's pinned buffers, the side-stream work) becomes one graph; pint_graph_launch
+ * replays it with one launch.  Device buffers and host pointers are fixed at capture, so a
+ * replay re-runs the same batch on whatever those buffers hold (e.g. new parameter tables
+ * written into the same pinned buffer).  pint_set_instances discards the graph. */
+int pint_capture_begin(pint_ctx *ctx);
+int pint_capture_end(pint_ctx *ctx);
+int pint_graph_launch(pint_ctx *ctx);
 /* Introspection: PINT_QUERY_NVGRAM = 1 returns the number of instances of the current batch
  * on the generated-Fourier path; negative status on error. */
 #define PINT_QUERY_NVGRAM 1
@@ -198,10 +210,11 @@ void pint_host_free(void *p);
  * (L^-1, packed lower). */
 int pint_debug_read(pint_ctx *ctx, int which, double *out);
 
-/* Device time (ms, HIP events on the library's stream) of the last launches, 6 values:
- * [0] eval (no design matrix), [1] resid, [2] ecorr+gram, [3] solve, [4] eval with design
- * matrix, [5] Woodbury chi2. */
-int pint_last_timing(pint_ctx *ctx, double *ms6);
+/* Device time (ms, HIP events on the streams the kernels run on) of the last launches, 8
+ * values: [0] eval (no design matrix), [1] resid, [2] ecorr + Gram + partial reduction,
+ * [3] solve, [4] eval with design matrix, [5] Woodbury chi2, [6] the Gram kernels alone
+ * (k_gram / k_gram_v), [7] the Gram partial reduction (k_greduce). */
+int pint_last_timing(pint_ctx *ctx, double *ms8);
 int pint_sync(pint_ctx *ctx);
 
 #ifdef __cplusplus

@@ -55,7 +55,7 @@ struct PsrDev {
     int K;   // ncol + 2*nred
     int Kp;  // padded K+1 (residual column) to 16
     int nep; // ECORR epochs (eliminated by Schur complement)
-    int vg;  // compact fit layout on the k_gram_v path (DMX slots as MFMA rows, F^T W F from k_trig)
+    int vg;  // compact fit layout on the k_gram_v path (DMX slots as MFMA rows, F^T W F from trig sums)
     int vns; // k_gram_v DMX slots (bins of an N-split are distinct mod vns)
     int vkp; // k_gram_v LDS width: [T | r | slots | F] padded to 16
     int pad_;
@@ -646,19 +646,22 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
 }
 
 // ---------------------------------------------------------------------------------
-// Compact fit layout, "vg" path (PsrDev::vg, PINT_OPT_VGRAM).
+// Compact fit layout, "vg" path (PsrDev::vg, PINT_OPT_VGRAM), one fused kernel k_gram_v.
 // The PLRedNoise basis (noise_model.py:861-880, frequencies :847-858) is a harmonic
 // series: F[:,2h] = sin((h+1) theta_i), F[:,2h+1] = cos((h+1) theta_i), theta_i =
 // 2 pi t_i f_1, t = tdbld * 86400 s, f_k = k f_1.  Hence
+//  - F is generated in the kernel by rotations of the per-TOA fundamental (k_redbase),
+//    never stored in M;
 //  - its Gram block F^T W F follows from the weighted trig sums C_m = sum_i w_i cos(m
 //    theta_i), S_m = sum_i w_i sin(m theta_i), m <= 2 nred, by the product-to-sum
-//    identities (k_trig, k_tsum, k_greduce): O(N nred) VALU work instead of O(N nred^2)
-//    MFMA work; harmonics are rotations of the per-TOA fundamental (k_redbase);
-//  - k_gram_v runs the MFMA tiles of the rows [T | r] (compact timing columns and the
-//    residual) against every column [T | r | F] of M: ~ (P+1)/(P+R+1) of the full Gram;
-//  - the DMX bin rows (bins are contiguous row ranges) are per-bin sums over the bin's
-//    rows of the timing columns and of the generated Fourier columns (k_trig), replacing
-//    k_dmx_rows' pass over the whole of M.
+//    identities (k_greduce), and every C_m, S_m (m < 64) is one 16x16 MFMA tile A^T B of
+//    A = [cos a theta | sin a theta], B = [cos 8b theta | sin 8b theta] (a, b < 8), since
+//    e^{i(a + 8b) theta} = e^{i a theta} e^{i 8b theta}: O(N) MFMA work instead of the
+//    O(N nred^2) of F^T W F;
+//  - the MFMA row tiles are [T | r | DMX slots] (compact timing columns, residual, and the
+//    DMX bins of the N-split in bin % vns slots: bins are contiguous row ranges, so each
+//    slot holds one bin per split) against every column [T | r | slots | F]: the DMX bin
+//    rows of the normal matrix come out of the same tiles.
 // ---------------------------------------------------------------------------------
 constexpr int VTRIG = 64;   // trig sums per kind: C_m, S_m weighted, U_m, V_m unweighted (m < 64)   // trig sums m = 0..63 (nred <= 31)
 constexpr int VMAXR0 = 48;  // timing columns + residual staged from M (<= 3 row tiles)
@@ -721,7 +724,8 @@ template <int NTR, int NTC>
 __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                     const double* __restrict__ M, const double* __restrict__ rtime,
                                                     const double* __restrict__ dmxv, int nsplit,
-                                                    double* __restrict__ Gpart, double* __restrict__ Sdp) {
+                                                    double* __restrict__ Gpart, double* __restrict__ Sdp,
+                                                    double* __restrict__ colsq, double* __restrict__ TSp) {
     extern __shared__ double lds[];
     constexpr int NTH = VW * 64;
     constexpr int CH = VCH;
@@ -737,7 +741,12 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
     const int nt = Kpv / 16;                                          // <= NTC; ntr == NTR
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
-    double* Ts = lds;       // [Kpv][CS] whitened rows
+    // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), A2 = the same times
+    // sigma (unweighted after the whitening), B = [cos 8b theta | sin 8b theta]/sigma (b < 8):
+    // the tiles A^T B and A2^T B hold every C_m, S_m (weighted) and U_m, V_m (unweighted),
+    // m = a + 8b < 64 -- F^T W F and the Fourier column norms (k_greduce)
+    const int tA = Kpv, tA2 = Kpv + 16, tB = Kpv + 32, Kpt = Kpv + 48;
+    double* Ts = lds;       // [Kpt][CS] whitened rows
     long i0, i1;
     split_rows(n, nsplit, split, i0, i1);
     const double* Mi = M + I.moff;
@@ -745,15 +754,19 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
     const double* xv = dmxv + I.ooff;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    double4_t acc[NT];
+    static_assert(VW == 4, "the trig blocks give each wave two harmonics of A and of B");
+    double4_t acc[NT], accW = {0, 0, 0, 0}, accU = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    for (int k = tid; k < Kpv * CS; k += NTH) Ts[k] = 0.0;  // slot and padding columns stay 0
+    for (int k = tid; k < Kpt * CS; k += NTH) Ts[k] = 0.0;  // slot and padding columns stay 0
+    double csq[QL];  // sums of squares of this wave's timing columns (lanes = rows)
+#pragma unroll
+    for (int q = 0; q < QL; q++) csq[q] = 0.0;
     // Fourier harmonics of this wave
     const int hper = (nred + VW - 1) / VW;
     const int hb = wave * hper, he = std::min(nred, (wave + 1) * hper);
     int slot_prev = -1;  // wave 0: the LDS slot column of this lane's previous row
-    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
+    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, sg_n = 1.0;
     double st[QL];
     int d_n = -1;
     bool ok_n = false;
@@ -767,7 +780,8 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
             x_n = xv[row];
             d_n = Pd.drow[row];
         }
-        if (hb < he) {
+        if (nred > 0) {
+            sg_n = Pd.sigma[row];
             c1_n = Pd.red_cs[2 * row];
             s1_n = Pd.red_cs[2 * row + 1];
         }
@@ -785,7 +799,26 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
 #pragma unroll
             for (int q = 0; q < QL; q++) {
                 const int c = wave + VW * q;
-                if (c < r0) Ts[c * CS + lane] = st[q] * iw;
+                if (c < r0) {
+                    Ts[c * CS + lane] = st[q] * iw;
+                    if (ok_n) csq[q] += st[q] * st[q];
+                }
+            }
+            if (nred > 0) {  // trig blocks: harmonics a = 2 wave, 2 wave + 1 and 8a of them
+                const double us = ok_n ? sg_n : 0.0;  // A2 = A * sigma^2, whitened: A * sigma
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int a = 2 * wave + u;
+                    double c, sn;
+                    cpow(c1_n, s1_n, a, c, sn);
+                    Ts[(tA + a) * CS + lane] = c * iw;
+                    Ts[(tA + 8 + a) * CS + lane] = sn * iw;
+                    Ts[(tA2 + a) * CS + lane] = c * us;
+                    Ts[(tA2 + 8 + a) * CS + lane] = sn * us;
+                    cpow(c1_n, s1_n, 8 * a, c, sn);
+                    Ts[(tB + a) * CS + lane] = c * iw;
+                    Ts[(tB + 8 + a) * CS + lane] = sn * iw;
+                }
             }
             if (wave == 0) {
                 Ts[r0 * CS + lane] = r_n * iw;
@@ -823,6 +856,20 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
                     if (tj < nt) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
                 }
             }
+            if (nred > 0) {
+                const double bB = Tr[tB * CS];
+                accW = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], bB, accW, 0, 0, 0);
+                accU = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA2 * CS], bB, accU, 0, 0, 0);
+            }
+        }
+    }
+    // timing-column sums of squares of this split (normalize_designmatrix)
+#pragma unroll
+    for (int q = 0; q < QL; q++) {
+        const int c = wave + VW * q;
+        if (c < r0) {
+            const double v = wave_sum(csq[q]);
+            if (lane == 0) colsq[(I.coff + c) * nsplit + split] = v;
         }
     }
     // sum the waves' partial tiles through LDS, TG tiles at a time, and store them:
@@ -872,6 +919,32 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
             }
         }
     }
+    if (nred > 0) {  // trig tiles: sum over the waves, then C, S, U, V of m = a + 8b
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            red[((wave * 2 + 0) * 4 + q) * 64 + lane] = accW[q];
+            red[((wave * 2 + 1) * 4 + q) * 64 + lane] = accU[q];
+        }
+        __syncthreads();
+        double* tsum = red + VW * 2 * 256;  // [2][256]
+        for (int e = tid; e < 512; e += NTH) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < VW; w++) v += red[w * 512 + e];
+            tsum[e] = v;
+        }
+        __syncthreads();
+        // tile element (i, j) at ((i >> 2) * 64 + (i & 3) * 16 + j) (f64 MFMA C/D layout)
+        auto tix = [](int i, int j) { return ((i >> 2) << 6) + ((i & 3) << 4) + j; };
+        double* out = TSp + ((long)I.self * nsplit + split) * (4 * VTRIG);
+        for (int e = tid; e < 2 * VTRIG; e += NTH) {
+            const int kind = e >> 6, m = e & 63, a = m & 7, b = m >> 3;
+            const double* T_ = tsum + kind * 256;
+            out[2 * VTRIG * kind + m] = T_[tix(a, b)] - T_[tix(8 + a, 8 + b)];          // C_m / U_m
+            out[2 * VTRIG * kind + VTRIG + m] = T_[tix(8 + a, b)] + T_[tix(a, 8 + b)];  // S_m / V_m
+        }
+    }
 }
 
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
@@ -887,71 +960,7 @@ __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __res
     cs[2 * i + 1] = s;
 }
 
-// k_trig: the trig sums of every vg instance (m <= 2 nred): weighted C_m = sum w cos(m
-// theta), S_m = sum w sin(m theta) for F^T W F, and unweighted U_m, V_m for the Fourier
-// column norms (sum sin^2(h theta) = (N - U_2h)/2).  One 256-thread block per (kind,
-// N-split, half of the m range): wave w accumulates m = 8(4 half + w) .. +7 over the
-// split's rows (harmonics by rotation of the per-TOA fundamental, k_redbase), one partial
-// per block -> TSp (summed by k_tsum).  Runs on the side stream, concurrent with k_gram_v
-// (one wave per SIMD, so it co-resides with k_gram_v's workgroups).  Blocks past 4 nsplit:
-// the unweighted sums of squares of the timing columns per N-split (normalize_designmatrix).
-__global__ __launch_bounds__(256) void k_trig(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                              int nsplit, const double* __restrict__ M, double* __restrict__ TSp,
-                                              double* __restrict__ colsq) {
-    const InstDev I = insts[blockIdx.y];
-    const PsrDev& Pd = psrs[I.psr];
-    if (!Pd.vg) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if ((int)blockIdx.x >= 4 * nsplit) {  // unweighted sums of squares of the timing columns
-        const int sp = blockIdx.x - 4 * nsplit;
-        long i0, i1;
-        split_rows(I.n, nsplit, sp, i0, i1);
-        for (int c = wave; c < Pd.red0c; c += 4) {
-            const double* col = M + I.moff + (long)c * I.n;
-            double a0 = 0.0, a1 = 0.0;
-            long i = i0 + lane;
-            for (; i + 64 < i1; i += 128) {
-                a0 += col[i] * col[i];
-                a1 += col[i + 64] * col[i + 64];
-            }
-            if (i < i1) a0 += col[i] * col[i];
-            const double v = wave_sum(a0 + a1);
-            if (lane == 0) colsq[(I.coff + c) * nsplit + sp] = v;
-        }
-        return;
-    }
-    const int x = blockIdx.x % (2 * nsplit), kind = blockIdx.x / (2 * nsplit), nred = Pd.spec->nred;
-    const int m0 = 8 * (4 * (x & 1) + wave);
-    if (nred <= 0 || m0 > 2 * nred) return;
-    long i0, i1;
-    split_rows(I.n, nsplit, x >> 1, i0, i1);
-    double C[8], Sn[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) C[u] = Sn[u] = 0.0;
-    for (long i = i0 + lane; i < i1; i += 64) {
-        const double is = Pd.isig[i], w = kind ? 1.0 : is * is;
-        const double c1 = Pd.red_cs[2 * i], s1 = Pd.red_cs[2 * i + 1];
-        double c, s;
-        cpow(c1, s1, m0, c, s);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            C[u] += w * c;
-            Sn[u] += w * s;
-            rot(c, s, c1, s1);
-        }
-    }
-    double* out = TSp + ((long)I.self * nsplit + (x >> 1)) * (4 * VTRIG) + 2 * VTRIG * kind + m0;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        const double cv = wave_sum(C[u]), sv = wave_sum(Sn[u]);
-        if (lane == 0) {
-            out[u] = cv;
-            out[VTRIG + u] = sv;
-        }
-    }
-}
-
-// k_tsum: k_trig's per-block trig-sum partials of an instance summed in a fixed order
+// k_tsum: k_gram_v's per-split trig-sum partials of an instance summed in a fixed order
 __global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               int nsplit, const double* __restrict__ TSp, double* __restrict__ TS) {
     const InstDev I = insts[blockIdx.x];
@@ -973,7 +982,7 @@ __global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, c
 
 // Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
 // triangle only, in a fixed order (deterministic), and the column sums of squares.
-// vg instances: the Fourier block F^T W F from the trig sums TS (k_trig + k_tsum) by the
+// vg instances: the Fourier block F^T W F from the trig sums TS (k_gram_v + k_tsum) by the
 // product-to-sum identities (a, b = harmonics 1..nred), and past block nbg the DMX bin
 // rows Sd, DD, DCS from k_gram_v's slot partials of the N-splits the bin's rows fall in:
 //   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
@@ -2059,9 +2068,11 @@ struct pint_ctx {
     int vgram = 1;       // PINT_OPT_VGRAM
     int n_vg = 0;        // instances on the k_gram_v path
     bool any_dmx_rows = false;  // compact instances still on k_dmx_rows / k_dmx
-    double *d_TSp = nullptr, *d_TS = nullptr;  // k_trig per-block trig sums, their totals
+    double *d_TSp = nullptr, *d_TS = nullptr;  // k_gram_v per-split trig sums, their totals
     double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
-    hipEvent_t ev_start = nullptr, ev_trig = nullptr;
+    hipGraph_t graph = nullptr;          // a captured launch sequence (pint_capture_*)
+    hipGraphExec_t graph_exec = nullptr;
+    bool capturing = false;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
     int nblk = 0;
@@ -2085,11 +2096,13 @@ struct pint_ctx {
     int max_nep = 0;
     int* d_status = nullptr;
     int maxK = 0;
-    // HIP event pairs: 0/1 eval, 2/3 eval with design matrix, 4/5 resid, 6/7 ecorr+gram,
-    // 7/8 solve, 10/11 Woodbury chi2
-    hipEvent_t ev[12];
-    bool rec[12] = {false};
-    float ms[6] = {0, 0, 0, 0, 0, 0};
+    // HIP event pairs: 0/1 eval, 2/3 eval with design matrix, 4/5 resid, 6/7 ecorr + Gram +
+    // reduction, 7/8 solve, 10/11 Woodbury chi2, 12/13 the Gram kernels alone, 14/15 k_greduce
+    // (side stream)
+    static constexpr int NEV = 16, NMS = 8;
+    hipEvent_t ev[NEV];
+    bool rec[NEV] = {false};
+    float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 static void dfree(void*& p) {
@@ -2145,9 +2158,7 @@ pint_ctx* pint_ctx_create(int device) {
     else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ctx->ev_trig, hipEventDisableTiming);
-    for (int i = 0; i < 12; i++) hipEventCreate(&ctx->ev[i]);
+    for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
     return ctx;
 }
@@ -2166,6 +2177,10 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_TSp, (void**)&ctx->d_TS};
     for (auto p : ps) dfree(*p);
+    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
+    if (ctx->graph) hipGraphDestroy(ctx->graph);
+    ctx->graph_exec = nullptr;
+    ctx->graph = nullptr;
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
 }
@@ -2339,6 +2354,16 @@ int pint_fit_layout(pint_ctx* ctx, int psr, int32_t* out4) {
     return PINT_OK;
 }
 
+int pint_vgram_layout(pint_ctx* ctx, int psr, int32_t* out4) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !out4) return PINT_E_INVALID;
+    const PsrDev& d = ctx->psrs[psr].dev;
+    out4[0] = d.vg;
+    out4[1] = d.vns;
+    out4[2] = d.vkp;
+    out4[3] = d.red0c;
+    return PINT_OK;
+}
+
 int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const int32_t* ep_idx,
                    const double* ep_phi) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || nep < 0) return PINT_E_INVALID;
@@ -2404,7 +2429,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     ctx->nsplit = nsplit;
     ctx->red_valid[0] = ctx->red_valid[1] = 0;
-    // vg compact path (k_gram_v + k_trig): contiguous DMX bins, no ECORR, nred <= 31, <= 47
+    // vg compact path (k_gram_v): contiguous DMX bins, no ECORR, nred <= 31, <= 47
     // timing columns; the DMX slots fill the [T | r] row tiles (+16 if needed) such that the
     // bins of every N-split are distinct mod vns; LDS width <= VMAXKP
     for (auto& ph : ctx->psrs) {
@@ -2606,14 +2631,14 @@ int pint_set_tables(pint_ctx* ctx, const double* tables) {
     return PINT_OK;
 }
 
-static void record(pint_ctx* ctx, int i) {
-    hipEventRecord(ctx->ev[i], ctx->stream);
+static void record(pint_ctx* ctx, int i, hipStream_t st = nullptr) {
+    hipEventRecord(ctx->ev[i], st ? st : ctx->stream);
     ctx->rec[i] = true;
 }
 
 static void update_timings(pint_ctx* ctx) {
-    const int pairs[6][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}};
-    for (int k = 0; k < 6; k++) {
+    const int pairs[pint_ctx::NMS][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}, {12, 13}, {14, 15}};
+    for (int k = 0; k < pint_ctx::NMS; k++) {
         float t = 0.0f;
         if (ctx->rec[pairs[k][0]] && ctx->rec[pairs[k][1]] &&
             hipEventElapsedTime(&t, ctx->ev[pairs[k][0]], ctx->ev[pairs[k][1]]) == hipSuccess)
@@ -2722,18 +2747,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
     }
     const int cmp = ctx->m_compact;
-    const bool vgp = cmp && ctx->n_vg > 0;  // k_gram_v / k_trig path for the vg instances
-    if (vgp) {  // trig sums on the side stream, concurrent with k_gram_v
-        HIPCHK(hipEventRecord(ctx->ev_start, ctx->stream));
-        HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_start, 0));
-        hipLaunchKernelGGL(k_trig, dim3(5 * ctx->nsplit, ctx->ninst), dim3(256), 0, ctx->sstream, ctx->d_psrs,
-                           ctx->d_inst, ctx->nsplit, ctx->d_M, ctx->d_TSp, ctx->d_colsq);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->sstream, ctx->d_psrs, ctx->d_inst,
-                           ctx->nsplit, ctx->d_TSp, ctx->d_TS);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(ctx->ev_trig, ctx->sstream));
-    }
+    const bool vgp = cmp && ctx->n_vg > 0;  // k_gram_v path for the vg instances
     if (cmp && ctx->max_ndc > 0 && ctx->any_dmx_rows) {
         int maxKd = 0;
         bool any_gather = false;
@@ -2752,6 +2766,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             HIPCHK(hipGetLastError());
         }
     }
+    record(ctx, 12);
     {
         // instances are launched in groups of equal tiles-per-wave T (template parameter);
         // per-instance tile counts are recomputed in-kernel from their own Kp.
@@ -2787,10 +2802,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         for (const KpGroup& kg : ctx->kp_groups_v) {
             const InstDev* di = ctx->d_inst_sorted_v + kg.first;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * std::max<size_t>((size_t)kg.maxKp * (VCH + 2) + VCH, VW * VTG * 256);
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)(kg.maxKp + 48) * (VCH + 2),
+                                                                 std::max(VW * VTG * 256, VW * 512 + 512));
 #define PINT_GRAMV(R_, C_)                                                                                       \
             hipLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,   \
-                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp)
+                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp)
             switch (kg.T) {
                 case 1: PINT_GRAMV(1, 6); break;
                 case 2: PINT_GRAMV(1, 9); break;
@@ -2801,7 +2817,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             }
 #undef PINT_GRAMV
         }
-        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_trig, 0));
+        record(ctx, 13);
+        hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->nsplit, ctx->d_TSp, ctx->d_TS);
+        HIPCHK(hipGetLastError());
+    } else {
+        record(ctx, 13);
     }
     HIPCHK(hipGetLastError());
     if (nparts > 1 || vgp) {
@@ -2811,10 +2832,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : I.Kp);
         }
         const int nbg = (maxKp * maxKp + 255) / 256;
+        record(ctx, 14);
         hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? ctx->max_ndc : 0), ctx->ninst), dim3(256), 0, ctx->stream,
                            ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
                            ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
         HIPCHK(hipGetLastError());
+        record(ctx, 15);
     }
     record(ctx, 7);
     // Woodbury Sigma factor on the side stream, concurrent with the per-instance solve
@@ -2968,6 +2991,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     int nsw = ctx->nsplit;  // same N-split as the Gram (fills the CUs)
     size_t need = (size_t)ctx->ninst * nsw * stride;
     if (need > ctx->wpart_cap) {
+        if (ctx->capturing) { ctx->err = "pint_chi2_gls: first call inside a graph capture"; return PINT_E_INVALID; }
         dfree((void*&)ctx->d_wpart);
         HIPCHK(hipMalloc(&ctx->d_wpart, sizeof(double) * need));
         ctx->wpart_cap = need;
@@ -3002,6 +3026,52 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     return PINT_E_INVALID;
 }
 
+// Stream capture of a launch sequence into a HIP graph (lazy mode): everything the calls
+// between pint_capture_begin and pint_capture_end enqueue -- kernels, copies to/from the
+// caller's pinned buffers, the side-stream kernels and copies -- becomes one graph that
+// pint_graph_launch replays with a single launch.  Device buffers and host pointers are
+// frozen at capture: replays re-run the same batch on whatever the buffers hold.
+static void join_side_streams(pint_ctx* ctx) {
+    if (ctx->sigma_pending) hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0);
+    if (ctx->copy_pending) hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0);
+    ctx->sigma_pending = ctx->copy_pending = false;
+}
+
+int pint_capture_begin(pint_ctx* ctx) {
+    if (!ctx || ctx->ninst <= 0 || ctx->capturing) return PINT_E_INVALID;
+    if (!ctx->lazy) { ctx->err = "graph capture needs lazy mode"; return PINT_E_INVALID; }
+    hipSetDevice(ctx->device);
+    HIPCHK(hipStreamSynchronize(ctx->cstream));
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->sigma_pending = ctx->copy_pending = false;
+    HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    ctx->capturing = true;
+    return PINT_OK;
+}
+
+int pint_capture_end(pint_ctx* ctx) {
+    if (!ctx || !ctx->capturing) return PINT_E_INVALID;
+    join_side_streams(ctx);
+    ctx->capturing = false;
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamEndCapture(ctx->stream, &g));
+    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
+    if (ctx->graph) hipGraphDestroy(ctx->graph);
+    ctx->graph = g;
+    ctx->graph_exec = nullptr;
+    HIPCHK(hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0));
+    return PINT_OK;
+}
+
+int pint_graph_launch(pint_ctx* ctx) {
+    if (!ctx || !ctx->graph_exec) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    join_side_streams(ctx);
+    HIPCHK(hipGraphLaunch(ctx->graph_exec, ctx->stream));
+    return PINT_OK;
+}
+
 int pint_query(pint_ctx* ctx, int key) {
     if (!ctx) return -PINT_E_INVALID;
     if (key == PINT_QUERY_NVGRAM) return ctx->n_vg;
@@ -3017,7 +3087,7 @@ int pint_check(pint_ctx* ctx) {
 
 int pint_last_timing(pint_ctx* ctx, double* ms) {
     update_timings(ctx);
-    for (int k = 0; k < 6; k++) ms[k] = ctx->ms[k];
+    for (int k = 0; k < pint_ctx::NMS; k++) ms[k] = ctx->ms[k];
     return PINT_OK;
 }
 

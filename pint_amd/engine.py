@@ -333,6 +333,8 @@ class Session:
         self.inst_layout: List[PulsarLayout] = []
         self.lazy = False
         self._pinned: Dict[str, tuple] = {}
+        self._inflight = set()  # pinned staging buffers with a copy still enqueued (lazy)
+        self._keep = []         # host arrays of enqueued copies (lazy)
 
     def close(self):
         if self.ctx:
@@ -402,12 +404,45 @@ class Session:
         self._check(self.L.pint_fit_step(self.ctx, int(mode)))
 
     def apply_step(self, lam):
-        lam = np.ascontiguousarray(np.broadcast_to(np.asarray(lam, dtype=np.float64), (len(self.inst_layout),)))
+        lam = np.broadcast_to(np.asarray(lam, dtype=np.float64), (len(self.inst_layout),))
+        if self.lazy and "lambda" not in self._inflight:
+            buf = self._pin("lambda", lam.size)  # pinned (fixed for graph replays); reused after check()
+            buf[:] = lam
+            lam = buf
+            self._inflight.add("lambda")
+        else:
+            lam = np.array(lam, dtype=np.float64)
+            self._keep.append(lam)
         self._check(self.L.pint_apply_step(self.ctx, L.ptr(lam)))
 
+    # -- HIP graphs ---------------------------------------------------------------------
+    def capture(self, fn):
+        """Capture the launches fn() enqueues (lazy mode) into a HIP graph; returns fn()'s
+        result (pinned output buffers that every replay refills)."""
+        self._check(self.L.pint_capture_begin(self.ctx))
+        try:
+            out = fn()
+        except Exception:
+            self.L.pint_capture_end(self.ctx)
+            raise
+        self._check(self.L.pint_capture_end(self.ctx))
+        return out
+
+    def replay(self):
+        """Launch the captured graph (complete after check())."""
+        self._check(self.L.pint_graph_launch(self.ctx))
+
     def set_tables(self, tabs):
-        tabs = np.ascontiguousarray(tabs, dtype=np.float64)
-        self._tab_keep = tabs  # lazy mode: the host buffer must outlive the enqueued copy
+        tabs = np.asarray(tabs, dtype=np.float64).ravel()
+        if self.lazy and "tables" not in self._inflight:
+            # pinned staging buffer (fixed for graph replays); reused only after check()
+            buf = self._pin("tables", tabs.size)
+            buf[:] = tabs
+            tabs = buf
+            self._inflight.add("tables")
+        else:
+            tabs = np.array(tabs, dtype=np.float64)
+            self._keep.append(tabs)  # lazy: must outlive the enqueued copy
         self._check(self.L.pint_set_tables(self.ctx, L.ptr(tabs)))
 
     # -- reads ----------------------------------------------------------------------
@@ -450,6 +485,12 @@ class Session:
         self._check(self.L.pint_fit_layout(self.ctx, lay.psr_id, L.ptr(out, C.c_int32)))
         return tuple(int(x) for x in out)
 
+    def vgram_layout(self, lay):
+        """(on the vg path, DMX slots, k_gram_v LDS width, compact timing columns)."""
+        out = np.zeros(4, dtype=np.int32)
+        self._check(self.L.pint_vgram_layout(self.ctx, lay.psr_id, L.ptr(out, C.c_int32)))
+        return tuple(int(x) for x in out)
+
     def set_blocked_solve(self, on=True):
         self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))
 
@@ -463,6 +504,8 @@ class Session:
 
     def check(self):
         self._check(self.L.pint_check(self.ctx))
+        self._inflight.clear()
+        self._keep.clear()
 
     def read_step(self, want_cov=True):
         kk = [l.K + 1 for l in self.inst_layout]
@@ -494,7 +537,7 @@ class Session:
         return c if self.lazy else c.copy()
 
     def timing(self):
-        ms = np.zeros(6)
+        ms = np.zeros(8)
         self.L.pint_last_timing(self.ctx, L.ptr(ms))
         return ms
 
