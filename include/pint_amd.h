@@ -189,6 +189,10 @@ int pint_check(pint_ctx *ctx);
  * keeps them in M (the tests cross-check the two).  Takes effect at pint_set_instances. */
 #define PINT_OPT_BLOCKED_SOLVE 1
 #define PINT_OPT_VGRAM 2
+/* PINT_OPT_TIMING_MASK: bit k enables timing slot k of pint_last_timing (default 0xff).
+ * Every HIP timing event costs device time (~5 us each), so a timed run enables only the
+ * slots it reports. */
+#define PINT_OPT_TIMING_MASK 3
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* HIP-graph capture of a launch sequence (lazy mode only).  Everything the calls between
  * pint_capture_begin and pint_capture_end enqueue (kernels, the copies to and from the

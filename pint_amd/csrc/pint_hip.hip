@@ -175,14 +175,13 @@ __global__ __launch_bounds__(64) void k_prep(const PsrDev* __restrict__ psrs, co
 }
 
 template <int WANT_M, int BIN>
-__global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                              const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
-                                              const double* __restrict__ tables, const InstConst* __restrict__ ic,
-                                              double* __restrict__ ph_hi, double* __restrict__ ph_lo,
-                                              double* __restrict__ ftay, double* __restrict__ delay_out,
-                                              double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                              int write_red, int* __restrict__ status) {
-    int b = blockIdx.x;
+__device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                           const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
+                                           const double* __restrict__ tables, const InstConst* __restrict__ ic,
+                                           double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                           double* __restrict__ ftay, double* __restrict__ delay_out,
+                                           double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
+                                           int write_red, int* __restrict__ status) {
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -231,6 +230,20 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
             colp[r + n] = cs;
         }
     }
+}
+
+// k_eval: one thread per TOA row; one launch per binary model (blocks of the isolated,
+// ELL1 or DD instances), so each instantiation carries only its own registers.
+template <int WANT_M, int BIN>
+__global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
+                                              const double* __restrict__ tables, const InstConst* __restrict__ ic,
+                                              double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                              double* __restrict__ ftay, double* __restrict__ delay_out,
+                                              double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
+                                              int write_red, int* __restrict__ status) {
+    eval_block<WANT_M, BIN>(blockIdx.x, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
+                            Mout, dmxv, compact, write_red, status);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2017,9 +2030,11 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     if (threadIdx.x == 0) chi2[inst] = (rwr - erwr) - q;
 }
 
-// tables += lambda * dpars on every timing column (skips Offset), double-double add
+// tables += lambda * dpars on every timing column (skips Offset), double-double add; then
+// the per-instance constants of the updated table (k_prep's work, saving its launch)
 __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, double* __restrict__ tables,
-                        const double* __restrict__ dpars, const double* __restrict__ lam) {
+                        const double* __restrict__ dpars, const double* __restrict__ lam,
+                        InstConst* __restrict__ ic) {
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const pint_spec_t& S = *psrs[I.psr].spec;
@@ -2030,6 +2045,12 @@ __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restri
         dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam[inst] * dpars[I.coff + c]);
         P[o] = v.hi;
         P[o + 1] = v.lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        InstConst C;
+        inst_setup(S, P, C);
+        ic[inst] = C;
     }
 }
 
@@ -2070,6 +2091,9 @@ struct pint_ctx {
     bool any_dmx_rows = false;  // compact instances still on k_dmx_rows / k_dmx
     double *d_TSp = nullptr, *d_TS = nullptr;  // k_gram_v per-split trig sums, their totals
     double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
+    bool ic_valid = false;  // per-instance constants (k_prep) current for the tables
+    bool no_events = false; // PINT_NO_EVENTS=1: no per-kernel timing events (their cost)
+    int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
     hipGraph_t graph = nullptr;          // a captured launch sequence (pint_capture_*)
     hipGraphExec_t graph_exec = nullptr;
     bool capturing = false;
@@ -2156,10 +2180,12 @@ pint_ctx* pint_ctx_create(int device) {
     // rocprof's per-kernel durations are not inflated by concurrent kernels
     if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
     else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
+    ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev[i]);
     hipMalloc(&ctx->d_status, sizeof(int));
+    hipMemset(ctx->d_status, 0, sizeof(int));
     return ctx;
 }
 
@@ -2429,6 +2455,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     ctx->nsplit = nsplit;
     ctx->red_valid[0] = ctx->red_valid[1] = 0;
+    ctx->ic_valid = false;
     // vg compact path (k_gram_v): contiguous DMX bins, no ECORR, nred <= 31, <= 47
     // timing columns; the DMX slots fill the [T | r] row tiles (+16 if needed) such that the
     // bins of every N-split are distinct mod vns; LDS width <= VMAXKP
@@ -2625,20 +2652,29 @@ int pint_get_tables(pint_ctx* ctx, double* out) {
 }
 
 int pint_set_tables(pint_ctx* ctx, const double* tables) {
+    ctx->ic_valid = false;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
+static const int kTimingPairs[pint_ctx::NMS][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}, {12, 13}, {14, 15}};
+
 static void record(pint_ctx* ctx, int i, hipStream_t st = nullptr) {
+    if (ctx->no_events) return;
+    bool on = false;  // only the events of the enabled timing slots (each costs device time)
+    for (int k = 0; k < pint_ctx::NMS; k++)
+        if ((ctx->timing_mask >> k) & 1) on |= kTimingPairs[k][0] == i || kTimingPairs[k][1] == i;
+    if (!on) return;
     hipEventRecord(ctx->ev[i], st ? st : ctx->stream);
     ctx->rec[i] = true;
 }
 
 static void update_timings(pint_ctx* ctx) {
-    const int pairs[pint_ctx::NMS][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}, {12, 13}, {14, 15}};
+    const auto& pairs = kTimingPairs;
     for (int k = 0; k < pint_ctx::NMS; k++) {
+        if (!((ctx->timing_mask >> k) & 1)) continue;
         float t = 0.0f;
         if (ctx->rec[pairs[k][0]] && ctx->rec[pairs[k][1]] &&
             hipEventElapsedTime(&t, ctx->ev[pairs[k][0]], ctx->ev[pairs[k][1]]) == hipSuccess)
@@ -2652,6 +2688,8 @@ static int check_status(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    // the status word accumulates error bits of everything enqueued since the last check
+    if (st) HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
     if (st & (1 << PINT_E_NOT_PD)) { ctx->err = "normal matrix not positive definite"; return PINT_E_NOT_PD; }
     if (st) { ctx->err = "device status " + std::to_string(st); return PINT_E_PARAM; }
@@ -2663,7 +2701,6 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     if (want_M < 0 || want_M > 2) return PINT_E_INVALID;
-    HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     if (want_M) ctx->m_compact = (want_M == 2) ? 1 : 0;
     // the full and compact layouts place the red-noise columns differently; each is written
     // once after pint_set_instances (M is reallocated there)
@@ -2674,10 +2711,13 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         ctx->red_valid[want_M != 2] = 0;  // the other layout's red columns get overwritten
     }
     record(ctx, want_M ? 2 : 0);
-    hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->ninst, ctx->d_tables, ctx->d_ic);
-    HIPCHK(hipGetLastError());
-    for (int t = 0; t < 3; t++) {
+    if (!ctx->ic_valid) {  // k_apply refreshes them itself
+        hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->ninst, ctx->d_tables, ctx->d_ic);
+        HIPCHK(hipGetLastError());
+        ctx->ic_valid = true;
+    }
+    for (int t = 0; t < 3; t++) {  // one launch per binary model, back to back on the stream
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
         const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
@@ -2734,7 +2774,6 @@ int pint_read_designmatrix(pint_ctx* ctx, double* M) {
 int pint_fit_step(pint_ctx* ctx, int mode) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
-    HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     const int nparts = ctx->nsplit + ((mode == 1 && ctx->max_nep > 0) ? 1 : 0);
     if (ctx->sigma_pending) {  // the previous k_sigma reads the Gram buffer this step overwrites
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
@@ -2976,8 +3015,9 @@ int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
-                       ctx->d_dpars, ctx->d_lam);
+                       ctx->d_dpars, ctx->d_lam, ctx->d_ic);
     HIPCHK(hipGetLastError());
+    ctx->ic_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -3022,6 +3062,12 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (!ctx) return PINT_E_INVALID;
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_TIMING_MASK) {
+        ctx->timing_mask = value & 0xff;
+        for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec[k] = false;
+        for (int k = 0; k < pint_ctx::NMS; k++) ctx->ms[k] = 0.0f;
+        return PINT_OK;
+    }
     ctx->err = "unknown option";
     return PINT_E_INVALID;
 }

@@ -494,6 +494,10 @@ class Session:
     def set_blocked_solve(self, on=True):
         self._check(self.L.pint_set_option(self.ctx, 1, 1 if on else 0))
 
+    def set_timing_mask(self, mask=0xFF):
+        """Timing slots of timing() whose HIP events are recorded (each costs device time)."""
+        self._check(self.L.pint_set_option(self.ctx, 3, int(mask)))
+
     def set_vgram(self, on=True):
         """Generated-Fourier compact fit path (k_gram_v); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 2, 1 if on else 0))
