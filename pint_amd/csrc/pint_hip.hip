@@ -734,7 +734,7 @@ __device__ __forceinline__ int vg_cidx(int p, int r0, int Kd) {
 // per 4-row k-step it reads NTR + nt operands and issues up to NT independent
 // v_mfma_f64_16x16x4f64.  The waves' partial tiles are summed through LDS at the end.
 template <int NTR, int NTC>
-__global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+__global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                     const double* __restrict__ M, const double* __restrict__ rtime,
                                                     const double* __restrict__ dmxv, int nsplit,
                                                     double* __restrict__ Gpart, double* __restrict__ Sdp,
@@ -752,7 +752,7 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
     const int n = I.n, Kd = Pd.Kd, Kp = Pd.Kpd, r0 = Pd.red0c, NS = Pd.vns, Kpv = Pd.vkp;
     const int nred = Pd.spec->nred;
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
-    const int nt = Kpv / 16;                                          // <= NTC; ntr == NTR
+    // Kpv == 16 NTC and f0 == 16 NTR (the launch groups instances by both)
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
     // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), A2 = the same times
     // sigma (unweighted after the whitening), B = [cos 8b theta | sin 8b theta]/sigma (b < 8):
@@ -860,14 +860,13 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
 #pragma unroll
             for (int t = 0; t < NTR; t++) a[t] = Tr[t * 16 * CS];
 #pragma unroll
-            for (int t = 0; t < NTC; t++) b[t] = t < nt ? Tr[t * 16 * CS] : 0.0;
+            for (int t = 0; t < NTC; t++) b[t] = Tr[t * 16 * CS];
             int k = 0;
 #pragma unroll
             for (int ti = 0; ti < NTR; ti++) {
 #pragma unroll
-                for (int tj = ti; tj < NTC; tj++, k++) {
-                    if (tj < nt) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
-                }
+                for (int tj = ti; tj < NTC; tj++, k++)
+                    acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
             }
             if (nred > 0) {
                 const double bB = Tr[tB * CS];
@@ -913,7 +912,6 @@ __global__ __launch_bounds__(VW * 64) void k_gram_v(const PsrDev* __restrict__ p
                     int tt = kbase + gg, r_ = 0;  // tile (r_, r_ + tt) of the row-major list
                     while (tt >= NTC - r_) { tt -= NTC - r_; r_++; }
                     const int tJ_ = r_ + tt;
-                    if (tJ_ >= nt) continue;
                     const int pr = r_ * 16 + (ln >> 4) + 4 * q, pc = tJ_ * 16 + (ln & 15);
                     if (pr > pc || pc >= Wv) continue;
                     const bool rs = pr >= s0, cs = pc >= s0 && pc < f0;
@@ -2572,7 +2570,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         std::vector<InstDev> sorted;
         std::vector<KpGroup>& groups = lay == 0 ? ctx->kp_groups : (lay == 1 ? ctx->kp_groups_c : ctx->kp_groups_v);
         groups.clear();
-        for (int T = 1; T <= GMAXT_ALL; T++) {
+        for (int T = 1; T <= (lay == 2 ? 29 : GMAXT_ALL); T++) {
             KpGroup g{T, (int)sorted.size(), 0, 16};
             for (auto& I : ctx->inst) {
                 const PsrDev& pd = ctx->psrs[I.psr].dev;
@@ -2581,9 +2579,9 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
                 const int nt = kp / 16;
                 int tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
-                if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column-tile bound (6 | 9)
+                if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column tiles (ntr..9)
                     const int ntr = (pd.red0c + 1 + pd.vns) / 16;
-                    tT = 2 * (ntr - 1) + (nt <= 6 ? 1 : 2);
+                    tT = 10 * (ntr - 1) + nt;
                 }
                 if (tT != T) continue;
                 sorted.push_back(I);
@@ -2847,12 +2845,31 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,   \
                                ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp)
             switch (kg.T) {
-                case 1: PINT_GRAMV(1, 6); break;
-                case 2: PINT_GRAMV(1, 9); break;
-                case 3: PINT_GRAMV(2, 6); break;
-                case 4: PINT_GRAMV(2, 9); break;
-                case 5: PINT_GRAMV(3, 6); break;
-                default: PINT_GRAMV(3, 9); break;
+                case 1: PINT_GRAMV(1, 1); break;
+                case 2: PINT_GRAMV(1, 2); break;
+                case 3: PINT_GRAMV(1, 3); break;
+                case 4: PINT_GRAMV(1, 4); break;
+                case 5: PINT_GRAMV(1, 5); break;
+                case 6: PINT_GRAMV(1, 6); break;
+                case 7: PINT_GRAMV(1, 7); break;
+                case 8: PINT_GRAMV(1, 8); break;
+                case 9: PINT_GRAMV(1, 9); break;
+                case 12: PINT_GRAMV(2, 2); break;
+                case 13: PINT_GRAMV(2, 3); break;
+                case 14: PINT_GRAMV(2, 4); break;
+                case 15: PINT_GRAMV(2, 5); break;
+                case 16: PINT_GRAMV(2, 6); break;
+                case 17: PINT_GRAMV(2, 7); break;
+                case 18: PINT_GRAMV(2, 8); break;
+                case 19: PINT_GRAMV(2, 9); break;
+                case 23: PINT_GRAMV(3, 3); break;
+                case 24: PINT_GRAMV(3, 4); break;
+                case 25: PINT_GRAMV(3, 5); break;
+                case 26: PINT_GRAMV(3, 6); break;
+                case 27: PINT_GRAMV(3, 7); break;
+                case 28: PINT_GRAMV(3, 8); break;
+                case 29: PINT_GRAMV(3, 9); break;
+                default: ctx->err = "k_gram_v layout out of range"; return PINT_E_INVALID;
             }
 #undef PINT_GRAMV
         }
