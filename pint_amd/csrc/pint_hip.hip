@@ -1622,10 +1622,26 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        const double* __restrict__ DCS, double* __restrict__ dpars,
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                       int* __restrict__ status) {
+                                                       int* __restrict__ status, int fuse_sigma) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
+    if (fuse_sigma && (int)blockIdx.x >= (int)gridDim.x / 2) {
+        // the Woodbury Sigma factor (k_sigma's work) in the second half of the grid, so it
+        // runs concurrently with the solves without a second stream
+        const InstDev I = insts[blockIdx.x - gridDim.x / 2];
+        const PsrDev& Pd = psrs[I.psr];
+        const pint_spec_t& S = *Pd.spec;
+        if (!(S.nred > 0 || Pd.nep > 0)) return;
+        if (threadIdx.x == 0) sflag = 0;
+        __syncthreads();
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const GramView G = gram_view(Pd, I, Gpart, Pd.dsplit != 0, Sd, DD);
+        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff))
+            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        return;
+    }
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -2896,41 +2912,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         record(ctx, 15);
     }
     record(ctx, 7);
-    // Woodbury Sigma factor on the side stream, concurrent with the per-instance solve
-    int do_sigma = 0;
-    if (mode == 1) {
-        int kn = 0;
-        bool any = false;
-        for (auto& I : ctx->inst) {
-            const PsrHost& ph = ctx->psrs[I.psr];
-            if (ph.spec.nred > 0 || ph.dev.nep > 0) { any = true; kn = std::max(kn, 2 * ph.spec.nred + 1); }
-        }
-        const int nbs = (kn + 15) / 16;
-        if (any && nbs <= BS_MAXNB && ctx->blocked_solve) {
-            HIPCHK(hipEventRecord(ctx->ev_gram, ctx->stream));
-            HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
-            const size_t lds_s = sizeof(double) * (size_t)nbs * (nbs + 1) / 2 * 256;
-            if (nbs <= 5)
-                hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
-                                   ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
-            else
-                hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
-                                   ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
-                                   ctx->d_status);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
-            ctx->sigma_pending = true;
-        } else if (any) {
-            do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
-        }
-    }
-    if (ctx->copy_pending) {  // the previous step's outputs may still be in flight to the host
-        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
-        ctx->copy_pending = false;
-    }
-    // DMX-eliminated solve for compact-layout instances (k_solve_dmx), when every such
-    // instance fits its LDS budget; the others (and everything in the full layout) go to the
-    // blocked MFMA solve, or the column-by-column one beyond its LDS budget.
+    // solve plan: the DMX-eliminated solve (k_solve_dmx) for compact-layout instances when
+    // every such instance fits its LDS budget; the others (and everything in the full
+    // layout) go to the blocked MFMA solve, or the column-by-column one beyond its budget.
     int Ks = 0, Kn = 0, ndmx_inst = 0;
     bool dmx_ok = cmp && ctx->blocked_solve;
     size_t lds_x = 0;
@@ -2956,10 +2940,48 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         ndmx_inst = 0;
     }
     const int skip = ndmx_inst > 0 ? 1 : 0;
+    // Woodbury Sigma factor: in k_solve_dmx's grid when every instance is solved there, else
+    // on the side stream, concurrent with the per-instance solve
+    int do_sigma = 0, fuse_sigma = 0;
+    size_t lds_s = 0;
+    if (mode == 1) {
+        int kn = 0;
+        bool any = false;
+        for (auto& I : ctx->inst) {
+            const PsrHost& ph = ctx->psrs[I.psr];
+            if (ph.spec.nred > 0 || ph.dev.nep > 0) { any = true; kn = std::max(kn, 2 * ph.spec.nred + 1); }
+        }
+        const int nbs = (kn + 15) / 16;
+        lds_s = sizeof(double) * (size_t)nbs * (nbs + 1) / 2 * 256;
+        if (any && nbs <= BS_MAXNB && ctx->blocked_solve && skip && Ks == 0) {
+            fuse_sigma = 1;
+        } else if (any && nbs <= BS_MAXNB && ctx->blocked_solve) {
+            HIPCHK(hipEventRecord(ctx->ev_gram, ctx->stream));
+            HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
+            if (nbs <= 5)
+                hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
+                                   ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
+            else
+                hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
+                                   ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
+                                   ctx->d_status);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
+            ctx->sigma_pending = true;
+        } else if (any) {
+            do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
+        }
+    }
+    if (ctx->copy_pending) {  // the previous step's outputs may still be in flight to the host
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
+        ctx->copy_pending = false;
+    }
     if (skip) {
-        hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst), dim3(1024), lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
+        hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
+                           fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
-                           ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status);
+                           ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
+                           fuse_sigma);
         HIPCHK(hipGetLastError());
     }
     const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
