@@ -194,6 +194,13 @@ int pint_check(pint_ctx *ctx);
  * slots it reports. */
 #define PINT_OPT_TIMING_MASK 3
 int pint_set_option(pint_ctx *ctx, int key, int value);
+/* Likelihood normalisation per instance, Residuals.calc_chi2(lognorm=True)
+ * (residuals.py:567-589, :638-667): gls != 0 gives logdet(C)/2 of the last pint_chi2_gls
+ * (C = N + U Phi U^T, U = [F, ECORR, 1], utils.py:3074 woodbury_dot), gls == 2 the same
+ * for a correlated-noise model whose basis has no columns (U = [1]), gls == 0 gives
+ * sum_i log sigma_i (s).  lnlikelihood = -(chi2/2 + lognorm). */
+int pint_lognorm(pint_ctx *ctx, int gls, double *out);
+
 /* HIP-graph capture of a launch sequence (lazy mode only).  Everything the calls between
  * pint_capture_begin and pint_capture_end enqueue (kernels, the copies to and from the
  * caller's pinned buffers, the side-stream work) becomes one graph; pint_graph_launch

@@ -831,6 +831,33 @@ def chi2_gls(om, toas, r, sigma_us):
     return float(xNy - xNU @ scipy.linalg.cho_solve(cf, xNU))
 
 
+def lognorm(om, toas, r, sigma_us, gls=True):
+    """Residuals.calc_chi2(lognorm=True)'s log_norm: sum log sigma_s (_calc_wls_chi2,
+    residuals.py:638-667) or logdet(C)/2 (_calc_gls_chi2 :567-589 via woodbury_dot
+    utils.py:3074-3126: logdet N + logdet Phi + slogdet Sigma, U = [noise basis, 1],
+    Phi = [phi, 1e40])."""
+    sig = sigma_us * 1e-6
+    U, phi = noise_basis(om, toas) if gls else (None, None)
+    if U is None:
+        return float(np.sum(np.log(sig)))
+    # a correlated-noise model always takes the Woodbury form, with the offset column even
+    # when its basis has no columns (ECORR without multi-TOA epochs)
+    N = sig ** 2
+    U = np.append(U, np.ones((len(r), 1)), axis=1)
+    phi = np.append(phi, [1e40])
+    Sigma = np.diag(1 / phi) + (U.T / N) @ U
+    _, ld_sigma = np.linalg.slogdet(Sigma)
+    return float(0.5 * (np.sum(np.log(N)) + np.sum(np.log(phi)) + ld_sigma))
+
+
+def lnlikelihood(om, toas, gls=True):
+    """Residuals.lnlikelihood (residuals.py:713-716): -(chi2/2 + log_norm)."""
+    r = residuals(om, toas)
+    corr = gls and noise_basis(om, toas)[0] is not None
+    c2 = chi2_gls(om, toas, r["time"], r["sigma_us"]) if corr else chi2_wls(r["time"], r["sigma_us"])
+    return -(c2 / 2 + lognorm(om, toas, r["time"], r["sigma_us"], corr))
+
+
 def _normalize(M):
     norm = np.sqrt((M ** 2).sum(0))
     norm[norm == 0] = 1

@@ -83,6 +83,7 @@ def lib():
     L.pint_query.restype = C.c_int
     L.pint_fit_layout.argtypes = [vp, C.c_int, C.POINTER(C.c_int32)]
     L.pint_vgram_layout.argtypes = [vp, C.c_int, C.POINTER(C.c_int32)]
+    L.pint_lognorm.argtypes = [vp, C.c_int, dptr]
     L.pint_host_alloc.restype = vp
     L.pint_host_alloc.argtypes = [C.c_size_t]
     L.pint_host_free.argtypes = [vp]
@@ -98,7 +99,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_devi
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",
             "pint_set_option", "pint_host_alloc", "pint_host_free",
             "pint_fit_layout", "pint_query", "pint_capture_begin", "pint_capture_end", "pint_graph_launch",
-            "pint_vgram_layout"]
+            "pint_vgram_layout", "pint_lognorm"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <cstdio>
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include "physics.hpp"
 
@@ -59,6 +60,8 @@ struct PsrDev {
     int vns; // k_gram_v DMX slots (bins of an N-split are distinct mod vns)
     int vkp; // k_gram_v LDS width: [T | r | slots | F] padded to 16
     int pad_;
+    double logsig;  // sum_i log sigma_i (s): the WLS likelihood normalisation (residuals.py:665)
+    double sumw;    // sum_i 1/sigma_i^2 (s^-2)
 };
 
 struct InstDev {
@@ -1987,7 +1990,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 const double* __restrict__ esum, const double* __restrict__ eD,
                                                 const double* __restrict__ eW, const double* __restrict__ wpart,
                                                 int nsplit, int stride, double* __restrict__ ecs,
-                                                double* __restrict__ chi2) {
+                                                double* __restrict__ chi2, double* __restrict__ lognorm) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
     const int inst = blockIdx.x;
@@ -2041,7 +2044,19 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
         q += s * s;
     }
     q = block_sum<4>(q, sh);
-    if (threadIdx.x == 0) chi2[inst] = (rwr - erwr) - q;
+    // log-normalisation of the likelihood, logdet(C)/2 (residuals.py:567-589 via
+    // utils.py:3074 woodbury_dot): logdet C = logdet N + logdet Phi + logdet Sigma, Phi =
+    // [phi_red, phi_ecorr, 1e40]; with the ECORR block eliminated, logdet Sigma =
+    // sum_e log D_e + logdet Sigma' and Sigma' = L L^T (X = L^-1 holds 1/L_jj on its diagonal)
+    double ld = 0.0;
+    for (int e = threadIdx.x; e < nep; e += blockDim.x) ld += log(Pd.ep_phi[e]) + log(eD[I.epoff + e]);
+    for (int k = threadIdx.x; k < R; k += blockDim.x) ld += log(Pd.red_phi[k]);
+    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(X[tri(j, j)]);
+    ld = block_sum<4>(ld, sh);
+    if (threadIdx.x == 0) {
+        chi2[inst] = (rwr - erwr) - q;
+        lognorm[inst] = 0.5 * (ld + 2.0 * Pd.logsig + log(1e40));
+    }
 }
 
 // tables += lambda * dpars on every timing column (skips Offset), double-double add; then
@@ -2124,6 +2139,7 @@ struct pint_ctx {
     double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
     double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
+    double* d_lognorm = nullptr;  // per instance: logdet(C)/2 of the last pint_chi2_gls
     InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
     double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
     int max_ndc = 0;
@@ -2211,7 +2227,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
-                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
+                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
@@ -2273,10 +2289,15 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->sigma_s, n, d.sigma);
     {
         std::vector<double> is(n);
+        double ls = 0.0, sw = 0.0;
         for (int i = 0; i < n; i++) {
             if (!(t->sigma_s[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; return -PINT_E_INVALID; }
             is[i] = 1.0 / t->sigma_s[i];
+            ls += std::log(t->sigma_s[i]);
+            sw += is[i] * is[i];
         }
+        d.logsig = ls;
+        d.sumw = sw;
         rc |= upload(ctx, ph, is.data(), n, d.isig);
     }
     rc |= upload(ctx, ph, t->pos_km, 3 * (n + 1), d.pos);
@@ -2636,6 +2657,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(hipMalloc(&ctx->d_rp, sizeof(double) * out));
     HIPCHK(hipMalloc(&ctx->d_chi2, sizeof(double) * ninst));
     HIPCHK(hipMalloc(&ctx->d_chi2g, sizeof(double) * ninst));
+    HIPCHK(hipMalloc(&ctx->d_lognorm, sizeof(double) * ninst));
     HIPCHK(hipMalloc(&ctx->d_chi2lin, sizeof(double) * ninst));
     HIPCHK(hipMalloc(&ctx->d_G, sizeof(double) * goff));
     HIPCHK(hipMalloc(&ctx->d_colsq, sizeof(double) * coff * nsplit));
@@ -3082,7 +3104,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
-                       stride, ctx->d_ecs, ctx->d_chi2g);
+                       stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm);
     HIPCHK(hipGetLastError());
     record(ctx, 11);
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
@@ -3154,6 +3176,26 @@ int pint_graph_launch(pint_ctx* ctx) {
     hipSetDevice(ctx->device);
     join_side_streams(ctx);
     HIPCHK(hipGraphLaunch(ctx->graph_exec, ctx->stream));
+    return PINT_OK;
+}
+
+// Likelihood normalisation per instance (Residuals.calc_chi2(lognorm=True)): gls == 1 the
+// logdet(C)/2 of the last pint_chi2_gls; gls == 2 a correlated-noise model whose basis has
+// no columns (C = N + 1e40 1 1^T: logdet C = logdet N + log 1e40 + log(1e-40 + sum w));
+// gls == 0 sum log sigma (residuals.py:638-667).
+int pint_lognorm(pint_ctx* ctx, int gls, double* out) {
+    if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
+    if (gls == 2) {
+        for (int k = 0; k < ctx->ninst; k++) {
+            const PsrDev& d = ctx->psrs[ctx->inst[k].psr].dev;
+            out[k] = 0.5 * (2.0 * d.logsig + std::log(1e40) + std::log(1e-40 + d.sumw));
+        }
+    } else if (gls) {
+        HIPCHK(hipMemcpyAsync(out, ctx->d_lognorm, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    } else {
+        for (int k = 0; k < ctx->ninst; k++) out[k] = ctx->psrs[ctx->inst[k].psr].dev.logsig;
+    }
     return PINT_OK;
 }
 

@@ -540,6 +540,14 @@ class Session:
         self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
         return c if self.lazy else c.copy()
 
+    def lognorm(self, gls):
+        """Per-instance likelihood normalisation: logdet(C)/2 of the last chi2_gls (gls=1), of
+        C = N + 1e40 11^T (gls=2: correlated model, no basis columns) or sum log sigma (gls=0)
+        (residuals.py:567-589, :638-667)."""
+        out = np.zeros(len(self.inst_layout))
+        self._check(self.L.pint_lognorm(self.ctx, int(gls), L.ptr(out)))
+        return out
+
     def timing(self):
         ms = np.zeros(8)
         self.L.pint_last_timing(self.ctx, L.ptr(ms))

@@ -47,6 +47,8 @@ class Residuals:
                 self._chi2 = float(s.chi2_gls()[0])
             else:
                 self._chi2 = float(c2[0])
+            ln_kind = 1 if corr else (2 if self.model.has_correlated_errors else 0)
+            self._lognorm = float(s.lognorm(ln_kind)[0])
         finally:
             s.close()
 
@@ -63,9 +65,14 @@ class Residuals:
         return self._chi2
 
     def calc_chi2(self, lognorm=False):
-        if lognorm:
-            raise NotImplementedError("lnlikelihood normalisation lands with §8(f) item 3")
-        return self._chi2
+        """residuals.py:669-711: (chi2, log_norm) with lognorm=True, log_norm = logdet(C)/2
+        (Woodbury, correlated noise) or sum log sigma (white noise), from the GPU."""
+        return (self._chi2, self._lognorm) if lognorm else self._chi2
+
+    def lnlikelihood(self) -> float:
+        """residuals.py:713-716: -(chi2/2 + log_norm)."""
+        chi2, log_norm = self.calc_chi2(lognorm=True)
+        return -(chi2 / 2 + log_norm)
 
     @property
     def dof(self) -> int:

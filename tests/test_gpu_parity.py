@@ -444,3 +444,16 @@ def test_graph_replay_matches_direct():
     again = snap(cap)
     assert np.array_equal(again[4], replayed[4])
     s.close()
+
+
+def test_lnlikelihood(fx):
+    """Residuals.calc_chi2(lognorm=True) / lnlikelihood (residuals.py:669-716) on the GPU
+    against the reference's values: log_norm = logdet(C)/2 (Woodbury determinant from the
+    device Cholesky factor of Sigma, ECORR D_e, phi) or sum log sigma."""
+    from pint_amd import Residuals
+    name, model, toas, z, meta = fx
+    r = Residuals(toas, model)
+    chi2, ln = r.calc_chi2(lognorm=True)
+    assert abs(ln - meta["res_lognorm"]) <= 1e-9 * abs(meta["res_lognorm"]), (ln, meta["res_lognorm"])
+    ref = meta["res_lnlikelihood"]
+    assert abs(r.lnlikelihood() - ref) <= 1e-6 * abs(meta["res_chi2"]) + 1e-9 * abs(ref)

@@ -181,3 +181,15 @@ def test_grid_chisq():
     # the reference's serial and parallel grids themselves differ by ~1e-8 relative
     assert np.allclose(z["grid_chi2_serial"], z["grid_chi2_parallel"], rtol=1e-7)
     assert np.allclose(c2, z["grid_chi2_serial"], rtol=1e-7, atol=0)
+
+
+def test_lnlikelihood(fx):
+    """Residuals.lnlikelihood (residuals.py:713): -(chi2/2 + log_norm), log_norm = logdet(C)/2
+    (Woodbury, utils.py:3074) or sum log sigma; against the reference's own value."""
+    name, om, toas, z, meta = fx
+    if "res_lnlikelihood" not in meta:
+        pytest.skip("no lnlikelihood in fixture")
+    ll = O.lnlikelihood(om, toas, gls=True)
+    ref = meta["res_lnlikelihood"]
+    # chi2/2 carries the oracle-vs-reference residual floor (<= 1.2e-6 relative, pta_ell1)
+    assert abs(ll - ref) <= 1e-6 * abs(meta["res_chi2"]) + 1e-9 * abs(ref), (ll, ref)
