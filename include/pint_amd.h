@@ -33,6 +33,7 @@ extern "C" {
 #define PINT_E_NOT_PD 3       /* normal matrix not positive definite (LinAlgError)    */
 #define PINT_E_KEPLER 4       /* Kepler iteration did not converge / ECC outside [0,1)*/
 #define PINT_E_PARAM 5        /* invalid model parameter region (InvalidModelParameters)*/
+#define PINT_E_SIGMA 6        /* Woodbury Sigma = Phi^-1 + U^T N^-1 U not positive definite */
 
 /* ---- limits -------------------------------------------------------------------- */
 #define PINT_MAX_COLS 320     /* design-matrix columns incl. Offset                   */
@@ -194,6 +195,18 @@ int pint_check(pint_ctx *ctx);
  * slots it reports. */
 #define PINT_OPT_TIMING_MASK 3
 int pint_set_option(pint_ctx *ctx, int key, int value);
+/* The SVD path of the fitters for degenerate normal equations (WLSState.step,
+ * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max
+ * dropped; GLSFitter fitter.py:2196-2230: SVD of mtcm when Cholesky fails), on the Gram of
+ * the last pint_fit_step(mode), threshold[i] per instance: eigendecomposition of the normalised normal matrix (Jacobi,
+ * on the device).  Replaces the outputs pint_read_step returns.  ndeg[i] = dropped
+ * directions of instance i (<= PINT_EIG_MAXDEG); degvec[(i * PINT_EIG_MAXDEG + d) *
+ * degstride + k] their components over the instance's fit columns, scaled to max |.| = 1,
+ * smallest singular value first (degstride >= the widest instance's column count). */
+#define PINT_EIG_MAXDEG 8
+int pint_solve_eig(pint_ctx *ctx, int mode, const double *threshold, int32_t *ndeg, double *degvec,
+                   int degstride);
+
 /* Likelihood normalisation per instance, Residuals.calc_chi2(lognorm=True)
  * (residuals.py:567-589, :638-667): gls != 0 gives logdet(C)/2 of the last pint_chi2_gls
  * (C = N + U Phi U^T, U = [F, ECORR, 1], utils.py:3074 woodbury_dot), gls == 2 the same

@@ -14,11 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
+EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
 B_NPAR = 22
 
 COL_OFFSET, COL_F, COL_LON, COL_LAT, COL_PMLON, COL_PMLAT, COL_PX, COL_DM, COL_DMX, COL_FD, COL_JUMP, COL_BIN = range(12)
 
-PINT_OK, PINT_E_INVALID, PINT_E_HIP, PINT_E_NOT_PD, PINT_E_KEPLER, PINT_E_PARAM = range(6)
+PINT_OK, PINT_E_INVALID, PINT_E_HIP, PINT_E_NOT_PD, PINT_E_KEPLER, PINT_E_PARAM, PINT_E_SIGMA = range(7)
 
 dptr = C.POINTER(C.c_double)
 
@@ -84,6 +85,7 @@ def lib():
     L.pint_fit_layout.argtypes = [vp, C.c_int, C.POINTER(C.c_int32)]
     L.pint_vgram_layout.argtypes = [vp, C.c_int, C.POINTER(C.c_int32)]
     L.pint_lognorm.argtypes = [vp, C.c_int, dptr]
+    L.pint_solve_eig.argtypes = [vp, C.c_int, dptr, C.POINTER(C.c_int32), dptr, C.c_int]
     L.pint_host_alloc.restype = vp
     L.pint_host_alloc.argtypes = [C.c_size_t]
     L.pint_host_free.argtypes = [vp]
@@ -99,7 +101,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_devi
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",
             "pint_set_option", "pint_host_alloc", "pint_host_free",
             "pint_fit_layout", "pint_query", "pint_capture_begin", "pint_capture_end", "pint_graph_launch",
-            "pint_vgram_layout", "pint_lognorm"]
+            "pint_vgram_layout", "pint_lognorm", "pint_solve_eig"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
         }
         __syncthreads();
         if (chol_lds(Sg, Dg, Kn, tg)) {
-            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
             return;
         }
         trinv_lds(Sg, Dg, Kn, tg);  // k_wsolve applies L^-1 as a matrix-vector product
@@ -1642,7 +1642,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const GramView G = gram_view(Pd, I, Gpart, Pd.dsplit != 0, Sd, DD);
         if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff))
-            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
         return;
     }
     const int inst = blockIdx.x;
@@ -1874,6 +1874,193 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     TS(6);
 }
 
+// ---------------------------------------------------------------------------------
+// k_eig: the SVD path of the fitters for degenerate normal equations (fitter.py:1282-1359
+// WLSState.step: SVD of the whitened normalised M, singular values <= threshold * s_max
+// dropped; fitter.py:2196-2230 GLSFitter: Cholesky, on failure SVD of mtcm).  The
+// normalised normal matrix A (= M^T M for WLS, mtcm for GLS) is symmetric, so its SVD is
+// its eigendecomposition: cyclic Jacobi with the round-robin ordering (K/2 disjoint
+// rotations per round, applied as a row pass and a column pass), one 1024-thread
+// workgroup per instance, A and V in global scratch (K x K each).  WLS: s = sqrt(lambda);
+// GLS: s = |lambda|; directions with s <= threshold * s_max are dropped and reported.
+// ---------------------------------------------------------------------------------
+constexpr int EIG_T = 1024;
+constexpr int EIG_MAXDEG = PINT_EIG_MAXDEG;
+__global__ __launch_bounds__(EIG_T) void k_eig(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                               const double* __restrict__ Gpart, const double* __restrict__ colsq,
+                                               int nsplit, int mode, int compact, const double* __restrict__ Sd,
+                                               const double* __restrict__ DD, const double* __restrict__ DCS,
+                                               const double* __restrict__ thresholds, double* __restrict__ work,
+                                               long wstride,
+                                               double* __restrict__ dpars, double* __restrict__ errs,
+                                               double* __restrict__ cov, double* __restrict__ chi2lin,
+                                               int* __restrict__ ndeg, double* __restrict__ degvec, int degstride) {
+    extern __shared__ double lds[];
+    __shared__ double sh[EIG_T / 64];
+    __shared__ int sflag;
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int Kfull = I.K, ncol = S.ncol;
+    const int K = (mode == 0) ? ncol : Kfull;
+    const int Ke = (K + 1) & ~1;  // even: one dummy index when K is odd
+    const bool cmp = compact && Pd.dsplit;
+    const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);
+    double* A = work + (long)inst * wstride;  // K x K, row-major
+    double* V = A + (long)K * K;              // K x K, columns = eigenvectors
+    double* nrm = lds;                        // K
+    double* bv = nrm + K;                     // K
+    double* cs = bv + K;                      // Ke/2 cosines
+    double* sn = cs + Ke / 2;                 // Ke/2 sines
+    double* lam = sn + Ke / 2;                // K
+    double* xh = lam + K;                     // K
+    const int tid = threadIdx.x;
+    for (int j = tid; j < K; j += EIG_T) {
+        double v = sqrt(mode == 0 ? G(j, j) : colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j));
+        nrm[j] = (v == 0.0) ? 1.0 : v;
+    }
+    __syncthreads();
+    for (long e = tid; e < (long)K * K; e += EIG_T) {
+        const int i = (int)(e / K), j = (int)(e % K);
+        double v = G(i, j) / (nrm[i] * nrm[j]);
+        if (i == j && mode == 1 && i >= ncol) v += 1.0 / Pd.red_phi[i - ncol] / (nrm[i] * nrm[i]);
+        A[e] = v;
+        V[e] = (i == j) ? 1.0 : 0.0;
+    }
+    for (int j = tid; j < K; j += EIG_T) bv[j] = G(j, Kfull) / nrm[j];
+    const double rwr = G(Kfull, Kfull);
+    __syncthreads();
+    double fro = 0.0;
+    for (long e = tid; e < (long)K * K; e += EIG_T) fro += A[e] * A[e];
+    fro = block_sum<EIG_T / 64>(fro, sh);
+    for (int sweep = 0; sweep < 40; sweep++) {
+        double off = 0.0;
+        for (long e = tid; e < (long)K * K; e += EIG_T)
+            if (e / K != e % K) off += A[e] * A[e];
+        off = block_sum<EIG_T / 64>(off, sh);
+        if (off <= 1e-30 * fro || off == 0.0) break;
+        for (int r = 0; r < Ke - 1; r++) {
+            // round-robin pairs: position 0 fixed, positions 1..Ke-1 rotated by r
+            auto at = [&](int k) { return k == 0 ? 0 : 1 + (k - 1 + r) % (Ke - 1); };
+            for (int k = tid; k < Ke / 2; k += EIG_T) {
+                int p = at(k), q = at(Ke - 1 - k);
+                if (p > q) { const int t = p; p = q; q = t; }
+                double c = 1.0, s = 0.0;
+                if (q < K) {
+                    const double apq = A[(long)p * K + q];
+                    if (apq != 0.0) {
+                        const double tau = (A[(long)q * K + q] - A[(long)p * K + p]) / (2.0 * apq);
+                        const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        s = t * c;
+                    }
+                }
+                cs[k] = c;
+                sn[k] = s;
+            }
+            __syncthreads();
+            // rows: p' = c p - s q, q' = s p + c q (J^T A)
+            for (long e = tid; e < (long)(Ke / 2) * K; e += EIG_T) {
+                const int k = (int)(e / K), j = (int)(e % K);
+                int p = at(k), q = at(Ke - 1 - k);
+                if (p > q) { const int t = p; p = q; q = t; }
+                if (q >= K || sn[k] == 0.0) continue;
+                const double c = cs[k], s = sn[k];
+                const double ap = A[(long)p * K + j], aq = A[(long)q * K + j];
+                A[(long)p * K + j] = c * ap - s * aq;
+                A[(long)q * K + j] = s * ap + c * aq;
+            }
+            __syncthreads();
+            // columns of A and V: p' = c p - s q, q' = s p + c q (A J, V J)
+            for (long e = tid; e < (long)(Ke / 2) * K; e += EIG_T) {
+                const int k = (int)(e / K), i = (int)(e % K);
+                int p = at(k), q = at(Ke - 1 - k);
+                if (p > q) { const int t = p; p = q; q = t; }
+                if (q >= K || sn[k] == 0.0) continue;
+                const double c = cs[k], s = sn[k];
+                double ap = A[(long)i * K + p], aq = A[(long)i * K + q];
+                A[(long)i * K + p] = c * ap - s * aq;
+                A[(long)i * K + q] = s * ap + c * aq;
+                ap = V[(long)i * K + p];
+                aq = V[(long)i * K + q];
+                V[(long)i * K + p] = c * ap - s * aq;
+                V[(long)i * K + q] = s * ap + c * aq;
+            }
+            __syncthreads();
+        }
+    }
+    // singular values and the dropped directions
+    for (int j = tid; j < K; j += EIG_T) lam[j] = A[(long)j * K + j];
+    __syncthreads();
+    const double threshold = thresholds[inst];
+    double smax = 0.0;
+    for (int j = 0; j < K; j++) {
+        const double sv = mode == 0 ? sqrt(fmax(lam[j], 0.0)) : fabs(lam[j]);
+        smax = fmax(smax, sv);
+    }
+    auto bad = [&](int j) {
+        const double sv = mode == 0 ? sqrt(fmax(lam[j], 0.0)) : fabs(lam[j]);
+        return !(sv > threshold * smax);
+    };
+    // xhat = sum_good V_j (V_j . b) / lambda_j
+    for (int j = tid; j < K; j += EIG_T) {
+        double pr = 0.0;
+        if (!bad(j)) {
+            for (int i = 0; i < K; i++) pr += V[(long)i * K + j] * bv[i];
+            pr /= lam[j];
+        }
+        xh[j] = pr;  // coefficient of eigenvector j
+    }
+    __syncthreads();
+    double bx = 0.0;
+    for (int i = tid; i < K; i += EIG_T) {
+        double x = 0.0;
+        for (int j = 0; j < K; j++) x += V[(long)i * K + j] * xh[j];
+        dpars[I.coff + i] = x / nrm[i];
+        bx += bv[i] * x;
+    }
+    bx = block_sum<EIG_T / 64>(bx, sh);
+    if (tid == 0) chi2lin[inst] = rwr - bx;
+    // xvar = sum_good V_j V_j^T / s_j (s_j = lambda_j for WLS, |lambda_j| for GLS)
+    double* C = cov + (long)I.cvoff;
+    for (long e = tid; e < (long)K * K; e += EIG_T) {
+        const int i = (int)(e / K), l = (int)(e % K);
+        if (i > l) continue;
+        if (l >= ncol && i != l) continue;  // timing block + the diagonal
+        double v = 0.0;
+        for (int j = 0; j < K; j++)
+            if (!bad(j)) v += V[(long)i * K + j] * V[(long)l * K + j] / fabs(lam[j]);
+        const double vv = v / (nrm[i] * nrm[l]);
+        if (l < ncol) {
+            C[(long)i * ncol + l] = vv;
+            C[(long)l * ncol + i] = vv;
+        }
+        if (i == l) errs[I.coff + i] = sqrt(v) / nrm[i];
+    }
+    // dropped directions, smallest singular value first, each scaled to max |component| = 1
+    if (tid == 0) {
+        int nd = 0;
+        unsigned long long used[4] = {0, 0, 0, 0};
+        while (nd < EIG_MAXDEG) {
+            int best = -1;
+            for (int j = 0; j < K; j++)
+                if (bad(j) && !((used[j >> 6] >> (j & 63)) & 1) &&
+                    (best < 0 || fabs(lam[j]) < fabs(lam[best])))
+                    best = j;
+            if (best < 0) break;
+            used[best >> 6] |= 1ull << (best & 63);
+            double mx = 0.0;
+            for (int i = 0; i < K; i++) mx = fmax(mx, fabs(V[(long)i * K + best]));
+            double* out = degvec + ((long)inst * EIG_MAXDEG + nd) * degstride;
+            for (int i = 0; i < K; i++) out[i] = V[(long)i * K + best] / (mx > 0 ? mx : 1.0);
+            nd++;
+        }
+        ndeg[inst] = nd;
+        sflag = nd;
+    }
+}
+
 // k_sigma: the Woodbury Sigma factor of every GLS instance (woodbury_sigma), launched on a
 // side stream right after the Gram so it runs on the CUs the per-instance solve leaves idle.
 template <int NW>
@@ -1894,7 +2081,7 @@ __global__ __launch_bounds__(NW * 64) void k_sigma(const PsrDev* __restrict__ ps
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const GramView G = gram_view(Pd, I, Gpart, compact && Pd.dsplit, Sd, DD);
     if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff)) {
-        if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
     }
 }
 
@@ -2140,6 +2327,10 @@ struct pint_ctx {
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
     double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
     double* d_lognorm = nullptr;  // per instance: logdet(C)/2 of the last pint_chi2_gls
+    double *d_eigw = nullptr, *d_degv = nullptr;  // k_eig scratch and dropped directions
+    int* d_ndeg = nullptr;
+    size_t eig_cap = 0;
+    int degv_cap = 0;
     InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
     double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
     int max_ndc = 0;
@@ -2227,7 +2418,8 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
-                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
+                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_eigw,
+                   (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
@@ -2239,6 +2431,8 @@ static void free_instances(pint_ctx* ctx) {
     ctx->graph = nullptr;
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
+    ctx->eig_cap = 0;
+    ctx->degv_cap = 0;
 }
 
 void pint_ctx_destroy(pint_ctx* ctx) {
@@ -2727,6 +2921,7 @@ static int check_status(pint_ctx* ctx) {
     // the status word accumulates error bits of everything enqueued since the last check
     if (st) HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
     if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
+    if (st & (1 << PINT_E_SIGMA)) { ctx->err = "Woodbury Sigma (noise basis) not positive definite"; return PINT_E_SIGMA; }
     if (st & (1 << PINT_E_NOT_PD)) { ctx->err = "normal matrix not positive definite"; return PINT_E_NOT_PD; }
     if (st) { ctx->err = "device status " + std::to_string(st); return PINT_E_PARAM; }
     return PINT_OK;
@@ -3042,6 +3237,49 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     int rc = check_status(ctx);
     update_timings(ctx);
     return rc;
+}
+
+// The SVD path of the fitters (k_eig) on the Gram of the last pint_fit_step: replaces the
+// step, errors, covariance and linearised chi2 of every instance; ndeg[i] dropped directions
+// of instance i (<= PINT_EIG_MAXDEG), degvec[(i * PINT_EIG_MAXDEG + d) * (K_i) ...] their
+// components over the instance's columns (stride degstride >= max K).
+int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* ndeg, double* degvec, int degstride) {
+    if (!ctx || ctx->ninst <= 0 || (mode != 0 && mode != 1) || !threshold) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    int maxK = 0;
+    for (auto& I : ctx->inst) maxK = std::max(maxK, mode == 0 ? ctx->psrs[I.psr].spec.ncol : I.K);
+    if (degstride < maxK) { ctx->err = "degstride < columns"; return PINT_E_INVALID; }
+    const long wstride = 2L * maxK * maxK;
+    if ((size_t)(wstride * ctx->ninst) > ctx->eig_cap) {
+        dfree((void*&)ctx->d_eigw);
+        HIPCHK(hipMalloc(&ctx->d_eigw, sizeof(double) * wstride * ctx->ninst));
+        ctx->eig_cap = wstride * ctx->ninst;
+        dfree((void*&)ctx->d_ndeg);
+        dfree((void*&)ctx->d_degv);
+        HIPCHK(hipMalloc(&ctx->d_ndeg, sizeof(int) * ctx->ninst));
+        HIPCHK(hipMalloc(&ctx->d_degv, sizeof(double) * ctx->ninst * PINT_EIG_MAXDEG * (size_t)maxK));
+        ctx->degv_cap = maxK;
+    }
+    if (ctx->degv_cap < maxK) { ctx->err = "eig scratch too small"; return PINT_E_INVALID; }
+    const size_t lds = sizeof(double) * (4 * (size_t)maxK + maxK + 2);
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
+    HIPCHK(hipMemcpyAsync(ctx->d_lam, threshold, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_eig, dim3(ctx->ninst), dim3(EIG_T), lds, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
+                       ctx->d_colsq, ctx->nsplit, mode, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_lam,
+                       ctx->d_eigw, wstride, ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_ndeg,
+                       ctx->d_degv, ctx->degv_cap);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ndeg, ctx->d_ndeg, sizeof(int) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<double> tmp((size_t)ctx->ninst * PINT_EIG_MAXDEG * ctx->degv_cap);
+    HIPCHK(hipMemcpyAsync(tmp.data(), ctx->d_degv, sizeof(double) * tmp.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < ctx->ninst; i++)
+        for (int d = 0; d < PINT_EIG_MAXDEG; d++)
+            for (int k = 0; k < maxK; k++)
+                degvec[((long)i * PINT_EIG_MAXDEG + d) * degstride + k] =
+                    tmp[((size_t)i * PINT_EIG_MAXDEG + d) * ctx->degv_cap + k];
+    return PINT_OK;
 }
 
 int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, double* chi2lin) {

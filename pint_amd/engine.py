@@ -540,6 +540,23 @@ class Session:
         self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
         return c if self.lazy else c.copy()
 
+    def solve_eig(self, mode, thresholds):
+        """SVD path of the fitters on the last fit_step's Gram (k_eig): replaces the step
+        outputs; returns, per instance, the dropped directions (list of arrays over the
+        instance's fit columns, smallest singular value first)."""
+        n = len(self.inst_layout)
+        th = np.ascontiguousarray(np.broadcast_to(np.asarray(thresholds, dtype=np.float64), (n,)))
+        kmax = max((len(l.columns) if mode == 0 else l.K) for l in self.inst_layout)
+        nd = np.zeros(n, dtype=np.int32)
+        dv = np.zeros(n * L.EIG_MAXDEG * kmax)
+        self._check(self.L.pint_solve_eig(self.ctx, int(mode), L.ptr(th), L.ptr(nd, C.c_int32), L.ptr(dv), kmax))
+        dv = dv.reshape(n, L.EIG_MAXDEG, kmax)
+        out = []
+        for k, lay in enumerate(self.inst_layout):
+            kk = len(lay.columns) if mode == 0 else lay.K
+            out.append([dv[k, d, :kk].copy() for d in range(nd[k])])
+        return out
+
     def lognorm(self, gls):
         """Per-instance likelihood normalisation: logdet(C)/2 of the last chi2_gls (gls=1), of
         C = N + 1e40 11^T (gls=2: correlated model, no basis columns) or sum log sigma (gls=0)

@@ -10,10 +10,12 @@ points, PTA pulsars) through one launch sequence per iteration.
 from __future__ import annotations
 
 import copy
+import warnings
 from typing import List, Optional, Sequence
 
 import numpy as np
 
+from . import _lib as L
 from .engine import Session, build_layout, pack_table, unpack_table
 
 
@@ -72,11 +74,19 @@ class BatchFit:
     """
 
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
-                 layouts=None, tables=None):
+                 layouts=None, tables=None, threshold=None, degeneracy_style=None):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
-        are bare parameter tables of already-uploaded pulsars, e.g. grid points)."""
+        are bare parameter tables of already-uploaded pulsars, e.g. grid points).
+
+        threshold: the SVD cut of the reference fitter (fitter.py:1314 WLS: None ->
+        1e-14 max(N, P); GLS: 0); used when the normal equations are degenerate.
+        degeneracy_style: the DegeneracyWarning text of "wls" (WLSState), "gls"
+        (GLSFitter) or "glsstate" (GLSState, the downhill GLS fitter)."""
         self.items = list(items) if items is not None else None
         self.mode = mode
+        self.threshold = threshold
+        self.degeneracy_style = degeneracy_style or mode
+        self.degenerate = None  # per instance: dropped directions of the last SVD-path step
         self.gls = mode == "gls"
         self.s = session or Session()
         if layouts is None:
@@ -108,7 +118,45 @@ class BatchFit:
 
     def _step(self):
         self.s.eval(want_M=Session.FIT)
-        self.s.fit_step(1 if self.gls else 0)
+        try:
+            self.s.fit_step(1 if self.gls else 0)
+        except L.PintError as e:
+            if e.code != L.PINT_E_NOT_PD or self.s.lazy:
+                raise
+            self._svd_step()
+
+    def _thresholds(self):
+        if self.threshold is not None:
+            return np.full(self.ninst, float(self.threshold))
+        if self.gls:
+            return np.zeros(self.ninst)
+        return np.array([1e-14 * max(l.n, len(l.columns)) for l in self.layouts])
+
+    def _svd_step(self):
+        """Degenerate normal equations: the reference's SVD path (fitter.py:1282-1359 WLS,
+        :2196-2230 GLSFitter, :1477-1500 GLSState) on the device (k_eig): directions with
+        singular values <= threshold * s_max are dropped, each reported as a
+        DegeneracyWarning with the reference's wording."""
+        th = self._thresholds()
+        dirs = self.s.solve_eig(1 if self.gls else 0, th)
+        self.degenerate = dirs
+        for k, (lay, vs) in enumerate(zip(self.layouts, dirs)):
+            params = list(lay.columns)
+            t = th[k]
+            for v in vs:
+                pairs = list(zip(v[:len(params)], params))
+                if self.degeneracy_style == "wls":
+                    comb = " + ".join(f"{co}*{p}" for (co, p) in sorted(pairs) if abs(co) > t)
+                    msg = f"Parameter degeneracy; the following linear combination yields almost no change: {comb}"
+                elif self.degeneracy_style == "glsstate":
+                    comb = " ".join(f"{p}" for (co, p) in sorted(pairs) if abs(co) > t)
+                    msg = ("Parameter degeneracy; the following combination of parameters yields almost no "
+                           f"change: {comb}")
+                else:
+                    comb = " ".join(f"{co}*{p}" for (co, p) in reversed(sorted(pairs)) if abs(co) > t)
+                    msg = ("Parameter degeneracy; the following combination of parameters yields almost no "
+                           f"change: {comb}")
+                warnings.warn(msg, DegeneracyWarning)
 
     def _finish(self, results):
         tabs = self.s.read_tables()
@@ -251,8 +299,8 @@ class Fitter:
     def get_designmatrix(self):
         return self.model.designmatrix(self.toas)
 
-    def _run(self, mode, plain=True, **kw):
-        bf = BatchFit([(self.model, self.toas)], mode=mode)
+    def _run(self, mode, plain=True, threshold=None, style=None, **kw):
+        bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style)
         try:
             res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
         finally:
@@ -273,7 +321,7 @@ class WLSFitter(Fitter):
     def fit_toas(self, maxiter=1, threshold=None, debug=False):
         if self.model.has_correlated_errors:
             pass  # the reference WLSFitter ignores correlated noise
-        res = self._run("wls", plain=True, maxiter=maxiter)
+        res = self._run("wls", plain=True, maxiter=maxiter, threshold=threshold, style="wls")
         return res.chi2
 
 
@@ -281,7 +329,7 @@ class GLSFitter(Fitter):
     def fit_toas(self, maxiter=1, threshold=0, full_cov=False, debug=False):
         if full_cov:
             raise NotImplementedError("full_cov=True (dense N x N covariance) is outside the GPU path")
-        res = self._run("gls", plain=True, maxiter=maxiter)
+        res = self._run("gls", plain=True, maxiter=maxiter, threshold=threshold, style="gls")
         return res.chi2
 
 
@@ -289,11 +337,15 @@ class DownhillFitter(Fitter):
     mode = "wls"
 
     def fit_toas(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,
-                 debug=False, **kw):
+                 debug=False, threshold=None, **kw):
         # fitter.py:1168-1175: no free noise params -> required_chi2_decrease passed as
-        # both max_chi2_increase and min_lambda
+        # both max_chi2_increase and min_lambda; threshold: WLSState (None -> 1e-14 max(N, P))
+        # or GLSState (fitter.py:1554 default 0)
+        if threshold is None and self.mode == "gls":
+            threshold = 0.0
         res = self._run(self.mode, plain=False, maxiter=maxiter, required_chi2_decrease=required_chi2_decrease,
-                        max_chi2_increase=required_chi2_decrease, min_lambda=required_chi2_decrease)
+                        max_chi2_increase=required_chi2_decrease, min_lambda=required_chi2_decrease,
+                        threshold=threshold, style="wls" if self.mode == "wls" else "glsstate")
         if res.status == "StepProblem":
             raise StepProblem("Unable to improve chi2 even with very small steps")
         if not res.converged:

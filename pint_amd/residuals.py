@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from . import _lib as L
 from .engine import Session, build_layout, pack_table
 
 
@@ -43,7 +44,11 @@ class Residuals:
             self.phase_resids = pr[0]
             self._sigma_us = lay.sigma_us
             if corr:
-                s.fit_step(1)
+                try:  # the step only provides the Woodbury factor; a degenerate timing solve is irrelevant
+                    s.fit_step(1)
+                except L.PintError as e:
+                    if e.code != L.PINT_E_NOT_PD:
+                        raise
                 self._chi2 = float(s.chi2_gls()[0])
             else:
                 self._chi2 = float(c2[0])

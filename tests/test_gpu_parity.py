@@ -457,3 +457,71 @@ def test_lnlikelihood(fx):
     assert abs(ln - meta["res_lognorm"]) <= 1e-9 * abs(meta["res_lognorm"]), (ln, meta["res_lognorm"])
     ref = meta["res_lnlikelihood"]
     assert abs(r.lnlikelihood() - ref) <= 1e-6 * abs(meta["res_chi2"]) + 1e-9 * abs(ref)
+
+
+@pytest.mark.parametrize("name", ["ngc6440e", "pta_dd", "b1855"])
+def test_svd_path_matches_cholesky(name):
+    """k_eig (the fitters' SVD path: Jacobi eigendecomposition of the normalised normal
+    matrix on the device) on a well-conditioned system keeps every direction and gives the
+    Cholesky step, errors and covariance (to the system's conditioning)."""
+    from pint_amd.fitter import BatchFit
+    model, toas, z, meta = load(name)
+    gls = name != "ngc6440e"
+    bf = BatchFit([(copy.deepcopy(model), toas)], mode="gls" if gls else "wls")
+    bf._step()
+    d1, e1, c1, l1 = [x[0].copy() if isinstance(x, list) else x.copy() for x in bf.s.read_step()]
+    th = bf._thresholds()
+    dirs = bf.s.solve_eig(1 if gls else 0, th)
+    assert dirs == [[]]
+    d2, e2, c2, l2 = [x[0].copy() if isinstance(x, list) else x.copy() for x in bf.s.read_step()]
+    bf.close()
+    n = len(e1) - 1
+    tol = 1e-3 if name == "b1855" else 1e-8   # B1855: normalised cond ~1e12
+    assert np.max(np.abs((d1[:n] - d2[:n]) / e1[:n])) < tol
+    assert np.max(np.abs(e2[:n] / e1[:n] - 1)) < tol
+    sc = np.sqrt(np.outer(np.diag(c1), np.diag(c1)))
+    assert np.max(np.abs(c1 - c2) / sc) < tol
+
+
+@pytest.mark.parametrize("name,Fitter", [("ngc6440e", "WLSFitter"), ("pta_dd", "GLSFitter"),
+                                         ("pta_dd", "DownhillGLSFitter")])
+def test_degenerate_column_svd_path(name, Fitter):
+    """A free JUMP that selects no TOA is an all-zero design-matrix column: the normal
+    matrix is singular, Cholesky fails, and the SVD path (fitter.py:1282-1359 / 2196-2230 /
+    1477-1500) drops that direction with a DegeneracyWarning naming it; the other
+    parameters come out as in the fit without the JUMP."""
+    import pint_amd.fitter as F
+    from pint_amd import get_model
+    from golden_util import GOLDEN, PARS
+    import os
+    model, toas, z, meta = load(name)
+    par = open(os.path.join(GOLDEN, PARS[name])).read() + "\nJUMP -fe NO_SUCH_RECEIVER 0 1\n"
+    mj = get_model(par)
+    mj.free_params = list(model.free_params) + ["JUMP1"]
+    cls = getattr(F, Fitter)
+    f0 = cls(toas, copy.deepcopy(model))
+    fj = cls(toas, mj)
+    with pytest.warns(F.DegeneracyWarning, match="JUMP1"):
+        if "Downhill" in Fitter:
+            try:
+                fj.fit_toas()
+            except F.MaxiterReached:
+                pass
+        else:
+            fj.fit_toas()
+    if "Downhill" in Fitter:
+        try:
+            f0.fit_toas()
+        except F.MaxiterReached:
+            pass
+    else:
+        f0.fit_toas()
+    assert fj.model["JUMP1"].value == 0.0
+    # eigen- vs Cholesky solve: rounding-level differences, which the downhill iterations
+    # carry through several steps
+    tol = 1e-4 if "Downhill" in Fitter else 1e-6
+    for p in model.free_params:
+        e = f0.model[p].uncertainty
+        d = float((np.longdouble(fj.model[p].value) - np.longdouble(f0.model[p].value)) / np.longdouble(e))
+        assert abs(d) < tol, (p, d)
+        assert abs(fj.model[p].uncertainty / e - 1) < tol, p
