@@ -19,6 +19,10 @@ from .fitter import (BatchFit, DownhillFitter, GLSFitter, DownhillGLSFitter, WLS
 from .parameter import LD
 
 
+GRID_BATCH_BYTES = 24e9   # device bytes one batch of grid points may take
+GRID_MAX_POINTS = None    # optional cap on points per batch
+
+
 def _fit_kind(ftr):
     gls = isinstance(ftr, (GLSFitter, DownhillGLSFitter))
     down = isinstance(ftr, DownhillFitter)
@@ -86,27 +90,34 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
         try:
             lay = s.add(build_layout(base, ftr.toas, use_gls_basis=(mode == "gls")))
             t0 = pack_table(lay, base)
-            tabs = np.tile(t0, (hi - lo, 1))
-            for p, vals in zip(parnames, flat):
-                v = np.asarray(vals[lo:hi], dtype=np.longdouble)
-                h = v.astype(np.float64)
-                l = (v - h.astype(np.longdouble)).astype(np.float64)
-                o = lay.offsets[p]
-                tabs[:, o] = h
-                tabs[:, o + 1] = l
-            bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (hi - lo), tables=list(tabs))
-            if down:
-                rq = fitargs.get("required_chi2_decrease", 1e-2)
-                res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
-                                      max_chi2_increase=rq, min_lambda=rq)
-            else:
-                res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1))
-            for k, r in enumerate(res):
-                # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
-                chi2[k] = np.nan if (down and r.status == "MaxiterReached") else r.chi2
-            for e in extraparnames:
-                o = lay.offsets[e]
-                extra[e][:] = [float(np.longdouble(t[o]) + np.longdouble(t[o + 1])) for t in bf.final_tables]
+            # points per batch: ~24 GB of per-instance device buffers (eval rows, design matrix,
+            # Gram partials) per batch keeps any grid within HBM
+            per_pt = 8.0 * (lay.n * (lay.K + 12) + 64 * (lay.K + 2) ** 2)
+            chunk = int(max(1, min(hi - lo, GRID_BATCH_BYTES // per_pt, GRID_MAX_POINTS or hi - lo)))
+            for c0 in range(lo, hi, chunk):
+                c1 = min(hi, c0 + chunk)
+                tabs = np.tile(t0, (c1 - c0, 1))
+                for p, vals in zip(parnames, flat):
+                    v = np.asarray(vals[c0:c1], dtype=np.longdouble)
+                    h = v.astype(np.float64)
+                    l = (v - h.astype(np.longdouble)).astype(np.float64)
+                    o = lay.offsets[p]
+                    tabs[:, o] = h
+                    tabs[:, o + 1] = l
+                bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (c1 - c0), tables=list(tabs))
+                if down:
+                    rq = fitargs.get("required_chi2_decrease", 1e-2)
+                    res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
+                                          max_chi2_increase=rq, min_lambda=rq)
+                else:
+                    res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1))
+                for k, r in enumerate(res):
+                    # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
+                    chi2[c0 - lo + k] = np.nan if (down and r.status == "MaxiterReached") else r.chi2
+                for e in extraparnames:
+                    o = lay.offsets[e]
+                    extra[e][c0 - lo:c1 - lo] = [float(np.longdouble(t[o]) + np.longdouble(t[o + 1]))
+                                                 for t in bf.final_tables]
         finally:
             s.close()
     chi2_all = gather_blocks(chi2, per, npts, dist)

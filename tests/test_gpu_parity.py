@@ -154,6 +154,15 @@ def test_grid_chisq_ngc():
     c2, _ = grid_chisq(f, ("F0", "F1"), (g0, g1))
     assert c2.shape == z["grid_chi2_parallel"].shape
     assert np.allclose(c2, z["grid_chi2_parallel"], rtol=1e-7, atol=0)
+    # the same grid in batches of 7 points (memory-budget chunking) gives the same chi2
+    from pint_amd import gridutils
+    old = gridutils.GRID_MAX_POINTS
+    gridutils.GRID_MAX_POINTS = 7
+    try:
+        c2c, _ = grid_chisq(f, ("F0", "F1"), (g0, g1))
+    finally:
+        gridutils.GRID_MAX_POINTS = old
+    assert np.allclose(c2c, c2, rtol=1e-12, atol=0)
 
 
 # ---- seeded perturbations against the oracle --------------------------------------------
