@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--ntoas", type=int, default=10000)
     ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--j0740", type=int, default=32,
+    ap.add_argument("--j0740", type=int, default=256,
                     help="(M2, SINI) grid side of the C3/C4 J0740 legs (0 = skip)")
     args = ap.parse_args()
 
@@ -273,18 +273,12 @@ def grid_leg(side, rank, world, dist, barrier):
             "chi2_min": float(np.nanmin(chi2))}
 
 
-def j0740_legs(side, rank, world, dist, barrier):
-    """C3 and the second C4 shape: J0740+6620 (ELL1 + Shapiro, 68 DMX, ECORR)
-    on 50k synthetic TOAs (make_fake_toas_uniform 56640-58461, 820/1400 MHz alternating, 1 us,
-    noise, flags -f Rcvr1_2_GUPPI -fe Rcvr1_2, seed 0), empty DMX/JUMP masks frozen
-    (find_empty_masks(freeze=True)).  C3: one DownhillGLSFitter(maxiter=10) fit, timed.
-    C4: grid_chisq over (M2, SINI) side x side, M2 in [0.2, 0.3] Msun, SINI = sin(86.25..88.5
-    deg) (profiling/bench_chisq_grid.py:33-35), GLSFitter per point, sharded over ranks."""
-    import copy
-    from pint_amd import DownhillGLSFitter, GLSFitter
+def j0740_data():
+    """C3 data: J0740+6620 (ELL1 + Shapiro, 68 DMX, ECORR) on 50k synthetic TOAs
+    (make_fake_toas_uniform 56640-58461, 820/1400 MHz alternating, 1 us, noise, flags
+    -f Rcvr1_2_GUPPI -fe Rcvr1_2, seed 0), empty DMX/JUMP masks frozen (the reference's
+    find_empty_masks(freeze=True) step of the C3 setup)."""
     from pint_amd import simulation as sim
-    from pint_amd.fitter import MaxiterReached
-    from pint_amd.gridutils import grid_chisq
     from pint_amd.timing_model import get_model
     model = get_model(os.path.join(ROOT, "tests", "golden", "J0740+6620.par"))
     toas = sim.make_fake_toas_uniform(56640, 58461, 50000, model, freq=[820.0, 1400.0], obs="geocenter",
@@ -303,6 +297,19 @@ def j0740_legs(side, rank, world, dist, barrier):
         if len(toas.select_mask(p.key, p.key_value)) == 0:
             p.frozen = True
             frozen.append(n)
+    return model, toas, frozen
+
+
+def j0740_legs(side, rank, world, dist, barrier):
+    """C3 and the second C4 shape on j0740_data().  C3: one
+    DownhillGLSFitter(maxiter=10) fit, timed.  C4: grid_chisq over (M2, SINI) side x side,
+    M2 in [0.2, 0.3] Msun, SINI = sin(86.25..88.5 deg) (profiling/bench_chisq_grid.py:33-35),
+    GLSFitter per point, sharded over ranks."""
+    import copy
+    from pint_amd import DownhillGLSFitter, GLSFitter
+    from pint_amd.fitter import MaxiterReached
+    from pint_amd.gridutils import grid_chisq
+    model, toas, frozen = j0740_data()
     out = {"workload": "J0740+6620 synthetic 50k TOAs (C3)", "free_params": len(model.free_params),
            "frozen_empty": len(frozen)}
     f = DownhillGLSFitter(toas, copy.deepcopy(model))
@@ -325,7 +332,7 @@ def j0740_legs(side, rank, world, dist, barrier):
     g.fit_toas(maxiter=1)
     m2 = np.linspace(0.2, 0.3, side)
     sini = np.sin(np.deg2rad(np.linspace(86.25, 88.5, side)))
-    grid_chisq(g, ("M2", "SINI"), (m2[:2], sini[:2]))  # warm-up
+    grid_chisq(g, ("M2", "SINI"), (m2, sini))  # warm-up (first-touch of the batch buffers)
     barrier()
     t0 = time.perf_counter()
     chi2, _ = grid_chisq(g, ("M2", "SINI"), (m2, sini))

@@ -107,6 +107,11 @@ typedef struct pint_ctx pint_ctx;
 pint_ctx *pint_ctx_create(int device);
 void pint_ctx_destroy(pint_ctx *ctx);
 const char *pint_last_error(pint_ctx *ctx);
+
+/* Instance buffers are drawn from a process-wide cache per device and returned to it by
+ * pint_set_instances / pint_ctx_destroy; this hands every idle cached buffer back to the
+ * HIP runtime (no reference counterpart: device memory management). */
+void pint_release_cache(void);
 int pint_device_count(void);
 
 /* Upload one pulsar (packed TOAs + model structure); returns its id >= 0, or -status.

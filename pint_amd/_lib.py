@@ -63,6 +63,8 @@ def lib():
     L.pint_ctx_destroy.argtypes = [vp]
     L.pint_last_error.restype = C.c_char_p
     L.pint_last_error.argtypes = [vp]
+    L.pint_release_cache.restype = None
+    L.pint_release_cache.argtypes = []
     L.pint_device_count.restype = C.c_int
     L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
     L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
@@ -95,7 +97,7 @@ def lib():
     return L
 
 
-EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_device_count", "pint_add_pulsar",
+EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_release_cache", "pint_device_count", "pint_add_pulsar",
             "pint_set_instances", "pint_get_tables", "pint_set_tables", "pint_eval", "pint_read_resids",
             "pint_read_eval", "pint_read_designmatrix", "pint_fit_step", "pint_read_step", "pint_apply_step",
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",

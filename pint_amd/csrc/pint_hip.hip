@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include "physics.hpp"
 
 using namespace pint;
@@ -2222,12 +2224,17 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     }
     if (threadIdx.x == 0) d[R] = rw1 - erw1;
     __syncthreads();
-    // y = L^-1 d with the explicit inverse factor from k_solve (row dot products)
+    // y = L^-1 d with the explicit inverse factor from k_solve (row dot products); with no
+    // noise basis Sigma is the 1x1 [1e-40 + 1^T N^-1 1], which the solves do not factor
+    const bool nobasis = (R == 0 && nep == 0);
+    const double x00 = 1.0 / sqrt(1e-40 + Pd.sumw);
     const double* X = sigL + I.soff;
     double q = 0.0;
     for (int i = threadIdx.x; i < Kn; i += blockDim.x) {
         double s = 0.0;
-        for (int j = 0; j <= i; j++) s += X[tri(i, j)] * d[j];
+        if (nobasis) s = x00 * d[0];
+        else
+            for (int j = 0; j <= i; j++) s += X[tri(i, j)] * d[j];
         q += s * s;
     }
     q = block_sum<4>(q, sh);
@@ -2238,7 +2245,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     double ld = 0.0;
     for (int e = threadIdx.x; e < nep; e += blockDim.x) ld += log(Pd.ep_phi[e]) + log(eD[I.epoff + e]);
     for (int k = threadIdx.x; k < R; k += blockDim.x) ld += log(Pd.red_phi[k]);
-    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(X[tri(j, j)]);
+    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(nobasis ? x00 : X[tri(j, j)]);
     ld = block_sum<4>(ld, sh);
     if (threadIdx.x == 0) {
         chi2[inst] = (rwr - erwr) - q;
@@ -2350,9 +2357,103 @@ struct pint_ctx {
     float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
+// Per-instance buffers (eval rows, design matrices, Gram partials: tens of GB for a large
+// grid batch) go through a process-wide cache per device: hipMalloc/hipFree of that much
+// memory costs ~0.3 s per batch, while grid_chisq / Session re-creation re-requests the same
+// sizes.  Freed buffers stay mapped and are handed out again to a request of <= their size
+// (within 25%); a failed hipMalloc releases the cache and retries.  pint_release_cache()
+// returns it all to the runtime.  PINT_CACHE_POISON=1 fills every handed-out buffer with
+// NaN bytes (checks that no kernel reads memory it did not write).
+struct DevCache {
+    std::multimap<size_t, void*> idle;
+    std::map<void*, size_t> live;
+    size_t idle_bytes = 0;
+};
+static std::mutex g_cache_mu;
+static DevCache g_cache[64];
+static const size_t CACHE_MAX_IDLE = (size_t)128 << 30;
+static int g_poison = -1;
+
+static size_t cache_round(size_t b) {
+    if (b == 0) b = 8;
+    if (b >= ((size_t)1 << 20)) return (b + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+    return (b + 255) & ~(size_t)255;
+}
+
+static void cache_trim(int dev, size_t keep) {  // caller holds g_cache_mu
+    DevCache& c = g_cache[dev & 63];
+    while (c.idle_bytes > keep && !c.idle.empty()) {
+        auto it = std::prev(c.idle.end());  // largest first
+        hipFree(it->second);
+        c.idle_bytes -= it->first;
+        c.idle.erase(it);
+    }
+}
+
+static hipError_t cmalloc(void** p, size_t bytes) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    size_t b = cache_round(bytes);
+    if (g_poison < 0) {
+        const char* e = getenv("PINT_CACHE_POISON");
+        g_poison = (e && e[0] == '1') ? 1 : 0;
+    }
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    DevCache& c = g_cache[dev & 63];
+    *p = nullptr;
+    auto it = c.idle.lower_bound(b);
+    if (it != c.idle.end() && it->first <= b + b / 4) {
+        *p = it->second;
+        c.live[*p] = it->first;
+        c.idle_bytes -= it->first;
+        c.idle.erase(it);
+    } else {
+        hipError_t e = hipMalloc(p, b);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            cache_trim(dev, 0);
+            e = hipMalloc(p, b);
+            if (e != hipSuccess) return e;
+        }
+        c.live[*p] = b;
+    }
+    if (g_poison == 1) {
+        hipError_t e = hipMemset(*p, 0xff, b);
+        return e != hipSuccess ? e : hipDeviceSynchronize();  // ordered before any stream's use
+    }
+    return hipSuccess;
+}
+
 static void dfree(void*& p) {
-    if (p) hipFree(p);
+    if (!p) return;
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    DevCache& c = g_cache[dev & 63];
+    auto it = c.live.find(p);
+    if (it == c.live.end()) {
+        hipFree(p);
+    } else {
+        c.idle.emplace(it->second, p);
+        c.idle_bytes += it->second;
+        c.live.erase(it);
+        cache_trim(dev, CACHE_MAX_IDLE);
+    }
     p = nullptr;
+}
+
+extern "C" void pint_release_cache(void) {
+    int n = 0;
+    hipGetDeviceCount(&n);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (int d = 0; d < n && d < 64; d++) {
+        if (g_cache[d].idle.empty()) continue;
+        hipSetDevice(d);
+        cache_trim(d, 0);
+    }
+    hipSetDevice(cur);
 }
 
 template <typename T>
@@ -2413,6 +2514,10 @@ pint_ctx* pint_ctx_create(int device) {
 const char* pint_last_error(pint_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static void free_instances(pint_ctx* ctx) {
+    // the buffers go back to the device cache, where another context may take them
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
+    if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
@@ -2795,7 +2900,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     ctx->blk_off[3] = (int)bi.size();
     ctx->nblk = (int)bi.size();
-    HIPCHK(hipMalloc(&ctx->d_inst, sizeof(InstDev) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
     for (int lay = 0; lay < 3; lay++) {  // k_gram launch groups: full, compact, compact + vg
         std::vector<InstDev> sorted;
@@ -2822,7 +2927,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             if (g.count) groups.push_back(g);
         }
         InstDev*& dst = lay == 0 ? ctx->d_inst_sorted : (lay == 1 ? ctx->d_inst_sorted_c : ctx->d_inst_sorted_v);
-        HIPCHK(hipMalloc(&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
+        HIPCHK(cmalloc((void**)&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
         if (!sorted.empty())
             HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * sorted.size(), hipMemcpyHostToDevice));
     }
@@ -2833,43 +2938,46 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             fprintf(stderr, "[pint] psr %zu: vg %d r0 %d Kd %d ns %d kpv %d ndc %d nsplit %d\n", k, d.vg, d.red0c, d.Kd, d.vns, d.vkp, d.ndc, nsplit);
         }
     }
-    HIPCHK(hipMalloc(&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
-    HIPCHK(hipMalloc(&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
-    HIPCHK(hipMalloc(&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
-    HIPCHK(hipMalloc(&ctx->d_blk_inst, sizeof(int) * bi.size()));
-    HIPCHK(hipMalloc(&ctx->d_blk_row0, sizeof(int) * br.size()));
+    HIPCHK(cmalloc((void**)&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
+    HIPCHK(cmalloc((void**)&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
+    HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
+    HIPCHK(cmalloc((void**)&ctx->d_blk_inst, sizeof(int) * bi.size()));
+    HIPCHK(cmalloc((void**)&ctx->d_blk_row0, sizeof(int) * br.size()));
     HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_blk_row0, br.data(), sizeof(int) * br.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&ctx->d_tables, sizeof(double) * toff));
+    HIPCHK(cmalloc((void**)&ctx->d_tables, sizeof(double) * toff));
     HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&ctx->d_phhi, sizeof(double) * roff));
-    HIPCHK(hipMalloc(&ctx->d_phlo, sizeof(double) * roff));
-    HIPCHK(hipMalloc(&ctx->d_ftay, sizeof(double) * roff));
-    HIPCHK(hipMalloc(&ctx->d_delay, sizeof(double) * roff));
-    HIPCHK(hipMalloc(&ctx->d_M, sizeof(double) * (moff > 0 ? moff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_rt, sizeof(double) * out));
-    HIPCHK(hipMalloc(&ctx->d_rp, sizeof(double) * out));
-    HIPCHK(hipMalloc(&ctx->d_chi2, sizeof(double) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_chi2g, sizeof(double) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_lognorm, sizeof(double) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_chi2lin, sizeof(double) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_G, sizeof(double) * goff));
-    HIPCHK(hipMalloc(&ctx->d_colsq, sizeof(double) * coff * nsplit));
-    HIPCHK(hipMalloc(&ctx->d_work, sizeof(double) * soff));
-    HIPCHK(hipMalloc(&ctx->d_cov, sizeof(double) * (cvoff > 0 ? cvoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_sigL, sizeof(double) * soff));
-    HIPCHK(hipMalloc(&ctx->d_dpars, sizeof(double) * coff));
-    HIPCHK(hipMalloc(&ctx->d_errs, sizeof(double) * coff));
-    HIPCHK(hipMalloc(&ctx->d_lam, sizeof(double) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_ic, sizeof(InstConst) * ninst));
-    HIPCHK(hipMalloc(&ctx->d_dmxv, sizeof(double) * (out > 0 ? out : 1)));
-    HIPCHK(hipMalloc(&ctx->d_Sd, sizeof(double) * (sdoff > 0 ? sdoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_DD, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
-    HIPCHK(hipMalloc(&ctx->d_DCS, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_phhi, sizeof(double) * roff));
+    HIPCHK(cmalloc((void**)&ctx->d_phlo, sizeof(double) * roff));
+    HIPCHK(cmalloc((void**)&ctx->d_ftay, sizeof(double) * roff));
+    HIPCHK(cmalloc((void**)&ctx->d_delay, sizeof(double) * roff));
+    HIPCHK(cmalloc((void**)&ctx->d_M, sizeof(double) * (moff > 0 ? moff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_rt, sizeof(double) * out));
+    HIPCHK(cmalloc((void**)&ctx->d_rp, sizeof(double) * out));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2g, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_lognorm, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2lin, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_G, sizeof(double) * goff));
+    HIPCHK(cmalloc((void**)&ctx->d_colsq, sizeof(double) * coff * nsplit));
+    HIPCHK(cmalloc((void**)&ctx->d_work, sizeof(double) * soff));
+    HIPCHK(cmalloc((void**)&ctx->d_cov, sizeof(double) * (cvoff > 0 ? cvoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_sigL, sizeof(double) * soff));
+    HIPCHK(cmalloc((void**)&ctx->d_dpars, sizeof(double) * coff));
+    HIPCHK(cmalloc((void**)&ctx->d_errs, sizeof(double) * coff));
+    // the per-instance slot past the last column (K+1 stride) is never written by a solve
+    HIPCHK(hipMemsetAsync(ctx->d_dpars, 0, sizeof(double) * coff, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_errs, 0, sizeof(double) * coff, ctx->stream));
+    HIPCHK(cmalloc((void**)&ctx->d_lam, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_ic, sizeof(InstConst) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_dmxv, sizeof(double) * (out > 0 ? out : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_Sd, sizeof(double) * (sdoff > 0 ? sdoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_DD, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_DCS, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
     HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * (cvoff > 0 ? cvoff : 1), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -3252,12 +3360,12 @@ int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* nd
     const long wstride = 2L * maxK * maxK;
     if ((size_t)(wstride * ctx->ninst) > ctx->eig_cap) {
         dfree((void*&)ctx->d_eigw);
-        HIPCHK(hipMalloc(&ctx->d_eigw, sizeof(double) * wstride * ctx->ninst));
+        HIPCHK(cmalloc((void**)&ctx->d_eigw, sizeof(double) * wstride * ctx->ninst));
         ctx->eig_cap = wstride * ctx->ninst;
         dfree((void*&)ctx->d_ndeg);
         dfree((void*&)ctx->d_degv);
-        HIPCHK(hipMalloc(&ctx->d_ndeg, sizeof(int) * ctx->ninst));
-        HIPCHK(hipMalloc(&ctx->d_degv, sizeof(double) * ctx->ninst * PINT_EIG_MAXDEG * (size_t)maxK));
+        HIPCHK(cmalloc((void**)&ctx->d_ndeg, sizeof(int) * ctx->ninst));
+        HIPCHK(cmalloc((void**)&ctx->d_degv, sizeof(double) * ctx->ninst * PINT_EIG_MAXDEG * (size_t)maxK));
         ctx->degv_cap = maxK;
     }
     if (ctx->degv_cap < maxK) { ctx->err = "eig scratch too small"; return PINT_E_INVALID; }
@@ -3332,7 +3440,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     if (need > ctx->wpart_cap) {
         if (ctx->capturing) { ctx->err = "pint_chi2_gls: first call inside a graph capture"; return PINT_E_INVALID; }
         dfree((void*&)ctx->d_wpart);
-        HIPCHK(hipMalloc(&ctx->d_wpart, sizeof(double) * need));
+        HIPCHK(cmalloc((void**)&ctx->d_wpart, sizeof(double) * need));
         ctx->wpart_cap = need;
     }
     record(ctx, 10);

@@ -461,6 +461,12 @@ class Session:
         self._check(self.L.pint_read_resids(self.ctx, L.ptr(tr), L.ptr(pr), L.ptr(c2)))
         return self._split(tr, n), self._split(pr, n), c2
 
+    def read_chi2(self):
+        """WLS chi2 per instance only (no residual rows copied back)."""
+        c2 = np.empty(len(self.inst_layout))
+        self._check(self.L.pint_read_resids(self.ctx, None, None, L.ptr(c2)))
+        return c2
+
     def read_eval(self):
         rows = [l.n + 1 for l in self.inst_layout]
         a = [np.empty(sum(rows)) for _ in range(4)]
@@ -569,6 +575,11 @@ class Session:
         ms = np.zeros(8)
         self.L.pint_last_timing(self.ctx, L.ptr(ms))
         return ms
+
+
+def release_cache():
+    """Hand the device-buffer cache back to the HIP runtime (pint_release_cache)."""
+    L.lib().pint_release_cache()
 
 
 # -- convenience single-model evaluations (used by TimingModel methods) ----------------

@@ -110,11 +110,11 @@ class BatchFit:
 
     # -- helpers ------------------------------------------------------------------------
     def _chi2_now(self):
-        tr, pr, c2 = self.s.read_resids()
+        c2 = self.s.read_chi2()
         if any(self.use_gls_chi2):
             cg = self.s.chi2_gls()
             c2 = np.where(self.use_gls_chi2, cg, c2)
-        return c2, tr
+        return c2, None
 
     def _step(self):
         self.s.eval(want_M=Session.FIT)
@@ -191,7 +191,6 @@ class BatchFit:
         for r, c in zip(results, c2):
             r.chi2 = float(c)
             r.converged = True
-        self.resid_time = self.s.read_resids()[0]
         return self._finish(results)
 
     # -- downhill (fitter.py:999-1105) ---------------------------------------------------
@@ -257,7 +256,6 @@ class BatchFit:
         self._errors_into(results)
         self.s.eval(want_M=False)
         c2, _ = self._chi2_now()
-        self.resid_time = self.s.read_resids()[0]
         for k, r in enumerate(results):
             r.chi2 = float(c2[k])
             r.converged = bool(converged[k])

@@ -57,16 +57,26 @@ def ecorr_epochs(t_sec: np.ndarray, dt: float = 1.0, nmin: int = 2):
     """get_ecorr_epochs (noise_model.py:808): 1-s buckets on sorted times, >= nmin TOAs."""
     if len(t_sec) == 0:
         return []
-    isort = np.argsort(t_sec)
-    ref = [t_sec[isort[0]]]
-    buckets = [[isort[0]]]
-    for i in isort[1:]:
-        if t_sec[i] - ref[-1] < dt:
-            buckets[-1].append(i)
-        else:
-            ref.append(t_sec[i])
-            buckets.append([i])
-    return [b for b in buckets if len(b) >= nmin]
+    isort = np.argsort(t_sec, kind="stable")
+    ts = t_sec[isort]
+    # a gap >= dt to the previous TOA always opens a bucket (the bucket reference time is
+    # <= the previous TOA); only clusters spanning >= dt need the sequential scan
+    cut = np.concatenate([[0], np.nonzero(np.diff(ts) >= dt)[0] + 1, [len(ts)]])
+    keep = np.nonzero(np.diff(cut) >= nmin)[0]
+    out = []
+    for a, b in zip(cut[keep].tolist(), cut[keep + 1].tolist()):
+        if ts[b - 1] - ts[a] < dt:
+            out.append(isort[a:b])
+            continue
+        s = a
+        for i in range(a + 1, b):
+            if ts[i] - ts[s] >= dt:
+                if i - s >= nmin:
+                    out.append(isort[s:i])
+                s = i
+        if b - s >= nmin:
+            out.append(isort[s:b])
+    return out
 
 
 def noise_basis(model, toas):
