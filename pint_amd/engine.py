@@ -388,8 +388,19 @@ class Session:
         """insts: sequence of (layout, table ndarray)."""
         ids = np.array([lay.psr_id for lay, _ in insts], dtype=np.int32)
         tabs = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64) for _, t in insts]))
-        self._check(self.L.pint_set_instances(self.ctx, len(insts), L.ptr(ids, C.c_int32), L.ptr(tabs)))
-        self.inst_layout = [lay for lay, _ in insts]
+        self._set(ids, tabs, [lay for lay, _ in insts])
+
+    def set_instances_of(self, lay: PulsarLayout, tables: np.ndarray):
+        """Many instances of one pulsar (grid points): tables is (ninst, tstride)."""
+        tables = np.ascontiguousarray(tables, dtype=np.float64)
+        if tables.ndim != 2 or tables.shape[1] != lay.tstride:
+            raise ValueError(f"tables must be (ninst, {lay.tstride}), got {tables.shape}")
+        ids = np.full(tables.shape[0], lay.psr_id, dtype=np.int32)
+        self._set(ids, tables.ravel(), [lay] * tables.shape[0])
+
+    def _set(self, ids, tabs, lays):
+        self._check(self.L.pint_set_instances(self.ctx, len(ids), L.ptr(ids, C.c_int32), L.ptr(tabs)))
+        self.inst_layout = lays
         self.ntab = len(tabs)
 
     # -- launches -------------------------------------------------------------------
@@ -537,9 +548,13 @@ class Session:
         return self._split(dp, kk), self._split(er, kk), covs, cl
 
     def read_tables(self):
+        return self._split(self.read_tables_flat(), [l.tstride for l in self.inst_layout])
+
+    def read_tables_flat(self):
+        """All instances' parameter tables, concatenated."""
         t = np.empty(self.ntab)
         self._check(self.L.pint_get_tables(self.ctx, L.ptr(t)))
-        return self._split(t, [l.tstride for l in self.inst_layout])
+        return t
 
     def chi2_gls(self):
         c = self._pin("chi2g", len(self.inst_layout))

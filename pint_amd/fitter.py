@@ -66,6 +66,16 @@ class FitResult:
         self.noise_coeffs = None
 
 
+class BatchOutcome:
+    """Per-instance fit outcomes as arrays (BatchFit with outputs=False, grid points)."""
+
+    def __init__(self, chi2, converged, exc):
+        self.chi2 = chi2
+        self.converged = converged
+        self.step_problem = exc
+        self.maxiter_reached = ~converged & ~exc
+
+
 class BatchFit:
     """Run the same fitter on many (model, toas) instances at once.
 
@@ -104,7 +114,10 @@ class BatchFit:
         if tables is None:
             tables = [pack_table(l, m) for l, (m, _) in zip(self.layouts, self.items)]
         self.tables = tables
-        self.s.set_instances(list(zip(self.layouts, self.tables)))
+        if isinstance(tables, np.ndarray) and tables.ndim == 2 and all(l is layouts[0] for l in layouts):
+            self.s.set_instances_of(layouts[0], tables)  # grid points of one pulsar
+        else:
+            self.s.set_instances(list(zip(self.layouts, self.tables)))
         self.ninst = len(self.layouts)
         self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in self.layouts]
 
@@ -180,29 +193,44 @@ class BatchFit:
                     m[name].uncertainty = float(res.errors[j])
 
     # -- plain WLS/GLS (fitter.py:1965-2087, :2104-2289) -------------------------------
-    def fit_plain(self, maxiter=1):
-        results = [FitResult() for _ in range(self.ninst)]
+    def fit_plain(self, maxiter=1, outputs=True):
+        """outputs=False (grid points): no per-instance FitResult, no step/covariance
+        read-back; returns a BatchOutcome of arrays (chi2, status)."""
+        results = [FitResult() for _ in range(self.ninst)] if outputs else None
         for _ in range(maxiter):
             self._step()
-            self._errors_into(results)
+            if outputs:
+                self._errors_into(results)
             self.s.apply_step(np.ones(self.ninst))
         self.s.eval(want_M=False)
         c2, _ = self._chi2_now()
+        if not outputs:
+            return self._finish_arrays(np.array(c2, dtype=np.float64), np.ones(self.ninst, dtype=bool),
+                                       np.zeros(self.ninst, dtype=bool))
         for r, c in zip(results, c2):
             r.chi2 = float(c)
             r.converged = True
         return self._finish(results)
 
+    def _finish_arrays(self, chi2, converged, exc):
+        self.final_tables = self.s.read_tables_flat()
+        return BatchOutcome(chi2, converged, exc)
+
     # -- downhill (fitter.py:999-1105) ---------------------------------------------------
-    def fit_downhill(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3):
+    def fit_downhill(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,
+                     outputs=True):
+        """The reference's per-fitter control flow (fitter.py:1015-1095), applied to every
+        instance at once: a lambda-halving line search on each instance's chi2, with the
+        best state tracked per instance.  Decisions are vectorised over instances; each
+        trial is one batched eval + chi2 of all undecided instances."""
         n = self.ninst
-        results = [FitResult() for _ in range(n)]
         self._step()                                     # step of the initial state
-        cur_tab = np.concatenate(self.s.read_tables())
-        sizes = [l.tstride for l in self.layouts]
-        offs = np.concatenate([[0], np.cumsum(sizes)])
+        cur_tab = self.s.read_tables_flat()
+        sizes = np.array([l.tstride for l in self.layouts])
+        ent = np.repeat(np.arange(n), sizes)             # instance of every table entry
         self.s.eval(want_M=False)
         cur_chi2, _ = self._chi2_now()
+        cur_chi2 = np.array(cur_chi2, dtype=np.float64)
         best_chi2 = cur_chi2.copy()
         best_tab = cur_tab.copy()
         active = np.ones(n, dtype=bool)
@@ -220,42 +248,47 @@ class BatchFit:
                 try:
                     self.s.eval(want_M=False)
                     new_chi2, _ = self._chi2_now()
+                    new_chi2 = np.array(new_chi2, dtype=np.float64)
                 except Exception:
                     new_chi2 = np.full(n, np.nan)
-                new_tab = np.concatenate(self.s.read_tables())
-                for k in np.where(~decided)[0]:
-                    c = new_chi2[k]
-                    d = cur_chi2[k] - c
-                    ok = np.isfinite(c)
-                    if ok and c < best_chi2[k]:
-                        best_chi2[k] = c
-                        best_tab[offs[k]:offs[k + 1]] = new_tab[offs[k]:offs[k + 1]]
-                    if (not ok) or d < -max_chi2_increase:
-                        lam[k] /= 2
-                        if lam[k] < min_lambda:
-                            exc[k] = True
-                            decided[k] = True
-                            dec[k] = 0.0
-                        continue
-                    cur_tab[offs[k]:offs[k + 1]] = new_tab[offs[k]:offs[k + 1]]
-                    cur_chi2[k] = c
-                    dec[k] = d
-                    decided[k] = True
-            for k in np.where(active)[0]:
-                if exc[k]:
-                    active[k] = False
-                elif -max_chi2_increase <= dec[k] < required_chi2_decrease and lam[k] == 1:
-                    converged[k] = True
-                    active[k] = False
+                new_tab = self.s.read_tables_flat()
+                und = ~decided
+                d = cur_chi2 - new_chi2
+                ok = np.isfinite(new_chi2)
+                better = und & ok & (new_chi2 < best_chi2)          # fitter.py:1046-1049
+                best_chi2[better] = new_chi2[better]
+                sel = better[ent]
+                best_tab[sel] = new_tab[sel]
+                bad = und & (~ok | (d < -max_chi2_increase))         # :1050-1062 halve lambda
+                lam[bad] /= 2
+                gone = bad & (lam < min_lambda)                      # :1058 StepProblem
+                exc |= gone
+                decided |= gone
+                dec[gone] = 0.0
+                good = und & ~bad                                    # :1063-1067 accept
+                sel = good[ent]
+                cur_tab[sel] = new_tab[sel]
+                cur_chi2[good] = new_chi2[good]
+                dec[good] = d[good]
+                decided |= good
+            done = active & exc
+            conv = active & ~exc & (-max_chi2_increase <= dec) & (dec < required_chi2_decrease) & (lam == 1)
+            converged |= conv                                        # :1076-1085
+            active &= ~(done | conv)
             if active.any() and it < maxiter - 1:
                 self.s.set_tables(cur_tab)
                 self._step()  # step at the new current states (inactive ones are ignored)
         # best state -> model, residuals; covariance from a step at the best state
         self.s.set_tables(best_tab)
         self._step()
-        self._errors_into(results)
+        results = None
+        if outputs:
+            results = [FitResult() for _ in range(n)]
+            self._errors_into(results)
         self.s.eval(want_M=False)
         c2, _ = self._chi2_now()
+        if not outputs:
+            return self._finish_arrays(np.array(c2, dtype=np.float64), converged, exc)
         for k, r in enumerate(results):
             r.chi2 = float(c2[k])
             r.converged = bool(converged[k])

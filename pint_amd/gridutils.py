@@ -104,20 +104,22 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
                     o = lay.offsets[p]
                     tabs[:, o] = h
                     tabs[:, o + 1] = l
-                bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (c1 - c0), tables=list(tabs))
+                bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (c1 - c0), tables=tabs)
                 if down:
                     rq = fitargs.get("required_chi2_decrease", 1e-2)
                     res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
-                                          max_chi2_increase=rq, min_lambda=rq)
-                else:
-                    res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1))
-                for k, r in enumerate(res):
+                                          max_chi2_increase=rq, min_lambda=rq, outputs=False)
                     # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
-                    chi2[c0 - lo + k] = np.nan if (down and r.status == "MaxiterReached") else r.chi2
-                for e in extraparnames:
-                    o = lay.offsets[e]
-                    extra[e][c0 - lo:c1 - lo] = [float(np.longdouble(t[o]) + np.longdouble(t[o + 1]))
-                                                 for t in bf.final_tables]
+                    chi2[c0 - lo:c1 - lo] = np.where(res.maxiter_reached, np.nan, res.chi2)
+                else:
+                    res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1), outputs=False)
+                    chi2[c0 - lo:c1 - lo] = res.chi2
+                if extraparnames:
+                    ft = bf.final_tables.reshape(c1 - c0, lay.tstride)
+                    for e in extraparnames:
+                        o = lay.offsets[e]
+                        extra[e][c0 - lo:c1 - lo] = (ft[:, o].astype(np.longdouble)
+                                                     + ft[:, o + 1].astype(np.longdouble)).astype(np.float64)
         finally:
             s.close()
     chi2_all = gather_blocks(chi2, per, npts, dist)

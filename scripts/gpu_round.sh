@@ -26,14 +26,19 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
-        -o run -- python3 bench.py --steps 10 --warmup 2 --grid 64 --cpu-baseline 0 \
+        -o run -- python3 bench.py --steps 10 --warmup 2 --grid 64 --j0740 0 --cpu-baseline 0 \
         > gpurun_out/prof.log 2>&1
     step pmc 0 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch \
-        -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --cpu-baseline 0 \
+        -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --cpu-baseline 0 \
         > gpurun_out/pmc_fetch.log 2>&1
     step pmc2 0 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write \
-        -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --cpu-baseline 0 \
+        -o run -- python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --cpu-baseline 0 \
         > gpurun_out/pmc_write.log 2>&1
+fi
+if [ "$MODE" = profj ]; then  # the J0740 legs (C3 Downhill, (M2,SINI) grid) on their own
+    step rocprofj 0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profj \
+        -o run -- python3 bench.py --steps 1 --warmup 1 --npsr 1 --grid 0 --j0740 256 --cpu-baseline 0 \
+        > gpurun_out/profj.log 2>&1
 fi
 if [ "$MODE" = all ] || [ "$MODE" = peaks ]; then
     step peaks 0 timeout -k 10 120 ./build/peaks > gpurun_out/peaks.json

@@ -534,3 +534,39 @@ def test_degenerate_column_svd_path(name, Fitter):
         d = float((np.longdouble(fj.model[p].value) - np.longdouble(f0.model[p].value)) / np.longdouble(e))
         assert abs(d) < tol, (p, d)
         assert abs(fj.model[p].uncertainty / e - 1) < tol, p
+
+
+def test_grid_downhill_extra_matches_single_fits():
+    """grid_chisq with a downhill fitter (vectorised batch line search, array outcomes) and
+    extraparnames gives, per point, the chi2 and extra parameter of a single
+    DownhillWLSFitter fit of that point (gridutils.py:72-111 parallel semantics)."""
+    import copy
+    from pint_amd import DownhillWLSFitter
+    from pint_amd.fitter import MaxiterReached, StepProblem
+    from pint_amd.gridutils import grid_chisq, grid_points
+    model, toas, z, meta = load("ngc6440e")
+    f = DownhillWLSFitter(toas, model)
+    f.fit_toas()
+    F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+    g0 = F0 + np.linspace(-4, 4, 3) * np.longdouble(f.model.F0.uncertainty)
+    g1 = F1 + np.linspace(-4, 4, 2) * np.longdouble(f.model.F1.uncertainty)
+    c2, ex = grid_chisq(f, ("F0", "F1"), (g0, g1), extraparnames=["DM"])
+    _, flat = grid_points((g0, g1))
+    for k in range(c2.size):
+        m = copy.deepcopy(f.model)
+        m["F0"].value, m["F1"].value = flat[0][k], flat[1][k]
+        m["F0"].frozen = m["F1"].frozen = True
+        g = DownhillWLSFitter(toas, m)
+        try:
+            g.fit_toas()
+            want = g.resids.chi2
+        except MaxiterReached:
+            want = np.nan
+        except StepProblem:
+            want = g.resids.chi2 if g.resids is not None else np.nan
+        got = c2.ravel()[k]
+        if np.isnan(want):
+            assert np.isnan(got), (k, got)
+        else:
+            assert abs(got / want - 1) < 1e-9, (k, got, want)
+            assert abs(ex["DM"][k] - float(g.model.DM.value)) < 1e-9 * abs(float(g.model.DM.value)), k
