@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(HERE, "libpint_hip.so")
+LIBPATH = os.environ.get("PINT_LIB") or os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
 EIG_MAXDEG = 8  # PINT_EIG_MAXDEG

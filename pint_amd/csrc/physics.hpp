@@ -25,6 +25,20 @@ constexpr double MASYR_RADS = 1.5362818500441604e-16;  // (mas/yr) in rad/s
 constexpr double YR_S = 31557600.0;
 constexpr double TWO_PI = 6.283185307179586;
 constexpr double PI_D = 3.141592653589793;
+// reciprocals of the constants divided by per TOA (x / c -> x * (1/c): <= 1 ulp)
+constexpr double INV_C_KMS = 1.0 / C_KMS;
+constexpr double INV_AU_KM = 1.0 / AU_KM;
+constexpr double INV_AUC = 1.0 / (AU_KM * C_KMS);
+constexpr double INV_KPC_KM = 1.0 / KPC_KM;
+constexpr double INV_DJY = 1.0 / DJY;
+constexpr double INV_TWO_PI = 1.0 / TWO_PI;
+// 1/k as double-double (hi correctly rounded, lo = 1/k - hi), k < 64: the Taylor-series
+// divisions by small integers become multiplications (exact to ~1e-32 relative)
+constexpr int NINV = 64;
+__device__ __constant__ const double INV_HI[NINV] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2, 0.16666666666666666, 0.14285714285714285, 0.125, 0.1111111111111111, 0.1, 0.09090909090909091, 0.08333333333333333, 0.07692307692307693, 0.07142857142857142, 0.06666666666666667, 0.0625, 0.058823529411764705, 0.05555555555555555, 0.05263157894736842, 0.05, 0.047619047619047616, 0.045454545454545456, 0.043478260869565216, 0.041666666666666664, 0.04, 0.038461538461538464, 0.037037037037037035, 0.03571428571428571, 0.034482758620689655, 0.03333333333333333, 0.03225806451612903, 0.03125, 0.030303030303030304, 0.029411764705882353, 0.02857142857142857, 0.027777777777777776, 0.02702702702702703, 0.02631578947368421, 0.02564102564102564, 0.025, 0.024390243902439025, 0.023809523809523808, 0.023255813953488372, 0.022727272727272728, 0.022222222222222223, 0.021739130434782608, 0.02127659574468085, 0.020833333333333332, 0.02040816326530612, 0.02, 0.0196078431372549, 0.019230769230769232, 0.018867924528301886, 0.018518518518518517, 0.01818181818181818, 0.017857142857142856, 0.017543859649122806, 0.017241379310344827, 0.01694915254237288, 0.016666666666666666, 0.01639344262295082, 0.016129032258064516, 0.015873015873015872};
+__device__ __constant__ const double INV_LO[NINV] = {0.0, 0.0, 0.0, 1.850371707708594e-17, 0.0, -1.1102230246251566e-17, 9.25185853854297e-18, 7.93016446160826e-18, 0.0, 6.1679056923619804e-18, -5.551115123125783e-18, -2.523234146875356e-18, 4.625929269271485e-18, -4.270088556250602e-18, 3.96508223080413e-18, 9.251858538542971e-19, 0.0, 8.163404592832033e-19, 3.0839528461809902e-18, 2.921639538487254e-18, -2.7755575615628915e-18, 2.64338815386942e-18, -1.261617073437678e-18, 1.206764157201257e-18, 2.3129646346357427e-18, -8.326672684688674e-19, -2.135044278125301e-18, 2.05596856412066e-18, 1.982541115402065e-18, 4.785444071660157e-19, 4.625929269271486e-19, 8.953411488912552e-19, 0.0, -8.410780489584519e-19, 4.0817022964160166e-19, 8.921435019309293e-19, 1.5419764230904951e-18, -1.50030138462859e-18, 1.460819769243627e-18, 8.896017825522087e-19, -1.3877787807814458e-18, -8.46206573647223e-19, 1.32169407693471e-18, 3.2273925134452225e-19, -6.30808536718839e-19, -8.480870326997723e-19, 6.033820786006285e-19, 5.167261417803255e-19, 1.1564823173178713e-18, 1.6285159162231251e-18, -4.163336342344337e-19, 2.7211348642773444e-19, -1.0675221390626506e-18, 7.20073895688486e-19, 1.02798428206033e-18, 8.831319514063744e-19, 9.912705577010326e-19, 9.73879846162418e-19, 2.3927220358300787e-19, 5.880418562633244e-20, 2.312964634635743e-19, -8.531426931033477e-19, 4.476705744456276e-19, 8.8112938462314e-19};
+PD double inv_int(int k) { return k < NINV ? INV_HI[k] : 1.0 / (double)k; }
+PD dd dd_div_int(dd a, int k) { return k < NINV ? dd_mul(a, dd_make(INV_HI[k], INV_LO[k])) : dd_div_d(a, (double)k); }
 
 PD double pval(const double* P, int o) { return P[o] + P[o + 1]; }
 PD dd pdd(const double* P, int o) { return dd_make(P[o], P[o + 1]); }
@@ -144,7 +158,9 @@ struct InstConst {
     double posep;        // POSEPOCH (MJD) or 0
     double plon, plat;   // rad (RAJ in hourangle, ELONG/ELAT/DECJ in deg -> rad)
     double cplat, splat;
+    double cplon, splon;
     double F0, iF0;
+    double ipb_hi, ipb_lo;  // 1/(PB in s) in dd (binary models)
     int has_pm;
     int pad_;
 };
@@ -156,6 +172,14 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
     C.L0[0] = 0.0; C.L0[1] = 0.0; C.L0[2] = 1.0;
     C.posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
     C.plon = C.plat = C.cplat = C.splat = 0.0;
+    C.cplon = 1.0;
+    C.splon = 0.0;
+    C.ipb_hi = C.ipb_lo = 0.0;
+    if (S.binary && S.o_bin[PINT_B_PB] >= 0) {
+        dd ipb = dd_div(dd_make(1.0), dd_mul_d(pdd(P, S.o_bin[PINT_B_PB]), DAYSEC));
+        C.ipb_hi = ipb.hi;
+        C.ipb_lo = ipb.lo;
+    }
     if (!S.astrometry) return;
     double lon = pval(P, S.o_lon), lat = pval(P, S.o_lat);
     double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
@@ -164,6 +188,8 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
     C.plat = lat * DEG_RAD;
     C.cplat = cos(C.plat);
     C.splat = sin(C.plat);
+    C.cplon = cos(C.plon);
+    C.splon = sin(C.plon);
     if (S.astrometry == 1) {
         double ra = lon * HA_RAD, dec = lat * DEG_RAD;
         C.L0[0] = cos(ra) * cos(dec);
@@ -231,6 +257,8 @@ struct BinState {
     // trigonometry shared by the delay and every derivative column (computed once)
     double s1, c1, s2, c2, s3, c3, s4, c4;                   // ELL1: sin/cos(k Phi)
     double snu, cnu, sw, cw, soPn, coPn, logNum, lgNum, sqTh, sqE;  // DD
+    double ipb, iPBs;  // 1/pb (pbprime), 1/PBs
+    double iomeE, isnu, ilogNum, isqTh, isqE;  // DD: 1/(1 - e cosE), 1/sin(nu), ...
     double delay;
     int status;
 };
@@ -251,8 +279,8 @@ PD double binp(const pint_spec_t& S, const double* P, int pid, double dflt = 0.0
 }
 
 // orbits (binary_orbits.py:98 OrbitPB.orbits) in dd; returns frac and floor
-PD void orbit_phase(dd tt0, double PBs_hi, double PBs_lo, double pbdot_sum, BinState& B) {
-    dd x = dd_div(tt0, dd_make(PBs_hi, PBs_lo));
+PD void orbit_phase(dd tt0, dd ipbs, double pbdot_sum, BinState& B) {
+    dd x = dd_mul(tt0, ipbs);  // tt0 / PB with the per-instance dd reciprocal
     double xd = dd_to_d(x);
     dd orb = dd_add_d(x, -0.5 * pbdot_sum * xd * xd);
     dd fl = dd_floor(orb);
@@ -262,7 +290,7 @@ PD void orbit_phase(dd tt0, double PBs_hi, double PBs_lo, double pbdot_sum, BinS
 }
 
 // ---- ELL1 (ELL1_model.py) ---------------------------------------------------------
-PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_delay, BinState& B) {
+PD void ell1_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B) {
     dd tasc = pdd(P, S.o_bin[PINT_B_TASC]);
     // ttasc = (t - TASC) in s with t = tdbld*day - acc_delay (pulsar_binary.py:398, ELL1_model.py:42)
     dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, tasc), DAYSEC), -acc_delay);
@@ -272,7 +300,8 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
     B.PBs = dd_to_d(PBs);
     B.PBDOT = binp(S, P, PINT_B_PBDOT);
     B.XPBDOT = binp(S, P, PINT_B_XPBDOT);
-    orbit_phase(tt, PBs.hi, PBs.lo, B.PBDOT + B.XPBDOT, B);
+    orbit_phase(tt, dd_make(C.ipb_hi, C.ipb_lo), B.PBDOT + B.XPBDOT, B);
+    B.iPBs = C.ipb_hi + C.ipb_lo;
     B.pb = B.PBs + B.PBDOT * B.tt0;  // pbprime (binary_orbits.py:107)
     B.A1DOT = binp(S, P, PINT_B_A1DOT);
     B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
@@ -283,8 +312,13 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
     B.TM2 = binp(S, P, PINT_B_M2) * TSUN;
     B.SINI = binp(S, P, PINT_B_SINI);
     double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2;
-    double s1 = sin(Phi), c1 = cos(Phi), s2 = sin(2 * Phi), c2 = cos(2 * Phi);
-    double s3 = sin(3 * Phi), c3 = cos(3 * Phi), s4 = sin(4 * Phi), c4 = cos(4 * Phi);
+    // sin/cos(k Phi), k = 2..4, by the angle-addition identities from one sincos (a few
+    // ulp of 1; they enter multiplied by a1 * eps <~ 1e-5 s)
+    double s1, c1;
+    sincos(Phi, &s1, &c1);
+    const double s2 = 2.0 * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
+    const double s3 = s2 * c1 + c2 * s1, c3 = c2 * c1 - s2 * s1;
+    const double s4 = 2.0 * s2 * c2, c4 = (c2 - s2) * (c2 + s2);
     B.s1 = s1; B.c1 = c1; B.s2 = s2; B.c2 = c2; B.s3 = s3; B.c3 = c3; B.s4 = s4; B.c4 = c4;
     double e1s = e1 * e1, e2s = e2 * e2;
     // d_delayR_da1 (ELL1_model.py:221-253)
@@ -305,10 +339,12 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_del
     B.Dre = B.a1 * B.R0;  // delayR (:317)
     B.Drep = B.a1 * B.R1;  // Drep (:398)
     B.Drepp = B.a1 * B.R2;  // Drepp (:478)
-    B.nhat = TWO_PI / B.pb;
+    B.ipb = 1.0 / B.pb;
+    B.nhat = TWO_PI * B.ipb;
     double nD = B.nhat * B.Drep;
     double delayI = B.Dre * (1 - nD + nD * nD + 0.5 * B.nhat * B.nhat * B.Dre * B.Drepp);  // :141-166
-    double delayS = -2 * B.TM2 * log(1 - B.SINI * s1);                                   // :599-603
+    B.lgNum = log(1 - B.SINI * s1);
+    double delayS = -2 * B.TM2 * B.lgNum;                                                // :599-603
     B.delay = delayI + delayS;
     B.status = 0;
 }
@@ -365,13 +401,13 @@ PD void ell1_grad(const BinState& B, Ell1Grad& g) {
     g.Phi = dI_dDre * Drep + dI_dDrep * Drepp + dI_dDrepp * dDrepp_dPhi + (-2 * B.TM2 / lg * (-B.SINI));
     g.e1 = dI_dDre * dDre_de1 + dI_dDrep * dDrep_de1 + dI_dDrepp * dDrepp_de1;
     g.e2 = dI_dDre * dDre_de2 + dI_dDrep * dDrep_de2 + dI_dDrepp * dDrepp_de2;
-    g.pb = dI_dnhat * (-TWO_PI / (B.pb * B.pb));
-    g.TM2 = -2 * log(lg);
+    g.pb = dI_dnhat * (-TWO_PI * B.ipb * B.ipb);
+    g.TM2 = -2 * B.lgNum;
     g.SINI = -2 * B.TM2 / lg * (-s1);
 }
 
 PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
-    double tt0 = B.tt0, PBs = B.PBs;
+    const double tt0 = B.tt0, i2 = B.iPBs * B.iPBs;
     switch (pid) {
         case PINT_B_A1: return g.a1;
         case PINT_B_A1DOT: return g.a1 * tt0;
@@ -381,11 +417,11 @@ PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
         case PINT_B_EPS2DOT: return g.e2 * tt0;
         case PINT_B_TASC:
             // d_Phi_d_TASC uses pb()=pbprime and pbdot() (ELL1_model.py:108)
-            return g.e1 * (-B.EPS1DOT) + g.e2 * (-B.EPS2DOT) + g.Phi * ((B.PBDOT * tt0 / B.pb - 1.0) * TWO_PI / B.pb);
+            return g.e1 * (-B.EPS1DOT) + g.e2 * (-B.EPS2DOT) + g.Phi * ((B.PBDOT * tt0 * B.ipb - 1.0) * TWO_PI * B.ipb);
         case PINT_B_PB:
-            return g.Phi * (TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs))) + g.pb;
-        case PINT_B_PBDOT: return g.Phi * (-PI_D * tt0 * tt0 / (PBs * PBs)) + g.pb * tt0;
-        case PINT_B_XPBDOT: return g.Phi * (-PI_D * tt0 * tt0 / (PBs * PBs));
+            return g.Phi * (TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 * i2 * B.iPBs - tt0 * i2)) + g.pb;
+        case PINT_B_PBDOT: return g.Phi * (-PI_D * tt0 * tt0 * i2) + g.pb * tt0;
+        case PINT_B_XPBDOT: return g.Phi * (-PI_D * tt0 * tt0 * i2);
         case PINT_B_M2: return g.TM2 * TSUN;
         case PINT_B_SINI: return g.SINI;
         default: return 0.0;
@@ -393,7 +429,7 @@ PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
 }
 
 // ---- DD (DD_model.py, binary_generic.py) ------------------------------------------
-PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_delay, BinState& B) {
+PD void ddm_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B) {
     dd T0 = pdd(P, S.o_bin[PINT_B_T0]);
     dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, T0), DAYSEC), -acc_delay);  // get_tt0 (binary_generic.py:372)
     B.tt0 = dd_to_d(tt);
@@ -402,7 +438,8 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_dela
     B.PBs = dd_to_d(PBs);
     B.PBDOT = binp(S, P, PINT_B_PBDOT);
     B.XPBDOT = binp(S, P, PINT_B_XPBDOT);
-    orbit_phase(tt, PBs.hi, PBs.lo, B.PBDOT + B.XPBDOT, B);
+    orbit_phase(tt, dd_make(C.ipb_hi, C.ipb_lo), B.PBDOT + B.XPBDOT, B);
+    B.iPBs = C.ipb_hi + C.ipb_lo;
     B.pb = B.PBs + B.PBDOT * B.tt0;
     B.A1DOT = binp(S, P, PINT_B_A1DOT);
     B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
@@ -419,32 +456,35 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_dela
     double e = B.ecc, M = B.Phi;
     if (!(e >= 0.0 && e < 1.0)) { B.status = PINT_E_KEPLER; B.delay = 0; return; }
     // compute_eccentric_anomaly (binary_generic.py:337-370): Newton from E0 = M, tol 5e-15
-    double U = M;
+    double U = M, sU, cU;
     int it = 0;
-    double kU = U - e * sin(U) - M;
+    sincos(U, &sU, &cU);
+    double kU = U - e * sU - M;
     while (fabs(kU) > 5e-15 && it < 64) {
-        U = U - kU / (1 - e * cos(U));
-        kU = U - e * sin(U) - M;
+        U = U - kU / (1 - e * cU);
+        sincos(U, &sU, &cU);
+        kU = U - e * sU - M;
         it++;
     }
     if (fabs(kU) > 5e-15) B.status = PINT_E_KEPLER;
     B.E = U;
-    B.sinE = sin(U);
-    B.cosE = cos(U);
+    B.sinE = sU;  // sin/cos of the converged U
+    B.cosE = cU;
     // nu (binary_generic.py:538-549), unwrapped: 2*pi*orbits + nu - M = 2*pi*floor(orbits) + nu
     double nu = 2 * atan(sqrt((1.0 + e) / (1.0 - e)) * tan(U / 2.0));
     if (nu < 0) nu += TWO_PI;
     B.nu = TWO_PI * B.floor_orbits + nu;
     B.OMDOT_rs = binp(S, P, PINT_B_OMDOT) * (DEG_RAD / YR_S);
-    B.k = B.OMDOT_rs / (TWO_PI / B.pb);              // DD_model.py:76 k
+    B.ipb = 1.0 / B.pb;
+    B.k = B.OMDOT_rs * B.pb * INV_TWO_PI;             // DD_model.py:76 k
     B.omega = binp(S, P, PINT_B_OM) * DEG_RAD + B.nu * B.k;  // :86
     B.er = e * (1 + B.DR);
     B.eTheta = e * (1 + B.DTH);
-    double sw = sin(B.omega), cw = cos(B.omega);
+    double sw, cw;
+    sincos(B.omega, &sw, &cw);
     B.sw = sw;
     B.cw = cw;
-    B.snu = sin(B.nu);
-    B.cnu = cos(B.nu);
+    sincos(B.nu, &B.snu, &B.cnu);
     B.sqTh = sqrt(1 - B.eTheta * B.eTheta);
     B.sqE = sqrt(1 - e * e);
     B.alpha = B.a1 * sw;                                    // :223
@@ -454,52 +494,57 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, dd tdb, double acc_dela
     B.Dre = delayR + B.GAMMA * sE;                          // :434 + delayE :786
     B.Drep = -B.alpha * sE + (B.beta + B.GAMMA) * cE;       // :470
     B.Drepp = -B.alpha * cE - (B.beta + B.GAMMA) * sE;      // :520
-    B.nhat = TWO_PI / B.pb / (1 - e * cE);                  // :562
+    B.iomeE = 1.0 / (1 - e * cE);
+    B.isnu = 1.0 / B.snu;
+    B.isqTh = 1.0 / B.sqTh;
+    B.isqE = 1.0 / B.sqE;
+    B.nhat = TWO_PI * B.ipb * B.iomeE;                      // :562
     double nH = B.nhat;
     double delayI = B.Dre * (1 - nH * B.Drep + (nH * B.Drep) * (nH * B.Drep) + 0.5 * nH * nH * B.Dre * B.Drepp -
-                             0.5 * e * sE / (1 - e * cE) * nH * nH * B.Dre * B.Drep);  // :602-646
+                             0.5 * e * sE * B.iomeE * nH * nH * B.Dre * B.Drep);  // :602-646
     double logNum = 1 - e * cE - B.SINI * (sw * (cE - e) + B.sqE * cw * sE);
     B.logNum = logNum;
     B.lgNum = log(logNum);
+    B.ilogNum = 1.0 / logNum;
     double delayS = -2 * B.TM2 * B.lgNum;                   // :700-720
     double oPn = B.omega + B.nu;
-    B.soPn = sin(oPn);
-    B.coPn = cos(oPn);
+    sincos(oPn, &B.soPn, &B.coPn);
     double delayA = B.A0 * (B.soPn + e * sw) + B.B0 * (B.coPn + e * cw);  // :794-806
     B.delay = delayI + delayS + delayA;
 }
 
 PD double ddm_deriv(const BinState& B, int pid) {
-    const double e = B.ecc, sE = B.sinE, cE = B.cosE, tt0 = B.tt0, PBs = B.PBs;
-    const double omeE = 1 - e * cE;
+    const double e = B.ecc, sE = B.sinE, cE = B.cosE, tt0 = B.tt0;
+    const double iP = B.iPBs, iP2 = iP * iP;
+    const double iom = B.iomeE;  // 1 / (1 - e cosE)
     // ---- seeds (binary_generic.py / binary_orbits.py / DD_model.py) ----
     bool orbit_par = (pid == PINT_B_PB || pid == PINT_B_PBDOT || pid == PINT_B_XPBDOT || pid == PINT_B_T0);
     double d_ecc = 0, d_a1 = 0, d_M = 0, d_pb = 0;
     switch (pid) {
         case PINT_B_T0: d_ecc = -B.EDOT; d_a1 = -B.A1DOT;
-            d_M = ((B.PBDOT - B.XPBDOT) * tt0 / PBs - 1.0) * TWO_PI / PBs;  // binary_orbits.py:114
+            d_M = ((B.PBDOT - B.XPBDOT) * tt0 * iP - 1.0) * TWO_PI * iP;  // binary_orbits.py:114
             d_pb = -B.PBDOT; break;
         case PINT_B_ECC: d_ecc = 1; break;
         case PINT_B_EDOT: d_ecc = tt0; break;
         case PINT_B_A1: d_a1 = 1; break;
         case PINT_B_A1DOT: d_a1 = tt0; break;
-        case PINT_B_PB: d_M = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 / (PBs * PBs * PBs) - tt0 / (PBs * PBs));
+        case PINT_B_PB: d_M = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 * iP2 * iP - tt0 * iP2);
             d_pb = 1; break;
-        case PINT_B_PBDOT: d_M = -PI_D * tt0 * tt0 / (PBs * PBs); d_pb = tt0; break;
-        case PINT_B_XPBDOT: d_M = -PI_D * tt0 * tt0 / (PBs * PBs); break;
+        case PINT_B_PBDOT: d_M = -PI_D * tt0 * tt0 * iP2; d_pb = tt0; break;
+        case PINT_B_XPBDOT: d_M = -PI_D * tt0 * tt0 * iP2; break;
         default: break;
     }
     // E (binary_generic.py:397-448)
-    double d_E_d_ECC = sE / (1.0 - e * cE);
+    double d_E_d_ECC = sE * iom;
     double d_E = 0;
-    if (pid == PINT_B_T0) d_E = (d_M - B.EDOT * sE) / (1.0 - cE * e);
+    if (pid == PINT_B_T0) d_E = (d_M - B.EDOT * sE) * iom;
     else if (pid == PINT_B_ECC) d_E = d_E_d_ECC;
     else if (pid == PINT_B_EDOT) d_E = tt0 * d_E_d_ECC;
-    else if (orbit_par) d_E = d_M / (1.0 - cE * e);
+    else if (orbit_par) d_E = d_M * iom;
     // nu (binary_generic.py:451-624)
     double snu = B.snu, cnu = B.cnu;
-    double d_nu_d_E = (1 + e * cnu) / (1 - e * cE) * (sE / snu);
-    double d_nu_d_ecc = sE * sE / ((e * cE - 1) * (e * cE - 1)) / snu;
+    double d_nu_d_E = (1 + e * cnu) * iom * (sE * B.isnu);
+    double d_nu_d_ecc = sE * sE * (iom * iom) * B.isnu;
     double d_nu = 0;
     if (pid == PINT_B_T0) d_nu = d_nu_d_ecc * (-B.EDOT) + d_nu_d_E * d_E;
     else if (pid == PINT_B_ECC) d_nu = d_nu_d_ecc + d_nu_d_E * d_E_d_ECC;
@@ -508,14 +553,14 @@ PD double ddm_deriv(const BinState& B, int pid) {
     // omega (DD_model.py:88-133)
     double d_omega;
     if (pid == PINT_B_OM) d_omega = 1;
-    else if (pid == PINT_B_OMDOT) d_omega = B.pb / TWO_PI * B.nu;
-    else if (orbit_par) d_omega = d_nu * B.k + d_pb * B.nu * B.OMDOT_rs / TWO_PI;
+    else if (pid == PINT_B_OMDOT) d_omega = B.pb * INV_TWO_PI * B.nu;
+    else if (orbit_par) d_omega = d_nu * B.k + d_pb * B.nu * B.OMDOT_rs * INV_TWO_PI;
     else d_omega = B.k * d_nu;
     // er / eTheta (DD_model.py:149-205): d_ecc_d_par only for T0/ECC/EDOT; DR/DTH -> ecc
     double d_er = (pid == PINT_B_DR) ? e : d_ecc;
     double d_eTh = (pid == PINT_B_DTH) ? e : d_ecc;
     double sw = B.sw, cw = B.cw;
-    double eTh = B.eTheta, sq = B.sqTh;
+    double eTh = B.eTheta, sq = B.sqTh, isq = B.isqTh;
     // alpha (DD_model.py:225-246)
     double d_alpha = d_a1 * sw + B.a1 * cw * d_omega;
     // beta (DD_model.py:277-407): specific d_beta_d_X methods take precedence in prtl_der
@@ -526,11 +571,11 @@ PD double ddm_deriv(const BinState& B, int pid) {
         case PINT_B_T0: d_beta = -B.A1DOT * sq * cw; break;
         case PINT_B_ECC: case PINT_B_EDOT: {
             double f = (pid == PINT_B_EDOT) ? tt0 : 1.0;
-            d_beta = B.a1 * ((-eTh) / sq * cw * f - sq * sw * d_omega);
+            d_beta = B.a1 * ((-eTh) * isq * cw * f - sq * sw * d_omega);
         } break;
-        case PINT_B_DTH: d_beta = B.a1 * (-eTh) / sq * cw; break;
+        case PINT_B_DTH: d_beta = B.a1 * (-eTh) * isq * cw; break;
         default:
-            d_beta = sq * cw * d_a1 + (-B.a1 * sq * sw) * d_omega + (B.a1 * (-eTh) / sq * cw) * d_eTh;
+            d_beta = sq * cw * d_a1 + (-B.a1 * sq * sw) * d_omega + (B.a1 * (-eTh) * isq * cw) * d_eTh;
     }
     double d_gamma = (pid == PINT_B_GAMMA) ? 1.0 : 0.0;
     double alpha = B.alpha, beta = B.beta, G = B.GAMMA;
@@ -540,11 +585,11 @@ PD double ddm_deriv(const BinState& B, int pid) {
     double dDrepp = -cE * d_alpha + (alpha * sE - (beta + G) * cE) * d_E - sE * (d_beta + d_gamma);
     // nhat (DD_model.py:564-590): uses prtl_der("PB") (1 only for PB)
     double dPB = (pid == PINT_B_PB) ? 1.0 : 0.0;
-    double d_nhat = -TWO_PI / B.pb / omeE * (dPB / B.pb - (cE * d_ecc - e * sE * d_E) / omeE);
+    double d_nhat = -TWO_PI * B.ipb * iom * (dPB * B.ipb - (cE * d_ecc - e * sE * d_E) * iom);
     // delayI (DD_model.py:648-698)
     double Dre = B.Dre, Drep = B.Drep, Drepp = B.Drepp, nH = B.nhat;
-    double x = -0.5 * e * sE / omeE;
-    double dx = -sE / (2 * omeE * omeE) * d_ecc + e * (e - cE) / (2 * omeE * omeE) * d_E;
+    double x = -0.5 * e * sE * iom;
+    double dx = -sE * (0.5 * iom * iom) * d_ecc + e * (e - cE) * (0.5 * iom * iom) * d_E;
     double dI_dDre = 1 + (Drep * nH) * (Drep * nH) + Dre * Drepp * nH * nH + Drep * nH * (2 * Dre * nH * x - 1);
     double dI_dDrep = Dre * nH * (2 * Drep * nH + Dre * nH * x - 1);
     double dI_dDrepp = (Dre * nH) * (Dre * nH) / 2;
@@ -553,15 +598,15 @@ PD double ddm_deriv(const BinState& B, int pid) {
     double dI = dDre * dI_dDre + dDrep * dI_dDrep + dDrepp * dI_dDrepp + dx * dI_dx + d_nhat * dI_dnhat;
     // delayS (DD_model.py:722-784)
     double sq1 = B.sqE;
-    double logNum = B.logNum;
+    double ilN = B.ilogNum;
     double d_TM2 = (pid == PINT_B_M2) ? TSUN : 0.0;
     double d_SINI = (pid == PINT_B_SINI) ? 1.0 : 0.0;
     double TM2 = B.TM2;
     double dS = d_TM2 * (-2 * B.lgNum) +
-                d_ecc * (-2 * TM2 / logNum * (-cE - B.SINI * (-e * cw * sE / sq1 - sw))) +
-                d_E * (-2 * TM2 / logNum * (e * sE - B.SINI * (sq1 * cE * cw - sE * sw))) +
-                d_omega * (2 * TM2 / logNum * B.SINI * ((cE - e) * cw - sq1 * sE * sw)) +
-                d_SINI * (-2 * TM2 / logNum * (-sq1 * cw * sE - (cE - e) * sw));
+                d_ecc * (-2 * TM2 * ilN * (-cE - B.SINI * (-e * cw * sE * B.isqE - sw))) +
+                d_E * (-2 * TM2 * ilN * (e * sE - B.SINI * (sq1 * cE * cw - sE * sw))) +
+                d_omega * (2 * TM2 * ilN * B.SINI * ((cE - e) * cw - sq1 * sE * sw)) +
+                d_SINI * (-2 * TM2 * ilN * (-sq1 * cw * sE - (cE - e) * sw));
     // delayA (DD_model.py:808-848)
     const double soPn = B.soPn, coPn = B.coPn;
     double dA;
@@ -599,7 +644,7 @@ PD dd spin_phase(const pint_spec_t& S, const double* P, dd dt) {
     int m = S.nf;
     dd r = pdd(P, S.o_F + 2 * (m - 1));
     for (int j = m - 1; j >= 1; j--) {
-        r = dd_add(dd_div_d(dd_mul(r, dt), (double)(j + 1)), pdd(P, S.o_F + 2 * (j - 1)));
+        r = dd_add(dd_div_int(dd_mul(r, dt), j + 1), pdd(P, S.o_F + 2 * (j - 1)));
     }
     return dd_mul(r, dt);
 }
@@ -607,7 +652,7 @@ PD dd spin_phase(const pint_spec_t& S, const double* P, dd dt) {
 PD double spin_freq(const pint_spec_t& S, const double* P, double dt) {
     int m = S.nf;
     double r = pval(P, S.o_F + 2 * (m - 1));
-    for (int j = m - 1; j >= 1; j--) r = r * dt / (double)j + pval(P, S.o_F + 2 * (j - 1));
+    for (int j = m - 1; j >= 1; j--) r = r * dt * inv_int(j) + pval(P, S.o_F + 2 * (j - 1));
     return r;
 }
 
@@ -643,10 +688,10 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         rr = t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1] + t.pos[2] * t.pos[2];
         re_dot_L = t.pos[0] * L[0] + t.pos[1] * L[1] + t.pos[2] * L[2];
         if (has_pos) {
-            double d = -re_dot_L / C_KMS;
+            double d = -re_dot_L * INV_C_KMS;
             if (px_mas != 0.0) {
-                double Lkm = KPC_KM / px_mas;
-                d += (0.5 * (rr / Lkm) * (1.0 - re_dot_L * re_dot_L / rr)) / C_KMS;
+                // r^2/L with L = kpc/PX: rr * PX / kpc
+                d += (0.5 * (rr * px_mas * INV_KPC_KM) * (1.0 - re_dot_L * re_dot_L / rr)) * INV_C_KMS;
             }
             delay += d;
         }
@@ -655,13 +700,13 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     if (S.shapiro && !is_bary) {
         double rs = sqrt(t.sun[0] * t.sun[0] + t.sun[1] * t.sun[1] + t.sun[2] * t.sun[2]);
         double rct = t.sun[0] * L[0] + t.sun[1] * L[1] + t.sun[2] * L[2];
-        delay += -2.0 * TSUN * log((rs - rct) / AU_KM);
+        delay += -2.0 * TSUN * log((rs - rct) * INV_AU_KM);
     }
     // ---- barycentric radio frequency (astrometry.py:359-364) ----
     double bfreq = t.freq;
     if (S.astrometry) {
         double vdl = t.vel[0] * L[0] + t.vel[1] * L[1] + t.vel[2] * L[2];
-        bfreq = t.freq * (1.0 - vdl / C_KMS);
+        bfreq = t.freq * (1.0 - vdl * INV_C_KMS);
     }
     double inv_f2 = 1.0 / (bfreq * bfreq);
     // ---- DispersionDM (dispersion_model.py:217-234) ----
@@ -671,11 +716,11 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         for (int k = 1; k < S.ndm; k++) any |= (pval(P, S.o_DM + 2 * k) != 0.0);
         if (S.o_DMEPOCH >= 0) {
             dd dtd = dd_sub(t.tdb, pdd(P, S.o_DMEPOCH));
-            dt_yr_dm = dd_to_d(dtd) / DJY;
+            dt_yr_dm = dd_to_d(dtd) * INV_DJY;
         }
         double x = any ? dt_yr_dm : 0.0;
         double dm = pval(P, S.o_DM + 2 * (S.ndm - 1));
-        for (int k = S.ndm - 1; k >= 1; k--) dm = dm * x / (double)k + pval(P, S.o_DM + 2 * (k - 1));
+        for (int k = S.ndm - 1; k >= 1; k--) dm = dm * x * inv_int(k) + pval(P, S.o_DM + 2 * (k - 1));
         delay += dm * DMCONST * inv_f2;
     }
     // ---- DMX (dispersion_model.py:659-678) ----
@@ -689,17 +734,18 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     BinState B;
     B.status = 0;
     if (BIN == 1) {
-        ell1_setup(S, P, t.tdb, delay, B);
+        ell1_setup(S, P, C, t.tdb, delay, B);
         delay += B.delay;
     } else if (BIN == 2) {
-        ddm_setup(S, P, t.tdb, delay, B);
+        ddm_setup(S, P, C, t.tdb, delay, B);
         delay += B.delay;
         if (B.status) o.status = B.status;
     }
     // ---- FD (frequency_dependent.py:70-101) ----
-    double logf = log(bfreq / 1000.0);
-    if (!isfinite(logf)) logf = 0.0;
+    double logf = 0.0;  // used by FD and its columns only
     if (S.nfd > 0) {
+        logf = log(bfreq * 1e-3);
+        if (!isfinite(logf)) logf = 0.0;
         double fd = 0.0;
         for (int k = S.nfd; k >= 1; k--) fd = fd * logf + pval(P, S.o_FD + 2 * (k - 1));
         fd *= logf;
@@ -726,28 +772,29 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities), once per TOA
     double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
     if (S.astrometry) {
-        double r_km = sqrt(rr);
-        double xy = sqrt(t.pos[0] * t.pos[0] + t.pos[1] * t.pos[1]);
-        double edec = atan2(t.pos[2], xy);
-        double era = atan2(t.pos[1], t.pos[0]);
+        // Earth direction angles (era, edec) of the SSB->observatory vector enter only as
+        // cos(edec) sin(plon - era), cos(edec) cos(plon - era) and sin(edec): formed from
+        // the vector itself, cos(edec) cos(era) = x/r etc. (no atan2/sin/cos per TOA)
+        double u[3] = {t.pos[0], t.pos[1], t.pos[2]};
         if (S.astrometry == 2) {
             // earth ecliptic lon/lat via ICRS->PulsarEcliptic (astrometry.py:1034-1055)
-            double ue[3] = {cos(era) * cos(edec), sin(era) * cos(edec), sin(edec)}, ee[3];
-            icrs_to_ecl(S.obliquity, ue, ee);
-            era = atan2(ee[1], ee[0]);
-            edec = atan2(ee[2], sqrt(ee[0] * ee[0] + ee[1] * ee[1]));
+            double ue[3] = {u[0], u[1], u[2]};
+            icrs_to_ecl(S.obliquity, ue, u);
         }
-        const double ced = cos(edec), sed = sin(edec);
-        const double sdl = sin(C.plon - era), cdl = cos(C.plon - era);
+        const double r_km = sqrt(rr);
+        const double ir = r_km > 0.0 ? 1.0 / r_km : 0.0;
+        const double ced_sdl = (C.splon * u[0] - C.cplon * u[1]) * ir;
+        const double ced_cdl = (C.cplon * u[0] + C.splon * u[1]) * ir;
+        const double sed = u[2] * ir;
         const double te_s = S.o_POSEPOCH >= 0 ? dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC)) : 0.0;
-        const double rc = chain * r_km / C_KMS;
+        const double rc = chain * r_km * INV_C_KMS;
         // d_delay_astrometry_d_RAJ / _ELONG, _DECJ / _ELAT, PM partials x te (astrometry.py:536-627, 1067-1170)
-        gLON = rc * (ced * C.cplat * sdl) * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
-        gLAT = rc * (ced * C.splat * cdl - sed * C.cplat) * DEG_RAD;
-        gPMLON = rc * (ced * sdl) * te_s * MASYR_RADS;
-        gPMLAT = rc * (ced * C.splat * cdl - C.cplat * sed) * te_s * MASYR_RADS;
+        gLON = rc * (ced_sdl * C.cplat) * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
+        gLAT = rc * (ced_cdl * C.splat - sed * C.cplat) * DEG_RAD;
+        gPMLON = rc * ced_sdl * te_s * MASYR_RADS;
+        gPMLAT = rc * (ced_cdl * C.splat - C.cplat * sed) * te_s * MASYR_RADS;
         // d_delay_astrometry_d_PX (astrometry.py:219-249)
-        gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) / (AU_KM * C_KMS)) * MAS_RAD;
+        gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
     }
     Ell1Grad eg;
     if (BIN == 1) ell1_grad(B, eg);
@@ -761,9 +808,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
             case PINT_COL_OFFSET: colp[r] = iF0; break;
             case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): -dt^(k+1)/(k+1)! / F0
                 double v = 1.0;
-                for (int j = 1; j <= R.idx0; j++) v = v * dtd / (double)j;
+                for (int j = 1; j <= R.idx0; j++) v = v * dtd * inv_int(j);
                 for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    v = v * dtd / (double)(R.idx0 + j + 1);
+                    v = v * dtd * inv_int(R.idx0 + j + 1);
                     colp[r] = -v * iF0;
                 }
             } break;
@@ -777,9 +824,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
             case PINT_COL_PX: colp[r] = gPX; break;
             case PINT_COL_DM: {  // d_dm_d_DMs (dispersion_model.py:253) * DMconst / bfreq^2
                 double v = 1.0;
-                for (int j = 1; j <= R.idx0; j++) v = v * dt_yr_dm / (double)j;
+                for (int j = 1; j <= R.idx0; j++) v = v * dt_yr_dm * inv_int(j);
                 for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    if (j > 0) v = v * dt_yr_dm / (double)(R.idx0 + j);
+                    if (j > 0) v = v * dt_yr_dm * inv_int(R.idx0 + j);
                     colp[r] = dmc * v;
                 }
             } break;
