@@ -3,8 +3,9 @@
 // Launch sequence per fit iteration (all instances of a batch in each launch):
 //   k_eval      one thread per TOA row: delays, dd phase, design-matrix row, red-noise
 //               Fourier columns (HBM-streaming; timing_model.py:1515/1548/2073)
-//   k_resid     one workgroup per instance: TZR subtraction, track mode, weighted mean,
-//               time residuals, WLS chi2 (residuals.py:314-667) — wave-shuffle reductions
+//   k_resid1/2  1024-row blocks of every instance: TZR subtraction, track mode, weighted
+//               mean, time residuals, WLS chi2 (residuals.py:314-667) — wave-shuffle
+//               reductions, block partials summed in a fixed order
 //   k_gram      FP64 MFMA (v_mfma_f64_16x16x4f64) Gram [T|r]^T W [T|r] over TOA chunks
 //               staged in LDS, split over N (fitter.py:2187-2192, :1425-1470)
 //   k_solve     one workgroup per instance: normalisation, Cholesky in LDS, xhat, inverse
@@ -85,7 +86,8 @@ struct InstDev {
     long ddoff;
     long vgoff;  // k_gram_v DMX slot partials offset (nsplit * vns * (Kd+3))
     int self;    // index of this instance in the batch
-    int pad_;
+    int nrb;     // k_resid row blocks of this instance (RES_RB rows each)
+    long rb0;    // first k_resid row block
 };
 
 // Symmetric view of an instance's Gram [T|r]^T W [T|r] in the original column order:
@@ -252,27 +254,34 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
 }
 
 // ---------------------------------------------------------------------------------
-// k_resid: one 1024-thread workgroup per instance — residuals.py:314-425, :483-538, :638-667
+// k_resid1/k_resid2 — residuals.py:314-425, :483-538, :638-667
 // ---------------------------------------------------------------------------------
-constexpr int RES_T = 1024;
-__global__ __launch_bounds__(RES_T) void k_resid(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                 const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
-                                                 const double* __restrict__ ftay, double* __restrict__ rtime,
-                                                 double* __restrict__ rphase, double* __restrict__ chi2) {
-    __shared__ double sh[RES_T / 64];
-    const InstDev I = insts[blockIdx.x];
+// The residual pass split over RES_RB-row blocks of every instance,
+// so a batch of a few large pulsars still fills the CUs.  k_resid1 forms the phase
+// residuals and each block's weighted sums; k_resid2 sums the instance's block partials in
+// a fixed order (deterministic), subtracts the weighted mean, converts to time and
+// accumulates chi2 partials, which k_rsum adds per instance.
+constexpr int RES_BT = 256;
+constexpr int RES_RB = 1024;  // rows per block (4 per thread)
+__global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const int* __restrict__ rblk_inst,
+                                                   const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
+                                                   double* __restrict__ rphase, double* __restrict__ rpart) {
+    __shared__ double sh[RES_BT / 64];
+    const int ii = rblk_inst[blockIdx.x];
+    const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
-    int n = I.n;
-    long ro = I.roff;
-    long oo = I.roff - blockIdx.x;  // output rows: n per instance (roff counts n+1)
-    dd tz = dd_make(ph_hi[ro + n], ph_lo[ro + n]);
+    const int n = I.n;
+    const long ro = I.roff;
+    const long oo = I.roff - ii;  // output rows: n per instance (roff counts n+1)
+    const int r0 = (int)(blockIdx.x - I.rb0) * RES_RB;
+    const int r1 = min(n, r0 + RES_RB);
+    const dd tz = dd_make(ph_hi[ro + n], ph_lo[ro + n]);
     dd d0 = dd_make(0.0);
-    if (!S.track_pn && S.subtract_mean) {
-        d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
-    }
+    if (!S.track_pn && S.subtract_mean) d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
     double sw = 0.0, swx = 0.0;
-    for (int i = threadIdx.x; i < n; i += RES_T) {
+    for (int i = r0 + threadIdx.x; i < r1; i += RES_BT) {
         dd d = dd_add_d(dd_sub(dd_make(ph_hi[ro + i], ph_lo[ro + i]), tz), Pd.dpn[i]);
         double full;
         if (S.track_pn) {
@@ -286,23 +295,63 @@ __global__ __launch_bounds__(RES_T) void k_resid(const PsrDev* __restrict__ psrs
         sw += w;
         swx += w * full;
     }
-    double mean = 0.0;
     if (S.subtract_mean) {
-        double a = block_sum<RES_T / 64>(swx, sh);
-        double bsum = block_sum<RES_T / 64>(sw, sh);
-        mean = a / bsum;
+        swx = block_sum<RES_BT / 64>(swx, sh);
+        sw = block_sum<RES_BT / 64>(sw, sh);
+        if (threadIdx.x == 0) {
+            rpart[3 * blockIdx.x] = sw;
+            rpart[3 * blockIdx.x + 1] = swx;
+        }
+    }
+}
+
+__global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const int* __restrict__ rblk_inst, const double* __restrict__ ftay,
+                                                   double* __restrict__ rtime, double* __restrict__ rphase,
+                                                   double* __restrict__ rpart) {
+    __shared__ double sh[RES_BT / 64];
+    const int ii = rblk_inst[blockIdx.x];
+    const InstDev I = insts[ii];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int n = I.n;
+    const long ro = I.roff;
+    const long oo = I.roff - ii;
+    const int r0 = (int)(blockIdx.x - I.rb0) * RES_RB;
+    const int r1 = min(n, r0 + RES_RB);
+    double mean = 0.0;
+    if (S.subtract_mean) {  // residuals.py:314-425 weighted mean (utils.py:2002), fixed tree order
+        double a = 0.0, b = 0.0;
+        for (int k = threadIdx.x; k < I.nrb; k += RES_BT) {
+            b += rpart[3 * (I.rb0 + k)];
+            a += rpart[3 * (I.rb0 + k) + 1];
+        }
+        a = block_sum<RES_BT / 64>(a, sh);
+        b = block_sum<RES_BT / 64>(b, sh);
+        mean = a / b;
     }
     double c2 = 0.0;
-    for (int i = threadIdx.x; i < n; i += RES_T) {
+    for (int i = r0 + threadIdx.x; i < r1; i += RES_BT) {
         double p = rphase[oo + i] - mean;
         rphase[oo + i] = p;
-        double rt = p / ftay[ro + i];
+        double rt = p / ftay[ro + i];  // calc_time_resids (residuals.py:483-538)
         rtime[oo + i] = rt;
         double z = rt * Pd.isig[i];
         c2 += z * z;
     }
-    c2 = block_sum<RES_T / 64>(c2, sh);
-    if (threadIdx.x == 0) chi2[blockIdx.x] = c2;
+    c2 = block_sum<RES_BT / 64>(c2, sh);
+    if (threadIdx.x == 0) rpart[3 * blockIdx.x + 2] = c2;
+}
+
+// _calc_wls_chi2 (residuals.py:638-667): one wave per instance sums its blocks' chi2
+// partials in a fixed tree order (a kernel boundary, not a device-wide fence, orders them)
+__global__ __launch_bounds__(64) void k_rsum(const InstDev* __restrict__ insts, const double* __restrict__ rpart,
+                                             double* __restrict__ chi2) {
+    const InstDev I = insts[blockIdx.x];
+    double t = 0.0;
+    for (int k = threadIdx.x; k < I.nrb; k += 64) t += rpart[3 * (I.rb0 + k) + 2];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) chi2[blockIdx.x] = t;
 }
 
 // ---------------------------------------------------------------------------------
@@ -2322,6 +2371,9 @@ struct pint_ctx {
     bool capturing = false;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
+    int* d_rblk_inst = nullptr;   // k_resid1/2 block -> instance
+    double* d_rpart = nullptr;    // per residual block: sum w, sum w x, chi2 partial
+    int nrblk = 0;
     int nblk = 0;
     int blk_off[4] = {0, 0, 0, 0};  // block ranges per binary type (0 none, 1 ELL1, 2 DD)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
@@ -2528,7 +2580,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
-                   (void**)&ctx->d_TSp, (void**)&ctx->d_TS};
+                   (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart};
     for (auto p : ps) dfree(*p);
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
@@ -2756,6 +2808,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     long sdoff = 0, ddoff = 0;
     int max_nep = 0, max_ndc = 0;
     std::vector<int> bti[3], btr[3];
+    std::vector<int> rbi;
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
@@ -2860,6 +2913,9 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             if (ph.dev.ndc > max_ndc) max_ndc = ph.dev.ndc;
         }
         I.self = k;
+        I.rb0 = (long)rbi.size();
+        I.nrb = std::max(1, (ph.n + RES_RB - 1) / RES_RB);
+        for (int b = 0; b < I.nrb; b++) rbi.push_back(k);
         eoff += (long)ph.dev.nep * I.Kp;
         epoff += ph.dev.nep;
         if (ph.dev.nep > max_nep) max_nep = ph.dev.nep;
@@ -2945,6 +3001,12 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_blk_row0, sizeof(int) * br.size()));
     HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_blk_row0, br.data(), sizeof(int) * br.size(), hipMemcpyHostToDevice));
+    ctx->nrblk = (int)rbi.size();
+    HIPCHK(cmalloc((void**)&ctx->d_rblk_inst, sizeof(int) * std::max<size_t>(1, rbi.size())));
+    if (!rbi.empty())
+        HIPCHK(hipMemcpy(ctx->d_rblk_inst, rbi.data(), sizeof(int) * rbi.size(), hipMemcpyHostToDevice));
+    HIPCHK(cmalloc((void**)&ctx->d_rpart, sizeof(double) * 3 * std::max<size_t>(1, rbi.size())));
+
     HIPCHK(cmalloc((void**)&ctx->d_tables, sizeof(double) * toff));
     HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
     HIPCHK(cmalloc((void**)&ctx->d_phhi, sizeof(double) * roff));
@@ -3075,8 +3137,13 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     }
     record(ctx, want_M ? 3 : 1);
     record(ctx, 4);
-    hipLaunchKernelGGL(k_resid, dim3(ctx->ninst), dim3(RES_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_phhi,
-                       ctx->d_phlo, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_chi2);
+    if (ctx->nrblk > 0) {
+        hipLaunchKernelGGL(k_resid1, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_rblk_inst, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
+        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart);
+        hipLaunchKernelGGL(k_rsum, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_inst, ctx->d_rpart, ctx->d_chi2);
+    }
     HIPCHK(hipGetLastError());
     record(ctx, 5);
     if (ctx->lazy) return PINT_OK;
