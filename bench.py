@@ -100,16 +100,28 @@ def main():
 
     SLOT_GRAM = 6
     s.set_timing_mask(1 << SLOT_GRAM)  # timed region: HIP events around the Gram kernel only
-    for _ in range(args.warmup):
-        step()
-        s.check()
+
+    def run(nsteps):
+        """nsteps steps, pipelined two deep: step k+1 is enqueued before the host waits for
+        step k (Session.step_end / check_step), so the device does not idle while the host
+        checks a step and issues the next.  Returns the summed Gram-kernel event time."""
+        kt, prev = 0.0, None
+        for _ in range(nsteps):
+            step()
+            cur = s.step_end()
+            if prev is not None:
+                s.check_step(prev)  # device status + the Gram kernel's HIP-event time
+                kt += s.timing()[SLOT_GRAM]
+            prev = cur
+        if prev is not None:
+            s.check_step(prev)
+            kt += s.timing()[SLOT_GRAM]
+        return kt
+
+    run(args.warmup)
     barrier()
     t0 = time.perf_counter()
-    kt_gram = 0.0
-    for _ in range(args.steps):
-        step()
-        s.check()              # device status + the Gram kernel's HIP-event time
-        kt_gram += s.timing()[SLOT_GRAM]
+    kt_gram = run(args.steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:

@@ -187,6 +187,16 @@ int pint_vgram_layout(pint_ctx *ctx, int psr, int32_t *out4);
  * buffers (pint_host_alloc) for the copies to run asynchronously. */
 int pint_set_lazy(pint_ctx *ctx, int lazy);
 int pint_check(pint_ctx *ctx);
+
+/* Pipelined steps (replaces the per-step pint_check of a lazy-mode loop; no reference
+ * counterpart -- the reference's fitters are synchronous).  pint_step_end closes the work
+ * enqueued since the previous step_end and returns its slot (0/1) in *slot; launches
+ * after it go to the other slot (own status word, timing events).  pint_check_step waits
+ * for that step only and returns its status, so the host enqueues step k+1 while the
+ * device runs step k.  At most two steps in flight: check slot s before ending the step
+ * after the next.  Pinned output buffers must be per slot. */
+int pint_step_end(pint_ctx *ctx, int *slot);
+int pint_check_step(pint_ctx *ctx, int slot);
 /* Engine options (no reference counterpart): PINT_OPT_BLOCKED_SOLVE = 1 (default) solves
  * the normal equations with the blocked FP64-MFMA kernel, 0 with the column-by-column
  * LDS kernel (used by the tests to cross-check the two).  PINT_OPT_VGRAM = 1 (default)

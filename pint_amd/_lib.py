@@ -93,6 +93,8 @@ def lib():
     L.pint_host_free.argtypes = [vp]
     L.pint_set_ecorr.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dptr]
     L.pint_check.argtypes = [vp]
+    L.pint_step_end.argtypes = [vp, C.POINTER(C.c_int)]
+    L.pint_check_step.argtypes = [vp, C.c_int]
     _lib = L
     return L
 
@@ -103,7 +105,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",
             "pint_set_option", "pint_host_alloc", "pint_host_free",
             "pint_fit_layout", "pint_query", "pint_capture_begin", "pint_capture_end", "pint_graph_launch",
-            "pint_vgram_layout", "pint_lognorm", "pint_solve_eig"]
+            "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

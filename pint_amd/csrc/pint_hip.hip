@@ -171,14 +171,33 @@ __device__ double block_sum(double v, double* sh) {
 // ---------------------------------------------------------------------------------
 // k_prep: per-instance constants of the evaluation (astrometry/starpm state, 1/F0), one
 // thread per instance, so k_eval's threads only do per-TOA work.
-__global__ __launch_bounds__(64) void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, int ninst,
-                       const double* __restrict__ tables, InstConst* __restrict__ ic) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ninst) return;
-    const InstDev I = insts[k];
-    InstConst C;
-    inst_setup(*psrs[I.psr].spec, tables + I.toff, C);
-    ic[k] = C;
+// The setup is one thread's serial code over a dozen parameters; its global loads would be
+// a chain of dependent round trips, so the block first stages the spec header (everything
+// before the column arrays, all that inst_setup reads) and the table in LDS, coalesced.
+constexpr int PREP_T = 64;
+constexpr int PREP_MAXTAB = 1024;  // doubles of a staged table (larger ones read in place)
+constexpr int PREP_HDR = (int)(offsetof(pint_spec_t, col_kind) + 7) / 8;  // spec header, doubles
+__device__ __forceinline__ void prep_one(const pint_spec_t* Sg, const double* Pg, int tstride, InstConst* out) {
+    __shared__ double sS[PREP_HDR];
+    __shared__ double sP[PREP_MAXTAB];
+    const double* hg = reinterpret_cast<const double*>(Sg);
+    for (int i = threadIdx.x; i < PREP_HDR; i += blockDim.x) sS[i] = hg[i];
+    const bool staged = tstride <= PREP_MAXTAB;
+    if (staged)
+        for (int i = threadIdx.x; i < tstride; i += blockDim.x) sP[i] = Pg[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        InstConst C;
+        inst_setup(*reinterpret_cast<const pint_spec_t*>(sS), staged ? sP : Pg, C);
+        *out = C;
+    }
+}
+
+__global__ __launch_bounds__(PREP_T) void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                 const double* __restrict__ tables, InstConst* __restrict__ ic) {
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    prep_one(Pd.spec, tables + I.toff, Pd.spec->tstride, ic + blockIdx.x);
 }
 
 template <int WANT_M, int BIN>
@@ -2319,11 +2338,7 @@ __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restri
         P[o + 1] = v.lo;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        InstConst C;
-        inst_setup(S, P, C);
-        ic[inst] = C;
-    }
+    prep_one(psrs[I.psr].spec, P, S.tstride, ic + inst);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2404,8 +2419,18 @@ struct pint_ctx {
     // reduction, 7/8 solve, 10/11 Woodbury chi2, 12/13 the Gram kernels alone, 14/15 k_greduce
     // (side stream)
     static constexpr int NEV = 16, NMS = 8;
-    hipEvent_t ev[NEV];
-    bool rec[NEV] = {false};
+    // pipelined steps (pint_step_end / pint_check_step): two slots, each with its own timing
+    // events, status word and end-of-step event; non-pipelined use stays in slot 0
+    int slot = 0;
+    hipEvent_t ev_slot[2][NEV];
+    bool rec_slot[2][NEV] = {{false}};
+    hipEvent_t* ev = ev_slot[0];  // the current slot's events
+    bool* rec = rec_slot[0];
+    hipEvent_t ev_done[2] = {nullptr, nullptr};
+    hipEvent_t ev_cdone[2] = {nullptr, nullptr};  // the step's output copies (copy stream)
+    bool cdone_rec[2] = {false, false};
+    int* d_status_slots = nullptr;  // 2 status words on the device
+    int* h_status = nullptr;        // their pinned host mirrors
     float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
@@ -2557,9 +2582,16 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
-    for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev[i]);
-    hipMalloc(&ctx->d_status, sizeof(int));
-    hipMemset(ctx->d_status, 0, sizeof(int));
+    for (int sl = 0; sl < 2; sl++) {
+        for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev_slot[sl][i]);
+        hipEventCreateWithFlags(&ctx->ev_done[sl], hipEventDisableTiming);
+        hipEventCreateWithFlags(&ctx->ev_cdone[sl], hipEventDisableTiming);
+    }
+    hipMalloc(&ctx->d_status_slots, 2 * sizeof(int));
+    hipMemset(ctx->d_status_slots, 0, 2 * sizeof(int));
+    ctx->d_status = ctx->d_status_slots;
+    hipHostMalloc(&ctx->h_status, 2 * sizeof(int), hipHostMallocDefault);
+    if (ctx->h_status) ctx->h_status[0] = ctx->h_status[1] = 0;
     return ctx;
 }
 
@@ -2601,8 +2633,13 @@ void pint_ctx_destroy(pint_ctx* ctx) {
         for (auto b : p.bufs) hipFree(b);
     }
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
-    if (ctx->d_status) hipFree(ctx->d_status);
-    for (int i = 0; i < 12; i++) hipEventDestroy(ctx->ev[i]);
+    if (ctx->d_status_slots) hipFree(ctx->d_status_slots);
+    if (ctx->h_status) hipHostFree(ctx->h_status);
+    for (int sl = 0; sl < 2; sl++) {
+        for (int i = 0; i < pint_ctx::NEV; i++) hipEventDestroy(ctx->ev_slot[sl][i]);
+        if (ctx->ev_done[sl]) hipEventDestroy(ctx->ev_done[sl]);
+        if (ctx->ev_cdone[sl]) hipEventDestroy(ctx->ev_cdone[sl]);
+    }
     if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
     if (ctx->ev_solved) hipEventDestroy(ctx->ev_solved);
     if (ctx->ev_copied) hipEventDestroy(ctx->ev_copied);
@@ -3082,6 +3119,8 @@ static void update_timings(pint_ctx* ctx) {
     }
 }
 
+static int decode_status(pint_ctx* ctx, int st);
+
 static int check_status(pint_ctx* ctx) {
     int st = 0;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
@@ -3090,6 +3129,10 @@ static int check_status(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     // the status word accumulates error bits of everything enqueued since the last check
     if (st) HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
+    return decode_status(ctx, st);
+}
+
+static int decode_status(pint_ctx* ctx, int st) {
     if (st & (1 << PINT_E_KEPLER)) { ctx->err = "Kepler equation: eccentricity outside [0,1) or no convergence"; return PINT_E_KEPLER; }
     if (st & (1 << PINT_E_SIGMA)) { ctx->err = "Woodbury Sigma (noise basis) not positive definite"; return PINT_E_SIGMA; }
     if (st & (1 << PINT_E_NOT_PD)) { ctx->err = "normal matrix not positive definite"; return PINT_E_NOT_PD; }
@@ -3113,8 +3156,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     }
     record(ctx, want_M ? 2 : 0);
     if (!ctx->ic_valid) {  // k_apply refreshes them itself
-        hipLaunchKernelGGL(k_prep, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->ninst, ctx->d_tables, ctx->d_ic);
+        hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->d_ic);
         HIPCHK(hipGetLastError());
         ctx->ic_valid = true;
     }
@@ -3538,7 +3581,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {
         ctx->timing_mask = value & 0xff;
-        for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec[k] = false;
+        for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec_slot[0][k] = ctx->rec_slot[1][k] = false;
         for (int k = 0; k < pint_ctx::NMS; k++) ctx->ms[k] = 0.0f;
         return PINT_OK;
     }
@@ -3623,6 +3666,54 @@ int pint_check(pint_ctx* ctx) {
     int rc = check_status(ctx);
     update_timings(ctx);
     return rc;
+}
+
+// Pipelined steps: pint_step_end closes the work enqueued since the previous step_end (the
+// side streams joined, the status word copied to its pinned mirror, an end event) and moves
+// the launches that follow to the other slot; pint_check_step(s) waits for step s only, so
+// the host enqueues step k+1 while the device still runs step k.  Two steps in flight at
+// most: the caller checks step s before ending the step after the next one.
+int pint_step_end(pint_ctx* ctx, int* slot) {
+    if (!ctx || ctx->capturing || !slot) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    // the output copies of this step stay on the copy stream, overlapped with the next
+    // step's evaluation and Gram: the next solve waits for them (copy_pending), and the
+    // step's completion covers them through ev_cdone
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
+    ctx->sigma_pending = false;
+    const int s = ctx->slot;
+    ctx->cdone_rec[s] = ctx->copy_pending;
+    if (ctx->copy_pending) HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
+    HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_done[s], ctx->stream));
+    ctx->slot = s ^ 1;
+    ctx->d_status = ctx->d_status_slots + ctx->slot;
+    ctx->ev = ctx->ev_slot[ctx->slot];
+    ctx->rec = ctx->rec_slot[ctx->slot];
+    for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec[k] = false;
+    *slot = s;
+    return PINT_OK;
+}
+
+int pint_check_step(pint_ctx* ctx, int s) {
+    if (!ctx || s < 0 || s > 1) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHK(hipEventSynchronize(ctx->ev_done[s]));
+    if (ctx->cdone_rec[s]) HIPCHK(hipEventSynchronize(ctx->ev_cdone[s]));
+    ctx->cdone_rec[s] = false;
+    const int st = ctx->h_status[s];
+    if (st) {
+        ctx->h_status[s] = 0;
+        HIPCHK(hipMemsetAsync(ctx->d_status_slots + s, 0, sizeof(int), ctx->stream));
+    }
+    hipEvent_t* ev = ctx->ev;
+    bool* rec = ctx->rec;
+    ctx->ev = ctx->ev_slot[s];
+    ctx->rec = ctx->rec_slot[s];
+    update_timings(ctx);
+    ctx->ev = ev;
+    ctx->rec = rec;
+    return decode_status(ctx, st);
 }
 
 int pint_last_timing(pint_ctx* ctx, double* ms) {

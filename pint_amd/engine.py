@@ -335,6 +335,9 @@ class Session:
         self._pinned: Dict[str, tuple] = {}
         self._inflight = set()  # pinned staging buffers with a copy still enqueued (lazy)
         self._keep = []         # host arrays of enqueued copies (lazy)
+        self._slot = 0          # pipelined steps: the slot the next launches belong to
+        self._slot_state = {0: (self._inflight, self._keep), 1: (set(), [])}
+        self._pending = set()   # slots of ended, not yet checked steps
 
     def close(self):
         if self.ctx:
@@ -346,8 +349,12 @@ class Session:
 
     def _pin(self, name, n):
         """Page-locked host buffer of n doubles (reused across calls, grown on demand), so
-        device->host copies of the fit outputs can run asynchronously."""
+        device->host copies of the fit outputs can run asynchronously.  One per pipeline
+        slot (step_end/check_step), so step k+1's copies never touch step k's buffers."""
         n = max(1, int(n))
+        if self._slot in self._pending:
+            raise RuntimeError("pipelined steps: enqueueing into a slot whose step was never checked")
+        name = f"{name}@{self._slot}"
         cur = self._pinned.get(name)
         if cur is not None and cur[1].size >= n:
             return cur[1][:n]
@@ -527,6 +534,29 @@ class Session:
         self._check(self.L.pint_check(self.ctx))
         self._inflight.clear()
         self._keep.clear()
+
+    # -- pipelined steps (lazy mode) ------------------------------------------------
+    def step_end(self) -> int:
+        """Close the step enqueued since the previous step_end; later launches, pinned
+        buffers and status go to the other slot.  Returns the closed step's slot for
+        check_step().  At most two steps in flight."""
+        sl = C.c_int(-1)
+        self._check(self.L.pint_step_end(self.ctx, C.byref(sl)))
+        self._slot_state[sl.value] = (self._inflight, self._keep)
+        self._pending.add(sl.value)
+        self._slot = sl.value ^ 1
+        self._inflight, self._keep = self._slot_state[self._slot]
+        return sl.value
+
+    def check_step(self, slot: int):
+        """Wait for the step closed as `slot`; its outputs (pinned buffers handed out while
+        it was enqueued) and timing() are then complete."""
+        rc = self.L.pint_check_step(self.ctx, int(slot))
+        self._pending.discard(int(slot))
+        inflight, keep = self._slot_state[slot]
+        inflight.clear()
+        keep.clear()
+        self._check(rc)
 
     def read_step(self, want_cov=True):
         kk = [l.K + 1 for l in self.inst_layout]

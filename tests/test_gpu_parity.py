@@ -455,6 +455,78 @@ def test_graph_replay_matches_direct():
     s.close()
 
 
+def test_pipelined_steps_match_synchronous():
+    """Steps pipelined two deep (Session.step_end / check_step: step k+1 enqueued before the
+    host waits for step k, per-slot pinned outputs and status words) give bit-identical
+    outputs to synchronous steps, each step's outputs intact after the next was enqueued;
+    a step's device error is reported by its own check_step."""
+    from pint_amd import _lib as L
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+    s = Session()
+    lays = [s.add(build_layout(m, t)) for m, t in items]
+    tabs = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
+    s.set_instances(list(zip(lays, tabs)))
+    flat = np.concatenate(tabs)
+    s.set_lazy(True)
+
+    def step(t):
+        s.set_tables(t)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        out = s.read_step()
+        s.apply_step(np.ones(len(lays)))
+        s.eval(want_M=False)
+        return out, s.chi2_gls()
+
+    def snap(res):
+        (dp, er, cov, cl), c2 = res
+        return [x.copy() for x in dp], [x.copy() for x in er], [x.copy() for x in cov], cl.copy(), c2.copy()
+
+    # three different tables: the second perturbs F0 of every instance by 1e-12 relative
+    tables = [flat, flat.copy(), flat]
+    for l in lays:
+        o = sum(x.tstride for x in lays[:lays.index(l)]) + l.offsets["F0"]
+        tables[1][o] *= 1 + 1e-12
+    want = []
+    for t in tables:
+        r = step(t)
+        s.check()
+        want.append(snap(r))
+    got, prev, pending = [], None, None
+    for t in tables:
+        r = step(t)
+        cur = s.step_end()
+        if prev is not None:
+            s.check_step(prev)
+            got.append(snap(pending))
+        prev, pending = cur, r
+    s.check_step(prev)
+    got.append(snap(pending))
+    for w, g in zip(want, got):
+        for a, b in zip(w[:3], g[:3]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
+        assert np.array_equal(w[3], g[3]) and np.array_equal(w[4], g[4])
+    assert not np.array_equal(want[0][4], want[1][4])
+    # an invalid DD eccentricity in the first of two in-flight steps: its check reports it,
+    # the next (valid) step's check does not
+    k_dd = 0
+    bad = flat.copy()
+    bad[lays[k_dd].offsets["ECC"]] = 1.5
+    bad[lays[k_dd].offsets["ECC"] + 1] = 0.0
+    s.set_tables(bad)
+    s.eval(want_M=False)
+    a = s.step_end()
+    s.set_tables(flat)
+    s.eval(want_M=False)
+    b = s.step_end()
+    with pytest.raises(L.PintError):
+        s.check_step(a)
+    s.check_step(b)
+    s.close()
+
+
 def test_lnlikelihood(fx):
     """Residuals.calc_chi2(lognorm=True) / lnlikelihood (residuals.py:669-716) on the GPU
     against the reference's values: log_norm = logdet(C)/2 (Woodbury determinant from the
