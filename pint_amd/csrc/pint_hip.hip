@@ -12,6 +12,7 @@
 //               (covariance), Woodbury Sigma factor for the GLS chi2 (utils.py:3074)
 //   k_apply     parameter update in double-double (fitter.py:957, :2073-2080)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <string>
 #include <vector>
 #include <cstring>
@@ -2863,18 +2864,28 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     int maxsplit = (maxN + 4 * GCH - 1) / (4 * GCH);
     if (maxsplit < 1) maxsplit = 1;
+    // Resident Gram workgroups per CU: k_gram runs one 1024-thread workgroup per CU,
+    // k_gram_v two 256-thread ones (launch bounds, LDS); the batch's majority path decides.
+    long nvgc = 0;
+    for (int k = 0; k < ninst; k++) {
+        const PsrHost& ph = ctx->psrs[inst_psr[k]];
+        const PsrDev& d = ph.dev;
+        nvgc += (ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
+                 d.red0c + 1 <= VMAXR0) ? 1 : 0;
+    }
+    const long slots = (long)ncu * (2 * nvgc > ninst ? 2 : 1);
     // (smallest split count within 3% of the best makespan: each split adds a partial
     // Gram that k_greduce must sum)
     double best = 1e30;
     for (int ns = 1; ns <= maxsplit && ns <= 4096; ns++) {
         long blocks = (long)ninst * ns;
-        double cost = (double)((blocks + ncu - 1) / ncu) / ns;
+        double cost = (double)((blocks + slots - 1) / slots) / ns;
         if (cost < best) best = cost;
     }
     int nsplit = 1;
     for (int ns = 1; ns <= maxsplit && ns <= 4096; ns++) {
         long blocks = (long)ninst * ns;
-        double cost = (double)((blocks + ncu - 1) / ncu) / ns;
+        double cost = (double)((blocks + slots - 1) / slots) / ns;
         if (cost <= best * 1.03) { nsplit = ns; break; }
     }
     ctx->nsplit = nsplit;
@@ -3254,7 +3265,13 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             HIPCHK(hipGetLastError());
         }
     }
-    record(ctx, 12);
+    // Gram-kernel timing: when the whole Gram is k_gram_v launches, the slot's start/stop
+    // events ride on the first/last dispatch packet (hipExtLaunchKernel) instead of marker
+    // packets between kernels, which cost the stream ~10 us each
+    const bool gram_t = !ctx->no_events && ((ctx->timing_mask >> 6) & 1);
+    const bool ext_t = gram_t && vgp && (cmp ? ctx->kp_groups_c : ctx->kp_groups).empty() &&
+                       !ctx->kp_groups_v.empty();
+    if (!ext_t) record(ctx, 12);
     {
         // instances are launched in groups of equal tiles-per-wave T (template parameter);
         // per-instance tile counts are recomputed in-kernel from their own Kp.
@@ -3287,14 +3304,18 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         }
     }
     if (vgp) {
-        for (const KpGroup& kg : ctx->kp_groups_v) {
+        for (size_t gi = 0; gi < ctx->kp_groups_v.size(); gi++) {
+            const KpGroup& kg = ctx->kp_groups_v[gi];
             const InstDev* di = ctx->d_inst_sorted_v + kg.first;
+            hipEvent_t e0 = (ext_t && gi == 0) ? ctx->ev[12] : nullptr;
+            hipEvent_t e1 = (ext_t && gi + 1 == ctx->kp_groups_v.size()) ? ctx->ev[13] : nullptr;
             dim3 grid(ctx->nsplit, kg.count);
             const size_t lds = sizeof(double) * std::max<size_t>((size_t)(kg.maxKp + 48) * (VCH + 2),
                                                                  std::max(VW * VTG * 256, VW * 512 + 512));
 #define PINT_GRAMV(R_, C_)                                                                                       \
-            hipLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), lds, ctx->stream, ctx->d_psrs, di, ctx->d_M,   \
-                               ctx->d_rt, ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp)
+            hipExtLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), (uint32_t)lds, ctx->stream, e0, e1, 0u,  \
+                                  (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M, (const double*)ctx->d_rt, \
+                                  (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp)
             switch (kg.T) {
                 case 1: PINT_GRAMV(1, 1); break;
                 case 2: PINT_GRAMV(1, 2); break;
@@ -3324,7 +3345,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             }
 #undef PINT_GRAMV
         }
-        record(ctx, 13);
+        if (ext_t) ctx->rec[12] = ctx->rec[13] = true;
+        else record(ctx, 13);
         hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->nsplit, ctx->d_TSp, ctx->d_TS);
         HIPCHK(hipGetLastError());
