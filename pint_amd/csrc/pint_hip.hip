@@ -273,6 +273,31 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                             Mout, dmxv, compact, write_red, status);
 }
 
+// k_eval_mix: all binary models in one launch (heaviest first: DD, ELL1, isolated blocks),
+// each block running its own instantiation; the kernel carries the largest register set,
+// and saves the two launch tails of the per-model launches.
+template <int WANT_M>
+__global__ __launch_bounds__(256) void k_eval_mix(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                  const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
+                                                  int off1, int off2, int off3,
+                                                  const double* __restrict__ tables, const InstConst* __restrict__ ic,
+                                                  double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                                  double* __restrict__ ftay, double* __restrict__ delay_out,
+                                                  double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
+                                                  int write_red, int* __restrict__ status) {
+    const int n2 = off3 - off2, n1 = off2 - off1;
+    const int b = blockIdx.x;
+    if (b < n2)
+        eval_block<WANT_M, 2>(off2 + b, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
+                              Mout, dmxv, compact, write_red, status);
+    else if (b < n2 + n1)
+        eval_block<WANT_M, 1>(off1 + b - n2, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay,
+                              delay_out, Mout, dmxv, compact, write_red, status);
+    else
+        eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
+                              Mout, dmxv, compact, write_red, status);
+}
+
 // ---------------------------------------------------------------------------------
 // k_resid1/k_resid2 — residuals.py:314-425, :483-538, :638-667
 // ---------------------------------------------------------------------------------
@@ -2390,6 +2415,7 @@ struct pint_ctx {
     int* d_rblk_inst = nullptr;   // k_resid1/2 block -> instance
     double* d_rpart = nullptr;    // per residual block: sum w, sum w x, chi2 partial
     int nrblk = 0;
+    int eval_merge = 0;  // bit 0: one k_eval_mix launch without M, bit 1: with M (PINT_EVAL_MERGE)
     int nblk = 0;
     int blk_off[4] = {0, 0, 0, 0};  // block ranges per binary type (0 none, 1 ELL1, 2 DD)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
@@ -2581,6 +2607,7 @@ pint_ctx* pint_ctx_create(int device) {
     if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
     else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
+    ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int sl = 0; sl < 2; sl++) {
@@ -3172,7 +3199,18 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         HIPCHK(hipGetLastError());
         ctx->ic_valid = true;
     }
-    for (int t = 0; t < 3; t++) {  // one launch per binary model, back to back on the stream
+    const bool mix = (ctx->eval_merge >> (want_M ? 1 : 0)) & 1;
+    if (mix && ctx->nblk > 0) {
+#define PINT_EVAL_MIX(WM)                                                                                      \
+        hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \
+                           ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
+                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status)
+        if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
+#undef PINT_EVAL_MIX
+        HIPCHK(hipGetLastError());
+    }
+    for (int t = 0; t < 3 && !mix; t++) {  // one launch per binary model, back to back on the stream
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
         const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
