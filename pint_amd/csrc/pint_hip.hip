@@ -1756,16 +1756,17 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     double* yv = bd + nbd * 16;                       // nbd*16
     double* bx = yv + nbd * 16;                       // nbk*16: b_x (normalised)
     double* Dn = bx + nbk * 16;                       // nbk*16: normalised D
-    double* nd = Dn + nbk * 16;                       // nbd*16: dense column norms
-    double* nx = nd + nbd * 16;                       // nbk*16: DMX column norms
+    double* ind = Dn + nbk * 16;                      // nbd*16: 1 / dense column norms
+    double* inx = ind + nbd * 16;                     // nbk*16: 1 / DMX column norms
+    double* isd = inx + nbk * 16;                     // nbk*16: 1 / sqrt(normalised D)
     const double* Gp = Gpart + I.goff;
     const double* Sdi = Sd + I.sdoff;
     auto Gd = [&](int i, int j) {  // dense compact Gram (upper storage)
         if (i > j) { int t = i; i = j; j = t; }
         return Gp[(long)i * Kp + j];
     };
-    auto nrm_d = [&](int c) { return nd[c]; };  // norms, staged in LDS below
-    auto nrm_x = [&](int a) { return nx[a]; };
+    // reciprocal norms (and D^-1/2), staged in LDS below: the per-element scalings are
+    // multiplications
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
@@ -1777,7 +1778,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             v = sqrt(mode == 0 ? Gd(c, c) : colsq[(I.coff + c) * nsplit]);
             v = v == 0.0 ? 1.0 : v;
         }
-        nd[c] = v;
+        ind[c] = 1.0 / v;
     }
     for (int a = tid; a < nbk * 16; a += NW * 64) {
         double d = 1.0, b = 0.0, na = 1.0;
@@ -1788,8 +1789,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             d = dd_ / (na * na);
             b = Sdi[(long)a * Kp + Kres] / na;
         }
-        nx[a] = na;
+        inx[a] = 1.0 / na;
         Dn[a] = d;
+        isd[a] = 1.0 / sqrt(d);
         bx[a] = b;
     }
     __syncthreads();
@@ -1801,9 +1803,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int gi = Ib * 16 + r, gj = Jb * 16 + c;
         double v;
         if (gi < Kd && gj < Kd) {
-            const double ni = nrm_d(gi), nj = nrm_d(gj);
-            v = Gd(gi, gj) / (ni * nj);
-            if (gi == gj && mode == 1 && gi >= red0) v += 1.0 / Pd.red_phi[gi - red0] / (ni * ni);
+            const double ni = ind[gi], nj = ind[gj];
+            v = Gd(gi, gj) * (ni * nj);
+            if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
         } else {
             v = (gi == gj) ? 1.0 : 0.0;
         }
@@ -1815,10 +1817,10 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int r = e & 15, c = (e >> 4) & 15;
         const int gi = Ib * 16 + r, a = kb * 16 + c;
         double v = 0.0;
-        if (gi < Kd && a < ndc) v = Sdi[(long)a * Kp + gi] / (nrm_d(gi) * nrm_x(a)) / sqrt(Dn[a]);
+        if (gi < Kd && a < ndc) v = Sdi[(long)a * Kp + gi] * (ind[gi] * inx[a]) * isd[a];
         A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = v;
     }
-    for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) / nrm_d(c) : 0.0;
+    for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) * ind[c] : 0.0;
     const double rwr = Gd(Kres, Kres);
     __syncthreads();
     TS(1);
@@ -1837,7 +1839,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         for (int c = g0; c < nbd * 16; c += NW * 16) {
             double sacc = 0.0;
             for (int a = sub; a < ndc; a += 4)
-                sacc += A[ublk(c >> 4, a >> 4, nbk, nblkS) + swz(c & 15, a & 15)] * bx[a] / sqrt(Dn[a]);
+                sacc += A[ublk(c >> 4, a >> 4, nbk, nblkS) + swz(c & 15, a & 15)] * (bx[a] * isd[a]);
             sacc += __shfl_xor(sacc, 1, 64);
             sacc += __shfl_xor(sacc, 2, 64);
             bnew = bd[c] - sacc;
@@ -1886,10 +1888,10 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         se += __shfl_xor(se, 2, 64);
         if (sub == 0) {
             const int o = Pd.dorig[g];
-            const double nd = nrm_d(g);
-            dpars[I.coff + o] = s1 / nd;
-            errs[I.coff + o] = sqrt(se) / nd;
-            bx_dot += Gd(g, Kres) / nd * s1;  // b_d . x_d
+            const double in_ = ind[g];
+            dpars[I.coff + o] = s1 * in_;
+            errs[I.coff + o] = sqrt(se) * in_;
+            bx_dot += Gd(g, Kres) * in_ * s1;  // b_d . x_d
         }
     }
     for (int a = g0; a < ndc; a += NW * 16) {
@@ -1904,11 +1906,11 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sw += __shfl_xor(sw, 1, 64);
         sw += __shfl_xor(sw, 2, 64);
         if (sub == 0) {
-            const double d = Dn[a], na = nrm_x(a);
-            const double xx = bx[a] / d - sz / sqrt(d);
+            const double d = Dn[a], ina = inx[a];
+            const double xx = bx[a] / d - sz * isd[a];
             const int o = Pd.xorig[a];
-            dpars[I.coff + o] = xx / na;
-            errs[I.coff + o] = sqrt(1.0 / d + sw / d) / na;
+            dpars[I.coff + o] = xx * ina;
+            errs[I.coff + o] = sqrt(1.0 / d + sw / d) * ina;
             bx_dot += bx[a] * xx;
         }
     }
@@ -1949,18 +1951,18 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                     if (ri >= red0 || cj >= red0) continue;
                     oi = Pd.dorig[ri];
                     oj = Pd.dorig[cj];
-                    v = acc[q] / (nrm_d(ri) * nrm_d(cj));
+                    v = acc[q] * (ind[ri] * ind[cj]);
                 } else if (kind == 1) {
                     if (ri >= ndc || cj >= ndc) continue;
                     oi = Pd.xorig[ri];
                     oj = Pd.xorig[cj];
-                    v = acc[q] / sqrt(Dn[ri] * Dn[cj]) + (ri == cj ? 1.0 / Dn[ri] : 0.0);
-                    v /= nrm_x(ri) * nrm_x(cj);
+                    v = acc[q] * (isd[ri] * isd[cj]) + (ri == cj ? 1.0 / Dn[ri] : 0.0);
+                    v *= inx[ri] * inx[cj];
                 } else {
                     if (ri >= ndc || cj >= red0) continue;
                     oi = Pd.xorig[ri];
                     oj = Pd.dorig[cj];
-                    v = -acc[q] / sqrt(Dn[ri]) / (nrm_x(ri) * nrm_d(cj));
+                    v = -acc[q] * isd[ri] * (inx[ri] * ind[cj]);
                 }
                 C[(long)oi * ncol + oj] = v;
                 C[(long)oj * ncol + oi] = v;
