@@ -149,12 +149,12 @@ def main():
     N = np.array([l.n for l in lays]).astype(float)
     R = K - P
     vl = [s.vgram_layout(l) for l in lays]
-    # k_gram_v: MFMA tiles [T|r|DMX slots] x [T|r|slots|F] of 16x16 + the two trig tiles,
+    # k_gram_v: MFMA tiles [T|r|DMX slots] x [T|r|slots|F] of 16x16 + the trig tile A^T B,
     # 2048 flops per tile per 4 rows
     tiles = []
     for vg, ns, kpv, r0 in vl:
         ntr, nt = (r0 + 1 + ns) // 16, kpv // 16
-        tiles.append(ntr * nt - ntr * (ntr - 1) // 2 + 2 if vg else 0)
+        tiles.append(ntr * nt - ntr * (ntr - 1) // 2 + 1 if vg else 0)
     tiles = np.array(tiles, dtype=float)
     flops = {
         "k_gram": float(np.sum(tiles * N * 512.0)),           # FP64 MFMA flops executed

@@ -40,6 +40,7 @@ struct PsrDev {
     const double* red_freq;  // nred
     const double* red_phi;   // 2*nred
     const double* red_cs;    // n x 2: (cos, sin) of the red-noise fundamental per TOA (k_redbase)
+    const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trigu)
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
@@ -853,11 +854,11 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
     // Kpv == 16 NTC and f0 == 16 NTR (the launch groups instances by both)
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
-    // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), A2 = the same times
-    // sigma (unweighted after the whitening), B = [cos 8b theta | sin 8b theta]/sigma (b < 8):
-    // the tiles A^T B and A2^T B hold every C_m, S_m (weighted) and U_m, V_m (unweighted),
-    // m = a + 8b < 64 -- F^T W F and the Fourier column norms (k_greduce)
-    const int tA = Kpv, tA2 = Kpv + 16, tB = Kpv + 32, Kpt = Kpv + 48;
+    // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), B = [cos 8b theta |
+    // sin 8b theta]/sigma (b < 8): the tile A^T B holds every C_m, S_m (weighted), m = a + 8b
+    // < 64 -- F^T W F (k_greduce).  The unweighted sums for the Fourier column norms depend
+    // on the TOAs only (PsrDev::trigU, formed at upload).
+    const int tA = Kpv, tB = Kpv + 16, Kpt = Kpv + 32;
     double* Ts = lds;       // [Kpt][CS] whitened rows
     long i0, i1;
     split_rows(n, nsplit, split, i0, i1);
@@ -867,7 +868,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     static_assert(VW == 4, "the trig blocks give each wave two harmonics of A and of B");
-    double4_t acc[NT], accW = {0, 0, 0, 0}, accU = {0, 0, 0, 0};
+    double4_t acc[NT], accW = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
     for (int k = tid; k < Kpt * CS; k += NTH) Ts[k] = 0.0;  // slot and padding columns stay 0
@@ -917,7 +918,6 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
                 }
             }
             if (nred > 0) {  // trig blocks: harmonics a = 2 wave, 2 wave + 1 and 8a of them
-                const double us = ok_n ? sg_n : 0.0;  // A2 = A * sigma^2, whitened: A * sigma
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const int a = 2 * wave + u;
@@ -925,8 +925,6 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
                     cpow(c1_n, s1_n, a, c, sn);
                     Ts[(tA + a) * CS + lane] = c * iw;
                     Ts[(tA + 8 + a) * CS + lane] = sn * iw;
-                    Ts[(tA2 + a) * CS + lane] = c * us;
-                    Ts[(tA2 + 8 + a) * CS + lane] = sn * us;
                     cpow(c1_n, s1_n, 8 * a, c, sn);
                     Ts[(tB + a) * CS + lane] = c * iw;
                     Ts[(tB + 8 + a) * CS + lane] = sn * iw;
@@ -967,11 +965,9 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
                 for (int tj = ti; tj < NTC; tj++, k++)
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
             }
-            if (nred > 0) {
-                const double bB = Tr[tB * CS];
-                accW = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], bB, accW, 0, 0, 0);
-                accU = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA2 * CS], bB, accU, 0, 0, 0);
-            }
+            // trig tile, unconditional (zero in LDS without red noise): no branch, and its
+            // operand reads share the step's LDS wait
+            accW = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], Tr[tB * CS], accW, 0, 0, 0);
         }
     }
     // timing-column sums of squares of this split (normalize_designmatrix)
@@ -1029,30 +1025,26 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
             }
         }
     }
-    if (nred > 0) {  // trig tiles: sum over the waves, then C, S, U, V of m = a + 8b
+    if (nred > 0) {  // trig tile: sum over the waves, then C, S of m = a + 8b
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            red[((wave * 2 + 0) * 4 + q) * 64 + lane] = accW[q];
-            red[((wave * 2 + 1) * 4 + q) * 64 + lane] = accU[q];
-        }
+        for (int q = 0; q < 4; q++) red[(wave * 4 + q) * 64 + lane] = accW[q];
         __syncthreads();
-        double* tsum = red + VW * 2 * 256;  // [2][256]
-        for (int e = tid; e < 512; e += NTH) {
+        double* tsum = red + VW * 256;  // [256]
+        for (int e = tid; e < 256; e += NTH) {
             double v = 0.0;
 #pragma unroll
-            for (int w = 0; w < VW; w++) v += red[w * 512 + e];
+            for (int w = 0; w < VW; w++) v += red[w * 256 + e];
             tsum[e] = v;
         }
         __syncthreads();
         // tile element (i, j) at ((i >> 2) * 64 + (i & 3) * 16 + j) (f64 MFMA C/D layout)
         auto tix = [](int i, int j) { return ((i >> 2) << 6) + ((i & 3) << 4) + j; };
         double* out = TSp + ((long)I.self * nsplit + split) * (4 * VTRIG);
-        for (int e = tid; e < 2 * VTRIG; e += NTH) {
-            const int kind = e >> 6, m = e & 63, a = m & 7, b = m >> 3;
-            const double* T_ = tsum + kind * 256;
-            out[2 * VTRIG * kind + m] = T_[tix(a, b)] - T_[tix(8 + a, 8 + b)];          // C_m / U_m
-            out[2 * VTRIG * kind + VTRIG + m] = T_[tix(8 + a, b)] + T_[tix(a, 8 + b)];  // S_m / V_m
+        for (int m = tid; m < VTRIG; m += NTH) {
+            const int a = m & 7, b = m >> 3;
+            out[m] = tsum[tix(a, b)] - tsum[tix(8 + a, 8 + b)];          // C_m
+            out[VTRIG + m] = tsum[tix(8 + a, b)] + tsum[tix(a, 8 + b)];  // S_m
         }
     }
 }
@@ -1070,6 +1062,29 @@ __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __res
     cs[2 * i + 1] = s;
 }
 
+// k_trigu: the unweighted trig sums U_m, V_m (m < 64) over the pulsar's TOAs, from which
+// k_greduce forms the Fourier column norms (sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2).
+// They depend on the TOAs only, so they are formed once at upload: grid = row blocks of
+// TRIGU_R rows, thread m (cos) / 64 + m (sin) per block, partials summed in block order by
+// k_trigu_sum.
+constexpr int TRIGU_R = 1024;
+__global__ __launch_bounds__(128) void k_trigu(const double* __restrict__ cs, int n, double* __restrict__ part) {
+    const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
+    const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);
+    double acc = 0.0;
+    for (int i = i0; i < i1; i++) {
+        double c, sn;
+        cpow(cs[2 * i], cs[2 * i + 1], m, c, sn);
+        acc += kind ? sn : c;
+    }
+    part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(128) void k_trigu_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
+    double acc = 0.0;
+    for (int b = 0; b < nb; b++) acc += part[(long)b * 128 + threadIdx.x];
+    out[threadIdx.x] = acc;
+}
+
 // k_tsum: k_gram_v's per-split trig-sum partials of an instance summed in a fixed order
 __global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               int nsplit, const double* __restrict__ TSp, double* __restrict__ TS) {
@@ -1077,6 +1092,10 @@ __global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, c
     const PsrDev& Pd = psrs[I.psr];
     if (!Pd.vg) return;
     const int m = threadIdx.x, nb = nsplit;
+    if (m >= 2 * VTRIG) {  // unweighted sums: TOA-only, formed at upload (k_trigu)
+        TS[(long)I.self * 4 * VTRIG + m] = Pd.trigU[m - 2 * VTRIG];
+        return;
+    }
     const double* p = TSp + (long)I.self * nsplit * (4 * VTRIG) + m;
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
     int x = 0;
@@ -2734,7 +2753,17 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         hipLaunchKernelGGL(k_redbase, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, d.tdb_hi, d.tdb_lo, n,
                            red_freq[0], (double*)d.red_cs);
         HIPCHK(hipGetLastError());
+    }
+    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
+    if (!rc && spec->nred > 0) {
+        const int nb = (n + TRIGU_R - 1) / TRIGU_R;
+        double* part = nullptr;
+        HIPCHK(hipMalloc((void**)&part, sizeof(double) * 128 * std::max(1, nb)));
+        hipLaunchKernelGGL(k_trigu, dim3(nb), dim3(128), 0, ctx->stream, d.red_cs, n, part);
+        hipLaunchKernelGGL(k_trigu_sum, dim3(1), dim3(128), 0, ctx->stream, part, nb, (double*)d.trigU);
+        HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipFree(part));
     }
     {
         // compact fit layout: DMX columns out of M when there are enough of them and no TOA
@@ -3350,8 +3379,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipEvent_t e0 = (ext_t && gi == 0) ? ctx->ev[12] : nullptr;
             hipEvent_t e1 = (ext_t && gi + 1 == ctx->kp_groups_v.size()) ? ctx->ev[13] : nullptr;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * std::max<size_t>((size_t)(kg.maxKp + 48) * (VCH + 2),
-                                                                 std::max(VW * VTG * 256, VW * 512 + 512));
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)(kg.maxKp + 32) * (VCH + 2),
+                                                                 std::max(VW * VTG * 256, VW * 256 + 256));
 #define PINT_GRAMV(R_, C_)                                                                                       \
             hipExtLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), (uint32_t)lds, ctx->stream, e0, e1, 0u,  \
                                   (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M, (const double*)ctx->d_rt, \
