@@ -2344,13 +2344,23 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     const bool nobasis = (R == 0 && nep == 0);
     const double x00 = 1.0 / sqrt(1e-40 + Pd.sumw);
     const double* X = sigL + I.soff;
+    // the packed factor staged in LDS with coalesced loads, then four lanes per row
+    double* Xs = d + Kn;  // Kn (Kn + 1) / 2
+    const int nX = nobasis ? 0 : Kn * (Kn + 1) / 2;
+    for (int e = threadIdx.x; e < nX; e += blockDim.x) Xs[e] = X[e];
+    __syncthreads();
     double q = 0.0;
-    for (int i = threadIdx.x; i < Kn; i += blockDim.x) {
+    for (int i0 = 0; i0 < Kn; i0 += blockDim.x / 4) {
+        const int i = i0 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
         double s = 0.0;
-        if (nobasis) s = x00 * d[0];
-        else
-            for (int j = 0; j <= i; j++) s += X[tri(i, j)] * d[j];
-        q += s * s;
+        if (i < Kn) {
+            if (nobasis) s = sub == 0 ? x00 * d[0] : 0.0;
+            else
+                for (int j = sub; j <= i; j += 4) s += Xs[tri(i, j)] * d[j];
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if (sub == 0 && i < Kn) q += s * s;
     }
     q = block_sum<4>(q, sh);
     // log-normalisation of the likelihood, logdet(C)/2 (residuals.py:567-589 via
@@ -2360,7 +2370,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     double ld = 0.0;
     for (int e = threadIdx.x; e < nep; e += blockDim.x) ld += log(Pd.ep_phi[e]) + log(eD[I.epoff + e]);
     for (int k = threadIdx.x; k < R; k += blockDim.x) ld += log(Pd.red_phi[k]);
-    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(nobasis ? x00 : X[tri(j, j)]);
+    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(nobasis ? x00 : Xs[tri(j, j)]);
     ld = block_sum<4>(ld, sh);
     if (threadIdx.x == 0) {
         chi2[inst] = (rwr - erwr) - q;
@@ -3649,7 +3659,8 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
                        ctx->d_rt, nsw, stride, ctx->m_compact, ctx->d_wpart);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * (R + 1), ctx->stream, ctx->d_psrs,
+    hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * ((R + 1) + (R + 1) * (R + 2) / 2),
+                       ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
                        stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm);
     HIPCHK(hipGetLastError());
