@@ -3078,25 +3078,31 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         std::vector<InstDev> sorted;
         std::vector<KpGroup>& groups = lay == 0 ? ctx->kp_groups : (lay == 1 ? ctx->kp_groups_c : ctx->kp_groups_v);
         groups.clear();
-        for (int T = 1; T <= (lay == 2 ? 29 : GMAXT_ALL); T++) {
-            KpGroup g{T, (int)sorted.size(), 0, 16};
-            for (auto& I : ctx->inst) {
-                const PsrDev& pd = ctx->psrs[I.psr].dev;
-                if (lay == 1 && pd.dsplit && pd.vg) continue;
-                if (lay == 2 && !(pd.dsplit && pd.vg)) continue;
-                const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
-                const int nt = kp / 16;
-                int tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
-                if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column tiles (ntr..9)
-                    const int ntr = (pd.red0c + 1 + pd.vns) / 16;
-                    tT = 10 * (ntr - 1) + nt;
-                }
-                if (tT != T) continue;
-                sorted.push_back(I);
-                g.count++;
-                if (kp > g.maxKp) g.maxKp = kp;
+        // bucket the instances by launch key in one pass (a grid batch has ~10^5 instances)
+        const int maxT = lay == 2 ? 29 : GMAXT_ALL;
+        std::vector<std::vector<int>> bucket(maxT + 1);
+        std::vector<int> bkp(maxT + 1, 16);
+        for (int k = 0; k < ninst; k++) {
+            const InstDev& I = ctx->inst[k];
+            const PsrDev& pd = ctx->psrs[I.psr].dev;
+            if (lay == 1 && pd.dsplit && pd.vg) continue;
+            if (lay == 2 && !(pd.dsplit && pd.vg)) continue;
+            const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
+            const int nt = kp / 16;
+            int tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
+            if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column tiles (ntr..9)
+                const int ntr = (pd.red0c + 1 + pd.vns) / 16;
+                tT = 10 * (ntr - 1) + nt;
             }
-            if (g.count) groups.push_back(g);
+            if (tT < 1 || tT > maxT) continue;
+            bucket[tT].push_back(k);
+            if (kp > bkp[tT]) bkp[tT] = kp;
+        }
+        for (int T = 1; T <= maxT; T++) {
+            if (bucket[T].empty()) continue;
+            KpGroup g{T, (int)sorted.size(), (int)bucket[T].size(), bkp[T]};
+            for (int k : bucket[T]) sorted.push_back(ctx->inst[k]);
+            groups.push_back(g);
         }
         InstDev*& dst = lay == 0 ? ctx->d_inst_sorted : (lay == 1 ? ctx->d_inst_sorted_c : ctx->d_inst_sorted_v);
         HIPCHK(cmalloc((void**)&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));

@@ -213,8 +213,12 @@ class BatchFit:
         return self._finish(results)
 
     def _finish_arrays(self, chi2, converged, exc):
-        self.final_tables = self.s.read_tables_flat()
+        # the final parameter tables stay on the device until asked for (final_tables_flat)
         return BatchOutcome(chi2, converged, exc)
+
+    def final_tables_flat(self):
+        """The instances' parameter tables after the fit, concatenated (device -> host)."""
+        return self.s.read_tables_flat()
 
     # -- downhill (fitter.py:999-1105) ---------------------------------------------------
     def fit_downhill(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,

@@ -66,6 +66,41 @@ def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
     return torch.cat([g.cpu() for g in gl]).numpy()[:npts]
 
 
+# The last grid's Session and uploaded pulsar stay resident (like the TOAs of a serving
+# process): another grid over the same TOAs and model structure reuses the upload.  The
+# key holds everything the layout depends on -- the TOA object, and every parameter's
+# name, value and frozen flag (noise parameters set the basis weights) -- so any change
+# re-uploads.
+_GRID = {}
+
+
+def _model_key(model):
+    return tuple((n, str(model[n].value), bool(model[n].frozen)) for n in model.params)
+
+
+def _grid_session(base, toas, gls):
+    from .engine import Session, build_layout
+    key = (id(toas), toas.ntoas, gls, _model_key(base))
+    cur = _GRID.get("cur")
+    if cur is not None and cur[0] == key and cur[3] is toas:
+        return cur[1], cur[2]
+    _drop_grid_session()
+    s = Session()
+    try:
+        lay = s.add(build_layout(base, toas, use_gls_basis=gls))
+    except Exception:
+        s.close()
+        raise
+    _GRID["cur"] = (key, s, lay, toas)
+    return s, lay
+
+
+def _drop_grid_session():
+    cur = _GRID.pop("cur", None)
+    if cur is not None:
+        cur[1].close()
+
+
 def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
                executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
     """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
@@ -86,9 +121,8 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     chi2 = np.full(hi - lo, np.nan)
     extra = {e: np.full(hi - lo, np.nan) for e in extraparnames}
     if hi > lo:
-        s = Session()
+        s, lay = _grid_session(base, ftr.toas, mode == "gls")
         try:
-            lay = s.add(build_layout(base, ftr.toas, use_gls_basis=(mode == "gls")))
             t0 = pack_table(lay, base)
             # points per batch: ~24 GB of per-instance device buffers (eval rows, design matrix,
             # Gram partials) per batch keeps any grid within HBM
@@ -115,12 +149,13 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
                     res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1), outputs=False)
                     chi2[c0 - lo:c1 - lo] = res.chi2
                 if extraparnames:
-                    ft = bf.final_tables.reshape(c1 - c0, lay.tstride)
+                    ft = bf.final_tables_flat().reshape(c1 - c0, lay.tstride)
                     for e in extraparnames:
                         o = lay.offsets[e]
                         extra[e][c0 - lo:c1 - lo] = (ft[:, o].astype(np.longdouble)
                                                      + ft[:, o + 1].astype(np.longdouble)).astype(np.float64)
-        finally:
-            s.close()
+        except Exception:
+            _drop_grid_session()
+            raise
     chi2_all = gather_blocks(chi2, per, npts, dist)
     return chi2_all.reshape(shape), {e: extra[e] for e in extraparnames}
