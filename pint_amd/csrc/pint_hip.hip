@@ -879,7 +879,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     const int hper = (nred + VW - 1) / VW;
     const int hb = wave * hper, he = std::min(nred, (wave + 1) * hper);
     int slot_prev = -1;  // wave 0: the LDS slot column of this lane's previous row
-    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, sg_n = 1.0;
+    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
     double st[QL];
     int d_n = -1;
     bool ok_n = false;
@@ -894,7 +894,6 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
             d_n = Pd.drow[row];
         }
         if (nred > 0) {
-            sg_n = Pd.sigma[row];
             c1_n = Pd.red_cs[2 * row];
             s1_n = Pd.red_cs[2 * row + 1];
         }
@@ -1066,8 +1065,8 @@ __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __res
 // k_greduce forms the Fourier column norms (sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2).
 // They depend on the TOAs only, so they are formed once at upload: grid = row blocks of
 // TRIGU_R rows, thread m (cos) / 64 + m (sin) per block, partials summed in block order by
-// k_trigu_sum.
-constexpr int TRIGU_R = 1024;
+// k_trigu_sum (one thread per sum: short row blocks keep its serial chain short).
+constexpr int TRIGU_R = 64;
 __global__ __launch_bounds__(128) void k_trigu(const double* __restrict__ cs, int n, double* __restrict__ part) {
     const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
     const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);

@@ -19,9 +19,12 @@ def load(path, counter):
             continue
         name = r["Kernel_Name"]
         m = re.match(r"void k_eval<(\d), (\d)>", name)
+        mm = re.match(r"void k_eval_mix<(\d)>", name)
         if m:
             key = "k_eval_M" if m.group(1) == "1" else "k_eval"
             key += f"<{m.group(2)}>"
+        elif mm:
+            key = "k_eval_M" if mm.group(1) == "1" else "k_eval"
         else:
             key = re.sub(r"<.*", "", name.split("(")[0].replace("void ", "").strip())
         per[key].append(float(r["Counter_Value"]) * 1024.0)
