@@ -248,6 +248,30 @@ void pint_host_free(void *p);
 /* Introspection for tests: 0 Gram partials, 1 column sums of squares, 2 Woodbury factor
  * (L^-1, packed lower). */
 int pint_debug_read(pint_ctx *ctx, int which, double *out);
+/* Stage-wise parity introspection (SURVEY.md 8(a) parity definition 2; no reference
+ * counterpart -- these expose the intermediate arrays of fitter.py:2164-2202):
+ * pint_debug_gram writes, per instance, the assembled unnormalised normal matrix
+ * [M | r]^T N^-1 [M | r] of the last pint_fit_step ((K_i+1)^2, original column order,
+ * residual last, ECORR block eliminated) followed by M's K_i unweighted column sums of
+ * squares (utils.py:2879 normalize_designmatrix).  pint_debug_set_resids replaces every
+ * instance's time residuals (n_i each) by the caller's, so that pint_fit_step and
+ * pint_chi2_gls run on e.g. the reference's own residual arrays. */
+int pint_debug_gram(pint_ctx *ctx, double *out);
+int pint_debug_set_resids(pint_ctx *ctx, const double *time_resid);
+
+/* Per-instance status bits (1 << PINT_E_*) raised by evaluations since the last call, one
+ * int32 per instance; reading clears them.  The batch status returned by pint_eval/
+ * pint_check names the first error of any instance; this names the instances, so one
+ * invalid grid point or trial state fails alone (fitter.py:926-935 InvalidModelParameters,
+ * gridutils.py:89-106 NaN per point). */
+int pint_inst_status(pint_ctx *ctx, int32_t *out);
+
+/* Noise realisations of the last pint_fit_step(mode=1), n_i per instance (either pointer
+ * may be NULL): red = F a (PLRedNoise basis times its fitted coefficients), ecorr = the
+ * ECORR epoch coefficients back-substituted from the eliminated block, per TOA.  Replaces
+ * Residuals.noise_resids as GLSFitter.fit_toas (fitter.py:2270-2282) and
+ * DownhillGLSFitter.fit_toas (:1582-1605) set it. */
+int pint_noise_resids(pint_ctx *ctx, double *red, double *ecorr);
 
 /* Device time (ms, HIP events on the streams the kernels run on) of the last launches, 8
  * values: [0] eval (no design matrix), [1] resid, [2] ecorr + Gram + partial reduction,

@@ -95,6 +95,10 @@ def lib():
     L.pint_check.argtypes = [vp]
     L.pint_step_end.argtypes = [vp, C.POINTER(C.c_int)]
     L.pint_check_step.argtypes = [vp, C.c_int]
+    L.pint_inst_status.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.pint_noise_resids.argtypes = [vp, dptr, dptr]
+    L.pint_debug_gram.argtypes = [vp, dptr]
+    L.pint_debug_set_resids.argtypes = [vp, dptr]
     _lib = L
     return L
 
@@ -105,7 +109,8 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",
             "pint_set_option", "pint_host_alloc", "pint_host_free",
             "pint_fit_layout", "pint_query", "pint_capture_begin", "pint_capture_end", "pint_graph_launch",
-            "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step"]
+            "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step",
+            "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -209,7 +209,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
                                            double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                            double* __restrict__ ftay, double* __restrict__ delay_out,
                                            double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                           int write_red, int* __restrict__ status) {
+                                           int write_red, int* __restrict__ status, int* __restrict__ istatus) {
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -237,7 +237,10 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     const bool cmp = WANT_M && compact && Pd.dsplit;
     eval_toa<BIN>(S, P, ic[ii], t, o, rowM ? Mb : nullptr, r, n, Pd.runs, Pd.nrun, cmp);
     if (rowM && cmp) dmxv[I.ooff + r] = o.dmc;
-    if (o.status) atomicOr(status, 1 << o.status);
+    if (o.status) {  // the batch's status word and this instance's own (pint_inst_status)
+        atomicOr(status, 1 << o.status);
+        atomicOr(istatus + ii, 1 << o.status);
+    }
     ph_hi[I.roff + r] = o.phase.hi;
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
@@ -269,9 +272,9 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                               double* __restrict__ ftay, double* __restrict__ delay_out,
                                               double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                              int write_red, int* __restrict__ status) {
+                                              int write_red, int* __restrict__ status, int* __restrict__ istatus) {
     eval_block<WANT_M, BIN>(blockIdx.x, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                            Mout, dmxv, compact, write_red, status);
+                            Mout, dmxv, compact, write_red, status, istatus);
 }
 
 // k_eval_mix: all binary models in one launch (heaviest first: DD, ELL1, isolated blocks),
@@ -285,18 +288,18 @@ __global__ __launch_bounds__(256) void k_eval_mix(const PsrDev* __restrict__ psr
                                                   double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                                   double* __restrict__ ftay, double* __restrict__ delay_out,
                                                   double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                                  int write_red, int* __restrict__ status) {
+                                                  int write_red, int* __restrict__ status, int* __restrict__ istatus) {
     const int n2 = off3 - off2, n1 = off2 - off1;
     const int b = blockIdx.x;
     if (b < n2)
         eval_block<WANT_M, 2>(off2 + b, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status);
+                              Mout, dmxv, compact, write_red, status, istatus);
     else if (b < n2 + n1)
         eval_block<WANT_M, 1>(off1 + b - n2, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay,
-                              delay_out, Mout, dmxv, compact, write_red, status);
+                              delay_out, Mout, dmxv, compact, write_red, status, istatus);
     else
         eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status);
+                              Mout, dmxv, compact, write_red, status, istatus);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2389,12 +2392,84 @@ __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restri
     for (int c = threadIdx.x; c < S.ncol; c += blockDim.x) {
         int o = S.col_toff[c];
         if (o < 0) continue;
+        if (lam[inst] == 0.0) continue;  // decided instances: a non-finite step must not touch them
         dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam[inst] * dpars[I.coff + c]);
         P[o] = v.hi;
         P[o + 1] = v.lo;
     }
     __syncthreads();
     prep_one(psrs[I.psr].spec, P, S.tstride, ic + inst);
+}
+
+// ---------------------------------------------------------------------------------
+// Noise realisations of the last fit step (fitter.py:2270-2282 GLSFitter, :1582-1605
+// DownhillGLSFitter: noise_resids[comp] = M[:, comp] @ xhat[comp] with M, xhat normalised,
+// i.e. F @ dpars in par units).
+//   k_noise_red    PLRedNoise: sum_k a_k sin(2 pi t f_k) + b_k cos(2 pi t f_k) per TOA, the
+//                  argument reduced in double-double as k_eval forms the basis
+//   k_noise_ecorr  ECORR: the eliminated epoch coefficients, back-substituted from the Schur
+//                  system, c_e = (s_e[r] - s_e . x) / D_e  (s_e = sum_{i in e} w_i [M | r]_i,
+//                  D_e = W_e + 1/phi_e from k_ecorr), written to every TOA of epoch e
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ dpars, double* __restrict__ out) {
+    const int inst = blockIdx.y;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= I.n) return;
+    const double* a = dpars + I.coff + S.ncol;
+    double v = 0.0;
+    if (S.nred > 0) {
+        const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
+        for (int k = 0; k < S.nred; k++) {
+            const dd x = dd_mul_d(ts, Pd.red_freq[k]);
+            const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
+            double sn, cs;
+            sincos(TWO_PI * fr, &sn, &cs);
+            v += a[2 * k] * sn + a[2 * k + 1] * cs;
+        }
+    }
+    out[I.roff - inst + i] = v;
+}
+
+__global__ __launch_bounds__(64) void k_noise_ecorr(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ dpars, const double* __restrict__ esum,
+                                                    const double* __restrict__ eD, double* __restrict__ out) {
+    const int inst = blockIdx.y, e = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    if (e >= Pd.nep) return;
+    const int K = I.K;
+    const double* se = esum + I.eoff + (long)e * I.Kp;
+    const double* x = dpars + I.coff;
+    double t = 0.0;
+    for (int c = threadIdx.x; c < K; c += 64) t += se[c] * x[c];
+    t = wave_sum(t);
+    const double ce = (se[K] - t) / eD[I.epoff + e];
+    double* o = out + (I.roff - inst);
+    for (int k = Pd.ep_ptr[e] + threadIdx.x; k < Pd.ep_ptr[e + 1]; k += 64) o[Pd.ep_idx[k]] = ce;
+}
+
+// Debug/parity introspection (pint_debug_gram): the assembled, unnormalised normal matrix
+// [M | r]^T N^-1 [M | r] of the last pint_fit_step in the original column order (the ECORR
+// block already eliminated by its Schur complement), (K+1)^2 per instance, followed by the K
+// unweighted column sums of squares of M (normalize_designmatrix).
+__global__ __launch_bounds__(256) void k_debug_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ Gpart, const double* __restrict__ colsq,
+                                                    int nsplit, int compact, const double* __restrict__ Sd,
+                                                    const double* __restrict__ DD, const double* __restrict__ DCS,
+                                                    const long* __restrict__ ooff, double* __restrict__ out) {
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const bool cmp = compact && Pd.dsplit;
+    const GramView g = gram_view(Pd, I, Gpart, cmp, Sd, DD);
+    const int W = I.K + 1;
+    double* o = out + ooff[inst];
+    for (long e = threadIdx.x; e < (long)W * W; e += blockDim.x) o[e] = g((int)(e / W), (int)(e % W));
+    for (int j = threadIdx.x; j < I.K; j += blockDim.x) o[(long)W * W + j] = colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2471,6 +2546,7 @@ struct pint_ctx {
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
     int* d_status = nullptr;
+    int* d_istatus = nullptr;  // per-instance status bits since the last pint_inst_status read
     int maxK = 0;
     // HIP event pairs: 0/1 eval, 2/3 eval with design matrix, 4/5 resid, 6/7 ecorr + Gram +
     // reduction, 7/8 solve, 10/11 Woodbury chi2, 12/13 the Gram kernels alone, 14/15 k_greduce
@@ -2662,7 +2738,7 @@ static void free_instances(pint_ctx* ctx) {
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
-                   (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2,
+                   (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2, (void**)&ctx->d_istatus,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_eigw,
@@ -3138,6 +3214,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_rt, sizeof(double) * out));
     HIPCHK(cmalloc((void**)&ctx->d_rp, sizeof(double) * out));
     HIPCHK(cmalloc((void**)&ctx->d_chi2, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_istatus, sizeof(int) * ninst));
+    HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ninst, ctx->stream));
     HIPCHK(cmalloc((void**)&ctx->d_chi2g, sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_lognorm, sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_chi2lin, sizeof(double) * ninst));
@@ -3251,7 +3329,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status)
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus)
         if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
 #undef PINT_EVAL_MIX
         HIPCHK(hipGetLastError());
@@ -3264,7 +3342,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status)
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus)
         if (want_M) {
             if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
         } else {
@@ -3845,6 +3923,88 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
     HIPCHK(hipMemcpyAsync(out, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return ctx->nsplit;
+}
+
+// Per-instance status bits (1 << PINT_E_*) raised by the evaluations since the last call,
+// one int per instance of the batch; reading clears them.  The batch status word still
+// reports the first error of any instance; this tells the host which instances raised it
+// (fitter.py:926-935 InvalidModelParameters is per fit, gridutils.py:89-106 NaN per point).
+int pint_inst_status(pint_ctx* ctx, int32_t* out) {
+    if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHK(hipMemcpyAsync(out, ctx->d_istatus, sizeof(int) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ctx->ninst, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+// Noise realisations of the last pint_fit_step(mode=1): red[n_i], ecorr[n_i] per instance
+// (either pointer may be NULL).
+int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    double* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(double) * std::max<long>(1, ctx->tot_out)));
+    int maxn = 1;
+    for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
+    int rc = PINT_OK;
+    if (red) {
+        hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_dpars, d);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(red, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            rc = PINT_E_HIP;
+    }
+    if (ecorr && rc == PINT_OK) {
+        hipMemsetAsync(d, 0, sizeof(double) * ctx->tot_out, ctx->stream);
+        if (ctx->max_nep > 0)
+            hipLaunchKernelGGL(k_noise_ecorr, dim3(ctx->max_nep, ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, d);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(ecorr, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            rc = PINT_E_HIP;
+    }
+    hipStreamSynchronize(ctx->stream);
+    hipFree(d);
+    if (rc) ctx->err = "pint_noise_resids: HIP error";
+    return rc;
+}
+
+// Parity introspection: the assembled normal matrix of the last pint_fit_step (see
+// k_debug_gram); out holds (K_i+1)^2 + K_i doubles per instance, concatenated.
+int pint_debug_gram(pint_ctx* ctx, double* out) {
+    if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    std::vector<long> off(ctx->ninst + 1, 0);
+    for (int k = 0; k < ctx->ninst; k++) {
+        const long W = ctx->inst[k].K + 1;
+        off[k + 1] = off[k] + W * W + ctx->inst[k].K;
+    }
+    double* d = nullptr;
+    long* doff = nullptr;
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
+    HIPCHK(hipMalloc(&d, sizeof(double) * off[ctx->ninst]));
+    HIPCHK(hipMalloc(&doff, sizeof(long) * ctx->ninst));
+    HIPCHK(hipMemcpy(doff, off.data(), sizeof(long) * ctx->ninst, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
+                       ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, doff, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, d, sizeof(double) * off[ctx->ninst], hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    hipFree(d);
+    hipFree(doff);
+    return PINT_OK;
+}
+
+// Parity introspection: replace the time residuals of every instance (n_i each) by the
+// caller's, e.g. the reference's own residual arrays, so that pint_fit_step / pint_chi2_gls
+// run on them (SURVEY.md 8(a) stage-wise parity).
+int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
+    if (!ctx || ctx->ninst <= 0 || !time_resid) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
 }
 
 int pint_sync(pint_ctx* ctx) {

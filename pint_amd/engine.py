@@ -621,6 +621,49 @@ class Session:
         self.L.pint_last_timing(self.ctx, L.ptr(ms))
         return ms
 
+    def inst_status(self):
+        """Per-instance status bits (1 << PINT_E_*) raised since the last read (cleared)."""
+        out = np.zeros(len(self.inst_layout), dtype=np.int32)
+        self._check(self.L.pint_inst_status(self.ctx, L.ptr(out, C.c_int32)))
+        return out
+
+    def noise_resids(self):
+        """Noise realisations of the last GLS fit_step: per instance {component: n-array}
+        with the reference's component names (fitter.py:2270-2282, noise_model_dimensions)."""
+        n = [l.n for l in self.inst_layout]
+        red = np.empty(sum(n))
+        ec = np.empty(sum(n))
+        self._check(self.L.pint_noise_resids(self.ctx, L.ptr(red), L.ptr(ec)))
+        out = []
+        for lay, r, e in zip(self.inst_layout, self._split(red, n), self._split(ec, n)):
+            d = {}
+            if "EcorrNoise" in lay.model.components:
+                d["ecorr_noise"] = e.copy()
+            if lay.nred > 0:
+                d["pl_red_noise"] = r.copy()
+            out.append(d)
+        return out
+
+    def debug_gram(self):
+        """Stage-wise parity introspection: per instance (G, colsq) of the last fit_step, G the
+        unnormalised (K+1)^2 normal matrix [M | r]^T N^-1 [M | r] (ECORR eliminated), colsq
+        M's unweighted column sums of squares."""
+        sizes = [(l.K + 1) ** 2 + l.K for l in self.inst_layout]
+        buf = np.empty(sum(sizes))
+        self._check(self.L.pint_debug_gram(self.ctx, L.ptr(buf)))
+        out = []
+        for lay, b in zip(self.inst_layout, self._split(buf, sizes)):
+            w = lay.K + 1
+            out.append((b[:w * w].reshape(w, w).copy(), b[w * w:].copy()))
+        return out
+
+    def debug_set_resids(self, resids):
+        """Replace every instance's time residuals (list of n-arrays, seconds)."""
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(r, dtype=np.float64) for r in resids]))
+        if flat.size != sum(l.n for l in self.inst_layout):
+            raise ValueError("residual arrays do not match the batch's TOA counts")
+        self._check(self.L.pint_debug_set_resids(self.ctx, L.ptr(flat)))
+
 
 def release_cache():
     """Hand the device-buffer cache back to the HIP runtime (pint_release_cache)."""

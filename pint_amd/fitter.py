@@ -64,6 +64,7 @@ class FitResult:
         self.converged = False
         self.status = "ok"
         self.noise_coeffs = None
+        self.noise_resids = {}
 
 
 class BatchOutcome:
@@ -76,15 +77,33 @@ class BatchOutcome:
         self.maxiter_reached = ~converged & ~exc
 
 
+def model_key(model):
+    """Everything a pulsar upload (build_layout) depends on besides the TOAs: every
+    parameter's name, value and frozen flag (noise values set sigma and the basis weights,
+    the frozen set the columns) and the component set."""
+    return (tuple((n, str(model[n].value), bool(model[n].frozen)) for n in model.params),
+            tuple(model.components), model.binary)
+
+
 class BatchFit:
     """Run the same fitter on many (model, toas) instances at once.
 
     mode: 'wls' | 'gls'; downhill: reference DownhillFitter control flow per instance.
     Each instance's model is updated in place at the end (like fitter.model).
+
+    Instances are independent: an instance whose evaluation raises an invalid-parameter
+    status (ECC outside [0, 1), a Kepler solve that does not converge, ...) fails alone.  At
+    a state the fit has to stand on (the initial model, or the result of a plain step) it is
+    taken out of the device batch and reported as failed (chi2 NaN, status
+    "InvalidModelParameters"; fitter.py:926-935 raises InvalidModelParameters for that fit
+    only, gridutils.py:89-106 returns NaN for that point); at a downhill trial state it
+    counts as a rejected trial, so that instance halves its lambda (fitter.py:1040-1057).
     """
 
+    EVAL_ERRORS = (L.PINT_E_KEPLER, L.PINT_E_PARAM)
+
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
-                 layouts=None, tables=None, threshold=None, degeneracy_style=None):
+                 layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
         are bare parameter tables of already-uploaded pulsars, e.g. grid points).
 
@@ -103,23 +122,63 @@ class BatchFit:
             layouts = []
             cache = {}
             for model, toas in self.items:
-                key = (id(toas), tuple(model.free_params), model.name)
+                key = (id(toas), model_key(model))
                 if key in cache:
                     layouts.append(cache[key])
                     continue
-                lay = self.s.add(build_layout(model, toas, use_gls_basis=self.gls))
+                lay = self.s.add(build_layout(model, toas, track_mode=track_mode, use_gls_basis=self.gls))
                 cache[key] = lay
                 layouts.append(lay)
-        self.layouts = layouts
         if tables is None:
-            tables = [pack_table(l, m) for l, (m, _) in zip(self.layouts, self.items)]
-        self.tables = tables
-        if isinstance(tables, np.ndarray) and tables.ndim == 2 and all(l is layouts[0] for l in layouts):
-            self.s.set_instances_of(layouts[0], tables)  # grid points of one pulsar
+            tables = [pack_table(l, m) for l, (m, _) in zip(layouts, self.items)]
+        self.n0 = len(layouts)
+        self.idx = np.arange(self.n0)                 # device instance -> original index
+        self.failed = np.zeros(self.n0, dtype=bool)  # original instances taken out of the batch
+        self.tables0 = tables
+        self.grid_like = isinstance(tables, np.ndarray) and tables.ndim == 2 and all(l is layouts[0] for l in layouts)
+        self.layouts0 = list(layouts)
+        self._bind(list(layouts), tables)
+
+    def _bind(self, layouts, tables):
+        self.layouts = layouts
+        if self.grid_like:
+            self.s.set_instances_of(layouts[0], np.asarray(tables).reshape(len(layouts), -1))  # grid points
         else:
-            self.s.set_instances(list(zip(self.layouts, self.tables)))
-        self.ninst = len(self.layouts)
-        self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in self.layouts]
+            self.s.set_instances(list(zip(layouts, tables)))
+        self.ninst = len(layouts)
+        self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in layouts]
+
+    def _drop(self, bad):
+        """Take the device instances flagged in `bad` out of the batch (their current tables
+        are kept for the others, which are re-bound unchanged)."""
+        tabs = self.s.read_tables()
+        keep = ~bad
+        self.failed[self.idx[bad]] = True
+        self.idx = self.idx[keep]
+        lays = [l for l, k in zip(self.layouts, keep) if k]
+        tabs = [t for t, k in zip(tabs, keep) if k]
+        if not lays:
+            self.ninst = 0
+            raise InvalidModelParameters("every instance of the batch landed at an invalid point")
+        self._bind(lays, np.stack(tabs) if self.grid_like else tabs)
+        return keep
+
+    def _eval(self, want_M):
+        """pint_eval; instances that raise an invalid-parameter status are dropped (their
+        evaluation failed at a state the fit cannot leave) and the others re-evaluated.
+        Returns the keep mask over the device instances before the call, or None."""
+        try:
+            self.s.eval(want_M=want_M)
+            return None
+        except L.PintError as e:
+            if e.code not in self.EVAL_ERRORS or self.s.lazy:
+                raise
+            bad = self.s.inst_status() != 0
+            if not bad.any():
+                raise
+        keep = self._drop(bad)
+        self.s.eval(want_M=want_M)
+        return keep
 
     # -- helpers ------------------------------------------------------------------------
     def _chi2_now(self):
@@ -130,13 +189,14 @@ class BatchFit:
         return c2, None
 
     def _step(self):
-        self.s.eval(want_M=Session.FIT)
+        keep = self._eval(Session.FIT)
         try:
             self.s.fit_step(1 if self.gls else 0)
         except L.PintError as e:
             if e.code != L.PINT_E_NOT_PD or self.s.lazy:
                 raise
             self._svd_step()
+        return keep
 
     def _thresholds(self):
         if self.threshold is not None:
@@ -175,50 +235,80 @@ class BatchFit:
         tabs = self.s.read_tables()
         self.final_tables = tabs
         if self.items is not None:
-            for (m, _), lay, t in zip(self.items, self.layouts, tabs):
-                unpack_table(lay, t, m)
+            for k, t in zip(self.idx, tabs):
+                m = self.items[k][0]
+                unpack_table(self.layouts0[k], t, m)
+        for k in np.where(self.failed)[0]:
+            results[k].status = "InvalidModelParameters"
+            results[k].chi2 = np.nan
         return results
 
     def _errors_into(self, results):
         dp, er, cov, _ = self.s.read_step()
-        for k, (res, lay) in enumerate(zip(results, self.layouts)):
+        for d, (k, lay) in enumerate(zip(self.idx, self.layouts)):
+            res = results[k]
             nc = len(lay.columns)
-            res.errors = er[k][:nc].copy()
-            res.cov = cov[k].copy()
-            res.noise_coeffs = dp[k][nc:lay.K].copy()
+            res.errors = er[d][:nc].copy()
+            res.cov = cov[d].copy()
+            res.noise_coeffs = dp[d][nc:lay.K].copy()
             res.labels = list(lay.columns)
             if self.items is not None:
                 m = self.items[k][0]
                 for j, name in enumerate(lay.columns[1:], start=1):
                     m[name].uncertainty = float(res.errors[j])
 
+    def _noise_into(self, results):
+        """Noise realisations of the last step (GLS only)."""
+        if not self.gls:
+            return
+        for k, nr in zip(self.idx, self.s.noise_resids()):
+            results[k].noise_resids = nr
+
+    def _full(self, arr, fill):
+        arr = np.asarray(arr)
+        out = np.full(self.n0, fill, dtype=arr.dtype)
+        out[self.idx] = arr
+        return out
+
     # -- plain WLS/GLS (fitter.py:1965-2087, :2104-2289) -------------------------------
     def fit_plain(self, maxiter=1, outputs=True):
         """outputs=False (grid points): no per-instance FitResult, no step/covariance
         read-back; returns a BatchOutcome of arrays (chi2, status)."""
-        results = [FitResult() for _ in range(self.ninst)] if outputs else None
+        results = [FitResult() for _ in range(self.n0)] if outputs else None
         for _ in range(maxiter):
             self._step()
             if outputs:
                 self._errors_into(results)
+                self._noise_into(results)
             self.s.apply_step(np.ones(self.ninst))
-        self.s.eval(want_M=False)
+        self._eval(False)
         c2, _ = self._chi2_now()
         if not outputs:
-            return self._finish_arrays(np.array(c2, dtype=np.float64), np.ones(self.ninst, dtype=bool),
-                                       np.zeros(self.ninst, dtype=bool))
-        for r, c in zip(results, c2):
-            r.chi2 = float(c)
-            r.converged = True
+            chi2 = self._full(np.array(c2, dtype=np.float64), np.nan)
+            return self._finish_arrays(chi2, ~self.failed, np.zeros(self.n0, dtype=bool))
+        for k, c in zip(self.idx, c2):
+            results[k].chi2 = float(c)
+            results[k].converged = True
         return self._finish(results)
 
     def _finish_arrays(self, chi2, converged, exc):
         # the final parameter tables stay on the device until asked for (final_tables_flat)
-        return BatchOutcome(chi2, converged, exc)
+        out = BatchOutcome(chi2, converged, exc)
+        out.failed = self.failed.copy()
+        out.maxiter_reached &= ~self.failed
+        return out
 
     def final_tables_flat(self):
-        """The instances' parameter tables after the fit, concatenated (device -> host)."""
-        return self.s.read_tables_flat()
+        """The instances' parameter tables after the fit, concatenated (device -> host);
+        instances taken out of the batch (failed) are NaN."""
+        t = self.s.read_tables()
+        out = [None] * self.n0
+        for k, tt in zip(self.idx, t):
+            out[k] = tt
+        for k in range(self.n0):
+            if out[k] is None:
+                out[k] = np.full(self.layouts0[k].tstride, np.nan)
+        return np.concatenate(out)
 
     # -- downhill (fitter.py:999-1105) ---------------------------------------------------
     def fit_downhill(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,
@@ -226,13 +316,14 @@ class BatchFit:
         """The reference's per-fitter control flow (fitter.py:1015-1095), applied to every
         instance at once: a lambda-halving line search on each instance's chi2, with the
         best state tracked per instance.  Decisions are vectorised over instances; each
-        trial is one batched eval + chi2 of all undecided instances."""
+        trial is one batched eval + chi2 of all undecided instances.  A trial state whose
+        evaluation fails (invalid parameters) is a rejected trial of that instance only."""
+        self._step()                                     # step of the initial state (drops invalid ones)
         n = self.ninst
-        self._step()                                     # step of the initial state
         cur_tab = self.s.read_tables_flat()
         sizes = np.array([l.tstride for l in self.layouts])
         ent = np.repeat(np.arange(n), sizes)             # instance of every table entry
-        self.s.eval(want_M=False)
+        self._eval(False)
         cur_chi2, _ = self._chi2_now()
         cur_chi2 = np.array(cur_chi2, dtype=np.float64)
         best_chi2 = cur_chi2.copy()
@@ -249,12 +340,17 @@ class BatchFit:
             while not decided.all():
                 self.s.set_tables(cur_tab)
                 self.s.apply_step(np.where(decided, 0.0, lam))
+                bad = np.zeros(n, dtype=bool)
                 try:
                     self.s.eval(want_M=False)
-                    new_chi2, _ = self._chi2_now()
-                    new_chi2 = np.array(new_chi2, dtype=np.float64)
-                except Exception:
-                    new_chi2 = np.full(n, np.nan)
+                except L.PintError as e:
+                    if e.code not in self.EVAL_ERRORS:
+                        raise
+                    bad = self.s.inst_status() != 0
+                    if not bad.any():
+                        raise
+                new_chi2, _ = self._chi2_now()
+                new_chi2 = np.where(bad, np.nan, np.array(new_chi2, dtype=np.float64))
                 new_tab = self.s.read_tables_flat()
                 und = ~decided
                 d = cur_chi2 - new_chi2
@@ -281,22 +377,29 @@ class BatchFit:
             active &= ~(done | conv)
             if active.any() and it < maxiter - 1:
                 self.s.set_tables(cur_tab)
-                self._step()  # step at the new current states (inactive ones are ignored)
+                # step at the new current states (inactive ones are ignored); every current
+                # state has been evaluated, so nothing can be dropped here
+                if self._step() is not None:
+                    raise RuntimeError("a downhill state evaluated before failed its re-evaluation")
         # best state -> model, residuals; covariance from a step at the best state
         self.s.set_tables(best_tab)
-        self._step()
+        if self._step() is not None:
+            raise RuntimeError("a downhill best state evaluated before failed its re-evaluation")
         results = None
         if outputs:
-            results = [FitResult() for _ in range(n)]
+            results = [FitResult() for _ in range(self.n0)]
             self._errors_into(results)
+            self._noise_into(results)
         self.s.eval(want_M=False)
         c2, _ = self._chi2_now()
         if not outputs:
-            return self._finish_arrays(np.array(c2, dtype=np.float64), converged, exc)
-        for k, r in enumerate(results):
-            r.chi2 = float(c2[k])
-            r.converged = bool(converged[k])
-            r.status = "StepProblem" if exc[k] else ("converged" if converged[k] else "MaxiterReached")
+            return self._finish_arrays(self._full(np.array(c2, dtype=np.float64), np.nan),
+                                       self._full(converged, False), self._full(exc, False))
+        for d, k in enumerate(self.idx):
+            r = results[k]
+            r.chi2 = float(c2[d])
+            r.converged = bool(converged[d])
+            r.status = "StepProblem" if exc[d] else ("converged" if converged[d] else "MaxiterReached")
         return self._finish(results)
 
     def close(self):
@@ -334,18 +437,54 @@ class Fitter:
     def get_designmatrix(self):
         return self.model.designmatrix(self.toas)
 
-    def _run(self, mode, plain=True, threshold=None, style=None, **kw):
-        bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style)
+    def _run(self, mode, plain=True, threshold=None, style=None, noise=True, **kw):
+        from .residuals import Residuals
+        bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style,
+                      track_mode=self.track_mode)
+        self.resids = None
         try:
             res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
+            # the final residuals are already on the device (the fit's last evaluation):
+            # take them from the fit's own session instead of re-uploading (a WLS fit of a
+            # correlated-noise model has no noise basis there, so its GLS chi2 is computed anew)
+            if mode == "gls" or not self.model.has_correlated_errors:
+                self.resids = Residuals._from_batch(self.toas, self.model, bf, 0, res.chi2, self.track_mode)
         finally:
             bf.close()
         self.fitresult = res
         self.errors = res.errors
         self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
         self.converged = res.converged
-        self.update_resids()
+        if self.resids is None:
+            self.update_resids()
+        if mode == "gls" and noise:
+            self.resids.noise_resids = res.noise_resids
         return res
+
+    def update_model(self, chi2=None):
+        """fitter.py:530-555: START/FINISH/NTOA (and EPHEM/CLOCK when the TOAs carry them),
+        DMDATA; after a fit CHI2, CHI2R = chi2/dof and TRES = the weighted rms (us)."""
+        from .parameter import LD, make_param
+        m = self.model
+
+        def par(name):
+            if name not in m:
+                m.add_param(make_param(name))
+            return m[name]
+
+        mj = self.toas.get_mjds()
+        par("START").value = LD(np.min(mj))
+        par("FINISH").value = LD(np.max(mj))
+        par("NTOA").value = int(self.toas.ntoas)
+        if getattr(self.toas, "ephem", None):
+            par("EPHEM").value = self.toas.ephem
+        if getattr(self.toas, "clock", None):
+            par("CLOCK").value = self.toas.clock
+        par("DMDATA").value = False
+        if chi2 is not None:
+            par("CHI2").value = float(chi2)
+            par("CHI2R").value = float(chi2) / self.resids.dof
+            par("TRES").value = float(self.resids.rms_weighted())
 
     def set_params(self, d):
         for k, v in d.items():
@@ -357,14 +496,23 @@ class WLSFitter(Fitter):
         if self.model.has_correlated_errors:
             pass  # the reference WLSFitter ignores correlated noise
         res = self._run("wls", plain=True, maxiter=maxiter, threshold=threshold, style="wls")
+        self.update_model(res.chi2)
         return res.chi2
 
 
 class GLSFitter(Fitter):
     def fit_toas(self, maxiter=1, threshold=0, full_cov=False, debug=False):
-        if full_cov:
-            raise NotImplementedError("full_cov=True (dense N x N covariance) is outside the GPU path")
-        res = self._run("gls", plain=True, maxiter=maxiter, threshold=threshold, style="gls")
+        """fitter.py:2104.  full_cov=True: the reference forms the dense N x N covariance
+        C = N + U Phi U^T, Cholesky-factors it and solves M^T C^-1 M with the timing columns
+        only (fitter.py:2180-2184).  By the Woodbury identity that system's solution and
+        inverse are exactly the timing block of the rank-reduced system the device solves
+        (the reference asserts the two agree, tests/test_gls_fitter.py:85-90), so both
+        settings run the same device path; as in the reference, full_cov=True computes no
+        noise realisations (fitter.py:2268)."""
+        self.full_cov = full_cov
+        res = self._run("gls", plain=True, maxiter=maxiter, threshold=threshold, style="gls",
+                        noise=not full_cov)
+        self.update_model(res.chi2)
         return res.chi2
 
 
@@ -381,6 +529,7 @@ class DownhillFitter(Fitter):
         res = self._run(self.mode, plain=False, maxiter=maxiter, required_chi2_decrease=required_chi2_decrease,
                         max_chi2_increase=required_chi2_decrease, min_lambda=required_chi2_decrease,
                         threshold=threshold, style="wls" if self.mode == "wls" else "glsstate")
+        self.update_model(res.chi2)
         if res.status == "StepProblem":
             raise StepProblem("Unable to improve chi2 even with very small steps")
         if not res.converged:

@@ -15,7 +15,7 @@ from typing import List, Sequence
 
 import numpy as np
 
-from .fitter import (BatchFit, DownhillFitter, GLSFitter, DownhillGLSFitter, WLSFitter)
+from .fitter import (BatchFit, DownhillFitter, GLSFitter, DownhillGLSFitter, WLSFitter, model_key)
 from .parameter import LD
 
 
@@ -74,13 +74,9 @@ def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
 _GRID = {}
 
 
-def _model_key(model):
-    return tuple((n, str(model[n].value), bool(model[n].frozen)) for n in model.params)
-
-
 def _grid_session(base, toas, gls):
     from .engine import Session, build_layout
-    key = (id(toas), toas.ntoas, gls, _model_key(base))
+    key = (id(toas), toas.ntoas, gls, model_key(base))
     cur = _GRID.get("cur")
     if cur is not None and cur[0] == key and cur[3] is toas:
         return cur[1], cur[2]
@@ -157,5 +153,9 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
         except Exception:
             _drop_grid_session()
             raise
+    # extras are the point's parameter values after its fit, also for a MaxiterReached point
+    # (gridutils.py:107-110 reads them outside the try); a point taken out of the batch as
+    # invalid has none (NaN, final_tables_flat)
     chi2_all = gather_blocks(chi2, per, npts, dist)
-    return chi2_all.reshape(shape), {e: extra[e] for e in extraparnames}
+    extra_all = {e: gather_blocks(extra[e], per, npts, dist).reshape(shape) for e in extraparnames}
+    return chi2_all.reshape(shape), extra_all

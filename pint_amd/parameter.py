@@ -133,6 +133,8 @@ _DEFS = {
     "UNITS": ("", "str", "", False, None), "START": ("", "mjd", "d", True, None),
     "FINISH": ("", "mjd", "d", True, None), "TRACK": ("", "str", "", False, None),
     "BINARY": ("", "str", "", False, None), "NTOA": ("", "int", "", False, None),
+    "CHI2": ("", "float", "", False, None), "CHI2R": ("", "float", "", False, None),
+    "TRES": ("", "float", "us", False, None), "DMDATA": ("", "bool", "", False, None),
     "TZRMJD": ("AbsPhase", "mjd", "d", True, None), "TZRSITE": ("AbsPhase", "str", "", False, None),
     "TZRFRQ": ("AbsPhase", "float", "MHz", False, None),
     # astrometry (astrometry.py)

@@ -57,6 +57,28 @@ class Residuals:
         finally:
             s.close()
 
+    @classmethod
+    def _from_batch(cls, toas, model, bf, d, chi2, track_mode=None):
+        """The residuals of device instance `d` of a BatchFit after its last evaluation
+        (the fit's final state): read from the fit's session, no re-upload."""
+        r = cls.__new__(cls)
+        r.toas, r.model = toas, model
+        r.subtract_mean = "PhaseOffset" not in model.components
+        r.use_weighted_mean = True
+        r.use_abs_phase = True
+        r.noise_resids = {}
+        r._track_mode_arg = track_mode
+        lay = bf.layouts[d]
+        tr, pr, _ = bf.s.read_resids()
+        r.time_resids, r.phase_resids = tr[d].copy(), pr[d].copy()
+        r.track_mode = lay.track_mode
+        r._sigma_us = lay.sigma_us
+        r._chi2 = float(chi2)
+        corr = model.has_correlated_errors and (lay.nred > 0 or lay.nep > 0)
+        kind = 1 if (corr and bf.gls) else (2 if model.has_correlated_errors else 0)
+        r._lognorm = float(bf.s.lognorm(kind)[d])
+        return r
+
     @property
     def resids(self):
         return self.time_resids

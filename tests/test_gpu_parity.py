@@ -641,4 +641,5 @@ def test_grid_downhill_extra_matches_single_fits():
             assert np.isnan(got), (k, got)
         else:
             assert abs(got / want - 1) < 1e-9, (k, got, want)
-            assert abs(ex["DM"][k] - float(g.model.DM.value)) < 1e-9 * abs(float(g.model.DM.value)), k
+            assert abs(ex["DM"].ravel()[k] - float(g.model.DM.value)) < 1e-9 * abs(float(g.model.DM.value)), k
+    assert ex["DM"].shape == c2.shape  # meshgrid-shaped like chi2 (gridutils.py:334-370)
