@@ -116,7 +116,8 @@ int pint_device_count(void);
 
 /* Upload one pulsar (packed TOAs + model structure); returns its id >= 0, or -status.
  * Replaces the TOAs.table hand-off of get_model_and_toas (model_builder.py:859) and the
- * param-independent noise bases: red_freq[nred] are the PLRedNoise Fourier frequencies
+ * param-independent noise bases: red_freq[2*nred] are the PLRedNoise Fourier frequencies
+ * as double-double pairs (hi[nred] then lo[nred]: the reference keeps them longdouble)
  * (noise_model.py:847 get_rednoise_freqs), red_phi[2*nred] their weights
  * (noise_model.py:780 get_noise_weights).  The library copies everything it needs. */
 int pint_add_pulsar(pint_ctx *ctx, const pint_toas_t *toas, const pint_spec_t *spec,
@@ -252,11 +253,12 @@ int pint_debug_read(pint_ctx *ctx, int which, double *out);
  * counterpart -- these expose the intermediate arrays of fitter.py:2164-2202):
  * pint_debug_gram writes, per instance, the assembled unnormalised normal matrix
  * [M | r]^T N^-1 [M | r] of the last pint_fit_step ((K_i+1)^2, original column order,
- * residual last, ECORR block eliminated) followed by M's K_i unweighted column sums of
+ * residual last; ECORR block eliminated, or with pre_ecorr != 0 its Schur term
+ * sum_e s_e s_e^T / D_e added back) followed by M's K_i unweighted column sums of
  * squares (utils.py:2879 normalize_designmatrix).  pint_debug_set_resids replaces every
  * instance's time residuals (n_i each) by the caller's, so that pint_fit_step and
  * pint_chi2_gls run on e.g. the reference's own residual arrays. */
-int pint_debug_gram(pint_ctx *ctx, double *out);
+int pint_debug_gram(pint_ctx *ctx, int pre_ecorr, double *out);
 int pint_debug_set_resids(pint_ctx *ctx, const double *time_resid);
 
 /* Per-instance status bits (1 << PINT_E_*) raised by evaluations since the last call, one

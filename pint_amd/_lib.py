@@ -97,7 +97,7 @@ def lib():
     L.pint_check_step.argtypes = [vp, C.c_int]
     L.pint_inst_status.argtypes = [vp, C.POINTER(C.c_int32)]
     L.pint_noise_resids.argtypes = [vp, dptr, dptr]
-    L.pint_debug_gram.argtypes = [vp, dptr]
+    L.pint_debug_gram.argtypes = [vp, C.c_int, dptr]
     L.pint_debug_set_resids.argtypes = [vp, dptr]
     _lib = L
     return L

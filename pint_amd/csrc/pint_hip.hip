@@ -37,7 +37,7 @@ struct PsrDev {
     const uint64_t* jmask;
     const int32_t *dmx_a, *dmx_b;
     const pint_spec_t* spec;
-    const double* red_freq;  // nred
+    const double* red_freq;  // 2 nred: the frequencies as double-double, hi[nred] then lo[nred]
     const double* red_phi;   // 2*nred
     const double* red_cs;    // n x 2: (cos, sin) of the red-noise fundamental per TOA (k_redbase)
     const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trigu)
@@ -253,7 +253,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
         dd ts = dd_mul_d(t.tdb, DAYSEC);
         double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
         for (int k = 0; k < S.nred; k++, colp += 2L * n) {
-            dd x = dd_mul_d(ts, Pd.red_freq[k]);
+            dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
             double fr = dd_to_d(dd_sub(x, dd_floor(x)));
             double sn, cs;
             sincos(TWO_PI * fr, &sn, &cs);
@@ -1055,11 +1055,11 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
 // with the phase t_i f_1 reduced in double-double; computed once at pint_add_pulsar
 // (TOA-only data, like tdb).  Harmonic m is reached by rotations of it.
 __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __restrict__ tdb_lo, int n, double f1,
-                          double* __restrict__ cs) {
+                          double f1_lo, double* __restrict__ cs) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double s, c;
-    dd_sincos_cyc(dd_mul_d(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), f1), &s, &c);
+    dd_sincos_cyc(dd_mul(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), dd_make(f1, f1_lo)), &s, &c);
     cs[2 * i] = c;
     cs[2 * i + 1] = s;
 }
@@ -1429,6 +1429,7 @@ __device__ unsigned long long g_ts[32];
 #define TS(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_ts[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 constexpr int BS_MAXNB = 12;  // 78 blocks x 2 KiB + 2 vectors fit the 160 KiB LDS
+constexpr int RSCR = 4 * 512;   // per-instance global scratch of the solves (4 vectors <= 512)
 
 __device__ __forceinline__ int swz(int r, int c) { return (c << 4) + (r ^ (c & 14)); }
 __device__ __forceinline__ int lblk(int I, int J) { return ((I * (I + 1)) / 2 + J) << 8; }
@@ -1469,6 +1470,18 @@ __device__ __forceinline__ void bstore(double* Z, const double4_t& v, int lane, 
 #pragma unroll
     for (int q = 0; q < 4; q++) Z[swz((lane >> 4) + 4 * q, lane & 15)] = s * v[q];
 }
+
+// Iterative refinement residuals r = b - A x are accumulated in double-double (two_prod +
+// dd_add, error-free): with an extended-precision residual each refinement pass contracts
+// the error by ~cond * eps, so two passes reach the correctly rounded solution of the FP64
+// system even at cond 1e12 -- below the rounding of the reference's own cho_solve.
+__device__ __forceinline__ void dd_acc(dd& s, double a, double b) { s = dd_add(s, two_prod(a, b)); }
+__device__ __forceinline__ dd dd_quad_sum(dd s) {  // sum over the 4 lanes of a lane quad
+    s = dd_add(s, dd_make(__shfl_xor(s.hi, 1, 64), __shfl_xor(s.lo, 1, 64)));
+    s = dd_add(s, dd_make(__shfl_xor(s.hi, 2, 64), __shfl_xor(s.lo, 2, 64)));
+    return s;
+}
+constexpr int REFINE_PASSES = 2;
 
 // One wave: Cholesky of the (full, symmetric) 16x16 block in registers (lane r holds row
 // r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
@@ -1612,7 +1625,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
                                                        double* __restrict__ dpars, double* __restrict__ errs,
                                                        double* __restrict__ cov, double* __restrict__ chi2lin,
                                                        double* __restrict__ sigL, int* __restrict__ status,
-                                                       int skip_dsplit) {
+                                                       int skip_dsplit, double* __restrict__ rscr) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -1628,33 +1641,41 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     double* A = lds;
     double* bv = A + nblk * 256;
     double* yv = bv + nb * 16;
+    // per-instance vectors in global scratch (the LDS holds the factor and two vectors at
+    // nb = 12): reciprocal column norms, the normalised solution, the refinement residual
+    double* inv = rscr + (long)inst * RSCR;
+    double* xs = inv + RSCR / 4;
+    double* rv = xs + RSCR / 4;
     const bool cmp = compact && Pd.dsplit;
     const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);
-    // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1)
-    auto nrmf = [&](int j) {
-        if (j >= K) return 1.0;
-        double v = sqrt(mode == 0 ? G(j, j) : colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j));
-        return v == 0.0 ? 1.0 : v;
-    };
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
+    // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1), as reciprocals
+    for (int j = tid; j < nb * 16; j += NW * 64) {
+        double v = 1.0;
+        if (j < K) {
+            v = sqrt(mode == 0 ? G(j, j) : colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j));
+            v = v == 0.0 ? 1.0 : v;
+        }
+        inv[j] = 1.0 / v;
+    }
+    __syncthreads();
+    // the normalised normal matrix element (i, j < K), built from the Gram in global memory
+    auto Aij = [&](int i, int j) {
+        double v = G(i, j) * (inv[i] * inv[j]);
+        if (i == j && mode == 1 && i >= ncol) v += (inv[i] * inv[i]) / Pd.red_phi[i - ncol];
+        return v;
+    };
     for (int e = tid; e < nblk * 256; e += NW * 64) {
         int Ib, Jb;
         tri_decode(e >> 8, Ib, Jb);
         const int r = e & 15, c = (e >> 4) & 15;
         const int gi = Ib * 16 + r, gj = Jb * 16 + c;
-        double v;
-        if (gi < K && gj < K) {
-            const double ni = nrmf(gi), nj = nrmf(gj);
-            v = G(gi, gj) / (ni * nj);
-            if (gi == gj && mode == 1 && gi >= ncol) v += 1.0 / Pd.red_phi[gi - ncol] / (ni * ni);
-        } else {
-            v = (gi == gj) ? 1.0 : 0.0;
-        }
+        const double v = (gi < K && gj < K) ? Aij(gi, gj) : (gi == gj ? 1.0 : 0.0);
         A[((e >> 8) << 8) + swz(r, c)] = v;
     }
-    for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) / nrmf(j) : 0.0;
+    for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) * inv[j] : 0.0;
     const double rwr = G(Kfull, Kfull);
     __syncthreads();
     if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag)) {
@@ -1674,45 +1695,64 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
             for (int q = 0; q < 4; q++) {
                 const int row = bi * 16 + (lane >> 4) + 4 * q, col = bj * 16 + (lane & 15);
                 if (row < ncol && col < ncol) {
-                    const double v = acc[q] / (nrmf(row) * nrmf(col));
+                    const double v = acc[q] * (inv[row] * inv[col]);
                     C[(long)row * ncol + col] = v;
                     C[(long)col * ncol + row] = v;
                 }
             }
         }
     }
-    // errors (all K columns) and y = X b, 4 lanes per column / row
+    // errors (all K columns); x = X^T (X b), then one step of iterative refinement
+    // x += X^T X (b - A x) with A rebuilt from the Gram: the explicit L^-1 loses ~cond(L)
+    // digits that LAPACK's triangular solves (cho_solve, fitter.py:2197) keep, and on a
+    // normalised system of cond 1e12 (J0740) that is ~10x the reference's own rounding
     const int g0 = tid >> 2, sub = tid & 3;
     for (int g = g0; g < nb * 16; g += NW * 16) {
         const int Jb = g >> 4, cc = g & 15;
-        double se = 0.0, sy = 0.0;
+        double se = 0.0;
         for (int rr = g + sub; rr < nb * 16; rr += 4) {
             const double x = A[lblk(rr >> 4, Jb) + swz(rr & 15, cc)];
             se += x * x;
         }
-        for (int c = sub; c <= g; c += 4) sy += A[lblk(Jb, c >> 4) + swz(cc, c & 15)] * bv[c];
         se += __shfl_xor(se, 1, 64);
         se += __shfl_xor(se, 2, 64);
-        sy += __shfl_xor(sy, 1, 64);
-        sy += __shfl_xor(sy, 2, 64);
-        if (sub == 0) {
-            if (g < K) errs[I.coff + g] = sqrt(se) / nrmf(g);
-            yv[g] = sy;
-        }
+        if (sub == 0 && g < K) errs[I.coff + g] = sqrt(se) * inv[g];
     }
-    __syncthreads();
-    // xhat = X^T y (normalised) -> dpars; chi2lin = r^T W r - |y|^2
-    double q2 = 0.0;
-    for (int g = g0; g < K; g += NW * 16) {
-        const int Jb = g >> 4, cc = g & 15;
-        double s = 0.0;
-        for (int rr = g + sub; rr < nb * 16; rr += 4) s += A[lblk(rr >> 4, Jb) + swz(rr & 15, cc)] * yv[rr];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        if (sub == 0) {
-            dpars[I.coff + g] = s / nrmf(g);
-            q2 += yv[g] * yv[g];
+    for (int pass = 0; pass <= REFINE_PASSES; pass++) {
+        const double* rhs = pass == 0 ? bv : rv;
+        for (int g = g0; g < nb * 16; g += NW * 16) {  // y = X rhs
+            const int Jb = g >> 4, cc = g & 15;
+            double sy = 0.0;
+            for (int c = sub; c <= g; c += 4) sy += A[lblk(Jb, c >> 4) + swz(cc, c & 15)] * rhs[c];
+            sy += __shfl_xor(sy, 1, 64);
+            sy += __shfl_xor(sy, 2, 64);
+            if (sub == 0) yv[g] = sy;
         }
+        __syncthreads();
+        for (int g = g0; g < nb * 16; g += NW * 16) {  // x (+)= X^T y
+            const int Jb = g >> 4, cc = g & 15;
+            double sx = 0.0;
+            for (int rr = g + sub; rr < nb * 16; rr += 4) sx += A[lblk(rr >> 4, Jb) + swz(rr & 15, cc)] * yv[rr];
+            sx += __shfl_xor(sx, 1, 64);
+            sx += __shfl_xor(sx, 2, 64);
+            if (sub == 0) xs[g] = (pass == 0 ? 0.0 : xs[g]) + (g < K ? sx : 0.0);
+        }
+        __syncthreads();
+        if (pass == REFINE_PASSES) break;
+        for (int g = g0; g < nb * 16; g += NW * 16) {  // r = b - A x, double-double
+            dd sa = dd_make(0.0);
+            if (g < K)
+                for (int j = sub; j < K; j += 4) dd_acc(sa, Aij(g, j), xs[j]);
+            sa = dd_quad_sum(sa);
+            if (sub == 0) rv[g] = g < K ? dd_to_d(dd_sub(dd_make(bv[g]), sa)) : 0.0;
+        }
+        __syncthreads();
+    }
+    // dpars = x / norm; chi2lin = r^T W r - b^T x (= the minimised linearised chi2)
+    double q2 = 0.0;
+    for (int g = tid; g < K; g += NW * 64) {
+        dpars[I.coff + g] = xs[g] * inv[g];
+        q2 += bv[g] * xs[g];
     }
     q2 = block_sum<NW>(q2, sh);
     if (tid == 0) chi2lin[inst] = rwr - q2;
@@ -1742,7 +1782,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        const double* __restrict__ DCS, double* __restrict__ dpars,
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                       int* __restrict__ status, int fuse_sigma) {
+                                                       int* __restrict__ status, int fuse_sigma, double* __restrict__ rscr) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -1894,8 +1934,11 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     }
     __syncthreads();
     TS(4);
-    // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors; chi2lin ----
-    double bx_dot = 0.0;
+    // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors ----
+    double* xd = rscr + (long)inst * RSCR;  // normalised x_d, x_x and the refinement residuals
+    double* xx = xd + RSCR / 4;
+    double* rd = xx + RSCR / 4;
+    double* rx = rd + RSCR / 4;
     for (int g = g0; g < Kd; g += NW * 16) {
         double s1 = 0.0, se = 0.0;
         for (int rr = g + sub; rr < nbd * 16; rr += 4) {
@@ -1908,11 +1951,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         se += __shfl_xor(se, 1, 64);
         se += __shfl_xor(se, 2, 64);
         if (sub == 0) {
-            const int o = Pd.dorig[g];
-            const double in_ = ind[g];
-            dpars[I.coff + o] = s1 * in_;
-            errs[I.coff + o] = sqrt(se) * in_;
-            bx_dot += Gd(g, Kres) * in_ * s1;  // b_d . x_d
+            xd[g] = s1;
+            errs[I.coff + Pd.dorig[g]] = sqrt(se) * ind[g];
         }
     }
     for (int a = g0; a < ndc; a += NW * 16) {
@@ -1927,13 +1967,80 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sw += __shfl_xor(sw, 1, 64);
         sw += __shfl_xor(sw, 2, 64);
         if (sub == 0) {
-            const double d = Dn[a], ina = inx[a];
-            const double xx = bx[a] / d - sz * isd[a];
-            const int o = Pd.xorig[a];
-            dpars[I.coff + o] = xx * ina;
-            errs[I.coff + o] = sqrt(1.0 / d + sw / d) * ina;
-            bx_dot += bx[a] * xx;
+            const double d = Dn[a];
+            xx[a] = bx[a] / d - sz * isd[a];
+            errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / d + sw / d) * inx[a];
         }
+    }
+    __syncthreads();
+    // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
+    // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
+    // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y).  The explicit L^-1 loses ~cond(L) digits that
+    // LAPACK's triangular solves keep (cho_solve, fitter.py:2197) ----
+    auto Ad = [&](int i, int j) {
+        double v = Gd(i, j) * (ind[i] * ind[j]);
+        if (i == j && mode == 1 && i >= red0) v += (ind[i] * ind[i]) / Pd.red_phi[i - red0];
+        return v;
+    };
+    for (int pass = 0; pass < REFINE_PASSES; pass++) {
+        for (int c = g0; c < Kd; c += NW * 16) {  // r_d = b_d - A_dd x_d - A_dx x_x (dd)
+            dd sa = dd_make(0.0);
+            for (int j = sub; j < Kd; j += 4) dd_acc(sa, Ad(c, j), xd[j]);
+            for (int a = sub; a < ndc; a += 4) dd_acc(sa, Sdi[(long)a * Kp + c] * (ind[c] * inx[a]), xx[a]);
+            sa = dd_quad_sum(sa);
+            if (sub == 0) rd[c] = dd_to_d(dd_sub(dd_make(Gd(c, Kres) * ind[c]), sa));
+        }
+        for (int a = g0; a < ndc; a += NW * 16) {  // r_x = b_x - A_xd x_d - D x_x (dd)
+            dd sa = dd_make(0.0);
+            for (int j = sub; j < Kd; j += 4) dd_acc(sa, Sdi[(long)a * Kp + j] * (ind[j] * inx[a]), xd[j]);
+            if (sub == 0) dd_acc(sa, Dn[a], xx[a]);
+            sa = dd_quad_sum(sa);
+            if (sub == 0) rx[a] = dd_to_d(dd_sub(dd_make(bx[a]), sa));
+        }
+        __syncthreads();
+        for (int c = g0; c < nbd * 16; c += NW * 16) {
+            double sa = 0.0;
+            if (c < Kd)
+                for (int a = sub; a < ndc; a += 4) sa += Sdi[(long)a * Kp + c] * (ind[c] * inx[a]) * (rx[a] / Dn[a]);
+            sa += __shfl_xor(sa, 1, 64);
+            sa += __shfl_xor(sa, 2, 64);
+            if (sub == 0) bd[c] = c < Kd ? rd[c] - sa : 0.0;
+        }
+        __syncthreads();
+        for (int g = g0; g < nbd * 16; g += NW * 16) {
+            double sy = 0.0;
+            for (int c = sub; c <= g; c += 4) sy += A[lblk(g >> 4, c >> 4) + swz(g & 15, c & 15)] * bd[c];
+            sy += __shfl_xor(sy, 1, 64);
+            sy += __shfl_xor(sy, 2, 64);
+            if (sub == 0) yv[g] = sy;
+        }
+        __syncthreads();
+        for (int g = g0; g < Kd; g += NW * 16) {
+            double s1 = 0.0;
+            for (int rr = g + sub; rr < nbd * 16; rr += 4) s1 += A[lblk(rr >> 4, g >> 4) + swz(rr & 15, g & 15)] * yv[rr];
+            s1 += __shfl_xor(s1, 1, 64);
+            s1 += __shfl_xor(s1, 2, 64);
+            if (sub == 0) xd[g] += s1;
+        }
+        for (int a = g0; a < ndc; a += NW * 16) {
+            double sz = 0.0;
+            for (int rr = sub; rr < nbd * 16; rr += 4)
+                sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * yv[rr];
+            sz += __shfl_xor(sz, 1, 64);
+            sz += __shfl_xor(sz, 2, 64);
+            if (sub == 0) xx[a] += rx[a] / Dn[a] - sz * isd[a];
+        }
+        __syncthreads();
+    }
+    // ---- steps (par units), chi2lin = r^T W r - b . x ----
+    double bx_dot = 0.0;
+    for (int g = tid; g < Kd; g += NW * 64) {
+        dpars[I.coff + Pd.dorig[g]] = xd[g] * ind[g];
+        bx_dot += Gd(g, Kres) * ind[g] * xd[g];
+    }
+    for (int a = tid; a < ndc; a += NW * 64) {
+        dpars[I.coff + Pd.xorig[a]] = xx[a] * inx[a];
+        bx_dot += bx[a] * xx[a];
     }
     bx_dot = block_sum<NW>(bx_dot, sh);
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
@@ -2424,7 +2531,7 @@ __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ ps
     if (S.nred > 0) {
         const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
         for (int k = 0; k < S.nred; k++) {
-            const dd x = dd_mul_d(ts, Pd.red_freq[k]);
+            const dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
             const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
             double sn, cs;
             sincos(TWO_PI * fr, &sn, &cs);
@@ -2460,15 +2567,24 @@ __global__ __launch_bounds__(256) void k_debug_gram(const PsrDev* __restrict__ p
                                                     const double* __restrict__ Gpart, const double* __restrict__ colsq,
                                                     int nsplit, int compact, const double* __restrict__ Sd,
                                                     const double* __restrict__ DD, const double* __restrict__ DCS,
-                                                    const long* __restrict__ ooff, double* __restrict__ out) {
+                                                    const double* __restrict__ esum, const double* __restrict__ eD,
+                                                    int pre_ecorr, const long* __restrict__ ooff,
+                                                    double* __restrict__ out) {
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const bool cmp = compact && Pd.dsplit;
     const GramView g = gram_view(Pd, I, Gpart, cmp, Sd, DD);
     const int W = I.K + 1;
+    const int nep = pre_ecorr ? Pd.nep : 0;  // ECORR part added back: the Gram before elimination
     double* o = out + ooff[inst];
-    for (long e = threadIdx.x; e < (long)W * W; e += blockDim.x) o[e] = g((int)(e / W), (int)(e % W));
+    for (long e = threadIdx.x; e < (long)W * W; e += blockDim.x) {
+        const int i = (int)(e / W), j = (int)(e % W);
+        double v = g(i, j);
+        for (int q = 0; q < nep; q++)
+            v += esum[I.eoff + (long)q * I.Kp + i] * esum[I.eoff + (long)q * I.Kp + j] / eD[I.epoff + q];
+        o[e] = v;
+    }
     for (int j = threadIdx.x; j < I.K; j += blockDim.x) o[(long)W * W + j] = colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j);
 }
 
@@ -2547,6 +2663,7 @@ struct pint_ctx {
     int max_nep = 0;
     int* d_status = nullptr;
     int* d_istatus = nullptr;  // per-instance status bits since the last pint_inst_status read
+    double* d_rscr = nullptr;  // per-instance scratch vectors of the solves (RSCR doubles each)
     int maxK = 0;
     // HIP event pairs: 0/1 eval, 2/3 eval with design matrix, 4/5 resid, 6/7 ecorr + Gram +
     // reduction, 7/8 solve, 10/11 Woodbury chi2, 12/13 the Gram kernels alone, 14/15 k_greduce
@@ -2738,7 +2855,7 @@ static void free_instances(pint_ctx* ctx) {
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
-                   (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2, (void**)&ctx->d_istatus,
+                   (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2, (void**)&ctx->d_istatus, (void**)&ctx->d_rscr,
                    (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
                    (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_eigw,
@@ -2831,12 +2948,12 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->jump_mask, n + 1, d.jmask);
     rc |= upload(ctx, ph, t->dmx_a, n + 1, d.dmx_a);
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
-    rc |= upload(ctx, ph, red_freq, (size_t)spec->nred, d.red_freq);
+    rc |= upload(ctx, ph, red_freq, (size_t)2 * spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * n, d.red_cs);
     if (!rc && spec->nred > 0) {
         hipLaunchKernelGGL(k_redbase, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, d.tdb_hi, d.tdb_lo, n,
-                           red_freq[0], (double*)d.red_cs);
+                           red_freq[0], red_freq[spec->nred], (double*)d.red_cs);
         HIPCHK(hipGetLastError());
     }
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
@@ -3215,6 +3332,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_rp, sizeof(double) * out));
     HIPCHK(cmalloc((void**)&ctx->d_chi2, sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_istatus, sizeof(int) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_rscr, sizeof(double) * RSCR * (size_t)ninst));
     HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ninst, ctx->stream));
     HIPCHK(cmalloc((void**)&ctx->d_chi2g, sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_lognorm, sizeof(double) * ninst));
@@ -3547,7 +3665,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             const int kd = mode == 0 ? ph.dev.red0c : ph.dev.Kd;
             const int nbd = (kd + 15) / 16, nbk = (ph.dev.ndc + 15) / 16, nbs = (kn + 15) / 16;
             const int blk = nbd * (nbd + 1) / 2 + nbd * nbk;
-            if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB) dmx_ok = false;
+            if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB || nbk * 16 > RSCR / 4) dmx_ok = false;
             lds_x = std::max(lds_x, sizeof(double) * ((size_t)std::max(blk, nbs * (nbs + 1) / 2) * 256 +
                                                       (size_t)(3 * nbd + 4 * nbk) * 16));
         } else {
@@ -3600,7 +3718,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                            fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
                            ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                           fuse_sigma);
+                           fuse_sigma, ctx->d_rscr);
         HIPCHK(hipGetLastError());
     }
     const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
@@ -3612,12 +3730,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr);
         else
             hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr);
     } else {
         int K = ctx->maxK;
         size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
@@ -3972,7 +4090,7 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
 
 // Parity introspection: the assembled normal matrix of the last pint_fit_step (see
 // k_debug_gram); out holds (K_i+1)^2 + K_i doubles per instance, concatenated.
-int pint_debug_gram(pint_ctx* ctx, double* out) {
+int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
     if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     std::vector<long> off(ctx->ninst + 1, 0);
@@ -3987,7 +4105,8 @@ int pint_debug_gram(pint_ctx* ctx, double* out) {
     HIPCHK(hipMalloc(&doff, sizeof(long) * ctx->ninst));
     HIPCHK(hipMemcpy(doff, off.data(), sizeof(long) * ctx->ninst, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_debug_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
-                       ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, doff, d);
+                       ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_esum,
+                       ctx->d_eD, pre_ecorr && ctx->max_nep > 0, doff, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, sizeof(double) * off[ctx->ninst], hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

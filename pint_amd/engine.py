@@ -379,7 +379,12 @@ class Session:
 
     def add(self, lay: PulsarLayout) -> PulsarLayout:
         t, keep = pack_toas(lay)
-        rf = np.ascontiguousarray(lay.red_freq if lay.red_freq is not None else np.zeros(1))
+        if lay.red_freq is not None:  # double-double frequencies: hi[nred] then lo[nred]
+            f = np.asarray(lay.red_freq, dtype=np.longdouble)
+            fh = f.astype(np.float64)
+            rf = np.ascontiguousarray(np.concatenate([fh, (f - fh.astype(np.longdouble)).astype(np.float64)]))
+        else:
+            rf = np.zeros(2)
         rp = np.ascontiguousarray(lay.red_phi if lay.red_phi is not None else np.zeros(1))
         pid = self.L.pint_add_pulsar(self.ctx, C.byref(t), C.byref(lay.spec), L.ptr(rf), L.ptr(rp))
         if pid < 0:
@@ -644,13 +649,13 @@ class Session:
             out.append(d)
         return out
 
-    def debug_gram(self):
+    def debug_gram(self, pre_ecorr=False):
         """Stage-wise parity introspection: per instance (G, colsq) of the last fit_step, G the
-        unnormalised (K+1)^2 normal matrix [M | r]^T N^-1 [M | r] (ECORR eliminated), colsq
-        M's unweighted column sums of squares."""
+        unnormalised (K+1)^2 normal matrix [M | r]^T N^-1 [M | r] (ECORR eliminated, or
+        before the elimination with pre_ecorr), colsq M's unweighted column sums of squares."""
         sizes = [(l.K + 1) ** 2 + l.K for l in self.inst_layout]
         buf = np.empty(sum(sizes))
-        self._check(self.L.pint_debug_gram(self.ctx, L.ptr(buf)))
+        self._check(self.L.pint_debug_gram(self.ctx, 1 if pre_ecorr else 0, L.ptr(buf)))
         out = []
         for lay, b in zip(self.inst_layout, self._split(buf, sizes)):
             w = lay.K + 1

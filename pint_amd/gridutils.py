@@ -97,13 +97,53 @@ def _drop_grid_session():
         cur[1].close()
 
 
+def _fit_block(s, lay, tabs, mode, down, fitargs, want_tables):
+    """Fit one batch of grid points of the uploaded pulsar `lay` (tables: (npts, tstride)),
+    every point its own instance.  Returns (chi2, final tables or None); a point that cannot
+    be evaluated is NaN (gridutils.py:101-106), and so is every point of a batch in which no
+    point can be."""
+    from .fitter import InvalidModelParameters
+    npts = tabs.shape[0]
+    bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * npts, tables=tabs)
+    try:
+        if down:
+            rq = fitargs.get("required_chi2_decrease", 1e-2)
+            res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
+                                  max_chi2_increase=rq, min_lambda=rq, outputs=False)
+            # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
+            chi2 = np.where(res.maxiter_reached, np.nan, res.chi2)
+        else:
+            res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1), outputs=False)
+            chi2 = res.chi2
+    except InvalidModelParameters:
+        return np.full(npts, np.nan), (np.full(tabs.shape, np.nan) if want_tables else None)
+    ft = bf.final_tables_flat().reshape(npts, lay.tstride) if want_tables else None
+    return chi2, ft
+
+
+def point_tables(lay, base_table, parnames, flat, c0, c1):
+    """Parameter tables of grid points c0..c1 (flattened meshgrid order): the base model's
+    table with each grid parameter's dd pair replaced."""
+    tabs = np.tile(base_table, (c1 - c0, 1))
+    for p, vals in zip(parnames, flat):
+        v = np.asarray(vals[c0:c1], dtype=np.longdouble)
+        h = v.astype(np.float64)
+        l = (v - h.astype(np.longdouble)).astype(np.float64)
+        o = lay.offsets[p]
+        tabs[:, o] = h
+        tabs[:, o + 1] = l
+    return tabs
+
+
 def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
                executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
     """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
-    Returns (chi2 array of meshgrid shape, dict of extra parameter arrays).  `executor`,
-    `ncpu`, `chunksize` are accepted for API compatibility: the points run as one GPU batch
-    per rank instead of a process pool."""
-    from .engine import Session, build_layout, pack_table, split_ld
+    Returns (chi2 array of meshgrid shape, dict of meshgrid-shaped extra parameter arrays).
+    `executor`, `ncpu`, `chunksize` are accepted for API compatibility: the points run as one
+    GPU batch per rank instead of a process pool.  With torch.distributed initialised, rank
+    r fits the r-th contiguous block of the flattened meshgrid and the blocks are
+    all-gathered, so every rank returns the whole grid."""
+    from .engine import pack_table
     mode, down = _fit_kind(ftr)
     out, flat = grid_points(parvalues)
     shape = out[0].shape
@@ -126,30 +166,13 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
             chunk = int(max(1, min(hi - lo, GRID_BATCH_BYTES // per_pt, GRID_MAX_POINTS or hi - lo)))
             for c0 in range(lo, hi, chunk):
                 c1 = min(hi, c0 + chunk)
-                tabs = np.tile(t0, (c1 - c0, 1))
-                for p, vals in zip(parnames, flat):
-                    v = np.asarray(vals[c0:c1], dtype=np.longdouble)
-                    h = v.astype(np.float64)
-                    l = (v - h.astype(np.longdouble)).astype(np.float64)
-                    o = lay.offsets[p]
-                    tabs[:, o] = h
-                    tabs[:, o + 1] = l
-                bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * (c1 - c0), tables=tabs)
-                if down:
-                    rq = fitargs.get("required_chi2_decrease", 1e-2)
-                    res = bf.fit_downhill(maxiter=fitargs.get("maxiter", 10), required_chi2_decrease=rq,
-                                          max_chi2_increase=rq, min_lambda=rq, outputs=False)
-                    # gridutils.py:89-106: NaN on MaxiterReached, chi2 kept on StepProblem
-                    chi2[c0 - lo:c1 - lo] = np.where(res.maxiter_reached, np.nan, res.chi2)
-                else:
-                    res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1), outputs=False)
-                    chi2[c0 - lo:c1 - lo] = res.chi2
-                if extraparnames:
-                    ft = bf.final_tables_flat().reshape(c1 - c0, lay.tstride)
-                    for e in extraparnames:
-                        o = lay.offsets[e]
-                        extra[e][c0 - lo:c1 - lo] = (ft[:, o].astype(np.longdouble)
-                                                     + ft[:, o + 1].astype(np.longdouble)).astype(np.float64)
+                tabs = point_tables(lay, t0, parnames, flat, c0, c1)
+                c2, ft = _fit_block(s, lay, tabs, mode, down, fitargs, bool(extraparnames))
+                chi2[c0 - lo:c1 - lo] = c2
+                for e in extraparnames:
+                    o = lay.offsets[e]
+                    extra[e][c0 - lo:c1 - lo] = (ft[:, o].astype(np.longdouble)
+                                                 + ft[:, o + 1].astype(np.longdouble)).astype(np.float64)
         except Exception:
             _drop_grid_session()
             raise
@@ -159,3 +182,14 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     chi2_all = gather_blocks(chi2, per, npts, dist)
     extra_all = {e: gather_blocks(extra[e], per, npts, dist).reshape(shape) for e in extraparnames}
     return chi2_all.reshape(shape), extra_all
+
+
+def best_point(chi2, parnames: Sequence[str], parvalues: Sequence):
+    """The grid's best-fit point: (meshgrid index, {name: value}, chi2).  Every rank holds the
+    all-gathered grid, so the reduction is a host argmin (NaN points never win)."""
+    c = np.asarray(chi2)
+    if np.all(np.isnan(c)):
+        raise ValueError("no grid point has a chi2")
+    k = np.unravel_index(int(np.nanargmin(c)), c.shape)
+    out, _ = grid_points(parvalues)
+    return k, {p: out[j][k] for j, p in enumerate(parnames)}, float(c[k])

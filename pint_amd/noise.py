@@ -29,7 +29,9 @@ def scaled_sigma_us(model, toas) -> np.ndarray:
 
 def red_noise_freqs_weights(model, toas):
     """(f_k [nmodes], phi [2 nmodes]) — get_rednoise_freqs (noise_model.py:847) with
-    T = max(t) - min(t) of t = tdbld*86400 in longdouble, powerlaw(f) * f[0] (:780-789)."""
+    T = max(t) - min(t) of t = tdbld*86400 in longdouble, powerlaw(f) * f[0] (:780-789).
+    f_k stays longdouble, as the reference builds its basis sin(2 pi t f_k) with it
+    (noise_model.py:861-880); the device receives it as a double-double pair."""
     amp, gam, nf = model.red_noise_params()
     t = toas.tdbld * np.longdouble(86400)
     T = t.max() - t.min()
@@ -39,7 +41,7 @@ def red_noise_freqs_weights(model, toas):
     ff[1::2] = f
     fyr = 1 / 3.16e7
     phi = amp ** 2 / 12.0 / np.pi ** 2 * fyr ** (gam - 3) * ff ** (-gam)
-    return np.asarray(ff[::2], dtype=np.float64), phi * ff[0]
+    return f, phi * ff[0]
 
 
 def fourier_basis(model, toas) -> np.ndarray:
