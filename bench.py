@@ -1,13 +1,18 @@
 """Benchmark: GLS fits/s on the synthetic 68-pulsar x 10k-TOA PTA (BASELINE.json metric),
 plus chi2-grid points/s, on N MI355X GPUs of one node.
 
-One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar of a
-68-pulsar PTA, batched in one launch sequence per GPU: design matrix + residuals
-(k_eval/k_resid), Gram on FP64 MFMA (k_gram_v, + trig sums k_trig), Cholesky/solve/
-covariance (k_solve_dmx), double-double parameter update (k_apply), post-fit residuals and
-Woodbury chi2 (k_wdot/k_wsolve), with the fit outputs (steps, errors, covariances, chi2)
-copied back to the host (on a copy stream, overlapped with the kernels).  Weak scaling: rank r fits its own 68-pulsar PTA (pulsar seeds 68r .. 68r+67),
-no data-path collective; the max over ranks is the step time and value = 68 x N / step.
+One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar of a rank's
+shard, batched in one launch sequence per GPU: design matrix + residuals (k_eval/k_resid),
+Gram on FP64 MFMA (k_gram_v), Cholesky/solve/covariance (k_solve_dmx; iterative refinement
+where the condition estimate asks for it), double-double parameter update (k_apply), post-fit residuals and Woodbury
+chi2 (k_wdot/k_wsolve), with the fit outputs (steps, errors, covariances, chi2) copied back
+to the host on a copy stream, overlapped with the kernels.
+
+Sharding (pint_amd.pta): the pulsars are assigned to ranks by
+longest-processing-time on the fit cost N K^2 + 8 N P; there is no data-path collective.
+* value ("scaling": "weak"): a PTA of 68 x N pulsars (pulsar i uses seed i) over N ranks,
+  ~68 pulsars per GPU; value = 68 N / max-over-ranks step time.
+* pta_strong (N > 1): the configured 68-pulsar PTA itself split over the N ranks.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -25,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 MI355X_HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 MI355X_FP64_MFMA_PEAK_TFLOPS = 78.6  # vendor FP64 matrix peak
+SLOT_GRAM = 6                      # pint_last_timing slot of the Gram kernels
 
 
 def log(*a):
@@ -40,6 +46,7 @@ def main():
     ap.add_argument("--ntoas", type=int, default=10000)
     ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--strong", type=int, default=1, help="also time the 68-pulsar PTA split over the ranks (N > 1)")
     ap.add_argument("--j0740", type=int, default=256,
                     help="(M2, SINI) grid side of the C3/C4 J0740 legs (0 = skip)")
     args = ap.parse_args()
@@ -60,32 +67,71 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    from pint_amd.engine import Session, build_layout, pack_table
-    from pint_amd.simulation import make_pta
+    def max_over_ranks(v):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    # ---- workload: this rank's own PTA (weak scaling; pulsar i uses seed i) ----
-    mine = list(range(rank * args.npsr, (rank + 1) * args.npsr))
-    t0 = time.time()
     from pint_amd import simulation as sim
-    from pint_amd.timing_model import get_model
-    specs = []
-    for i in mine:
-        kind = "ELL1" if i % 6 in (1, 4) else ("DD" if i % 6 == 2 else "")
-        m = get_model(sim.pta_par(i, kind))
-        specs.append(dict(model=m, start=53000, end=56652, ntoas=args.ntoas, freq=[800, 1200, 1600, 2000],
-                          obs="geocenter", error_us=0.5, add_noise=True, add_correlated_noise=True, seed=i))
-    toas = sim.make_fake_toas_batch(specs)
-    items = [(sp["model"], t) for sp, t in zip(specs, toas)]
-    log(f"[rank {rank}] generated {len(items)} pulsars x {args.ntoas} TOAs in {time.time()-t0:.1f}s")
+    from pint_amd.pta import fit_cost, lpt_shard
 
-    s = Session(device=local)
+    # ---- weak scaling: a 68 x N pulsar PTA, LPT-sharded over the N ranks ----
+    ntot = args.npsr * world
+    models = [sim.pta_model(i) for i in range(ntot)]
+    costs = [fit_cost(m, n=args.ntoas) for m in models]
+    shards = lpt_shard(costs, world)
+    leg = pta_leg(shards[rank], models, args, rank, barrier, max_over_ranks, profile=True)
+    fits_per_s = ntot / (leg["dt"] / args.steps)
+    strong = None
+    if world > 1 and args.strong:
+        sh2 = lpt_shard(costs[:args.npsr], world)
+        leg2 = pta_leg(sh2[rank], models, args, rank, barrier, max_over_ranks, profile=False)
+        strong = {"metric": "GLS fits/sec, the 68-pulsar PTA split over the ranks (strong scaling)",
+                  "value": round(args.npsr / (leg2["dt"] / args.steps), 3), "unit": "fits/s",
+                  "ms_per_step": round(leg2["dt"] / args.steps * 1e3, 4),
+                  "pulsars_per_rank": [len(s) for s in sh2]}
+
+    roof = leg["roofline"]
+    grid = grid_leg(args.grid, dist, barrier, max_over_ranks) if args.grid > 0 else None
+    j0740 = j0740_legs(args.j0740, dist, barrier, max_over_ranks) if args.j0740 > 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(leg["items"][:16])
+
+    if rank == 0:
+        out = {"metric": "GLS fits/sec, 68-PSR x 10k-TOA synthetic PTA (whole node)", "value": round(fits_per_s, 3),
+               "unit": "fits/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(leg["dt"] / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f64+dd",
+               "data": "synthetic (make_fake_toas-style PTA, TOAs generated and zeroed on the GPU)",
+               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1 per GPU "
+                                      f"(a {ntot}-pulsar PTA, LPT-sharded over {world} rank(s))",
+                          "npsr": args.npsr, "npsr_total": ntot, "ntoas": args.ntoas,
+                          "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
+                          "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
+               "roofline": roof, "pta_strong": strong, "grid": grid, "j0740": j0740, "cpu_baseline": cpu}
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
+    """Time K steps (GLSFitter maxiter=1 of every pulsar in `mine`) on this rank's GPU;
+    returns the max-over-ranks wall time and, with profile, the roofline record."""
+    from pint_amd import simulation as sim
+    from pint_amd.engine import Session, build_layout, pack_table
+    t0 = time.time()
+    items = sim.make_pta(ntoas=args.ntoas, indices=mine, models=[models[i] for i in mine])
+    log(f"[rank {rank}] generated {len(items)} pulsars x {args.ntoas} TOAs in {time.time() - t0:.1f}s")
+    s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
     lays = [s.add(build_layout(m, t)) for m, t in items]
     tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
     s.set_instances(list(zip(lays, tabs0)))
     flat0 = np.concatenate(tabs0)
-    nin = len(lays)
-    ones = np.ones(nin)
-
+    ones = np.ones(len(lays))
     s.set_lazy(True)
 
     def step():
@@ -98,19 +144,17 @@ def main():
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
         return out, c2
 
-    SLOT_GRAM = 6
-    s.set_timing_mask(1 << SLOT_GRAM)  # timed region: HIP events around the Gram kernel only
+    s.set_timing_mask(1 << SLOT_GRAM)  # timed region: HIP events on the Gram dispatches only
 
     def run(nsteps):
-        """nsteps steps, pipelined two deep: step k+1 is enqueued before the host waits for
-        step k (Session.step_end / check_step), so the device does not idle while the host
-        checks a step and issues the next.  Returns the summed Gram-kernel event time."""
+        """nsteps steps pipelined two deep (Session.step_end / check_step); returns the
+        summed Gram-kernel event time."""
         kt, prev = 0.0, None
         for _ in range(nsteps):
             step()
             cur = s.step_end()
             if prev is not None:
-                s.check_step(prev)  # device status + the Gram kernel's HIP-event time
+                s.check_step(prev)
                 kt += s.timing()[SLOT_GRAM]
             prev = cur
         if prev is not None:
@@ -123,16 +167,56 @@ def main():
     t0 = time.perf_counter()
     kt_gram = run(args.steps)
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    kt_gram /= args.steps
-    ms_step = dt / args.steps * 1e3
-    # per-kernel breakdown: a separate instrumented pass (every timing slot's events on; they
-    # cost ~5 us each, so this pass is not the timed one)
+    dt = max_over_ranks(time.perf_counter() - t0)
+    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays))}
+    if profile:
+        out["roofline"] = roofline(s, lays, kt_gram / args.steps, step, args)
+    s.close()
+    return out
+
+
+def roofline(s, lays, kt_gram, step, args):
+    """Roofline record of the dominant kernel (DESIGN.md §3 defines every count used here).
+
+    k_gram_v (FP64 MFMA):
+      alg_flops   useful flops of the normal matrix it forms, per TOA row: 2 x [(P+1)(P+2)/2
+                  ([T|r]^T W [T|r], upper) + (P+1) R ([T|r]^T W F) + (P+2) (the row's DMX bin
+                  entry against [T|r] and itself) + R (DMX x F) + 2 (2 nred + 1) (the weighted
+                  trig sums C_m, S_m that give F^T W F)], P = compact timing columns, R = 2 nred;
+      exec_flops  the MFMAs it issues, counted exactly as the kernel loops them: per N-split
+                  ceil(rows / 64) chunks x 16 k-steps x (NT + 1) tiles x 2048 flop (NT = the
+                  [T|r|slots] x [T|r|slots|F] upper tiles, + the trig tile); equals the PMC
+                  SQ_INSTS_MFMA x 2048 of the profile (profiles/pmc_gram_r02.json).
+    achieved = alg_flops / event time; exec_TFLOP/s beside it."""
+    from pint_amd.pta import fit_cost  # noqa: F401
+    nsplit = s.nsplit()
+    alg = exe = 0.0
+    for l in lays:
+        vg, ns, kpv, r0 = s.vgram_layout(l)
+        if not vg:
+            continue
+        n, R, nred = l.n, 2 * l.nred, l.nred
+        P = r0
+        alg += 2.0 * n * ((P + 1) * (P + 2) / 2 + (P + 1) * R + (P + 2) + R + 2 * (2 * nred + 1))
+        ntr, ntc = (r0 + 1 + ns) // 16, kpv // 16
+        nt = ntr * ntc - ntr * (ntr - 1) // 2 + 1
+        per = -(-n // nsplit)
+        per = -(-per // 4) * 4
+        chunks = sum(-(-max(0, min(n, (q + 1) * per) - min(n, q * per)) // 64) for q in range(nsplit))
+        exe += chunks * 16.0 * nt * 2048.0
+    # bytes the evaluation kernels move per TOA (DESIGN.md §3): inputs tdb (16) + freq (8) +
+    # pos/vel/sun (72) + flags (4) + jump mask (8) + DMX ids (8) = 116 B; outputs phase hi/lo,
+    # Taylor F, delay (32 B); with the fit layout also the compact timing columns (8 P B) and
+    # the row's DMX value (8 B)
+    nrow = float(sum(l.n + 1 for l in lays))
+    pc = [s.vgram_layout(l)[3] for l in lays]
+    nbytes = {
+        "k_eval": nrow * 148.0,
+        "k_eval_M": float(sum((l.n + 1) * 148.0 + l.n * (8.0 * p + 8.0) for l, p in zip(lays, pc))),
+        "k_resid": float(sum(l.n for l in lays)) * 80.0,       # two passes of 40 B (DESIGN.md §3)
+        "k_woodbury": float(sum(l.n for l in lays)) * 32.0,    # r, 1/sigma, fundamental (cos, sin)
+    }
+    # per-kernel breakdown: a separate instrumented pass (every timing slot's events on)
     s.set_timing_mask(0xFF)
     kt = np.zeros(8)
     nprof = 3
@@ -141,123 +225,55 @@ def main():
         s.check()
         kt += s.timing()
     kt /= nprof
-    fits_per_s = args.npsr * world / (dt / args.steps)
-
-    # ---- roofline: work per launch / HIP-event time of that kernel ----
-    K = np.array([l.K for l in lays])                # timing + red-noise columns
-    P = np.array([len(l.columns) for l in lays])     # timing columns
-    N = np.array([l.n for l in lays]).astype(float)
-    R = K - P
-    vl = [s.vgram_layout(l) for l in lays]
-    # k_gram_v: MFMA tiles [T|r|DMX slots] x [T|r|slots|F] of 16x16 + the trig tile A^T B,
-    # 2048 flops per tile per 4 rows
-    tiles = []
-    for vg, ns, kpv, r0 in vl:
-        ntr, nt = (r0 + 1 + ns) // 16, kpv // 16
-        tiles.append(ntr * nt - ntr * (ntr - 1) // 2 + 1 if vg else 0)
-    tiles = np.array(tiles, dtype=float)
-    flops = {
-        "k_gram": float(np.sum(tiles * N * 512.0)),           # FP64 MFMA flops executed
-        "k_solve": float(np.sum(K.astype(float) ** 3)),       # chol K^3/3 + inverse/cov 2K^3/3
-    }
-    # the full GLS Gram the reference forms (2 N K^2, SURVEY.md 8(d) F_gram) for reference
-    gram_equiv = float(np.sum(2.0 * N * (K + 1.0) ** 2))
-    nbytes = {
-        "k_eval_M": float(np.sum(N * (120 + 8 * P))),          # SURVEY.md 8(d) B_dm
-        "k_eval": float(np.sum(N * (120 + 8))),                # B_res
-        "k_resid": float(np.sum(N * (8 * 4 + 8 * 2))),        # phase hi/lo, ftaylor, sigma in; resid out
-        "k_woodbury": float(np.sum(N * (8 * 4))),              # r, sigma, fundamental (cos, sin) in
-    }
     names = ["k_eval", "k_resid", "gram_span", "k_solve", "k_eval_M", "k_woodbury", "k_gram", "k_greduce"]
     kms = {n: float(v) for n, v in zip(names, kt)}
-    dom = max((n for n in names if n not in ("gram_span", "k_greduce")), key=lambda n: kms[n])
-    if dom == "k_gram":
-        kms[dom] = kt_gram  # the dominant kernel's time from the timed region itself
-    peaks = load_peaks()
-    if kms[dom] <= 0:  # no per-kernel events (PINT_NO_EVENTS)
-        roof = {"kernel": dom, "bound": None, "achieved": None, "peak": None, "unit": None, "frac": None}
-    elif dom in flops:
-        ach = flops[dom] / (kms[dom] * 1e-3) / 1e12
-        pk = MI355X_FP64_MFMA_PEAK_TFLOPS
-        roof = {"kernel": "k_gram_v" if dom == "k_gram" else dom, "bound": "mfma" if dom == "k_gram" else "fp64",
-                "achieved": round(ach, 3), "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4)}
-    else:
-        ach = nbytes[dom] / (kms[dom] * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4)}
-    roof["traffic"] = pmc_traffic(roof["kernel"], args)
-    roof["kernel_ms"] = {n: round(v, 4) for n, v in kms.items()}
-    roof["kernel_ms_source"] = ("k_gram: HIP events in the timed region; others: a separate instrumented pass "
-                                f"of {nprof} steps (gram_span = ecorr + Gram + reduction)")
-    roof["per_kernel"] = {}
-    for n in names:
-        if kms[n] <= 0:
-            continue
-        if n in flops:
-            roof["per_kernel"][n] = {"TFLOP/s": round(flops[n] / (kms[n] * 1e-3) / 1e12, 3)}
-        if n in nbytes:
-            roof["per_kernel"][n] = {"GB/s": round(nbytes[n] / (kms[n] * 1e-3) / 1e9, 1)}
-    if kms["k_gram"] > 0:
-        roof["gram_full_equiv_tflops"] = round(gram_equiv / (kms["k_gram"] * 1e-3) / 1e12, 2)
+    kms["k_gram"] = kt_gram  # the dominant kernel's time from the timed region itself
+    ach = alg / (kt_gram * 1e-3) / 1e12 if kt_gram > 0 else None
+    roof = {"kernel": "k_gram_v", "bound": "mfma",
+            "achieved": round(ach, 3) if ach else None, "peak": MI355X_FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / MI355X_FP64_MFMA_PEAK_TFLOPS, 4) if ach else None,
+            "traffic": pmc_value("pmc_r02.json", "k_gram_v", "hbm_bytes", args),
+            "alg_gflop_per_launch": round(alg / 1e9, 4), "exec_gflop_per_launch": round(exe / 1e9, 4),
+            "exec_tflops": round(exe / (kt_gram * 1e-3) / 1e12, 3) if kt_gram > 0 else None,
+            "exec_frac": round(exe / (kt_gram * 1e-3) / 1e12 / MI355X_FP64_MFMA_PEAK_TFLOPS, 4) if kt_gram > 0 else None,
+            "pmc_exec_gflop_per_launch": pmc_value("pmc_gram_r02.json", "k_gram_v", "mfma_gflop", args),
+            "pmc_mfma_busy_frac": pmc_value("pmc_gram_r02.json", "k_gram_v", "mfma_busy_frac", args),
+            "kernel_ms": {n: round(v, 4) for n, v in kms.items()},
+            "kernel_ms_source": ("k_gram: HIP events on its dispatches in the timed region; others: a separate "
+                                 f"instrumented pass of {nprof} steps (gram_span = Gram + reduction)")}
+    roof["per_kernel"] = {n: {"GB/s": round(b / (kms[n] * 1e-3) / 1e9, 1), "frac_hbm":
+                              round(b / (kms[n] * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4)}
+                          for n, b in nbytes.items() if kms.get(n, 0) > 0}
+    gram_equiv = float(sum(2.0 * l.n * (l.K + 1.0) ** 2 for l in lays))
+    roof["gram_full_equiv_tflops"] = round(gram_equiv / (kt_gram * 1e-3) / 1e12, 2) if kt_gram > 0 else None
+    peaks = load_json("peaks_r01.json")
     if peaks:
         roof["measured_peaks"] = peaks
-
-    # ---- chi2-grid leg (C4 shape: 256x256 (F0,F1) WLS grid of the NGC6440E fixture) ----
-    grid = None
-    if args.grid > 0:
-        grid = grid_leg(args.grid, rank, world, dist, barrier)
-
-    j0740 = None
-    if args.j0740 > 0:
-        j0740 = j0740_legs(args.j0740, rank, world, dist, barrier)
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu = cpu_baseline(items[:1])
-
-    if rank == 0:
-        out = {"metric": "GLS fits/sec, 68-PSR x 10k-TOA synthetic PTA (whole node)", "value": round(fits_per_s, 3),
-               "unit": "fits/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "f64+dd", "data": "synthetic (make_fake_toas-style, GPU-zeroed)",
-               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1 per GPU",
-                          "npsr": args.npsr, "npsr_total": args.npsr * world, "ntoas": args.ntoas,
-                          "K_cols_max": int(K.max() - 1),
-                          "parallelism": f"one PTA per GPU x{world} (weak)"},
-               "roofline": roof, "grid": grid, "j0740": j0740, "cpu_baseline": cpu}
-        print(json.dumps(out))
-    s.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return roof
 
 
-def load_peaks():
-    """Peaks measured on an MI355X by bench/peaks.hip (committed under profiles/)."""
-    f = os.path.join(ROOT, "profiles", "peaks_r01.json")
+def load_json(name):
+    f = os.path.join(ROOT, "profiles", name)
     if os.path.exists(f):
         with open(f) as fh:
             return json.load(fh)
     return None
 
 
-def pmc_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    same bench command (FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md, + WRITE_SIZE)."""
-    f = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if not os.path.exists(f):
-        return None
-    with open(f) as fh:
-        d = json.load(fh)
-    if d.get("workload") != f"pta{args.npsr}x{args.ntoas}":
+def pmc_value(fname, kernel, key, args):
+    """A per-launch PMC figure of `kernel` from the committed rocprofv3 summary of this same
+    bench workload (profiles/; HBM bytes = FETCH_SIZE x2 on gfx950 + WRITE_SIZE per
+    MI355X_MICROARCH.md)."""
+    d = load_json(fname)
+    if not d or d.get("workload") != f"pta{args.npsr}x{args.ntoas}":
         return None
     k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k.get("hbm_bytes")
+    return None if k is None else k.get(key)
 
 
-def grid_leg(side, rank, world, dist, barrier):
+def grid_leg(side, dist, barrier, max_over_ranks):
     """chi2 over a side x side (F0, F1) grid, WLSFitter per point (gridutils.py:166 parallel
     semantics), points sharded over ranks; timed over one full grid."""
-    import copy
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from golden_util import load
     from pint_amd import WLSFitter
@@ -274,14 +290,9 @@ def grid_leg(side, rank, world, dist, barrier):
     t0 = time.perf_counter()
     chi2, _ = grid_chisq(f, ("F0", "F1"), (g0, g1))
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
     return {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
-            "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 3),
+            "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 4),
             "chi2_min": float(np.nanmin(chi2))}
 
 
@@ -296,23 +307,11 @@ def j0740_data():
     toas = sim.make_fake_toas_uniform(56640, 58461, 50000, model, freq=[820.0, 1400.0], obs="geocenter",
                                       error=1.0, add_noise=True, flags={"f": "Rcvr1_2_GUPPI", "fe": "Rcvr1_2"},
                                       seed=0)
-    mjd = toas.get_mjds()
-    frozen = []
-    for n in model.dmx_params():
-        tag = n.split("_")[1]
-        r1, r2 = float(model["DMXR1_" + tag].value), float(model["DMXR2_" + tag].value)
-        if not np.any((mjd >= r1) & (mjd <= r2)):
-            model[n].frozen = True
-            frozen.append(n)
-    for n in model.mask_params("JUMP"):
-        p = model[n]
-        if len(toas.select_mask(p.key, p.key_value)) == 0:
-            p.frozen = True
-            frozen.append(n)
+    frozen = model.find_empty_masks(toas, freeze=True)
     return model, toas, frozen
 
 
-def j0740_legs(side, rank, world, dist, barrier):
+def j0740_legs(side, dist, barrier, max_over_ranks):
     """C3 and the second C4 shape on j0740_data().  C3: one
     DownhillGLSFitter(maxiter=10) fit, timed.  C4: grid_chisq over (M2, SINI) side x side,
     M2 in [0.2, 0.3] Msun, SINI = sin(86.25..88.5 deg) (profiling/bench_chisq_grid.py:33-35),
@@ -324,20 +323,16 @@ def j0740_legs(side, rank, world, dist, barrier):
     model, toas, frozen = j0740_data()
     out = {"workload": "J0740+6620 synthetic 50k TOAs (C3)", "free_params": len(model.free_params),
            "frozen_empty": len(frozen)}
-    f = DownhillGLSFitter(toas, copy.deepcopy(model))
-    try:
-        f.fit_toas(maxiter=10)  # warm-up (library load, first-call allocations)
-    except MaxiterReached:
-        pass
-    barrier()
-    f = DownhillGLSFitter(toas, copy.deepcopy(model))
-    t0 = time.perf_counter()
-    try:
-        f.fit_toas(maxiter=10)
-        conv = True
-    except MaxiterReached:
-        conv = False
-    dt = time.perf_counter() - t0
+    for rep in range(2):  # the first fit is the warm-up (library load, first-call allocations)
+        f = DownhillGLSFitter(toas, copy.deepcopy(model))
+        barrier()
+        t0 = time.perf_counter()
+        try:
+            f.fit_toas(maxiter=10)
+            conv = True
+        except MaxiterReached:
+            conv = False
+        dt = time.perf_counter() - t0
     out["downhill_gls"] = {"metric": "DownhillGLSFitter fits/sec (maxiter=10)", "value": round(1.0 / dt, 3),
                            "seconds": round(dt, 4), "converged": conv, "chi2": float(f.resids.chi2)}
     g = GLSFitter(toas, copy.deepcopy(model))
@@ -349,46 +344,123 @@ def j0740_legs(side, rank, world, dist, barrier):
     t0 = time.perf_counter()
     chi2, _ = grid_chisq(g, ("M2", "SINI"), (m2, sini))
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
     out["grid_m2_sini"] = {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1),
                            "unit": "points/s", "workload": f"J0740 50k TOAs {side}x{side} (M2,SINI) GLSFitter",
                            "seconds": round(dt, 3), "chi2_min": float(np.nanmin(chi2))}
     return out
 
 
-def cpu_baseline(items):
-    """The oracle (numpy longdouble restatement, oracle/pint_oracle.py) timed on this host
-    on a bounded sample: GLS fits of one 10k-TOA PTA pulsar, scaled to fits/s."""
-    try:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pint_oracle as O
-    except Exception as e:  # oracle missing: report, never fall back
-        return {"value": None, "error": repr(e)}
-    model, toas = items[0]
+# ---- CPU baseline: the oracle (numpy longdouble restatement) on the host's cores ---------
+_CPU_ITEMS = None
+
+
+def _cpu_init(items, root):
+    global _CPU_ITEMS
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
     try:
         from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
+        threadpool_limits(1)  # one BLAS thread per worker process
     except Exception:
-        lim = None
+        pass
+    _CPU_ITEMS = items
+
+
+def _cpu_fits(args):
+    """Worker: GLS fits (maxiter=1 + post-fit chi2) of item k for `budget` seconds."""
+    k, budget = args
+    import pint_oracle as O
+    model, toas = _CPU_ITEMS[k]
     t0 = time.perf_counter()
-    nfit = 0
+    n = 0
     while True:
         O.gls_fit_from_product_inputs(model, toas)
-        nfit += 1
-        if time.perf_counter() - t0 > 12.0 or nfit >= 200:
-            break
-    dt = time.perf_counter() - t0
-    if lim is not None:
-        lim.unregister() if hasattr(lim, "unregister") else None
-    return {"value": round(nfit / dt, 4), "unit": "fits/s", "cores": 1, "kind": "port",
-            "sample": f"{nfit} GLS fit(s) (maxiter=1 + post-fit GLS chi2) of one {toas.ntoas}-TOA PTA pulsar "
-                      f"(K={len(model.free_params)+1} + {2 * (model.red_noise_params()[2])} red-noise columns), "
-                      f"numpy longdouble oracle, BLAS limited to 1 thread, {dt:.1f} s"}
+        n += 1
+        if time.perf_counter() - t0 > budget:
+            return n
+
+
+def _cpu_grid(args):
+    """Worker: WLS fits of NGC6440E grid points (F0, F1 frozen at the point) for `budget` s."""
+    k, budget = args
+    import pint_oracle as O
+    om, ot, f0s, f1s = _CPU_ITEMS
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        j = (k * 7919 + n) % len(f0s)
+        O.grid_chisq(om, ot, ("F0", "F1"), ([f0s[j]], [f1s[j]]), gls=False)
+        n += 1
+        if time.perf_counter() - t0 > budget:
+            return n
+
+
+def cpu_baseline(items):
+    """The oracle (oracle/pint_oracle.py, numpy longdouble) timed on this host on bounded
+    samples, one process per core of the job's CPU share (at most 16 on the GPU box):
+    GLS fits of the PTA's own 10k-TOA pulsars, and WLS grid points of NGC6440E -- the GPU
+    workloads' units.  The reference's own CPU rates (measured in the build container; the
+    reference cannot travel to the GPU box) are attached from bench/reference_cpu.json."""
+    import multiprocessing as mp
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pint_oracle as O  # noqa: F401
+    except Exception as e:  # oracle missing: report, never fall back
+        return {"value": None, "error": repr(e)}
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    nproc = max(1, min(16, ncores, len(items)))
+    ctx = mp.get_context("spawn")  # never fork a process that holds a GPU context
+    # one BLAS/OpenMP thread per worker (the box exports OMP_NUM_THREADS=16: 16 workers x 16
+    # threads would oversubscribe the job's cores); the spawned workers inherit this
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in saved:
+        os.environ[k] = "1"
+    try:
+        return _cpu_baseline_pools(items, ctx, nproc, ncores)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _cpu_baseline_pools(items, ctx, nproc, ncores):
+    budget = 10.0
+    with ctx.Pool(nproc, initializer=_cpu_init, initargs=(items[:nproc], ROOT)) as pool:
+        t0 = time.perf_counter()
+        counts = pool.map(_cpu_fits, [(k, budget) for k in range(nproc)])
+        dt = time.perf_counter() - t0
+    fits = sum(counts)
+    out = {"value": round(fits / dt, 4), "unit": "fits/s", "cores": nproc, "kind": "port",
+           "sample": f"{fits} GLS fits (maxiter=1 + post-fit GLS chi2) of {nproc} of the PTA's 10k-TOA pulsars, "
+                     f"one oracle process per core (numpy longdouble, 1 BLAS thread each), {dt:.1f} s wall; "
+                     f"host cpu_count {os.cpu_count()}, job CPU share {ncores}"}
+    # grid points: NGC6440E (F0, F1) WLS fits, the grid leg's unit
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import load
+    import pint_oracle as O
+    model, toas, z, _ = load("ngc6440e")
+    om, ot = O.from_product_model(model), O.toas_from_product(toas)
+    g0 = z["grid_F0_hi"].astype(np.longdouble) + z["grid_F0_lo"]
+    g1 = z["grid_F1_hi"].astype(np.longdouble) + z["grid_F1_lo"]
+    f0s, f1s = [x.ravel() for x in np.meshgrid(g0, g1)]
+    gb = 5.0
+    with ctx.Pool(nproc, initializer=_cpu_init, initargs=((om, ot, f0s, f1s), ROOT)) as pool:
+        t0 = time.perf_counter()
+        counts = pool.map(_cpu_grid, [(k, gb) for k in range(nproc)])
+        dt = time.perf_counter() - t0
+    out["grid"] = {"value": round(sum(counts) / dt, 2), "unit": "points/s", "cores": nproc,
+                   "sample": f"{sum(counts)} NGC6440E (F0,F1) WLS grid points, {nproc} processes, {dt:.1f} s"}
+    ref = os.path.join(ROOT, "bench", "reference_cpu.json")
+    if os.path.exists(ref):
+        with open(ref) as fh:
+            out["reference_container"] = json.load(fh)
+    return out
 
 
 if __name__ == "__main__":

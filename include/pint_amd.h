@@ -210,6 +210,12 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * Every HIP timing event costs device time (~5 us each), so a timed run enables only the
  * slots it reports. */
 #define PINT_OPT_TIMING_MASK 3
+/* PINT_OPT_REFINE = 1 (default): a normal-equations solve whose condition estimate
+ * max diag(A) * max diag(A^-1) exceeds 1e8 gets one pass of iterative refinement with a
+ * double-double residual (the explicit L^-1 of the blocked solves otherwise loses ~cond(L)
+ * digits that LAPACK's cho_solve keeps); 0 skips it (grid points: their post-fit chi2 is
+ * second order in a step error along the weak directions). */
+#define PINT_OPT_REFINE 4
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max
@@ -240,8 +246,10 @@ int pint_capture_begin(pint_ctx *ctx);
 int pint_capture_end(pint_ctx *ctx);
 int pint_graph_launch(pint_ctx *ctx);
 /* Introspection: PINT_QUERY_NVGRAM = 1 returns the number of instances of the current batch
- * on the generated-Fourier path; negative status on error. */
+ * on the generated-Fourier path, PINT_QUERY_NSPLIT = 2 the Gram's N-split count (row blocks
+ * per instance); negative status on error. */
 #define PINT_QUERY_NVGRAM 1
+#define PINT_QUERY_NSPLIT 2
 int pint_query(pint_ctx *ctx, int key);
 /* Page-locked host memory for the output buffers (hipHostMalloc); NULL on failure. */
 void *pint_host_alloc(size_t bytes);

@@ -1473,7 +1473,7 @@ __device__ __forceinline__ void bstore(double* Z, const double4_t& v, int lane, 
 
 // Iterative refinement residuals r = b - A x are accumulated in double-double (two_prod +
 // dd_add, error-free): with an extended-precision residual each refinement pass contracts
-// the error by ~cond * eps, so two passes reach the correctly rounded solution of the FP64
+// the error by ~cond * eps, so one pass takes the error from ~cond * eps to ~(cond * eps)^2 of the FP64
 // system even at cond 1e12 -- below the rounding of the reference's own cho_solve.
 __device__ __forceinline__ void dd_acc(dd& s, double a, double b) { s = dd_add(s, two_prod(a, b)); }
 __device__ __forceinline__ dd dd_quad_sum(dd s) {  // sum over the 4 lanes of a lane quad
@@ -1481,7 +1481,26 @@ __device__ __forceinline__ dd dd_quad_sum(dd s) {  // sum over the 4 lanes of a 
     s = dd_add(s, dd_make(__shfl_xor(s.hi, 2, 64), __shfl_xor(s.lo, 2, 64)));
     return s;
 }
-constexpr int REFINE_PASSES = 2;
+__device__ __forceinline__ dd dd_wave_sum(dd s) {  // sum over the 64 lanes of a wave
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s = dd_add(s, dd_make(__shfl_xor(s.hi, o, 64), __shfl_xor(s.lo, o, 64)));
+    return s;
+}
+constexpr int REFINE_PASSES = 1;
+constexpr double REFINE_KAPPA = 1e8;  // refine when the condition estimate exceeds this
+template <int NW>
+__device__ double block_max(double v, double* sh) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double t = sh[0];
+#pragma unroll
+    for (int i = 1; i < NW; i++) t = fmax(t, sh[i]);
+    return t;
+}
 
 // One wave: Cholesky of the (full, symmetric) 16x16 block in registers (lane r holds row
 // r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
@@ -1625,7 +1644,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
                                                        double* __restrict__ dpars, double* __restrict__ errs,
                                                        double* __restrict__ cov, double* __restrict__ chi2lin,
                                                        double* __restrict__ sigL, int* __restrict__ status,
-                                                       int skip_dsplit, double* __restrict__ rscr) {
+                                                       int skip_dsplit, double* __restrict__ rscr, int refine) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -1707,6 +1726,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     // digits that LAPACK's triangular solves (cho_solve, fitter.py:2197) keep, and on a
     // normalised system of cond 1e12 (J0740) that is ~10x the reference's own rounding
     const int g0 = tid >> 2, sub = tid & 3;
+    double amax = 0.0, vmax = 0.0;
     for (int g = g0; g < nb * 16; g += NW * 16) {
         const int Jb = g >> 4, cc = g & 15;
         double se = 0.0;
@@ -1716,8 +1736,14 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
         }
         se += __shfl_xor(se, 1, 64);
         se += __shfl_xor(se, 2, 64);
-        if (sub == 0 && g < K) errs[I.coff + g] = sqrt(se) * inv[g];
+        if (sub == 0 && g < K) {
+            errs[I.coff + g] = sqrt(se) * inv[g];
+            vmax = fmax(vmax, se);
+            amax = fmax(amax, Aij(g, g));
+        }
     }
+    // refine only where the solve can lose digits (see k_solve_dmx)
+    const bool do_ref = refine && block_max<NW>(amax, sh) * block_max<NW>(vmax, sh) > REFINE_KAPPA;
     for (int pass = 0; pass <= REFINE_PASSES; pass++) {
         const double* rhs = pass == 0 ? bv : rv;
         for (int g = g0; g < nb * 16; g += NW * 16) {  // y = X rhs
@@ -1738,8 +1764,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
             if (sub == 0) xs[g] = (pass == 0 ? 0.0 : xs[g]) + (g < K ? sx : 0.0);
         }
         __syncthreads();
-        if (pass == REFINE_PASSES) break;
-        for (int g = g0; g < nb * 16; g += NW * 16) {  // r = b - A x, double-double
+        if (pass == REFINE_PASSES || !do_ref) break;
+        for (int g = g0; g < nb * 16; g += NW * 16) {  // r = b - A x, double-double, a lane quad per row
             dd sa = dd_make(0.0);
             if (g < K)
                 for (int j = sub; j < K; j += 4) dd_acc(sa, Aij(g, j), xs[j]);
@@ -1782,7 +1808,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        const double* __restrict__ DCS, double* __restrict__ dpars,
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                       int* __restrict__ status, int fuse_sigma, double* __restrict__ rscr) {
+                                                       int* __restrict__ status, int fuse_sigma, int refine) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -1820,6 +1846,10 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     double* ind = Dn + nbk * 16;                      // nbd*16: 1 / dense column norms
     double* inx = ind + nbd * 16;                     // nbk*16: 1 / DMX column norms
     double* isd = inx + nbk * 16;                     // nbk*16: 1 / sqrt(normalised D)
+    double* xd = isd + nbk * 16;                      // nbd*16: normalised x_d (refinement)
+    double* xx = xd + nbd * 16;                       // nbk*16: normalised x_x
+    double* rd = xx + nbk * 16;                       // nbd*16: residual r_d
+    double* rx = rd + nbd * 16;                       // nbk*16: residual r_x
     const double* Gp = Gpart + I.goff;
     const double* Sdi = Sd + I.sdoff;
     auto Gd = [&](int i, int j) {  // dense compact Gram (upper storage)
@@ -1935,10 +1965,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     __syncthreads();
     TS(4);
     // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors ----
-    double* xd = rscr + (long)inst * RSCR;  // normalised x_d, x_x and the refinement residuals
-    double* xx = xd + RSCR / 4;
-    double* rd = xx + RSCR / 4;
-    double* rx = rd + RSCR / 4;
+    double amax = 0.0, vmax = 0.0;  // max diag(A) and max diag(A^-1): the condition estimate
     for (int g = g0; g < Kd; g += NW * 16) {
         double s1 = 0.0, se = 0.0;
         for (int rr = g + sub; rr < nbd * 16; rr += 4) {
@@ -1953,6 +1980,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         if (sub == 0) {
             xd[g] = s1;
             errs[I.coff + Pd.dorig[g]] = sqrt(se) * ind[g];
+            vmax = fmax(vmax, se);
+            amax = fmax(amax, Gd(g, g) * (ind[g] * ind[g]));
         }
     }
     for (int a = g0; a < ndc; a += NW * 16) {
@@ -1970,8 +1999,14 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             const double d = Dn[a];
             xx[a] = bx[a] / d - sz * isd[a];
             errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / d + sw / d) * inx[a];
+            vmax = fmax(vmax, (1.0 + sw) / d);
+            amax = fmax(amax, d);
         }
     }
+    // refine only where the solve can lose digits: kappa >= max diag(A) max diag(A^-1)
+    // (a lower bound of cond(A)); measured, the unrefined error is ~1e-17 kappa sigma
+    // (PTA pulsars kappa 1e5..1e7: <= 3e-12 sigma; J0740 7e12: 8e-5 sigma)
+    const bool do_ref = refine && block_max<NW>(amax, sh) * block_max<NW>(vmax, sh) > REFINE_KAPPA;
     __syncthreads();
     // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
     // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
@@ -1982,22 +2017,28 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         if (i == j && mode == 1 && i >= red0) v += (ind[i] * ind[i]) / Pd.red_phi[i - red0];
         return v;
     };
-    for (int pass = 0; pass < REFINE_PASSES; pass++) {
-        for (int c = g0; c < Kd; c += NW * 16) {  // r_d = b_d - A_dd x_d - A_dx x_x (dd)
+    TS(17);
+    for (int pass = 0; do_ref && pass < REFINE_PASSES; pass++) {
+        // r_d = b_d - A_dd x_d - A_dx x_x and r_x = b_x - A_xd x_d - D x_x in double-double,
+        // a lane quad per row: every row's loads are in flight at once
+        for (int c = g0; c < Kd + ndc; c += NW * 16) {
             dd sa = dd_make(0.0);
-            for (int j = sub; j < Kd; j += 4) dd_acc(sa, Ad(c, j), xd[j]);
-            for (int a = sub; a < ndc; a += 4) dd_acc(sa, Sdi[(long)a * Kp + c] * (ind[c] * inx[a]), xx[a]);
+            if (c < Kd) {
+                for (int j = sub; j < Kd; j += 4) dd_acc(sa, Ad(c, j), xd[j]);
+                for (int a = sub; a < ndc; a += 4) dd_acc(sa, Sdi[(long)a * Kp + c] * (ind[c] * inx[a]), xx[a]);
+            } else {
+                const int a = c - Kd;
+                for (int j = sub; j < Kd; j += 4) dd_acc(sa, Sdi[(long)a * Kp + j] * (ind[j] * inx[a]), xd[j]);
+                if (sub == 0) dd_acc(sa, Dn[a], xx[a]);
+            }
             sa = dd_quad_sum(sa);
-            if (sub == 0) rd[c] = dd_to_d(dd_sub(dd_make(Gd(c, Kres) * ind[c]), sa));
-        }
-        for (int a = g0; a < ndc; a += NW * 16) {  // r_x = b_x - A_xd x_d - D x_x (dd)
-            dd sa = dd_make(0.0);
-            for (int j = sub; j < Kd; j += 4) dd_acc(sa, Sdi[(long)a * Kp + j] * (ind[j] * inx[a]), xd[j]);
-            if (sub == 0) dd_acc(sa, Dn[a], xx[a]);
-            sa = dd_quad_sum(sa);
-            if (sub == 0) rx[a] = dd_to_d(dd_sub(dd_make(bx[a]), sa));
+            if (sub == 0) {
+                if (c < Kd) rd[c] = dd_to_d(dd_sub(dd_make(Gd(c, Kres) * ind[c]), sa));
+                else rx[c - Kd] = dd_to_d(dd_sub(dd_make(bx[c - Kd]), sa));
+            }
         }
         __syncthreads();
+        TS(18);
         for (int c = g0; c < nbd * 16; c += NW * 16) {
             double sa = 0.0;
             if (c < Kd)
@@ -2007,6 +2048,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             if (sub == 0) bd[c] = c < Kd ? rd[c] - sa : 0.0;
         }
         __syncthreads();
+        TS(19);
         for (int g = g0; g < nbd * 16; g += NW * 16) {
             double sy = 0.0;
             for (int c = sub; c <= g; c += 4) sy += A[lblk(g >> 4, c >> 4) + swz(g & 15, c & 15)] * bd[c];
@@ -2015,6 +2057,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             if (sub == 0) yv[g] = sy;
         }
         __syncthreads();
+        TS(20);
         for (int g = g0; g < Kd; g += NW * 16) {
             double s1 = 0.0;
             for (int rr = g + sub; rr < nbd * 16; rr += 4) s1 += A[lblk(rr >> 4, g >> 4) + swz(rr & 15, g & 15)] * yv[rr];
@@ -2032,6 +2075,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         }
         __syncthreads();
     }
+    TS(21);
     // ---- steps (par units), chi2lin = r^T W r - b . x ----
     double bx_dot = 0.0;
     for (int g = tid; g < Kd; g += NW * 64) {
@@ -2642,6 +2686,7 @@ struct pint_ctx {
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
     int lazy = 0;
     int blocked_solve = 1;  // k_solve_blk (MFMA, blocked) vs the column-by-column k_solve
+    int refine = 1;         // PINT_OPT_REFINE: iterative refinement of ill-conditioned solves
     int nsplit = 1;
     double *d_tables = nullptr, *d_phhi = nullptr, *d_phlo = nullptr, *d_ftay = nullptr, *d_delay = nullptr;
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
@@ -3665,9 +3710,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             const int kd = mode == 0 ? ph.dev.red0c : ph.dev.Kd;
             const int nbd = (kd + 15) / 16, nbk = (ph.dev.ndc + 15) / 16, nbs = (kn + 15) / 16;
             const int blk = nbd * (nbd + 1) / 2 + nbd * nbk;
-            if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB || nbk * 16 > RSCR / 4) dmx_ok = false;
+            if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB) dmx_ok = false;
             lds_x = std::max(lds_x, sizeof(double) * ((size_t)std::max(blk, nbs * (nbs + 1) / 2) * 256 +
-                                                      (size_t)(3 * nbd + 4 * nbk) * 16));
+                                                      (size_t)(5 * nbd + 6 * nbk) * 16));
+            if (lds_x > 160 * 1024) dmx_ok = false;
         } else {
             Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
         }
@@ -3718,7 +3764,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                            fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
                            ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                           fuse_sigma, ctx->d_rscr);
+                           fuse_sigma, ctx->refine);
         HIPCHK(hipGetLastError());
     }
     const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
@@ -3730,12 +3776,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine);
         else
             hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine);
     } else {
         int K = ctx->maxK;
         size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
@@ -3882,6 +3928,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (!ctx) return PINT_E_INVALID;
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {
         ctx->timing_mask = value & 0xff;
         for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec_slot[0][k] = ctx->rec_slot[1][k] = false;
@@ -3961,6 +4008,7 @@ int pint_lognorm(pint_ctx* ctx, int gls, double* out) {
 int pint_query(pint_ctx* ctx, int key) {
     if (!ctx) return -PINT_E_INVALID;
     if (key == PINT_QUERY_NVGRAM) return ctx->n_vg;
+    if (key == PINT_QUERY_NSPLIT) return ctx->nsplit;
     ctx->err = "unknown query";
     return -PINT_E_INVALID;
 }

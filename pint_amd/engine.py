@@ -527,6 +527,10 @@ class Session:
         """Timing slots of timing() whose HIP events are recorded (each costs device time)."""
         self._check(self.L.pint_set_option(self.ctx, 3, int(mask)))
 
+    def set_refine(self, on=True):
+        """Iterative refinement of ill-conditioned solves (PINT_OPT_REFINE, default on)."""
+        self._check(self.L.pint_set_option(self.ctx, 4, 1 if on else 0))
+
     def set_vgram(self, on=True):
         """Generated-Fourier compact fit path (k_gram_v); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 2, 1 if on else 0))
@@ -534,6 +538,10 @@ class Session:
     def n_vgram(self):
         """Instances of the current batch on the generated-Fourier compact path."""
         return int(self.L.pint_query(self.ctx, 1))
+
+    def nsplit(self):
+        """The Gram's N-split count of the current batch (row blocks per instance)."""
+        return int(self.L.pint_query(self.ctx, 2))
 
     def check(self):
         self._check(self.L.pint_check(self.ctx))

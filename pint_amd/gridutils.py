@@ -82,6 +82,9 @@ def _grid_session(base, toas, gls):
         return cur[1], cur[2]
     _drop_grid_session()
     s = Session()
+    # a grid point reports its post-fit chi2, which is second order in a step error along
+    # the weak directions: the solves' iterative refinement (PINT_OPT_REFINE) buys nothing
+    s.set_refine(False)
     try:
         lay = s.add(build_layout(base, toas, use_gls_basis=gls))
     except Exception:

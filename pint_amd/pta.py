@@ -24,9 +24,9 @@ STATUS_CODES = {"ok": 0, "converged": 1, "MaxiterReached": 2, "StepProblem": 3, 
 STATUS_NAMES = {v: k for k, v in STATUS_CODES.items()}
 
 
-def fit_cost(model, toas) -> float:
+def fit_cost(model, toas=None, n: Optional[int] = None) -> float:
     """Cost of one fit: N K^2 (Gram) + 8 N P (design matrix), K = P + 2 nred."""
-    n = toas.ntoas
+    n = toas.ntoas if toas is not None else n
     P = len(model.free_params) + 1
     nred = model.red_noise_params()[2] if "PLRedNoise" in model.components else 0
     K = P + 2 * nred

@@ -260,15 +260,26 @@ GAMMA 0.0
     return par
 
 
-def make_pta(npsr: int = 68, ntoas: int = 10000, ndmx: int = 100, seed0: int = 0):
-    """The C5 synthetic PTA: about 1/3 ELL1 and 1/6 DD binaries."""
+def pta_kind(i: int) -> str:
+    """Binary model of PTA pulsar i: about 1/3 ELL1 and 1/6 DD."""
+    return "ELL1" if i % 6 in (1, 4) else ("DD" if i % 6 == 2 else "")
+
+
+def pta_model(i: int, ndmx: int = 100):
     from .timing_model import get_model
+    return get_model(pta_par(i, pta_kind(i), ndmx=ndmx))
+
+
+def make_pta(npsr: int = 68, ntoas: int = 10000, ndmx: int = 100, seed0: int = 0, indices=None, models=None):
+    """The C5 synthetic PTA (pulsar i uses seed i), or the pulsars `indices` of it (a rank's
+    shard): every pulsar's data depends on its own index only."""
+    idx = list(indices) if indices is not None else list(range(seed0, seed0 + npsr))
     specs = []
-    for i in range(npsr):
-        kind = "ELL1" if i % 6 in (1, 4) else ("DD" if i % 6 == 2 else "")
-        m = get_model(pta_par(seed0 + i, kind, ndmx=ndmx))
+    for k, i in enumerate(idx):
+        m = models[k] if models is not None else pta_model(i, ndmx)
         specs.append(dict(model=m, start=53000, end=56652, ntoas=ntoas, freq=[800, 1200, 1600, 2000],
-                          obs="geocenter", error_us=0.5, add_noise=True, add_correlated_noise=True,
-                          seed=seed0 + i))
+                          obs="geocenter", error_us=0.5, add_noise=True, add_correlated_noise=True, seed=i))
+    if not specs:
+        return []
     toas = make_fake_toas_batch(specs)
     return [(sp["model"], t) for sp, t in zip(specs, toas)]

@@ -18,3 +18,4 @@ for it in range(2):
     print("phases us:", np.round(np.diff(out[:9]), 2), "total", round(out[8], 2))
     print("  diag factor %.2f us" % (out[10]-out[9]))
     print("  chol: diag0 %.2f barrier %.2f panel0 %.2f trail0 %.2f | rest-of-chol %.2f | inv step1 %.2f rest %.2f" % tuple(np.diff(np.concatenate([[out[2]], out[10:17]]))))
+    print("  refine: residual %.2f b'' %.2f y %.2f update %.2f | steps %.2f" % tuple(np.diff(np.concatenate([[out[17]], out[18:22], [out[5]]]))))
