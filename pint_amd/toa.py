@@ -38,6 +38,8 @@ class TOAs:
             self.arrays["is_bary"] = np.zeros(n, dtype=np.uint8)
         self.tzr = tzr
         self.name = name
+        self.ephem = None   # the host preparation's ephemeris / clock chain, when known
+        self.clock = None   # (update_model writes them into the model as EPHEM / CLOCK)
         self._uid = id(self)
 
     # -- reference-like accessors ------------------------------------------------------
