@@ -39,7 +39,7 @@ struct PsrDev {
     const pint_spec_t* spec;
     const double* red_freq;  // 2 nred: the frequencies as double-double, hi[nred] then lo[nred]
     const double* red_phi;   // 2*nred
-    const double* red_cs;    // n x 2: (cos, sin) of the red-noise fundamental per TOA (k_redbase)
+    const double* red_cs;    // n x 4: (cos, sin) of theta and of 8 theta, theta = 2 pi t f_1 (k_redbase)
     const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trigu)
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
@@ -781,9 +781,12 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
 // ---------------------------------------------------------------------------------
 constexpr int VTRIG = 64;   // trig sums per kind: C_m, S_m weighted, U_m, V_m unweighted (m < 64)   // trig sums m = 0..63 (nred <= 31)
 constexpr int VMAXR0 = 48;  // timing columns + residual staged from M (<= 3 row tiles)
-constexpr int VMAXKP = 144; // widest k_gram_v LDS tile [T | r | slots | F] (9 column tiles)
+constexpr int VMAXKP = 112; // widest k_gram_v LDS tile [T | r | slots | F] (7 column tiles: two
+                            // row blocks of VMAXKP + 33 columns fit the 160 KB of LDS)
 constexpr int VCH = 64;     // k_gram_v rows per chunk
-constexpr int VW = 4;       // k_gram_v waves per workgroup
+constexpr int GW = 4;       // k_gram_v waves per workgroup (one per SIMD)
+constexpr int GVB = 1;      // k_gram_v LDS row-block buffers (1: two workgroups per CU)
+constexpr int GWG = 2;      // k_gram_v workgroups per CU
 constexpr int VTG = 4;      // k_gram_v tiles per round of the cross-wave reduction
 
 // sin/cos of 2 pi frac(x) for a phase x in cycles (double-double argument reduction)
@@ -826,29 +829,83 @@ __device__ __forceinline__ int vg_cidx(int p, int r0, int Kd) {
     return p < r0 ? p : (p == r0 ? Kd : (p <= Kd ? p - 1 : p));
 }
 
-// k_gram_v: one VW-wave workgroup per (N-split, instance).  Chunks of VCH = 64 rows are
-// staged in LDS as the whitened row block [T | r | DMX slots | F] (column-major, stride
-// VCH+2), one row per lane: wave w stages the timing columns w, w + VW, ... and generates
-// its share of the Fourier harmonics from the row's fundamental (k_redbase) by rotation;
-// wave 0 also stages the residual and the row's DMX slot entry (the slot block is zero
-// except one entry per row, so only the previous and the new entry of the row are
-// rewritten).  Each wave then takes 16 rows of the chunk
-// and accumulates ALL the tiles (row tiles < ntr x column tiles >= row tile) of its rows:
-// per 4-row k-step it reads NTR + nt operands and issues up to NT independent
-// v_mfma_f64_16x16x4f64.  The waves' partial tiles are summed through LDS at the end.
+// p ? a : b as a per-lane value: the compiler turns a select between two store addresses
+// on a wave-uniform condition into branches, which is what the staging must not have
+__device__ __forceinline__ int vsel(bool p, int a, int b) {
+    int r = p ? a : b;
+    asm("" : "+v"(r));
+    return r;
+}
+
+// a pointer in the global address space (loads through it are global_load, not flat_load)
+template <typename T>
+using gptr = const T __attribute__((address_space(1)))*;
+
+// (experiment) per-workgroup phase timestamps of k_gram_v
+__device__ unsigned long long g_gvts[4096 * 5];
+#define GVTS(k) do { const int b_ = blockIdx.y * gridDim.x + blockIdx.x; \
+    if ((dbg & 8) && threadIdx.x == 0 && b_ < 4096) g_gvts[b_ * 5 + k] = (k) == 4 ? (unsigned long long)__smid() : __builtin_amdgcn_s_memrealtime(); } while (0)
+
+// e^{i k theta} from e^{i theta} for a wave-uniform 0 <= k < 8: scalar branches on k's bits,
+// at most two squarings and two products
+__device__ __forceinline__ void cpow_u8(double c1, double s1, int k, double& c, double& s) {
+    c = 1.0;
+    s = 0.0;
+    if (k & 1) {
+        c = c1;
+        s = s1;
+    }
+    if (k & 6) {
+        double bc = c1, bs = s1;
+        rot(bc, bs, c1, s1);  // e^{2 i theta}
+        if (k & 2) rot(c, s, bc, bs);
+        if (k & 4) {
+            rot(bc, bs, bc, bs);  // e^{4 i theta}
+            rot(c, s, bc, bs);
+        }
+    }
+}
+
+// k_gram_v: one GW-wave workgroup per (N-split, instance), GWG workgroups per CU.  Chunks of
+// VCH = 64 rows are staged in LDS as the whitened row block [T | r | DMX slots | F | A | B]
+// (column-major, stride VCH+2), one row per lane: wave w stages the timing columns w, w + GW,
+// ..., the trig-block harmonics a = w, w + GW (A: e^{i a theta}, B: e^{i 8a theta}) and from
+// each A harmonic the Fourier harmonics a + 1 + 8u, by short powers and rotations of the row's
+// e^{i theta}, e^{i 8 theta} (k_redbase) that carry the weight along; the residual and the
+// row's DMX slot entry (the slot block is zero except one entry per row, so only the previous
+// and the new entry of the row are rewritten) come with wave 0's share.  Each wave then takes
+// 16 rows of the chunk (four 4-row k-steps) and accumulates ALL the tiles (row tiles < ntr x
+// column tiles >= row tile) of its rows with v_mfma_f64_16x16x4f64, plus the trig tile A^T B;
+// the tiles whose rows and columns are all DMX slots hold only the bins' DD, which k_greduce
+// forms from the TOAs, and are skipped.
+// Measured on gfx950 (bench/coissue_probe.hip, bench/valu_probe.hip): an FP64 MFMA holds its
+// SIMD's vector issue for its whole 64 cycles, and a dependent FP64 vector op has ~40 cycles
+// of latency.  So staging and MFMAs cannot overlap within a SIMD; the layout minimises their
+// sum and hides latencies with the second workgroup: with one LDS buffer each (GVB = 1) two
+// workgroups share a CU, one's staging, barriers, loads, prologue and epilogue fill the
+// other's gaps (0.125 ms on the bench PTA; one 8-wave double-buffered workgroup per CU:
+// 0.15 ms).  The row data of chunk c+1 is loaded into registers while chunk c is in the MFMAs.
+// Unused columns go to a dummy LDS column (no branches in the staging).  The waves' partial
+// tiles are summed through LDS at the end.  (Built with MFMA accumulators in VGPRs: in AGPRs
+// the loop-carried tiles were copied out and back every chunk.)
 template <int NTR, int NTC>
-__global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+__global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                     const double* __restrict__ M, const double* __restrict__ rtime,
                                                     const double* __restrict__ dmxv, int nsplit,
                                                     double* __restrict__ Gpart, double* __restrict__ Sdp,
-                                                    double* __restrict__ colsq, double* __restrict__ TSp) {
+                                                    double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
     extern __shared__ double lds[];
-    constexpr int NTH = VW * 64;
+    constexpr int NTH = GW * 64;
     constexpr int CH = VCH;
     constexpr int CS = CH + 2;  // column stride (= 2 mod 32 doubles)
-    constexpr int QL = (VMAXR0 + VW - 1) / VW;  // timing columns staged per lane (bound)
+    constexpr int QL = (16 * NTR + GW - 1) / GW;  // timing columns staged per lane (r0 < 16 NTR)
     constexpr int NT = NTR * NTC - NTR * (NTR - 1) / 2;
-    constexpr int KS = CH / 4 / VW;  // k-steps per wave per chunk
+    constexpr int KS = CH / 4 / GW;  // k-steps per wave per chunk
+    constexpr int TA = 8 / GW;  // trig-block harmonics per wave
+    constexpr int HMAX = 4;     // Fourier harmonics per A harmonic (a + 1 + 8u < 32)
+    static_assert(8 % GW == 0 && KS >= 1 && (GVB == 1 || GVB == 2), "k_gram_v layout");
+    GVTS(0);
+    GVTS(4);
     const InstDev I = insts[blockIdx.y];
     const int split = blockIdx.x;
     const PsrDev& Pd = psrs[I.psr];
@@ -860,9 +917,10 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), B = [cos 8b theta |
     // sin 8b theta]/sigma (b < 8): the tile A^T B holds every C_m, S_m (weighted), m = a + 8b
     // < 64 -- F^T W F (k_greduce).  The unweighted sums for the Fourier column norms depend
-    // on the TOAs only (PsrDev::trigU, formed at upload).
-    const int tA = Kpv, tB = Kpv + 16, Kpt = Kpv + 32;
-    double* Ts = lds;       // [Kpt][CS] whitened rows
+    // on the TOAs only (PsrDev::trigU, formed at upload).  DUM: the write-only dummy column.
+    const int tA = Kpv, tB = Kpv + 16, DUM = Kpv + 32, Kpt = Kpv + 33;
+    double* const Tb0 = lds;
+    double* const Tb1 = lds + (GVB - 1) * Kpt * CS;
     long i0, i1;
     split_rows(n, nsplit, split, i0, i1);
     const double* Mi = M + I.moff;
@@ -870,91 +928,94 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     const double* xv = dmxv + I.ooff;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    static_assert(VW == 4, "the trig blocks give each wave two harmonics of A and of B");
     double4_t acc[NT], accW = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
-    for (int k = tid; k < Kpt * CS; k += NTH) Ts[k] = 0.0;  // slot and padding columns stay 0
     double csq[QL];  // sums of squares of this wave's timing columns (lanes = rows)
 #pragma unroll
     for (int q = 0; q < QL; q++) csq[q] = 0.0;
-    // Fourier harmonics of this wave
-    const int hper = (nred + VW - 1) / VW;
-    const int hb = wave * hper, he = std::min(nred, (wave + 1) * hper);
-    int slot_prev = -1;  // wave 0: the LDS slot column of this lane's previous row
-    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0;
+    const bool w0 = wave == 0;
+    int sp0 = -1, sp1 = -1;  // per buffer: the slot column of this lane's row of two chunks ago
+    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, c8_n = 1.0, s8_n = 0.0;
     double st[QL];
     int d_n = -1;
     bool ok_n = false;
-    auto load = [&](long c0) {
+    auto load = [&](long c0) {  // the next chunk's row data -> registers (clamped, no branches)
         long row = c0 + lane;
         ok_n = row < i1;
-        if (!ok_n) row = i1 - 1;
-        w_n = Pd.isig[row];
-        if (wave == 0) {
-            r_n = ri[row];
-            x_n = xv[row];
-            d_n = Pd.drow[row];
-        }
-        if (nred > 0) {
-            c1_n = Pd.red_cs[2 * row];
-            s1_n = Pd.red_cs[2 * row + 1];
-        }
+        row = ok_n ? row : i1 - 1;
+        // (global-address-space loads: through generic pointers they would be flat loads,
+        // which also count against lgkmcnt, so every LDS wait would wait for them too)
+        w_n = ((gptr<double>)Pd.isig)[row];
+        r_n = ri[row];
+        x_n = xv[row];
+        d_n = ((gptr<int>)Pd.drow)[row];
+        const double4_t z = ((gptr<double4_t>)Pd.red_cs)[row];
+        c1_n = z[0];
+        s1_n = z[1];
+        c8_n = z[2];
+        s8_n = z[3];
 #pragma unroll
         for (int q = 0; q < QL; q++) {
-            const int c = wave + VW * q;
-            if (c < r0) st[q] = Mi[(long)c * n + row];
+            const int c = wave + GW * q;
+            st[q] = Mi[(long)(c < r0 ? c : 0) * n + row];
         }
     };
-    if (i0 < i1) load(i0);
-    for (long c0 = i0; c0 < i1; c0 += CH) {
-        __syncthreads();  // the previous chunk's MFMAs are done with the LDS tile
-        {
-            const double iw = ok_n ? w_n : 0.0;
+    auto stage = [&](double* Ts, int& sp) {  // registers -> whitened row block in LDS
+        const double iw = ok_n ? w_n : 0.0;
+        double* col = Ts + lane;
 #pragma unroll
-            for (int q = 0; q < QL; q++) {
-                const int c = wave + VW * q;
-                if (c < r0) {
-                    Ts[c * CS + lane] = st[q] * iw;
-                    if (ok_n) csq[q] += st[q] * st[q];
-                }
-            }
-            if (nred > 0) {  // trig blocks: harmonics a = 2 wave, 2 wave + 1 and 8a of them
+        for (int q = 0; q < QL; q++) {
+            const int c = wave + GW * q;
+            const int cc = vsel(c < r0, c, DUM);
+            col[cc * CS] = st[q] * iw;
+            csq[q] += (cc != DUM && ok_n) ? st[q] * st[q] : 0.0;
+        }
+        {  // residual and DMX slot entry (wave 0's share; the other waves write DUM)
+            col[vsel(w0, r0, DUM) * CS] = r_n * iw;
+            const int sl = (ok_n && d_n >= 0) ? d_n % NS : -1;
+            col[vsel(w0 && sp >= 0, s0 + sp, DUM) * CS] = 0.0;
+            col[vsel(w0 && sl >= 0, s0 + sl, DUM) * CS] = x_n * iw;
+            sp = sl;
+        }
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const int a = 2 * wave + u;
-                    double c, sn;
-                    cpow(c1_n, s1_n, a, c, sn);
-                    Ts[(tA + a) * CS + lane] = c * iw;
-                    Ts[(tA + 8 + a) * CS + lane] = sn * iw;
-                    cpow(c1_n, s1_n, 8 * a, c, sn);
-                    Ts[(tB + a) * CS + lane] = c * iw;
-                    Ts[(tB + 8 + a) * CS + lane] = sn * iw;
-                }
-            }
-            if (wave == 0) {
-                Ts[r0 * CS + lane] = r_n * iw;
-                const int sl = (ok_n && d_n >= 0) ? d_n % NS : -1;
-                if (slot_prev >= 0) Ts[(s0 + slot_prev) * CS + lane] = 0.0;
-                if (sl >= 0) Ts[(s0 + sl) * CS + lane] = x_n * iw;
-                slot_prev = sl;
-            }
-            if (hb < he) {
-                double c, s;
-                cpow(c1_n, s1_n, hb + 1, c, s);
-                double* dst = Ts + (f0 + 2 * hb) * CS + lane;
-                for (int h = hb; h < he; h++, dst += 2 * CS) {
-                    dst[0] = s * iw;
-                    dst[CS] = c * iw;
-                    rot(c, s, c1_n, s1_n);
-                }
+        for (int j = 0; j < TA; j++) {
+            // trig blocks: harmonic a of A and 8a of B, a = wave + GW j (weighted: the
+            // rotations below are linear, so they carry the weight along)
+            const int a = wave + GW * j;
+            double ca, sa, cb, sb;
+            cpow_u8(c1_n, s1_n, a, ca, sa);
+            cpow_u8(c8_n, s8_n, a, cb, sb);
+            ca *= iw;
+            sa *= iw;
+            col[(tA + a) * CS] = ca;
+            col[(tA + 8 + a) * CS] = sa;
+            col[(tB + a) * CS] = cb * iw;
+            col[(tB + 8 + a) * CS] = sb * iw;
+            // Fourier harmonics a + 1 + 8u (<= nred): from the A harmonic by one rotation by
+            // e^{i theta}, then by e^{i 8 theta}
+            double c = ca, s = sa;
+            rot(c, s, c1_n, s1_n);
+#pragma unroll
+            for (int u = 0; u < HMAX; u++) {
+                const int h = a + 8 * u;  // harmonic h + 1 -> columns f0 + 2h (sin), +1 (cos)
+                const int cs = vsel(h < nred, f0 + 2 * h, DUM);
+                col[cs * CS] = s;
+                col[(cs + (cs != DUM)) * CS] = c;
+                if (u + 1 < HMAX) rot(c, s, c8_n, s8_n);
             }
         }
-        __syncthreads();
-        if (c0 + CH < i1) load(c0 + CH);  // prefetch the next chunk (overlaps the MFMAs)
+    };
+    auto mfma = [&](const double* Ts) {
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
-            const double* Tr = Ts + (lane & 15) * CS + (wave * KS + ks) * 4 + (lane >> 4);
+            // the row offset of this k-step is laundered through an empty asm so the
+            // compiler cannot pair reads of consecutive k-steps (4 doubles apart) into
+            // ds_read2_b64: that form is serviced as 16-lane groups banked mod 32, where the
+            // column stride CS = 66 puts lanes c and c + 8 on one bank (2-way conflict)
+            int roff = (wave * KS + ks) * 4;
+            asm volatile("" : "+v"(roff));
+            const double* Tr = Ts + (lane & 15) * CS + (lane >> 4) + roff;
             double a[NTR], b[NTC];
 #pragma unroll
             for (int t = 0; t < NTR; t++) a[t] = Tr[t * 16 * CS];
@@ -964,18 +1025,54 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
 #pragma unroll
             for (int ti = 0; ti < NTR; ti++) {
 #pragma unroll
-                for (int tj = ti; tj < NTC; tj++, k++)
+                for (int tj = ti; tj < NTC; tj++, k++) {
+                    // rows and columns all DMX slots (f0 = 16 NTR): only the DD diagonal
+                    if (ti > 0 && tj < NTR && ti * 16 >= s0) continue;
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
+                }
             }
-            // trig tile, unconditional (zero in LDS without red noise): no branch, and its
-            // operand reads share the step's LDS wait
+            // trig tile, unconditional (zero in LDS without red noise)
             accW = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], Tr[tB * CS], accW, 0, 0, 0);
         }
+    };
+    const long nch = i1 > i0 ? (i1 - i0 + CH - 1) / CH : 0;
+    if (nch > 0) load(i0);  // in flight while the buffers are zeroed
+    for (int k = tid; k < GVB * Kpt * CS; k += NTH) lds[k] = 0.0;  // slot and padding columns stay 0
+    __syncthreads();
+    if constexpr (GVB == 2) {
+        if (nch > 0) {
+            stage(Tb0, sp0);
+            load(i0 + CH);
+        }
+        __syncthreads();
+        GVTS(1);
+        for (long c = 0; c < nch; c++) {
+            const bool odd = c & 1;
+            // chunk c+1 into the other buffer (past the last chunk: rows with iw = 0, never read)
+            int sp = odd ? sp0 : sp1;
+            if (!(dbg & 4)) stage(odd ? Tb0 : Tb1, sp);
+            if (odd) sp0 = sp;
+            else sp1 = sp;
+            if (!(dbg & 1)) load(i0 + (c + 2) * CH);
+            if (!(dbg & 2)) mfma(odd ? Tb1 : Tb0);
+            __syncthreads();
+        }
+    } else {
+        // one buffer, two workgroups per CU: one's staging and barriers fill the other's gaps
+        GVTS(1);
+        for (long c = 0; c < nch; c++) {
+            if (!(dbg & 4)) stage(Tb0, sp0);
+            if (!(dbg & 1)) load(i0 + (c + 1) * CH);  // past the last chunk: clamped, unused
+            __syncthreads();
+            if (!(dbg & 2)) mfma(Tb0);
+            __syncthreads();
+        }
     }
+    GVTS(2);
     // timing-column sums of squares of this split (normalize_designmatrix)
 #pragma unroll
     for (int q = 0; q < QL; q++) {
-        const int c = wave + VW * q;
+        const int c = wave + GW * q;
         if (c < r0) {
             const double v = wave_sum(csq[q]);
             if (lane == 0) colsq[(I.coff + c) * nsplit + split] = v;
@@ -988,7 +1085,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
     double* Sp = Sdp + I.vgoff + (long)split * NS * SW;
     auto cidx = [&](int p) { return p < r0 ? p : (p == r0 ? Kd : r0 + (p - f0)); };
     constexpr int TG = NT < VTG ? NT : VTG;
-    double* red = lds;  // [VW][TG][256] (the host sizes LDS for it)
+    double* red = lds;  // [GW][TG][256] (the host sizes LDS for it)
     int k = 0;
 #pragma unroll
     for (int ti = 0; ti < NTR; ti++) {
@@ -1005,7 +1102,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
                     const int gg = e >> 8, q = (e >> 6) & 3, ln = e & 63;
                     double v = 0.0;
 #pragma unroll
-                    for (int w = 0; w < VW; w++) v += red[((w * TG + gg) * 4 + q) * 64 + ln];
+                    for (int w = 0; w < GW; w++) v += red[((w * TG + gg) * 4 + q) * 64 + ln];
                     int tt = kbase + gg, r_ = 0;  // tile (r_, r_ + tt) of the row-major list
                     while (tt >= NTC - r_) { tt -= NTC - r_; r_++; }
                     const int tJ_ = r_ + tt;
@@ -1019,7 +1116,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
                     } else if (!rs) {
                         Sp[(long)(pc - s0) * SW + cidx(pr)] = v;            // DMX x [T|r]
                     } else if (cs) {
-                        if (pr == pc) Sp[(long)(pr - s0) * SW + Kd + 1] = v;  // DD
+                        // DMX x DMX: diagonal, DD (k_greduce forms it from the TOAs)
                     } else {
                         Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F
                     }
@@ -1032,11 +1129,11 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
 #pragma unroll
         for (int q = 0; q < 4; q++) red[(wave * 4 + q) * 64 + lane] = accW[q];
         __syncthreads();
-        double* tsum = red + VW * 256;  // [256]
+        double* tsum = red + GW * 256;  // [256]
         for (int e = tid; e < 256; e += NTH) {
             double v = 0.0;
 #pragma unroll
-            for (int w = 0; w < VW; w++) v += red[w * 256 + e];
+            for (int w = 0; w < GW; w++) v += red[w * 256 + e];
             tsum[e] = v;
         }
         __syncthreads();
@@ -1049,6 +1146,7 @@ __global__ __launch_bounds__(VW * 64, 2) void k_gram_v(const PsrDev* __restrict_
             out[VTRIG + m] = tsum[tix(8 + a, b)] + tsum[tix(a, 8 + b)];  // S_m
         }
     }
+    GVTS(3);
 }
 
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
@@ -1058,33 +1156,40 @@ __global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __res
                           double f1_lo, double* __restrict__ cs) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double s, c;
-    dd_sincos_cyc(dd_mul(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), dd_make(f1, f1_lo)), &s, &c);
-    cs[2 * i] = c;
-    cs[2 * i + 1] = s;
+    const dd x = dd_mul(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), dd_make(f1, f1_lo));
+    double s, c, s8, c8;
+    dd_sincos_cyc(x, &s, &c);
+    dd_sincos_cyc(dd_make(8.0 * x.hi, 8.0 * x.lo), &s8, &c8);  // 8 theta: exact scaling of the dd phase
+    cs[4 * i] = c;
+    cs[4 * i + 1] = s;
+    cs[4 * i + 2] = c8;
+    cs[4 * i + 3] = s8;
 }
 
 // k_trigu: the unweighted trig sums U_m, V_m (m < 64) over the pulsar's TOAs, from which
 // k_greduce forms the Fourier column norms (sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2).
 // They depend on the TOAs only, so they are formed once at upload: grid = row blocks of
-// TRIGU_R rows, thread m (cos) / 64 + m (sin) per block, partials summed in block order by
-// k_trigu_sum (one thread per sum: short row blocks keep its serial chain short).
-constexpr int TRIGU_R = 64;
+// TRIGU_R rows (short, so the grid fills the chip), thread m (cos) / 64 + m (sin) per block;
+// k_trigu_sum then adds the block partials of each sum, one workgroup per sum, in a fixed
+// tree order (deterministic).
+constexpr int TRIGU_R = 16;
 __global__ __launch_bounds__(128) void k_trigu(const double* __restrict__ cs, int n, double* __restrict__ part) {
     const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
     const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);
     double acc = 0.0;
     for (int i = i0; i < i1; i++) {
         double c, sn;
-        cpow(cs[2 * i], cs[2 * i + 1], m, c, sn);
+        cpow(cs[4 * i], cs[4 * i + 1], m, c, sn);
         acc += kind ? sn : c;
     }
     part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
 }
-__global__ __launch_bounds__(128) void k_trigu_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_trigu_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
+    __shared__ double sh[4];
     double acc = 0.0;
-    for (int b = 0; b < nb; b++) acc += part[(long)b * 128 + threadIdx.x];
-    out[threadIdx.x] = acc;
+    for (int b = threadIdx.x; b < nb; b += 256) acc += part[(long)b * 128 + blockIdx.x];
+    acc = block_sum<4>(acc, sh);
+    if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
 // k_tsum: k_gram_v's per-split trig-sum partials of an instance summed in a fixed order
@@ -1141,19 +1246,25 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         per = (per + 3) / 4 * 4;
         const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
         const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
-        for (int c = threadIdx.x; c <= Kc + 1; c += blockDim.x) {
+        for (int c = threadIdx.x; c <= Kc; c += blockDim.x) {
             double v = 0.0;
             for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
-            if (c <= Kc) Sd[I.sdoff + (long)a * Kp + c] = v;
-            else DD[I.ddoff + a] = v;
+            Sd[I.sdoff + (long)a * Kp + c] = v;
         }
-        double q2 = 0.0;  // DCS = sum x^2 over the bin
+        // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
+        // square norm is the bin's only DMX x DMX entry: k_gram_v skips those tiles)
+        double q2 = 0.0, qw = 0.0;
         for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-            const double xx = dmxv[I.ooff + i];
+            const double xx = dmxv[I.ooff + i], xw = xx * Pd.isig[i];
             q2 += xx * xx;
+            qw += xw * xw;
         }
         q2 = block_sum<4>(q2, sh);
-        if (threadIdx.x == 0) DCS[I.ddoff + a] = q2;
+        qw = block_sum<4>(qw, sh);
+        if (threadIdx.x == 0) {
+            DCS[I.ddoff + a] = q2;
+            DD[I.ddoff + a] = qw;
+        }
         return;
     }
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2396,9 +2507,10 @@ __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, c
                 r1 += wr;
             }
             if (act) {
-                const double c1 = Pd.red_cs[2 * i], s1 = Pd.red_cs[2 * i + 1];
+                const double c1 = Pd.red_cs[4 * i], s1 = Pd.red_cs[4 * i + 1];
                 double sn, cs;
-                cpow(c1, s1, h0 + 1, cs, sn);
+                cpow(Pd.red_cs[4 * i + 2], Pd.red_cs[4 * i + 3], wave, cs, sn);  // e^{i 8w theta}
+                rot(cs, sn, c1, s1);                                             // e^{i (8w+1) theta}
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     a[2 * u] += sn * wr;
@@ -2687,6 +2799,7 @@ struct pint_ctx {
     int lazy = 0;
     int blocked_solve = 1;  // k_solve_blk (MFMA, blocked) vs the column-by-column k_solve
     int refine = 1;         // PINT_OPT_REFINE: iterative refinement of ill-conditioned solves
+    int gvdbg = 0;          // (experiment) k_gram_v phases switched off
     int nsplit = 1;
     double *d_tables = nullptr, *d_phhi = nullptr, *d_phlo = nullptr, *d_ftay = nullptr, *d_delay = nullptr;
     double *d_M = nullptr, *d_rt = nullptr, *d_rp = nullptr, *d_chi2 = nullptr, *d_chi2lin = nullptr;
@@ -2995,7 +3108,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
     rc |= upload(ctx, ph, red_freq, (size_t)2 * spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
-    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * n, d.red_cs);
+    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)4 * n, d.red_cs);
     if (!rc && spec->nred > 0) {
         hipLaunchKernelGGL(k_redbase, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, d.tdb_hi, d.tdb_lo, n,
                            red_freq[0], red_freq[spec->nred], (double*)d.red_cs);
@@ -3007,7 +3120,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         double* part = nullptr;
         HIPCHK(hipMalloc((void**)&part, sizeof(double) * 128 * std::max(1, nb)));
         hipLaunchKernelGGL(k_trigu, dim3(nb), dim3(128), 0, ctx->stream, d.red_cs, n, part);
-        hipLaunchKernelGGL(k_trigu_sum, dim3(1), dim3(128), 0, ctx->stream, part, nb, (double*)d.trigU);
+        hipLaunchKernelGGL(k_trigu_sum, dim3(128), dim3(256), 0, ctx->stream, part, nb, (double*)d.trigU);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(ctx->stream));
         HIPCHK(hipFree(part));
@@ -3169,8 +3282,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     int maxsplit = (maxN + 4 * GCH - 1) / (4 * GCH);
     if (maxsplit < 1) maxsplit = 1;
-    // Resident Gram workgroups per CU: k_gram runs one 1024-thread workgroup per CU,
-    // k_gram_v two 256-thread ones (launch bounds, LDS); the batch's majority path decides.
+    // Resident Gram workgroups per CU: k_gram runs one per CU, k_gram_v GWG; the batch's
+    // majority path decides
     long nvgc = 0;
     for (int k = 0; k < ninst; k++) {
         const PsrHost& ph = ctx->psrs[inst_psr[k]];
@@ -3178,7 +3291,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         nvgc += (ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
                  d.red0c + 1 <= VMAXR0) ? 1 : 0;
     }
-    const long slots = (long)ncu * (2 * nvgc > ninst ? 2 : 1);
+    const long slots = (long)ncu * (2 * nvgc > ninst ? GWG : 1);
     // (smallest split count within 3% of the best makespan: each split adds a partial
     // Gram that k_greduce must sum)
     double best = 1e30;
@@ -3208,7 +3321,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         long per = (ph.n + nsplit - 1) / nsplit;
         per = (per + 3) / 4 * 4;
         const int wt = d.red0c + 1, R = d.Kd - d.red0c;
-        for (int ntr = (wt + 15) / 16; ntr <= (wt + 15) / 16 + 2; ntr++) {
+        for (int ntr = (wt + 15) / 16; ntr <= std::min(3, (wt + 15) / 16 + 2); ntr++) {
             const int ns = 16 * ntr - wt, kpv = (16 * ntr + R + 15) / 16 * 16;
             if (ns < 1 || kpv > VMAXKP) continue;
             bool ok = true;
@@ -3635,12 +3748,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipEvent_t e0 = (ext_t && gi == 0) ? ctx->ev[12] : nullptr;
             hipEvent_t e1 = (ext_t && gi + 1 == ctx->kp_groups_v.size()) ? ctx->ev[13] : nullptr;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * std::max<size_t>((size_t)(kg.maxKp + 32) * (VCH + 2),
-                                                                 std::max(VW * VTG * 256, VW * 256 + 256));
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)GVB * (kg.maxKp + 33) * (VCH + 2),
+                                                                 std::max(GW * VTG * 256, GW * 256 + 256));
 #define PINT_GRAMV(R_, C_)                                                                                       \
-            hipExtLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(VW * 64), (uint32_t)lds, ctx->stream, e0, e1, 0u,  \
+            hipExtLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, 0u,  \
                                   (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M, (const double*)ctx->d_rt, \
-                                  (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp)
+                                  (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->gvdbg)
             switch (kg.T) {
                 case 1: PINT_GRAMV(1, 1); break;
                 case 2: PINT_GRAMV(1, 2); break;
@@ -3649,23 +3762,17 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 case 5: PINT_GRAMV(1, 5); break;
                 case 6: PINT_GRAMV(1, 6); break;
                 case 7: PINT_GRAMV(1, 7); break;
-                case 8: PINT_GRAMV(1, 8); break;
-                case 9: PINT_GRAMV(1, 9); break;
                 case 12: PINT_GRAMV(2, 2); break;
                 case 13: PINT_GRAMV(2, 3); break;
                 case 14: PINT_GRAMV(2, 4); break;
                 case 15: PINT_GRAMV(2, 5); break;
                 case 16: PINT_GRAMV(2, 6); break;
                 case 17: PINT_GRAMV(2, 7); break;
-                case 18: PINT_GRAMV(2, 8); break;
-                case 19: PINT_GRAMV(2, 9); break;
                 case 23: PINT_GRAMV(3, 3); break;
                 case 24: PINT_GRAMV(3, 4); break;
                 case 25: PINT_GRAMV(3, 5); break;
                 case 26: PINT_GRAMV(3, 6); break;
                 case 27: PINT_GRAMV(3, 7); break;
-                case 28: PINT_GRAMV(3, 8); break;
-                case 29: PINT_GRAMV(3, 9); break;
                 default: ctx->err = "k_gram_v layout out of range"; return PINT_E_INVALID;
             }
 #undef PINT_GRAMV
@@ -3929,6 +4036,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
+    if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {
         ctx->timing_mask = value & 0xff;
         for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec_slot[0][k] = ctx->rec_slot[1][k] = false;
@@ -4077,6 +4185,13 @@ int pint_last_timing(pint_ctx* ctx, double* ms) {
 // 1 = column sums of squares, 2 = Woodbury Sigma factor, 3 = L^-1 work
 int pint_debug_read(pint_ctx* ctx, int which, double* out) {
     HIPCHK(hipStreamSynchronize(ctx->sstream));
+    if (which == 5) {  // (experiment) k_gram_v per-workgroup timestamps
+        static unsigned long long t[4096 * 5];
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_gvts), sizeof(t)));
+        for (int i = 0; i < 4096 * 5; i++) out[i] = (double)t[i];
+        return 4096;
+    }
     if (which == 4) {  // phase timestamps (us) of k_solve_dmx workgroup 0
         unsigned long long ts[32];
         HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round profile on the GPU box: rocprofv3 kernel stats of the bench workload (J0740 legs
+# off), the HBM PMC passes (FETCH_SIZE, WRITE_SIZE: one counter group per run) and the
+# Gram MFMA / LDS / activity passes.  Outputs under gpurun_out/; summaries are made on the
+# host by scripts/*_summary.py.  Each GPU step has its own time limit; any failure stops it.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+B="python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --cpu-baseline 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --grid 64 --j0740 0 --cpu-baseline 0 > gpurun_out/prof.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $B > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- $B > gpurun_out/pmc_write.log 2>&1 || exit $?
+export PINT_SERIAL=1
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_mfma -o run -- $B > gpurun_out/pmc_mfma.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv -d gpurun_out/pmc_lds -o run -- $B > gpurun_out/pmc_lds.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAVES SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_act -o run -- $B > gpurun_out/pmc_act.log 2>&1 || exit $?
+echo prof-done
