@@ -888,13 +888,12 @@ __device__ __forceinline__ void cpow_u8(double c1, double s1, int k, double& c, 
 // Unused columns go to a dummy LDS column (no branches in the staging).  The waves' partial
 // tiles are summed through LDS at the end.  (Built with MFMA accumulators in VGPRs: in AGPRs
 // the loop-carried tiles were copied out and back every chunk.)
-template <int NTR, int NTC>
-__global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                    const double* __restrict__ M, const double* __restrict__ rtime,
-                                                    const double* __restrict__ dmxv, int nsplit,
-                                                    double* __restrict__ Gpart, double* __restrict__ Sdp,
-                                                    double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
-    extern __shared__ double lds[];
+template <int NTR, int NTC, int NSK>
+__device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restrict__ psrs,
+                                            const InstDev* __restrict__ insts, const double* __restrict__ M,
+                                            const double* __restrict__ rtime, const double* __restrict__ dmxv,
+                                            int nsplit, double* __restrict__ Gpart, double* __restrict__ Sdp,
+                                            double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
     constexpr int NTH = GW * 64;
     constexpr int CH = VCH;
     constexpr int CS = CH + 2;  // column stride (= 2 mod 32 doubles)
@@ -910,7 +909,7 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
     const int split = blockIdx.x;
     const PsrDev& Pd = psrs[I.psr];
     const int n = I.n, Kd = Pd.Kd, Kp = Pd.Kpd, r0 = Pd.red0c, NS = Pd.vns, Kpv = Pd.vkp;
-    const int nred = Pd.spec->nred;
+    const int nred = __builtin_amdgcn_readfirstlane(Pd.spec->nred);  // (a flat load: not known uniform)
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
     // Kpv == 16 NTC and f0 == 16 NTR (the launch groups instances by both)
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
@@ -937,16 +936,16 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
     const bool w0 = wave == 0;
     int sp0 = -1, sp1 = -1;  // per buffer: the slot column of this lane's row of two chunks ago
     double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, c8_n = 1.0, s8_n = 0.0;
-    double st[QL];
+    double st[QL] = {};
     int d_n = -1;
     bool ok_n = false;
-    auto load = [&](long c0) {  // the next chunk's row data -> registers (clamped, no branches)
+    auto load = [&](long c0) {  // the next chunk's row data -> registers (clamped rows)
         long row = c0 + lane;
         ok_n = row < i1;
         row = ok_n ? row : i1 - 1;
         // (global-address-space loads: through generic pointers they would be flat loads,
         // which also count against lgkmcnt, so every LDS wait would wait for them too)
-        w_n = ((gptr<double>)Pd.isig)[row];
+        w_n = ok_n ? ((gptr<double>)Pd.isig)[row] : 0.0;  // rows past the split weigh 0
         r_n = ri[row];
         x_n = xv[row];
         d_n = ((gptr<int>)Pd.drow)[row];
@@ -958,24 +957,30 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
 #pragma unroll
         for (int q = 0; q < QL; q++) {
             const int c = wave + GW * q;
-            st[q] = Mi[(long)(c < r0 ? c : 0) * n + row];
+            if (c < r0) st[q] = ok_n ? Mi[(long)c * n + row] : 0.0;  // uniform guard
         }
     };
-    auto stage = [&](double* Ts, int& sp) {  // registers -> whitened row block in LDS
-        const double iw = ok_n ? w_n : 0.0;
-        double* col = Ts + lane;
+    // LDS stores through a 32-bit (address space 3) pointer: column index x CS + lane
+    typedef double __attribute__((address_space(3))) ldsd;
+    auto put = [&](ldsd* Ts, int colidx, double v) { Ts[colidx * CS + lane] = v; };
+    auto stage = [&](double* Tsg, int& sp) {  // registers -> whitened row block in LDS
+        ldsd* Ts = (ldsd*)Tsg;
+        const double iw = w_n;
 #pragma unroll
         for (int q = 0; q < QL; q++) {
             const int c = wave + GW * q;
-            const int cc = vsel(c < r0, c, DUM);
-            col[cc * CS] = st[q] * iw;
-            csq[q] += (cc != DUM && ok_n) ? st[q] * st[q] : 0.0;
+            if (c < r0) {  // uniform guard (scalar branch)
+                put(Ts, c, st[q] * iw);
+                csq[q] += st[q] * st[q];  // 0 past the split
+            }
         }
-        {  // residual and DMX slot entry (wave 0's share; the other waves write DUM)
-            col[vsel(w0, r0, DUM) * CS] = r_n * iw;
+        {  // residual and DMX slot entry (wave 0's share)
             const int sl = (ok_n && d_n >= 0) ? d_n % NS : -1;
-            col[vsel(w0 && sp >= 0, s0 + sp, DUM) * CS] = 0.0;
-            col[vsel(w0 && sl >= 0, s0 + sl, DUM) * CS] = x_n * iw;
+            if (w0) {
+                put(Ts, r0, r_n * iw);
+                put(Ts, vsel(sp >= 0, s0 + sp, DUM), 0.0);
+                put(Ts, vsel(sl >= 0, s0 + sl, DUM), x_n * iw);
+            }
             sp = sl;
         }
 #pragma unroll
@@ -988,10 +993,10 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
             cpow_u8(c8_n, s8_n, a, cb, sb);
             ca *= iw;
             sa *= iw;
-            col[(tA + a) * CS] = ca;
-            col[(tA + 8 + a) * CS] = sa;
-            col[(tB + a) * CS] = cb * iw;
-            col[(tB + 8 + a) * CS] = sb * iw;
+            put(Ts, tA + a, ca);
+            put(Ts, tA + 8 + a, sa);
+            put(Ts, tB + a, cb * iw);
+            put(Ts, tB + 8 + a, sb * iw);
             // Fourier harmonics a + 1 + 8u (<= nred): from the A harmonic by one rotation by
             // e^{i theta}, then by e^{i 8 theta}
             double c = ca, s = sa;
@@ -999,9 +1004,10 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
 #pragma unroll
             for (int u = 0; u < HMAX; u++) {
                 const int h = a + 8 * u;  // harmonic h + 1 -> columns f0 + 2h (sin), +1 (cos)
-                const int cs = vsel(h < nred, f0 + 2 * h, DUM);
-                col[cs * CS] = s;
-                col[(cs + (cs != DUM)) * CS] = c;
+                if (h < nred) {           // uniform guard
+                    put(Ts, f0 + 2 * h, s);
+                    put(Ts, f0 + 2 * h + 1, c);
+                }
                 if (u + 1 < HMAX) rot(c, s, c8_n, s8_n);
             }
         }
@@ -1026,8 +1032,9 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
             for (int ti = 0; ti < NTR; ti++) {
 #pragma unroll
                 for (int tj = ti; tj < NTC; tj++, k++) {
-                    // rows and columns all DMX slots (f0 = 16 NTR): only the DD diagonal
-                    if (ti > 0 && tj < NTR && ti * 16 >= s0) continue;
+                    // rows and columns all DMX slots (the last NSK row tiles, f0 = 16 NTR):
+                    // only the DD diagonal (compile-time after unrolling)
+                    if (ti >= NTR - NSK && tj < NTR) continue;
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
                 }
             }
@@ -1147,6 +1154,26 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
         }
     }
     GVTS(3);
+}
+
+// one launch per (row tiles, column tiles) layout; the number of trailing all-slot row tiles
+// (whose tiles hold only DD and are skipped) picks the body inside, so layouts that differ
+// only in it share the launch (a launch per variant would run their tails one after another)
+template <int NTR, int NTC>
+__global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ M, const double* __restrict__ rtime,
+                                                    const double* __restrict__ dmxv, int nsplit,
+                                                    double* __restrict__ Gpart, double* __restrict__ Sdp,
+                                                    double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
+    extern __shared__ double lds[];
+    const PsrDev& Pd = psrs[insts[blockIdx.y].psr];
+    const int nsk = __builtin_amdgcn_readfirstlane(NTR - (Pd.red0c + 1 + 15) / 16);
+    if (nsk <= 0) {
+        gram_v_body<NTR, NTC, 0>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
+    } else if constexpr (NTR >= 2) {
+        if (nsk == 1) gram_v_body<NTR, NTC, 1>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
+        else if constexpr (NTR >= 3) gram_v_body<NTR, NTC, 2>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
+    }
 }
 
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
@@ -3440,7 +3467,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             const int kp = lay == 2 ? pd.vkp : ((lay && pd.dsplit) ? pd.Kpd : I.Kp);
             const int nt = kp / 16;
             int tT = (nt * (nt + 1) / 2 + GWAVES - 1) / GWAVES;
-            if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column tiles (ntr..9)
+            if (lay == 2) {  // k_gram_v template key: row tiles (1..3) x column tiles (ntr..7)
                 const int ntr = (pd.red0c + 1 + pd.vns) / 16;
                 tT = 10 * (ntr - 1) + nt;
             }
