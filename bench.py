@@ -185,7 +185,8 @@ def roofline(s, lays, kt_gram, step, args):
                   trig sums C_m, S_m that give F^T W F)], P = compact timing columns, R = 2 nred;
       exec_flops  the MFMAs it issues, counted exactly as the kernel loops them: per N-split
                   ceil(rows / 64) chunks x 16 k-steps x (NT + 1) tiles x 2048 flop (NT = the
-                  [T|r|slots] x [T|r|slots|F] upper tiles, + the trig tile); equals the PMC
+                  [T|r|slots] x [T|r|slots|F] upper tiles less the all-slot (DD-only) tiles the
+                  kernel skips, + the trig tile); equals the PMC
                   SQ_INSTS_MFMA x 2048 of the profile (profiles/pmc_gram_r02.json).
     achieved = alg_flops / event time; exec_TFLOP/s beside it."""
     from pint_amd.pta import fit_cost  # noqa: F401
@@ -199,7 +200,8 @@ def roofline(s, lays, kt_gram, step, args):
         P = r0
         alg += 2.0 * n * ((P + 1) * (P + 2) / 2 + (P + 1) * R + (P + 2) + R + 2 * (2 * nred + 1))
         ntr, ntc = (r0 + 1 + ns) // 16, kpv // 16
-        nt = ntr * ntc - ntr * (ntr - 1) // 2 + 1
+        nsk = ntr - (r0 + 1 + 15) // 16  # trailing all-slot row tiles: their DD-only tiles are skipped
+        nt = ntr * ntc - ntr * (ntr - 1) // 2 - nsk * (nsk + 1) // 2 + 1
         per = -(-n // nsplit)
         per = -(-per // 4) * 4
         chunks = sum(-(-max(0, min(n, (q + 1) * per) - min(n, q * per)) // 64) for q in range(nsplit))
@@ -246,7 +248,7 @@ def roofline(s, lays, kt_gram, step, args):
                           for n, b in nbytes.items() if kms.get(n, 0) > 0}
     gram_equiv = float(sum(2.0 * l.n * (l.K + 1.0) ** 2 for l in lays))
     roof["gram_full_equiv_tflops"] = round(gram_equiv / (kt_gram * 1e-3) / 1e12, 2) if kt_gram > 0 else None
-    peaks = load_json("peaks_r01.json")
+    peaks = load_json("peaks_r02.json")
     if peaks:
         roof["measured_peaks"] = peaks
     return roof
