@@ -92,6 +92,11 @@ typedef struct {
     /* table offsets (doubles; each parameter is a dd pair at [off], [off+1]); -1 absent */
     int32_t o_F, o_PEPOCH, o_lon, o_lat, o_pmlon, o_pmlat, o_px, o_POSEPOCH;
     int32_t o_DM, o_DMEPOCH, o_DMX, o_FD, o_JUMP, o_bin[PINT_B_NPAR];
+    int32_t o_PHOFF;        /* PhaseOffset: table slot of PHOFF (-1 none); the TOAs' phase gets
+                               -PHOFF, the TZR TOA's does not (phase_offset.py offset_phase)    */
+    int32_t wb_noones;      /* 1: the Woodbury chi2 has no offset column of ones (PHOFF free,
+                               residuals.py:583-585); the ECORR-only Sherman-Morrison chi2 of
+                               :591-636 is this form with the ECORR basis alone             */
     double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
     double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
     double red_t0;          /* unused reserve                                           */

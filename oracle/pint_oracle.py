@@ -618,6 +618,12 @@ def evaluate(om: OModel, toas: dict, with_tzr=True):
     for name in sorted((k for k in om.masks if re.match(r"^JUMP\d+$", k)), key=lambda x: int(x[4:])):
         sel = select_rows(toas, *om.masks[name], with_tzr=with_tzr)
         ph = ph + np.where(sel, LD(om.v(name)) * F[0], LD(0))
+    # PhaseOffset.offset_phase (phase_offset.py): -PHOFF on the TOAs, 0 on the TZR TOA
+    if "PhaseOffset" in om.comps:
+        off = np.full(n, -LD(om.v("PHOFF")), dtype=LD)
+        if with_tzr:
+            off[-1] = LD(0)
+        ph = ph + off
     out["phase"] = ph
     out["dt"] = dt
     out["dt0"] = (tdb - LD(om.v("PEPOCH"))) * LD(DAYSEC)
@@ -645,7 +651,9 @@ def scaled_sigma_us(om, toas):
 
 
 def residuals(om: OModel, toas: dict, track_mode=None, subtract_mean=True, use_weighted_mean=True):
-    """Residuals.calc_phase_resids / calc_time_resids (residuals.py:314-538)."""
+    """Residuals.calc_phase_resids / calc_time_resids (residuals.py:314-538); no implicit
+    mean subtraction with a PhaseOffset (residuals.py:124-128, :348-352)."""
+    subtract_mean = subtract_mean and "PhaseOffset" not in om.comps
     ev = evaluate(om, toas, True)
     ph = ev["phase"]
     n = len(toas["tdb_hi"])
@@ -713,10 +721,13 @@ def designmatrix(om: OModel, toas: dict):
     dm_terms = ["DM"] + om.prefix(r"^DM(\d+)$") if om.has("DM") else []
     fds = om.prefix(r"^FD(\d+)$")
     B = ev["binary_obj"]
-    cols, names = [np.full(n, 1.0 / F0)], ["Offset"]
+    # the implicit Offset column unless a PhaseOffset is present (timing_model.py:2145)
+    cols, names = ([], []) if "PhaseOffset" in om.comps else ([np.full(n, 1.0 / F0)], ["Offset"])
     for p in om.free:
         m = re.match(r"^F(\d+)$", p)
-        if m:
+        if p == "PHOFF":  # -d_offset_phase_d_PHOFF / F0 (phase_offset.py)
+            col = np.full(n, 1.0 / F0)
+        elif m:
             k = int(m.group(1))
             col = -(dt ** (k + 1) / LD(math.factorial(k + 1))).astype(float) / F0
         elif p in ("RAJ", "ELONG"):
@@ -816,14 +827,47 @@ def noise_basis(om, toas):
     return np.hstack(mats), np.concatenate(wts)
 
 
+def ecorr_only(om):
+    """calc_chi2's Sherman-Morrison branch (residuals.py:705-709): ECORR without
+    time-correlated noise and with a PhaseOffset."""
+    return "PhaseOffset" in om.comps and "PLRedNoise" not in om.comps and \
+        any(re.match(r"^ECORR\d+$", k) for k in om.masks)
+
+
+def chi2_ecorr(om, toas, r, sigma_us, lognorm=False):
+    """_calc_ecorr_chi2 (residuals.py:591-636): TOAs outside every epoch by r^2/N, each
+    ECORR epoch by sherman_morrison_dot (utils.py:3024-3071) with v = 1, w = ECORR^2."""
+    if "PHOFF" not in om.free:
+        raise AssertionError("the ECORR-only chi2 needs a free PHOFF (residuals.py:595-599)")
+    mats, wts = ecorr_basis(om, toas)
+    N = (sigma_us * 1e-6) ** 2
+    U = np.hstack(mats) if mats else np.zeros((len(r), 0))
+    w = np.concatenate(wts) if wts else np.zeros(0)
+    noec = ~np.any(U.astype(bool), axis=1)
+    chi2 = float(np.dot(r[noec], r[noec] / N[noec]))
+    ld = float(np.sum(np.log(N[noec])))
+    for j in range(U.shape[1]):
+        m = U[:, j].astype(bool)
+        Ninv = 1 / N[m]
+        denom = 1 + w[j] * Ninv.sum()
+        s = np.dot(r[m], Ninv)
+        chi2 += float(np.dot(r[m], Ninv * r[m]) - w[j] * s * s / denom)
+        ld += float(np.sum(np.log(N[m])) + np.log(denom))
+    return (chi2, 0.5 * ld) if lognorm else chi2
+
+
 def chi2_gls(om, toas, r, sigma_us):
-    """_calc_gls_chi2 via woodbury_dot (residuals.py:567-589, utils.py:3074)."""
+    """_calc_gls_chi2 via woodbury_dot (residuals.py:567-589, utils.py:3074); the offset
+    column of ones only without a free PHOFF (:583-585)."""
+    if ecorr_only(om):
+        return chi2_ecorr(om, toas, r, sigma_us)
     U, phi = noise_basis(om, toas)
     N = (sigma_us * 1e-6) ** 2
     if U is None or U.shape[1] == 0:
         return chi2_wls(r, sigma_us)
-    U = np.append(U, np.ones((len(r), 1)), axis=1)
-    phi = np.append(phi, [1e40])
+    if "PHOFF" not in om.free:
+        U = np.append(U, np.ones((len(r), 1)), axis=1)
+        phi = np.append(phi, [1e40])
     xNy = np.sum(r * r / N)
     xNU = (r / N) @ U
     Sigma = np.diag(1 / phi) + (U.T / N) @ U
@@ -840,11 +884,14 @@ def lognorm(om, toas, r, sigma_us, gls=True):
     U, phi = noise_basis(om, toas) if gls else (None, None)
     if U is None:
         return float(np.sum(np.log(sig)))
+    if ecorr_only(om):
+        return chi2_ecorr(om, toas, r, sigma_us, lognorm=True)[1]
     # a correlated-noise model always takes the Woodbury form, with the offset column even
-    # when its basis has no columns (ECORR without multi-TOA epochs)
+    # when its basis has no columns (ECORR without multi-TOA epochs), unless PHOFF is free
     N = sig ** 2
-    U = np.append(U, np.ones((len(r), 1)), axis=1)
-    phi = np.append(phi, [1e40])
+    if "PHOFF" not in om.free:
+        U = np.append(U, np.ones((len(r), 1)), axis=1)
+        phi = np.append(phi, [1e40])
     Sigma = np.diag(1 / phi) + (U.T / N) @ U
     _, ld_sigma = np.linalg.slogdet(Sigma)
     return float(0.5 * (np.sum(np.log(N)) + np.sum(np.log(phi)) + ld_sigma))

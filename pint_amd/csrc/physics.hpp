@@ -761,6 +761,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         for (int k = 0; k < S.njump; k++)
             if ((t.jmask >> k) & 1ull) ph = dd_add(ph, dd_mul(dd_make(pval(P, S.o_JUMP + 2 * k)), F0));
     }
+    // PhaseOffset.offset_phase (phase_offset.py): -PHOFF on the TOAs, nothing on the TZR TOA
+    // (row ld = n)
+    if (S.o_PHOFF >= 0 && r < (unsigned)ld) ph = dd_sub(ph, pdd(P, S.o_PHOFF));
     o.phase = ph;
     double dtd = dd_to_d(dt);
     o.fdt = spin_freq(S, P, dtd);

@@ -1527,8 +1527,13 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
             int j = e - i * (i + 1) / 2;
             int ci = (i < R) ? ncol + i : 0, cj = (j < R) ? ncol + j : 0;
             double si = (i < R) ? 1.0 : F0, sj = (j < R) ? 1.0 : F0;
-            double v = G(ci, cj) * si * sj;
-            if (i == j) v += (i < R) ? 1.0 / Pd.red_phi[i] : 1e-40;
+            double v;
+            if (S.wb_noones && (i == R || j == R)) {
+                v = (i == j) ? 1.0 : 0.0;  // no ones column: a decoupled unit row
+            } else {
+                v = G(ci, cj) * si * sj;
+                if (i == j) v += (i < R) ? 1.0 / Pd.red_phi[i] : 1e-40;
+            }
             Sg[e] = v;
         }
         __syncthreads();
@@ -1756,8 +1761,12 @@ __device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& 
         if (gi < Kn && gj < Kn) {
             const int ci = (gi < R) ? ncol + gi : 0, cj = (gj < R) ? ncol + gj : 0;
             const double si = (gi < R) ? 1.0 : F0, sj = (gj < R) ? 1.0 : F0;
-            v = G(ci, cj) * si * sj;
-            if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
+            if (S.wb_noones && (gi == R || gj == R)) {
+                v = (gi == gj) ? 1.0 : 0.0;  // no ones column (PHOFF free): a decoupled unit row
+            } else {
+                v = G(ci, cj) * si * sj;
+                if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
+            }
         } else {
             v = (gi == gj) ? 1.0 : 0.0;
         }
@@ -2629,12 +2638,12 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
         for (int e = 0; e < nep; e++) v -= Ei[(long)e * I.Kp + S.ncol + j] * ce[e];
         d[j] = v;
     }
-    if (threadIdx.x == 0) d[R] = rw1 - erw1;
+    if (threadIdx.x == 0) d[R] = S.wb_noones ? 0.0 : rw1 - erw1;  // the ones column's entry
     __syncthreads();
     // y = L^-1 d with the explicit inverse factor from k_solve (row dot products); with no
     // noise basis Sigma is the 1x1 [1e-40 + 1^T N^-1 1], which the solves do not factor
     const bool nobasis = (R == 0 && nep == 0);
-    const double x00 = 1.0 / sqrt(1e-40 + Pd.sumw);
+    const double x00 = S.wb_noones ? 1.0 : 1.0 / sqrt(1e-40 + Pd.sumw);
     const double* X = sigL + I.soff;
     // the packed factor staged in LDS with coalesced loads, then four lanes per row
     double* Xs = d + Kn;  // Kn (Kn + 1) / 2
@@ -2666,7 +2675,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     ld = block_sum<4>(ld, sh);
     if (threadIdx.x == 0) {
         chi2[inst] = (rwr - erwr) - q;
-        lognorm[inst] = 0.5 * (ld + 2.0 * Pd.logsig + log(1e40));
+        lognorm[inst] = 0.5 * (ld + 2.0 * Pd.logsig + (S.wb_noones ? 0.0 : log(1e40)));
     }
 }
 
@@ -4129,7 +4138,9 @@ int pint_lognorm(pint_ctx* ctx, int gls, double* out) {
     if (gls == 2) {
         for (int k = 0; k < ctx->ninst; k++) {
             const PsrDev& d = ctx->psrs[ctx->inst[k].psr].dev;
-            out[k] = 0.5 * (2.0 * d.logsig + std::log(1e40) + std::log(1e-40 + d.sumw));
+            out[k] = ctx->psrs[ctx->inst[k].psr].spec.wb_noones
+                         ? d.logsig
+                         : 0.5 * (2.0 * d.logsig + std::log(1e40) + std::log(1e-40 + d.sumw));
         }
     } else if (gls) {
         HIPCHK(hipMemcpyAsync(out, ctx->d_lognorm, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));

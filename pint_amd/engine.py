@@ -82,7 +82,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         return offs[name]
 
     for s in ("o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px", "o_POSEPOCH", "o_DM",
-              "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP"):
+              "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP", "o_PHOFF"):
         setattr(spec, s, -1)
     for i in range(L.B_NPAR):
         spec.o_bin[i] = -1
@@ -92,6 +92,17 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
     for n in F:
         place(n)
     spec.o_PEPOCH = place("PEPOCH")
+    has_phoff = "PhaseOffset" in model.components
+    if has_phoff:
+        if model.PHOFF.value is None:
+            model.PHOFF.value = 0.0
+        spec.o_PHOFF = place("PHOFF")
+    phoff_free = has_phoff and "PHOFF" in model.free_params
+    spec.wb_noones = 1 if phoff_free else 0
+    if has_phoff and not phoff_free and use_gls_basis and model.has_correlated_errors:
+        # the Woodbury chi2 then appends a column of ones the fit layout does not carry
+        raise NotImplementedError("PhaseOffset with a frozen PHOFF and correlated noise "
+                                  "(residuals.py:583-585 ones column) is not supported")
     ak = model.astrometry_kind
     spec.astrometry = ak
     if ak:
@@ -142,9 +153,9 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
                 raise ValueError(f"binary parameter {n} missing")
     tstride = pos
     spec.tstride = tstride
-    # ---- columns: Offset + free params in params order (timing_model.py:2141-2173)
-    cols = ["Offset"]
-    kinds, idxs, toffs = [L.COL_OFFSET], [0], [-1]
+    # ---- columns: Offset (unless a PhaseOffset is present, timing_model.py:2145) + free
+    # params in params order (timing_model.py:2141-2173)
+    cols, kinds, idxs, toffs = ([], [], [], []) if has_phoff else (["Offset"], [L.COL_OFFSET], [0], [-1])
     noise_like = {"EFAC", "EQUAD", "ECORR", "TNEQ"}
     for n in model.free_params:
         p = model[n]
@@ -153,7 +164,9 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
             continue
         if n in ("TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX"):
             continue
-        if n in F:
+        if n == "PHOFF":  # -d_offset_phase_d_PHOFF / F0 = 1/F0, the Offset column's values
+            k, i = L.COL_OFFSET, 0
+        elif n in F:
             k, i = L.COL_F, F.index(n)
         elif n in ("RAJ", "ELONG"):
             k, i = L.COL_LON, 0
@@ -193,7 +206,6 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.col_toff[j] = toffs[j]
     tm = _track_mode(model, toas, track_mode)
     spec.track_pn = 1 if tm == "use_pulse_numbers" else 0
-    has_phoff = "PhaseOffset" in model.components
     spec.subtract_mean = 1 if (subtract_mean and not has_phoff) else 0
     spec.weighted_mean = 1 if use_weighted_mean else 0
     nred = 0

@@ -254,8 +254,9 @@ class BatchFit:
             res.labels = list(lay.columns)
             if self.items is not None:
                 m = self.items[k][0]
-                for j, name in enumerate(lay.columns[1:], start=1):
-                    m[name].uncertainty = float(res.errors[j])
+                for j, name in enumerate(lay.columns):
+                    if name != "Offset":
+                        m[name].uncertainty = float(res.errors[j])
 
     def _noise_into(self, results):
         """Noise realisations of the last step (GLS only)."""

@@ -139,6 +139,7 @@ _DEFS = {
     "TZRFRQ": ("AbsPhase", "float", "MHz", False, None),
     # astrometry (astrometry.py)
     "POSEPOCH": ("Astrometry", "mjd", "d", True, None), "PX": ("Astrometry", "float", "mas", False, None),
+    "PHOFF": ("PhaseOffset", "float", "", False, None),
     "RAJ": ("AstrometryEquatorial", "hourangle", "hourangle", False, None),
     "DECJ": ("AstrometryEquatorial", "degangle", "deg", False, None),
     "PMRA": ("AstrometryEquatorial", "float", "mas / yr", False, None),

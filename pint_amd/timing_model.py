@@ -22,7 +22,7 @@ from .parameter import LD, Param
 # components supported on the hot path
 DELAY_ORDER = ["AstrometryEquatorial", "AstrometryEcliptic", "TroposphereDelay", "SolarSystemShapiro",
                "SolarWindDispersion", "DispersionDM", "DispersionDMX", "BinaryELL1", "BinaryDD", "FD"]
-PHASE_ORDER = ["AbsPhase", "Spindown", "PhaseJump"]
+PHASE_ORDER = ["AbsPhase", "Spindown", "PhaseOffset", "PhaseJump"]
 NOISE = ["ScaleToaError", "EcorrNoise", "PLRedNoise"]
 
 ELL1_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "EDOT", "OMDOT", "M2", "SINI", "TASC", "EPS1", "EPS2",
