@@ -75,6 +75,9 @@ class Param:
     scale: Optional[tuple] = None  # (scale_factor, threshold) unit_scale params
     component: str = ""
     description: str = ""
+    alias: Optional[str] = None       # the par-file spelling when it was an alias (use_alias)
+    mjd_pair: Optional[tuple] = None  # MJDs: the parsed (day, fraction) float64 pair
+    implicit: bool = False            # a 0 default standing in for the reference's unset value
 
     # -- value handling ---------------------------------------------------------------
     def set_from_string(self, s: str):
@@ -88,7 +91,9 @@ class Param:
         elif k == "hourangle" or k == "degangle":
             self.value = parse_sexagesimal(s) if ":" in s else fortran_float(s)
         elif k == "mjd":
+            from .parfile import str_to_mjds
             self.value = mjd_string_to_longdouble(s)
+            self.mjd_pair = str_to_mjds(s)
         else:
             v = data2longdouble(s) if self.long_double else fortran_float(s)
             if self.scale is not None and abs(float(v)) > abs(self.scale[1]):
@@ -97,7 +102,9 @@ class Param:
 
     def set_uncertainty_from_string(self, s: str):
         try:
-            u = fortran_float(s)
+            # long-double parameters keep a longdouble uncertainty (parameter.py
+            # _set_uncertainty parses it like the value)
+            u = data2longdouble(s) if (self.long_double and self.kind in ("float", "mjd")) else fortran_float(s)
         except ValueError:
             return
         if self.kind == "hourangle":  # uncertainty in seconds of time (parameter.py AngleParameter)
@@ -135,6 +142,8 @@ _DEFS = {
     "BINARY": ("", "str", "", False, None), "NTOA": ("", "int", "", False, None),
     "CHI2": ("", "float", "", False, None), "CHI2R": ("", "float", "", False, None),
     "TRES": ("", "float", "us", False, None), "DMDATA": ("", "bool", "", False, None),
+    "INFO": ("", "str", "", False, None), "TIMEEPH": ("", "str", "", False, None),
+    "T2CMETHOD": ("", "str", "", False, None), "DILATEFREQ": ("", "bool", "", False, None),
     "TZRMJD": ("AbsPhase", "mjd", "d", True, None), "TZRSITE": ("AbsPhase", "str", "", False, None),
     "TZRFRQ": ("AbsPhase", "float", "MHz", False, None),
     # astrometry (astrometry.py)
@@ -205,8 +214,7 @@ MASK_PARAMS = {"JUMP": ("PhaseJump", "s"), "EFAC": ("ScaleToaError", ""),
                "EQUAD": ("ScaleToaError", "us"), "TNEQ": ("ScaleToaError", "log10(s)"),
                "ECORR": ("EcorrNoise", "us")}
 
-IGNORED = {"MODE", "NITS", "INFO", "TRES", "CHI2", "CHI2R", "DMRES", "TIMEEPH", "T2CMETHOD",
-           "DILATEFREQ", "DMDATA", "NTOA", "IBOOT", "RM", "SWP", "DMXEP", "DMXF1", "DMXF2"}
+IGNORED = {"MODE", "NITS", "DMRES", "IBOOT", "RM", "SWP", "DMXEP", "DMXF1", "DMXF2"}
 
 
 def make_param(name: str) -> Optional[Param]:

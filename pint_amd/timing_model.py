@@ -84,6 +84,16 @@ class TimingModel:
         other = [n for n in self._params if n not in seen]
         return top + astro + spin + rest + other
 
+    def as_parfile(self, include_info: bool = True, comment: str = None) -> str:
+        """The model as par-file text (timing_model.py:2747 as_parfile, format "pint")."""
+        from .parfile import as_parfile
+        return as_parfile(self, include_info=include_info, comment=comment)
+
+    def write_parfile(self, filename, include_info: bool = True, comment: str = None):
+        """timing_model.py:2823 write_parfile."""
+        from .parfile import write_parfile
+        write_parfile(self, filename, include_info=include_info, comment=comment)
+
     @property
     def free_params(self) -> List[str]:
         return [p for p in self.params if not self._params[p].frozen]
@@ -252,9 +262,11 @@ def _parse_mask_line(model: TimingModel, base: str, fields: List[str], counters:
     p.value = v
     if len(rest) > 1:
         p.frozen = rest[1] != "1"
+        p.uncertainty_value = 0.0
     if len(rest) > 2:
         p.set_uncertainty_from_string(rest[2])
     model.add_param(p)
+    return p
 
 
 def get_model(parfile) -> TimingModel:
@@ -280,6 +292,12 @@ def get_model(parfile) -> TimingModel:
         defaults += [("POSEPOCH", None), ("PX", 0.0), ("ELONG", None), ("ELAT", None), ("PMELONG", 0.0),
                      ("PMELAT", 0.0), ("ECL", "IERS2010")]
     defaults += [("F0", None), ("PEPOCH", None)]
+    # top-level parameters every reference model carries (timing_model.py:330-350)
+    defaults += [("DILATEFREQ", False), ("DMDATA", False), ("NTOA", 0)]
+    if has_eq or has_ecl:
+        defaults += [("PLANET_SHAPIRO", False)]
+    if any(n in ("NE_SW", "SOLARN0") for n in names):
+        defaults += [("SWM", 0)]
     if any(n == "DM" or re.match(r"^DM\d+$", n) for n in names):
         defaults += [("DM", LD(0)), ("DMEPOCH", None)]
     if binary == "ELL1":
@@ -297,6 +315,8 @@ def get_model(parfile) -> TimingModel:
         if n in ("PB", "OM", "OMDOT", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "DM") and v is not None:
             v = LD(v)
         p.value = v
+        # ELL1's rates are unset (None) in the reference (binary_ell1.py), 0 here
+        p.implicit = binary == "ELL1" and n in ("PBDOT", "A1DOT", "EDOT", "OMDOT", "EPS1DOT", "EPS2DOT")
         if p.component == "Binary":
             p.component = "Binary"
         model.add_param(p)
@@ -307,7 +327,9 @@ def get_model(parfile) -> TimingModel:
             continue
         if name in P.MASK_PARAMS or raw in ("T2EFAC", "T2EQUAD", "TNECORR"):
             base = P._ALIASES.get(raw, raw)
-            _parse_mask_line(model, base, l.fields, counters)
+            mp = _parse_mask_line(model, base, l.fields, counters)
+            if raw != base and mp is not None:
+                mp.alias = raw
             continue
         if name == "BINARY":
             p = model._params.get("BINARY") or P.make_param("BINARY")
@@ -323,13 +345,25 @@ def get_model(parfile) -> TimingModel:
                 raise NotImplementedError(f"parameter {raw} is outside the supported hot path")
             model.add_param(p)
         p = model[name]
+        if raw != name:
+            p.alias = raw
         if not l.fields:
             continue
         p.set_from_string(l.fields[0])
+        # TimingModel.validate (timing_model.py:405-413): the only values PINT supports
+        if name == "TIMEEPH" and p.value not in (None, "FB90"):
+            p.value = "FB90"
+        elif name == "T2CMETHOD" and p.value not in (None, "IAU2000B"):
+            p.value = "IAU2000B"
+        elif name == "DILATEFREQ" and p.value:
+            p.value = False
         if len(l.fields) > 1 and p.kind not in ("str", "bool"):
+            # parameter.py:551-576: a third field is a fit flag (uncertainty 0 unless a
+            # fourth field gives it) or an uncertainty
             fl = l.fields[1]
             if fl in ("0", "1"):
                 p.frozen = fl != "1"
+                p.uncertainty_value = 0.0
                 if len(l.fields) > 2:
                     p.set_uncertainty_from_string(l.fields[2])
             else:
