@@ -295,6 +295,42 @@ int pint_noise_resids(pint_ctx *ctx, double *red, double *ecorr);
 int pint_last_timing(pint_ctx *ctx, double *ms8);
 int pint_sync(pint_ctx *ctx);
 
+/* ---- noise-parameter fitting ------------------------------------------
+ * DownhillFitter._fit_noise (fitter.py:1230-1273) maximises the likelihood over the free
+ * EFAC/EQUAD/ECORR/red-noise parameters with the residuals of the current timing model held
+ * fixed (fitter.py:1239-1247: one Residuals object, only its model's noise values change).
+ *
+ * pint_set_resids replaces every instance's time residuals (n_i each, s): the fixed
+ * residuals of such a fit (= pint_debug_set_resids).
+ * pint_set_sigma replaces pulsar psr's scaled TOA uncertainties (s) in place
+ * (ScaleToaError.scale_toa_sigma, noise_model.py:159, at trial EFAC/EQUAD values) and
+ * pint_set_noise_weights its noise-basis prior variances (PLRedNoise 2 nred, ECORR nep; s^2;
+ * either NULL), for a Woodbury likelihood (pint_fit_step(ctx,1) + pint_chi2_gls +
+ * pint_lognorm(ctx,1)) at trial noise parameters of a model with time-correlated noise. */
+int pint_set_resids(pint_ctx *ctx, const double *time_resid);
+int pint_set_sigma(pint_ctx *ctx, int psr, const double *sigma_s);
+int pint_set_noise_weights(pint_ctx *ctx, int psr, const double *red_phi, const double *ep_phi);
+/* White-noise classes of pulsar psr: its TOAs grouped by the set of EFAC/EQUAD masks that
+ * select them, CSR (cls_ptr[ncls+1], cls_idx[n]; every TOA in exactly one class), with the
+ * raw TOA uncertainties sigma0_us[n] (us).  A class's scaled variance is
+ * N_i = (sigma0_i^2 + Q^2) F^2, Q^2 = sum of its EQUAD^2, F = product of its EFACs. */
+int pint_set_noise_classes(pint_ctx *ctx, int psr, int ncls, const int32_t *cls_ptr, const int32_t *cls_idx,
+                           const double *sigma0_us);
+/* Log-likelihood of the current (fixed) residuals of every instance at trial noise
+ * parameters, one device pass: Residuals.lnlikelihood (residuals.py:713) with
+ * kind[k] = 0 diagonal N (_calc_wls_chi2, :638), 1 N + ECORR blocks by Sherman-Morrison
+ * (_calc_ecorr_chi2, :591; PHOFF free), 2 as 1 plus the 1e40 offset column of
+ * _calc_gls_chi2 (:583-587).  cls_qf: (Q^2 [us^2], F) per class, instances' classes
+ * concatenated; ep_w: ECORR variance (s^2) per epoch of the batch (NULL when no instance
+ * has kind > 0 and epochs).  out3[3k] = lnL, [3k+1] = chi2, [3k+2] = logdet(C)/2.
+ * Gradients (kinds 0 and 1; either pointer may be NULL): cls_g[2c] = sum_{i in c} N_i
+ * dlnL/dN_i, cls_g[2c+1] = sum_{i in c} dlnL/dN_i (s^-2), ep_g[e] = dlnL/dw_e (s^-2) --
+ * the chain-rule pieces of Residuals.d_lnlikelihood_d_param (residuals.py:718-828):
+ * dlnL/dEFAC_p = sum_{c ∋ p} 2 cls_g[2c] / EFAC_p, dlnL/dEQUAD_p = sum_{c ∋ p}
+ * 2 EQUAD_p F_c^2 1e-12 cls_g[2c+1], dlnL/dECORR_p = sum_{e of p} 2 ECORR_p 1e-12 ep_g[e]. */
+int pint_noise_lnlike(pint_ctx *ctx, const int32_t *kind, const double *cls_qf, const double *ep_w, double *out3,
+                      double *cls_g, double *ep_g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -863,11 +863,15 @@ def chi2_gls(om, toas, r, sigma_us):
         return chi2_ecorr(om, toas, r, sigma_us)
     U, phi = noise_basis(om, toas)
     N = (sigma_us * 1e-6) ** 2
-    if U is None or U.shape[1] == 0:
+    if U is None:
         return chi2_wls(r, sigma_us)
+    # a correlated-noise model takes the Woodbury form even when its basis has no columns
+    # (ECORR without multi-TOA epochs): the offset column alone, unless PHOFF is free
     if "PHOFF" not in om.free:
         U = np.append(U, np.ones((len(r), 1)), axis=1)
         phi = np.append(phi, [1e40])
+    if U.shape[1] == 0:
+        return chi2_wls(r, sigma_us)
     xNy = np.sum(r * r / N)
     xNU = (r / N) @ U
     Sigma = np.diag(1 / phi) + (U.T / N) @ U
@@ -903,6 +907,42 @@ def lnlikelihood(om, toas, gls=True):
     corr = gls and noise_basis(om, toas)[0] is not None
     c2 = chi2_gls(om, toas, r["time"], r["sigma_us"]) if corr else chi2_wls(r["time"], r["sigma_us"])
     return -(c2 / 2 + lognorm(om, toas, r["time"], r["sigma_us"], corr))
+
+
+def lnlikelihood_of(om, toas, r):
+    """Residuals.lnlikelihood (residuals.py:713) of FIXED time residuals r at om's noise
+    values -- the objective DownhillFitter._fit_noise evaluates (fitter.py:1239-1247: one
+    Residuals object, only its model's noise values change)."""
+    sig = scaled_sigma_us(om, toas)
+    corr = noise_basis(om, toas)[0] is not None
+    c2 = chi2_gls(om, toas, r, sig) if corr else chi2_wls(r, sig)
+    return -(c2 / 2 + lognorm(om, toas, r, sig, corr))
+
+
+def d_lnlikelihood_d_param(om, toas, r, name):
+    """Residuals.d_lnlikelihood_d_param (residuals.py:809-828) for EFAC/EQUAD without
+    correlated noise: sum_i dlnL/dN_i dN_i/dp, dlnL/dN_i = -(-r^2/N^2 + 1/N)/2
+    (residuals.py:718-728), dN_i/dp = 2 sigma_i dsigma_i/dp (:772-777) with
+    dsigma/dEFAC = sigma/EFAC and dsigma/dEQUAD = sigma EQUAD / (sigma0^2 + sum EQUAD^2)
+    on the parameter's mask (noise_model.py:183-214).  In s, us and 1/us as the reference."""
+    if noise_basis(om, toas)[0] is not None:
+        raise NotImplementedError("restated for white noise only")
+    sig = scaled_sigma_us(om, toas)
+    N = (sig * 1e-6) ** 2
+    dl_dN = -0.5 * (-(r ** 2) / N ** 2 + 1 / N)
+    sel = select_mask(toas, *om.masks[name])
+    ds = np.zeros(len(r))
+    if name.startswith("EFAC"):
+        ds[sel] = sig[sel] * 1e-6 / float(om.v(name))
+    elif name.startswith("EQUAD"):
+        s2 = np.array(toas["err_us"], dtype=float) ** 2
+        for n in (k for k in om.masks if re.match(r"^EQUAD\d+$", k)):
+            m = select_mask(toas, *om.masks[n])
+            s2[m] += float(om.v(n)) ** 2
+        ds[sel] = sig[sel] * float(om.v(name)) / s2[sel] * 1e-6  # s per us
+    else:
+        raise NotImplementedError(name)
+    return float(np.sum(dl_dN * 2 * sig * 1e-6 * ds))
 
 
 def _normalize(M):

@@ -99,6 +99,11 @@ def lib():
     L.pint_noise_resids.argtypes = [vp, dptr, dptr]
     L.pint_debug_gram.argtypes = [vp, C.c_int, dptr]
     L.pint_debug_set_resids.argtypes = [vp, dptr]
+    L.pint_set_resids.argtypes = [vp, dptr]
+    L.pint_set_sigma.argtypes = [vp, C.c_int, dptr]
+    L.pint_set_noise_weights.argtypes = [vp, C.c_int, dptr, dptr]
+    L.pint_set_noise_classes.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dptr]
+    L.pint_noise_lnlike.argtypes = [vp, C.POINTER(C.c_int32), dptr, dptr, dptr, dptr, dptr]
     _lib = L
     return L
 
@@ -110,7 +115,9 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_set_option", "pint_host_alloc", "pint_host_free",
             "pint_fit_layout", "pint_query", "pint_capture_begin", "pint_capture_end", "pint_graph_launch",
             "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step",
-            "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids"]
+            "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
+            "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
+            "pint_noise_lnlike"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -44,6 +44,13 @@ struct PsrDev {
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
+    const int32_t* toa_ep;   // n: the ECORR epoch of each TOA (-1: none)
+    // white-noise classes for noise-parameter fits (pint_set_noise_classes): TOAs grouped by
+    // the set of EFAC/EQUAD masks selecting them, CSR; raw TOA errors (us)
+    const int32_t *cls_ptr, *cls_idx, *toa_cls;
+    const double* sigma0;
+    int ncls;
+    int ep_overlap;          // some TOA lies in two ECORR epochs (no per-epoch Sherman-Morrison)
     const ColRun* runs;      // design-matrix column runs
     int nrun;
     // sparse-DMX fit layout: the DMX columns (one nonzero value per TOA, in its bin) are
@@ -2751,6 +2758,102 @@ __global__ __launch_bounds__(64) void k_noise_ecorr(const PsrDev* __restrict__ p
     for (int k = Pd.ep_ptr[e] + threadIdx.x; k < Pd.ep_ptr[e + 1]; k += 64) o[Pd.ep_idx[k]] = ce;
 }
 
+// k_noise_lnl: log-likelihood of the fixed time residuals under trial white-noise parameters,
+// the objective of the noise-parameter fit (fitter.py:1242-1261 _mloglike/_mloglike_grad with
+// residuals.py:591-667 and :718-807).  One workgroup per instance; the residuals r stay those
+// of the last evaluation, as the reference keeps Residuals.time_resids while it changes the
+// noise parameters.  Per TOA N_i = (sigma0_i^2 + Q_c^2) F_c^2 (us^2 -> s^2) from the (Q^2, F) of
+// its class c.  kind (meta[3k+1]): 0 diagonal N (residuals.py:638); 1 N plus one ECORR block
+// per epoch, Sherman-Morrison (residuals.py:591); 2 as 1 plus the 1e40 offset column of
+// _calc_gls_chi2 (residuals.py:583-587), eliminated last.  Writes (lnL, chi2, logdet C / 2) and,
+// for kinds 0/1, sum_i g_i N_i and sum_i g_i per class (g_i = dlnL/dN_i) and dlnL/dw_e per epoch.
+__global__ __launch_bounds__(256) void k_noise_lnl(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                  const double* __restrict__ rtime, const long* __restrict__ meta,
+                                                  const double* __restrict__ qf, const double* __restrict__ epw,
+                                                  double* __restrict__ epsv, double* __restrict__ out,
+                                                  double* __restrict__ clsg, double* __restrict__ epg) {
+    __shared__ double sh[4];
+    const int inst = blockIdx.x;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const long q0 = meta[3 * inst];
+    const int kind = (int)meta[3 * inst + 1];
+    const double* ri = rtime + I.ooff;
+    const double* Q = qf + 2 * q0;
+    const int nep = kind ? Pd.nep : 0;
+    // per epoch: s = sum r/N, v = sum 1/N over its TOAs; the Sherman-Morrison terms
+    double ec = 0.0, el = 0.0, ea = 0.0, eb = 0.0;
+    for (int e = threadIdx.x; e < nep; e += 256) {
+        double s = 0.0, v = 0.0;
+        for (int k = Pd.ep_ptr[e]; k < Pd.ep_ptr[e + 1]; k++) {
+            const int i = Pd.ep_idx[k], c = Pd.toa_cls[i];
+            const double s0 = Pd.sigma0[i], f = Q[2 * c + 1];
+            const double iN = 1.0 / ((s0 * s0 + Q[2 * c]) * (f * f) * 1e-12);
+            s += ri[i] * iN;
+            v += iN;
+        }
+        const double w = epw[I.epoff + e], den = 1.0 + w * v;
+        epsv[2 * (I.epoff + e)] = s;
+        epsv[2 * (I.epoff + e) + 1] = v;
+        ec += w * s * s / den;
+        el += log(den);
+        ea += w * s * v / den;
+        eb += w * v * v / den;
+        if (kind == 1) epg[I.epoff + e] = 0.5 * (s * s / (den * den) - v / den);
+    }
+    __syncthreads();
+    double t1 = 0.0, t2 = 0.0, S = 0.0, V = 0.0;
+    bool neg = false;
+    for (int c = 0; c < Pd.ncls; c++) {
+        const double q2 = Q[2 * c], f = Q[2 * c + 1], f2 = f * f;
+        neg |= f < 0.0;
+        double A = 0.0, B = 0.0;
+        for (int k = Pd.cls_ptr[c] + threadIdx.x; k < Pd.cls_ptr[c + 1]; k += 256) {
+            const int i = Pd.cls_idx[k];
+            const double s0 = Pd.sigma0[i], N = (s0 * s0 + q2) * f2 * 1e-12, iN = 1.0 / N, r = ri[i], rn = r * iN;
+            t1 += r * rn;
+            t2 += log(N);
+            S += rn;
+            V += iN;
+            double g = 0.5 * (rn * rn - iN);
+            const int e = nep ? Pd.toa_ep[i] : -1;
+            if (e >= 0) {
+                const double s = epsv[2 * (I.epoff + e)], v = epsv[2 * (I.epoff + e) + 1];
+                const double w = epw[I.epoff + e], den = 1.0 / (1.0 + w * v);
+                g += (-w * s * r * den + 0.5 * w * w * s * s * den * den + 0.5 * w * den) * iN * iN;
+            }
+            A += g * N;
+            B += g;
+        }
+        A = block_sum<4>(A, sh);
+        B = block_sum<4>(B, sh);
+        if (threadIdx.x == 0 && kind < 2) {
+            clsg[2 * (q0 + c)] = A;
+            clsg[2 * (q0 + c) + 1] = B;
+        }
+    }
+    t1 = block_sum<4>(t1, sh);
+    t2 = block_sum<4>(t2, sh);
+    S = block_sum<4>(S, sh);
+    V = block_sum<4>(V, sh);
+    ec = block_sum<4>(ec, sh);
+    el = block_sum<4>(el, sh);
+    ea = block_sum<4>(ea, sh);
+    eb = block_sum<4>(eb, sh);
+    if (threadIdx.x == 0) {
+        double chi2 = t1 - ec, ln = 0.5 * (t2 + el);
+        if (kind == 2) {
+            const double a = S - ea, b = 1e-40 + (V - eb);
+            chi2 -= a * a / b;
+            ln += 0.5 * (log(1e40) + log(b));
+        }
+        if (kind == 0 && neg) ln = __builtin_nan("");  // sum log sigma of a negative EFAC (residuals.py:666)
+        out[3 * inst] = -(0.5 * chi2 + ln);
+        out[3 * inst + 1] = chi2;
+        out[3 * inst + 2] = ln;
+    }
+}
+
 // Debug/parity introspection (pint_debug_gram): the assembled, unnormalised normal matrix
 // [M | r]^T N^-1 [M | r] of the last pint_fit_step in the original column order (the ECORR
 // block already eliminated by its Schur complement), (K+1)^2 per instance, followed by the K
@@ -2876,6 +2979,8 @@ struct pint_ctx {
     int* d_status_slots = nullptr;  // 2 status words on the device
     int* h_status = nullptr;        // their pinned host mirrors
     float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double* d_nz = nullptr;  // pint_noise_lnlike scratch (parameters, epoch sums, outputs)
+    size_t nz_cap = 0;
 };
 
 // Per-instance buffers (eval rows, design matrices, Gram partials: tens of GB for a large
@@ -3078,6 +3183,7 @@ void pint_ctx_destroy(pint_ctx* ctx) {
         for (auto b : p.bufs) hipFree(b);
     }
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
+    if (ctx->d_nz) hipFree(ctx->d_nz);
     if (ctx->d_status_slots) hipFree(ctx->d_status_slots);
     if (ctx->h_status) hipHostFree(ctx->h_status);
     for (int sl = 0; sl < 2; sl++) {
@@ -3285,6 +3391,17 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
     rc |= upload(ctx, ph, ep_ptr, (size_t)nep + 1, ph.dev.ep_ptr);
     rc |= upload(ctx, ph, ep_idx, (size_t)ep_ptr[nep], ph.dev.ep_idx);
     rc |= upload(ctx, ph, ep_phi, (size_t)nep, ph.dev.ep_phi);
+    {
+        std::vector<int32_t> te(ph.n, -1);
+        int overlap = 0;
+        for (int e = 0; e < nep; e++)
+            for (int k = ep_ptr[e]; k < ep_ptr[e + 1]; k++) {
+                overlap |= te[ep_idx[k]] >= 0;
+                te[ep_idx[k]] = e;
+            }
+        ph.dev.ep_overlap = overlap;
+        rc |= upload(ctx, ph, te.data(), (size_t)ph.n, ph.dev.toa_ep);
+    }
     if (rc) return PINT_E_HIP;
     ph.dev.nep = nep;
     ph.dev.dsplit = 0;  // the ECORR Schur rows span every column: keep the full layout
@@ -4323,6 +4440,138 @@ int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
     if (!ctx || ctx->ninst <= 0 || !time_resid) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_set_resids(pint_ctx* ctx, const double* time_resid) { return pint_debug_set_resids(ctx, time_resid); }
+
+// Replace the scaled TOA uncertainties (s) of pulsar psr in place: the weights of later
+// Gram / Woodbury / likelihood evaluations (a noise-parameter fit's trial EFAC/EQUAD,
+// fitter.py:1242-1247); the residuals on the device are left as they are.
+int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !sigma_s) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    PsrHost& ph = ctx->psrs[psr];
+    const int n = ph.n;
+    std::vector<double> is(n);
+    double ls = 0.0, sw = 0.0;
+    for (int i = 0; i < n; i++) {
+        if (!(sigma_s[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; return PINT_E_INVALID; }
+        is[i] = 1.0 / sigma_s[i];
+        ls += std::log(sigma_s[i]);
+        sw += is[i] * is[i];
+    }
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
+    HIPCHK(hipMemcpyAsync((void*)ph.dev.sigma, sigma_s, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync((void*)ph.dev.isig, is.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ph.dev.logsig = ls;
+    ph.dev.sumw = sw;
+    return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
+}
+
+// Replace the noise-basis prior variances of pulsar psr in place: red_phi (2 nred, the
+// PLRedNoise weights, s^2) and/or ep_phi (nep ECORR variances, s^2); either may be NULL.
+int pint_set_noise_weights(pint_ctx* ctx, int psr, const double* red_phi, const double* ep_phi) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size()) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    PsrHost& ph = ctx->psrs[psr];
+    const int nred = ph.spec.nred, nep = ph.dev.nep;
+    if (red_phi)
+        for (int k = 0; k < 2 * nred; k++)
+            if (!(red_phi[k] > 0.0)) { ctx->err = "red-noise weight must be > 0"; return PINT_E_INVALID; }
+    if (ep_phi)
+        for (int e = 0; e < nep; e++)
+            if (!(ep_phi[e] > 0.0)) { ctx->err = "ECORR weight must be > 0"; return PINT_E_INVALID; }
+    HIPCHK(hipStreamSynchronize(ctx->sstream));
+    if (red_phi && nred > 0)
+        HIPCHK(hipMemcpyAsync((void*)ph.dev.red_phi, red_phi, sizeof(double) * 2 * nred, hipMemcpyHostToDevice, ctx->stream));
+    if (ep_phi && nep > 0)
+        HIPCHK(hipMemcpyAsync((void*)ph.dev.ep_phi, ep_phi, sizeof(double) * nep, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_set_noise_classes(pint_ctx* ctx, int psr, int ncls, const int32_t* cls_ptr, const int32_t* cls_idx,
+                           const double* sigma0_us) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || ncls <= 0 || !cls_ptr || !cls_idx || !sigma0_us)
+        return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    PsrHost& ph = ctx->psrs[psr];
+    const int n = ph.n;
+    if (cls_ptr[0] != 0 || cls_ptr[ncls] != n) { ctx->err = "noise classes must cover every TOA once"; return PINT_E_INVALID; }
+    std::vector<int32_t> tc(n, -1);
+    for (int c = 0; c < ncls; c++) {
+        if (cls_ptr[c + 1] < cls_ptr[c]) { ctx->err = "bad noise class list"; return PINT_E_INVALID; }
+        for (int k = cls_ptr[c]; k < cls_ptr[c + 1]; k++) {
+            const int i = cls_idx[k];
+            if (i < 0 || i >= n || tc[i] >= 0) { ctx->err = "noise classes must cover every TOA once"; return PINT_E_INVALID; }
+            tc[i] = c;
+        }
+    }
+    for (int i = 0; i < n; i++)
+        if (!(sigma0_us[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; return PINT_E_INVALID; }
+    int rc = 0;
+    rc |= upload(ctx, ph, cls_ptr, (size_t)ncls + 1, ph.dev.cls_ptr);
+    rc |= upload(ctx, ph, cls_idx, (size_t)n, ph.dev.cls_idx);
+    rc |= upload(ctx, ph, tc.data(), (size_t)n, ph.dev.toa_cls);
+    rc |= upload(ctx, ph, sigma0_us, (size_t)n, ph.dev.sigma0);
+    if (rc) return PINT_E_HIP;
+    ph.dev.ncls = ncls;
+    return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
+}
+
+int pint_noise_lnlike(pint_ctx* ctx, const int32_t* kind, const double* cls_qf, const double* ep_w, double* out3,
+                      double* cls_g, double* ep_g) {
+    if (!ctx || ctx->ninst <= 0 || !kind || !cls_qf || !out3) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    const int ni = ctx->ninst;
+    std::vector<long> meta(3 * (size_t)ni);
+    long nq = 0;
+    bool any_ep = false;
+    for (int k = 0; k < ni; k++) {
+        const PsrDev& d = ctx->psrs[ctx->inst[k].psr].dev;
+        if (d.ncls <= 0) { ctx->err = "pint_noise_lnlike: no noise classes (pint_set_noise_classes)"; return PINT_E_INVALID; }
+        if (kind[k] < 0 || kind[k] > 2) { ctx->err = "pint_noise_lnlike: bad kind"; return PINT_E_INVALID; }
+        if (kind[k] > 0 && d.nep > 0) {
+            if (d.ep_overlap) { ctx->err = "pint_noise_lnlike: overlapping ECORR epochs"; return PINT_E_INVALID; }
+            any_ep = true;
+        }
+        meta[3 * k] = nq;
+        meta[3 * k + 1] = kind[k];
+        meta[3 * k + 2] = 0;
+        nq += d.ncls;
+    }
+    if (any_ep && !ep_w) { ctx->err = "pint_noise_lnlike: ECORR weights required"; return PINT_E_INVALID; }
+    const long nep = std::max<long>(1, ctx->tot_ep);
+    // scratch: meta (as doubles' storage) | qf 2nq | clsg 2nq | epw nep | epsv 2nep | epg nep | out 3ni
+    const size_t need = (size_t)3 * ni + 4 * nq + 4 * nep + 3 * ni;
+    if (need > ctx->nz_cap) {
+        if (ctx->d_nz) hipFree(ctx->d_nz);
+        ctx->d_nz = nullptr;
+        ctx->nz_cap = 0;
+        HIPCHK(hipMalloc(&ctx->d_nz, sizeof(double) * need));
+        ctx->nz_cap = need;
+    }
+    long* d_meta = (long*)ctx->d_nz;
+    double* d_q = ctx->d_nz + 3 * ni;
+    double* d_g = d_q + 2 * nq;
+    double* d_w = d_g + 2 * nq;
+    double* d_sv = d_w + nep;
+    double* d_eg = d_sv + 2 * nep;
+    double* d_out = d_eg + nep;
+    static_assert(sizeof(long) == sizeof(double), "meta packing");
+    HIPCHK(hipMemcpyAsync(d_meta, meta.data(), sizeof(long) * meta.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(d_q, cls_qf, sizeof(double) * 2 * nq, hipMemcpyHostToDevice, ctx->stream));
+    if (any_ep) HIPCHK(hipMemcpyAsync(d_w, ep_w, sizeof(double) * ctx->tot_ep, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_noise_lnl, dim3(ni), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt, d_meta,
+                       d_q, d_w, d_sv, d_out, d_g, d_eg);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out3, d_out, sizeof(double) * 3 * ni, hipMemcpyDeviceToHost, ctx->stream));
+    if (cls_g) HIPCHK(hipMemcpyAsync(cls_g, d_g, sizeof(double) * 2 * nq, hipMemcpyDeviceToHost, ctx->stream));
+    if (ep_g && ctx->tot_ep > 0)
+        HIPCHK(hipMemcpyAsync(ep_g, d_eg, sizeof(double) * ctx->tot_ep, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }

@@ -51,6 +51,7 @@ class PulsarLayout:
     ep_ptr: Optional[np.ndarray] = None
     ep_idx: Optional[np.ndarray] = None
     ep_phi: Optional[np.ndarray] = None
+    ep_param: Optional[list] = None  # the ECORR parameter of each epoch
 
 
 def _track_mode(model, toas, track_mode):
@@ -213,7 +214,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
     if use_gls_basis and "PLRedNoise" in model.components:
         rf, rp = red_noise_freqs_weights(model, toas)
         nred = len(rf)
-    ep_lists, ep_phi = [], []
+    ep_lists, ep_phi, ep_param = [], [], []
     if model.mask_params("ECORR") and use_gls_basis:
         from .noise import ecorr_epochs
         t = np.asarray(toas.tdbld * LD(86400))
@@ -223,6 +224,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
             for b in ecorr_epochs(t[idx]):
                 ep_lists.append(np.sort(idx[b]))
                 ep_phi.append((float(p.value) * 1e-6) ** 2)
+                ep_param.append(name)
     spec.nred = nred
     lay = PulsarLayout(model=model, toas=toas, n=toas.ntoas, offsets=offs, tstride=tstride, columns=cols,
                        spec=spec, nred=nred, K=len(cols) + 2 * nred, red_freq=rf, red_phi=rp, track_mode=tm)
@@ -231,6 +233,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         lay.ep_ptr = np.concatenate([[0], np.cumsum([len(e) for e in ep_lists])]).astype(np.int32)
         lay.ep_idx = np.concatenate(ep_lists).astype(np.int32)
         lay.ep_phi = np.asarray(ep_phi, dtype=np.float64)
+        lay.ep_param = ep_param
     return lay
 
 
@@ -681,6 +684,49 @@ class Session:
             w = lay.K + 1
             out.append((b[:w * w].reshape(w, w).copy(), b[w * w:].copy()))
         return out
+
+    # -- noise-parameter fits (fitter.py:1230-1273) -----------------------------------
+    def set_resids(self, resids):
+        """Replace every instance's time residuals (list of n-arrays, seconds)."""
+        self.debug_set_resids(resids)
+
+    def set_sigma(self, lay, sigma_s):
+        """Replace a pulsar's scaled TOA uncertainties (seconds) in place."""
+        sg = np.ascontiguousarray(sigma_s, dtype=np.float64)
+        if sg.shape != (lay.n,):
+            raise ValueError(f"sigma must have {lay.n} entries")
+        self._check(self.L.pint_set_sigma(self.ctx, lay.psr_id, L.ptr(sg)))
+
+    def set_noise_weights(self, lay, red_phi=None, ep_phi=None):
+        """Replace a pulsar's PLRedNoise (2 nred) and/or ECORR (nep) prior variances (s^2)."""
+        rp = None if red_phi is None else np.ascontiguousarray(red_phi, dtype=np.float64)
+        ep = None if ep_phi is None else np.ascontiguousarray(ep_phi, dtype=np.float64)
+        if rp is not None and rp.shape != (2 * lay.nred,):
+            raise ValueError(f"red_phi must have {2 * lay.nred} entries")
+        if ep is not None and ep.shape != (lay.nep,):
+            raise ValueError(f"ep_phi must have {lay.nep} entries")
+        self._check(self.L.pint_set_noise_weights(self.ctx, lay.psr_id, L.ptr(rp), L.ptr(ep)))
+
+    def set_noise_classes(self, lay, cls_ptr, cls_idx, sigma0_us):
+        cp = np.ascontiguousarray(cls_ptr, dtype=np.int32)
+        ci = np.ascontiguousarray(cls_idx, dtype=np.int32)
+        s0 = np.ascontiguousarray(sigma0_us, dtype=np.float64)
+        self._check(self.L.pint_set_noise_classes(self.ctx, lay.psr_id, len(cp) - 1, L.ptr(cp, C.c_int32),
+                                                  L.ptr(ci, C.c_int32), L.ptr(s0)))
+
+    def noise_lnlike(self, kinds, cls_qf, ep_w=None, grad=True):
+        """k_noise_lnl over the batch: (out [ninst, 3] = (lnL, chi2, logdet C / 2),
+        cls_g [sum ncls, 2], ep_g [sum nep]) -- see include/pint_amd.h pint_noise_lnlike."""
+        kd = np.ascontiguousarray(kinds, dtype=np.int32)
+        q = np.ascontiguousarray(cls_qf, dtype=np.float64).ravel()
+        w = None if ep_w is None else np.ascontiguousarray(ep_w, dtype=np.float64)
+        out = np.empty(3 * len(kd))
+        g = np.empty(q.size) if grad else None
+        nep = sum(l.nep for l in self.inst_layout)
+        eg = np.empty(max(nep, 1)) if grad else None
+        self._check(self.L.pint_noise_lnlike(self.ctx, L.ptr(kd, C.c_int32), L.ptr(q), L.ptr(w), L.ptr(out),
+                                             L.ptr(g), L.ptr(eg)))
+        return out.reshape(-1, 3), (g.reshape(-1, 2) if grad else None), (eg[:nep] if grad else None)
 
     def debug_set_resids(self, resids):
         """Replace every instance's time residuals (list of n-arrays, seconds)."""

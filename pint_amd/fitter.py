@@ -520,15 +520,50 @@ class GLSFitter(Fitter):
 class DownhillFitter(Fitter):
     mode = "wls"
 
-    def fit_toas(self, maxiter=10, required_chi2_decrease=1e-2, max_chi2_increase=1e-2, min_lambda=1e-3,
-                 debug=False, threshold=None, **kw):
-        # fitter.py:1168-1175: no free noise params -> required_chi2_decrease passed as
-        # both max_chi2_increase and min_lambda; threshold: WLSState (None -> 1e-14 max(N, P))
-        # or GLSState (fitter.py:1554 default 0)
+    def fit_toas(self, maxiter=20, noise_fit_niter=2, required_chi2_decrease=1e-2, max_chi2_increase=1e-2,
+                 min_lambda=1e-3, noisefit_method="Newton-CG", compute_noise_uncertainties=True, debug=False,
+                 threshold=None, **kw):
+        """fitter.py:1107-1204.  No free noise parameters: one downhill fit, with
+        required_chi2_decrease passed as both max_chi2_increase and min_lambda (a reference
+        quirk, fitter.py:1168-1175).  Free EFAC/EQUAD/ECORR/red-noise parameters: timing
+        fits alternate with noise-likelihood maximisations (pint_amd.noisefit.fit_noise, on
+        the device) noise_fit_niter times, then a final timing fit; the last noise fit also
+        sets the noise uncertainties when compute_noise_uncertainties.  Exceptions of the
+        timing fits (StepProblem, MaxiterReached) propagate as in the reference."""
+        from .noisefit import fit_noise
+        free_noise = self._get_free_noise_params()
+        if not free_noise:
+            return self._fit_toas(maxiter, required_chi2_decrease, required_chi2_decrease, required_chi2_decrease,
+                                  threshold)
+        for ii in range(noise_fit_niter):
+            self._fit_toas(maxiter, required_chi2_decrease, max_chi2_increase, min_lambda, threshold)
+            if ii == noise_fit_niter - 1 and compute_noise_uncertainties:
+                values, errors = fit_noise(self.toas, self.model, noisefit_method, uncertainty=True)
+                self._update_noise_params(values, errors)
+            else:
+                values = fit_noise(self.toas, self.model, noisefit_method, uncertainty=False)
+                self._update_noise_params(values)
+        return self._fit_toas(maxiter, required_chi2_decrease, max_chi2_increase, min_lambda, threshold)
+
+    def _get_free_noise_params(self):
+        """fitter.py:1210."""
+        from .noisefit import free_noise_params
+        return free_noise_params(self.model)
+
+    def _update_noise_params(self, values, errors=None):
+        """fitter.py:1218."""
+        for k, fp in enumerate(self._get_free_noise_params()):
+            self.model[fp].value = float(values[k])
+            if errors is not None:
+                self.model[fp].uncertainty_value = float(errors[k])
+
+    def _fit_toas(self, maxiter, required_chi2_decrease, max_chi2_increase, min_lambda, threshold=None):
+        """fitter.py:1023-1105 (threshold: WLSState None -> 1e-14 max(N, P), GLSState
+        fitter.py:1554 default 0)."""
         if threshold is None and self.mode == "gls":
             threshold = 0.0
         res = self._run(self.mode, plain=False, maxiter=maxiter, required_chi2_decrease=required_chi2_decrease,
-                        max_chi2_increase=required_chi2_decrease, min_lambda=required_chi2_decrease,
+                        max_chi2_increase=max_chi2_increase, min_lambda=min_lambda,
                         threshold=threshold, style="wls" if self.mode == "wls" else "glsstate")
         self.update_model(res.chi2)
         if res.status == "StepProblem":
