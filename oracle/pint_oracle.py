@@ -136,6 +136,11 @@ def select_mask(toas: dict, key: str, key_value, tzr=False) -> np.ndarray:
         if len(key_value) == 2:
             return (col >= float(key_value[0])) & (col <= float(key_value[1]))
         return col == float(key_value[0])
+    if kl == "tel":  # parameter.py:1868, :2156: canonical site names (fixture obs_names)
+        if tzr or "obs" not in toas:
+            return np.zeros(n, dtype=bool)
+        want = str(key_value[0]).lower()
+        return np.array([o == want or want in toas["obs_alias"].get(o, ()) for o in toas["obs"]], dtype=bool)
     k = key[1:] if key.startswith("-") else key
     fl = {} if tzr else toas.get("flags", {})
     if k not in fl:
@@ -158,6 +163,9 @@ def toas_from_fixture(z: dict, meta: dict) -> dict:
     if "pulse_number" in z:
         d["pulse_number"] = np.asarray(z["pulse_number"])
     d["flags"] = meta.get("flag_columns", {})
+    if "obs_index" in z and meta.get("obs_names"):
+        d["obs"] = [meta["obs_names"][i] for i in np.asarray(z["obs_index"])]
+        d["obs_alias"] = {k: [a.lower() for a in v] for k, v in meta.get("obs_aliases", {}).items()}
     d["tzr"] = {k[4:]: np.asarray(z[k]) for k in z if k.startswith("tzr_")}
     return d
 

@@ -13,6 +13,13 @@
                 one Residuals object, its model's noise values changed): wls_noise (diagonal N),
                 ecorr_phoff (ECORR Sherman-Morrison), j0740 (ECORR + offset column), pta_iso
                 and b1855 (Woodbury with PLRedNoise).
+* white_mjd   : tests/test_noisefit.py:10-22's white-noise pulsar (EFAC on mjd 50000-53000,
+                EQUAD on mjd 53000-55000, both free; EPHEM builtin for the offline run), 200
+                fake TOAs seed 11: DownhillWLSFitter fits from the par values and from
+                EFAC 1.5 / EQUAD 0.5 (test_white_noise_fit / test_white_noise_refit).
+* ecorr_fit   : tests/datafile/ecorr_fit_test.par/.tim (ECORR and EFAC on tel arecibo,
+                PHOFF free): DownhillGLSFitter fits from the par values and from ECORR 0.75
+                (test_ecorr_fit / test_ecorr_refit).
 compute_noise_uncertainties=False: the reference's Hessian needs numdifftools, which is not
 installed here.  Writes tests/golden/noise_fit.json.  Usage: run_ref.sh gen_noise.py
 """
@@ -84,6 +91,72 @@ def case(name, seed, ecorr, free_noise, fitter_cls, base_name):
                          else float(getattr(f.model, p).uncertainty_value)) for p in f.model.free_params}
     print(name, out["status"], out["chi2"], {p: out["params"][p][0] for p in free_noise}, file=sys.stderr)
     return out
+
+
+WHITE_MJD_PAR = """PSR WHITEMJD
+ELAT    1.3     1
+ELONG   2.5     1
+F0      100     1
+F1      1e-13   1
+PEPOCH  55000
+EPHEM   builtin
+EFAC mjd 50000 53000 2      1
+EQUAD mjd 53000 55000 0.8    1
+"""
+
+
+def fit_record(f, free_noise):
+    out = {}
+    try:
+        f.fit_toas(maxiter=5 if isinstance(f, DownhillWLSFitter) else 20, compute_noise_uncertainties=False)
+        out["status"] = "converged"
+    except Exception as e:
+        out["status"] = type(e).__name__
+    out["chi2"] = float(f.resids.chi2)
+    out["lnlikelihood"] = float(f.resids.lnlikelihood())
+    out["params"] = {p: list(map(float, split_ld(np.longdouble(getattr(f.model, p).value))))
+                     for p in f.model.free_params}
+    print(out["status"], out["chi2"], {p: out["params"][p][0] for p in free_noise}, file=sys.stderr)
+    return out
+
+
+def frozen_noise(m):
+    """The plain WLS/GLS fitters of capture() cannot take free noise parameters
+    (fitter.py:2074): the fixture's free list is the timing parameters; tests free them."""
+    m = copy.deepcopy(m)
+    for p in m.free_params:
+        if p.startswith(("EFAC", "EQUAD", "ECORR")):
+            getattr(m, p).frozen = True
+    return m
+
+
+def gen_datafile_cases():
+    from refcommon import REFDATA
+    import pint.toa as toa
+    res = {}
+    np.random.seed(11)
+    m = get_model(io.StringIO(WHITE_MJD_PAR))
+    t = sim.make_fake_toas_uniform(50000, 55000, 200, m, add_noise=True, include_bipm=False)
+    with open(os.path.join(GOLDEN, "white_mjd.par"), "w") as f:
+        f.write(WHITE_MJD_PAR)
+    capture("white_mjd", frozen_noise(m), t, fit="wls")
+    free = ["EFAC1", "EQUAD1"]
+    res["white_mjd"] = {"free_noise": free, "fit": fit_record(DownhillWLSFitter(t, copy.deepcopy(m)), free)}
+    m2 = copy.deepcopy(m)
+    m2.EFAC1.value, m2.EQUAD1.value = 1.5, 0.5
+    res["white_mjd"]["refit"] = fit_record(DownhillWLSFitter(t, m2), free)
+    m = get_model(f"{REFDATA}/ecorr_fit_test.par")
+    t = toa.get_TOAs(f"{REFDATA}/ecorr_fit_test.tim", ephem="builtin", include_bipm=False, planets=False, model=m)
+    with open(f"{REFDATA}/ecorr_fit_test.par") as fi, open(os.path.join(GOLDEN, "ecorr_fit.par"), "w") as fo:
+        fo.write(fi.read())
+    capture("ecorr_fit", frozen_noise(m), t, fit="gls")
+    free = ["ECORR1", "EFAC1"]
+    res["ecorr_fit"] = {"free_noise": free, "truth": {"ECORR1": float(m.ECORR1.value), "EFAC1": float(m.EFAC1.value)},
+                        "fit": fit_record(DownhillGLSFitter(t, copy.deepcopy(m)), free)}
+    m2 = copy.deepcopy(m)
+    m2.ECORR1.value = 0.75
+    res["ecorr_fit"]["refit"] = fit_record(DownhillGLSFitter(t, m2), free)
+    return res
 
 
 def perturbations(model):
@@ -170,5 +243,6 @@ if __name__ == "__main__":
     res = {"wls_noise": case("wls_noise", 7, False, ["EFAC1", "EQUAD1"], DownhillWLSFitter, "wls_noise"),
            "ecorr_noise": case("ecorr_noise", 6, True, ["EFAC1", "ECORR1"], DownhillGLSFitter, "ecorr_phoff"),
            "lnl_points": all_lnl_points()}
+    res.update(gen_datafile_cases())
     with open(os.path.join(GOLDEN, "noise_fit.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)

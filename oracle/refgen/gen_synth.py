@@ -121,6 +121,11 @@ def capture(name, model, toas, fit="gls", n_dm_rows=None):
     no, nm = noise_outputs(model, toas)
     arrays.update(no)
     meta = {"name": name, "model": export_model(model), "flags": flags}
+    obs = [str(o) for o in toas.get_obss()]
+    meta["obs_names"] = sorted(set(obs))
+    arrays["obs_index"] = np.array([meta["obs_names"].index(o) for o in obs], dtype=np.int16)
+    from pint.observatory import get_observatory
+    meta["obs_aliases"] = {o: list(get_observatory(o).aliases) for o in meta["obs_names"]}
     meta.update(rm)
     meta.update(dmm)
     meta.update(nm)

@@ -198,7 +198,7 @@ _DEFS = {
 _ALIASES = {
     "RA": "RAJ", "DEC": "DECJ", "LAMBDA": "ELONG", "BETA": "ELAT", "PMLAMBDA": "PMELONG",
     "PMBETA": "PMELAT", "E": "ECC", "ECCDOT": "EDOT", "XDOT": "A1DOT", "T2EFAC": "EFAC",
-    "T2EQUAD": "EQUAD", "TNECORR": "ECORR", "SOLARN0": "NE_SW", "CLK": "CLOCK",
+    "T2EQUAD": "EQUAD", "TNECORR": "ECORR", "SOLARN0": "NE_SW", "CLK": "CLOCK", "PSRJ": "PSR", "PSRB": "PSR",
 }
 
 _PREFIX = {  # prefix params: regex -> (component, units template, long_double)

@@ -202,7 +202,15 @@ def parfile_line(p: Param) -> str:
     name = _display_name(p)
     if p.kind == "mask":
         line = "%-15s %s " % (name, p.key)
+        kl = p.key.lower()
         for kv in p.key_value:
+            # parameter.py:1864-1869 key_identifier: mjd/freq keys are floats (MHz), tel the
+            # canonical site name
+            if kl in ("mjd", "freq"):
+                kv = str(float(kv))
+            elif kl == "tel":
+                from .observatory import get_observatory_name
+                kv = get_observatory_name(kv)
             line += f"{kv} "
         line += "%25s" % value_string(p)
     else:

@@ -293,7 +293,7 @@ def get_model(parfile) -> TimingModel:
                      ("PMELAT", 0.0), ("ECL", "IERS2010")]
     defaults += [("F0", None), ("PEPOCH", None)]
     # top-level parameters every reference model carries (timing_model.py:330-350)
-    defaults += [("DILATEFREQ", False), ("DMDATA", False), ("NTOA", 0)]
+    defaults += [("DILATEFREQ", False), ("DMDATA", False), ("NTOA", 0), ("UNITS", "TDB")]
     if has_eq or has_ecl:
         defaults += [("PLANET_SHAPIRO", False)]
     if any(n in ("NE_SW", "SOLARN0") for n in names):

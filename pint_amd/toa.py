@@ -25,7 +25,7 @@ FIELDS = ["tdb_hi", "tdb_lo", "freq_mhz", "err_us", "ssb_obs_pos_km", "ssb_obs_v
 
 class TOAs:
     def __init__(self, arrays: Dict[str, np.ndarray], flag_columns: Optional[Dict[str, List[str]]] = None,
-                 tzr: Optional[Dict[str, np.ndarray]] = None, name: str = ""):
+                 tzr: Optional[Dict[str, np.ndarray]] = None, name: str = "", obs: Optional[List[str]] = None):
         self.arrays = {k: np.asarray(v) for k, v in arrays.items()}
         n = len(self.arrays["tdb_hi"])
         self.flag_columns = {k: list(v) for k, v in (flag_columns or {}).items()}
@@ -38,6 +38,10 @@ class TOAs:
             self.arrays["is_bary"] = np.zeros(n, dtype=np.uint8)
         self.tzr = tzr
         self.name = name
+        # observatory (canonical site name) of each TOA, when known: TEL masks select on it
+        self.obs = None if obs is None else np.asarray([str(o) for o in obs], dtype=object)
+        if self.obs is not None and len(self.obs) != n:
+            raise ValueError(f"obs has {len(self.obs)} rows, expected {n}")
         self.ephem = None   # the host preparation's ephemeris / clock chain, when known
         self.clock = None   # (update_model writes them into the model as EPHEM / CLOCK)
         self._uid = id(self)
@@ -81,7 +85,13 @@ class TOAs:
         idx = np.arange(self.ntoas)[idx]
         arr = {k: v[idx] for k, v in self.arrays.items()}
         fl = {k: [v[i] for i in idx] for k, v in self.flag_columns.items()}
-        return TOAs(arr, fl, self.tzr, self.name)
+        return TOAs(arr, fl, self.tzr, self.name, None if self.obs is None else self.obs[idx])
+
+    def get_obss(self):
+        """Site name of each TOA (toa.py get_obss)."""
+        if self.obs is None:
+            raise ValueError("these TOAs carry no observatory names")
+        return self.obs
 
     # -- mask selection (parameter.py:2124 select_toa_mask, toa_select.py:101) ----------
     def select_mask(self, key: str, key_value: List[str], tzr: bool = False) -> np.ndarray:
@@ -89,10 +99,18 @@ class TOAs:
         TOA instead (returns [0] or [])."""
         k = key[1:] if key.startswith("-") else key
         kl = key.lower()
-        if kl in ("mjd", "freq", "tel"):
-            col = {"mjd": "mjd_float", "freq": "freq_mhz"}.get(kl)
-            if col is None:
-                raise NotImplementedError("TEL masks need observatory names (not in the packed schema)")
+        if kl == "tel":  # parameter.py:1868 / :2156: the canonical site name vs the obs column
+            from .observatory import get_observatory_name
+            site = get_observatory_name(key_value[0])
+            if tzr:
+                o = (self.tzr or {}).get("obs")
+                return np.array([0]) if o is not None and get_observatory_name(str(np.atleast_1d(o)[0])) == site \
+                    else np.array([], dtype=int)
+            if self.obs is None:
+                raise NotImplementedError("TEL masks need the TOAs' observatory names")
+            return np.where(self.obs == site)[0]
+        if kl in ("mjd", "freq"):
+            col = {"mjd": "mjd_float", "freq": "freq_mhz"}[kl]
             src = (self.tzr or {}).get(col, np.zeros(0)) if tzr else self.arrays[col]
             src = np.asarray(src, dtype=float)
             if len(key_value) == 2:
@@ -113,34 +131,42 @@ class TOAs:
     def save(self, path: str):
         base = path[:-4] if path.endswith(".npz") else path
         arr = dict(self.arrays)
+        names = None
+        if self.obs is not None:
+            names = sorted(set(self.obs.tolist()))
+            arr["obs_index"] = np.array([names.index(o) for o in self.obs], dtype=np.int16)
         if self.tzr:
             arr.update({"tzr_" + k: np.atleast_1d(v) for k, v in self.tzr.items() if k != "flags"})
         np.savez_compressed(base + ".npz", **arr)
         with open(base + ".json", "w") as f:
-            json.dump({"flag_columns": self.flag_columns, "name": self.name}, f)
+            json.dump({"flag_columns": self.flag_columns, "name": self.name, "obs_names": names}, f)
 
 
-def from_arrays_with_tzr(z: Dict[str, np.ndarray], flag_columns=None, name="") -> TOAs:
+def from_arrays_with_tzr(z: Dict[str, np.ndarray], flag_columns=None, name="", obs_names=None) -> TOAs:
     arrays = {k: np.asarray(z[k]) for k in z if not k.startswith("tzr_") and (k in FIELDS or k in (
         "pulse_number", "ssb_obs_vel_ecl_kms"))}
     tzr = None
     if "tzr_tdb_hi" in z:
         tzr = {k[4:]: np.asarray(z[k]) for k in z if k.startswith("tzr_")}
         tzr["flags"] = {}
-    return TOAs(arrays, flag_columns, tzr, name)
+    obs = None
+    if obs_names is not None and "obs_index" in z:
+        obs = [obs_names[i] for i in np.asarray(z["obs_index"])]
+    return TOAs(arrays, flag_columns, tzr, name, obs)
 
 
 def get_TOAs(path: str, **kwargs) -> TOAs:
     """Load packed TOAs (``.npz`` + optional ``.json`` with ``flag_columns``)."""
     base = path[:-4] if path.endswith(".npz") else path
     z = dict(np.load(base + ".npz", allow_pickle=False))
-    fl, name = None, os.path.basename(base)
+    fl, name, obs = None, os.path.basename(base), None
     if os.path.exists(base + ".json"):
         with open(base + ".json") as f:
             meta = json.load(f)
         fl = meta.get("flag_columns")
         name = meta.get("name", name)
-    return from_arrays_with_tzr(z, fl, name)
+        obs = meta.get("obs_names")
+    return from_arrays_with_tzr(z, fl, name, obs)
 
 
 def get_model_and_toas(parfile: str, timfile: str, **kwargs):

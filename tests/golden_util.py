@@ -7,7 +7,8 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "j0740": "J0740+6620.par",
         "pta_iso": "pta_iso.par", "pta_ell1": "pta_ell1.par", "pta_dd": "pta_dd.par",
-        "wls_phoff": "wls_phoff.par", "ecorr_phoff": "ecorr_phoff.par", "wls_noise": "wls_noise.par"}
+        "wls_phoff": "wls_phoff.par", "ecorr_phoff": "ecorr_phoff.par", "wls_noise": "wls_noise.par",
+        "ecorr_fit": "ecorr_fit.par", "white_mjd": "white_mjd.par"}
 
 
 def load(name):
@@ -15,7 +16,7 @@ def load(name):
     from pint_amd.toa import from_arrays_with_tzr
     z = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
     meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
-    toas = from_arrays_with_tzr(z, meta["flag_columns"], name)
+    toas = from_arrays_with_tzr(z, meta["flag_columns"], name, meta.get("obs_names"))
     model = get_model(os.path.join(GOLDEN, PARS[name]))
     free = [p for p in meta["model"]["free_params"]]
     model.free_params = [p for p in free if p in model]

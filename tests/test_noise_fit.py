@@ -262,3 +262,54 @@ def test_noise_uncertainties_degenerate():
     f.fit_toas(maxiter=10, compute_noise_uncertainties=True)
     errs = [f.model[p].uncertainty_value for p in ("EFAC1", "EQUAD1")]
     assert all(e is not None and np.isfinite(e) and e > 1.0 for e in errs), errs
+
+
+# ---------------------------------------------------------------------------------------
+# the reference's own noise-fit tests (tests/test_noisefit.py) on their inputs
+# ---------------------------------------------------------------------------------------
+def _fit_case(name, fitter, start=None, maxiter=None):
+    import pint_amd.fitter as F
+    model, toas, z, meta = load(name)
+    ref = NOISE[name]
+    for p in ref["free_noise"]:
+        model[p].frozen = False
+    for p, v in (start or {}).items():
+        model[p].value = v
+    f = getattr(F, fitter)(toas, model)
+    f.fit_toas(**({"maxiter": maxiter} if maxiter else {}))
+    return f, ref
+
+
+def _check_against(f, rec, free, tol):
+    assert rec["status"] == "converged"
+    for p in free:
+        v, rv = float(f.model[p].value), rec["params"][p][0]
+        assert abs(v - rv) < tol * abs(rv), (p, v, rv)
+    assert abs(f.resids.chi2 - rec["chi2"]) < 1e-4 * rec["chi2"], (f.resids.chi2, rec["chi2"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("start", [None, {"EFAC1": 1.5, "EQUAD1": 0.5}])
+def test_white_noise_fit_mjd_masks(start):
+    """test_noisefit.py:29-67 (test_white_noise_fit / _refit): EFAC on an MJD range and EQUAD
+    on another, fitted with uncertainties; within 4 sigma of the simulated values and equal
+    to the reference's fit (its run without uncertainties: numdifftools is absent)."""
+    f, ref = _fit_case("white_mjd", "DownhillWLSFitter", start, maxiter=5)
+    for p, truth in (("EFAC1", 2.0), ("EQUAD1", 0.8)):
+        err = f.model[p].uncertainty_value
+        assert err is not None and err > 0
+        assert abs(float(f.model[p].value) - truth) / err < 4, (p, f.model[p].value, err)
+    _check_against(f, ref["refit" if start else "fit"], ref["free_noise"], 3e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("start", [None, {"ECORR1": 0.75}])
+def test_ecorr_fit_tel_masks(start):
+    """test_noisefit.py:70-94 (test_ecorr_fit / _refit) on ecorr_fit_test.par/.tim: ECORR and
+    EFAC on 'tel arecibo' with PHOFF free, Nelder-Mead on the Sherman-Morrison likelihood.
+    The fixture's TOAs were prepared with the builtin ephemeris (offline), so the epoch-
+    correlated ephemeris error moves ECORR far from the value the data file was simulated
+    with; the check is against the reference's own fit of the same TOAs."""
+    f, ref = _fit_case("ecorr_fit", "DownhillGLSFitter", start)
+    assert f.model["ECORR1"].uncertainty_value > 0
+    _check_against(f, ref["refit" if start else "fit"], ref["free_noise"], 3e-4)

@@ -10,7 +10,7 @@ from golden_util import GOLDEN
 
 import pint_oracle as O
 
-NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise"]
+NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise", "white_mjd", "ecorr_fit"]
 DELAY_MAP = {"delay_solar_system_geometric_delay": "geometric", "delay_solar_system_shapiro_delay": "shapiro",
              "delay_constant_dispersion_delay": "dm", "delay_DMX_dispersion_delay": "dmx",
              "delay_binarymodel_delay": "binary", "delay_FD_delay": "fd", "delay_total": "delay"}
