@@ -263,7 +263,7 @@ def pack_toas(lay: PulsarLayout):
     model, toas = lay.model, lay.toas
     n = toas.ntoas
     A = toas.arrays
-    tz = toas.tzr if "AbsPhase" in model.components else None
+    tz = (toas.tzr_for(model) if hasattr(toas, "tzr_for") else toas.tzr) if "AbsPhase" in model.components else None
     if tz is None:
         tz = make_tzr_row(model, toas)
 

@@ -38,6 +38,8 @@ class TOAs:
             self.arrays["is_bary"] = np.zeros(n, dtype=np.uint8)
         self.tzr = tzr
         self.name = name
+        self.prepared = None  # tim-file TOAs: the preparation options (TZR TOAs are prepared alike)
+        self.commands = []
         # observatory (canonical site name) of each TOA, when known: TEL masks select on it
         self.obs = None if obs is None else np.asarray([str(o) for o in obs], dtype=object)
         if self.obs is not None and len(self.obs) != n:
@@ -86,6 +88,19 @@ class TOAs:
         arr = {k: v[idx] for k, v in self.arrays.items()}
         fl = {k: [v[i] for i in idx] for k, v in self.flag_columns.items()}
         return TOAs(arr, fl, self.tzr, self.name, None if self.obs is None else self.obs[idx])
+
+    def tzr_for(self, model):
+        """The TZR TOA row of ``model`` (absolute_phase.py:79-127 get_TZR_toa): the stored one
+        (packed fixtures), else -- for TOAs prepared from a tim file -- TZRMJD at TZRSITE with
+        TZRFRQ prepared with the same options, cached on (TZRMJD, TZRSITE, TZRFRQ)."""
+        if self.tzr is not None or self.prepared is None or "TZRMJD" not in model or model.TZRMJD.value is None:
+            return self.tzr
+        key = (str(model.TZRMJD.value), str(model.TZRSITE.value) if "TZRSITE" in model else None,
+               None if "TZRFRQ" not in model or model.TZRFRQ.value is None else float(model.TZRFRQ.value))
+        cache = self.prepared.setdefault("tzr_cache", {})
+        if key not in cache:
+            cache[key] = tzr_row(model, self.prepared)
+        return cache[key]
 
     def get_obss(self):
         """Site name of each TOA (toa.py get_obss)."""
@@ -155,8 +170,120 @@ def from_arrays_with_tzr(z: Dict[str, np.ndarray], flag_columns=None, name="", o
     return TOAs(arrays, flag_columns, tzr, name, obs)
 
 
-def get_TOAs(path: str, **kwargs) -> TOAs:
-    """Load packed TOAs (``.npz`` + optional ``.json`` with ``flag_columns``)."""
+def _is_tim(path) -> bool:
+    if hasattr(path, "readlines"):
+        return True
+    p = str(path)
+    return not (p.endswith(".npz") or os.path.exists(p + ".npz"))
+
+
+def _ephem_choice(ephem, model):
+    if ephem is None and model is not None and "EPHEM" in model and model.EPHEM.value:
+        ephem = str(model.EPHEM.value)
+    ephem = "builtin" if ephem is None else ephem
+    if str(ephem).lower() != "builtin":
+        raise NotImplementedError(
+            f"ephemeris {ephem!r} is not available offline: only the 'builtin' (erfa epv00) table is bundled "
+            "(pass ephem='builtin')")
+    return "builtin"
+
+
+def _bipm_choice(include_bipm, model):
+    """toa.py:196-225: CLOCK = TT(TAI) or UNCORR -> no BIPM correction."""
+    if include_bipm is None and model is not None and "CLOCK" in model and model.CLOCK.value:
+        clk = str(model.CLOCK.value)
+        if clk in ("TT(TAI)", "UNCORR"):
+            include_bipm = False
+    if include_bipm is None:
+        include_bipm = True
+    if include_bipm:
+        raise NotImplementedError("the TT(BIPM) clock table is not bundled: pass include_bipm=False "
+                                  "(TT(TAI)), as the model's CLOCK = TT(TAI) does")
+    return False
+
+
+def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, include_pn=True,
+             clock_files=None) -> TOAs:
+    """get_TOAs for a tim file (toa.py:109-330) without PINT/astropy: read (pint_amd.tim),
+    clock corrections (TIME statements as -to flags, plus optional per-site clock files,
+    pint_amd.clock), TDB and posvels (pint_amd.prep), pulse numbers and PHASE/-padd
+    (toa.py:1959-1983).  Options follow the reference (EPHEM/CLOCK from the model); only the
+    builtin ephemeris is available offline, and BIPM corrections are not bundled."""
+    from . import prep
+    from .tim import read_tim
+    ephem = _ephem_choice(ephem, model)
+    _bipm_choice(include_bipm, model)
+    if planets is None:
+        planets = bool(model is not None and "PLANET_SHAPIRO" in model and model.PLANET_SHAPIRO.value)
+    if planets:
+        raise NotImplementedError("planet positions are outside the supported hot path (PLANET_SHAPIRO)")
+    recs, commands = read_tim(timfile)
+    if not recs:
+        raise ValueError("No TOAs found!")
+    n = len(recs)
+    day = np.array([r.imjd for r in recs], dtype=np.float64)
+    frac = np.array([r.fmjd for r in recs], dtype=np.float64)
+    obs = [r.obs for r in recs]
+    flags = [dict(r.flags) for r in recs]
+    corr = np.array([float(f.get("to", 0.0)) for f in flags])
+    if clock_files:
+        from .clock import site_corrections
+        corr = corr + site_corrections(clock_files, obs, day + frac)
+    for f, c in zip(flags, corr):
+        if c != 0:
+            f["clkcorr"] = str(c)
+    cols = prep.prepare(day, frac, obs, corr)
+    cols["freq_mhz"] = np.array([r.freq_mhz for r in recs], dtype=np.float64)
+    cols["err_us"] = np.array([r.error_us for r in recs], dtype=np.float64)
+    # phase_columns_from_flags (toa.py:1959-1983)
+    dph = np.array([float(f.get("phase", 0)) + float(f.get("padd", 0)) for f in flags])
+    cols["delta_pulse_number"] = dph
+    pns = np.array([float(f.get("pn", np.nan)) for f in flags])
+    if include_pn and not np.all(np.isnan(pns)):
+        cols["pulse_number"] = pns
+    for f in flags:
+        f.pop("pn", None)
+        f.pop("padd", None)
+    keys = list(dict.fromkeys(k for f in flags for k in f))
+    fc = {k: [f.get(k, "") for f in flags] for k in keys}
+    name = getattr(timfile, "name", None) or os.path.basename(str(timfile))
+    t = TOAs(cols, fc, None, name, obs)
+    t.ephem = ephem
+    t.clock = "TT(TAI)"
+    t.commands = commands
+    t.prepared = {"ephem": ephem, "include_bipm": False, "clock_files": clock_files}
+    return t
+
+
+def tzr_row(model, prepared) -> dict:
+    """get_TZR_toa (absolute_phase.py:79-127) prepared like the TOAs: TZRMJD (its parsed
+    day + fraction) at TZRSITE (default barycenter) with TZRFRQ (none/0 -> infinite)."""
+    from . import prep
+    from .observatory import get_observatory_name
+    p = model.TZRMJD
+    day, frac = p.mjd_pair if p.mjd_pair is not None else (float(np.floor(p.value)), float(p.value - np.floor(p.value)))
+    site = get_observatory_name(model.TZRSITE.value if "TZRSITE" in model and model.TZRSITE.value else "ssb")
+    fr = float(model.TZRFRQ.value) if "TZRFRQ" in model and model.TZRFRQ.value is not None else np.inf
+    if fr == 0.0:
+        fr = np.inf
+    corr = None
+    if prepared.get("clock_files"):
+        from .clock import site_corrections
+        corr = site_corrections(prepared["clock_files"], [site], np.array([day + frac]))
+    cols = prep.prepare(np.array([day]), np.array([frac]), [site], corr)
+    cols["freq_mhz"] = np.array([fr])
+    cols["delta_pulse_number"] = np.zeros(1)
+    cols["flags"] = {}
+    cols["obs"] = np.array([site])
+    return cols
+
+
+def get_TOAs(path, ephem=None, include_bipm=None, planets=None, include_pn=True, model=None, **kwargs) -> TOAs:
+    """Load TOAs (toa.py:109 get_TOAs): a tim file is read and prepared on the host
+    (load_tim); a packed ``.npz`` (+ optional ``.json`` with ``flag_columns``) is loaded as is."""
+    if _is_tim(path):
+        return load_tim(path, model=model, ephem=ephem, include_bipm=include_bipm, planets=planets,
+                        include_pn=include_pn, clock_files=kwargs.get("clock_files"))
     base = path[:-4] if path.endswith(".npz") else path
     z = dict(np.load(base + ".npz", allow_pickle=False))
     fl, name, obs = None, os.path.basename(base), None
@@ -169,7 +296,11 @@ def get_TOAs(path: str, **kwargs) -> TOAs:
     return from_arrays_with_tzr(z, fl, name, obs)
 
 
-def get_model_and_toas(parfile: str, timfile: str, **kwargs):
-    """Reference API (model_builder.py:859).  ``timfile`` must be a packed TOA file."""
+def get_model_and_toas(parfile: str, timfile: str, ephem=None, include_bipm=None, planets=None,
+                       include_pn=True, **kwargs):
+    """Reference API (model_builder.py:859): the model, then its TOAs prepared with the
+    model's EPHEM/CLOCK/PLANET_SHAPIRO (a tim file) or loaded packed (``.npz``)."""
     from .timing_model import get_model
-    return get_model(parfile), get_TOAs(timfile)
+    m = get_model(parfile)
+    return m, get_TOAs(timfile, ephem=ephem, include_bipm=include_bipm, planets=planets, include_pn=include_pn,
+                       model=m, **kwargs)

@@ -1,0 +1,196 @@
+"""Host TOA preparation: tim reading, clock corrections, TT/TDB and the
+observatory/Earth/Sun vectors, against the reference's own get_TOAs on the same tim files
+(tests/golden/prep_*.npz/.json.gz by oracle/refgen/gen_prep.py: ephem builtin, no BIPM,
+clockless sites).  CPU, plus one GPU test that fits from a tim file end to end."""
+import gzip
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN
+import pint_oracle as O
+
+LD = np.longdouble
+CASES = {"ngc6440e": ("NGC6440E.tim", "NGC6440E.par"), "b1855": ("B1855+09_NANOGrav_9yv1.tim.gz",
+                                                                 "B1855+09_NANOGrav_9yv1.gls.par"),
+         "mixed": ("prep_mixed.tim", None)}
+
+
+def _ref(name):
+    z = dict(np.load(os.path.join(GOLDEN, f"prep_{name}.npz"), allow_pickle=False))
+    meta = json.load(gzip.open(os.path.join(GOLDEN, f"prep_{name}.json.gz"), "rt"))
+    return z, meta
+
+
+def _load(name, with_model=True):
+    from pint_amd import get_model
+    from pint_amd.toa import load_tim
+    tim, par = CASES[name]
+    m = get_model(os.path.join(GOLDEN, par)) if (par and with_model) else None
+    return m, load_tim(os.path.join(GOLDEN, tim), model=m, ephem="builtin", include_bipm=False)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_tim_reader(name):
+    """read_toa_file/_parse_TOA_line (toa.py:441-858): every TOA's site, error, frequency
+    and flag dict (implicit format/name/ddm, -to/-phase/-jump/-info from commands, EFAC/EQUAD
+    commands, EMIN/FMIN filters, SKIP, INCLUDE, pn/padd removed) and the command list."""
+    from pint_amd.tim import read_tim
+    z, meta = _ref(name)
+    recs, cmds = read_tim(os.path.join(GOLDEN, CASES[name][0]))
+    assert [r.obs for r in recs] == meta["obs"]
+    _, t = _load(name)
+    mine = [{k: v[i] for k, v in t.flag_columns.items() if v[i] != ""} for i in range(t.ntoas)]
+    assert mine == meta["flags"]
+    assert np.array_equal(t.arrays["err_us"], z["err_us"])
+    assert np.array_equal(t.arrays["freq_mhz"], z["freq_mhz"])
+    assert np.array_equal(t.arrays["delta_pulse_number"], z["delta_pulse_number"])
+    if "pulse_number" in z:
+        assert np.array_equal(t.arrays["pulse_number"], z["pulse_number"], equal_nan=True)
+    ref_cmds = [(c[0][0], c[1]) for c in meta["commands"]]
+    assert [(c[0][0], c[1]) for c in cmds] == ref_cmds
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_time_scales(name):
+    """UTC -> TT -> TDB (compute_TDBs, toa.py:2251: astropy Time.tdb with the site's
+    location): TT and TDB within 1 ns (measured 0.31 ns: one longdouble ulp of the MJD),
+    mjd_float exact."""
+    from pint_amd import prep
+    z, meta = _ref(name)
+    _, t = _load(name)
+    A = t.arrays
+    tdb = LD(A["tdb_hi"]) + LD(A["tdb_lo"])
+    ref = LD(z["tdb_hi"]) + LD(z["tdb_lo"])
+    assert float(np.max(np.abs(tdb - ref))) * 86400 < 1e-9
+    assert np.array_equal(A["mjd_float"], z["mjd_float"])
+    topo = np.array([o != "barycenter" for o in meta["obs"]])
+    utc = LD(z["utc_jd1"]) - LD(2400000.5) + LD(z["utc_jd2"])
+    day = np.floor(utc.astype(np.float64))
+    tt = prep.utc_to_tt(day, (utc - LD(day)).astype(np.float64))
+    ttref = LD(z["tt_jd1"]) - LD(2400000.5) + LD(z["tt_jd2"])
+    assert float(np.max(np.abs((tt - ttref)[topo]))) * 86400 < 1e-9
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_posvels(name):
+    """compute_posvels (toa.py:2323): Earth (builtin epv00) + the site's GCRS vector (astropy
+    get_gcrs_posvel: CIP X/Y/s, ERA of UT1, polar motion) and the Sun: positions within 10 cm
+    (measured 1.2 cm, 0.04 ns of light time), velocities within 1e-9 km/s."""
+    from pint_amd import prep
+    z, meta = _ref(name)
+    _, t = _load(name)
+    A = t.arrays
+    for k, tol in (("ssb_obs_pos_km", 1e-4), ("obs_sun_pos_km", 1e-4), ("ssb_obs_vel_kms", 1e-9)):
+        assert np.max(np.abs(A[k] - z[k])) < tol, (k, np.max(np.abs(A[k] - z[k])))
+    tdb = LD(z["tdb_hi"]) + LD(z["tdb_lo"])
+    ep, ev = prep.earth_posvel(tdb.astype(np.float64))
+    assert np.max(np.abs(ep - z["earth_pos_km"])) < 1e-4 and np.max(np.abs(ev - z["earth_vel_kms"])) < 1e-9
+    obs = np.array(meta["obs"])
+    for site in set(obs) - {"barycenter", "geocenter"}:
+        sel = obs == site
+        gp, gv = prep.site_gcrs_posvel(prep.site_info(site)["itrf"], tdb[sel])
+        assert np.max(np.abs(gp - z["gcrs_pos_km"][sel])) < 1e-6     # 1 mm
+        assert np.max(np.abs(gv - z["gcrs_vel_kms"][sel])) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["ngc6440e", "b1855"])
+def test_tzr_toa_and_residuals(name):
+    """get_TZR_toa (absolute_phase.py:79-127) prepared like the TOAs, and the oracle's
+    residuals of the prepared TOAs against the reference's residuals (fixture <name>.npz):
+    within 1 ns (measured 0.2 / 0.4 ns)."""
+    z, meta = _ref(name)
+    m, t = _load(name)
+    tz = t.tzr_for(m)
+    d = (LD(tz["tdb_hi"]) + LD(tz["tdb_lo"])) - (LD(z["tzr_tdb_hi"]) + LD(z["tzr_tdb_lo"]))
+    assert float(abs(d[0])) * 86400 < 1e-9
+    assert np.max(np.abs(tz["ssb_obs_pos_km"] - z["tzr_ssb_obs_pos_km"])) < 1e-4
+    assert tz["freq_mhz"][0] == z["tzr_freq_mhz"][0]
+    fx = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    fmeta = json.load(open(os.path.join(GOLDEN, f"{name}.json")))
+    ot = O.toas_from_product(t)
+    ot["tzr"] = {k: np.asarray(v) for k, v in tz.items() if k not in ("flags", "obs")}
+    r = O.residuals(O.from_fixture(fmeta), ot)
+    assert np.max(np.abs(r["time"] - fx["res_time"])) < 1e-9
+
+
+def test_clock_file():
+    """read_tempo2_clock_file + ClockFile.evaluate (clock_file.py:432-546, :143-188) on the
+    reference's wsrt2gps.clk: rows, interpolation and end clamping."""
+    from pint_amd import clock
+    ref = json.load(open(os.path.join(GOLDEN, "prep_clock.json")))
+    path = os.path.join(GOLDEN, ref["file"])
+    t, c = clock.read_tempo2_clock_file(path)
+    assert len(t) == ref["n"] and t[0] == ref["first"] and t[-1] == ref["last"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        v = clock.evaluate(path, np.array(ref["mjd"]))
+    assert np.allclose(v, ref["corr_s"], rtol=0, atol=1e-18)
+    with pytest.raises(ValueError):
+        clock.evaluate(path, np.array([50000.0]), limits="error")
+
+
+def test_clock_files_applied():
+    """A site's clock file shifts its TOAs' TT by the interpolated correction and sets the
+    clkcorr flag (toa.py:2236-2242)."""
+    from pint_amd.toa import load_tim
+    base = load_tim(os.path.join(GOLDEN, "prep_mixed.tim"), ephem="builtin", include_bipm=False)
+    path = os.path.join(GOLDEN, "clk_test.clk")
+    with open(path, "w") as f:
+        f.write("# UTC(gbt) UTC(GPS)\n50000.0 1.0e-6\n60000.0 3.0e-6\n")
+    try:
+        t = load_tim(os.path.join(GOLDEN, "prep_mixed.tim"), ephem="builtin", include_bipm=False,
+                     clock_files={"gbt": path})
+    finally:
+        os.remove(path)
+    obs = np.array(t.get_obss())
+    dt = ((LD(t.arrays["tdb_hi"]) + LD(t.arrays["tdb_lo"])) - (LD(base.arrays["tdb_hi"]) + LD(base.arrays["tdb_lo"])))
+    dt = dt.astype(np.float64) * 86400
+    mjd = base.arrays["mjd_float"]
+    want = np.where(obs == "gbt", 1e-6 + 2e-6 * (mjd - 50000.0) / 10000.0, 0.0)
+    assert np.allclose(dt, want, atol=2e-10)
+    assert all((t.flag_columns["clkcorr"][i] != "") == (obs[i] == "gbt" or base.flag_columns.get("clkcorr", [""] * len(obs))[i] != "")
+               for i in range(len(obs)))
+
+
+def test_offline_limits():
+    """Only the builtin ephemeris and TT(TAI) are available offline: the others raise."""
+    from pint_amd.toa import load_tim
+    from pint_amd import get_model
+    path = os.path.join(GOLDEN, "NGC6440E.tim")
+    m = get_model(os.path.join(GOLDEN, "NGC6440E.par"))   # EPHEM DE421, CLK UTC(NIST)
+    with pytest.raises(NotImplementedError):
+        load_tim(path, model=m, include_bipm=False)
+    with pytest.raises(NotImplementedError):
+        load_tim(path, ephem="builtin")                        # BIPM by default
+    from pint_amd import prep
+    with pytest.raises(ValueError):
+        prep.prepare(np.array([40000.0]), np.array([0.5]), ["gbt"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ngc6440e", "b1855"])
+def test_residuals_and_fit_from_tim(name):
+    """get_model_and_toas(par, tim) -> Residuals and a fit on the device, against the
+    reference's residuals (<= 1 ns) and its WLS/GLS fit (fixture <name>.json)."""
+    from pint_amd import Residuals
+    from pint_amd.toa import get_model_and_toas
+    import pint_amd.fitter as F
+    tim, par = CASES[name]
+    m, t = get_model_and_toas(os.path.join(GOLDEN, par), os.path.join(GOLDEN, tim), ephem="builtin",
+                              include_bipm=False)
+    fmeta = json.load(open(os.path.join(GOLDEN, f"{name}.json")))
+    m.free_params = [p for p in fmeta["model"]["free_params"] if p in m]
+    fx = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    r = Residuals(t, m)
+    assert np.max(np.abs(r.time_resids - fx["res_time"])) < 1e-9
+    key = "gls" if name == "b1855" else "wls"
+    f = (F.GLSFitter if key == "gls" else F.WLSFitter)(t, m)
+    chi2 = f.fit_toas(maxiter=1)
+    assert abs(chi2 / fmeta[f"{key}_chi2"] - 1) < 1e-5
+    for p, (hi, lo) in fmeta[f"{key}_params"].items():
+        sig = fmeta[f"{key}_errors"][p]
+        assert abs(float(LD(f.model[p].value) - (LD(hi) + LD(lo)))) < 1e-3 * sig, p
