@@ -66,13 +66,18 @@ enum {
     PINT_COL_PMLON = 4, PINT_COL_PMLAT = 5, PINT_COL_PX = 6, PINT_COL_DM = 7,
     PINT_COL_DMX = 8, PINT_COL_FD = 9, PINT_COL_JUMP = 10, PINT_COL_BIN = 11
 };
-/* binary parameter ids (stand_alone_psr_binaries/binary_generic.py, ELL1_model.py, DD_model.py) */
+/* binary parameter ids (stand_alone_psr_binaries/binary_generic.py, ELL1_model.py, DD_model.py,
+ * ELL1H_model.py (H3, H4, STIGMA), DDK_model.py (KIN, KOM)) */
 enum {
     PINT_B_PB = 0, PINT_B_PBDOT, PINT_B_XPBDOT, PINT_B_A1, PINT_B_A1DOT, PINT_B_ECC,
     PINT_B_EDOT, PINT_B_T0, PINT_B_OM, PINT_B_OMDOT, PINT_B_M2, PINT_B_SINI, PINT_B_GAMMA,
     PINT_B_DR, PINT_B_DTH, PINT_B_A0, PINT_B_B0, PINT_B_TASC, PINT_B_EPS1, PINT_B_EPS2,
-    PINT_B_EPS1DOT, PINT_B_EPS2DOT, PINT_B_NPAR
+    PINT_B_EPS1DOT, PINT_B_EPS2DOT, PINT_B_H3, PINT_B_H4, PINT_B_STIGMA, PINT_B_KIN, PINT_B_KOM,
+    PINT_B_NPAR
 };
+/* binary models (spec.binary) */
+enum { PINT_BIN_NONE = 0, PINT_BIN_ELL1 = 1, PINT_BIN_DD = 2, PINT_BIN_ELL1H = 3, PINT_BIN_BT = 4, PINT_BIN_DDK = 5,
+       PINT_NBIN = 6 };
 
 typedef struct {
     int32_t nf;             /* spin terms F0..F{nf-1}                                   */
@@ -80,7 +85,7 @@ typedef struct {
     int32_t shapiro;        /* SolarSystemShapiro present (sun only)                    */
     int32_t ndm;            /* DispersionDM taylor terms (0 = component absent)         */
     int32_t ndmx;           /* DMX bins                                                 */
-    int32_t binary;         /* 0 none, 1 ELL1, 2 DD                                     */
+    int32_t binary;         /* PINT_BIN_*: 0 none, 1 ELL1, 2 DD, 3 ELL1H, 4 BT, 5 DDK   */
     int32_t nfd;            /* FD terms                                                 */
     int32_t njump;          /* phase JUMPs                                              */
     int32_t track_pn;       /* 1: use_pulse_numbers, 0: nearest  (residuals.py:133-149) */
@@ -97,6 +102,10 @@ typedef struct {
     int32_t wb_noones;      /* 1: the Woodbury chi2 has no offset column of ones (PHOFF free,
                                residuals.py:583-585); the ECORR-only Sherman-Morrison chi2 of
                                :591-636 is this form with the ECORR basis alone             */
+    int32_t ell1h;          /* ELL1H Shapiro form (binary_ell1.py:383-405): 1 H3 alone (Eq. 19,
+                               stigma 0), 2 H3 + H4 (Eq. 19, stigma = H4/H3), 3 H3 + STIGMA
+                               (exact, Eq. 29); 0 otherwise                                 */
+    int32_t nharms;         /* ELL1H: last harmonic of Eq. 19 (NHARMS; max(NHARMS, 7) with H4) */
     double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
     double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
     double red_t0;          /* unused reserve                                           */

@@ -86,7 +86,7 @@ def from_fixture(meta) -> OModel:
         if d.get("key"):
             masks[name] = (d["key"], d.get("key_value") or [])
     comps = set(mm["components"])
-    binary = "ELL1" if "BinaryELL1" in comps else ("DD" if "BinaryDD" in comps else None)
+    binary = next((b for b in ("ELL1H", "ELL1", "DD", "DDK", "BT") if "Binary" + b in comps), None)
     ecl = mm["values"].get("ECL", {}).get("value") or "IERS2010"
     return OModel(vals, list(mm["free_params"]), comps, masks, binary, ecl)
 
@@ -387,6 +387,78 @@ class _ELL1:
         return dI + dS
 
 
+class _ELL1H(_ELL1):
+    """ELL1H_model.py (Freire & Wex 2010) on binary_ell1.py:312-417's setup: ELL1's delayI
+    plus the H3 Shapiro delay, no M2/SINI.  Modes (binary_ell1.py:383-405): H3 alone -> the
+    approximate 3rd-and-higher harmonics (Eq. 19) with stigma = 0; H3 + H4 -> the same with
+    stigma = H4/H3 and NHARMS = max(NHARMS, 7); H3 + STIGMA -> the exact form (Eq. 29)."""
+
+    def __init__(self, om, bt_days, acc):
+        super().__init__(om, bt_days, acc)  # M2 = SINI = 0: ELL1's delayS vanishes
+        H3 = LD(om.v("H3"))
+        self.H3 = H3
+        P = self.Phi
+        if om.has("H4"):
+            self.mode = 2
+            H4 = LD(om.v("H4"))
+            self.sig = LD(0) if H3 == 0 else H4 / H3
+            self.dsig_dH3 = LD(0) if H3 == 0 else -H4 / H3 / H3
+            self.dsig_dH4 = LD(0) if H3 == 0 else 1 / H3
+            self.N = max(int(om.v("NHARMS", 7) or 7), 7)
+        elif om.has("STIGMA"):
+            self.mode = 3
+            self.sig = LD(om.v("STIGMA"))
+            self.dsig_dH3, self.dsig_dH4 = LD(0), LD(0)
+        else:
+            self.mode = 1
+            self.sig = LD(0)
+            self.dsig_dH3, self.dsig_dH4 = LD(0), LD(0)
+            self.N = int(om.v("NHARMS", 3) or 3)
+        sg = self.sig
+        if self.mode == 3:
+            lg = 1 + sg * sg - 2 * sg * np.sin(P)
+            self.dS = -2 * H3 / sg ** 3 * np.log(lg)
+            self.dS_dH3 = -2 / sg ** 3 * np.log(lg)
+            self.dS_dsig = -2 * H3 / sg ** 4 * (-3 * np.log(lg) + 2 * sg * (sg - np.sin(P)) / lg)
+            self.dS_dPhi = 4 * H3 / sg ** 2 * (np.cos(P) / lg)
+        else:
+            # Eq. (19): -2 H3 sum_{k=3}^{N} c_k stigma^(k-3) basis_k(k Phi), c_k = (-1)^pwr 2/k,
+            # odd k: sin, pwr = (k+1)/2; even k: cos, pwr = (k+2)/2 (ELL1H_model.py:90-140)
+            f = np.zeros_like(P)
+            fs = np.zeros_like(P)
+            fp = np.zeros_like(P)
+            for k in range(3, self.N + 1):
+                pwr = (k + 1) // 2 if k % 2 else (k + 2) // 2
+                ck = LD((-1) ** pwr * 2.0 / k)
+                b = np.sin(k * P) if k % 2 else np.cos(k * P)
+                db = k * np.cos(k * P) if k % 2 else -k * np.sin(k * P)
+                f = f + ck * sg ** (k - 3) * b
+                fp = fp + ck * sg ** (k - 3) * db
+                if k > 3:
+                    fs = fs + ck * (k - 3) * sg ** (k - 4) * b
+            self.dS = -2 * H3 * f
+            self.dS_dH3 = -2 * f
+            self.dS_dsig = -2 * H3 * fs
+            self.dS_dPhi = -2 * H3 * fp
+        self.delayS = self.dS
+        self.delay = self.delayI + self.dS
+
+    def deriv(self, par):
+        """d_ELL1Hdelay_d_par: d_delayI_d_par + d_delayS_d_par (ELL1H_model.py:326-359)."""
+        base = super().deriv(par) if par not in ("H3", "H4", "STIGMA") else np.zeros_like(self.tt0)
+        tt0, PBs = self.tt0, self.PBs
+        d_Phi = LD(0)
+        if par == "TASC":
+            d_Phi = (self.PBDOT * tt0 / self.pb - 1.0) * LD(2 * np.pi) / self.pb
+        elif par == "PB":
+            d_Phi = LD(2 * np.pi) * ((self.PBDOT + self.XPBDOT) * tt0 ** 2 / PBs ** 3 - tt0 / PBs ** 2)
+        elif par in ("PBDOT", "XPBDOT"):
+            d_Phi = -LD(np.pi) * tt0 ** 2 / PBs ** 2
+        d_sig = {"H3": self.dsig_dH3, "H4": self.dsig_dH4, "STIGMA": LD(1)}.get(par, LD(0))
+        d_H3 = LD(1) if par == "H3" else LD(0)
+        return base + self.dS_dH3 * d_H3 + self.dS_dPhi * d_Phi + self.dS_dsig * d_sig
+
+
 class _DD:
     """DD_model.py + binary_generic.py (Kepler Newton, nu, omega, er/eTheta, alpha/beta,
     delayInverse, delayS, delayA) and the reference's prtl_der chain."""
@@ -525,7 +597,8 @@ class _DD:
 BIN_UNIT = {"PB": DAYSEC, "T0": DAYSEC, "TASC": DAYSEC, "OM": DEG_RAD, "OMDOT": DEG_RAD / YR_S,
             "EPS1DOT": 1e-12, "EPS2DOT": 1e-12}
 BIN_PARAMS = {"PB", "PBDOT", "XPBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "GAMMA",
-              "DR", "DTH", "A0", "B0", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT"}
+              "DR", "DTH", "A0", "B0", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "H3", "H4", "STIGMA",
+              "KIN", "KOM"}
 
 
 # ----------------------------------------------------------------------------------
@@ -599,7 +672,7 @@ def evaluate(om: OModel, toas: dict, with_tzr=True):
     out["binary_obj"] = None
     if om.binary:
         bt = tdb  # barycentric days; acc_delay = delay so far (pulsar_binary.py:398)
-        B = (_ELL1 if om.binary == "ELL1" else _DD)(om, bt, delay.astype(LD))
+        B = {"ELL1": _ELL1, "ELL1H": _ELL1H, "DD": _DD}[om.binary](om, bt, delay.astype(LD))
         d = B.delay.astype(float)
         out["binary"] = d
         out["binary_obj"] = B

@@ -90,6 +90,18 @@ EPS2 {rng.normal(0, 1e-5):.6e} 1
 M2 0.25
 SINI 0.95
 """
+    elif binary.startswith("ELL1H"):
+        # binary_ell1.py:312-417 (Freire & Wex 2010): H3 alone, H3 + H4, or H3 + STIGMA
+        extra = {"ELL1H_H3": "NHARMS 3\n", "ELL1H_H4": "H4 3.1e-7 1\nNHARMS 8\n",
+                 "ELL1H_STIG": "STIGMA 0.6 1\n"}[binary]
+        par += f"""BINARY ELL1H
+A1 {rng.uniform(1, 20):.9f} 1
+PB {rng.uniform(1, 30):.12f} 1
+TASC 54801.123456789 1
+EPS1 {rng.normal(0, 1e-5):.6e} 1
+EPS2 {rng.normal(0, 1e-5):.6e} 1
+H3 5.2e-7 1
+""" + extra
     elif binary == "DD":
         par += f"""BINARY DD
 A1 {rng.uniform(5, 30):.9f} 1
@@ -191,7 +203,8 @@ def gen_pta(seed, binary, n=1000):
                                     add_correlated_noise=True, include_bipm=False,
                                     multi_freqs_in_epoch=False)
     model.find_empty_masks(ts, freeze=True)
-    name = {"": "pta_iso", "ELL1": "pta_ell1", "DD": "pta_dd"}[binary]
+    name = {"": "pta_iso", "ELL1": "pta_ell1", "DD": "pta_dd", "ELL1H_H3": "ell1h_h3", "ELL1H_H4": "ell1h_h4",
+            "ELL1H_STIG": "ell1h_stig"}[binary]
     with open(__import__("os").path.join(__import__("refcommon").GOLDEN, name + ".par"), "w") as f:
         f.write(pta_par(seed, binary))
     capture(name, model, ts, fit="gls")
@@ -208,3 +221,6 @@ if __name__ == "__main__":
         gen_pta(2, "ELL1")
     if "pta_dd" in which:
         gen_pta(3, "DD")
+    for i, b in enumerate(("ELL1H_H3", "ELL1H_H4", "ELL1H_STIG")):
+        if b.lower() in which:
+            gen_pta(11 + i, b)

@@ -15,7 +15,8 @@ LIBPATH = os.environ.get("PINT_LIB") or os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
 EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
-B_NPAR = 22
+B_NPAR = 27
+BIN_NONE, BIN_ELL1, BIN_DD, BIN_ELL1H, BIN_BT, BIN_DDK = range(6)
 
 COL_OFFSET, COL_F, COL_LON, COL_LAT, COL_PMLON, COL_PMLAT, COL_PX, COL_DM, COL_DMX, COL_FD, COL_JUMP, COL_BIN = range(12)
 
@@ -36,7 +37,7 @@ class SpecT(C.Structure):
                                           "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
                                           "o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px",
                                           "o_POSEPOCH", "o_DM", "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP")] + [
-        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
+        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
         ("col_kind", C.c_int32 * MAX_COLS), ("col_index", C.c_int32 * MAX_COLS), ("col_toff", C.c_int32 * MAX_COLS)]
 
 

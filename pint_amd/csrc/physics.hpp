@@ -252,6 +252,8 @@ struct BinState {
     double eps1, eps2, EPS1DOT, EPS2DOT, nhat;
     double R0, R1, R2;  // d_delayR_da1 and Phi derivatives (ELL1_model.py:221-315)
     double Dre, Drep, Drepp;
+    // ELL1H (ELL1H_model.py): the H3 Shapiro delay's partials and d(stigma)/d(H3, H4)
+    double hS_H3, hS_sig, hS_Phi, dsig_dH3, dsig_dH4;
     // DD
     double E, sinE, cosE, nu, k, omega, OMDOT_rs, er, eTheta, alpha, beta;
     // trigonometry shared by the delay and every derivative column (computed once)
@@ -269,6 +271,7 @@ PD double bin_unit_factor(int pid) {
         case PINT_B_OM: return DEG_RAD;
         case PINT_B_OMDOT: return DEG_RAD / YR_S;
         case PINT_B_EPS1DOT: case PINT_B_EPS2DOT: return 1e-12;  // units 1e-12/s (binary_ell1.py:142)
+        case PINT_B_KIN: case PINT_B_KOM: return DEG_RAD;
         default: return 1.0;
     }
 }
@@ -289,7 +292,65 @@ PD void orbit_phase(dd tt0, dd ipbs, double pbdot_sum, BinState& B) {
     B.Phi = B.orbits_frac * TWO_PI;  // orbit_phase(): (orbits - floor)*2pi (binary_orbits.py:25)
 }
 
-// ---- ELL1 (ELL1_model.py) ---------------------------------------------------------
+// ---- ELL1H Shapiro delay (ELL1H_model.py, Freire & Wex 2010) ------------------------
+// binary_ell1.py:383-405 picks the form: S.ell1h 1 = H3 alone (Eq. 19, stigma = 0), 2 = H3 + H4
+// (Eq. 19, stigma = H4/H3, harmonics 3..NHARMS), 3 = H3 + STIGMA (the exact Eq. 29).  Eq. 19:
+// -2 H3 sum_{k=3}^{N} c_k stigma^(k-3) b_k(k Phi), c_k = (-1)^pwr 2/k, odd k: sin, pwr = (k+1)/2,
+// even k: cos, pwr = (k+2)/2 (ELL1H_model.py:90-140); sin/cos(k Phi) by rotation from k = 3.
+// Returns the delay; sets its partials in H3, stigma and Phi (:238-330).
+PD double ell1h_shapiro(const pint_spec_t& S, const double* P, BinState& B) {
+    const double H3 = binp(S, P, PINT_B_H3);
+    double sig = 0.0;
+    B.dsig_dH3 = 0.0;
+    B.dsig_dH4 = 0.0;
+    if (S.ell1h == 2) {
+        const double H4 = binp(S, P, PINT_B_H4);
+        if (H3 != 0.0) {
+            const double i3 = 1.0 / H3;
+            sig = H4 * i3;
+            B.dsig_dH3 = -H4 * i3 * i3;  // d_STIGMA_d_H3 (:283-297)
+            B.dsig_dH4 = i3;             // d_STIGMA_d_H4 (:280)
+        }
+    } else if (S.ell1h == 3) {
+        sig = binp(S, P, PINT_B_STIGMA);
+    }
+    if (S.ell1h == 3) {  // delayS_H3_STIGMA_exact and partials (:300-330)
+        const double sP = B.s1, cP = B.c1;
+        const double lg = 1.0 + sig * sig - 2.0 * sig * sP, L = log(lg), is = 1.0 / sig, il = 1.0 / lg;
+        const double is2 = is * is, is3 = is2 * is;
+        B.hS_H3 = -2.0 * is3 * L;
+        B.hS_sig = -2.0 * H3 * is3 * is * (-3.0 * L + 2.0 * sig * (sig - sP) * il);
+        B.hS_Phi = 4.0 * H3 * is2 * cP * il;
+        return H3 * B.hS_H3;
+    }
+    const int N = S.ell1h == 1 ? 3 : S.nharms;
+    const double s1 = B.s1, c1 = B.c1;
+    double sk = B.s3, ck = B.c3;  // sin/cos(k Phi) from k = 3
+    double pw = 1.0, pwm = 0.0;   // stigma^(k-3), stigma^(k-4)
+    double f = 0.0, fs = 0.0, fp = 0.0;
+    for (int k = 3; k <= N; k++) {
+        const bool odd = k & 1;
+        const int pwr = odd ? (k + 1) / 2 : (k + 2) / 2;
+        const double c = ((pwr & 1) ? -2.0 : 2.0) / (double)k;
+        const double b = odd ? sk : ck;
+        const double db = odd ? (double)k * ck : -(double)k * sk;
+        f += c * pw * b;
+        fp += c * pw * db;
+        if (k > 3) fs += c * (double)(k - 3) * pwm * b;
+        pwm = pw;
+        pw *= sig;
+        const double sn = sk * c1 + ck * s1;
+        ck = ck * c1 - sk * s1;
+        sk = sn;
+    }
+    B.hS_H3 = -2.0 * f;
+    B.hS_sig = -2.0 * H3 * fs;
+    B.hS_Phi = -2.0 * H3 * fp;
+    return H3 * B.hS_H3;
+}
+
+// ---- ELL1 (ELL1_model.py); H: ELL1H (binary_ell1.py:312, no M2/SINI, the H3 Shapiro delay)
+template <bool H>
 PD void ell1_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B) {
     dd tasc = pdd(P, S.o_bin[PINT_B_TASC]);
     // ttasc = (t - TASC) in s with t = tdbld*day - acc_delay (pulsar_binary.py:398, ELL1_model.py:42)
@@ -309,8 +370,8 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd
     B.EPS2DOT = binp(S, P, PINT_B_EPS2DOT) * 1e-12;
     B.eps1 = binp(S, P, PINT_B_EPS1) + B.tt0 * B.EPS1DOT;
     B.eps2 = binp(S, P, PINT_B_EPS2) + B.tt0 * B.EPS2DOT;
-    B.TM2 = binp(S, P, PINT_B_M2) * TSUN;
-    B.SINI = binp(S, P, PINT_B_SINI);
+    B.TM2 = H ? 0.0 : binp(S, P, PINT_B_M2) * TSUN;
+    B.SINI = H ? 0.0 : binp(S, P, PINT_B_SINI);
     double Phi = B.Phi, e1 = B.eps1, e2 = B.eps2;
     // sin/cos(k Phi), k = 2..4, by the angle-addition identities from one sincos (a few
     // ulp of 1; they enter multiplied by a1 * eps <~ 1e-5 s)
@@ -343,8 +404,15 @@ PD void ell1_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd
     B.nhat = TWO_PI * B.ipb;
     double nD = B.nhat * B.Drep;
     double delayI = B.Dre * (1 - nD + nD * nD + 0.5 * B.nhat * B.nhat * B.Dre * B.Drepp);  // :141-166
-    B.lgNum = log(1 - B.SINI * s1);
-    double delayS = -2 * B.TM2 * B.lgNum;                                                // :599-603
+    double delayS;
+    if (H) {
+        B.lgNum = 0.0;
+        delayS = ell1h_shapiro(S, P, B);  // ELL1Hdelay = delayI + delayS (ELL1H_model.py:78)
+    } else {
+        B.lgNum = log(1 - B.SINI * s1);
+        delayS = -2 * B.TM2 * B.lgNum;  // :599-603
+        B.hS_H3 = B.hS_sig = B.hS_Phi = B.dsig_dH3 = B.dsig_dH4 = 0.0;
+    }
     B.delay = delayI + delayS;
     B.status = 0;
 }
@@ -358,6 +426,7 @@ struct Ell1Grad {
     double a1, Phi, e1, e2, pb, TM2, SINI;
 };
 
+template <bool H>
 PD void ell1_grad(const BinState& B, Ell1Grad& g) {
     double e1 = B.eps1, e2 = B.eps2, a1 = B.a1;
     double s1 = B.s1, c1 = B.c1, s2 = B.s2, c2 = B.c2, s3 = B.s3, c3 = B.c3, s4 = B.s4, c4 = B.c4;
@@ -398,7 +467,8 @@ PD void ell1_grad(const BinState& B, Ell1Grad& g) {
     // d_delayS_d_par (:605-631) -- note the reference's d_delayS_d_Phi omits cos(Phi) (:620)
     double lg = 1 - B.SINI * s1;
     g.a1 = dI_dDre * B.R0 + dI_dDrep * B.R1 + dI_dDrepp * B.R2;
-    g.Phi = dI_dDre * Drep + dI_dDrep * Drepp + dI_dDrepp * dDrepp_dPhi + (-2 * B.TM2 / lg * (-B.SINI));
+    g.Phi = dI_dDre * Drep + dI_dDrep * Drepp + dI_dDrepp * dDrepp_dPhi +
+            (H ? B.hS_Phi : (-2 * B.TM2 / lg * (-B.SINI)));
     g.e1 = dI_dDre * dDre_de1 + dI_dDrep * dDrep_de1 + dI_dDrepp * dDrepp_de1;
     g.e2 = dI_dDre * dDre_de2 + dI_dDrep * dDrep_de2 + dI_dDrepp * dDrepp_de2;
     g.pb = dI_dnhat * (-TWO_PI * B.ipb * B.ipb);
@@ -424,6 +494,10 @@ PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
         case PINT_B_XPBDOT: return g.Phi * (-PI_D * tt0 * tt0 * i2);
         case PINT_B_M2: return g.TM2 * TSUN;
         case PINT_B_SINI: return g.SINI;
+        // ELL1H: d_delayS_d_par (ELL1H_model.py:326-359) through H3, stigma
+        case PINT_B_H3: return B.hS_H3 + B.hS_sig * B.dsig_dH3;
+        case PINT_B_H4: return B.hS_sig * B.dsig_dH4;
+        case PINT_B_STIGMA: return B.hS_sig;
         default: return 0.0;
     }
 }
@@ -733,8 +807,8 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
     BinState B;
     B.status = 0;
-    if (BIN == 1) {
-        ell1_setup(S, P, C, t.tdb, delay, B);
+    if (BIN == 1 || BIN == 3) {
+        ell1_setup<BIN == 3>(S, P, C, t.tdb, delay, B);
         delay += B.delay;
     } else if (BIN == 2) {
         ddm_setup(S, P, C, t.tdb, delay, B);
@@ -800,7 +874,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
     }
     Ell1Grad eg;
-    if (BIN == 1) ell1_grad(B, eg);
+    if (BIN == 1 || BIN == 3) ell1_grad<BIN == 3>(B, eg);
     const double dmc = chain * DMCONST * inv_f2;
     o.dmc = dmc;
     for (int u = 0; u < nrun; u++) {
@@ -851,7 +925,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
                 for (int j = 0; j < R.cnt; j++, colp += ld) {
                     const int pid = S.col_index[R.col0 + j];
                     double d = 0.0;
-                    if (BIN == 1) d = ell1_deriv(B, eg, pid);
+                    if (BIN == 1 || BIN == 3) d = ell1_deriv(B, eg, pid);
                     if (BIN == 2) d = ddm_deriv(B, pid);
                     colp[r] = chain * d * bin_unit_factor(pid);
                 }

@@ -2933,7 +2933,7 @@ struct pint_ctx {
     int nrblk = 0;
     int eval_merge = 0;  // bit 0: one k_eval_mix launch without M, bit 1: with M (PINT_EVAL_MERGE)
     int nblk = 0;
-    int blk_off[4] = {0, 0, 0, 0};  // block ranges per binary type (0 none, 1 ELL1, 2 DD)
+    int blk_off[PINT_NBIN + 1] = {0};  // block ranges per binary model (PINT_BIN_*)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
     int lazy = 0;
     int blocked_solve = 1;  // k_solve_blk (MFMA, blocked) vs the column-by-column k_solve
@@ -3215,6 +3215,12 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     int Kp = (K + 1 + 15) / 16 * 16;
     if (Kp > GMAXKP) { ctx->err = "design matrix too wide for k_gram (K+1 > 256)"; return -PINT_E_INVALID; }
     if (spec->njump > PINT_MAX_JUMP) { ctx->err = "too many JUMPs"; return -PINT_E_INVALID; }
+    if (spec->binary < 0 || spec->binary > PINT_BIN_ELL1H) { ctx->err = "unsupported binary model"; return -PINT_E_INVALID; }
+    if (spec->binary == PINT_BIN_ELL1H &&
+        (spec->ell1h < 1 || spec->ell1h > 3 || (spec->ell1h == 2 && (spec->nharms < 3 || spec->nharms > 64)))) {
+        ctx->err = "bad ELL1H Shapiro form";
+        return -PINT_E_INVALID;
+    }
     PsrHost ph;
     ph.spec = *spec;
     ph.n = n;
@@ -3416,7 +3422,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0, eoff = 0, epoff = 0;
     long sdoff = 0, ddoff = 0;
     int max_nep = 0, max_ndc = 0;
-    std::vector<int> bti[3], btr[3];
+    std::vector<int> bti[PINT_NBIN], btr[PINT_NBIN];
     std::vector<int> rbi;
     int maxK = 0, maxN = 0;
     for (int k = 0; k < ninst; k++) {
@@ -3541,6 +3547,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         cvoff += (long)ph.spec.ncol * ph.spec.ncol;
         toff += ph.spec.tstride;
         int bt = ph.spec.binary;
+        if (bt < 0 || bt >= PINT_NBIN) { ctx->err = "bad binary model"; return PINT_E_INVALID; }
         for (int r0 = 0; r0 <= ph.n; r0 += 256) {
             bti[bt].push_back(k);
             btr[bt].push_back(r0);
@@ -3568,13 +3575,13 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->max_nep = max_nep;
     ctx->max_ndc = max_ndc;
     std::vector<int> bi, br;
-    for (int t = 0; t < 3; t++) {
+    for (int t = 0; t < PINT_NBIN; t++) {
         ctx->blk_off[t] = (int)bi.size();
         bi.insert(bi.end(), bti[t].begin(), bti[t].end());
         br.insert(br.end(), btr[t].begin(), btr[t].end());
     }
-    ctx->blk_off[3] = (int)bi.size();
-    ctx->nblk = (int)bi.size();
+    ctx->blk_off[PINT_NBIN] = (int)bi.size();
+    ctx->nblk = ctx->blk_off[3];  // k_eval_mix covers the isolated, ELL1 and DD blocks
     HIPCHK(cmalloc((void**)&ctx->d_inst, sizeof(InstDev) * ninst));
     HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
     for (int lay = 0; lay < 3; lay++) {  // k_gram launch groups: full, compact, compact + vg
@@ -3763,7 +3770,10 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #undef PINT_EVAL_MIX
         HIPCHK(hipGetLastError());
     }
-    for (int t = 0; t < 3 && !mix; t++) {  // one launch per binary model, back to back on the stream
+    // one launch per binary model, back to back on the stream: all models without the merged
+    // launch; ELL1H/BT/DDK always (they stay out of k_eval_mix so its register set, which
+    // every block of the merged launch carries, is not raised by the rarer models)
+    for (int t = mix ? 3 : 0; t < PINT_NBIN; t++) {
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
         const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
@@ -3773,9 +3783,19 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
                            ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus)
         if (want_M) {
-            if (t == 0) PINT_EVAL_LAUNCH(1, 0); else if (t == 1) PINT_EVAL_LAUNCH(1, 1); else PINT_EVAL_LAUNCH(1, 2);
+            switch (t) {
+                case 0: PINT_EVAL_LAUNCH(1, 0); break;
+                case 1: PINT_EVAL_LAUNCH(1, 1); break;
+                case 2: PINT_EVAL_LAUNCH(1, 2); break;
+                default: PINT_EVAL_LAUNCH(1, 3); break;
+            }
         } else {
-            if (t == 0) PINT_EVAL_LAUNCH(0, 0); else if (t == 1) PINT_EVAL_LAUNCH(0, 1); else PINT_EVAL_LAUNCH(0, 2);
+            switch (t) {
+                case 0: PINT_EVAL_LAUNCH(0, 0); break;
+                case 1: PINT_EVAL_LAUNCH(0, 1); break;
+                case 2: PINT_EVAL_LAUNCH(0, 2); break;
+                default: PINT_EVAL_LAUNCH(0, 3); break;
+            }
         }
 #undef PINT_EVAL_LAUNCH
         HIPCHK(hipGetLastError());

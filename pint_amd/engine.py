@@ -143,12 +143,25 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.o_JUMP = pos
         for n in jumps:
             place(n)
-    spec.binary = {None: 0, "ELL1": 1, "DD": 2}[model.binary]
+    spec.binary = {None: L.BIN_NONE, "ELL1": L.BIN_ELL1, "DD": L.BIN_DD, "ELL1H": L.BIN_ELL1H}[model.binary]
     if model.binary:
         for n, pid in BIN_IDS.items():
             if n in model:
                 spec.o_bin[pid] = place(n)
-        need = ["PB", "A1", "TASC" if model.binary == "ELL1" else "T0"]
+        if model.binary == "ELL1H":
+            # BinaryELL1H.setup (binary_ell1.py:383-405)
+            has4 = model.H4.value is not None
+            hasst = model.STIGMA.value is not None
+            nh = model.NHARMS.value
+            if has4 and hasst:
+                raise ValueError("ELL1H can use H4 or STIGMA but not both")
+            if hasst and not float(model.STIGMA.value) > 0:
+                raise ValueError("STIGMA must be greater than zero.")
+            if has4 and float(model.H3.value or 0.0) == 0.0 and float(model.H4.value) != 0.0:
+                raise ValueError("To use H4, H3 needs to be significant(H3 != 0).")
+            spec.ell1h = 2 if has4 else (3 if hasst else 1)
+            spec.nharms = max(int(nh), 7) if (has4 and nh is not None) else (7 if has4 else int(nh or 3))
+        need = ["PB", "A1", "TASC" if model.binary in ("ELL1", "ELL1H") else "T0"]
         for n in need:
             if n not in model or model[n].value is None:
                 raise ValueError(f"binary parameter {n} missing")

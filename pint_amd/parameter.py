@@ -181,6 +181,9 @@ _DEFS = {
     "OM": ("Binary", "float", "deg", True, None),
     "OMDOT": ("Binary", "float", "deg / yr", True, None),
     "M2": ("Binary", "float", "solMass", False, None),
+    # ELL1H (binary_ell1.py:345-378): H3/H4 (s) and STIGMA longdouble, NHARMS an int
+    "H3": ("Binary", "float", "s", True, None), "H4": ("Binary", "float", "s", True, None),
+    "STIGMA": ("Binary", "float", "", True, None), "NHARMS": ("Binary", "int", "", False, None),
     "SINI": ("Binary", "float", "", False, None),
     "GAMMA": ("Binary", "float", "s", False, None),
     "DR": ("Binary", "float", "", False, None), "DTH": ("Binary", "float", "", False, None),
@@ -198,7 +201,7 @@ _DEFS = {
 _ALIASES = {
     "RA": "RAJ", "DEC": "DECJ", "LAMBDA": "ELONG", "BETA": "ELAT", "PMLAMBDA": "PMELONG",
     "PMBETA": "PMELAT", "E": "ECC", "ECCDOT": "EDOT", "XDOT": "A1DOT", "T2EFAC": "EFAC",
-    "T2EQUAD": "EQUAD", "TNECORR": "ECORR", "SOLARN0": "NE_SW", "CLK": "CLOCK", "PSRJ": "PSR", "PSRB": "PSR",
+    "T2EQUAD": "EQUAD", "TNECORR": "ECORR", "SOLARN0": "NE_SW", "CLK": "CLOCK", "PSRJ": "PSR", "PSRB": "PSR", "VARSIGMA": "STIGMA", "STIG": "STIGMA",
 }
 
 _PREFIX = {  # prefix params: regex -> (component, units template, long_double)

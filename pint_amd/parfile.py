@@ -231,6 +231,8 @@ _ORDER = {
     "DD": ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "A0", "B0", "GAMMA",
            "DR", "DTH"],
     "ELL1": ["PB", "PBDOT", "A1", "A1DOT", "M2", "SINI", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT"],
+    "ELL1H": ["PB", "PBDOT", "A1", "A1DOT", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "H3", "H4", "STIGMA",
+              "NHARMS"],
     "PLRedNoise": ["RNAMP", "RNIDX", "TNREDAMP", "TNREDGAM", "TNREDC"],
 }
 MIDDLE = ["TroposphereDelay", "SolarSystemShapiro", "SolarWindDispersion", "DispersionDM", "DispersionDMX",
@@ -277,7 +279,7 @@ def _astrometry_params(model) -> List[str]:
 def _ell1_comments(model) -> str:
     """ELL1's derived ECC and OM (binary_ell1.py:25-33 _eps_to_e / _eps_to_om, funcParameter
     lines written commented out, parameter.py:2593-2598)."""
-    if model.binary != "ELL1" or "EPS1" not in model or "EPS2" not in model:
+    if model.binary not in ("ELL1", "ELL1H") or "EPS1" not in model or "EPS2" not in model:
         return ""
     e1, e2 = model["EPS1"].value, model["EPS2"].value
     if e1 is None or e2 is None:
@@ -318,7 +320,10 @@ def as_parfile(model, include_info: bool = True, comment: str = None) -> str:
         head += "# Format: pint\n"
     body = ""
     names = ordered_params(model)
-    last_bin = max((i for i, n in enumerate(names) if model[n].component == "Binary"), default=None)
+    # ELL1's ECC/OM comment lines follow the ELL1 parameters (ELL1H's own come after them)
+    h_own = ("H3", "H4", "STIGMA", "NHARMS") if model.binary == "ELL1H" else ()
+    last_bin = max((i for i, n in enumerate(names) if model[n].component == "Binary" and n not in h_own
+                    and (model[n].value is not None or n == "BINARY")), default=None)
     for i, n in enumerate(names):
         body += parfile_line(model[n])
         if i == last_bin:

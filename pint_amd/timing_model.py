@@ -31,7 +31,8 @@ DD_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "
              "GAMMA", "DR", "DTH"]
 BIN_IDS = {"PB": 0, "PBDOT": 1, "XPBDOT": 2, "A1": 3, "A1DOT": 4, "ECC": 5, "EDOT": 6, "T0": 7, "OM": 8,
            "OMDOT": 9, "M2": 10, "SINI": 11, "GAMMA": 12, "DR": 13, "DTH": 14, "A0": 15, "B0": 16,
-           "TASC": 17, "EPS1": 18, "EPS2": 19, "EPS1DOT": 20, "EPS2DOT": 21}
+           "TASC": 17, "EPS1": 18, "EPS2": 19, "EPS1DOT": 20, "EPS2DOT": 21, "H3": 22, "H4": 23, "STIGMA": 24,
+           "KIN": 25, "KOM": 26}
 # obliquity values (rad) from the reference's runtime ecliptic.dat (pulsar_ecliptic.py:29)
 OBLIQUITY = {"IERS2010": 0.4090926006005829, "IERS2003": 0.40909260011576914,
              "DEFAULT": 84381.406 / 206264.80624709636}
@@ -279,8 +280,8 @@ def get_model(parfile) -> TimingModel:
     for l in lines:
         if l.name == "BINARY" and l.fields:
             binary = l.fields[0].upper()
-    if binary not in (None, "ELL1", "DD"):
-        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, DD)")
+    if binary not in (None, "ELL1", "DD", "ELL1H"):
+        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, ELL1H, DD)")
     model.binary = binary
     has_eq = any(n in ("RAJ", "RA") for n in names)
     has_ecl = any(n in ("ELONG", "LAMBDA") for n in names)
@@ -300,9 +301,11 @@ def get_model(parfile) -> TimingModel:
         defaults += [("SWM", 0)]
     if any(n == "DM" or re.match(r"^DM\d+$", n) for n in names):
         defaults += [("DM", LD(0)), ("DMEPOCH", None)]
-    if binary == "ELL1":
-        defaults += [(n, 0.0) for n in ELL1_PARAMS]
+    if binary in ("ELL1", "ELL1H"):
+        defaults += [(n, 0.0) for n in ELL1_PARAMS if not (binary == "ELL1H" and n in ("M2", "SINI"))]
         defaults += [("TASC", None)]
+        if binary == "ELL1H":  # binary_ell1.py:345-378 (no values by default)
+            defaults += [("H3", None), ("H4", None), ("STIGMA", None), ("NHARMS", None)]
     elif binary == "DD":
         defaults += [(n, 0.0) for n in DD_PARAMS]
         defaults += [("T0", None)]
@@ -316,7 +319,7 @@ def get_model(parfile) -> TimingModel:
             v = LD(v)
         p.value = v
         # ELL1's rates are unset (None) in the reference (binary_ell1.py), 0 here
-        p.implicit = binary == "ELL1" and n in ("PBDOT", "A1DOT", "EDOT", "OMDOT", "EPS1DOT", "EPS2DOT")
+        p.implicit = binary in ("ELL1", "ELL1H") and n in ("PBDOT", "A1DOT", "EDOT", "OMDOT", "EPS1DOT", "EPS2DOT")
         if p.component == "Binary":
             p.component = "Binary"
         model.add_param(p)
