@@ -459,6 +459,77 @@ class _ELL1H(_ELL1):
         return base + self.dS_dH3 * d_H3 + self.dS_dPhi * d_Phi + self.dS_dsig * d_sig
 
 
+class _BT:
+    """BT_model.py (Blandford & Teukolsky 1976): (delayL1 + delayL2) * delayR with
+    omega = OM + OMDOT tt0 (binary_generic.py:631), and the reference's derivative chain
+    d_BTdelay_d_par = delayR (dL1 + dL2) (:258; delayR's derivatives ignored, d_delayL1_d_ECC
+    with +a1 sin(omega) as written at :189, T0 through E only)."""
+
+    def __init__(self, om, bt_days, acc):
+        tt0 = (bt_days - LD(om.v("T0"))) * LD(DAYSEC) - np.asarray(acc, dtype=LD)
+        self.tt0 = tt0
+        self.PBs = LD(om.v("PB")) * LD(DAYSEC)
+        self.PBDOT, self.XPBDOT = LD(om.v("PBDOT")), LD(om.v("XPBDOT"))
+        orbits, _, M = _orbits(om, tt0)
+        self.pb = self.PBs + self.PBDOT * tt0
+        self.EDOT = LD(om.v("EDOT"))
+        self.ecc = LD(om.v("ECC")) + tt0 * self.EDOT
+        self.A1DOT = LD(om.v("A1DOT"))
+        self.a1 = LD(om.v("A1")) + tt0 * self.A1DOT
+        self.GAMMA = LD(om.v("GAMMA"))
+        e = self.ecc
+        E = M.copy()
+        for _ in range(100):  # compute_eccentric_anomaly (binary_generic.py:337)
+            dE = (E - e * np.sin(E) - M) / (1 - e * np.cos(E))
+            E = E - dE
+            if np.all(np.abs(E - e * np.sin(E) - M) < 5e-15):
+                break
+        self.E = E
+        self.omega = LD(om.v("OM")) * LD(DEG_RAD) + LD(om.v("OMDOT")) * LD(DEG_RAD / YR_S) * tt0
+        sw, cw = np.sin(self.omega), np.cos(self.omega)
+        sE, cE = np.sin(E), np.cos(E)
+        sq = np.sqrt(1 - e * e)
+        a1 = self.a1
+        self.L1 = a1 * sw * (cE - e)
+        self.L2 = (a1 * cw * sq + self.GAMMA) * sE
+        num = a1 * cw * sq * cE - a1 * sw * sE
+        self.R = 1.0 - LD(2 * np.pi) * num / ((1.0 - e * cE) * self.pb)
+        self.delay = (self.L1 + self.L2) * self.R
+        self.sw, self.cw, self.sE, self.cE, self.sq = sw, cw, sE, cE, sq
+
+    def deriv(self, par):
+        e, a1, tt0 = self.ecc, self.a1, self.tt0
+        sw, cw, sE, cE, sq = self.sw, self.cw, self.sE, self.cE, self.sq
+        iom = 1.0 / (1.0 - e * cE)
+        dL1_dE = -a1 * sw * sE
+        dL2_dE = (a1 * cw * sq + self.GAMMA) * cE
+        z = np.zeros_like(tt0)
+        PBs = self.PBs
+        f = tt0 if par in ("A1DOT", "OMDOT", "EDOT") else z + 1
+        if par in ("A1", "A1DOT"):
+            dL1, dL2 = f * sw * (cE - e), f * cw * sq * sE
+        elif par in ("OM", "OMDOT"):
+            dL1, dL2 = f * a1 * cw * (cE - e), -f * a1 * sw * sq * sE
+        elif par in ("ECC", "EDOT"):
+            dEe = sE * iom
+            dL1 = f * (a1 * sw + dL1_dE * dEe)
+            dL2 = f * (-a1 * cw * e * sE / sq + dL2_dE * dEe)
+        elif par == "GAMMA":
+            dL1, dL2 = z, sE
+        elif par in ("T0", "PB", "PBDOT", "XPBDOT"):
+            if par == "T0":
+                dM = ((self.PBDOT - self.XPBDOT) * tt0 / PBs - 1.0) * LD(2 * np.pi) / PBs
+                dE = (dM - self.EDOT * sE) * iom
+            elif par == "PB":
+                dE = LD(2 * np.pi) * ((self.PBDOT + self.XPBDOT) * tt0 ** 2 / PBs ** 3 - tt0 / PBs ** 2) * iom
+            else:
+                dE = -LD(np.pi) * tt0 ** 2 / PBs ** 2 * iom
+            dL1, dL2 = dL1_dE * dE, dL2_dE * dE
+        else:
+            return z
+        return self.R * (dL1 + dL2)
+
+
 class _DD:
     """DD_model.py + binary_generic.py (Kepler Newton, nu, omega, er/eTheta, alpha/beta,
     delayInverse, delayS, delayA) and the reference's prtl_der chain."""
@@ -672,7 +743,7 @@ def evaluate(om: OModel, toas: dict, with_tzr=True):
     out["binary_obj"] = None
     if om.binary:
         bt = tdb  # barycentric days; acc_delay = delay so far (pulsar_binary.py:398)
-        B = {"ELL1": _ELL1, "ELL1H": _ELL1H, "DD": _DD}[om.binary](om, bt, delay.astype(LD))
+        B = {"ELL1": _ELL1, "ELL1H": _ELL1H, "DD": _DD, "BT": _BT}[om.binary](om, bt, delay.astype(LD))
         d = B.delay.astype(float)
         out["binary"] = d
         out["binary_obj"] = B

@@ -102,6 +102,17 @@ EPS1 {rng.normal(0, 1e-5):.6e} 1
 EPS2 {rng.normal(0, 1e-5):.6e} 1
 H3 5.2e-7 1
 """ + extra
+    elif binary == "BT":
+        par += f"""BINARY BT
+A1 {rng.uniform(5, 30):.9f} 1
+PB {rng.uniform(5, 60):.12f} 1
+T0 54801.987654321 1
+ECC {rng.uniform(0.05, 0.4):.8f} 1
+OM {rng.uniform(0, 360):.6f} 1
+OMDOT 0.01 1
+GAMMA 0.0004 1
+PBDOT 1e-12 1
+"""
     elif binary == "DD":
         par += f"""BINARY DD
 A1 {rng.uniform(5, 30):.9f} 1
@@ -204,7 +215,7 @@ def gen_pta(seed, binary, n=1000):
                                     multi_freqs_in_epoch=False)
     model.find_empty_masks(ts, freeze=True)
     name = {"": "pta_iso", "ELL1": "pta_ell1", "DD": "pta_dd", "ELL1H_H3": "ell1h_h3", "ELL1H_H4": "ell1h_h4",
-            "ELL1H_STIG": "ell1h_stig"}[binary]
+            "ELL1H_STIG": "ell1h_stig", "BT": "pta_bt"}[binary]
     with open(__import__("os").path.join(__import__("refcommon").GOLDEN, name + ".par"), "w") as f:
         f.write(pta_par(seed, binary))
     capture(name, model, ts, fit="gls")
@@ -221,6 +232,8 @@ if __name__ == "__main__":
         gen_pta(2, "ELL1")
     if "pta_dd" in which:
         gen_pta(3, "DD")
+    if "pta_bt" in which:
+        gen_pta(14, "BT")
     for i, b in enumerate(("ELL1H_H3", "ELL1H_H4", "ELL1H_STIG")):
         if b.lower() in which:
             gen_pta(11 + i, b)

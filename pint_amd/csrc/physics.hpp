@@ -692,6 +692,100 @@ PD double ddm_deriv(const BinState& B, int pid) {
     return dI + dS + dA;
 }
 
+// ---- BT (BT_model.py, Blandford & Teukolsky 1976) -----------------------------------
+// delay = (delayL1 + delayL2) * delayR with delayL1 = a1 sin(w) (cosE - e), delayL2 =
+// (a1 cos(w) sqrt(1 - e^2) + GAMMA) sinE, delayR = 1 - 2 pi (a1 cos(w) sqrt(1-e^2) cosE -
+// a1 sin(w) sinE) / ((1 - e cosE) pb'), w = OM + OMDOT tt0 (binary_generic.py:631).
+// Kepler's equation as in DD.  B.Dre = L1 + L2, B.R0 = delayR.
+PD void bt_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B) {
+    dd T0 = pdd(P, S.o_bin[PINT_B_T0]);
+    dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, T0), DAYSEC), -acc_delay);  // get_tt0 (binary_generic.py:372)
+    B.tt0 = dd_to_d(tt);
+    dd PBs = dd_mul_d(pdd(P, S.o_bin[PINT_B_PB]), DAYSEC);
+    B.PBs = dd_to_d(PBs);
+    B.PBDOT = binp(S, P, PINT_B_PBDOT);
+    B.XPBDOT = binp(S, P, PINT_B_XPBDOT);
+    orbit_phase(tt, dd_make(C.ipb_hi, C.ipb_lo), B.PBDOT + B.XPBDOT, B);
+    B.iPBs = C.ipb_hi + C.ipb_lo;
+    B.pb = B.PBs + B.PBDOT * B.tt0;
+    B.A1DOT = binp(S, P, PINT_B_A1DOT);
+    B.a1 = binp(S, P, PINT_B_A1) + B.tt0 * B.A1DOT;
+    B.EDOT = binp(S, P, PINT_B_EDOT);
+    B.ecc = binp(S, P, PINT_B_ECC) + B.tt0 * B.EDOT;
+    B.GAMMA = binp(S, P, PINT_B_GAMMA);
+    B.status = 0;
+    const double e = B.ecc, M = B.Phi;
+    if (!(e >= 0.0 && e < 1.0)) { B.status = PINT_E_KEPLER; B.delay = 0; return; }
+    double U = M, sU, cU;
+    int it = 0;
+    sincos(U, &sU, &cU);
+    double kU = U - e * sU - M;
+    while (fabs(kU) > 5e-15 && it < 64) {
+        U = U - kU / (1 - e * cU);
+        sincos(U, &sU, &cU);
+        kU = U - e * sU - M;
+        it++;
+    }
+    if (fabs(kU) > 5e-15) B.status = PINT_E_KEPLER;
+    B.E = U;
+    B.sinE = sU;
+    B.cosE = cU;
+    B.OMDOT_rs = binp(S, P, PINT_B_OMDOT) * (DEG_RAD / YR_S);
+    B.omega = binp(S, P, PINT_B_OM) * DEG_RAD + B.OMDOT_rs * B.tt0;
+    sincos(B.omega, &B.sw, &B.cw);
+    B.sqE = sqrt(1 - e * e);
+    B.ipb = 1.0 / B.pb;
+    B.iomeE = 1.0 / (1 - e * cU);
+    const double L1 = B.a1 * B.sw * (cU - e);
+    const double L2 = (B.a1 * B.cw * B.sqE + B.GAMMA) * sU;
+    const double num = B.a1 * B.cw * B.sqE * cU - B.a1 * B.sw * sU;
+    B.R0 = 1.0 - TWO_PI * num * B.iomeE * B.ipb;
+    B.Dre = L1 + L2;
+    B.delay = B.Dre * B.R0;
+}
+
+// d_BTdelay_d_par = delayR (d_delayL1_d_par + d_delayL2_d_par) (BT_model.py:258): delayR's own
+// derivatives are ignored, d_delayL1_d_ECC carries +a1 sin(w) (:189, as the reference has
+// it), d_delayL*_d_T0 goes through E only (:212-216); other orbit parameters through E.
+PD double bt_deriv(const BinState& B, int pid) {
+    const double e = B.ecc, sE = B.sinE, cE = B.cosE, tt0 = B.tt0, a1 = B.a1;
+    const double sw = B.sw, cw = B.cw, sq = B.sqE, iom = B.iomeE;
+    const double iP = B.iPBs, iP2 = iP * iP;
+    const double dL1_dE = -a1 * sw * sE;
+    const double dL2_dE = (a1 * cw * sq + B.GAMMA) * cE;
+    const double dE_dECC = sE * iom;
+    double dL1 = 0.0, dL2 = 0.0, dE = 0.0;
+    switch (pid) {
+        case PINT_B_A1: case PINT_B_A1DOT: {
+            const double f = (pid == PINT_B_A1DOT) ? tt0 : 1.0;
+            dL1 = f * sw * (cE - e);
+            dL2 = f * cw * sq * sE;
+        } break;
+        case PINT_B_OM: case PINT_B_OMDOT: {
+            const double f = (pid == PINT_B_OMDOT) ? tt0 : 1.0;
+            dL1 = f * a1 * cw * (cE - e);
+            dL2 = -f * a1 * sw * sq * sE;
+        } break;
+        case PINT_B_ECC: case PINT_B_EDOT: {
+            const double f = (pid == PINT_B_EDOT) ? tt0 : 1.0;
+            dL1 = f * (a1 * sw + dL1_dE * dE_dECC);
+            dL2 = f * (-a1 * cw * e * sE / sq + dL2_dE * dE_dECC);
+        } break;
+        case PINT_B_GAMMA: dL2 = sE; break;
+        case PINT_B_T0:
+            dE = (((B.PBDOT - B.XPBDOT) * tt0 * iP - 1.0) * TWO_PI * iP - B.EDOT * sE) * iom;
+            break;
+        case PINT_B_PB: dE = TWO_PI * ((B.PBDOT + B.XPBDOT) * tt0 * tt0 * iP2 * iP - tt0 * iP2) * iom; break;
+        case PINT_B_PBDOT: case PINT_B_XPBDOT: dE = -PI_D * tt0 * tt0 * iP2 * iom; break;
+        default: break;
+    }
+    if (dE != 0.0) {
+        dL1 = dL1_dE * dE;
+        dL2 = dL2_dE * dE;
+    }
+    return B.R0 * (dL1 + dL2);
+}
+
 // ------------------------------------------------------------------------------------
 // Per-TOA evaluation
 // ------------------------------------------------------------------------------------
@@ -814,6 +908,10 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         ddm_setup(S, P, C, t.tdb, delay, B);
         delay += B.delay;
         if (B.status) o.status = B.status;
+    } else if (BIN == 4) {
+        bt_setup(S, P, C, t.tdb, delay, B);
+        delay += B.delay;
+        if (B.status) o.status = B.status;
     }
     // ---- FD (frequency_dependent.py:70-101) ----
     double logf = 0.0;  // used by FD and its columns only
@@ -927,6 +1025,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
                     double d = 0.0;
                     if (BIN == 1 || BIN == 3) d = ell1_deriv(B, eg, pid);
                     if (BIN == 2) d = ddm_deriv(B, pid);
+                    if (BIN == 4) d = bt_deriv(B, pid);
                     colp[r] = chain * d * bin_unit_factor(pid);
                 }
                 break;

@@ -29,6 +29,7 @@ ELL1_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "EDOT", "OMDOT", "M2", "SINI", "TAS
                "EPS1DOT", "EPS2DOT"]
 DD_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "A0", "B0",
              "GAMMA", "DR", "DTH"]
+BT_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "GAMMA"]
 BIN_IDS = {"PB": 0, "PBDOT": 1, "XPBDOT": 2, "A1": 3, "A1DOT": 4, "ECC": 5, "EDOT": 6, "T0": 7, "OM": 8,
            "OMDOT": 9, "M2": 10, "SINI": 11, "GAMMA": 12, "DR": 13, "DTH": 14, "A0": 15, "B0": 16,
            "TASC": 17, "EPS1": 18, "EPS2": 19, "EPS1DOT": 20, "EPS2DOT": 21, "H3": 22, "H4": 23, "STIGMA": 24,
@@ -180,7 +181,7 @@ class TimingModel:
             raise NotImplementedError("solar-wind dispersion (NE_SW != 0) is outside the supported hot path")
         if "CORRECT_TROPOSPHERE" in self and self.CORRECT_TROPOSPHERE.value:
             raise NotImplementedError("troposphere delay is outside the supported hot path")
-        if self.binary == "DD":
+        if self.binary in ("DD", "BT"):
             e = float(self.ECC.value or 0.0)
             if not (0 <= e < 1):
                 raise ValueError("Eccentricity should be in the range of [0,1).")
@@ -280,8 +281,8 @@ def get_model(parfile) -> TimingModel:
     for l in lines:
         if l.name == "BINARY" and l.fields:
             binary = l.fields[0].upper()
-    if binary not in (None, "ELL1", "DD", "ELL1H"):
-        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, ELL1H, DD)")
+    if binary not in (None, "ELL1", "DD", "ELL1H", "BT"):
+        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, ELL1H, DD, BT)")
     model.binary = binary
     has_eq = any(n in ("RAJ", "RA") for n in names)
     has_ecl = any(n in ("ELONG", "LAMBDA") for n in names)
@@ -308,6 +309,9 @@ def get_model(parfile) -> TimingModel:
             defaults += [("H3", None), ("H4", None), ("STIGMA", None), ("NHARMS", None)]
     elif binary == "DD":
         defaults += [(n, 0.0) for n in DD_PARAMS]
+        defaults += [("T0", None)]
+    elif binary == "BT":  # binary_bt.py:38-69: no M2/SINI, GAMMA 0, rates 0
+        defaults += [(n, 0.0) for n in BT_PARAMS if n != "T0"]
         defaults += [("T0", None)]
     for n, v in defaults:
         if n in model:

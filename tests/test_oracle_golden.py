@@ -11,7 +11,7 @@ from golden_util import GOLDEN
 import pint_oracle as O
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise", "white_mjd", "ecorr_fit",
-         "ell1h_h3", "ell1h_h4", "ell1h_stig"]
+         "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt"]
 DELAY_MAP = {"delay_solar_system_geometric_delay": "geometric", "delay_solar_system_shapiro_delay": "shapiro",
              "delay_constant_dispersion_delay": "dm", "delay_DMX_dispersion_delay": "dmx",
              "delay_binarymodel_delay": "binary", "delay_FD_delay": "fd", "delay_total": "delay"}
@@ -157,7 +157,7 @@ def test_wls_fit_phoff():
 
 
 @pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ell1h_h3", "ell1h_h4",
-                                  "ell1h_stig"])
+                                  "ell1h_stig", "pta_bt"])
 def test_gls_fit(name):
     om, toas, z, meta = fixture(name)
     om2, st, chi2 = O.fit_once(om, toas, gls=True)
