@@ -106,6 +106,10 @@ typedef struct {
                                stigma 0), 2 H3 + H4 (Eq. 19, stigma = H4/H3), 3 H3 + STIGMA
                                (exact, Eq. 29); 0 otherwise                                 */
     int32_t nharms;         /* ELL1H: last harmonic of Eq. 19 (NHARMS; max(NHARMS, 7) with H4) */
+    int32_t dmn0;           /* first PLDMNoise mode among the nred Fourier modes (= nred: none);
+                               modes >= dmn0 are scaled by (1400 MHz / f_bary)^2 per TOA
+                               (noise_model.py:443-540 PLDMNoise.get_noise_basis)           */
+    int32_t pad_;
     double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
     double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
     double red_t0;          /* unused reserve                                           */
@@ -296,6 +300,9 @@ int pint_inst_status(pint_ctx *ctx, int32_t *out);
  * Residuals.noise_resids as GLSFitter.fit_toas (fitter.py:2270-2282) and
  * DownhillGLSFitter.fit_toas (:1582-1605) set it. */
 int pint_noise_resids(pint_ctx *ctx, double *red, double *ecorr);
+/* The PLDMNoise realisation of the same step (its modes times (1400 MHz / f_bary)^2), n_i per
+ * instance: Residuals.noise_resids["pl_DM_noise"] (zeros for pulsars without PLDMNoise). */
+int pint_noise_resids_dm(pint_ctx *ctx, double *dm);
 
 /* Device time (ms, HIP events on the streams the kernels run on) of the last launches, 8
  * values: [0] eval (no design matrix), [1] resid, [2] ecorr + Gram + partial reduction,

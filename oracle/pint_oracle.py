@@ -963,12 +963,38 @@ def ecorr_basis(om, toas):
     return mats, wts
 
 
+def dm_noise(om, toas):
+    """PLDMNoise basis and weights (noise_model.py:443-540): the Fourier basis of TNDMC modes
+    scaled by (1400 MHz / f_bary)^2 per TOA, weights powerlaw(f, 10^TNDMAMP, TNDMGAM) f_1."""
+    nf = int(om.v("TNDMC", 30)) if om.has("TNDMC") else 30
+    amp, gam = 10 ** float(om.v("TNDMAMP")), float(om.v("TNDMGAM"))
+    t = (np.asarray(toas["tdb_hi"], dtype=LD) + np.asarray(toas["tdb_lo"], dtype=LD)) * LD(86400)
+    T = t.max() - t.min()
+    f = np.linspace(1 / T, nf / T, nf)
+    ff = np.zeros(2 * nf)
+    ff[::2] = f
+    ff[1::2] = f
+    n = len(t)
+    bf = np.asarray(evaluate(om, toas, True)["bfreq"][:n], dtype=float)
+    D = (1400.0 / bf) ** 2
+    Fm = np.zeros((n, 2 * nf))
+    Fm[:, ::2] = np.sin(2 * np.pi * t[:, None] * ff[::2])
+    Fm[:, 1::2] = np.cos(2 * np.pi * t[:, None] * ff[1::2])
+    phi = amp ** 2 / 12.0 / np.pi ** 2 * (1 / 3.16e7) ** (gam - 3) * ff ** (-gam)
+    return Fm * D[:, None], phi * ff[0]
+
+
 def noise_basis(om, toas):
     """noise_model_designmatrix / noise_model_basis_weight (timing_model.py:1631-1660):
-    PLRedNoise block first, then ECORR (component order of the fixtures' models)."""
+    PLRedNoise, then PLDMNoise, then ECORR (the reference's order of the three follows its
+    component order, which is not fixed: tests compare blocks through noise_dims)."""
     mats, wts = [], []
     if "PLRedNoise" in om.comps:
         Fm, phi = red_noise(om, toas)
+        mats.append(Fm)
+        wts.append(phi)
+    if "PLDMNoise" in om.comps:
+        Fm, phi = dm_noise(om, toas)
         mats.append(Fm)
         wts.append(phi)
     em, ew = ecorr_basis(om, toas)

@@ -205,9 +205,19 @@ def gen_j0740(n=1000):
     capture("j0740", model, ts, fit="gls")
 
 
-def gen_pta(seed, binary, n=1000):
+extra_name = None
+
+
+def _par(seed, binary, extra):
+    par = pta_par(seed, binary)
+    if "TNDMAMP" in extra:  # PLDMNoise models DM variations in place of DMX (noise_model.py:443)
+        par = "\n".join(l for l in par.splitlines() if not l.startswith("DMX")) + "\n"
+    return par + extra
+
+
+def gen_pta(seed, binary, n=1000, extra=""):
     np.random.seed(seed)
-    model = get_model(io.StringIO(pta_par(seed, binary)))
+    model = get_model(io.StringIO(_par(seed, binary, extra)))
     ts = sim.make_fake_toas_uniform(53000, 56652, n, model,
                                     freq=np.array([800, 1200, 1600, 2000]) * u.MHz,
                                     obs="geocenter", error=0.5 * u.us, add_noise=True,
@@ -215,9 +225,9 @@ def gen_pta(seed, binary, n=1000):
                                     multi_freqs_in_epoch=False)
     model.find_empty_masks(ts, freeze=True)
     name = {"": "pta_iso", "ELL1": "pta_ell1", "DD": "pta_dd", "ELL1H_H3": "ell1h_h3", "ELL1H_H4": "ell1h_h4",
-            "ELL1H_STIG": "ell1h_stig", "BT": "pta_bt"}[binary]
+            "ELL1H_STIG": "ell1h_stig", "BT": "pta_bt"}[binary] if not extra else extra_name
     with open(__import__("os").path.join(__import__("refcommon").GOLDEN, name + ".par"), "w") as f:
-        f.write(pta_par(seed, binary))
+        f.write(_par(seed, binary, extra))
     capture(name, model, ts, fit="gls")
 
 
@@ -234,6 +244,10 @@ if __name__ == "__main__":
         gen_pta(3, "DD")
     if "pta_bt" in which:
         gen_pta(14, "BT")
+    if "pta_dmn" in which:  # PLDMNoise (noise_model.py:443) beside PLRedNoise
+        extra_name = "pta_dmn"
+        gen_pta(15, "ELL1", extra="TNDMAMP -13.2\nTNDMGAM 2.8\nTNDMC 20\n")
+        extra_name = None
     for i, b in enumerate(("ELL1H_H3", "ELL1H_H4", "ELL1H_STIG")):
         if b.lower() in which:
             gen_pta(11 + i, b)

@@ -37,7 +37,7 @@ class SpecT(C.Structure):
                                           "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
                                           "o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px",
                                           "o_POSEPOCH", "o_DM", "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP")] + [
-        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
+        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("dmn0", C.c_int32), ("pad_", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
         ("col_kind", C.c_int32 * MAX_COLS), ("col_index", C.c_int32 * MAX_COLS), ("col_toff", C.c_int32 * MAX_COLS)]
 
 
@@ -98,6 +98,7 @@ def lib():
     L.pint_check_step.argtypes = [vp, C.c_int]
     L.pint_inst_status.argtypes = [vp, C.POINTER(C.c_int32)]
     L.pint_noise_resids.argtypes = [vp, dptr, dptr]
+    L.pint_noise_resids_dm.argtypes = [vp, dptr]
     L.pint_debug_gram.argtypes = [vp, C.c_int, dptr]
     L.pint_debug_set_resids.argtypes = [vp, dptr]
     L.pint_set_resids.argtypes = [vp, dptr]
@@ -118,7 +119,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step",
             "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
-            "pint_noise_lnlike"]
+            "pint_noise_lnlike", "pint_noise_resids_dm"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

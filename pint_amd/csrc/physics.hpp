@@ -804,6 +804,7 @@ struct EvalOut {
     double fdt;      // spin frequency at dt incl. delay (for d_phase_d_delay)
     double ftaylor;  // spin frequency at dt without delay (residuals.py:295-310)
     double dmc;      // value of this TOA's DMX design-matrix entries (compact layout)
+    double inv_f2;   // 1 / f_bary^2 (MHz^-2): PLDMNoise's basis scale (1400 MHz)^2 / f_bary^2
     int status;
 };
 
@@ -877,6 +878,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         bfreq = t.freq * (1.0 - vdl * INV_C_KMS);
     }
     double inv_f2 = 1.0 / (bfreq * bfreq);
+    o.inv_f2 = inv_f2;
     // ---- DispersionDM (dispersion_model.py:217-234) ----
     double dt_yr_dm = 0.0;
     if (S.ndm > 0) {

@@ -216,7 +216,8 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
                                            double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                            double* __restrict__ ftay, double* __restrict__ delay_out,
                                            double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                           int write_red, int* __restrict__ status, int* __restrict__ istatus) {
+                                           int write_red, int* __restrict__ status, int* __restrict__ istatus,
+                                           double* __restrict__ dfac) {
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -252,20 +253,24 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     ph_lo[I.roff + r] = o.phase.lo;
     ftay[I.roff + r] = o.ftaylor;
     delay_out[I.roff + r] = o.delay;
-    if (WANT_M && rowM && S.nred > 0 && write_red && !(cmp && Pd.vg)) {  // vg: generated where used
+    const bool dmn = S.dmn0 < S.nred;  // PLDMNoise modes: rescaled per TOA, rewritten every time
+    const double Dfac = 1400.0 * 1400.0 * o.inv_f2;
+    if (WANT_M && rowM && dmn) dfac[I.ooff + r] = Dfac;
+    if (WANT_M && rowM && S.nred > 0 && (write_red || dmn) && !(cmp && Pd.vg)) {  // vg: generated where used
         // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
         // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.  The basis
         // does not depend on the timing parameters: it is written once per instance and
         // layout (write_red) and stays resident in M across fit iterations.
         dd ts = dd_mul_d(t.tdb, DAYSEC);
         double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
-        for (int k = 0; k < S.nred; k++, colp += 2L * n) {
+        for (int k = write_red ? 0 : S.dmn0; k < S.nred; k++) {
             dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
             double fr = dd_to_d(dd_sub(x, dd_floor(x)));
             double sn, cs;
             sincos(TWO_PI * fr, &sn, &cs);
-            colp[r] = sn;
-            colp[r + n] = cs;
+            const double sc = k >= S.dmn0 ? Dfac : 1.0;
+            colp[2L * k * n + r] = sn * sc;
+            colp[2L * k * n + r + n] = cs * sc;
         }
     }
 }
@@ -279,9 +284,10 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                               double* __restrict__ ftay, double* __restrict__ delay_out,
                                               double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                              int write_red, int* __restrict__ status, int* __restrict__ istatus) {
+                                              int write_red, int* __restrict__ status, int* __restrict__ istatus,
+                                              double* __restrict__ dfac) {
     eval_block<WANT_M, BIN>(blockIdx.x, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                            Mout, dmxv, compact, write_red, status, istatus);
+                            Mout, dmxv, compact, write_red, status, istatus, dfac);
 }
 
 // k_eval_mix: all binary models in one launch (heaviest first: DD, ELL1, isolated blocks),
@@ -295,18 +301,19 @@ __global__ __launch_bounds__(256) void k_eval_mix(const PsrDev* __restrict__ psr
                                                   double* __restrict__ ph_hi, double* __restrict__ ph_lo,
                                                   double* __restrict__ ftay, double* __restrict__ delay_out,
                                                   double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
-                                                  int write_red, int* __restrict__ status, int* __restrict__ istatus) {
+                                                  int write_red, int* __restrict__ status, int* __restrict__ istatus,
+                                                  double* __restrict__ dfac) {
     const int n2 = off3 - off2, n1 = off2 - off1;
     const int b = blockIdx.x;
     if (b < n2)
         eval_block<WANT_M, 2>(off2 + b, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac);
     else if (b < n2 + n1)
         eval_block<WANT_M, 1>(off1 + b - n2, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay,
-                              delay_out, Mout, dmxv, compact, write_red, status, istatus);
+                              delay_out, Mout, dmxv, compact, write_red, status, istatus, dfac);
     else
         eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2718,7 +2725,8 @@ __global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restri
 //                  D_e = W_e + 1/phi_e from k_ecorr), written to every TOA of epoch e
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                   const double* __restrict__ dpars, double* __restrict__ out) {
+                                                   const double* __restrict__ dpars, double* __restrict__ out,
+                                                   int dm, const double* __restrict__ dfac) {
     const int inst = blockIdx.y;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -2727,15 +2735,17 @@ __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ ps
     if (i >= I.n) return;
     const double* a = dpars + I.coff + S.ncol;
     double v = 0.0;
-    if (S.nred > 0) {
+    const int k0 = dm ? S.dmn0 : 0, k1 = dm ? S.nred : S.dmn0;
+    if (k1 > k0) {
         const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
-        for (int k = 0; k < S.nred; k++) {
+        for (int k = k0; k < k1; k++) {
             const dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
             const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
             double sn, cs;
             sincos(TWO_PI * fr, &sn, &cs);
             v += a[2 * k] * sn + a[2 * k + 1] * cs;
         }
+        if (dm) v *= dfac[I.ooff + i];
     }
     out[I.roff - inst + i] = v;
 }
@@ -2952,6 +2962,7 @@ struct pint_ctx {
     int degv_cap = 0;
     InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
     double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
+    double* d_dfac = nullptr;  // PLDMNoise basis scale per TOA row (only with PLDMNoise pulsars)
     int max_ndc = 0;
     int m_compact = 0;  // layout of the design matrix written by the last pint_eval(want_M)
     int red_valid[2] = {0, 0};  // red-noise columns of M already written (full, compact layout)
@@ -3161,7 +3172,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
-                   (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
+                   (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart};
     for (auto p : ps) dfree(*p);
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
@@ -3475,6 +3486,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         PsrDev& d = ph.dev;
         d.vg = 0;
         if (!(ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
+              ph.spec.dmn0 >= ph.spec.nred &&  // PLDMNoise: stored, per-TOA scaled basis
               d.red0c + 1 <= VMAXR0))
             continue;
         long per = (ph.n + nsplit - 1) / nsplit;
@@ -3672,6 +3684,11 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_ic, sizeof(InstConst) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_dmxv, sizeof(double) * (out > 0 ? out : 1)));
+    {
+        bool any_dmn = false;
+        for (int k = 0; k < ninst; k++) any_dmn |= ctx->psrs[ctx->inst[k].psr].spec.dmn0 < ctx->psrs[ctx->inst[k].psr].spec.nred;
+        HIPCHK(cmalloc((void**)&ctx->d_dfac, sizeof(double) * (any_dmn && out > 0 ? out : 1)));
+    }
     HIPCHK(cmalloc((void**)&ctx->d_Sd, sizeof(double) * (sdoff > 0 ? sdoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_DD, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_DCS, sizeof(double) * (ddoff > 0 ? ddoff : 1)));
@@ -3765,7 +3782,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus)
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac)
         if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
 #undef PINT_EVAL_MIX
         HIPCHK(hipGetLastError());
@@ -3781,7 +3798,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus)
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac)
         if (want_M) {
             switch (t) {
                 case 0: PINT_EVAL_LAUNCH(1, 0); break;
@@ -4408,7 +4425,7 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     int rc = PINT_OK;
     if (red) {
         hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
-                           ctx->d_inst, ctx->d_dpars, d);
+                           ctx->d_inst, ctx->d_dpars, d, 0, ctx->d_dfac);
         if (hipGetLastError() != hipSuccess ||
             hipMemcpyAsync(red, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
             rc = PINT_E_HIP;
@@ -4425,6 +4442,25 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     hipStreamSynchronize(ctx->stream);
     hipFree(d);
     if (rc) ctx->err = "pint_noise_resids: HIP error";
+    return rc;
+}
+
+int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
+    if (!ctx || ctx->ninst <= 0 || !dm) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    double* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(double) * std::max<long>(1, ctx->tot_out)));
+    int maxn = 1;
+    for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
+    hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+                       ctx->d_inst, ctx->d_dpars, d, 1, ctx->d_dfac);
+    int rc = PINT_OK;
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(dm, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+        rc = PINT_E_HIP;
+    hipStreamSynchronize(ctx->stream);
+    hipFree(d);
+    if (rc) ctx->err = "pint_noise_resids_dm: HIP error";
     return rc;
 }
 

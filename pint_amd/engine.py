@@ -176,7 +176,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         base = "".join(ch for ch in n if not ch.isdigit())
         if p.kind == "mask" and base in noise_like:
             continue
-        if n in ("TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX"):
+        if n in ("TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX", "TNDMAMP", "TNDMGAM", "TNDMC"):
             continue
         if n == "PHOFF":  # -d_offset_phase_d_PHOFF / F0 = 1/F0, the Offset column's values
             k, i = L.COL_OFFSET, 0
@@ -224,8 +224,10 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
     spec.weighted_mean = 1 if use_weighted_mean else 0
     nred = 0
     rf = rp = None
-    if use_gls_basis and "PLRedNoise" in model.components:
-        rf, rp = red_noise_freqs_weights(model, toas)
+    dmn0 = 0
+    if use_gls_basis and ("PLRedNoise" in model.components or "PLDMNoise" in model.components):
+        from .noise import fourier_modes
+        rf, rp, dmn0 = fourier_modes(model, toas)
         nred = len(rf)
     ep_lists, ep_phi, ep_param = [], [], []
     if model.mask_params("ECORR") and use_gls_basis:
@@ -239,6 +241,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
                 ep_phi.append((float(p.value) * 1e-6) ** 2)
                 ep_param.append(name)
     spec.nred = nred
+    spec.dmn0 = dmn0 if (use_gls_basis and "PLDMNoise" in model.components) else nred
     lay = PulsarLayout(model=model, toas=toas, n=toas.ntoas, offsets=offs, tstride=tstride, columns=cols,
                        spec=spec, nred=nred, K=len(cols) + 2 * nred, red_freq=rf, red_phi=rp, track_mode=tm)
     if ep_lists:
@@ -675,13 +678,19 @@ class Session:
         red = np.empty(sum(n))
         ec = np.empty(sum(n))
         self._check(self.L.pint_noise_resids(self.ctx, L.ptr(red), L.ptr(ec)))
+        anydm = any(l.spec.dmn0 < l.nred for l in self.inst_layout)
+        dm = np.zeros(sum(n))
+        if anydm:
+            self._check(self.L.pint_noise_resids_dm(self.ctx, L.ptr(dm)))
         out = []
-        for lay, r, e in zip(self.inst_layout, self._split(red, n), self._split(ec, n)):
+        for lay, r, e, m in zip(self.inst_layout, self._split(red, n), self._split(ec, n), self._split(dm, n)):
             d = {}
             if "EcorrNoise" in lay.model.components:
                 d["ecorr_noise"] = e.copy()
-            if lay.nred > 0:
+            if lay.spec.dmn0 > 0:
                 d["pl_red_noise"] = r.copy()
+            if lay.spec.dmn0 < lay.nred:
+                d["pl_DM_noise"] = m.copy()
             out.append(d)
         return out
 

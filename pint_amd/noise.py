@@ -44,6 +44,40 @@ def red_noise_freqs_weights(model, toas):
     return f, phi * ff[0]
 
 
+def dm_noise_freqs_weights(model, toas):
+    """PLDMNoise (noise_model.py:443-540): (f_k [nmodes], phi [2 nmodes]) as for PLRedNoise
+    with TNDMAMP/TNDMGAM/TNDMC; its basis is the Fourier basis times (1400 MHz / f_bary)^2 per
+    TOA, formed on the device (the barycentric frequency depends on the model)."""
+    amp, gam, nf = model.dm_noise_params()
+    t = toas.tdbld * np.longdouble(86400)
+    T = t.max() - t.min()
+    f = np.linspace(1 / T, nf / T, nf)
+    ff = np.zeros(2 * nf)
+    ff[::2] = f
+    ff[1::2] = f
+    fyr = 1 / 3.16e7
+    phi = amp ** 2 / 12.0 / np.pi ** 2 * fyr ** (gam - 3) * ff ** (-gam)
+    return f, phi * ff[0]
+
+
+def fourier_modes(model, toas):
+    """All Fourier noise modes of the model in the device's order: PLRedNoise, then
+    PLDMNoise.  Returns (f [nmodes], phi [2 nmodes], first DM mode)."""
+    fs, ph = [], []
+    if "PLRedNoise" in model.components:
+        f, p = red_noise_freqs_weights(model, toas)
+        fs.append(f)
+        ph.append(p)
+    n_red = sum(len(f) for f in fs)
+    if "PLDMNoise" in model.components:
+        f, p = dm_noise_freqs_weights(model, toas)
+        fs.append(f)
+        ph.append(p)
+    if not fs:
+        return None, None, 0
+    return np.concatenate(fs), np.concatenate(ph), n_red
+
+
 def fourier_basis(model, toas) -> np.ndarray:
     """Host copy of the red-noise basis for API/parity use (noise_model.py:861).  The device
     generates the same columns inside k_eval."""
@@ -88,6 +122,9 @@ def noise_basis(model, toas):
     if "PLRedNoise" in model.components:
         mats.append(fourier_basis(model, toas))
         wts.append(red_noise_freqs_weights(model, toas)[1])
+    if "PLDMNoise" in model.components:
+        raise NotImplementedError("the PLDMNoise basis depends on the barycentric frequency: it is formed on the "
+                                  "device (use noise_model_basis_weight for its weights)")
     if "EcorrNoise" in model.components or model.mask_params("ECORR"):
         t = np.asarray(toas.tdbld * np.longdouble(86400))
         for name in model.mask_params("ECORR"):

@@ -39,10 +39,10 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Session, build_layout, pack_table
-from .noise import red_noise_freqs_weights
+from .noise import fourier_modes
 
-NOISE_COMPONENTS = ("ScaleToaError", "EcorrNoise", "PLRedNoise")
-RED_PARAMS = ("TNREDAMP", "TNREDGAM", "RNAMP", "RNIDX")
+NOISE_COMPONENTS = ("ScaleToaError", "EcorrNoise", "PLRedNoise", "PLDMNoise")
+RED_PARAMS = ("TNREDAMP", "TNREDGAM", "RNAMP", "RNIDX", "TNDMAMP", "TNDMGAM")
 KIND_WLS, KIND_ECORR, KIND_ECORR_OFFSET, KIND_WOODBURY = range(4)
 
 
@@ -189,7 +189,7 @@ class NoiseLikelihood:
     def _eval_woodbury(self):
         s, lay = self.s, self.lay
         s.set_sigma(lay, self.sigma_us() * 1e-6)
-        red = red_noise_freqs_weights(self.model, self.toas)[1] if lay.nred > 0 else None
+        red = fourier_modes(self.model, self.toas)[1] if lay.nred > 0 else None
         s.set_noise_weights(lay, red, self._ep_w())
         try:  # only the Woodbury factor of the noise block is needed (cf. Residuals.update)
             s.fit_step(1)

@@ -196,6 +196,8 @@ _DEFS = {
     "TNREDAMP": ("PLRedNoise", "float", "", False, None), "TNREDGAM": ("PLRedNoise", "float", "", False, None),
     "TNREDC": ("PLRedNoise", "float", "", False, None), "RNAMP": ("PLRedNoise", "float", "", False, None),
     "RNIDX": ("PLRedNoise", "float", "", False, None),
+    "TNDMAMP": ("PLDMNoise", "float", "", False, None), "TNDMGAM": ("PLDMNoise", "float", "", False, None),
+    "TNDMC": ("PLDMNoise", "float", "", False, None),
 }
 
 _ALIASES = {

@@ -235,9 +235,11 @@ _ORDER = {
     "ELL1H": ["PB", "PBDOT", "A1", "A1DOT", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "H3", "H4", "STIGMA",
               "NHARMS"],
     "PLRedNoise": ["RNAMP", "RNIDX", "TNREDAMP", "TNREDGAM", "TNREDC"],
+    "PLDMNoise": ["TNDMAMP", "TNDMGAM", "TNDMC"],
 }
 MIDDLE = ["TroposphereDelay", "SolarSystemShapiro", "SolarWindDispersion", "DispersionDM", "DispersionDMX",
-          "Binary", "FD", "AbsPhase", "PhaseOffset", "PhaseJump", "EcorrNoise", "ScaleToaError", "PLRedNoise"]
+          "Binary", "FD", "AbsPhase", "PhaseOffset", "PhaseJump", "EcorrNoise", "ScaleToaError", "PLRedNoise",
+          "PLDMNoise"]
 
 
 def _by_index(names, prefix):

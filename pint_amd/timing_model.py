@@ -23,7 +23,7 @@ from .parameter import LD, Param
 DELAY_ORDER = ["AstrometryEquatorial", "AstrometryEcliptic", "TroposphereDelay", "SolarSystemShapiro",
                "SolarWindDispersion", "DispersionDM", "DispersionDMX", "BinaryELL1", "BinaryDD", "FD"]
 PHASE_ORDER = ["AbsPhase", "Spindown", "PhaseOffset", "PhaseJump"]
-NOISE = ["ScaleToaError", "EcorrNoise", "PLRedNoise"]
+NOISE = ["ScaleToaError", "EcorrNoise", "PLRedNoise", "PLDMNoise"]
 
 ELL1_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "EDOT", "OMDOT", "M2", "SINI", "TASC", "EPS1", "EPS2",
                "EPS1DOT", "EPS2DOT"]
@@ -120,11 +120,11 @@ class TimingModel:
 
     @property
     def has_correlated_errors(self) -> bool:
-        return "PLRedNoise" in self.components or "EcorrNoise" in self.components
+        return any(c in self.components for c in ("PLRedNoise", "PLDMNoise", "EcorrNoise"))
 
     @property
     def has_time_correlated_errors(self) -> bool:
-        return "PLRedNoise" in self.components
+        return "PLRedNoise" in self.components or "PLDMNoise" in self.components
 
     @property
     def astrometry_kind(self) -> int:
@@ -195,6 +195,11 @@ class TimingModel:
         fac = (86400.0 * 365.24 * 1e6) / (2.0 * np.pi * np.sqrt(3.0))
         return float(self.RNAMP.value) / fac, -1.0 * float(self.RNIDX.value), nf
 
+    def dm_noise_params(self):
+        """(amp, gamma, nmodes) of PLDMNoise (noise_model.py:508-511 get_pl_vals)."""
+        nf = int(self.TNDMC.value) if "TNDMC" in self and self.TNDMC.value is not None else 30
+        return 10.0 ** float(self.TNDMAMP.value), float(self.TNDMGAM.value), nf
+
     def find_empty_masks(self, toas, freeze=False):
         """Free mask/DMX parameters that select no TOAs (timing_model.py:2895)."""
         bad = []
@@ -238,11 +243,24 @@ class TimingModel:
         return noise_basis(self, toas)[0]
 
     def noise_model_basis_weight(self, toas):
-        from .noise import noise_basis
-        return noise_basis(self, toas)[1]
+        """timing_model.py:1716: the prior variances, PLRedNoise, PLDMNoise, then ECORR."""
+        from .noise import fourier_modes, noise_basis
+        if "PLDMNoise" not in self.components:
+            return noise_basis(self, toas)[1]
+        _, phi, _ = fourier_modes(self, toas)
+        ec = noise_basis(_without(self, "PLRedNoise", "PLDMNoise"), toas)[1] if self.mask_params("ECORR") else None
+        return phi if ec is None else np.concatenate([phi, ec])
 
     def __repr__(self):
         return f"<TimingModel {self.name}: {', '.join(self.component_names)}>"
+
+
+def _without(model, *comps):
+    """A shallow view of model without the named components (for the ECORR weights)."""
+    import copy as _copy
+    m = _copy.copy(model)
+    m.components = {k: v for k, v in model.components.items() if k not in comps}
+    return m
 
 
 def _parse_mask_line(model: TimingModel, base: str, fields: List[str], counters: Dict[str, int]):
@@ -394,6 +412,8 @@ def get_model(parfile) -> TimingModel:
     for noise in ("TNREDAMP", "RNAMP"):
         if noise in model and model[noise].value is not None:
             model.components.setdefault("PLRedNoise", [])
+    if "TNDMAMP" in model and model.TNDMAMP.value is not None:
+        model.components.setdefault("PLDMNoise", [])
     # normalise the components dict keys used above for the binary
     for n, p in model._params.items():
         if p.component == "Binary":

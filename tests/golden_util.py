@@ -9,7 +9,8 @@ PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "
         "pta_iso": "pta_iso.par", "pta_ell1": "pta_ell1.par", "pta_dd": "pta_dd.par",
         "wls_phoff": "wls_phoff.par", "ecorr_phoff": "ecorr_phoff.par", "wls_noise": "wls_noise.par",
         "ecorr_fit": "ecorr_fit.par", "white_mjd": "white_mjd.par", "ell1h_h3": "ell1h_h3.par",
-        "ell1h_h4": "ell1h_h4.par", "ell1h_stig": "ell1h_stig.par", "pta_bt": "pta_bt.par"}
+        "ell1h_h4": "ell1h_h4.par", "ell1h_stig": "ell1h_stig.par", "pta_bt": "pta_bt.par",
+        "pta_dmn": "pta_dmn.par"}
 
 
 def load(name):

@@ -17,9 +17,9 @@ import pint_oracle as O
 pytestmark = pytest.mark.gpu
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise",
-         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt"]
+         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn"]
 GLS_NAMES = ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ecorr_fit", "ell1h_h3", "ell1h_h4",
-             "ell1h_stig", "pta_bt"]
+             "ell1h_stig", "pta_bt", "pta_dmn"]
 
 
 @pytest.fixture(scope="module", params=NAMES)
@@ -695,3 +695,18 @@ def test_grid_downhill_extra_matches_single_fits():
             assert abs(got / want - 1) < 1e-9, (k, got, want)
             assert abs(ex["DM"].ravel()[k] - float(g.model.DM.value)) < 1e-9 * abs(float(g.model.DM.value)), k
     assert ex["DM"].shape == c2.shape  # meshgrid-shaped like chi2 (gridutils.py:334-370)
+
+
+def test_pldm_noise_resids():
+    """PLDMNoise (noise_model.py:443-540) in the GLS fit: its basis (Fourier modes times
+    (1400 MHz / f_bary)^2) and weights beside PLRedNoise's; the fit's noise realisations
+    per component (fitter.py:2270-2282) against the reference's."""
+    from pint_amd import GLSFitter
+    model, toas, z, meta = load("pta_dmn")
+    f = GLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    for comp in ("pl_red_noise", "pl_DM_noise"):
+        v = z["gls_noise_" + comp]
+        err = np.max(np.abs(f.resids.noise_resids[comp] - v)) / np.max(np.abs(v))
+        # end to end, the realisations carry the step's conditioning (cf. TOL_NOISE, test_gpu_stage.py)
+        assert err < 1e-4, (comp, err)
