@@ -109,7 +109,8 @@ typedef struct {
     int32_t dmn0;           /* first PLDMNoise mode among the nred Fourier modes (= nred: none);
                                modes >= dmn0 are scaled by (1400 MHz / f_bary)^2 per TOA
                                (noise_model.py:443-540 PLDMNoise.get_noise_basis)           */
-    int32_t pad_;
+    int32_t k96;            /* DDK: 1 = Kopeikin (1996) proper-motion terms on a1, omega and i
+                               (K96, the reference default; DDK_model.py:157-349), 0 = off */
     double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
     double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
     double red_t0;          /* unused reserve                                           */

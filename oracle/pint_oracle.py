@@ -83,6 +83,8 @@ def from_fixture(meta) -> OModel:
         val = d.get("value")
         if isinstance(val, list):
             vals[name] = LD(val[0]) + LD(val[1])
+        elif d.get("kind") == "boolParameter" and val is not None:  # e.g. DDK's K96
+            vals[name] = 1.0 if str(val).strip().upper() in ("TRUE", "1", "Y", "T") else 0.0
         if d.get("key"):
             masks[name] = (d["key"], d.get("key_value") or [])
     comps = set(mm["components"])
@@ -95,7 +97,11 @@ def from_product_model(model) -> OModel:
     vals, masks = {}, {}
     for n in model.params:
         p = model[n]
-        if p.kind in ("str", "bool"):
+        if p.kind == "bool":  # e.g. DDK's K96 (unset: the binary's default True)
+            if p.value is not None:
+                vals[n] = 1.0 if p.value else 0.0
+            continue
+        if p.kind == "str":
             continue
         if p.value is not None:
             vals[n] = LD(p.value) if (p.long_double or p.kind == "mjd") else float(p.value)
@@ -232,6 +238,12 @@ def _rot_ecl_to_icrs(obl, v):
     c, s = np.cos(obl), np.sin(obl)
     v = np.atleast_2d(v)
     return np.stack([v[:, 0], c * v[:, 1] - s * v[:, 2], s * v[:, 1] + c * v[:, 2]], axis=1)
+
+
+def _rot_icrs_to_ecl(obl, v):
+    c, s = np.cos(obl), np.sin(obl)
+    v = np.atleast_2d(v)
+    return np.stack([v[:, 0], c * v[:, 1] + s * v[:, 2], -s * v[:, 1] + c * v[:, 2]], axis=1)
 
 
 def psr_dir_icrs(om: OModel, epoch_mjd: np.ndarray) -> np.ndarray:
@@ -560,6 +572,8 @@ class _DD:
         self.OMDOT = LD(om.v("OMDOT")) * LD(DEG_RAD) / LD(YR_S)
         self.k = self.OMDOT / (LD(2 * np.pi) / self.pb)
         self.omega = LD(om.v("OM")) * LD(DEG_RAD) + self.nu * self.k
+        self.SINI = LD(om.v("SINI"))
+        self._kopeikin()
         self.DR, self.DTH = LD(om.v("DR")), LD(om.v("DTH"))
         self.er, self.eTh = e * (1 + self.DR), e * (1 + self.DTH)
         self.sw, self.cw = np.sin(self.omega), np.cos(self.omega)
@@ -575,13 +589,19 @@ class _DD:
         dI = self.Dre * (1 - nH * self.Drep + (nH * self.Drep) ** 2 + 0.5 * nH ** 2 * self.Dre * self.Drepp
                          - 0.5 * e * sE / (1 - e * cE) * nH ** 2 * self.Dre * self.Drep)
         self.TM2 = LD(om.v("M2")) * LD(TSUN)
-        self.SINI = LD(om.v("SINI"))
         self.logNum = 1 - e * cE - self.SINI * (self.sw * (cE - e) + np.sqrt(1 - e ** 2) * self.cw * sE)
         dS = -2 * self.TM2 * np.log(self.logNum)
         self.A0, self.B0 = LD(om.v("A0")), LD(om.v("B0"))
         oPn = self.omega + self.nu
         dA = self.A0 * (np.sin(oPn) + e * self.sw) + self.B0 * (np.cos(oPn) + e * self.cw)
         self.delay = dI + dS + dA
+
+    def _kopeikin(self):
+        """DDK's corrections to a1, omega and SINI (none for DD)."""
+
+    def _kop_deriv(self, par):
+        """DDK's extra d(a1)/d(par), d(omega)/d(par) (SI) and prtl_der('SINI', par)."""
+        return 0.0, 0.0, (1.0 if par == "SINI" else 0.0)
 
     def deriv(self, par):
         """d_DDdelay_d_par (DD_model.py:855) per SI unit of par."""
@@ -602,6 +622,7 @@ class _DD:
             d_pb = z + 1
         elif par == "PBDOT": d_M, d_pb = -LD(np.pi) * tt0 ** 2 / PBs ** 2, tt0
         elif par == "XPBDOT": d_M = -LD(np.pi) * tt0 ** 2 / PBs ** 2
+        ka1, kom, d_SI = self._kop_deriv(par)
         omeE = 1 - e * cE
         dEdECC = sE / (1.0 - e * cE)
         if par == "T0": d_E = (d_M - self.EDOT * sE) / (1.0 - cE * e)
@@ -621,6 +642,8 @@ class _DD:
         elif par == "OMDOT": d_om = self.pb / LD(2 * np.pi) * self.nu
         elif orbit: d_om = d_nu * self.k + d_pb * self.nu * self.OMDOT / LD(2 * np.pi)
         else: d_om = self.k * d_nu
+        d_om = d_om + kom
+        d_a1 = d_a1 + ka1  # alpha and d_beta_d_par; DD's d_beta_d_T0 keeps d_a1_d_T0 (DD_model.py:352)
         d_er = e if par == "DR" else d_ecc
         d_eTh = e if par == "DTH" else d_ecc
         sw, cw, eTh = self.sw, self.cw, self.eTh
@@ -651,7 +674,6 @@ class _DD:
         sq1 = np.sqrt(1 - e ** 2)
         ln, TM2, SI = self.logNum, self.TM2, self.SINI
         d_TM2 = LD(TSUN) if par == "M2" else 0.0
-        d_SI = 1.0 if par == "SINI" else 0.0
         dS = (d_TM2 * (-2 * np.log(ln)) + d_ecc * (-2 * TM2 / ln * (-cE - SI * (-e * cw * sE / sq1 - sw)))
               + d_E * (-2 * TM2 / ln * (e * sE - SI * (sq1 * cE * cw - sE * sw)))
               + d_om * (2 * TM2 / ln * SI * ((cE - e) * cw - sq1 * sE * sw))
@@ -665,8 +687,94 @@ class _DD:
         return dI + dS + dA
 
 
+class _DDK(_DD):
+    """DDK_model.py: DD with Kopeikin (1995) annual-orbital parallax terms on a1 and omega
+    (:355-524, Eqs. 15-19) and, with K96, the Kopeikin (1996) proper-motion terms on a1,
+    omega and the inclination (:157-349); SINI = sin(kin) (:140).  obs_pos and psr_pos are
+    in the astrometry's frame (pulsar_binary.py:398-416).  Derivatives follow the
+    reference's prtl_der chain: d_a1_d_par / d_omega_d_par gain d_delta_*_d_{KIN,KOM,T0}
+    (:547-602), d_SINI_d_{KIN,KOM,T0} as written (:176-195, incl. its T0 and non-K96 forms),
+    and DD's d_beta_d_T0 still uses binary_generic's d_a1_d_T0."""
+
+    def __init__(self, om, bt_days, acc, obs_pos, psr_pos):
+        self.obs_pos = np.asarray(obs_pos, dtype=float)
+        self.psr_pos = np.asarray(psr_pos, dtype=float)
+        super().__init__(om, bt_days, acc)
+
+    def _kopeikin(self):
+        om = self.om
+        self.K96 = bool(om.v("K96", 1.0))
+        ecl = "AstrometryEcliptic" in om.comps
+        pml = LD(om.v("PMELONG" if ecl else "PMRA")) * LD(MASYR_RADS)
+        pmb = LD(om.v("PMELAT" if ecl else "PMDEC")) * LD(MASYR_RADS)
+        KIN, KOM = LD(om.v("KIN")) * LD(DEG_RAD), LD(om.v("KOM")) * LD(DEG_RAD)
+        sK, cK = np.sin(KOM), np.cos(KOM)
+        tt0 = self.tt0
+        A = -pml * sK + pmb * cK           # d kin / dt (delta_kin_proper_motion)
+        Bv = pml * cK + pmb * sK
+        dkin = A * tt0 if self.K96 else 0 * tt0
+        kin = KIN + dkin
+        sk, ck = np.sin(kin), np.cos(kin)
+        tk = sk / ck
+        # psr_pos setter (:106-121), delta_I0 / delta_J0 (:355-373)
+        sl = self.psr_pos[:, 2].astype(LD)
+        cl = np.cos(np.arcsin(sl))
+        slo, clo = self.psr_pos[:, 1] / cl, self.psr_pos[:, 0] / cl
+        ox, oy, oz = (self.obs_pos[:, i].astype(LD) for i in range(3))
+        dI0 = -ox * slo + oy * clo
+        dJ0 = -ox * sl * clo - oy * sl * slo + oz * cl
+        ipx = LD(om.v("PX")) / LD(KPC_KM)  # 1/PX_kpc per km
+        P1 = (dI0 * sK - dJ0 * cK) * ipx
+        P2 = (dI0 * cK + dJ0 * sK) * ipx
+        P3 = (-dI0 * sK + dJ0 * cK) * ipx
+        a1b = self.a1
+        a1pm = a1b * dkin / tk if self.K96 else 0 * tt0
+        a1p = a1b + a1pm
+        self.a1 = a1p + a1p / tk * P1
+        wpm = Bv / sk * tt0 if self.K96 else 0 * tt0
+        self.omega = self.omega + wpm - P2 / sk
+        self.SINI = sk
+        # derivative pieces per (KIN, KOM, T0), SI units
+        z = 0 * tt0
+        dk = {"KIN": z + 1, "KOM": -Bv * tt0 if self.K96 else z, "T0": z - A if self.K96 else z}
+        dpm_a1 = {"KIN": -a1b * dkin / sk ** 2,
+                  "KOM": a1b * (-Bv * tt0) * (-dkin / sk ** 2 + 1 / tk),
+                  "T0": a1b * (-A) * (-dkin / sk ** 2 + 1 / tk)} if self.K96 else {k: z for k in dk}
+        base_a1 = {"KIN": z, "KOM": z, "T0": z - self.A1DOT}
+        out = {}
+        for p in ("KIN", "KOM", "T0"):
+            da1p = base_a1[p] + dpm_a1[p]   # d_a1_k_d_par(p, pm=K96, px=False)
+            dpx = (da1p / tk - a1p * dk[p] / sk ** 2) * P1
+            if p == "KOM":
+                dpx = dpx + a1p / tk * P2
+            ka1 = dpm_a1[p] + dpx
+            if self.K96:
+                if p == "KIN":
+                    dwpm = -ck / sk ** 2 * Bv * tt0
+                elif p == "KOM":
+                    dwpm = (-ck / sk ** 2 * (-Bv * tt0) * Bv + A / sk) * tt0
+                else:
+                    dwpm = (-ck / sk ** 2 * (-A) * tt0 - 1 / sk) * Bv
+            else:
+                dwpm = z
+            dwpx = ck / sk ** 2 * dk[p] * P2
+            if p == "KOM":
+                dwpx = dwpx - P3 / sk
+            if p == "KIN":
+                dsi = ck
+            elif p == "KOM":  # non-K96: cos(kin) per degree, 1 per day (:180-195)
+                dsi = -Bv * tt0 * ck if self.K96 else ck / LD(DEG_RAD)
+            else:
+                dsi = z - A if self.K96 else z + 1 / LD(DAYSEC)
+            out[p] = (ka1, dwpm + dwpx, dsi)
+        self._kd = out
+
+    def _kop_deriv(self, par):
+        return self._kd.get(par, (0.0, 0.0, 0.0))
+
+
 BIN_UNIT = {"PB": DAYSEC, "T0": DAYSEC, "TASC": DAYSEC, "OM": DEG_RAD, "OMDOT": DEG_RAD / YR_S,
-            "EPS1DOT": 1e-12, "EPS2DOT": 1e-12}
+            "EPS1DOT": 1e-12, "EPS2DOT": 1e-12, "KIN": DEG_RAD, "KOM": DEG_RAD}
 BIN_PARAMS = {"PB", "PBDOT", "XPBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "GAMMA",
               "DR", "DTH", "A0", "B0", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "H3", "H4", "STIGMA",
               "KIN", "KOM"}
@@ -743,7 +851,13 @@ def evaluate(om: OModel, toas: dict, with_tzr=True):
     out["binary_obj"] = None
     if om.binary:
         bt = tdb  # barycentric days; acc_delay = delay so far (pulsar_binary.py:398)
-        B = {"ELL1": _ELL1, "ELL1H": _ELL1H, "DD": _DD, "BT": _BT}[om.binary](om, bt, delay.astype(LD))
+        if om.binary == "DDK":  # obs_pos / psr_pos in the astrometry's frame (pulsar_binary.py:398-416)
+            op, pp = pos, L
+            if "AstrometryEcliptic" in om.comps:
+                op, pp = _rot_icrs_to_ecl(OBL[om.ecl], pos), _rot_icrs_to_ecl(OBL[om.ecl], L)
+            B = _DDK(om, bt, delay.astype(LD), op, pp)
+        else:
+            B = {"ELL1": _ELL1, "ELL1H": _ELL1H, "DD": _DD, "BT": _BT}[om.binary](om, bt, delay.astype(LD))
         d = B.delay.astype(float)
         out["binary"] = d
         out["binary_obj"] = B

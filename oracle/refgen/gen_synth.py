@@ -113,6 +113,20 @@ OMDOT 0.01 1
 GAMMA 0.0004 1
 PBDOT 1e-12 1
 """
+    elif binary.startswith("DDK"):
+        # binary_ddk.py / DDK_model.py: KIN/KOM replace SINI; Kopeikin (1995) annual-orbital
+        # parallax and (1996) proper-motion terms on a1, omega and i; K96 N drops the latter
+        par += f"""BINARY DDK
+A1 {rng.uniform(5, 30):.9f} 1
+PB {rng.uniform(5, 60):.12f} 1
+T0 54801.987654321 1
+ECC {rng.uniform(0.05, 0.4):.8f} 1
+OM {rng.uniform(0, 360):.6f} 1
+OMDOT 0.01 1
+M2 0.3 1
+KIN {rng.uniform(50, 80):.6f} 1
+KOM {rng.uniform(0, 360):.6f} 1
+""" + ("K96 N\n" if binary == "DDK_NK" else "")
     elif binary == "DD":
         par += f"""BINARY DD
 A1 {rng.uniform(5, 30):.9f} 1
@@ -225,7 +239,8 @@ def gen_pta(seed, binary, n=1000, extra=""):
                                     multi_freqs_in_epoch=False)
     model.find_empty_masks(ts, freeze=True)
     name = {"": "pta_iso", "ELL1": "pta_ell1", "DD": "pta_dd", "ELL1H_H3": "ell1h_h3", "ELL1H_H4": "ell1h_h4",
-            "ELL1H_STIG": "ell1h_stig", "BT": "pta_bt"}[binary] if not extra else extra_name
+            "ELL1H_STIG": "ell1h_stig", "BT": "pta_bt",
+            "DDK": "pta_ddk", "DDK_NK": "pta_ddk_nk"}[binary] if not extra else extra_name
     with open(__import__("os").path.join(__import__("refcommon").GOLDEN, name + ".par"), "w") as f:
         f.write(_par(seed, binary, extra))
     capture(name, model, ts, fit="gls")
@@ -244,6 +259,10 @@ if __name__ == "__main__":
         gen_pta(3, "DD")
     if "pta_bt" in which:
         gen_pta(14, "BT")
+    if "pta_ddk" in which:
+        gen_pta(16, "DDK")
+    if "pta_ddk_nk" in which:
+        gen_pta(17, "DDK_NK")
     if "pta_dmn" in which:  # PLDMNoise (noise_model.py:443) beside PLRedNoise
         extra_name = "pta_dmn"
         gen_pta(15, "ELL1", extra="TNDMAMP -13.2\nTNDMGAM 2.8\nTNDMC 20\n")

@@ -37,7 +37,7 @@ class SpecT(C.Structure):
                                           "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
                                           "o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px",
                                           "o_POSEPOCH", "o_DM", "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP")] + [
-        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("dmn0", C.c_int32), ("pad_", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
+        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("dmn0", C.c_int32), ("k96", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
         ("col_kind", C.c_int32 * MAX_COLS), ("col_index", C.c_int32 * MAX_COLS), ("col_toff", C.c_int32 * MAX_COLS)]
 
 

@@ -261,6 +261,8 @@ struct BinState {
     double snu, cnu, sw, cw, soPn, coPn, logNum, lgNum, sqTh, sqE;  // DD
     double ipb, iPBs;  // 1/pb (pbprime), 1/PBs
     double iomeE, isnu, ilogNum, isqTh, isqE;  // DD: 1/(1 - e cosE), 1/sin(nu), ...
+    // DDK: the Kopeikin terms' d(a1), d(omega) (SI) and prtl_der("SINI", .) per KIN, KOM, T0
+    double kA1[3], kOM[3], kSI[3];
     double delay;
     int status;
 };
@@ -502,8 +504,71 @@ PD double ell1_deriv(const BinState& B, const Ell1Grad& g, int pid) {
     }
 }
 
+// ---- DDK (DDK_model.py): Kopeikin corrections to DD's a1, omega and SINI -------------
+// a1 = a1b (1 + dkin cot(kin)) (1 + cot(kin) P1), omega += K96 csc(kin) Bv tt0 - csc(kin) P2,
+// SINI = sin(kin), kin = KIN + K96 A tt0 (:157-174, :233-252, :291-308, :399-414, :470-483,
+// :526-584), A = -mu_l sin KOM + mu_b cos KOM, Bv = mu_l cos KOM + mu_b sin KOM (proper motion
+// in the astrometry's frame, PMRA/PMDEC or PMELONG/PMELAT, rad/s), P1 = (dI0 sin KOM - dJ0 cos
+// KOM)/d, P2 = (dI0 cos KOM + dJ0 sin KOM)/d with dI0, dJ0 the observatory position projected
+// on the sky's east and north directions at the pulsar (Kopeikin 1995 Eqs. 15-16, :355-373) and
+// d = 1 kpc / PX.  obs (km) and psr (unit) are in the astrometry's frame.  The derivative
+// pieces per KIN, KOM, T0 follow d_a1_k_d_par / d_omega_k_d_par (:547-602) and
+// d_SINI_d_{KIN,KOM,T0} as written (:176-195, incl. the T0 form without cos(kin) and the
+// non-K96 forms in per-degree / per-day units).
+PD void ddk_kopeikin(const pint_spec_t& S, const double* P, const double obs[3], const double psr[3], BinState& B) {
+    const bool k96 = S.k96 != 0;
+    const double mul = (S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0) * MASYR_RADS;
+    const double mub = (S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0) * MASYR_RADS;
+    const double KIN = binp(S, P, PINT_B_KIN) * DEG_RAD, KOM = binp(S, P, PINT_B_KOM) * DEG_RAD;
+    double sK, cK;
+    sincos(KOM, &sK, &cK);
+    const double tt0 = B.tt0;
+    const double A = -mul * sK + mub * cK, Bv = mul * cK + mub * sK;
+    const double dkin = k96 ? A * tt0 : 0.0;
+    double sk, ck;
+    sincos(KIN + dkin, &sk, &ck);
+    const double isk = 1.0 / sk, cot = ck * isk, isk2 = isk * isk;
+    // psr_pos setter (:106-121)
+    const double sl = psr[2], cl = cos(asin(sl)), icl = 1.0 / cl;
+    const double slo = psr[1] * icl, clo = psr[0] * icl;
+    const double dI0 = -obs[0] * slo + obs[1] * clo;
+    const double dJ0 = -obs[0] * sl * clo - obs[1] * sl * slo + obs[2] * cl;
+    const double ipx = (S.o_px >= 0 ? pval(P, S.o_px) : 0.0) * INV_KPC_KM;
+    const double P1 = (dI0 * sK - dJ0 * cK) * ipx, P2 = (dI0 * cK + dJ0 * sK) * ipx;
+    const double P3 = (-dI0 * sK + dJ0 * cK) * ipx;
+    const double a1b = B.a1;
+    const double a1p = k96 ? a1b + a1b * dkin * cot : a1b;
+    B.a1 = a1p + a1p * cot * P1;
+    B.omega += (k96 ? Bv * isk * tt0 : 0.0) - P2 * isk;
+    B.SINI = sk;
+    const double dk[3] = {1.0, k96 ? -Bv * tt0 : 0.0, k96 ? -A : 0.0};
+    for (int j = 0; j < 3; j++) {
+        // d_delta_a1_proper_motion_d_{KIN,KOM,T0} (:254-289)
+        double dpm = 0.0;
+        if (k96) dpm = (j == 0) ? -a1b * dkin * isk2 : a1b * dk[j] * (-dkin * isk2 + cot);
+        const double da1p = (j == 2 ? -B.A1DOT : 0.0) + dpm;  // d_a1_k_d_par(., pm=K96, px=False)
+        double dpx = (da1p * cot - a1p * dk[j] * isk2) * P1;  // d_delta_a1_parallax_d_* (:416-468)
+        if (j == 1) dpx += a1p * cot * P2;
+        B.kA1[j] = dpm + dpx;
+        double dwpm = 0.0;  // d_delta_omega_proper_motion_d_* (:310-349)
+        if (k96) {
+            if (j == 0) dwpm = -ck * isk2 * Bv * tt0;
+            else if (j == 1) dwpm = (-ck * isk2 * dk[1] * Bv + A * isk) * tt0;
+            else dwpm = (-ck * isk2 * (-A) * tt0 - isk) * Bv;
+        }
+        double dwpx = ck * isk2 * dk[j] * P2;  // d_delta_omega_parallax_d_* (:485-524)
+        if (j == 1) dwpx -= P3 * isk;
+        B.kOM[j] = dwpm + dwpx;
+    }
+    B.kSI[0] = ck;
+    B.kSI[1] = k96 ? -Bv * tt0 * ck : ck * (1.0 / DEG_RAD);
+    B.kSI[2] = k96 ? -A : 1.0 / DAYSEC;
+}
+
 // ---- DD (DD_model.py, binary_generic.py) ------------------------------------------
-PD void ddm_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B) {
+template <bool K = false>
+PD void ddm_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd tdb, double acc_delay, BinState& B,
+                  const double* kobs = nullptr, const double* kpsr = nullptr) {
     dd T0 = pdd(P, S.o_bin[PINT_B_T0]);
     dd tt = dd_add_d(dd_mul_d(dd_sub(tdb, T0), DAYSEC), -acc_delay);  // get_tt0 (binary_generic.py:372)
     B.tt0 = dd_to_d(tt);
@@ -552,6 +617,7 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd 
     B.ipb = 1.0 / B.pb;
     B.k = B.OMDOT_rs * B.pb * INV_TWO_PI;             // DD_model.py:76 k
     B.omega = binp(S, P, PINT_B_OM) * DEG_RAD + B.nu * B.k;  // :86
+    if (K) ddk_kopeikin(S, P, kobs, kpsr, B);
     B.er = e * (1 + B.DR);
     B.eTheta = e * (1 + B.DTH);
     double sw, cw;
@@ -587,6 +653,7 @@ PD void ddm_setup(const pint_spec_t& S, const double* P, const InstConst& C, dd 
     B.delay = delayI + delayS + delayA;
 }
 
+template <bool K = false>
 PD double ddm_deriv(const BinState& B, int pid) {
     const double e = B.ecc, sE = B.sinE, cE = B.cosE, tt0 = B.tt0;
     const double iP = B.iPBs, iP2 = iP * iP;
@@ -607,6 +674,17 @@ PD double ddm_deriv(const BinState& B, int pid) {
         case PINT_B_PBDOT: d_M = -PI_D * tt0 * tt0 * iP2; d_pb = tt0; break;
         case PINT_B_XPBDOT: d_M = -PI_D * tt0 * tt0 * iP2; break;
         default: break;
+    }
+    // DDK: Kopeikin pieces of d_a1_d_par / d_omega_d_par / prtl_der("SINI", .)
+    double k_a1 = 0.0, k_om = 0.0, k_si = (pid == PINT_B_SINI) ? 1.0 : 0.0;
+    if (K) {
+        const int j = pid == PINT_B_KIN ? 0 : (pid == PINT_B_KOM ? 1 : (pid == PINT_B_T0 ? 2 : -1));
+        k_si = 0.0;
+        if (j >= 0) {
+            k_a1 = B.kA1[j];
+            k_om = B.kOM[j];
+            k_si = B.kSI[j];
+        }
     }
     // E (binary_generic.py:397-448)
     double d_E_d_ECC = sE * iom;
@@ -630,6 +708,8 @@ PD double ddm_deriv(const BinState& B, int pid) {
     else if (pid == PINT_B_OMDOT) d_omega = B.pb * INV_TWO_PI * B.nu;
     else if (orbit_par) d_omega = d_nu * B.k + d_pb * B.nu * B.OMDOT_rs * INV_TWO_PI;
     else d_omega = B.k * d_nu;
+    d_omega += k_om;
+    d_a1 += k_a1;  // alpha and d_beta_d_par; DD's d_beta_d_T0 keeps d_a1_d_T0 (DD_model.py:352)
     // er / eTheta (DD_model.py:149-205): d_ecc_d_par only for T0/ECC/EDOT; DR/DTH -> ecc
     double d_er = (pid == PINT_B_DR) ? e : d_ecc;
     double d_eTh = (pid == PINT_B_DTH) ? e : d_ecc;
@@ -674,7 +754,7 @@ PD double ddm_deriv(const BinState& B, int pid) {
     double sq1 = B.sqE;
     double ilN = B.ilogNum;
     double d_TM2 = (pid == PINT_B_M2) ? TSUN : 0.0;
-    double d_SINI = (pid == PINT_B_SINI) ? 1.0 : 0.0;
+    double d_SINI = k_si;
     double TM2 = B.TM2;
     double dS = d_TM2 * (-2 * B.lgNum) +
                 d_ecc * (-2 * TM2 * ilN * (-cE - B.SINI * (-e * cw * sE * B.isqE - sw))) +
@@ -914,6 +994,16 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         bt_setup(S, P, C, t.tdb, delay, B);
         delay += B.delay;
         if (B.status) o.status = B.status;
+    } else if (BIN == 5) {
+        // obs_pos / psr_pos in the astrometry's frame (pulsar_binary.py:398-416)
+        double ko[3] = {t.pos[0], t.pos[1], t.pos[2]}, kp[3] = {L[0], L[1], L[2]};
+        if (S.astrometry == 2) {
+            icrs_to_ecl(S.obliquity, t.pos, ko);
+            icrs_to_ecl(S.obliquity, L, kp);
+        }
+        ddm_setup<true>(S, P, C, t.tdb, delay, B, ko, kp);
+        delay += B.delay;
+        if (B.status) o.status = B.status;
     }
     // ---- FD (frequency_dependent.py:70-101) ----
     double logf = 0.0;  // used by FD and its columns only
@@ -1028,6 +1118,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
                     if (BIN == 1 || BIN == 3) d = ell1_deriv(B, eg, pid);
                     if (BIN == 2) d = ddm_deriv(B, pid);
                     if (BIN == 4) d = bt_deriv(B, pid);
+                    if (BIN == 5) d = ddm_deriv<true>(B, pid);
                     colp[r] = chain * d * bin_unit_factor(pid);
                 }
                 break;

@@ -3226,7 +3226,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     int Kp = (K + 1 + 15) / 16 * 16;
     if (Kp > GMAXKP) { ctx->err = "design matrix too wide for k_gram (K+1 > 256)"; return -PINT_E_INVALID; }
     if (spec->njump > PINT_MAX_JUMP) { ctx->err = "too many JUMPs"; return -PINT_E_INVALID; }
-    if (spec->binary < 0 || spec->binary > PINT_BIN_BT) { ctx->err = "unsupported binary model"; return -PINT_E_INVALID; }
+    if (spec->binary < 0 || spec->binary > PINT_BIN_DDK) { ctx->err = "unsupported binary model"; return -PINT_E_INVALID; }
     if (spec->binary == PINT_BIN_ELL1H &&
         (spec->ell1h < 1 || spec->ell1h > 3 || (spec->ell1h == 2 && (spec->nharms < 3 || spec->nharms > 64)))) {
         ctx->err = "bad ELL1H Shapiro form";
@@ -3805,7 +3805,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                 case 1: PINT_EVAL_LAUNCH(1, 1); break;
                 case 2: PINT_EVAL_LAUNCH(1, 2); break;
                 case 3: PINT_EVAL_LAUNCH(1, 3); break;
-                default: PINT_EVAL_LAUNCH(1, 4); break;
+                case 4: PINT_EVAL_LAUNCH(1, 4); break;
+                default: PINT_EVAL_LAUNCH(1, 5); break;
             }
         } else {
             switch (t) {
@@ -3813,7 +3814,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                 case 1: PINT_EVAL_LAUNCH(0, 1); break;
                 case 2: PINT_EVAL_LAUNCH(0, 2); break;
                 case 3: PINT_EVAL_LAUNCH(0, 3); break;
-                default: PINT_EVAL_LAUNCH(0, 4); break;
+                case 4: PINT_EVAL_LAUNCH(0, 4); break;
+                default: PINT_EVAL_LAUNCH(0, 5); break;
             }
         }
 #undef PINT_EVAL_LAUNCH

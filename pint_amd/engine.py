@@ -143,7 +143,9 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.o_JUMP = pos
         for n in jumps:
             place(n)
-    spec.binary = {None: L.BIN_NONE, "ELL1": L.BIN_ELL1, "DD": L.BIN_DD, "ELL1H": L.BIN_ELL1H, "BT": L.BIN_BT}[model.binary]
+    spec.binary = {None: L.BIN_NONE, "ELL1": L.BIN_ELL1, "DD": L.BIN_DD, "ELL1H": L.BIN_ELL1H, "BT": L.BIN_BT,
+                   "DDK": L.BIN_DDK}[model.binary]
+    spec.k96 = 0 if (model.binary == "DDK" and "K96" in model and model.K96.value is False) else 1
     if model.binary:
         for n, pid in BIN_IDS.items():
             if n in model:

@@ -187,6 +187,9 @@ _DEFS = {
     "SINI": ("Binary", "float", "", False, None),
     "GAMMA": ("Binary", "float", "s", False, None),
     "DR": ("Binary", "float", "", False, None), "DTH": ("Binary", "float", "", False, None),
+    # DDK (binary_ddk.py:120-145): inclination and node longitude (deg), the K96 flag
+    "KIN": ("Binary", "float", "deg", False, None), "KOM": ("Binary", "float", "deg", False, None),
+    "K96": ("Binary", "bool", "", False, None),
     "A0": ("Binary", "float", "s", False, None), "B0": ("Binary", "float", "s", False, None),
     "TASC": ("Binary", "mjd", "d", True, None),
     "EPS1": ("Binary", "float", "", True, None), "EPS2": ("Binary", "float", "", True, None),

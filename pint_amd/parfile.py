@@ -231,6 +231,8 @@ _ORDER = {
     "DD": ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "A0", "B0", "GAMMA",
            "DR", "DTH"],
     "ELL1": ["PB", "PBDOT", "A1", "A1DOT", "M2", "SINI", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT"],
+    "DDK": ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "A0", "B0", "GAMMA",
+            "DR", "DTH", "KIN", "KOM", "K96"],
     "BT": ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "GAMMA"],
     "ELL1H": ["PB", "PBDOT", "A1", "A1DOT", "TASC", "EPS1", "EPS2", "EPS1DOT", "EPS2DOT", "H3", "H4", "STIGMA",
               "NHARMS"],
@@ -296,6 +298,18 @@ def _ell1_comments(model) -> str:
     return "# " + "%-15s %25s" % ("ECC", str(ecc)) + "\n" + "# " + "%-15s %25s" % ("OM", str(om)) + "\n"
 
 
+def _ddk_comments(model) -> str:
+    """DDK's funcParameters KINIAU = 180 deg - KIN, KOMIAU = 90 deg - KOM and SINI = sin(KIN)
+    (binary_ddk.py:14-41, :148-174), written commented out like ELL1's."""
+    if model.binary != "DDK" or model["KIN"].value is None or model["KOM"].value is None:
+        return ""
+    kin, kom = float(model["KIN"].value), float(model["KOM"].value)
+    out = ""
+    for n, v in (("KINIAU", 180.0 - kin), ("KOMIAU", 90.0 - kom), ("SINI", np.sin(kin * (math.pi / 180)))):
+        out += "# " + "%-15s %25s" % (n, str(v)) + "\n"
+    return out
+
+
 def ordered_params(model) -> List[str]:
     top = [n for n in TOP_LEVEL if n in model._params and model[n].component in ("", "TimingModel")]
     top += [n for n, p in model._params.items() if p.component in ("", "TimingModel") and n not in top
@@ -330,7 +344,7 @@ def as_parfile(model, include_info: bool = True, comment: str = None) -> str:
     for i, n in enumerate(names):
         body += parfile_line(model[n])
         if i == last_bin:
-            body += _ell1_comments(model)
+            body += _ell1_comments(model) + _ddk_comments(model)
     return head + body
 
 

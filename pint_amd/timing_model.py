@@ -29,6 +29,7 @@ ELL1_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "EDOT", "OMDOT", "M2", "SINI", "TAS
                "EPS1DOT", "EPS2DOT"]
 DD_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "M2", "SINI", "A0", "B0",
              "GAMMA", "DR", "DTH"]
+DDK_PARAMS = [n for n in DD_PARAMS if n != "SINI"] + ["KIN", "KOM"]  # binary_ddk.py:120-145
 BT_PARAMS = ["PB", "PBDOT", "A1", "A1DOT", "ECC", "EDOT", "T0", "OM", "OMDOT", "GAMMA"]
 BIN_IDS = {"PB": 0, "PBDOT": 1, "XPBDOT": 2, "A1": 3, "A1DOT": 4, "ECC": 5, "EDOT": 6, "T0": 7, "OM": 8,
            "OMDOT": 9, "M2": 10, "SINI": 11, "GAMMA": 12, "DR": 13, "DTH": 14, "A0": 15, "B0": 16,
@@ -41,6 +42,10 @@ OBLIQUITY = {"IERS2010": 0.4090926006005829, "IERS2003": 0.40909260011576914,
 
 class MissingParameter(ValueError):
     pass
+
+
+class TimingModelError(ValueError):
+    """timing_model.py TimingModelError (an invalid model structure)."""
 
 
 class TimingModel:
@@ -181,10 +186,15 @@ class TimingModel:
             raise NotImplementedError("solar-wind dispersion (NE_SW != 0) is outside the supported hot path")
         if "CORRECT_TROPOSPHERE" in self and self.CORRECT_TROPOSPHERE.value:
             raise NotImplementedError("troposphere delay is outside the supported hot path")
-        if self.binary in ("DD", "BT"):
+        if self.binary in ("DD", "BT", "DDK"):
             e = float(self.ECC.value or 0.0)
             if not (0 <= e < 1):
                 raise ValueError("Eccentricity should be in the range of [0,1).")
+        if self.binary == "DDK":  # BinaryDDK.validate (binary_ddk.py:200-231)
+            if not self.astrometry_kind:
+                raise TimingModelError("No valid AstrometryEcliptic or AstrometryEquatorial component found")
+            if "PX" not in self or self.PX.value is None or self.PX.value <= 0.0:
+                raise TimingModelError("DDK model needs a valid `PX` value.")
 
     # -- noise ------------------------------------------------------------------------
     def red_noise_params(self):
@@ -299,8 +309,8 @@ def get_model(parfile) -> TimingModel:
     for l in lines:
         if l.name == "BINARY" and l.fields:
             binary = l.fields[0].upper()
-    if binary not in (None, "ELL1", "DD", "ELL1H", "BT"):
-        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, ELL1H, DD, BT)")
+    if binary not in (None, "ELL1", "DD", "ELL1H", "BT", "DDK"):
+        raise NotImplementedError(f"BINARY {binary} is outside the supported hot path (ELL1, ELL1H, DD, DDK, BT)")
     model.binary = binary
     has_eq = any(n in ("RAJ", "RA") for n in names)
     has_ecl = any(n in ("ELONG", "LAMBDA") for n in names)
@@ -328,6 +338,9 @@ def get_model(parfile) -> TimingModel:
     elif binary == "DD":
         defaults += [(n, 0.0) for n in DD_PARAMS]
         defaults += [("T0", None)]
+    elif binary == "DDK":  # DD's parameters less SINI, KIN/KOM 0, K96 unset (default True)
+        defaults += [(n, 0.0) for n in DDK_PARAMS]
+        defaults += [("T0", None), ("K96", None)]
     elif binary == "BT":  # binary_bt.py:38-69: no M2/SINI, GAMMA 0, rates 0
         defaults += [(n, 0.0) for n in BT_PARAMS if n != "T0"]
         defaults += [("T0", None)]

@@ -17,9 +17,9 @@ import pint_oracle as O
 pytestmark = pytest.mark.gpu
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise",
-         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn"]
+         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk"]
 GLS_NAMES = ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ecorr_fit", "ell1h_h3", "ell1h_h4",
-             "ell1h_stig", "pta_bt", "pta_dmn"]
+             "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk"]
 
 
 @pytest.fixture(scope="module", params=NAMES)

@@ -12,7 +12,7 @@ import pint_oracle as O
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise", "white_mjd", "ecorr_fit",
          "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt",
-         "pta_dmn"]
+         "pta_dmn", "pta_ddk", "pta_ddk_nk"]
 DELAY_MAP = {"delay_solar_system_geometric_delay": "geometric", "delay_solar_system_shapiro_delay": "shapiro",
              "delay_constant_dispersion_delay": "dm", "delay_DMX_dispersion_delay": "dmx",
              "delay_binarymodel_delay": "binary", "delay_FD_delay": "fd", "delay_total": "delay"}
@@ -169,7 +169,7 @@ def test_wls_fit_phoff():
 
 
 @pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ell1h_h3", "ell1h_h4",
-                                  "ell1h_stig", "pta_bt", "pta_dmn"])
+                                  "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk"])
 def test_gls_fit(name):
     om, toas, z, meta = fixture(name)
     om2, st, chi2 = O.fit_once(om, toas, gls=True)
@@ -187,7 +187,11 @@ def test_gls_fit(name):
     # the end-to-end chi2 floor (~1e-6 relative at 0.5 us TOA errors).
     d = r2["time"] - z["gls_post_resid"]
     assert np.std(d) < 2e-11 and np.max(np.abs(d)) < 1e-10
-    assert abs(chi2 / meta["gls_chi2"] - 1) < 5e-6, chi2 / meta["gls_chi2"] - 1
+    # pta_ddk_nk: the reference's non-K96 d_SINI_d_T0 (1/day, DDK_model.py:191-195) leaves a
+    # step that does not reach the minimum (its own Downhill stops with StepProblem), so the
+    # post-fit chi2 is ~10x more sensitive to the residual floor
+    tol = 2e-5 if name == "pta_ddk_nk" else 5e-6
+    assert abs(chi2 / meta["gls_chi2"] - 1) < tol, chi2 / meta["gls_chi2"] - 1
 
 
 def test_downhill_wls():
