@@ -186,7 +186,8 @@ def roofline(s, lays, kt_gram, step, args):
       exec_flops  the MFMAs it issues, counted exactly as the kernel loops them: per N-split
                   ceil(rows / 64) chunks x 16 k-steps x (NT + 1) tiles x 2048 flop (NT = the
                   [T|r|slots] x [T|r|slots|F] upper tiles less the all-slot (DD-only) tiles the
-                  kernel skips, + the trig tile); equals the PMC
+                  kernel skips, + the trig tile; with the binned DMX x F tile (PINT_OPT_VBIN) the
+                  all-slot row tiles go entirely and the binned tile comes); equals the PMC
                   SQ_INSTS_MFMA x 2048 of the profile (profiles/pmc_gram_r02.json).
     achieved = alg_flops / event time; exec_TFLOP/s beside it."""
     from pint_amd.pta import fit_cost  # noqa: F401
@@ -196,12 +197,15 @@ def roofline(s, lays, kt_gram, step, args):
         vg, ns, kpv, r0 = s.vgram_layout(l)
         if not vg:
             continue
+        vb = bool(vg & 2)  # binned DMX x F tile: the all-slot row tiles go, one binned tile comes
         n, R, nred = l.n, 2 * l.nred, l.nred
         P = r0
         alg += 2.0 * n * ((P + 1) * (P + 2) / 2 + (P + 1) * R + (P + 2) + R + 2 * (2 * nred + 1))
         ntr, ntc = (r0 + 1 + ns) // 16, kpv // 16
         nsk = ntr - (r0 + 1 + 15) // 16  # trailing all-slot row tiles: their DD-only tiles are skipped
-        nt = ntr * ntc - ntr * (ntr - 1) // 2 - nsk * (nsk + 1) // 2 + 1
+        nt = 1 + (1 if vb else 0)  # the trig tile (+ the binned tile)
+        for ti in range(ntr):      # as the kernel's loop skips them (gram_v_body)
+            nt += sum(1 for tj in range(ti, ntc) if not (ti >= ntr - nsk and (tj < ntr or vb)))
         per = -(-n // nsplit)
         per = -(-per // 4) * 4
         chunks = sum(-(-max(0, min(n, (q + 1) * per) - min(n, q * per)) // 64) for q in range(nsplit))

@@ -195,8 +195,9 @@ int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const
  * columns, no TOA in two free bins, no ECORR): pint_eval(ctx, 2) then writes the compact
  * design matrix, and pint_fit_step forms their Gram rows as bin sums. */
 int pint_fit_layout(pint_ctx *ctx, int psr, int32_t *out4);
-/* The k_gram_v layout of a pulsar in the current batch: (on the vg path, DMX slots, LDS
- * width [T | r | slots | F] padded to 16, timing columns of the compact layout). */
+/* The k_gram_v layout of a pulsar in the current batch: (on the vg path (+2 with the
+ * binned DMX x Fourier tile, PINT_OPT_VBIN), DMX slots, LDS width [T | r | slots | F]
+ * padded to 16, timing columns of the compact layout). */
 int pint_vgram_layout(pint_ctx *ctx, int psr, int32_t *out4);
 
 /* Lazy mode (1): launches return without synchronising or checking the device status;
@@ -235,6 +236,11 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * digits that LAPACK's cho_solve keeps); 0 skips it (grid points: their post-fit chi2 is
  * second order in a step error along the weak directions). */
 #define PINT_OPT_REFINE 4
+/* PINT_OPT_VBIN = 1 (default): k_gram_v forms the DMX bins' Fourier entries from one binned
+ * trig tile per k-step (the accumulator holds an even and an odd bin) instead of the DMX-slot
+ * row tiles x Fourier columns; pulsars whose aligned 4-row groups hold more than two bins
+ * (or two of one parity) leave the vg path.  Takes effect at pint_set_instances. */
+#define PINT_OPT_VBIN 5
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

@@ -71,7 +71,7 @@ struct PsrDev {
     int vg;  // compact fit layout on the k_gram_v path (DMX slots as MFMA rows, F^T W F from trig sums)
     int vns; // k_gram_v DMX slots (bins of an N-split are distinct mod vns)
     int vkp; // k_gram_v LDS width: [T | r | slots | F] padded to 16
-    int pad_;
+    int vb;  // k_gram_v binned DMX x Fourier tile (VB) for this pulsar
     double logsig;  // sum_i log sigma_i (s): the WLS likelihood normalisation (residuals.py:665)
     double sumw;    // sum_i 1/sigma_i^2 (s^-2)
 };
@@ -94,6 +94,7 @@ struct InstDev {
     long sdoff;  // DMX cross-sum offset (ndc*Kpd) / per-column sums offset (ndc)
     long ddoff;
     long vgoff;  // k_gram_v DMX slot partials offset (nsplit * vns * (Kd+3))
+    long vboff;  // k_gram_v binned DMX x Fourier partials offset (nsplit * GW * vns * 128)
     int self;    // index of this instance in the batch
     int nrb;     // k_resid row blocks of this instance (RES_RB rows each)
     long rb0;    // first k_resid row block
@@ -902,12 +903,50 @@ __device__ __forceinline__ void cpow_u8(double c1, double s1, int k, double& c, 
 // Unused columns go to a dummy LDS column (no branches in the staging).  The waves' partial
 // tiles are summed through LDS at the end.  (Built with MFMA accumulators in VGPRs: in AGPRs
 // the loop-carried tiles were copied out and back every chunk.)
-template <int NTR, int NTC, int NSK>
+// VB (binned DMX x F): the DMX bin rows' Fourier entries sum_{i in bin} x_i w_i e^{i k theta_i}
+// come from one more 16x16 tile per k-step, A^T B'' with A the trig block [cos a theta | sin a
+// theta]/sigma and B'' = x [cos 8c theta | sin 8c theta]/sigma (c < 4) in the 8 columns of the
+// row's bin parity (the other 8 zero), k = a + 8c: the accumulator holds two bins (even, odd)
+// and a half is flushed to its bin's partial (per split and wave) when a new bin of its
+// parity arrives.  It replaces the all-slot row tiles x F (4 tiles per k-step: each row has
+// one nonzero slot).  Each wave takes a contiguous quarter of the split (lane l of a chunk
+// stages row quarter (l >> 4), offset 16c + (l & 15)), so a wave meets each bin once; the
+// flushes happen once per chunk, before its MFMAs, from the first and last bin of the wave's
+// 16 rows: the host admits the layout only if every such 16-row group holds <= 2 bins, of
+// distinct parity.
+// VB: write the half of accB that holds a bin (parity p) to the bin's partial dst and clear it
+// (lanes of columns 8p..8p+7 hold it: row 4q + (lane >> 4), column lane & 7)
+__device__ __forceinline__ void vb_flush(double4_t& acc, double* __restrict__ dst, int p, int lane) {
+    const bool mine = ((lane >> 3) & 1) == p;
+    if (mine) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) dst[(4 * q + (lane >> 4)) * 8 + (lane & 7)] = acc[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[q] = mine ? 0.0 : acc[q];
+}
+// VB: bin b enters the accumulator half of its parity; a half holding another bin is flushed
+#define VB_ENTER(b)                                                                                  \
+    do {                                                                                             \
+        const int b_ = (b);                                                                          \
+        if (b_ & 1) {                                                                                \
+            if (cur1 != b_) {                                                                        \
+                if (cur1 >= 0) vb_flush(accB, vbase + (long)(cur1 % NS) * 128, 1, lane);            \
+                cur1 = b_;                                                                           \
+            }                                                                                        \
+        } else if (cur0 != b_) {                                                                     \
+            if (cur0 >= 0) vb_flush(accB, vbase + (long)(cur0 % NS) * 128, 0, lane);                 \
+            cur0 = b_;                                                                               \
+        }                                                                                            \
+    } while (0)
+
+template <int NTR, int NTC, int NSK, bool VB>
 __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restrict__ psrs,
                                             const InstDev* __restrict__ insts, const double* __restrict__ M,
                                             const double* __restrict__ rtime, const double* __restrict__ dmxv,
                                             int nsplit, double* __restrict__ Gpart, double* __restrict__ Sdp,
-                                            double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
+                                            double* __restrict__ colsq, double* __restrict__ TSp,
+                                            double* __restrict__ BFp, int dbg) {
     constexpr int NTH = GW * 64;
     constexpr int CH = VCH;
     constexpr int CS = CH + 2;  // column stride (= 2 mod 32 doubles)
@@ -916,7 +955,8 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     constexpr int KS = CH / 4 / GW;  // k-steps per wave per chunk
     constexpr int TA = 8 / GW;  // trig-block harmonics per wave
     constexpr int HMAX = 4;     // Fourier harmonics per A harmonic (a + 1 + 8u < 32)
-    static_assert(8 % GW == 0 && KS >= 1 && (GVB == 1 || GVB == 2), "k_gram_v layout");
+    static_assert(8 % GW == 0 && KS >= 1 && (GVB == 1 || GVB == 2) && (!VB || (GVB == 1 && GW == 4 && NTC <= 6)),
+                  "k_gram_v layout");
     GVTS(0);
     GVTS(4);
     const InstDev I = insts[blockIdx.y];
@@ -931,11 +971,13 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     // sin 8b theta]/sigma (b < 8): the tile A^T B holds every C_m, S_m (weighted), m = a + 8b
     // < 64 -- F^T W F (k_greduce).  The unweighted sums for the Fourier column norms depend
     // on the TOAs only (PsrDev::trigU, formed at upload).  DUM: the write-only dummy column.
-    const int tA = Kpv, tB = Kpv + 16, DUM = Kpv + 32, Kpt = Kpv + 33;
+    const int tA = Kpv, tB = Kpv + 16, DUM = Kpv + 32, tX = Kpv + 33, Kpt = Kpv + (VB ? 49 : 33);
     double* const Tb0 = lds;
     double* const Tb1 = lds + (GVB - 1) * Kpt * CS;
     long i0, i1;
     split_rows(n, nsplit, split, i0, i1);
+    // VB: chunk c, lane l -> row i0 + (l >> 4) Q + 16 c + (l & 15) (each wave a quarter)
+    const long QV = (i1 - i0 + CH - 1) / CH * 16;
     const double* Mi = M + I.moff;
     const double* ri = rtime + I.ooff;
     const double* xv = dmxv + I.ooff;
@@ -953,8 +995,17 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     double st[QL] = {};
     int d_n = -1;
     bool ok_n = false;
+    int binc = -1;              // VB: the DMX bin of this lane's staged row (-1: none)
+    int cur0 = -1, cur1 = -1;   // VB: bins held by the even / odd half of accB (wave-uniform)
+    double4_t accB = {0, 0, 0, 0};
+    double* const vbase = BFp + I.vboff + ((long)split * GW + wave) * NS * 128;
     auto load = [&](long c0) {  // the next chunk's row data -> registers (clamped rows)
         long row = c0 + lane;
+        if (VB) {  // c0 = i0 + 16 c
+            const long rel = (c0 - i0) + (long)(lane >> 4) * QV + (lane & 15);
+            row = i0 + rel;
+            if (rel >= (long)(lane >> 4) * QV + QV) row = i1;  // past this quarter (unused)
+        }
         ok_n = row < i1;
         row = ok_n ? row : i1 - 1;
         // (global-address-space loads: through generic pointers they would be flat loads,
@@ -996,6 +1047,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                 put(Ts, vsel(sl >= 0, s0 + sl, DUM), x_n * iw);
             }
             sp = sl;
+            binc = (ok_n && d_n >= 0) ? d_n : -1;
         }
 #pragma unroll
         for (int j = 0; j < TA; j++) {
@@ -1011,6 +1063,16 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
             put(Ts, tA + 8 + a, sa);
             put(Ts, tB + a, cb * iw);
             put(Ts, tB + 8 + a, sb * iw);
+            if (VB && j == 0) {
+                // B'' = x [cos 8a theta | sin 8a theta]/sigma (a < 4) in the 8 columns of the
+                // row's bin parity, zeros in the other 8
+                const bool odd = (d_n & 1) != 0;
+                const double vx = (ok_n && d_n >= 0) ? x_n * iw : 0.0;
+                put(Ts, vsel(odd, tX + 8 + a, tX + a), vx * cb);
+                put(Ts, vsel(odd, tX + 12 + a, tX + 4 + a), vx * sb);
+                put(Ts, vsel(odd, tX + a, tX + 8 + a), 0.0);
+                put(Ts, vsel(odd, tX + 4 + a, tX + 12 + a), 0.0);
+            }
             // Fourier harmonics a + 1 + 8u (<= nred): from the A harmonic by one rotation by
             // e^{i theta}, then by e^{i 8 theta}
             double c = ca, s = sa;
@@ -1048,12 +1110,14 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                 for (int tj = ti; tj < NTC; tj++, k++) {
                     // rows and columns all DMX slots (the last NSK row tiles, f0 = 16 NTR):
                     // only the DD diagonal (compile-time after unrolling)
-                    if (ti >= NTR - NSK && tj < NTR) continue;
+                    if (ti >= NTR - NSK && (tj < NTR || VB)) continue;
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
                 }
             }
             // trig tile, unconditional (zero in LDS without red noise)
-            accW = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], Tr[tB * CS], accW, 0, 0, 0);
+            const double ta = Tr[tA * CS];
+            accW = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, Tr[tB * CS], accW, 0, 0, 0);
+            if (VB) accB = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, Tr[tX * CS], accB, 0, 0, 0);
         }
     };
     const long nch = i1 > i0 ? (i1 - i0 + CH - 1) / CH : 0;
@@ -1081,13 +1145,31 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     } else {
         // one buffer, two workgroups per CU: one's staging and barriers fill the other's gaps
         GVTS(1);
+        const long CHS = VB ? 16 : CH;  // row step of a chunk (VB: per quarter)
         for (long c = 0; c < nch; c++) {
             if (!(dbg & 4)) stage(Tb0, sp0);
-            if (!(dbg & 1)) load(i0 + (c + 1) * CH);  // past the last chunk: clamped, unused
+            if (!(dbg & 1)) load(i0 + (c + 1) * CHS);  // past the last chunk: clamped, unused
             __syncthreads();
+            if (VB) {
+                // the bins of the wave's 16 rows (staging lanes 16 wave ..): the first and the
+                // last row with a bin (bins are contiguous row ranges; the host admits <= 2 per
+                // group, of distinct parity)
+                const unsigned long long m = __ballot(binc >= 0);
+                const unsigned mw = (unsigned)((m >> (16 * wave)) & 0xffffull);
+                if (mw != 0u) {
+                    const int lf = 16 * wave + __builtin_ctz(mw), ll = 16 * wave + 31 - __builtin_clz(mw);
+                    const int bf = __builtin_amdgcn_readlane(binc, lf), bl = __builtin_amdgcn_readlane(binc, ll);
+                    VB_ENTER(bf);
+                    VB_ENTER(bl);
+                }
+            }
             if (!(dbg & 2)) mfma(Tb0);
             __syncthreads();
         }
+    }
+    if (VB) {
+        if (cur0 >= 0) vb_flush(accB, vbase + (long)(cur0 % NS) * 128, 0, lane);
+        if (cur1 >= 0) vb_flush(accB, vbase + (long)(cur1 % NS) * 128, 1, lane);
     }
     GVTS(2);
     // timing-column sums of squares of this split (normalize_designmatrix)
@@ -1138,8 +1220,8 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                         Sp[(long)(pc - s0) * SW + cidx(pr)] = v;            // DMX x [T|r]
                     } else if (cs) {
                         // DMX x DMX: diagonal, DD (k_greduce forms it from the TOAs)
-                    } else {
-                        Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F
+                    } else if (!VB) {
+                        Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F (VB: binned)
                     }
                 }
             }
@@ -1173,21 +1255,32 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
 // one launch per (row tiles, column tiles) layout; the number of trailing all-slot row tiles
 // (whose tiles hold only DD and are skipped) picks the body inside, so layouts that differ
 // only in it share the launch (a launch per variant would run their tails one after another)
-template <int NTR, int NTC>
+template <int NTR, int NTC, bool VB>
+__device__ __forceinline__ void gram_v_nsk(double* lds, const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                           const double* __restrict__ M, const double* __restrict__ rtime,
+                                           const double* __restrict__ dmxv, int nsplit, double* __restrict__ Gpart,
+                                           double* __restrict__ Sdp, double* __restrict__ colsq, double* __restrict__ TSp,
+                                           double* __restrict__ BFp, int dbg, int nsk) {
+    if (nsk <= 0) {  // no all-slot row tile: VB would add a tile and remove none (PsrDev::vb = 0)
+        gram_v_body<NTR, NTC, 0, false>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
+    } else if constexpr (NTR >= 2) {
+        if (nsk == 1) gram_v_body<NTR, NTC, 1, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
+        else if constexpr (NTR >= 3) gram_v_body<NTR, NTC, 2, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
+    }
+}
+
+template <int NTR, int NTC, bool VB>
 __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                     const double* __restrict__ M, const double* __restrict__ rtime,
                                                     const double* __restrict__ dmxv, int nsplit,
                                                     double* __restrict__ Gpart, double* __restrict__ Sdp,
-                                                    double* __restrict__ colsq, double* __restrict__ TSp, int dbg) {
+                                                    double* __restrict__ colsq, double* __restrict__ TSp,
+                                                    double* __restrict__ BFp, int dbg) {
     extern __shared__ double lds[];
     const PsrDev& Pd = psrs[insts[blockIdx.y].psr];
     const int nsk = __builtin_amdgcn_readfirstlane(NTR - (Pd.red0c + 1 + 15) / 16);
-    if (nsk <= 0) {
-        gram_v_body<NTR, NTC, 0>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
-    } else if constexpr (NTR >= 2) {
-        if (nsk == 1) gram_v_body<NTR, NTC, 1>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
-        else if constexpr (NTR >= 3) gram_v_body<NTR, NTC, 2>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, dbg);
-    }
+    if constexpr (!VB || NTC <= 6)
+        gram_v_nsk<NTR, NTC, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, nsk);
 }
 
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
@@ -1269,7 +1362,8 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
                                                  double* __restrict__ Gpart, double* __restrict__ colsq,
                                                  const double* __restrict__ TS, const double* __restrict__ Sdp,
                                                  const double* __restrict__ dmxv, double* __restrict__ Sd,
-                                                 double* __restrict__ DD, double* __restrict__ DCS) {
+                                                 double* __restrict__ DD, double* __restrict__ DCS,
+                                                 const double* __restrict__ BFp, int vb) {
     __shared__ double sh[8];
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
@@ -1289,7 +1383,28 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
         for (int c = threadIdx.x; c <= Kc; c += blockDim.x) {
             double v = 0.0;
-            for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
+            if (vb && Pd.vb && c >= r0 && c < Kc) {
+                // binned DMX x F (k_gram_v VB): the 16x8 blocks D of the (split, wave) quarters
+                // the bin's rows touch; harmonic k = a_ + 8 cc: cos = D[a_][cc] - D[8+a_][4+cc],
+                // sin = D[8+a_][cc] + D[a_][4+cc]; column r0 + 2h is sin((h+1) theta), +1 cos
+                const int h = (c - r0) >> 1, k = h + 1, a_ = k & 7, cc = k >> 3;
+                const bool isin = ((c - r0) & 1) == 0;
+                const int e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
+                const int e1 = isin ? a_ * 8 + 4 + cc : (8 + a_) * 8 + 4 + cc;
+                const double sg = isin ? 1.0 : -1.0;
+                for (int q = q0; q <= q1; q++) {
+                    const long s0_ = (long)q * per, s1_ = min((long)I.n, s0_ + per), len = s1_ - s0_;
+                    const long QV = (len + VCH - 1) / VCH * 16;
+                    for (int w = 0; w < GW; w++) {
+                        const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
+                        if (w0 >= w1 || hi <= w0 || lo >= w1) continue;  // no row of the bin here
+                        const double* D = BFp + I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
+                        v += D[e0] + sg * D[e1];
+                    }
+                }
+            } else {
+                for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
+            }
             Sd[I.sdoff + (long)a * Kp + c] = v;
         }
         // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
@@ -2900,6 +3015,7 @@ struct PsrHost {
     PsrDev dev;
     pint_spec_t spec;
     std::vector<int> dlo, dhi;  // row range of each DMX column's bin (compact layout)
+    std::vector<int> drow_host; // DMX column of each TOA (-1: none), compact layout
     std::vector<void*> bufs;
     int n, K;
 };
@@ -2926,10 +3042,13 @@ struct pint_ctx {
     InstDev* d_inst_sorted_v = nullptr; // ... compact layout, generated Fourier basis (k_gram_v)
     std::vector<KpGroup> kp_groups, kp_groups_c, kp_groups_v;
     int vgram = 1;       // PINT_OPT_VGRAM
+    int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
     int n_vg = 0;        // instances on the k_gram_v path
     bool any_dmx_rows = false;  // compact instances still on k_dmx_rows / k_dmx
     double *d_TSp = nullptr, *d_TS = nullptr;  // k_gram_v per-split trig sums, their totals
     double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
+    double* d_BFp = nullptr;                    // k_gram_v binned DMX x Fourier partials (VB)
+    int vb_on = 0;                              // the batch's vg instances use VB
     bool ic_valid = false;  // per-instance constants (k_prep) current for the tables
     bool no_events = false; // PINT_NO_EVENTS=1: no per-kernel timing events (their cost)
     int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
@@ -3141,6 +3260,7 @@ pint_ctx* pint_ctx_create(int device) {
     else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
+    ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int sl = 0; sl < 2; sl++) {
@@ -3173,7 +3293,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
-                   (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart};
+                   (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart};
     for (auto p : ps) dfree(*p);
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
@@ -3324,6 +3444,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
             }
         }
         rc |= upload(ctx, ph, drow.data(), drow.size(), d.drow);
+        ph.drow_host.assign(drow.begin(), drow.end());
         ph.dlo.assign(ndc, 0);
         ph.dhi.assign(ndc, 0);
         for (int a = 0; a < ndc; a++)
@@ -3384,7 +3505,7 @@ int pint_fit_layout(pint_ctx* ctx, int psr, int32_t* out4) {
 int pint_vgram_layout(pint_ctx* ctx, int psr, int32_t* out4) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !out4) return PINT_E_INVALID;
     const PsrDev& d = ctx->psrs[psr].dev;
-    out4[0] = d.vg;
+    out4[0] = d.vg + 2 * d.vb;  // bit 1: the binned DMX x Fourier tile (PINT_OPT_VBIN)
     out4[1] = d.vns;
     out4[2] = d.vkp;
     out4[3] = d.red0c;
@@ -3485,6 +3606,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     for (auto& ph : ctx->psrs) {
         PsrDev& d = ph.dev;
         d.vg = 0;
+        d.vb = 0;
         if (!(ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
               ph.spec.dmn0 >= ph.spec.nred &&  // PLDMNoise: stored, per-TOA scaled basis
               d.red0c + 1 <= VMAXR0))
@@ -3512,10 +3634,34 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 break;
             }
         }
+        d.vb = 0;
+        // VB only with an all-slot row tile to drop (the [T | r] columns leave >= 16 slots)
+        if (d.vg && ctx->vbin && d.vkp <= 96 && d.vns >= 16) {
+            // VB (binned DMX x F): the 16 rows a wave takes from one chunk (split sp, quarter w,
+            // rows i0 + w QV + 16 c ..) hold at most two bins, of distinct parity (drow)
+            const std::vector<int>& dr = ph.drow_host;
+            for (int sp = 0; d.vg && sp < nsplit; sp++) {
+                const long i0 = std::min<long>((long)sp * per, ph.n), i1 = std::min<long>(i0 + per, ph.n);
+                const long QV = (i1 - i0 + VCH - 1) / VCH * 16;
+                for (long g = 0; d.vg && g < i1 - i0; g += 16) {  // g = w QV + 16 c
+                    const long gend = std::min<long>(g + 16, (g / QV + 1) * QV);
+                    int b0 = -1, b1 = -1;
+                    for (long r = g; r < gend && r < i1 - i0; r++) {
+                        const int b = dr[i0 + r];
+                        if (b < 0 || b == b0 || b == b1) continue;
+                        if (b0 < 0) b0 = b;
+                        else if (b1 < 0 && ((b ^ b0) & 1)) b1 = b;
+                        else d.vg = 0;
+                    }
+                }
+            }
+            d.vb = d.vg;
+        }
     }
     if (refresh_psrs(ctx)) return PINT_E_HIP;
-    long vgoff = 0;
+    long vgoff = 0, vboff = 0;
     ctx->n_vg = 0;
+    ctx->vb_on = ctx->vbin;
     ctx->any_dmx_rows = false;
     for (int k = 0; k < ninst; k++) {
         int p = inst_psr[k];
@@ -3538,8 +3684,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.sdoff = sdoff;
         I.ddoff = ddoff;
         I.vgoff = vgoff;
+        I.vboff = vboff;
         if (ph.dev.vg) {
             vgoff += (long)nsplit * ph.dev.vns * (ph.dev.Kd + 3);
+            if (ph.dev.vb) vboff += (long)nsplit * GW * ph.dev.vns * 128;
             ctx->n_vg++;
         } else if (ph.dev.dsplit) {
             ctx->any_dmx_rows = true;
@@ -3620,6 +3768,25 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             bucket[tT].push_back(k);
             if (kp > bkp[tT]) bkp[tT] = kp;
         }
+        if (lay == 2) {
+            // heaviest first within a launch (MFMAs per k-step x rows): the light blocks fill
+            // the tail of the second resident round
+            auto cost = [&](int k) {
+                const PsrDev& pd = ctx->psrs[ctx->inst[k].psr].dev;
+                const int ntr = (pd.red0c + 1 + pd.vns) / 16, ntc = pd.vkp / 16;
+                const int nsk = ntr - (pd.red0c + 1 + 15) / 16;
+                int t = 1 + (pd.vb ? 1 : 0);
+                for (int ti = 0; ti < ntr; ti++)
+                    for (int tj = ti; tj < ntc; tj++)
+                        if (!(ti >= ntr - nsk && (tj < ntr || pd.vb))) t++;
+                return (long)t * ctx->inst[k].n;
+            };
+            std::vector<long> ck(ninst, 0);
+            for (auto& b : bucket) {
+                for (int k : b) ck[k] = cost(k);
+                std::stable_sort(b.begin(), b.end(), [&](int x, int y) { return ck[x] > ck[y]; });
+            }
+        }
         for (int T = 1; T <= maxT; T++) {
             if (bucket[T].empty()) continue;
             KpGroup g{T, (int)sorted.size(), (int)bucket[T].size(), bkp[T]};
@@ -3639,6 +3806,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         }
     }
     HIPCHK(cmalloc((void**)&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
+    HIPCHK(cmalloc((void**)&ctx->d_BFp, sizeof(double) * std::max<long>(1, vboff)));
     HIPCHK(cmalloc((void**)&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_blk_inst, sizeof(int) * bi.size()));
@@ -3942,12 +4110,19 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipEvent_t e0 = (ext_t && gi == 0) ? ctx->ev[12] : nullptr;
             hipEvent_t e1 = (ext_t && gi + 1 == ctx->kp_groups_v.size()) ? ctx->ev[13] : nullptr;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * std::max<size_t>((size_t)GVB * (kg.maxKp + 33) * (VCH + 2),
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)GVB * (kg.maxKp + (ctx->vb_on && kg.maxKp <= 96 ? 49 : 33)) * (VCH + 2),
                                                                  std::max(GW * VTG * 256, GW * 256 + 256));
 #define PINT_GRAMV(R_, C_)                                                                                       \
-            hipExtLaunchKernelGGL((k_gram_v<R_, C_>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, 0u,  \
-                                  (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M, (const double*)ctx->d_rt, \
-                                  (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G, ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->gvdbg)
+            if (ctx->vb_on && C_ <= 6)                                                                               \
+                hipExtLaunchKernelGGL((k_gram_v<R_, C_, true>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, \
+                                      0u, (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M,                    \
+                                      (const double*)ctx->d_rt, (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G,     \
+                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg);                   \
+            else                                                                                                     \
+                hipExtLaunchKernelGGL((k_gram_v<R_, C_, false>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, \
+                                      0u, (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M,                    \
+                                      (const double*)ctx->d_rt, (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G,     \
+                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg)
             switch (kg.T) {
                 case 1: PINT_GRAMV(1, 1); break;
                 case 2: PINT_GRAMV(1, 2); break;
@@ -3990,7 +4165,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         record(ctx, 14);
         hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? ctx->max_ndc : 0), ctx->ninst), dim3(256), 0, ctx->stream,
                            ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
-                           ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+                           ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_BFp, ctx->vb_on);
         HIPCHK(hipGetLastError());
         record(ctx, 15);
     }
@@ -4229,6 +4404,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (!ctx) return PINT_E_INVALID;
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_VBIN) { ctx->vbin = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {

@@ -548,7 +548,8 @@ class Session:
         return tuple(int(x) for x in out)
 
     def vgram_layout(self, lay):
-        """(on the vg path, DMX slots, k_gram_v LDS width, compact timing columns)."""
+        """(on the vg path (bit 1: with the binned DMX x F tile), DMX slots, k_gram_v LDS
+        width, compact timing columns)."""
         out = np.zeros(4, dtype=np.int32)
         self._check(self.L.pint_vgram_layout(self.ctx, lay.psr_id, L.ptr(out, C.c_int32)))
         return tuple(int(x) for x in out)
@@ -567,6 +568,10 @@ class Session:
     def set_vgram(self, on=True):
         """Generated-Fourier compact fit path (k_gram_v); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 2, 1 if on else 0))
+
+    def set_vbin(self, on=True):
+        """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
+        self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))
 
     def n_vgram(self):
         """Instances of the current batch on the generated-Fourier compact path."""

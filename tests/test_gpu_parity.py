@@ -410,11 +410,12 @@ def test_compact_dmx_layout_matches_full(name):
     assert abs(g1 / g2 - 1) < 1e-10
 
 
-def _fit_once_paths(items, vgram):
+def _fit_once_paths(items, vgram, vbin=True):
     from pint_amd.engine import Session
     from pint_amd.fitter import BatchFit
     s = Session()
     s.set_vgram(vgram)
+    s.set_vbin(vbin)
     bf = BatchFit([(copy.deepcopy(m), t) for m, t in items], mode="gls", session=s)
     nvg = s.n_vgram()
     s.eval(want_M=Session.FIT)
@@ -460,6 +461,29 @@ def test_generated_fourier_path_full_size():
     assert (n1, n0) == (3, 0)
     for x, y in zip(a, b):
         _assert_same_fit(x, y)
+
+
+def test_binned_dmx_fourier_tile_matches_slot_tiles():
+    """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN, one trig tile per k-step whose
+    accumulator holds an even and an odd bin, flushed per bin and wave) against the DMX-slot
+    row tiles x Fourier columns on bench-shaped pulsars (isolated and ELL1 take VB; DD, with
+    no all-slot row tile, keeps the slot tiles): the same normal equations to rounding, and
+    the VB flag as the layout reports it."""
+    from pint_amd import simulation as sim
+    from pint_amd.engine import Session, build_layout
+    items = sim.make_pta(npsr=6, ntoas=10000)
+    s = Session()
+    lays = [s.add(build_layout(m, t)) for m, t in items]
+    from pint_amd.engine import pack_table
+    s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+    flags = [s.vgram_layout(l)[0] for l in lays]
+    s.close()
+    assert all(f & 1 for f in flags) and any(f & 2 for f in flags), flags
+    n1, a = _fit_once_paths(items, True, vbin=True)
+    n0, b = _fit_once_paths(items, True, vbin=False)
+    assert n1 == n0 == len(items)
+    for x, y in zip(a, b):
+        _assert_same_fit(x, y, tol_step=1e-9, tol_err=1e-11, tol_chi2=1e-12)
 
 
 def test_graph_replay_matches_direct():
