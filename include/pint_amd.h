@@ -64,7 +64,8 @@ typedef struct {
 enum {
     PINT_COL_OFFSET = 0, PINT_COL_F = 1, PINT_COL_LON = 2, PINT_COL_LAT = 3,
     PINT_COL_PMLON = 4, PINT_COL_PMLAT = 5, PINT_COL_PX = 6, PINT_COL_DM = 7,
-    PINT_COL_DMX = 8, PINT_COL_FD = 9, PINT_COL_JUMP = 10, PINT_COL_BIN = 11
+    PINT_COL_DMX = 8, PINT_COL_FD = 9, PINT_COL_JUMP = 10, PINT_COL_BIN = 11,
+    PINT_COL_ZERO = 12      /* a parameter without a delay (DMJUMP, dispersion_model.py:797) */
 };
 /* binary parameter ids (stand_alone_psr_binaries/binary_generic.py, ELL1_model.py, DD_model.py,
  * ELL1H_model.py (H3, H4, STIGMA), DDK_model.py (KIN, KOM)) */
@@ -111,6 +112,9 @@ typedef struct {
                                (noise_model.py:443-540 PLDMNoise.get_noise_basis)           */
     int32_t k96;            /* DDK: 1 = Kopeikin (1996) proper-motion terms on a1, omega and i
                                (K96, the reference default; DDK_model.py:157-349), 0 = off */
+    int32_t o_DMJUMP;       /* DispersionJump: table slot of the first DMJUMP (-1 none); they
+                               offset the modelled DM values only (dispersion_model.py:724-795) */
+    int32_t ndmjump;        /* DMJUMPs (<= 64; bit k of the per-TOA DMJUMP mask selects DMJUMP k+1) */
     double obliquity;       /* rad, ecliptic models (pulsar_ecliptic.py OBL[ECL])       */
     double red_f0;          /* red-noise fundamental 1/T (Hz), noise_model.py:847       */
     double red_t0;          /* unused reserve                                           */
@@ -199,6 +203,21 @@ int pint_fit_layout(pint_ctx *ctx, int psr, int32_t *out4);
  * binned DMX x Fourier tile, PINT_OPT_VBIN), DMX slots, LDS width [T | r | slots | F]
  * padded to 16, timing columns of the compact layout). */
 int pint_vgram_layout(pint_ctx *ctx, int psr, int32_t *out4);
+/* Wideband DM data of pulsar `psr` (n TOAs): the measured DMs pp_dm and their errors pp_dme
+ * (the -pp_dm / -pp_dme TOA flags, toa.py:1767-1791), the errors scaled by DMEFAC/DMEQUAD
+ * (ScaleDmError.scale_dm_sigma, noise_model.py:291), and each TOA's DMJUMP mask (bit k:
+ * DMJUMP k+1 selects it).  All in pc/cm^3.  Replaces WidebandDMResiduals.get_dm_data
+ * (residuals.py:1044-1071). */
+int pint_set_wideband(pint_ctx *ctx, int psr, const double *pp_dm, const double *pp_dme,
+                      const double *dm_sigma, const uint64_t *dmjump_mask);
+/* WidebandDMResiduals.calc_resids / calc_chi2 (residuals.py:1000-1031) of every instance
+ * whose pulsar has wideband data: pp_dm - total_dm (DispersionDM Taylor series + DMX +
+ * DMJUMP, timing_model.py:1593) at the instance's parameters, the mean (weighted by
+ * 1/pp_dme^2 unless use_weighted_mean = 0) removed if subtract_mean; chi2 with the scaled
+ * errors.  resid_out: the instances' TOA rows concatenated (n per instance, 0 for pulsars
+ * without wideband data), chi2_out[ninst] (NaN without wideband data). */
+int pint_dm_resids(pint_ctx *ctx, int subtract_mean, int use_weighted_mean, double *resid_out,
+                   double *chi2_out);
 
 /* Lazy mode (1): launches return without synchronising or checking the device status;
  * pint_check() synchronises and returns the accumulated status.  In lazy mode

@@ -173,6 +173,8 @@ def toas_from_fixture(z: dict, meta: dict) -> dict:
         d["obs"] = [meta["obs_names"][i] for i in np.asarray(z["obs_index"])]
         d["obs_alias"] = {k: [a.lower() for a in v] for k, v in meta.get("obs_aliases", {}).items()}
     d["tzr"] = {k[4:]: np.asarray(z[k]) for k in z if k.startswith("tzr_")}
+    if "wb_pp_dm" in z:  # wideband DM measurements (-pp_dm / -pp_dme flags)
+        d["pp_dm"], d["pp_dme"] = np.asarray(z["wb_pp_dm"]), np.asarray(z["wb_pp_dme"])
     return d
 
 
@@ -1169,6 +1171,74 @@ def chi2_gls(om, toas, r, sigma_us):
     Sigma = np.diag(1 / phi) + (U.T / N) @ U
     cf = scipy.linalg.cho_factor(Sigma)
     return float(xNy - xNU @ scipy.linalg.cho_solve(cf, xNU))
+
+
+# ----------------------------------------------------------------------------------
+# wideband DM residuals (residuals.py:908-1071, :1146-1271)
+# ----------------------------------------------------------------------------------
+def total_dm(om: OModel, toas: dict) -> np.ndarray:
+    """TimingModel.total_dm (timing_model.py:1593): DispersionDM.base_dm (Taylor series in
+    years from DMEPOCH, dispersion_model.py:217-234) + DispersionDMX.dmx_dm (:659-678) +
+    DispersionJump.jump_dm (-DMJUMP on the selected TOAs, :773-785); pc/cm^3."""
+    n = len(toas["tdb_hi"])
+    tdb = np.asarray(toas["tdb_hi"], dtype=LD) + np.asarray(toas["tdb_lo"], dtype=LD)
+    out = np.zeros(n)
+    dm_terms = ["DM"] + om.prefix(r"^DM(\d+)$") if om.has("DM") else []
+    if dm_terms:
+        if any(LD(om.v(t)) != 0 for t in dm_terms[1:]):
+            x = ((tdb - LD(om.v("DMEPOCH", 0.0))) / LD(DJY)).astype(float)
+        else:
+            x = np.zeros(n)
+        dm = np.zeros(n)
+        fact = len(dm_terms)
+        for t in dm_terms[::-1]:  # utils.py:449 taylor_horner
+            dm = dm * x / fact + float(om.v(t))
+            fact -= 1
+        out = out + dm
+    for name, sel in _dmx_bins(om, np.asarray(toas["mjd_float"], dtype=float)):
+        out = out + np.where(sel, float(om.v(name)), 0.0)
+    for name in sorted((k for k in om.masks if re.match(r"^DMJUMP\d+$", k)), key=lambda x: int(x[6:])):
+        out = out + np.where(select_mask(toas, *om.masks[name]), -float(om.v(name)), 0.0)
+    return out
+
+
+def scaled_dm_sigma(om: OModel, toas: dict) -> np.ndarray:
+    """ScaleDmError.scale_dm_sigma (noise_model.py:291-315): DMEQUADs (hypot), then DMEFACs."""
+    s = np.array(toas["pp_dme"], dtype=float)
+    for n in sorted((k for k in om.masks if re.match(r"^DMEQUAD\d+$", k)), key=lambda x: int(x[7:])):
+        sel = select_mask(toas, *om.masks[n])
+        s[sel] = np.hypot(s[sel], float(om.v(n)))
+    for n in sorted((k for k in om.masks if re.match(r"^DMEFAC\d+$", k)), key=lambda x: int(x[6:])):
+        sel = select_mask(toas, *om.masks[n])
+        s[sel] *= float(om.v(n))
+    return s
+
+
+def dm_residuals(om: OModel, toas: dict, subtract_mean=False, use_weighted_mean=True):
+    """WidebandDMResiduals.calc_resids / calc_chi2 (residuals.py:1000-1031): pp_dm - total_dm,
+    the mean (weighted by the unscaled DM errors) removed only with subtract_mean; chi2 with
+    the scaled errors."""
+    r = np.asarray(toas["pp_dm"], dtype=float) - total_dm(om, toas)
+    if subtract_mean:
+        if use_weighted_mean:
+            w = 1.0 / np.asarray(toas["pp_dme"], dtype=float) ** 2
+            r = r - np.sum(r * w) / np.sum(w)
+        else:
+            r = r - r.mean()
+    sig = scaled_dm_sigma(om, toas)
+    return {"resids": r, "sigma": sig, "chi2": float(np.sum((r / sig) ** 2))}
+
+
+def wideband_chi2(om: OModel, toas: dict) -> float:
+    """WidebandTOAResiduals.calc_chi2 (residuals.py:1206-1246): a WidebandTOAFitter pass with
+    no free parameters, i.e. GLS over [TOA rows; DM rows] with the Offset column (zero on the
+    DM rows) and the TOA noise basis: the TOA residuals' GLS (offset-marginalised) chi2 plus
+    the DM rows' white chi2."""
+    rr = residuals(om, toas)
+    c2 = chi2_gls(om, toas, rr["time"], rr["sigma_us"]) if noise_basis(om, toas)[0] is not None else \
+        chi2_wls(rr["time"] - np.sum(rr["time"] / rr["sigma_us"] ** 2) / np.sum(1 / rr["sigma_us"] ** 2),
+                 rr["sigma_us"])
+    return c2 + dm_residuals(om, toas)["chi2"]
 
 
 def lognorm(om, toas, r, sigma_us, gls=True):

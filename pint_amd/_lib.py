@@ -18,7 +18,7 @@ EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
 B_NPAR = 27
 BIN_NONE, BIN_ELL1, BIN_DD, BIN_ELL1H, BIN_BT, BIN_DDK = range(6)
 
-COL_OFFSET, COL_F, COL_LON, COL_LAT, COL_PMLON, COL_PMLAT, COL_PX, COL_DM, COL_DMX, COL_FD, COL_JUMP, COL_BIN = range(12)
+COL_OFFSET, COL_F, COL_LON, COL_LAT, COL_PMLON, COL_PMLAT, COL_PX, COL_DM, COL_DMX, COL_FD, COL_JUMP, COL_BIN, COL_ZERO = range(13)
 
 PINT_OK, PINT_E_INVALID, PINT_E_HIP, PINT_E_NOT_PD, PINT_E_KEPLER, PINT_E_PARAM, PINT_E_SIGMA = range(7)
 
@@ -37,7 +37,7 @@ class SpecT(C.Structure):
                                           "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
                                           "o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px",
                                           "o_POSEPOCH", "o_DM", "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP")] + [
-        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("dmn0", C.c_int32), ("k96", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
+        ("o_bin", C.c_int32 * B_NPAR), ("o_PHOFF", C.c_int32), ("wb_noones", C.c_int32), ("ell1h", C.c_int32), ("nharms", C.c_int32), ("dmn0", C.c_int32), ("k96", C.c_int32), ("o_DMJUMP", C.c_int32), ("ndmjump", C.c_int32), ("obliquity", C.c_double), ("red_f0", C.c_double), ("red_t0", C.c_double),
         ("col_kind", C.c_int32 * MAX_COLS), ("col_index", C.c_int32 * MAX_COLS), ("col_toff", C.c_int32 * MAX_COLS)]
 
 
@@ -107,6 +107,8 @@ def lib():
     L.pint_set_noise_classes.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dptr]
     L.pint_noise_lnlike.argtypes = [vp, C.POINTER(C.c_int32), dptr, dptr, dptr, dptr, dptr]
     _lib = L
+    L.pint_set_wideband.argtypes = [vp, C.c_int, dptr, dptr, dptr, C.POINTER(C.c_uint64)]
+    L.pint_dm_resids.argtypes = [vp, C.c_int, C.c_int, dptr, dptr]
     return L
 
 
@@ -119,7 +121,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step",
             "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
-            "pint_noise_lnlike", "pint_noise_resids_dm"]
+            "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -49,6 +49,10 @@ struct PsrDev {
     // the set of EFAC/EQUAD masks selecting them, CSR; raw TOA errors (us)
     const int32_t *cls_ptr, *cls_idx, *toa_cls;
     const double* sigma0;
+    // wideband DM data (pint_set_wideband): measured DMs, raw and scaled errors, DMJUMP masks
+    const double *pp_dm, *pp_dme, *dm_sig;
+    const uint64_t* dmjmask;
+    int wb;
     int ncls;
     int ep_overlap;          // some TOA lies in two ECORR epochs (no per-epoch Sherman-Morrison)
     const ColRun* runs;      // design-matrix column runs
@@ -1281,6 +1285,75 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
     const int nsk = __builtin_amdgcn_readfirstlane(NTR - (Pd.red0c + 1 + 15) / 16);
     if constexpr (!VB || NTC <= 6)
         gram_v_nsk<NTR, NTC, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, nsk);
+}
+
+// k_dm_resid: WidebandDMResiduals (residuals.py:1000-1031) of an instance, one workgroup per
+// instance: the modelled DM (timing_model.py:1593 total_dm: DispersionDM.base_dm, a Taylor
+// series in Julian years from DMEPOCH, dispersion_model.py:217-234; DispersionDMX.dmx_dm
+// :659-678; DispersionJump.jump_dm, -DMJUMP on its TOAs :773-785) at the instance's
+// parameters, r = pp_dm - DM; the mean (weights 1/pp_dme^2, unscaled) removed if asked; chi2
+// with the scaled errors.  Sums in a fixed order (deterministic).  Bandwidth: ~48 B/TOA.
+constexpr int DMR_T = 256;
+__global__ __launch_bounds__(DMR_T) void k_dm_resid(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ tables, int subtract_mean,
+                                                    int use_weighted_mean, double* __restrict__ rout,
+                                                    double* __restrict__ chi2) {
+    __shared__ double sh[DMR_T / 64];
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const int n = I.n;
+    double* r = rout + I.ooff;
+    if (!Pd.wb) {
+        for (int i = threadIdx.x; i < n; i += DMR_T) r[i] = 0.0;
+        if (threadIdx.x == 0) chi2[blockIdx.x] = __builtin_nan("");
+        return;
+    }
+    const pint_spec_t& S = *Pd.spec;
+    const double* P = tables + I.toff;
+    bool any = false;
+    for (int k = 1; k < S.ndm; k++) any |= (pval(P, S.o_DM + 2 * k) != 0.0);
+    const dd ep = S.o_DMEPOCH >= 0 ? pdd(P, S.o_DMEPOCH) : dd_make(0.0);
+    double swr = 0.0, sw = 0.0;
+    for (int i = threadIdx.x; i < n; i += DMR_T) {
+        double dm = 0.0;
+        if (S.ndm > 0) {  // base_dm: Horner in dt (yr), 0 when only DM is nonzero
+            const double x = any ? dd_to_d(dd_sub(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), ep)) * INV_DJY : 0.0;
+            dm = pval(P, S.o_DM + 2 * (S.ndm - 1));
+            for (int k = S.ndm - 1; k >= 1; k--) dm = dm * x * inv_int(k) + pval(P, S.o_DM + 2 * (k - 1));
+        }
+        if (S.ndmx > 0) {
+            const int a = Pd.dmx_a[i], b = Pd.dmx_b[i];
+            if (a >= 0) dm += pval(P, S.o_DMX + 2 * a);
+            if (b >= 0) dm += pval(P, S.o_DMX + 2 * b);
+        }
+        if (S.ndmjump > 0) {
+            const uint64_t m = Pd.dmjmask[i];
+            for (int k = 0; k < S.ndmjump; k++)
+                if ((m >> k) & 1ull) dm -= pval(P, S.o_DMJUMP + 2 * k);
+        }
+        const double v = Pd.pp_dm[i] - dm;
+        r[i] = v;
+        if (subtract_mean) {
+            const double w = use_weighted_mean ? 1.0 / (Pd.pp_dme[i] * Pd.pp_dme[i]) : 1.0;
+            swr += w * v;
+            sw += w;
+        }
+    }
+    double mean = 0.0;
+    if (subtract_mean) {
+        swr = block_sum<DMR_T / 64>(swr, sh);
+        sw = block_sum<DMR_T / 64>(sw, sh);
+        mean = swr / sw;
+    }
+    double c2 = 0.0;
+    for (int i = threadIdx.x; i < n; i += DMR_T) {  // each thread rereads its own rows
+        const double v = r[i] - mean;
+        r[i] = v;
+        const double z = v / Pd.dm_sig[i];
+        c2 += z * z;
+    }
+    c2 = block_sum<DMR_T / 64>(c2, sh);
+    if (threadIdx.x == 0) chi2[blockIdx.x] = c2;
 }
 
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
@@ -3086,6 +3159,8 @@ struct pint_ctx {
     int m_compact = 0;  // layout of the design matrix written by the last pint_eval(want_M)
     int red_valid[2] = {0, 0};  // red-noise columns of M already written (full, compact layout)
     size_t wpart_cap = 0;
+    double *d_dmr = nullptr, *d_dmc2 = nullptr;  // wideband DM residuals / chi2 (pint_dm_resids)
+    long dmr_cap = 0, dmc2_cap = 0;
     long tot_e = 0, tot_ep = 0;
     int max_nep = 0;
     int* d_status = nullptr;
@@ -3314,6 +3389,8 @@ void pint_ctx_destroy(pint_ctx* ctx) {
         for (auto b : p.bufs) hipFree(b);
     }
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
+    if (ctx->d_dmr) hipFree(ctx->d_dmr);
+    if (ctx->d_dmc2) hipFree(ctx->d_dmc2);
     if (ctx->d_nz) hipFree(ctx->d_nz);
     if (ctx->d_status_slots) hipFree(ctx->d_status_slots);
     if (ctx->h_status) hipHostFree(ctx->h_status);
@@ -3346,6 +3423,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     int Kp = (K + 1 + 15) / 16 * 16;
     if (Kp > GMAXKP) { ctx->err = "design matrix too wide for k_gram (K+1 > 256)"; return -PINT_E_INVALID; }
     if (spec->njump > PINT_MAX_JUMP) { ctx->err = "too many JUMPs"; return -PINT_E_INVALID; }
+    if (spec->ndmjump < 0 || spec->ndmjump > 64) { ctx->err = "too many DMJUMPs"; return -PINT_E_INVALID; }
     if (spec->binary < 0 || spec->binary > PINT_BIN_DDK) { ctx->err = "unsupported binary model"; return -PINT_E_INVALID; }
     if (spec->binary == PINT_BIN_ELL1H &&
         (spec->ell1h < 1 || spec->ell1h > 3 || (spec->ell1h == 2 && (spec->nharms < 3 || spec->nharms > 64)))) {
@@ -4010,6 +4088,51 @@ int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, dou
     if (time_resid) HIPCHK(hipMemcpyAsync(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (phase_resid) HIPCHK(hipMemcpyAsync(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (chi2) HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_set_wideband(pint_ctx* ctx, int psr, const double* pp_dm, const double* pp_dme, const double* dm_sigma,
+                      const uint64_t* dmjump_mask) {
+    if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !pp_dm || !pp_dme || !dm_sigma) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    PsrHost& ph = ctx->psrs[psr];
+    if (ph.spec.ndmjump > 0 && !dmjump_mask) { ctx->err = "DMJUMPs without masks"; return PINT_E_INVALID; }
+    for (int i = 0; i < ph.n; i++)
+        if (!(dm_sigma[i] > 0.0) || !(pp_dme[i] > 0.0)) {
+            ctx->err = "Some DM errors are zero - cannot calculate the weighted residuals.";
+            return PINT_E_INVALID;
+        }
+    int rc = 0;
+    rc |= upload(ctx, ph, pp_dm, (size_t)ph.n, ph.dev.pp_dm);
+    rc |= upload(ctx, ph, pp_dme, (size_t)ph.n, ph.dev.pp_dme);
+    rc |= upload(ctx, ph, dm_sigma, (size_t)ph.n, ph.dev.dm_sig);
+    if (ph.spec.ndmjump > 0) rc |= upload(ctx, ph, dmjump_mask, (size_t)ph.n, ph.dev.dmjmask);
+    if (rc) return PINT_E_HIP;
+    ph.dev.wb = 1;
+    return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
+}
+
+int pint_dm_resids(pint_ctx* ctx, int subtract_mean, int use_weighted_mean, double* resid_out, double* chi2_out) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    if (ctx->tot_out > ctx->dmr_cap) {
+        if (ctx->d_dmr) hipFree(ctx->d_dmr);
+        ctx->d_dmr = nullptr;
+        HIPCHK(hipMalloc((void**)&ctx->d_dmr, sizeof(double) * std::max<long>(1, ctx->tot_out)));
+        ctx->dmr_cap = ctx->tot_out;
+    }
+    if (ctx->ninst > ctx->dmc2_cap) {
+        if (ctx->d_dmc2) hipFree(ctx->d_dmc2);
+        ctx->d_dmc2 = nullptr;
+        HIPCHK(hipMalloc((void**)&ctx->d_dmc2, sizeof(double) * ctx->ninst));
+        ctx->dmc2_cap = ctx->ninst;
+    }
+    hipLaunchKernelGGL(k_dm_resid, dim3(ctx->ninst), dim3(DMR_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                       ctx->d_tables, subtract_mean, use_weighted_mean, ctx->d_dmr, ctx->d_dmc2);
+    HIPCHK(hipGetLastError());
+    if (resid_out) HIPCHK(hipMemcpyAsync(resid_out, ctx->d_dmr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
+    if (chi2_out) HIPCHK(hipMemcpyAsync(chi2_out, ctx->d_dmc2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }

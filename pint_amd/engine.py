@@ -83,7 +83,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         return offs[name]
 
     for s in ("o_F", "o_PEPOCH", "o_lon", "o_lat", "o_pmlon", "o_pmlat", "o_px", "o_POSEPOCH", "o_DM",
-              "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP", "o_PHOFF"):
+              "o_DMEPOCH", "o_DMX", "o_FD", "o_JUMP", "o_PHOFF", "o_DMJUMP"):
         setattr(spec, s, -1)
     for i in range(L.B_NPAR):
         spec.o_bin[i] = -1
@@ -172,7 +172,17 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
     # ---- columns: Offset (unless a PhaseOffset is present, timing_model.py:2145) + free
     # params in params order (timing_model.py:2141-2173)
     cols, kinds, idxs, toffs = ([], [], [], []) if has_phoff else (["Offset"], [L.COL_OFFSET], [0], [-1])
-    noise_like = {"EFAC", "EQUAD", "ECORR", "TNEQ"}
+    dmjumps = model.mask_params("DMJUMP")
+    spec.ndmjump = len(dmjumps)
+    if len(dmjumps) > 64:
+        raise NotImplementedError("more than 64 DMJUMPs")
+    if dmjumps:
+        spec.o_DMJUMP = pos
+        for n in dmjumps:
+            place(n)
+        tstride = pos
+        spec.tstride = tstride
+    noise_like = {"EFAC", "EQUAD", "ECORR", "TNEQ", "DMEFAC", "DMEQUAD"}
     for n in model.free_params:
         p = model[n]
         base = "".join(ch for ch in n if not ch.isdigit())
@@ -202,6 +212,8 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
             k, i = L.COL_FD, fds.index(n)
         elif n in jumps:
             k, i = L.COL_JUMP, jumps.index(n)
+        elif n in dmjumps:  # DMJUMPs leave the delay alone: a zero column (dispersion_model.py:797)
+            k, i = L.COL_ZERO, dmjumps.index(n)
         elif model.binary and n in BIN_IDS and n in offs:
             k, i = L.COL_BIN, BIN_IDS[n]
         else:
@@ -516,6 +528,39 @@ class Session:
         c2 = np.empty(len(n))
         self._check(self.L.pint_read_resids(self.ctx, L.ptr(tr), L.ptr(pr), L.ptr(c2)))
         return self._split(tr, n), self._split(pr, n), c2
+
+    def set_wideband(self, lay):
+        """Upload a pulsar's wideband DM data (pint_set_wideband): -pp_dm / -pp_dme, the errors
+        scaled by DMEFAC/DMEQUAD (host preparation, noise_model.py:291) and the DMJUMP masks
+        (bit k: the k-th DMJUMP, the layout's table order)."""
+        from .noise import scaled_dm_sigma
+        model, toas = lay.model, lay.toas
+        try:
+            dm, dme = toas.get_dms(), toas.get_dm_errors()
+        except AttributeError:
+            raise ValueError("Input TOA object does not have wideband DM values")
+        if len(dm) != lay.n or len(dme) != lay.n:
+            raise ValueError("Input TOA object' DM data and DM errors do not match.")
+        sig = scaled_dm_sigma(model, toas)
+        jm = np.zeros(lay.n, dtype=np.uint64)
+        for k, name in enumerate(model.mask_params("DMJUMP")):
+            p = model[name]
+            jm[toas.select_mask(p.key, p.key_value)] |= np.uint64(1) << np.uint64(k)
+        dm, dme = np.ascontiguousarray(dm, dtype=np.float64), np.ascontiguousarray(dme, dtype=np.float64)
+        self._check(self.L.pint_set_wideband(self.ctx, lay.psr_id, L.ptr(dm), L.ptr(dme), L.ptr(sig),
+                                             L.ptr(jm, C.c_uint64)))
+        lay.keep += [dm, dme, sig, jm]
+        lay.dm_data, lay.dm_error, lay.dm_sigma = dm, dme, sig
+
+    def dm_resids(self, subtract_mean=False, use_weighted_mean=True):
+        """WidebandDMResiduals of every instance (pint_dm_resids): (residual rows per
+        instance, chi2 per instance), pc/cm^3."""
+        n = [l.n for l in self.inst_layout]
+        r = np.empty(sum(n))
+        c2 = np.empty(len(n))
+        self._check(self.L.pint_dm_resids(self.ctx, 1 if subtract_mean else 0, 1 if use_weighted_mean else 0,
+                                          L.ptr(r), L.ptr(c2)))
+        return self._split(r, n), c2
 
     def read_chi2(self):
         """WLS chi2 per instance only (no residual rows copied back)."""

@@ -27,6 +27,25 @@ def scaled_sigma_us(model, toas) -> np.ndarray:
     return sigma
 
 
+def scaled_dm_sigma(model, toas) -> np.ndarray:
+    """ScaleDmError.scale_dm_sigma (noise_model.py:291-315): DMEQUADs in quadrature, then
+    DMEFACs, on the -pp_dme errors (pc/cm^3); host preparation at upload like the TOA errors."""
+    sigma = np.array(toas.get_dm_errors(), dtype=np.float64, copy=True)
+    for name in model.mask_params("DMEQUAD"):
+        p = model[name]
+        if p.value is None:
+            continue
+        idx = toas.select_mask(p.key, p.key_value)
+        if len(idx):
+            sigma[idx] = np.hypot(sigma[idx], float(p.value))
+    for name in model.mask_params("DMEFAC"):
+        p = model[name]
+        idx = toas.select_mask(p.key, p.key_value)
+        if len(idx):
+            sigma[idx] *= float(p.value)
+    return sigma
+
+
 def red_noise_freqs_weights(model, toas):
     """(f_k [nmodes], phi [2 nmodes]) — get_rednoise_freqs (noise_model.py:847) with
     T = max(t) - min(t) of t = tdbld*86400 in longdouble, powerlaw(f) * f[0] (:780-789).

@@ -220,7 +220,11 @@ _PREFIX = {  # prefix params: regex -> (component, units template, long_double)
 
 MASK_PARAMS = {"JUMP": ("PhaseJump", "s"), "EFAC": ("ScaleToaError", ""),
                "EQUAD": ("ScaleToaError", "us"), "TNEQ": ("ScaleToaError", "log10(s)"),
-               "ECORR": ("EcorrNoise", "us")}
+               "ECORR": ("EcorrNoise", "us"),
+               # wideband DM data (dispersion_model.py:724 DispersionJump; noise_model.py:228
+               # ScaleDmError): DM offsets and DM-error scaling, pc/cm^3
+               "DMJUMP": ("DispersionJump", "pc / cm3"), "DMEFAC": ("ScaleDmError", ""),
+               "DMEQUAD": ("ScaleDmError", "pc / cm3")}
 
 IGNORED = {"MODE", "NITS", "DMRES", "IBOOT", "RM", "SWP", "DMXEP", "DMXF1", "DMXF2"}
 

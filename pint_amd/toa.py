@@ -79,6 +79,29 @@ class TOAs:
             return [fill_value] * self.ntoas, []
         return [c if c != "" else fill_value for c in col], [i for i, c in enumerate(col) if c != ""]
 
+    def is_wideband(self) -> bool:
+        """toa.py:1656: every TOA carries a -pp_dm measurement."""
+        col = self.flag_columns.get("pp_dm")
+        return col is not None and all(c != "" for c in col)
+
+    @property
+    def wideband(self) -> bool:
+        return self.is_wideband()
+
+    def get_dms(self) -> np.ndarray:
+        """The wideband DM measurements, pc/cm^3 (toa.py:1767, the -pp_dm flags)."""
+        v, valid = self.get_flag_value("pp_dm")
+        if valid == []:
+            raise AttributeError("No DM is provided.")
+        return np.array([float(v[i]) for i in valid])
+
+    def get_dm_errors(self) -> np.ndarray:
+        """Their uncertainties, pc/cm^3 (toa.py:1780, the -pp_dme flags)."""
+        v, valid = self.get_flag_value("pp_dme")
+        if valid == []:
+            raise AttributeError("No DM error is provided.")
+        return np.array([float(v[i]) for i in valid])
+
     def get_Tspan(self) -> float:
         m = self.get_mjds()
         return float(m.max() - m.min())

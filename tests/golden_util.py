@@ -10,7 +10,8 @@ PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "
         "wls_phoff": "wls_phoff.par", "ecorr_phoff": "ecorr_phoff.par", "wls_noise": "wls_noise.par",
         "ecorr_fit": "ecorr_fit.par", "white_mjd": "white_mjd.par", "ell1h_h3": "ell1h_h3.par",
         "ell1h_h4": "ell1h_h4.par", "ell1h_stig": "ell1h_stig.par", "pta_bt": "pta_bt.par",
-        "pta_dmn": "pta_dmn.par", "pta_ddk": "pta_ddk.par", "pta_ddk_nk": "pta_ddk_nk.par"}
+        "pta_dmn": "pta_dmn.par", "pta_ddk": "pta_ddk.par", "pta_ddk_nk": "pta_ddk_nk.par",
+        "wb_dd": "wb_dd.par"}
 
 
 def load(name):
@@ -18,7 +19,11 @@ def load(name):
     from pint_amd.toa import from_arrays_with_tzr
     z = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
     meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
-    toas = from_arrays_with_tzr(z, meta["flag_columns"], name, meta.get("obs_names"))
+    fc = dict(meta["flag_columns"])
+    if "wb_pp_dm" in z:  # the wideband -pp_dm / -pp_dme flags, as the tim file carries them
+        fc["pp_dm"] = [repr(float(x)) for x in z["wb_pp_dm"]]
+        fc["pp_dme"] = [repr(float(x)) for x in z["wb_pp_dme"]]
+    toas = from_arrays_with_tzr(z, fc, name, meta.get("obs_names"))
     model = get_model(os.path.join(GOLDEN, PARS[name]))
     free = [p for p in meta["model"]["free_params"]]
     model.free_params = [p for p in free if p in model]

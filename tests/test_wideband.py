@@ -1,0 +1,80 @@
+"""Wideband DM residuals (residuals.py:908-1271): the CPU oracle pinned to the reference's
+fixture (wb_dd: DD + red noise, DMX, DMJUMP, DMEFAC, DMEQUAD on MJD ranges, make_fake_toas
+wideband DMs; oracle/refgen/gen_wideband.py), and the HIP path (k_dm_resid through the
+C-ABI) against both."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN
+
+import pint_oracle as O
+
+
+def _fixture():
+    z = dict(np.load(os.path.join(GOLDEN, "wb_dd.npz"), allow_pickle=False))
+    meta = json.load(open(os.path.join(GOLDEN, "wb_dd.json")))
+    return O.from_fixture(meta), O.toas_from_fixture(z, meta), z, meta
+
+
+def test_oracle_total_dm_and_resids():
+    om, toas, z, meta = _fixture()
+    assert np.max(np.abs(O.total_dm(om, toas) - z["wb_total_dm"])) < 1e-12
+    d = O.dm_residuals(om, toas)
+    assert np.max(np.abs(d["resids"] - z["wb_dm_resids"])) < 1e-12
+    assert np.max(np.abs(d["sigma"] / z["wb_dm_sigma"] - 1)) < 1e-15
+    assert abs(d["chi2"] / meta["wb_dm_chi2"] - 1) < 1e-12
+    dm = O.dm_residuals(om, toas, subtract_mean=True)
+    assert np.max(np.abs(dm["resids"] - z["wb_dm_resids_mean"])) < 1e-12
+
+
+def test_oracle_wideband_chi2():
+    """The combined chi2 of the reference's WidebandTOAFitter pass = the TOA residuals' GLS
+    chi2 + the DM chi2 (the TOA part at the end-to-end residual floor, 5e-6)."""
+    om, toas, z, meta = _fixture()
+    c2 = O.wideband_chi2(om, toas)
+    assert abs(c2 / meta["wb_chi2"] - 1) < 5e-6
+    assert abs(meta["wb_toa_chi2"] + meta["wb_dm_chi2_combined"] - meta["wb_chi2"]) < 1e-9 * meta["wb_chi2"]
+
+
+@pytest.mark.gpu
+def test_gpu_wideband_dm_resids():
+    """WidebandDMResiduals on the GPU (k_dm_resid) against the reference's resids, scaled
+    errors, chi2, dof and weighted RMS; with subtract_mean against the reference's too."""
+    from golden_util import load
+    from pint_amd import WidebandDMResiduals, Residuals
+    model, toas, z, meta = load("wb_dd")
+    r = Residuals(toas, model, residual_type="dm")
+    assert isinstance(r, WidebandDMResiduals)
+    assert np.max(np.abs(r.resids - z["wb_dm_resids"])) < 1e-12
+    assert np.max(np.abs(r.get_data_error() / z["wb_dm_sigma"] - 1)) < 1e-15
+    assert abs(r.chi2 / meta["wb_dm_chi2"] - 1) < 1e-12
+    assert r.dof == meta["wb_dm_dof"]
+    assert abs(r.rms_weighted() / meta["wb_dm_rms_weighted"] - 1) < 1e-10
+    rm = WidebandDMResiduals(toas, model, subtract_mean=True)
+    assert np.max(np.abs(rm.resids - z["wb_dm_resids_mean"])) < 1e-12
+
+
+@pytest.mark.gpu
+def test_gpu_wideband_toa_resids():
+    """WidebandTOAResiduals: the reference's combined chi2 (its WidebandTOAFitter pass), dof,
+    reduced chi2 and per-type weighted RMS; and the device's against the oracle's."""
+    from golden_util import load
+    from pint_amd import WidebandTOAResiduals
+    model, toas, z, meta = load("wb_dd")
+    w = WidebandTOAResiduals(toas, model)
+    assert abs(w.chi2 / meta["wb_chi2"] - 1) < 5e-6  # the TOA part at the end-to-end residual floor
+    assert abs(w.dm.chi2 / meta["wb_dm_chi2_combined"] - 1) < 1e-12
+    assert w.dof == meta["wb_dof"]
+    assert abs(w.reduced_chi2 / meta["wb_reduced_chi2"] - 1) < 5e-6
+    rw = w.rms_weighted()
+    assert abs(rw["toa"] / meta["wb_rms_weighted"]["toa_us"] - 1) < 1e-6
+    assert abs(rw["dm"] / meta["wb_rms_weighted"]["dm"] - 1) < 1e-10
+    om, ot, _, _ = _fixture()
+    assert abs(w.dm.chi2 / O.dm_residuals(om, ot)["chi2"] - 1) < 1e-12
+    # the TOA part: two independent dd / longdouble phase evaluations (~ps) -> ~1e-7
+    assert abs(w.chi2 / O.wideband_chi2(om, ot) - 1) < 5e-6
+    with pytest.raises(AttributeError):
+        w.dm.dof
