@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
 // each block running its own instantiation; the kernel carries the largest register set,
 // and saves the two launch tails of the per-model launches.
 template <int WANT_M>
-__global__ __launch_bounds__(256) void k_eval_mix(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+__device__ __forceinline__ void eval_mix_body(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                   const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
                                                   int off1, int off2, int off3,
                                                   const double* __restrict__ tables, const InstConst* __restrict__ ic,
@@ -319,6 +319,27 @@ __global__ __launch_bounds__(256) void k_eval_mix(const PsrDev* __restrict__ psr
     else
         eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
                               Mout, dmxv, compact, write_red, status, istatus, dfac);
+}
+#define PINT_EVAL_MIX_ARGS                                                                                      \
+    const PsrDev *__restrict__ psrs, const InstDev *__restrict__ insts, const int *__restrict__ blk_inst,        \
+        const int *__restrict__ blk_row0, int off1, int off2, int off3, const double *__restrict__ tables,      \
+        const InstConst *__restrict__ ic, double *__restrict__ ph_hi, double *__restrict__ ph_lo,               \
+        double *__restrict__ ftay, double *__restrict__ delay_out, double *__restrict__ Mout,                   \
+        double *__restrict__ dmxv, int compact, int write_red, int *__restrict__ status,                        \
+        int *__restrict__ istatus, double *__restrict__ dfac
+#define PINT_EVAL_MIX_PASS                                                                                      \
+    psrs, insts, blk_inst, blk_row0, off1, off2, off3, tables, ic, ph_hi, ph_lo, ftay, delay_out, Mout, dmxv,  \
+        compact, write_red, status, istatus, dfac
+template <int WANT_M>
+__global__ __launch_bounds__(256) void k_eval_mix(PINT_EVAL_MIX_ARGS) {
+    eval_mix_body<WANT_M>(PINT_EVAL_MIX_PASS);
+}
+// the same with the register budget of W resident waves per SIMD: the evaluation with the
+// design matrix is latency-bound (dependent FP64 / double-double chains, ~40 cycles each),
+// so a third wave per SIMD hides more than its 108 B of spills cost (PINT_EVAL_WPE)
+template <int WANT_M, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void k_eval_mix_w(PINT_EVAL_MIX_ARGS) {
+    eval_mix_body<WANT_M>(PINT_EVAL_MIX_PASS);
 }
 
 // ---------------------------------------------------------------------------------
@@ -3116,6 +3137,8 @@ struct pint_ctx {
     std::vector<KpGroup> kp_groups, kp_groups_c, kp_groups_v;
     int vgram = 1;       // PINT_OPT_VGRAM
     int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
+    int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
+                         // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
     int n_vg = 0;        // instances on the k_gram_v path
     bool any_dmx_rows = false;  // compact instances still on k_dmx_rows / k_dmx
     double *d_TSp = nullptr, *d_TS = nullptr;  // k_gram_v per-split trig sums, their totals
@@ -3336,6 +3359,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
     ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
+    ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int sl = 0; sl < 2; sl++) {
@@ -4029,7 +4053,17 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
                            ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
                            ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac)
-        if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
+        if (want_M && ctx->eval_wpe == 3) {
+            hipLaunchKernelGGL((k_eval_mix_w<1, 3>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],
+                               ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
+                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac);
+        } else if (want_M && ctx->eval_wpe == 4) {
+            hipLaunchKernelGGL((k_eval_mix_w<1, 4>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],
+                               ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
+                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac);
+        } else if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
 #undef PINT_EVAL_MIX
         HIPCHK(hipGetLastError());
     }
