@@ -260,6 +260,11 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * row tiles x Fourier columns; pulsars whose aligned 4-row groups hold more than two bins
  * (or two of one parity) leave the vg path.  Takes effect at pint_set_instances. */
 #define PINT_OPT_VBIN 5
+/* PINT_OPT_WBFIT = 1: pint_fit_step adds the wideband DM rows (pint_set_wideband) of every
+ * compact-layout instance to its normal equations (WidebandTOAFitter.fit_toas,
+ * fitter.py:2465-2637: design matrix [M_toa | F; M_dm | 0], residuals [r; pp_dm - DM]);
+ * default 0. */
+#define PINT_OPT_WBFIT 6
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

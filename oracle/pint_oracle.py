@@ -1019,10 +1019,12 @@ def designmatrix(om: OModel, toas: dict):
             col = chain * logf ** (fds.index(p) + 1)
         elif re.match(r"^JUMP\d+$", p):
             col = np.where(select_mask(toas, *om.masks[p]), -1.0, 0.0)
+        elif re.match(r"^DMJUMP\d+$", p):  # DMJUMPs leave the delay alone (dispersion_model.py:797)
+            col = np.zeros(n)
         elif p in BIN_PARAMS and B is not None:
             d = B.deriv(p)[:n].astype(float)
             col = chain * d * BIN_UNIT.get(p, 1.0)
-        elif re.match(r"^(EFAC|EQUAD|ECORR|TNEQ)\d+$", p) or p.startswith(("TNRED", "RN")):
+        elif re.match(r"^(EFAC|EQUAD|ECORR|TNEQ|DMEFAC|DMEQUAD)\d+$", p) or p.startswith(("TNRED", "RN")):
             continue
         else:
             raise ValueError(f"unfittable {p}")
@@ -1239,6 +1241,70 @@ def wideband_chi2(om: OModel, toas: dict) -> float:
         chi2_wls(rr["time"] - np.sum(rr["time"] / rr["sigma_us"] ** 2) / np.sum(1 / rr["sigma_us"] ** 2),
                  rr["sigma_us"])
     return c2 + dm_residuals(om, toas)["chi2"]
+
+
+def dm_designmatrix(om: OModel, names, toas: dict) -> np.ndarray:
+    """The DM rows' design matrix (TimingModel.d_dm_d_param, timing_model.py:2039, through
+    DesignMatrixMaker("dm"), pint_matrix.py:395-439): Offset 0; DMk: dt^k/k! (dt in Julian
+    years from DMEPOCH, dispersion_model.py:253-275); DMX_i: 1 in its bin (:684-708);
+    DMJUMP: -1 on its TOAs (:787-795); every other parameter 0."""
+    n = len(toas["tdb_hi"])
+    tdb = np.asarray(toas["tdb_hi"], dtype=LD) + np.asarray(toas["tdb_lo"], dtype=LD)
+    dm_terms = ["DM"] + om.prefix(r"^DM(\d+)$") if om.has("DM") else []
+    x = ((tdb - LD(om.v("DMEPOCH", 0.0))) / LD(DJY)).astype(float)
+    dmx = dict(_dmx_bins(om, np.asarray(toas["mjd_float"], dtype=float)))
+    out = np.zeros((n, len(names)))
+    for j, p in enumerate(names):
+        if p in dm_terms:
+            k = dm_terms.index(p)
+            out[:, j] = x ** k / math.factorial(k)
+        elif p in dmx:
+            out[:, j] = dmx[p].astype(float)
+        elif re.match(r"^DMJUMP\d+$", p):
+            out[:, j] = np.where(select_mask(toas, *om.masks[p]), -1.0, 0.0)
+    return out
+
+
+def wideband_gls_step(om: OModel, toas: dict):
+    """WidebandTOAFitter.fit_toas, one iteration (fitter.py:2465-2637, full_cov=False): the TOA
+    design matrix + noise basis over the TOA rows, the DM design matrix (noise columns 0)
+    over the DM rows, residuals [TOA residuals (s); DM residuals (pc/cm^3)] with errors [scaled
+    TOA errors; scaled DM errors]; normalised columns; GLS with the noise priors; Cholesky
+    (SVD fallback).  Returns the step, errors, covariance and the linearised chi2."""
+    res = residuals(om, toas)
+    M, names = designmatrix(om, toas)
+    ntm = M.shape[1]
+    Md = dm_designmatrix(om, names, toas)
+    dr = dm_residuals(om, toas)
+    U, phi = noise_basis(om, toas)
+    phiinv = np.zeros(ntm)
+    if U is not None:
+        phiinv = np.concatenate((phiinv, 1 / phi))
+        M = np.hstack((M, U))
+        Md = np.hstack((Md, np.zeros((Md.shape[0], U.shape[1]))))
+    M = np.vstack((M, Md))
+    M, norm = _normalize(M)
+    phiinv = phiinv / norm ** 2
+    y = np.concatenate((res["time"], dr["resids"]))
+    Nvec = np.concatenate(((res["sigma_us"] * 1e-6) ** 2, dr["sigma"] ** 2))
+    cinv = 1 / Nvec
+    mtcm = M.T @ (cinv[:, None] * M) + np.diag(phiinv)
+    mtcy = M.T @ (cinv * y)
+    try:
+        c = scipy.linalg.cho_factor(mtcm)
+        xhat = scipy.linalg.cho_solve(c, mtcy)
+        xvar = scipy.linalg.cho_solve(c, np.eye(len(mtcy)))
+    except scipy.linalg.LinAlgError:
+        Uu, s, Vt = scipy.linalg.svd(mtcm, full_matrices=False)
+        s = np.where(s <= 0, np.inf, s)
+        xvar = (Vt.T / s) @ Vt
+        xhat = Vt.T @ ((Uu.T @ mtcy) / s)
+    newres = y - M @ xhat
+    chi2 = float(newres @ (cinv * newres) + xhat @ (phiinv * xhat))
+    dpars = xhat / norm
+    errs = np.sqrt(np.diag(xvar)) / norm
+    cov = (xvar / norm).T / norm
+    return dict(dpars=dpars[:ntm], errs=errs[:ntm], cov=cov[:ntm, :ntm], names=names, chi2=chi2)
 
 
 def lognorm(om, toas, r, sigma_us, gls=True):

@@ -19,6 +19,9 @@ from refcommon import (register_clockless_sites, pack_toas, export_model, mask_t
 import pint.simulation as sim
 from pint.models import get_model
 from pint.residuals import Residuals, WidebandDMResiduals, WidebandTOAResiduals
+from pint.fitter import WidebandTOAFitter
+from refcommon import split_ld
+import copy
 from gen_synth import pta_par
 
 EXTRA = """DMJUMP mjd 53000 54200 0.0012 1
@@ -76,6 +79,16 @@ def main():
     rw = wt.rms_weighted()
     meta["wb_rms_weighted"] = {"toa_us": float(rw["toa"].to_value(u.us)),
                                "dm": float(rw["dm"].to_value(u.pc / u.cm ** 3))}
+    # WidebandTOAFitter (fitter.py:2292-2637): one GLS step over [TOA rows; DM rows]
+    f = WidebandTOAFitter(ts, copy.deepcopy(model))
+    chi2 = f.fit_toas(maxiter=1)
+    meta["wbfit_chi2"] = float(chi2)
+    meta["wbfit_params"] = {p: list(map(float, split_ld(getattr(f.model, p).value))) for p in f.model.free_params}
+    meta["wbfit_errors"] = {p: float(getattr(f.model, p).uncertainty_value) for p in f.model.free_params}
+    meta["wbfit_post_chi2"] = float(f.resids.chi2)
+    arrays["wbfit_post_toa_resid"] = np.asarray(f.resids.toa.time_resids.to_value(u.s), dtype=np.float64)
+    arrays["wbfit_post_dm_resid"] = np.asarray(f.resids.dm.resids.to_value(u.pc / u.cm ** 3), dtype=np.float64)
+    arrays["wbfit_cov"] = np.asarray(f.parameter_covariance_matrix.matrix, dtype=np.float64)
     save("wb_dd", arrays, meta)
 
 

@@ -1377,6 +1377,148 @@ __global__ __launch_bounds__(DMR_T) void k_dm_resid(const PsrDev* __restrict__ p
     if (threadIdx.x == 0) chi2[blockIdx.x] = c2;
 }
 
+// k_wb_gram: the DM rows of WidebandTOAFitter (fitter.py:2465-2637) added to an instance's
+// normal equations after k_greduce: the combined design matrix is [M_toa | F; M_dm | 0] with
+// M_dm the DM derivatives (Offset 0, DMk dt^k/k!, DMX 1 in its bin, DMJUMP -1 on its TOAs,
+// every other column 0; pint_matrix.py:395-439), residuals pp_dm - DM and weights
+// 1/sigma_dm^2.  Only the DM-type columns and the residual gain entries: the dense compact
+// Gram (DM Taylor / DMJUMP columns x themselves and the residual, r^T W r), their column
+// sums of squares (the normalisation, utils.py:2879), and per DMX bin DD += sum w, DCS +=
+// count, Sd[.][c] += sum w d_c, Sd[.][res] += sum w r (the bin stays diagonal).  Compact
+// layout only (the host checks).  One workgroup per instance; sums in a fixed order.
+constexpr int WB_MAXC = 8;  // dense DM-type columns (DM Taylor terms + DMJUMPs)
+__device__ __forceinline__ void wb_row(const PsrDev& Pd, const pint_spec_t& S, const double* P, int i, bool any,
+                                       dd ep, double& r, double& w, double& dtyr) {
+    double dm = 0.0;
+    dtyr = S.o_DMEPOCH >= 0 ? dd_to_d(dd_sub(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), ep)) * INV_DJY : 0.0;
+    if (S.ndm > 0) {
+        const double x = any ? dtyr : 0.0;
+        dm = pval(P, S.o_DM + 2 * (S.ndm - 1));
+        for (int k = S.ndm - 1; k >= 1; k--) dm = dm * x * inv_int(k) + pval(P, S.o_DM + 2 * (k - 1));
+    }
+    if (S.ndmx > 0) {
+        const int a = Pd.dmx_a[i], b = Pd.dmx_b[i];
+        if (a >= 0) dm += pval(P, S.o_DMX + 2 * a);
+        if (b >= 0) dm += pval(P, S.o_DMX + 2 * b);
+    }
+    if (S.ndmjump > 0) {
+        const uint64_t m = Pd.dmjmask[i];
+        for (int k = 0; k < S.ndmjump; k++)
+            if ((m >> k) & 1ull) dm -= pval(P, S.o_DMJUMP + 2 * k);
+    }
+    r = Pd.pp_dm[i] - dm;
+    const double is = 1.0 / Pd.dm_sig[i];
+    w = is * is;
+}
+__device__ __forceinline__ double wb_deriv(const PsrDev& Pd, int kind, int idx, int i, double dtyr) {
+    if (kind == PINT_COL_DM) {  // d_dm_d_DMs (dispersion_model.py:253-275)
+        double v = 1.0;
+        for (int j = 1; j <= idx; j++) v = v * dtyr * inv_int(j);
+        return v;
+    }
+    return ((Pd.dmjmask[i] >> idx) & 1ull) ? -1.0 : 0.0;  // DMJUMP (:787-795)
+}
+__global__ __launch_bounds__(256) void k_wb_gram(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                 const double* __restrict__ tables, int nsplit,
+                                                 double* __restrict__ Gpart, double* __restrict__ colsq,
+                                                 double* __restrict__ Sd, double* __restrict__ DD,
+                                                 double* __restrict__ DCS) {
+    __shared__ double red[4][(WB_MAXC + 1) * (WB_MAXC + 2) / 2 + WB_MAXC];
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.wb || !Pd.dsplit) return;
+    const pint_spec_t& S = *Pd.spec;
+    const double* P = tables + I.toff;
+    const int n = I.n, Kp = Pd.Kpd, Kres = Pd.Kd;
+    // the dense DM-type columns (compact index, kind, index)
+    int cc[WB_MAXC], kd[WB_MAXC], ix[WB_MAXC], m = 0;
+    for (int c = 0; c < S.ncol && m < WB_MAXC; c++) {
+        const int k = S.col_kind[c];
+        if ((k == PINT_COL_DM || k == PINT_COL_ZERO) && Pd.cmap[c] >= 0) {
+            cc[m] = Pd.cmap[c];
+            kd[m] = k;
+            ix[m] = S.col_index[c];
+            m++;
+        }
+    }
+    bool any = false;
+    for (int k = 1; k < S.ndm; k++) any |= (pval(P, S.o_DM + 2 * k) != 0.0);
+    const dd ep = S.o_DMEPOCH >= 0 ? pdd(P, S.o_DMEPOCH) : dd_make(0.0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // (a) dense pairs (i <= j over the m columns and the residual) and column sums of squares
+    constexpr int NP = (WB_MAXC + 1) * (WB_MAXC + 2) / 2;
+    double acc[NP + WB_MAXC];
+#pragma unroll
+    for (int p = 0; p < NP + WB_MAXC; p++) acc[p] = 0.0;
+    for (int i = tid; i < n; i += 256) {
+        double r, w, dtyr;
+        wb_row(Pd, S, P, i, any, ep, r, w, dtyr);
+        double d[WB_MAXC + 1];
+#pragma unroll
+        for (int a = 0; a < WB_MAXC; a++) d[a] = a < m ? wb_deriv(Pd, kd[a], ix[a], i, dtyr) : 0.0;
+        d[WB_MAXC] = r;
+        int p = 0;
+#pragma unroll
+        for (int a = 0; a <= WB_MAXC; a++)
+#pragma unroll
+            for (int b = a; b <= WB_MAXC; b++, p++) acc[p] += w * d[a] * d[b];
+#pragma unroll
+        for (int a = 0; a < WB_MAXC; a++) acc[NP + a] += d[a] * d[a];
+    }
+#pragma unroll
+    for (int p = 0; p < NP + WB_MAXC; p++) {
+        const double v = wave_sum(acc[p]);
+        if (lane == 0) red[wave][p] = v;
+    }
+    __syncthreads();
+    double* G = Gpart + I.goff;
+    if (tid < NP + WB_MAXC) {
+        const double v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        if (tid < NP) {
+            int a = 0, p = tid;  // pair (a, b), a <= b over columns 0..WB_MAXC (WB_MAXC = residual)
+            while (p > WB_MAXC - a) { p -= WB_MAXC - a + 1; a++; }
+            const int b = a + p;
+            const bool va = a < m || a == WB_MAXC, vb = b < m || b == WB_MAXC;
+            if (va && vb) {
+                int ca = a == WB_MAXC ? Kres : cc[a], cb = b == WB_MAXC ? Kres : cc[b];
+                if (ca > cb) { const int t = ca; ca = cb; cb = t; }
+                G[(long)ca * Kp + cb] += v;
+            }
+        } else if (tid - NP < m) {
+            colsq[(I.coff + cc[tid - NP]) * nsplit] += v;
+        }
+    }
+    // (b) the DMX bins: one wave per bin
+    for (int a = wave; a < Pd.ndc; a += 4) {
+        const int k0 = Pd.dptr[a], k1 = Pd.dptr[a + 1];
+        double sw = 0.0, cnt = 0.0, swr = 0.0, swd[WB_MAXC];
+#pragma unroll
+        for (int c = 0; c < WB_MAXC; c++) swd[c] = 0.0;
+        for (int k = k0 + lane; k < k1; k += 64) {
+            const int i = Pd.didx[k];
+            double r, w, dtyr;
+            wb_row(Pd, S, P, i, any, ep, r, w, dtyr);
+            sw += w;
+            cnt += 1.0;
+            swr += w * r;
+#pragma unroll
+            for (int c = 0; c < WB_MAXC; c++) swd[c] += c < m ? w * wb_deriv(Pd, kd[c], ix[c], i, dtyr) : 0.0;
+        }
+        sw = wave_sum(sw);
+        cnt = wave_sum(cnt);
+        swr = wave_sum(swr);
+#pragma unroll
+        for (int c = 0; c < WB_MAXC; c++) swd[c] = wave_sum(swd[c]);
+        if (lane == 0) {
+            DD[I.ddoff + a] += sw;
+            DCS[I.ddoff + a] += cnt;
+            double* row = Sd + I.sdoff + (long)a * Kp;
+            row[Kres] += swr;
+            for (int c = 0; c < m; c++) row[cc[c]] += swd[c];
+        }
+    }
+}
+
 // k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
 // with the phase t_i f_1 reduced in double-double; computed once at pint_add_pulsar
 // (TOA-only data, like tdb).  Harmonic m is reached by rotations of it.
@@ -3137,6 +3279,7 @@ struct pint_ctx {
     std::vector<KpGroup> kp_groups, kp_groups_c, kp_groups_v;
     int vgram = 1;       // PINT_OPT_VGRAM
     int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
+    int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
     int n_vg = 0;        // instances on the k_gram_v path
@@ -4326,6 +4469,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipGetLastError());
         record(ctx, 15);
     }
+    if (ctx->wbfit && cmp) {  // WidebandTOAFitter: the DM rows join the normal equations
+        hipLaunchKernelGGL(k_wb_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->nsplit, ctx->d_G, ctx->d_colsq, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+        HIPCHK(hipGetLastError());
+    }
     record(ctx, 7);
     // solve plan: the DMX-eliminated solve (k_solve_dmx) for compact-layout instances when
     // every such instance fits its LDS budget; the others (and everything in the full
@@ -4562,6 +4710,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_BLOCKED_SOLVE) { ctx->blocked_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VBIN) { ctx->vbin = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_WBFIT) { ctx->wbfit = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {

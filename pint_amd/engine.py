@@ -614,6 +614,10 @@ class Session:
         """Generated-Fourier compact fit path (k_gram_v); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 2, 1 if on else 0))
 
+    def set_wbfit(self, on=True):
+        """Wideband DM rows in the fit steps (PINT_OPT_WBFIT, WidebandTOAFitter)."""
+        self._check(self.L.pint_set_option(self.ctx, 6, 1 if on else 0))
+
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))

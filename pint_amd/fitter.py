@@ -244,7 +244,8 @@ class BatchFit:
         return results
 
     def _errors_into(self, results):
-        dp, er, cov, _ = self.s.read_step()
+        dp, er, cov, cl = self.s.read_step()
+        self.last_chi2_lin = cl  # the steps' linearised chi2 (WidebandTOAFitter returns it)
         for d, (k, lay) in enumerate(zip(self.idx, self.layouts)):
             res = results[k]
             nc = len(lay.columns)
@@ -481,11 +482,16 @@ class Fitter:
             par("EPHEM").value = self.toas.ephem
         if getattr(self.toas, "clock", None):
             par("CLOCK").value = self.toas.clock
-        par("DMDATA").value = False
+        par("DMDATA").value = hasattr(self.resids, "dm")
         if chi2 is not None:
             par("CHI2").value = float(chi2)
             par("CHI2R").value = float(chi2) / self.resids.dof
-            par("TRES").value = float(self.resids.rms_weighted())
+            rw = self.resids.rms_weighted()
+            if isinstance(rw, dict):  # wideband: TRES (us) and DMRES (pc/cm^3)
+                par("TRES").value = float(rw["toa"])
+                par("DMRES").value = float(rw["dm"])
+            else:
+                par("TRES").value = float(rw)
 
     def set_params(self, d):
         for k, v in d.items():
@@ -515,6 +521,61 @@ class GLSFitter(Fitter):
                         noise=not full_cov)
         self.update_model(res.chi2)
         return res.chi2
+
+
+class WidebandTOAFitter(Fitter):
+    """fitter.py:2292-2637: a GLS fit of TOAs and their wideband DM measurements.  The design
+    matrix is [M_toa | F; M_dm | 0] (the DM derivatives of every free parameter, zero
+    noise-basis columns), the residuals [TOA residuals; pp_dm - DM] with the scaled TOA and
+    DM errors.  On the device the DM rows only touch the DM-type columns and the residual of
+    the normal equations (k_wb_gram, PINT_OPT_WBFIT); the rest is the GLS step.  Needs the
+    compact DMX layout (>= 8 free DMX bins, no TOA in two bins, no ECORR)."""
+
+    def __init__(self, fit_data, model, fit_data_names=["toa", "dm"], track_mode=None, additional_args={}):
+        toas = fit_data[0] if isinstance(fit_data, (list, tuple)) else fit_data
+        if not hasattr(toas, "is_wideband"):
+            raise ValueError(f"The first data set should be a TOAs object but is {toas}.")
+        if len(fit_data_names) == 0:
+            raise ValueError("Please specify the fit data.")
+        super().__init__(toas, model, track_mode=track_mode)
+        self.fit_data_names = list(fit_data_names)
+        self.additional_args = dict(additional_args)
+        self.is_wideband = True
+        self.method = "General_Data_Fitter"
+        self.update_resids()
+        self.resids_init = self.resids
+
+    def make_resids(self, model):
+        from .residuals import WidebandTOAResiduals
+        ta = dict(self.additional_args.get("toa", {}))
+        if self.track_mode is not None:
+            ta["track_mode"] = self.track_mode
+        return WidebandTOAResiduals(self.toas, model, toa_resid_args=ta, dm_resid_args=self.additional_args.get("dm", {}))
+
+    def fit_toas(self, maxiter=1, threshold=0, full_cov=False, debug=False):
+        """Returns the last step's linearised chi2 (newres^T C^-1 newres + xhat^T phi^-1 xhat,
+        fitter.py:2546-2552); full_cov=True solves the same system (Woodbury identity)."""
+        self.model.validate()
+        bf = BatchFit([(self.model, self.toas)], mode="gls", threshold=threshold, degeneracy_style="gls",
+                      track_mode=self.track_mode)
+        try:
+            lay = bf.layouts[0]
+            if bf.s.fit_layout(lay)[0] != 1:
+                raise NotImplementedError("WidebandTOAFitter on the device needs the compact DMX layout (>= 8 "
+                                          "free DMX bins, no TOA in two free bins, no ECORR)")
+            bf.s.set_wideband(lay)
+            bf.s.set_wbfit(True)
+            res = bf.fit_plain(maxiter=maxiter)[0]
+            chi2 = float(bf.last_chi2_lin[0])
+        finally:
+            bf.close()
+        self.fitresult = res
+        self.errors = res.errors
+        self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
+        self.converged = res.converged
+        self.update_resids()
+        self.update_model(chi2)
+        return chi2
 
 
 class DownhillFitter(Fitter):

@@ -142,6 +142,7 @@ _DEFS = {
     "BINARY": ("", "str", "", False, None), "NTOA": ("", "int", "", False, None),
     "CHI2": ("", "float", "", False, None), "CHI2R": ("", "float", "", False, None),
     "TRES": ("", "float", "us", False, None), "DMDATA": ("", "bool", "", False, None),
+    "DMRES": ("", "float", "pc / cm3", False, None),
     "INFO": ("", "str", "", False, None), "TIMEEPH": ("", "str", "", False, None),
     "T2CMETHOD": ("", "str", "", False, None), "DILATEFREQ": ("", "bool", "", False, None),
     "TZRMJD": ("AbsPhase", "mjd", "d", True, None), "TZRSITE": ("AbsPhase", "str", "", False, None),
@@ -226,7 +227,7 @@ MASK_PARAMS = {"JUMP": ("PhaseJump", "s"), "EFAC": ("ScaleToaError", ""),
                "DMJUMP": ("DispersionJump", "pc / cm3"), "DMEFAC": ("ScaleDmError", ""),
                "DMEQUAD": ("ScaleDmError", "pc / cm3")}
 
-IGNORED = {"MODE", "NITS", "DMRES", "IBOOT", "RM", "SWP", "DMXEP", "DMXF1", "DMXF2"}
+IGNORED = {"MODE", "NITS", "IBOOT", "RM", "SWP", "DMXEP", "DMXF1", "DMXF2"}
 
 
 def make_param(name: str) -> Optional[Param]:

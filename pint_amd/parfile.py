@@ -39,7 +39,7 @@ from .parameter import LD, Param
 DJM0 = 2400000.5
 UTC_MJD_PARAMS = {"TZRMJD"}  # + DMXR1_/DMXR2_ (dispersion_model.py:411-428)
 TOP_LEVEL = ["PSR", "EPHEM", "CLOCK", "CLK", "UNITS", "START", "FINISH", "INFO", "TIMEEPH", "T2CMETHOD", "TRACK",
-             "DILATEFREQ", "DMDATA", "NTOA", "CHI2", "CHI2R", "TRES"]
+             "DILATEFREQ", "DMDATA", "NTOA", "CHI2", "CHI2R", "TRES", "DMRES"]
 
 
 # ---- exact float64 day + fraction (astropy time.utils.day_frac / two_sum, restated) ----

@@ -12,6 +12,8 @@ from golden_util import GOLDEN
 
 import pint_oracle as O
 
+LD = np.longdouble
+
 
 def _fixture():
     z = dict(np.load(os.path.join(GOLDEN, "wb_dd.npz"), allow_pickle=False))
@@ -78,3 +80,49 @@ def test_gpu_wideband_toa_resids():
     assert abs(w.chi2 / O.wideband_chi2(om, ot) - 1) < 5e-6
     with pytest.raises(AttributeError):
         w.dm.dof
+
+
+def _ref_pars(meta, key):
+    return {p: np.longdouble(v[0]) + np.longdouble(v[1]) for p, v in meta[key].items()}
+
+
+def test_oracle_wideband_fit():
+    """The oracle's WidebandTOAFitter step (fitter.py:2465-2637) against the reference's fit:
+    parameters <= 1e-3 sigma (the TOA-residual floor), errors 1e-6, the linearised chi2 at
+    the end-to-end floor."""
+    om, toas, z, meta = _fixture()
+    st = O.wideband_gls_step(om, toas)
+    ref = _ref_pars(meta, "wbfit_params")
+    for j, p in enumerate(st["names"]):
+        if p == "Offset":
+            continue
+        sig = meta["wbfit_errors"][p]
+        d = float(LD(om.values[p]) + LD(st["dpars"][j]) - ref[p]) / sig
+        assert abs(d) < 1e-3, (p, d)
+        assert abs(st["errs"][j] / sig - 1) < 1e-6, (p, st["errs"][j] / sig - 1)
+    assert abs(st["chi2"] / meta["wbfit_chi2"] - 1) < 5e-6
+
+
+@pytest.mark.gpu
+def test_gpu_wideband_fit():
+    """WidebandTOAFitter on the device (the DM rows added to the normal equations by
+    k_wb_gram) against the reference's fit: parameters <= 1e-3 sigma, errors 1e-5, the
+    linearised chi2 at the end-to-end floor; post-fit residuals; the model's DMDATA/DMRES."""
+    from golden_util import load
+    from pint_amd import WidebandTOAFitter
+    model, toas, z, meta = load("wb_dd")
+    f = WidebandTOAFitter(toas, model)
+    c2 = f.fit_toas(maxiter=1)
+    ref = _ref_pars(meta, "wbfit_params")
+    worst = 0.0
+    for p in meta["wbfit_params"]:
+        s = meta["wbfit_errors"][p]
+        d = float((LD(f.model[p].value) - ref[p]) / LD(s))
+        worst = max(worst, abs(d))
+        assert abs(f.model[p].uncertainty / s - 1) < 1e-5, (p, f.model[p].uncertainty / s - 1)
+    assert worst < 1e-3, worst
+    assert abs(c2 / meta["wbfit_chi2"] - 1) < 5e-6
+    assert abs(f.resids.chi2 / meta["wbfit_post_chi2"] - 1) < 5e-6
+    assert np.max(np.abs(f.resids.toa.time_resids - z["wbfit_post_toa_resid"])) < 2e-10
+    assert np.max(np.abs(f.resids.dm.resids - z["wbfit_post_dm_resid"])) < 1e-9
+    assert f.model["DMDATA"].value is True and f.model["DMRES"].value > 0
