@@ -329,7 +329,8 @@ def j0740_legs(side, dist, barrier, max_over_ranks):
     model, toas, frozen = j0740_data()
     out = {"workload": "J0740+6620 synthetic 50k TOAs (C3)", "free_params": len(model.free_params),
            "frozen_empty": len(frozen)}
-    for rep in range(2):  # the first fit is the warm-up (library load, first-call allocations)
+    dts = []
+    for rep in range(4):  # the first fit is the warm-up (library load, first-call allocations)
         f = DownhillGLSFitter(toas, copy.deepcopy(model))
         barrier()
         t0 = time.perf_counter()
@@ -338,9 +339,11 @@ def j0740_legs(side, dist, barrier, max_over_ranks):
             conv = True
         except MaxiterReached:
             conv = False
-        dt = time.perf_counter() - t0
+        dts.append(time.perf_counter() - t0)
+    dt = float(np.median(dts[1:]))  # one fit is ~30-40 ms of mostly host work: the median of 3
     out["downhill_gls"] = {"metric": "DownhillGLSFitter fits/sec (maxiter=10)", "value": round(1.0 / dt, 3),
-                           "seconds": round(dt, 4), "converged": conv, "chi2": float(f.resids.chi2)}
+                           "seconds": round(dt, 4), "seconds_all": [round(x, 4) for x in dts[1:]],
+                           "converged": conv, "chi2": float(f.resids.chi2)}
     g = GLSFitter(toas, copy.deepcopy(model))
     g.fit_toas(maxiter=1)
     m2 = np.linspace(0.2, 0.3, side)
