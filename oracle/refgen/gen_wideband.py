@@ -19,7 +19,7 @@ from refcommon import (register_clockless_sites, pack_toas, export_model, mask_t
 import pint.simulation as sim
 from pint.models import get_model
 from pint.residuals import Residuals, WidebandDMResiduals, WidebandTOAResiduals
-from pint.fitter import WidebandTOAFitter
+from pint.fitter import WidebandTOAFitter, WidebandDownhillFitter
 from refcommon import split_ld
 import copy
 from gen_synth import pta_par
@@ -89,6 +89,16 @@ def main():
     arrays["wbfit_post_toa_resid"] = np.asarray(f.resids.toa.time_resids.to_value(u.s), dtype=np.float64)
     arrays["wbfit_post_dm_resid"] = np.asarray(f.resids.dm.resids.to_value(u.pc / u.cm ** 3), dtype=np.float64)
     arrays["wbfit_cov"] = np.asarray(f.parameter_covariance_matrix.matrix, dtype=np.float64)
+    # WidebandDownhillFitter (fitter.py:1812-1895): the downhill line search on the combined chi2
+    fd = WidebandDownhillFitter(ts, copy.deepcopy(model))
+    try:
+        fd.fit_toas(maxiter=10)
+        meta["wbdown_status"] = "converged"
+    except Exception as e:
+        meta["wbdown_status"] = type(e).__name__
+    meta["wbdown_chi2"] = float(fd.resids.chi2)
+    meta["wbdown_params"] = {p: list(map(float, split_ld(getattr(fd.model, p).value))) for p in fd.model.free_params}
+    meta["wbdown_errors"] = {p: float(getattr(fd.model, p).uncertainty_value) for p in fd.model.free_params}
     save("wb_dd", arrays, meta)
 
 

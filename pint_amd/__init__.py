@@ -10,6 +10,7 @@ from .timing_model import TimingModel, get_model  # noqa: F401
 from .toa import TOAs, get_TOAs, get_model_and_toas  # noqa: F401
 from .residuals import Residuals, WidebandDMResiduals, WidebandTOAResiduals  # noqa: F401
 from .fitter import (Fitter, WLSFitter, GLSFitter, DownhillWLSFitter, DownhillGLSFitter, WidebandTOAFitter,  # noqa: F401
+                     WidebandDownhillFitter,  # noqa: F401
                      MaxiterReached, StepProblem, InvalidModelParameters, CorrelatedErrors)
 from .gridutils import grid_chisq  # noqa: F401
 

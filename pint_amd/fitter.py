@@ -103,7 +103,8 @@ class BatchFit:
     EVAL_ERRORS = (L.PINT_E_KEPLER, L.PINT_E_PARAM)
 
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
-                 layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None):
+                 layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None,
+                 wideband=False):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
         are bare parameter tables of already-uploaded pulsars, e.g. grid points).
 
@@ -138,6 +139,16 @@ class BatchFit:
         self.grid_like = isinstance(tables, np.ndarray) and tables.ndim == 2 and all(l is layouts[0] for l in layouts)
         self.layouts0 = list(layouts)
         self._bind(list(layouts), tables)
+        # wideband (WidebandTOAFitter / WidebandDownhillFitter): the DM rows join every fit
+        # step (k_wb_gram) and every chi2 (the DM chi2 of WidebandTOAResiduals)
+        self.wideband = bool(wideband)
+        if self.wideband:
+            for lay in {id(l): l for l in layouts}.values():
+                if self.s.fit_layout(lay)[0] != 1:
+                    raise NotImplementedError("wideband fits on the device need the compact DMX layout (>= 8 "
+                                              "free DMX bins, no TOA in two free bins, no ECORR)")
+                self.s.set_wideband(lay)
+            self.s.set_wbfit(True)
 
     def _bind(self, layouts, tables):
         self.layouts = layouts
@@ -186,6 +197,8 @@ class BatchFit:
         if any(self.use_gls_chi2):
             cg = self.s.chi2_gls()
             c2 = np.where(self.use_gls_chi2, cg, c2)
+        if self.wideband:  # WidebandTOAResiduals.chi2 = the TOA chi2 + the DM chi2 (residuals.py:1206)
+            c2 = c2 + self.s.dm_resids()[1]
         return c2, None
 
     def _step(self):
@@ -441,15 +454,16 @@ class Fitter:
 
     def _run(self, mode, plain=True, threshold=None, style=None, noise=True, **kw):
         from .residuals import Residuals
+        wideband = getattr(self, "is_wideband", False)
         bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style,
-                      track_mode=self.track_mode)
+                      track_mode=self.track_mode, wideband=wideband)
         self.resids = None
         try:
             res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
             # the final residuals are already on the device (the fit's last evaluation):
             # take them from the fit's own session instead of re-uploading (a WLS fit of a
             # correlated-noise model has no noise basis there, so its GLS chi2 is computed anew)
-            if mode == "gls" or not self.model.has_correlated_errors:
+            if not wideband and (mode == "gls" or not self.model.has_correlated_errors):
                 self.resids = Residuals._from_batch(self.toas, self.model, bf, 0, res.chi2, self.track_mode)
         finally:
             bf.close()
@@ -459,7 +473,7 @@ class Fitter:
         self.converged = res.converged
         if self.resids is None:
             self.update_resids()
-        if mode == "gls" and noise:
+        if mode == "gls" and noise and not wideband:
             self.resids.noise_resids = res.noise_resids
         return res
 
@@ -557,14 +571,8 @@ class WidebandTOAFitter(Fitter):
         fitter.py:2546-2552); full_cov=True solves the same system (Woodbury identity)."""
         self.model.validate()
         bf = BatchFit([(self.model, self.toas)], mode="gls", threshold=threshold, degeneracy_style="gls",
-                      track_mode=self.track_mode)
+                      track_mode=self.track_mode, wideband=True)
         try:
-            lay = bf.layouts[0]
-            if bf.s.fit_layout(lay)[0] != 1:
-                raise NotImplementedError("WidebandTOAFitter on the device needs the compact DMX layout (>= 8 "
-                                          "free DMX bins, no TOA in two free bins, no ECORR)")
-            bf.s.set_wideband(lay)
-            bf.s.set_wbfit(True)
             res = bf.fit_plain(maxiter=maxiter)[0]
             chi2 = float(bf.last_chi2_lin[0])
         finally:
@@ -632,6 +640,34 @@ class DownhillFitter(Fitter):
         if not res.converged:
             raise MaxiterReached(f"Convergence not detected after {maxiter} steps.")
         return self.converged
+
+
+class WidebandDownhillFitter(DownhillFitter):
+    """fitter.py:1812-1895: the downhill line search (DownhillFitter._fit_toas) with the
+    wideband step (WidebandState: the GLS step over [TOA rows; DM rows], fitter.py:1612-1810)
+    and the wideband chi2 (WidebandTOAResiduals); on the device the step is the GLS step with
+    k_wb_gram and every trial's chi2 adds the DM chi2 (BatchFit(wideband=True))."""
+    mode = "gls"
+
+    def __init__(self, toas, model, track_mode=None, residuals=None, add_args=None):
+        self.add_args = {} if add_args is None else add_args
+        self.is_wideband = True
+        self.full_cov = False
+        self.threshold = 0
+        super().__init__(toas, model, track_mode, residuals)
+        self.method = "downhill_wideband"
+
+    def make_resids(self, model):
+        from .residuals import WidebandTOAResiduals
+        return WidebandTOAResiduals(self.toas, model, toa_resid_args=self.add_args.get("toa", {}),
+                                    dm_resid_args=self.add_args.get("dm", {}))
+
+    def fit_toas(self, maxiter=10, threshold=1e-14, full_cov=False, debug=False, **kwargs):
+        """threshold: WidebandState's SVD cut (the device solves by Cholesky and takes the SVD
+        path only for degenerate normal equations); full_cov solves the same system."""
+        self.threshold = threshold
+        self.full_cov = full_cov
+        return super().fit_toas(maxiter=maxiter, debug=debug, threshold=threshold, **kwargs)
 
 
 class DownhillWLSFitter(DownhillFitter):

@@ -126,3 +126,27 @@ def test_gpu_wideband_fit():
     assert np.max(np.abs(f.resids.toa.time_resids - z["wbfit_post_toa_resid"])) < 2e-10
     assert np.max(np.abs(f.resids.dm.resids - z["wbfit_post_dm_resid"])) < 1e-9
     assert f.model["DMDATA"].value is True and f.model["DMRES"].value > 0
+
+
+@pytest.mark.gpu
+def test_gpu_wideband_downhill():
+    """WidebandDownhillFitter on the device (the wideband GLS step + the combined chi2 in the
+    line search) against the reference's: status, chi2 at the end-to-end floor, parameters
+    within the Downhill bar of tests/test_gpu_parity.py::test_downhill_gls (5e-2 sigma: the
+    best-iterate choice follows each side's own chi2 rounding)."""
+    from golden_util import load
+    from pint_amd import WidebandDownhillFitter
+    from pint_amd.fitter import MaxiterReached, StepProblem
+    model, toas, z, meta = load("wb_dd")
+    f = WidebandDownhillFitter(toas, model)
+    try:
+        f.fit_toas(maxiter=10)
+        status = "converged"
+    except (MaxiterReached, StepProblem) as e:
+        status = type(e).__name__
+    assert status == meta["wbdown_status"]
+    assert abs(f.resids.chi2 / meta["wbdown_chi2"] - 1) < 5e-6, (f.resids.chi2, meta["wbdown_chi2"])
+    ref = _ref_pars(meta, "wbdown_params")
+    worst = max(abs(float((LD(f.model[p].value) - ref[p]) / LD(meta["wbdown_errors"][p]))) for p in ref)
+    print(f"wideband downhill: chi2 {f.resids.chi2:.6f} ref {meta['wbdown_chi2']:.6f}, worst {worst:.2e} sigma")
+    assert worst < 5e-2, worst
