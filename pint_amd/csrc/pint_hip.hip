@@ -1600,16 +1600,16 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
                                                  const double* __restrict__ dmxv, double* __restrict__ Sd,
                                                  double* __restrict__ DD, double* __restrict__ DCS,
                                                  const double* __restrict__ BFp, int vb) {
-    __shared__ double sh[8];
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const bool cmp = compact && Pd.dsplit;
     const bool vg = cmp && Pd.vg;
     const int Kp = cmp ? Pd.Kpd : I.Kp, Kc = cmp ? Pd.Kd : I.K;
     const int r0 = Pd.red0c;
-    if ((int)blockIdx.x >= nbg) {  // DMX bin a of a vg instance: its slot partials
-        const int a = blockIdx.x - nbg;
-        if (!vg || a >= Pd.ndc) return;
+    if ((int)blockIdx.x >= nbg) {  // DMX bins of a vg instance (one per wave): slot partials
+        const int lane = threadIdx.x & 63;
+        const int a = (blockIdx.x - nbg) * 4 + (threadIdx.x >> 6);
+        if (!vg || a >= Pd.ndc) return;  // wave-uniform: only wave-level reductions below
         const int SW = Kc + 3;
         const int cnt = Pd.dptr[a + 1] - Pd.dptr[a];
         const long lo = cnt > 0 ? Pd.didx[Pd.dptr[a]] : 0, hi = lo + cnt;
@@ -1617,7 +1617,7 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         per = (per + 3) / 4 * 4;
         const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
         const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
-        for (int c = threadIdx.x; c <= Kc; c += blockDim.x) {
+        for (int c = lane; c <= Kc; c += 64) {
             double v = 0.0;
             if (vb && Pd.vb && c >= r0 && c < Kc) {
                 // binned DMX x F (k_gram_v VB): the 16x8 blocks D of the (split, wave) quarters
@@ -1646,14 +1646,14 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
         // square norm is the bin's only DMX x DMX entry: k_gram_v skips those tiles)
         double q2 = 0.0, qw = 0.0;
-        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        for (long i = lo + lane; i < hi; i += 64) {
             const double xx = dmxv[I.ooff + i], xw = xx * Pd.isig[i];
             q2 += xx * xx;
             qw += xw * xw;
         }
-        q2 = block_sum<4>(q2, sh);
-        qw = block_sum<4>(qw, sh);
-        if (threadIdx.x == 0) {
+        q2 = wave_sum(q2);
+        qw = wave_sum(qw);
+        if (lane == 0) {
             DCS[I.ddoff + a] = q2;
             DD[I.ddoff + a] = qw;
         }
@@ -3045,8 +3045,10 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
 }
 
 // tables += lambda * dpars on every timing column (skips Offset), double-double add; then
-// the per-instance constants of the updated table (k_prep's work, saving its launch)
-__global__ void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, double* __restrict__ tables,
+// the per-instance constants of the updated table (k_prep's work, saving its launch).
+// Launched with PREP_T threads: the bound lets the setup keep k_prep's registers (the
+// default 1024-thread budget of 128 VGPRs spilled 252 B/lane into its serial chain)
+__global__ __launch_bounds__(PREP_T) void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, double* __restrict__ tables,
                         const double* __restrict__ dpars, const double* __restrict__ lam,
                         InstConst* __restrict__ ic) {
     const int inst = blockIdx.x;
@@ -4463,7 +4465,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         }
         const int nbg = (maxKp * maxKp + 255) / 256;
         record(ctx, 14);
-        hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? ctx->max_ndc : 0), ctx->ninst), dim3(256), 0, ctx->stream,
+        hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? (ctx->max_ndc + 3) / 4 : 0), ctx->ninst), dim3(256), 0, ctx->stream,
                            ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
                            ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_BFp, ctx->vb_on);
         HIPCHK(hipGetLastError());
@@ -4660,7 +4662,7 @@ void pint_host_free(void* p) {
 int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
+    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
                        ctx->d_dpars, ctx->d_lam, ctx->d_ic);
     HIPCHK(hipGetLastError());
     ctx->ic_valid = true;
