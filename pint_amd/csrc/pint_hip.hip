@@ -99,6 +99,7 @@ struct InstDev {
     long ddoff;
     long vgoff;  // k_gram_v DMX slot partials offset (nsplit * vns * (Kd+3))
     long vboff;  // k_gram_v binned DMX x Fourier partials offset (nsplit * GW * vns * 128)
+    long xwoff;  // k_solve_dmx -> k_cov_dmx export offset (X, W blocks and the scalings)
     int self;    // index of this instance in the batch
     int nrb;     // k_resid row blocks of this instance (RES_RB rows each)
     long rb0;    // first k_resid row block
@@ -2312,6 +2313,62 @@ constexpr int SD_MAXBLK = 76;  // S + U blocks (2 KiB each) that fit next to the
 
 __device__ __forceinline__ int ublk(int I, int k, int nbk, int nblkS) { return (nblkS + I * nbk + k) << 8; }
 
+// The timing covariance (ncol x ncol, original order) of the DMX-eliminated solve from X =
+// L_S^-1 (lower blocks of A) and W = X U (U blocks): C_dd = X^T X, C_xx = D^-1 + D^-1/2 W^T W
+// D^-1/2, C_xd = -D^-1/2 W^T X; block pairs w0, w0 + ws, ... (wave-uniform)
+__device__ __forceinline__ void cov_dmx_blocks(const double* A, const double* ind, const double* inx, const double* isd,
+                                               const double* Dn, const PsrDev& Pd, double* __restrict__ C, int ncol,
+                                               int red0, int ndc, int nbd, int nbk, int nblkS, int w0, int ws, int lane) {
+    const int nbt = (red0 + 15) >> 4;  // dense timing columns: compact 0..red0-1
+    const int nd_pairs = nbt * (nbt + 1) / 2, nx_pairs = nbk * (nbk + 1) / 2, ndx = nbk * nbt;
+    for (int p = w0; p < nd_pairs + nx_pairs + ndx; p += ws) {
+        double4_t acc = {0, 0, 0, 0};
+        int kind, bi, bj;
+        if (p < nd_pairs) {  // C_dd = X^T X
+            kind = 0;
+            tri_decode(p, bj, bi);
+            for (int k = bj; k < nbd; k++) bmma<true, true>(acc, A + lblk(k, bi), A + lblk(k, bj), lane, false);
+        } else if (p < nd_pairs + nx_pairs) {  // (W^T W)_ab
+            kind = 1;
+            tri_decode(p - nd_pairs, bj, bi);
+            for (int k = 0; k < nbd; k++)
+                bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + ublk(k, bj, nbk, nblkS), lane, false);
+        } else {  // (W^T X)_{a c}: DMX block bi x dense block bj
+            kind = 2;
+            const int q = p - nd_pairs - nx_pairs;
+            bi = q / nbt;
+            bj = q % nbt;
+            for (int k = bj; k < nbd; k++)
+                bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + lblk(k, bj), lane, false);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int ri = bi * 16 + (lane >> 4) + 4 * q, cj = bj * 16 + (lane & 15);
+            int oi, oj;
+            double v;
+            if (kind == 0) {
+                if (ri >= red0 || cj >= red0) continue;
+                oi = Pd.dorig[ri];
+                oj = Pd.dorig[cj];
+                v = acc[q] * (ind[ri] * ind[cj]);
+            } else if (kind == 1) {
+                if (ri >= ndc || cj >= ndc) continue;
+                oi = Pd.xorig[ri];
+                oj = Pd.xorig[cj];
+                v = acc[q] * (isd[ri] * isd[cj]) + (ri == cj ? 1.0 / Dn[ri] : 0.0);
+                v *= inx[ri] * inx[cj];
+            } else {
+                if (ri >= ndc || cj >= red0) continue;
+                oi = Pd.xorig[ri];
+                oj = Pd.dorig[cj];
+                v = -acc[q] * isd[ri] * (inx[ri] * ind[cj]);
+            }
+            C[(long)oi * ncol + oj] = v;
+            C[(long)oj * ncol + oi] = v;
+        }
+    }
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
@@ -2320,7 +2377,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        const double* __restrict__ DCS, double* __restrict__ dpars,
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                       int* __restrict__ status, int fuse_sigma, int refine) {
+                                                       int* __restrict__ status, int fuse_sigma, int refine,
+                                                       double* __restrict__ xw) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -2466,12 +2524,19 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sy += __shfl_xor(sy, 2, 64);
         if (sub == 0) yv[g] = sy;
     }
-    for (int kb = wave; kb < nbk; kb += NW) {
-        for (int Ib = nbd - 1; Ib >= 0; Ib--) {
+    {
+        // (block row Ib, block column kb) pairs in rounds of NW, block rows descending: a
+        // round's products have read their U blocks before its W blocks are stored, and a
+        // later round (smaller or equal Ib, other pairs) never reads a block stored earlier
+        const int npair = nbd * nbk;
+        for (int r = 0; r < npair; r += NW) {
+            const int p = r + wave, Ib = nbd - 1 - p / nbk, kb = p % nbk;
             double4_t acc = {0, 0, 0, 0};
-            for (int Jb = 0; Jb <= Ib; Jb++)
-                bmma<false, true>(acc, A + lblk(Ib, Jb), A + ublk(Jb, kb, nbk, nblkS), lane, false);
-            bstore(A + ublk(Ib, kb, nbk, nblkS), acc, lane, 1.0);
+            if (p < npair)
+                for (int Jb = 0; Jb <= Ib; Jb++)
+                    bmma<false, true>(acc, A + lblk(Ib, Jb), A + ublk(Jb, kb, nbk, nblkS), lane, false);
+            __syncthreads();
+            if (p < npair) bstore(A + ublk(Ib, kb, nbk, nblkS), acc, lane, 1.0);
         }
     }
     __syncthreads();
@@ -2601,59 +2666,49 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     bx_dot = block_sum<NW>(bx_dot, sh);
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
     TS(5);
-    // ---- covariance of the timing parameters (ncol x ncol, original order) ----
-    {
-        double* C = cov + (long)I.cvoff;
-        const int nbt = (red0 + 15) >> 4;  // dense timing columns: compact 0..red0-1
-        const int nd_pairs = nbt * (nbt + 1) / 2, nx_pairs = nbk * (nbk + 1) / 2, ndx = nbk * nbt;
-        for (int p = wave; p < nd_pairs + nx_pairs + ndx; p += NW) {
-            double4_t acc = {0, 0, 0, 0};
-            int kind, bi, bj;
-            if (p < nd_pairs) {  // C_dd = X^T X
-                kind = 0;
-                tri_decode(p, bj, bi);
-                for (int k = bj; k < nbd; k++) bmma<true, true>(acc, A + lblk(k, bi), A + lblk(k, bj), lane, false);
-            } else if (p < nd_pairs + nx_pairs) {  // (W^T W)_ab
-                kind = 1;
-                tri_decode(p - nd_pairs, bj, bi);
-                for (int k = 0; k < nbd; k++)
-                    bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + ublk(k, bj, nbk, nblkS), lane, false);
-            } else {  // (W^T X)_{a c}: DMX block bi x dense block bj
-                kind = 2;
-                const int q = p - nd_pairs - nx_pairs;
-                bi = q / nbt;
-                bj = q % nbt;
-                for (int k = bj; k < nbd; k++)
-                    bmma<true, true>(acc, A + ublk(k, bi, nbk, nblkS), A + lblk(k, bj), lane, false);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int ri = bi * 16 + (lane >> 4) + 4 * q, cj = bj * 16 + (lane & 15);
-                int oi, oj;
-                double v;
-                if (kind == 0) {
-                    if (ri >= red0 || cj >= red0) continue;
-                    oi = Pd.dorig[ri];
-                    oj = Pd.dorig[cj];
-                    v = acc[q] * (ind[ri] * ind[cj]);
-                } else if (kind == 1) {
-                    if (ri >= ndc || cj >= ndc) continue;
-                    oi = Pd.xorig[ri];
-                    oj = Pd.xorig[cj];
-                    v = acc[q] * (isd[ri] * isd[cj]) + (ri == cj ? 1.0 / Dn[ri] : 0.0);
-                    v *= inx[ri] * inx[cj];
-                } else {
-                    if (ri >= ndc || cj >= red0) continue;
-                    oi = Pd.xorig[ri];
-                    oj = Pd.dorig[cj];
-                    v = -acc[q] * isd[ri] * (inx[ri] * ind[cj]);
-                }
-                C[(long)oi * ncol + oj] = v;
-                C[(long)oj * ncol + oi] = v;
-            }
+    // ---- covariance of the timing parameters ----
+    if (xw) {  // deferred to k_cov_dmx (several workgroups per instance, at the read)
+        double* o = xw + I.xwoff;
+        const int na = (nblkS + nbd * nbk) * 256;
+        for (int e = tid; e < na; e += NW * 64) o[e] = A[e];
+        for (int e = tid; e < nbd * 16; e += NW * 64) o[na + e] = ind[e];
+        for (int e = tid; e < nbk * 16; e += NW * 64) {
+            o[na + nbd * 16 + e] = inx[e];
+            o[na + nbd * 16 + nbk * 16 + e] = isd[e];
+            o[na + nbd * 16 + 2 * nbk * 16 + e] = Dn[e];
         }
+        return;
     }
+    cov_dmx_blocks(A, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, ncol, red0, ndc, nbd, nbk, nblkS, wave, NW, lane);
     TS(6);
+}
+
+// k_cov_dmx: the covariance blocks of k_solve_dmx, COV_WG workgroups per instance, each
+// staging the instance's X, W and scalings (d_xw) in LDS; launched by pint_read_step when
+// the covariance is read (on the copy stream, off the fit step's critical path)
+constexpr int COV_WG = 3;
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                     const double* __restrict__ xw, int mode, double* __restrict__ cov) {
+    extern __shared__ double lds[];
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.dsplit) return;
+    const int ndc = Pd.ndc, red0 = Pd.red0c;
+    const int Kd = (mode == 0) ? red0 : Pd.Kd;
+    const int nbd = (Kd + 15) >> 4, nbk = (ndc + 15) >> 4, nblkS = nbd * (nbd + 1) / 2;
+    const int na = (nblkS + nbd * nbk) * 256, nv = na + (nbd + 3 * nbk) * 16;
+    const double* src = xw + I.xwoff;
+    for (int e = threadIdx.x; e < nv; e += NW * 64) lds[e] = src[e];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const double* ind = lds + na;
+    const double* inx = ind + nbd * 16;
+    const double* isd = inx + nbk * 16;
+    const double* Dn = isd + nbk * 16;
+    cov_dmx_blocks(lds, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, Pd.spec->ncol, red0, ndc, nbd, nbk, nblkS,
+                   blockIdx.y * NW + wave, gridDim.y * NW, lane);
 }
 
 // ---------------------------------------------------------------------------------
@@ -3290,6 +3345,11 @@ struct pint_ctx {
     double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
     double* d_BFp = nullptr;                    // k_gram_v binned DMX x Fourier partials (VB)
     int vb_on = 0;                              // the batch's vg instances use VB
+    double* d_xw = nullptr;     // k_solve_dmx's X, W and scalings for the deferred covariance
+    int cov_defer = 1;          // PINT_COV_DEFER: the DMX-eliminated covariance in k_cov_dmx
+    bool cov_pending = false;   // d_cov of the last solve not formed yet (k_cov_dmx at the read)
+    int cov_mode = 0;
+    size_t cov_lds = 0;
     bool ic_valid = false;  // per-instance constants (k_prep) current for the tables
     bool no_events = false; // PINT_NO_EVENTS=1: no per-kernel timing events (their cost)
     int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
@@ -3504,6 +3564,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
     ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
+    ctx->cov_defer = getenv("PINT_COV_DEFER") ? (atoi(getenv("PINT_COV_DEFER")) ? 1 : 0) : 1;
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
@@ -3537,7 +3598,8 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
-                   (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart};
+                   (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
+                   (void**)&ctx->d_xw};
     for (auto p : ps) dfree(*p);
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
@@ -3906,8 +3968,9 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         }
     }
     if (refresh_psrs(ctx)) return PINT_E_HIP;
-    long vgoff = 0, vboff = 0;
+    long vgoff = 0, vboff = 0, xwoff = 0;
     ctx->n_vg = 0;
+    ctx->cov_pending = false;
     ctx->vb_on = ctx->vbin;
     ctx->any_dmx_rows = false;
     for (int k = 0; k < ninst; k++) {
@@ -3932,6 +3995,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         I.ddoff = ddoff;
         I.vgoff = vgoff;
         I.vboff = vboff;
+        I.xwoff = xwoff;
         if (ph.dev.vg) {
             vgoff += (long)nsplit * ph.dev.vns * (ph.dev.Kd + 3);
             if (ph.dev.vb) vboff += (long)nsplit * GW * ph.dev.vns * 128;
@@ -3942,6 +4006,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         if (ph.dev.dsplit) {
             sdoff += (long)ph.dev.ndc * ph.dev.Kpd;
             ddoff += ph.dev.ndc;
+            const long nbd = (ph.dev.Kd + 15) / 16, nbk = (ph.dev.ndc + 15) / 16;
+            xwoff += (nbd * (nbd + 1) / 2 + nbd * nbk) * 256 + (nbd + 3 * nbk) * 16;
             if (ph.dev.ndc > max_ndc) max_ndc = ph.dev.ndc;
         }
         I.self = k;
@@ -4054,6 +4120,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     HIPCHK(cmalloc((void**)&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
     HIPCHK(cmalloc((void**)&ctx->d_BFp, sizeof(double) * std::max<long>(1, vboff)));
+    if (xwoff > 0 && xwoff <= (1L << 28)) HIPCHK(cmalloc((void**)&ctx->d_xw, sizeof(double) * xwoff));
     HIPCHK(cmalloc((void**)&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_blk_inst, sizeof(int) * bi.size()));
@@ -4542,13 +4609,18 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
         ctx->copy_pending = false;
     }
+    ctx->cov_pending = false;
     if (skip) {
+        double* xw = (ctx->cov_defer && ctx->d_xw) ? ctx->d_xw : nullptr;
         hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
                            fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
                            ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                           fuse_sigma, ctx->refine);
+                           fuse_sigma, ctx->refine, xw);
         HIPCHK(hipGetLastError());
+        ctx->cov_pending = xw != nullptr;
+        ctx->cov_mode = mode;
+        ctx->cov_lds = lds_x;
     }
     const int nbx = std::max((Ks + 15) / 16, (Kn + 15) / 16);
     if (skip && Ks == 0) {
@@ -4613,6 +4685,7 @@ int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* nd
     const size_t lds = sizeof(double) * (4 * (size_t)maxK + maxK + 2);
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
     HIPCHK(hipMemcpyAsync(ctx->d_lam, threshold, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
+    ctx->cov_pending = false;  // k_eig writes every instance's covariance
     hipLaunchKernelGGL(k_eig, dim3(ctx->ninst), dim3(EIG_T), lds, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
                        ctx->d_colsq, ctx->nsplit, mode, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_lam,
                        ctx->d_eigw, wstride, ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_ndeg,
@@ -4636,6 +4709,12 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
     // follow; the caller's buffers (pinned: pint_host_alloc) are valid after pint_check().
     hipStream_t st = ctx->lazy ? ctx->cstream : ctx->stream;
     if (ctx->lazy) HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_solved, 0));
+    if (cov && ctx->cov_pending) {  // the DMX-eliminated solve's covariance blocks
+        hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ctx->ninst, COV_WG), dim3(1024), ctx->cov_lds, st, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_xw, ctx->cov_mode, ctx->d_cov);
+        HIPCHK(hipGetLastError());
+        ctx->cov_pending = false;
+    }
     if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
     if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
     if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, hipMemcpyDeviceToHost, st));
