@@ -156,7 +156,8 @@ def test_gls_fit(name):
         # FP64 normal-equation solves agree to ~cond*eps: J0740's normalised normal matrix
         # has cond 7e12 (B1855 with the dense ECORR block 1e16, 3e11 after elimination),
         # so its weakest-determined errors agree with the reference's LAPACK to ~1e-3
-        etol = {"j0740": 5e-3, "b1855": 5e-4}.get(name, 1e-5)
+        # (measured on MI355X, scripts/diag/downhill_margin.py: J0740 JUMP1 1.3e-3, B1855 T0 1.2e-4)
+        etol = {"j0740": 3e-3, "b1855": 5e-4}.get(name, 1e-5)
         assert abs(f.model[p].uncertainty / s - 1) < etol, (p, f.model[p].uncertainty / s - 1)
     assert worst < 1e-3, worst
     assert abs(c2 / meta["gls_chi2"] - 1) < 5e-6
@@ -176,10 +177,15 @@ def test_downhill_gls(name):
         status = type(e).__name__
     assert status == meta["down_status"]
     assert abs(f.resids.chi2 / meta["down_chi2"] - 1) < 5e-6
+    # measured on MI355X (scripts/diag/downhill_margin.py): <= 2.5e-5 sigma, except pta_dd's
+    # SINI at 1.3e-2 sigma: M2 and SINI are nearly degenerate there (the Shapiro pair), so
+    # the accepted iterate's SINI moves along that valley by the rounding of each trial's
+    # chi2 (see test_oracle_golden.test_downhill_gls)
+    tol = 5e-2 if name == "pta_dd" else 1e-3
     for p in meta["down_params"]:
         s = meta["down_errors"][p]
         d = float((np.longdouble(f.model[p].value) - ref_value(meta, "down_params", p)) / np.longdouble(s))
-        assert abs(d) < 5e-2, (p, d)  # see test_oracle_golden.test_downhill_gls
+        assert abs(d) < tol, (p, d)
 
 
 def test_downhill_wls_ngc():
