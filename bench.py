@@ -40,8 +40,8 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)  # 0.5 ms each: steady state, not the first steps
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--npsr", type=int, default=68)
     ap.add_argument("--ntoas", type=int, default=10000)
     ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")

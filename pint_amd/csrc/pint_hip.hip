@@ -3346,7 +3346,8 @@ struct pint_ctx {
     double* d_BFp = nullptr;                    // k_gram_v binned DMX x Fourier partials (VB)
     int vb_on = 0;                              // the batch's vg instances use VB
     double* d_xw = nullptr;     // k_solve_dmx's X, W and scalings for the deferred covariance
-    int cov_defer = 1;          // PINT_COV_DEFER: the DMX-eliminated covariance in k_cov_dmx
+    int cov_defer = 1;          // PINT_COV_DEFER: the DMX-eliminated covariance in k_cov_dmx (0 never,
+                                // 1 batches of >= 16 instances, 2 always)
     bool cov_pending = false;   // d_cov of the last solve not formed yet (k_cov_dmx at the read)
     int cov_mode = 0;
     size_t cov_lds = 0;
@@ -3564,7 +3565,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
     ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
-    ctx->cov_defer = getenv("PINT_COV_DEFER") ? (atoi(getenv("PINT_COV_DEFER")) ? 1 : 0) : 1;
+    ctx->cov_defer = getenv("PINT_COV_DEFER") ? atoi(getenv("PINT_COV_DEFER")) : 1;  // 0 off, 1 batches, 2 always
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
@@ -4611,7 +4612,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     ctx->cov_pending = false;
     if (skip) {
-        double* xw = (ctx->cov_defer && ctx->d_xw) ? ctx->d_xw : nullptr;
+        // deferred covariance for batches (a single fit would pay a launch on its read instead)
+        double* xw = (ctx->d_xw && (ctx->cov_defer == 2 || (ctx->cov_defer == 1 && ctx->ninst >= 16))) ? ctx->d_xw : nullptr;
         hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
                            fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,

@@ -740,3 +740,22 @@ def test_pldm_noise_resids():
         err = np.max(np.abs(f.resids.noise_resids[comp] - v)) / np.max(np.abs(v))
         # end to end, the realisations carry the step's conditioning (cf. TOL_NOISE, test_gpu_stage.py)
         assert err < 1e-4, (comp, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pta_dd", "j0740"])
+def test_deferred_covariance_matches_in_kernel(name, monkeypatch):
+    """k_cov_dmx (the covariance blocks read after the DMX-eliminated solve, PINT_COV_DEFER=2
+    forces it for a single fit) gives the in-kernel covariance of k_solve_dmx bit for bit
+    (the same block products in the same order)."""
+    from pint_amd import GLSFitter
+    covs = []
+    for mode in ("0", "2"):
+        monkeypatch.setenv("PINT_COV_DEFER", mode)
+        model, toas, z, meta = load(name)
+        f = GLSFitter(toas, model)
+        f.fit_toas(maxiter=1)
+        covs.append(np.asarray(f.parameter_covariance_matrix.matrix, dtype=np.float64))
+    assert covs[0].shape == covs[1].shape
+    assert np.all(np.isfinite(covs[1]))
+    assert np.array_equal(covs[0], covs[1]), np.max(np.abs(covs[0] - covs[1]))
