@@ -265,6 +265,11 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * fitter.py:2465-2637: design matrix [M_toa | F; M_dm | 0], residuals [r; pp_dm - DM]);
  * default 0. */
 #define PINT_OPT_WBFIT 6
+/* PINT_OPT_COV_DEFER (default 1, env PINT_COV_DEFER): the covariance of the DMX-eliminated
+ * solve is formed by pint_read_step (k_cov_dmx, several workgroups per instance, on the copy
+ * stream) instead of inside the solve: 0 never, 1 for batches of >= 16 instances, 2 always.
+ * Same values bit for bit; takes effect at the next pint_fit_step. */
+#define PINT_OPT_COV_DEFER 7
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

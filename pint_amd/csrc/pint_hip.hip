@@ -4794,6 +4794,11 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_VGRAM) { ctx->vgram = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_VBIN) { ctx->vbin = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_WBFIT) { ctx->wbfit = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_COV_DEFER) {
+        if (value < 0 || value > 2) return PINT_E_INVALID;
+        ctx->cov_defer = value;
+        return PINT_OK;
+    }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {

@@ -618,6 +618,11 @@ class Session:
         """Wideband DM rows in the fit steps (PINT_OPT_WBFIT, WidebandTOAFitter)."""
         self._check(self.L.pint_set_option(self.ctx, 6, 1 if on else 0))
 
+    def set_cov_defer(self, mode=1):
+        """Covariance of the DMX-eliminated solve formed at the read (PINT_OPT_COV_DEFER: 0
+        never, 1 batches of >= 16 instances, 2 always)."""
+        self._check(self.L.pint_set_option(self.ctx, 7, int(mode)))
+
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))
