@@ -10,9 +10,12 @@ to the host on a copy stream, overlapped with the kernels.
 
 Sharding (pint_amd.pta): the pulsars are assigned to ranks by
 longest-processing-time on the fit cost N K^2 + 8 N P; there is no data-path collective.
-* value ("scaling": "weak"): a PTA of 68 x N pulsars (pulsar i uses seed i) over N ranks,
-  ~68 pulsars per GPU; value = 68 N / max-over-ranks step time.
-* pta_strong (N > 1): the configured 68-pulsar PTA itself split over the N ranks.
+* value ("scaling": "strong"): the configured 68-pulsar PTA split over the N ranks
+  (north_star's target); value = 68 / max-over-ranks step time.
+* pta_weak (N > 1): a PTA of 68 x N pulsars (pulsar i uses seed i) over N ranks, ~68 per GPU.
+
+The step includes the noise realisations GLSFitter.fit_toas computes when full_cov=False
+(fitter.py:2269-2282): k_noise_red after the solve, the per-pulsar arrays copied to the host.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -46,7 +49,7 @@ def main():
     ap.add_argument("--ntoas", type=int, default=10000)
     ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--strong", type=int, default=1, help="also time the 68-pulsar PTA split over the ranks (N > 1)")
+    ap.add_argument("--weak", type=int, default=1, help="also time a 68 x N pulsar PTA over the N ranks (N > 1)")
     ap.add_argument("--j0740", type=int, default=256,
                     help="(M2, SINI) grid side of the C3/C4 J0740 legs (0 = skip)")
     args = ap.parse_args()
@@ -78,41 +81,45 @@ def main():
     from pint_amd import simulation as sim
     from pint_amd.pta import fit_cost, lpt_shard
 
-    # ---- weak scaling: a 68 x N pulsar PTA, LPT-sharded over the N ranks ----
-    ntot = args.npsr * world
-    models = [sim.pta_model(i) for i in range(ntot)]
+    # ---- value ("scaling": "strong"): the configured 68-pulsar PTA, LPT-sharded over the N
+    # ranks (north_star: the 68-pulsar x 10k-TOA PTA at 1/2/4/8 GPUs) ----
+    models = [sim.pta_model(i) for i in range(args.npsr)]
     costs = [fit_cost(m, n=args.ntoas) for m in models]
     shards = lpt_shard(costs, world)
     leg = pta_leg(shards[rank], models, args, rank, barrier, max_over_ranks, profile=True)
-    fits_per_s = ntot / (leg["dt"] / args.steps)
-    strong = None
-    if world > 1 and args.strong:
-        sh2 = lpt_shard(costs[:args.npsr], world)
-        leg2 = pta_leg(sh2[rank], models, args, rank, barrier, max_over_ranks, profile=False)
-        strong = {"metric": "GLS fits/sec, the 68-pulsar PTA split over the ranks (strong scaling)",
-                  "value": round(args.npsr / (leg2["dt"] / args.steps), 3), "unit": "fits/s",
-                  "ms_per_step": round(leg2["dt"] / args.steps * 1e3, 4),
-                  "pulsars_per_rank": [len(s) for s in sh2]}
+    fits_per_s = args.npsr / (leg["dt"] / args.steps)
+    weak = None
+    if world > 1 and args.weak:
+        # extra: weak scaling, a 68 x N pulsar PTA (pulsar i uses seed i), ~68 per rank
+        ntot = args.npsr * world
+        models_w = models + [sim.pta_model(i) for i in range(args.npsr, ntot)]
+        costs_w = costs + [fit_cost(m, n=args.ntoas) for m in models_w[args.npsr:]]
+        sh2 = lpt_shard(costs_w, world)
+        leg2 = pta_leg(sh2[rank], models_w, args, rank, barrier, max_over_ranks, profile=False)
+        weak = {"metric": f"GLS fits/sec, a {ntot}-pulsar PTA over {world} ranks (~{args.npsr} per GPU, weak scaling)",
+                "value": round(ntot / (leg2["dt"] / args.steps), 3), "unit": "fits/s",
+                "ms_per_step": round(leg2["dt"] / args.steps * 1e3, 4),
+                "pulsars_per_rank": [len(s) for s in sh2]}
 
     roof = leg["roofline"]
     grid = grid_leg(args.grid, dist, barrier, max_over_ranks) if args.grid > 0 else None
     j0740 = j0740_legs(args.j0740, dist, barrier, max_over_ranks) if args.j0740 > 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu = cpu_baseline(leg["items"][:16])
+        cpu = cpu_baseline(leg["items"])
 
     if rank == 0:
         out = {"metric": "GLS fits/sec, 68-PSR x 10k-TOA synthetic PTA (whole node)", "value": round(fits_per_s, 3),
                "unit": "fits/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(leg["dt"] / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+               "ms_per_step": round(leg["dt"] / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
                "vs_baseline": None, "dtype": "f64+dd",
                "data": "synthetic (make_fake_toas-style PTA, TOAs generated and zeroed on the GPU)",
-               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter maxiter=1 per GPU "
-                                      f"(a {ntot}-pulsar PTA, LPT-sharded over {world} rank(s))",
-                          "npsr": args.npsr, "npsr_total": ntot, "ntoas": args.ntoas,
+               "config": {"workload": f"pta{args.npsr}x{args.ntoas // 1000}k GLSFitter.fit_toas(maxiter=1) incl. noise "
+                                      f"realisations (the {args.npsr}-pulsar PTA, LPT-sharded over {world} rank(s))",
+                          "npsr": args.npsr, "ntoas": args.ntoas,
                           "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
                           "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
-               "roofline": roof, "pta_strong": strong, "grid": grid, "j0740": j0740, "cpu_baseline": cpu}
+               "roofline": roof, "pta_weak": weak, "grid": grid, "j0740": j0740, "cpu_baseline": cpu}
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
@@ -139,10 +146,11 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
         s.eval(want_M=Session.FIT)
         s.fit_step(1)
         out = s.read_step()    # steps, errors, timing covariance -> host (fit outputs)
+        nz = s.noise_resids()  # noise realisations -> host (fitter.py:2269-2282, full_cov=False)
         s.apply_step(ones)
         s.eval(want_M=False)
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
-        return out, c2
+        return out, nz, c2
 
     s.set_timing_mask(1 << SLOT_GRAM)  # timed region: HIP events on the Gram dispatches only
 
@@ -238,12 +246,15 @@ def roofline(s, lays, kt_gram, step, args):
     roof = {"kernel": "k_gram_v", "bound": "mfma",
             "achieved": round(ach, 3) if ach else None, "peak": MI355X_FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / MI355X_FP64_MFMA_PEAK_TFLOPS, 4) if ach else None,
-            "traffic": pmc_value("pmc_r02.json", "k_gram_v", "hbm_bytes", args),
+            "traffic": pmc_value("pmc", "k_gram_v", "hbm_bytes", args)[0],
+            "traffic_source": pmc_value("pmc", "k_gram_v", "hbm_bytes", args)[1],
             "alg_gflop_per_launch": round(alg / 1e9, 4), "exec_gflop_per_launch": round(exe / 1e9, 4),
             "exec_tflops": round(exe / (kt_gram * 1e-3) / 1e12, 3) if kt_gram > 0 else None,
             "exec_frac": round(exe / (kt_gram * 1e-3) / 1e12 / MI355X_FP64_MFMA_PEAK_TFLOPS, 4) if kt_gram > 0 else None,
-            "pmc_exec_gflop_per_launch": pmc_value("pmc_gram_r02.json", "k_gram_v", "mfma_gflop", args),
-            "pmc_mfma_busy_frac": pmc_value("pmc_gram_r02.json", "k_gram_v", "mfma_busy_frac", args),
+            "pmc_exec_gflop_per_launch": pmc_value("pmc_gram", "k_gram_v", "mfma_gflop", args)[0],
+            "pmc_mfma_busy_frac": pmc_value("pmc_gram", "k_gram_v", "mfma_busy_frac", args)[0],
+            "pmc_valu_per_mfma": pmc_value("pmc_gram", "k_gram_v", "valu_per_mfma", args)[0],
+            "pmc_source": pmc_value("pmc_gram", "k_gram_v", "mfma_gflop", args)[1],
             "kernel_ms": {n: round(v, 4) for n, v in kms.items()},
             "kernel_ms_source": ("k_gram: HIP events on its dispatches in the timed region; others: a separate "
                                  f"instrumented pass of {nprof} steps (gram_span = Gram + reduction)")}
@@ -252,7 +263,7 @@ def roofline(s, lays, kt_gram, step, args):
                           for n, b in nbytes.items() if kms.get(n, 0) > 0}
     gram_equiv = float(sum(2.0 * l.n * (l.K + 1.0) ** 2 for l in lays))
     roof["gram_full_equiv_tflops"] = round(gram_equiv / (kt_gram * 1e-3) / 1e12, 2) if kt_gram > 0 else None
-    peaks = load_json("peaks_r02.json")
+    peaks = load_json("peaks_r03.json") or load_json("peaks_r02.json")
     if peaks:
         roof["measured_peaks"] = peaks
     return roof
@@ -266,15 +277,25 @@ def load_json(name):
     return None
 
 
-def pmc_value(fname, kernel, key, args):
-    """A per-launch PMC figure of `kernel` from the committed rocprofv3 summary of this same
-    bench workload (profiles/; HBM bytes = FETCH_SIZE x2 on gfx950 + WRITE_SIZE per
-    MI355X_MICROARCH.md)."""
-    d = load_json(fname)
-    if not d or d.get("workload") != f"pta{args.npsr}x{args.ntoas}":
-        return None
-    k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k.get(key)
+PROFILE_ROUNDS = ("r03", "r02")  # newest first: the committed PMC summaries of this workload
+
+
+def pmc_value(stem, kernel, key, args):
+    """A per-launch PMC figure of `kernel` from the newest committed rocprofv3 summary
+    (profiles/<stem>_rNN.json) of this same bench workload; HBM bytes = FETCH_SIZE x2 on
+    gfx950 + WRITE_SIZE per MI355X_MICROARCH.md.  Returns (value, file) or (None, None)."""
+    want = f"pta{args.npsr}x{args.ntoas // 1000}k"
+    for r in PROFILE_ROUNDS:
+        fname = f"{stem}_{r}.json"
+        d = load_json(fname)
+        if not d:
+            continue
+        if d.get("workload_key", d.get("workload", "").split(" ")[0]) != want:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k is not None and k.get(key) is not None:
+            return k.get(key), fname
+    return None, None
 
 
 def grid_leg(side, dist, barrier, max_over_ranks):
@@ -380,7 +401,7 @@ def _cpu_fits(args):
     """Worker: GLS fits (maxiter=1 + post-fit chi2) of item k for `budget` seconds."""
     k, budget = args
     import pint_oracle as O
-    model, toas = _CPU_ITEMS[k]
+    model, toas = _CPU_ITEMS[k % len(_CPU_ITEMS)]
     t0 = time.perf_counter()
     n = 0
     while True:
@@ -405,9 +426,38 @@ def _cpu_grid(args):
             return n
 
 
+def host_cores():
+    """The job's CPU share: the cgroup v2 quota (cpu.max "quota period") when one is set,
+    capped by the affinity mask; otherwise the affinity mask.  Returns (cores, note)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    note = f"affinity {aff}, os.cpu_count {os.cpu_count()}"
+    for f in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(f).read().split()
+        except OSError:
+            continue
+        if f.endswith("cpu.max"):
+            if txt and txt[0] != "max":
+                q = int(txt[0]) / int(txt[1])
+                note += f", cgroup cpu.max {txt[0]} {txt[1]} = {q:g} cores"
+                return max(1, min(aff, int(q + 0.5))), note
+            note += ", cgroup cpu.max: no quota"
+        else:
+            q = int(txt[0])
+            if q > 0:
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                note += f", cfs quota {q}/{per}"
+                return max(1, min(aff, int(q / per + 0.5))), note
+        break
+    return aff, note
+
+
 def cpu_baseline(items):
     """The oracle (oracle/pint_oracle.py, numpy longdouble) timed on this host on bounded
-    samples, one process per core of the job's CPU share (at most 16 on the GPU box):
+    samples, one process per core of the job's CPU share (host_cores: cgroup quota, else affinity):
     GLS fits of the PTA's own 10k-TOA pulsars, and WLS grid points of NGC6440E -- the GPU
     workloads' units.  The reference's own CPU rates (measured in the build container; the
     reference cannot travel to the GPU box) are attached from bench/reference_cpu.json."""
@@ -417,11 +467,8 @@ def cpu_baseline(items):
         import pint_oracle as O  # noqa: F401
     except Exception as e:  # oracle missing: report, never fall back
         return {"value": None, "error": repr(e)}
-    try:
-        ncores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncores = os.cpu_count() or 1
-    nproc = max(1, min(16, ncores, len(items)))
+    ncores, quota_note = host_cores()
+    nproc = max(1, ncores)
     ctx = mp.get_context("spawn")  # never fork a process that holds a GPU context
     # one BLAS/OpenMP thread per worker (the box exports OMP_NUM_THREADS=16: 16 workers x 16
     # threads would oversubscribe the job's cores); the spawned workers inherit this
@@ -429,7 +476,7 @@ def cpu_baseline(items):
     for k in saved:
         os.environ[k] = "1"
     try:
-        return _cpu_baseline_pools(items, ctx, nproc, ncores)
+        return _cpu_baseline_pools(items, ctx, nproc, quota_note)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -438,7 +485,7 @@ def cpu_baseline(items):
                 os.environ[k] = v
 
 
-def _cpu_baseline_pools(items, ctx, nproc, ncores):
+def _cpu_baseline_pools(items, ctx, nproc, quota_note):
     budget = 10.0
     with ctx.Pool(nproc, initializer=_cpu_init, initargs=(items[:nproc], ROOT)) as pool:
         t0 = time.perf_counter()
@@ -446,9 +493,9 @@ def _cpu_baseline_pools(items, ctx, nproc, ncores):
         dt = time.perf_counter() - t0
     fits = sum(counts)
     out = {"value": round(fits / dt, 4), "unit": "fits/s", "cores": nproc, "kind": "port",
-           "sample": f"{fits} GLS fits (maxiter=1 + post-fit GLS chi2) of {nproc} of the PTA's 10k-TOA pulsars, "
+           "sample": f"{fits} GLS fits (maxiter=1 + post-fit GLS chi2) of {min(nproc, len(items))} of the PTA's 10k-TOA pulsars, "
                      f"one oracle process per core (numpy longdouble, 1 BLAS thread each), {dt:.1f} s wall; "
-                     f"host cpu_count {os.cpu_count()}, job CPU share {ncores}"}
+                     f"job CPU share: {quota_note}"}
     # grid points: NGC6440E (F0, F1) WLS fits, the grid leg's unit
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from golden_util import load

@@ -38,7 +38,7 @@ def j0740_model():
     return get_model(io.StringIO("".join(lines)))
 
 
-def pta_par(seed, binary):
+def pta_par(seed, binary, ndmx=20):
     rng = np.random.default_rng(1000 + seed)
     ra = rng.uniform(0, 2 * np.pi)
     dec = np.arcsin(rng.uniform(-1, 1))
@@ -75,7 +75,6 @@ TNRedAmp {rng.uniform(-14.5, -13.5):.4f}
 TNRedGam {rng.uniform(3, 5):.4f}
 TNRedC 30
 """
-    ndmx = 20
     edges = np.linspace(53000, 56652.01, ndmx + 1)
     par += "DMX 14.0\n"
     for i in range(ndmx):

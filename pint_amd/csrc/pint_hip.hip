@@ -2512,6 +2512,12 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     TS(2);
     if (!blk_cholinv<NW>(A, nbd, wave, lane, &sflag)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
+        if (xw) {  // no X/W to export: the deferred covariance of this instance comes out NaN,
+                   // not from the previous step's (or uninitialised) export
+            double* o = xw + I.xwoff + (nblkS + nbd * nbk) * 256;
+            for (int e = tid; e < nbd * 16; e += NW * 64) o[e] = __builtin_nan("");
+            for (int e = tid; e < 3 * nbk * 16; e += NW * 64) o[nbd * 16 + e] = __builtin_nan("");
+        }
         return;
     }
     TS(3);
@@ -3144,7 +3150,17 @@ __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ ps
     const double* a = dpars + I.coff + S.ncol;
     double v = 0.0;
     const int k0 = dm ? S.dmn0 : 0, k1 = dm ? S.nred : S.dmn0;
-    if (k1 > k0) {
+    if (!dm && k1 > 0) {
+        // PLRedNoise block: harmonics 1..dmn0 of f_1 = red_freq[0] (get_rednoise_freqs is
+        // linspace(1/T, nmodes/T)), by rotations of the row's e^{i theta} (k_redbase) instead
+        // of a double-double reduction and a sincos per harmonic
+        const double c1 = Pd.red_cs[4 * i], s1 = Pd.red_cs[4 * i + 1];
+        double cs = c1, sn = s1;
+        for (int k = 0; k < k1; k++) {
+            v += a[2 * k] * sn + a[2 * k + 1] * cs;
+            rot(cs, sn, c1, s1);
+        }
+    } else if (k1 > k0) {
         const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
         for (int k = k0; k < k1; k++) {
             const dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
@@ -3415,6 +3431,9 @@ struct pint_ctx {
     float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
     double* d_nz = nullptr;  // pint_noise_lnlike scratch (parameters, epoch sums, outputs)
     size_t nz_cap = 0;
+    double* d_noise = nullptr;  // pint_noise_resids: red and ECORR realisations (2 tot_out)
+    long noise_cap = 0;
+    hipEvent_t ev_noise = nullptr;
 };
 
 // Per-instance buffers (eval rows, design matrices, Gram partials: tens of GB for a large
@@ -3558,6 +3577,7 @@ pint_ctx* pint_ctx_create(int device) {
     hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
     hipEventCreateWithFlags(&ctx->ev_solved, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_copied, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_noise, hipEventDisableTiming);
     // PINT_SERIAL=1 (profiling aid): side-stream kernels run on the main stream, so
     // rocprof's per-kernel durations are not inflated by concurrent kernels
     if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
@@ -3600,8 +3620,9 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
-                   (void**)&ctx->d_xw};
+                   (void**)&ctx->d_xw, (void**)&ctx->d_noise};
     for (auto p : ps) dfree(*p);
+    ctx->noise_cap = 0;
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
     ctx->graph_exec = nullptr;
@@ -3634,6 +3655,7 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
     if (ctx->ev_solved) hipEventDestroy(ctx->ev_solved);
     if (ctx->ev_copied) hipEventDestroy(ctx->ev_copied);
+    if (ctx->ev_noise) hipEventDestroy(ctx->ev_noise);
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     if (ctx->ev_gram) hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_sigma) hipEventDestroy(ctx->ev_sigma);
@@ -4404,6 +4426,20 @@ int pint_read_designmatrix(pint_ctx* ctx, double* M) {
 int pint_fit_step(pint_ctx* ctx, int mode) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (ctx->wbfit) {
+        // k_wb_gram carries at most WB_MAXC free DM-type columns (DM Taylor terms + DMJUMPs):
+        // refuse more instead of leaving the extra columns without their DM rows
+        for (auto& I : ctx->inst) {
+            const pint_spec_t& sp = ctx->psrs[I.psr].spec;
+            if (!ctx->psrs[I.psr].dev.wb) continue;
+            int m = 0;
+            for (int c = 0; c < sp.ncol; c++) m += (sp.col_kind[c] == PINT_COL_DM || sp.col_kind[c] == PINT_COL_ZERO);
+            if (m > WB_MAXC) {
+                ctx->err = "wideband fit: more than 8 free DM-type columns (DM Taylor terms + DMJUMPs)";
+                return PINT_E_INVALID;
+            }
+        }
+    }
     const int nparts = ctx->nsplit + ((mode == 1 && ctx->max_nep > 0) ? 1 : 0);
     if (ctx->sigma_pending) {  // the previous k_sigma reads the Gram buffer this step overwrites
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
@@ -4986,35 +5022,50 @@ int pint_inst_status(pint_ctx* ctx, int32_t* out) {
 }
 
 // Noise realisations of the last pint_fit_step(mode=1): red[n_i], ecorr[n_i] per instance
-// (either pointer may be NULL).
+// (either pointer may be NULL).  The kernels run on the main stream right after the solve
+// (they read its dpars and ECORR epoch sums) into a device buffer kept by the context.
+// Lazy mode (GLSFitter.fit_toas's noise_resids inside a pipelined step): the device->host
+// copies go to the copy stream after them, into the caller's pinned buffers, valid after
+// pint_check / pint_check_step; the next solve waits for them (copy_pending).
 int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
-    double* d = nullptr;
-    HIPCHK(hipMalloc(&d, sizeof(double) * std::max<long>(1, ctx->tot_out)));
+    const long need = 2 * std::max<long>(1, ctx->tot_out);
+    if (need > ctx->noise_cap) {
+        if (ctx->capturing) { ctx->err = "pint_noise_resids: first call inside a graph capture"; return PINT_E_INVALID; }
+        dfree((void*&)ctx->d_noise);
+        HIPCHK(cmalloc((void**)&ctx->d_noise, sizeof(double) * need));
+        ctx->noise_cap = need;
+    }
+    double* dr = ctx->d_noise;
+    double* de = ctx->d_noise + std::max<long>(1, ctx->tot_out);
     int maxn = 1;
     for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
-    int rc = PINT_OK;
-    if (red) {
+    if (red)
         hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
-                           ctx->d_inst, ctx->d_dpars, d, 0, ctx->d_dfac);
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(red, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-            rc = PINT_E_HIP;
-    }
-    if (ecorr && rc == PINT_OK) {
-        hipMemsetAsync(d, 0, sizeof(double) * ctx->tot_out, ctx->stream);
+                           ctx->d_inst, ctx->d_dpars, dr, 0, ctx->d_dfac);
+    if (ecorr) {
+        HIPCHK(hipMemsetAsync(de, 0, sizeof(double) * ctx->tot_out, ctx->stream));
         if (ctx->max_nep > 0)
             hipLaunchKernelGGL(k_noise_ecorr, dim3(ctx->max_nep, ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs,
-                               ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, d);
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(ecorr, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-            rc = PINT_E_HIP;
+                               ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, de);
     }
-    hipStreamSynchronize(ctx->stream);
-    hipFree(d);
-    if (rc) ctx->err = "pint_noise_resids: HIP error";
-    return rc;
+    if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids: launch failed"; return PINT_E_HIP; }
+    hipStream_t st = ctx->stream;
+    if (ctx->lazy) {
+        HIPCHK(hipEventRecord(ctx->ev_noise, ctx->stream));
+        HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_noise, 0));
+        st = ctx->cstream;
+    }
+    if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
+    if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
+    if (ctx->lazy) {
+        HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
+        ctx->copy_pending = true;
+        return PINT_OK;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return PINT_OK;
 }
 
 int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {

@@ -736,9 +736,33 @@ class Session:
         """Noise realisations of the last GLS fit_step: per instance {component: n-array}
         with the reference's component names (fitter.py:2270-2282, noise_model_dimensions)."""
         n = [l.n for l in self.inst_layout]
-        red = np.empty(sum(n))
-        ec = np.empty(sum(n))
+        anyred = any(l.spec.dmn0 > 0 for l in self.inst_layout)
+        anyec = any("EcorrNoise" in l.model.components for l in self.inst_layout)
+        if self.lazy and any(l.spec.dmn0 < l.nred for l in self.inst_layout):
+            raise NotImplementedError("lazy noise_resids: PLDMNoise realisations need a synchronous session")
+        if self.lazy:
+            # enqueued (kernels after the solve, copies on the copy stream into pinned
+            # buffers): the arrays handed out are complete after check()/check_step()
+            red = self._pin("noise_red", sum(n)) if anyred else None
+            ec = self._pin("noise_ec", sum(n)) if anyec else None
+        else:
+            red = np.empty(sum(n)) if anyred else None
+            ec = np.empty(sum(n)) if anyec else None
         self._check(self.L.pint_noise_resids(self.ctx, L.ptr(red), L.ptr(ec)))
+        if self.lazy:
+            out = []
+            o = 0
+            for lay, k in zip(self.inst_layout, n):
+                d = {}
+                if anyec and "EcorrNoise" in lay.model.components:
+                    d["ecorr_noise"] = ec[o:o + k]
+                if anyred and lay.spec.dmn0 > 0:
+                    d["pl_red_noise"] = red[o:o + k]
+                out.append(d)
+                o += k
+            return out
+        red = red if red is not None else np.zeros(sum(n))
+        ec = ec if ec is not None else np.zeros(sum(n))
         anydm = any(l.spec.dmn0 < l.nred for l in self.inst_layout)
         dm = np.zeros(sum(n))
         if anydm:

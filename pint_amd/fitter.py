@@ -17,6 +17,7 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Session, build_layout, pack_table, unpack_table
+from .pint_matrix import CorrelationMatrix, CovarianceMatrix  # noqa: F401  (re-exported)
 
 
 class ConvergenceFailure(ValueError):
@@ -44,16 +45,6 @@ class DegeneracyWarning(UserWarning):
     pass
 
 
-class CovarianceMatrix:
-    def __init__(self, matrix, labels):
-        self.matrix = np.asarray(matrix)
-        self.labels = list(labels)
-
-    def get_label_matrix(self, labels):
-        idx = [self.labels.index(l) for l in labels]
-        return self.matrix[np.ix_(idx, idx)]
-
-
 class FitResult:
     """Per-instance fit outcome of a BatchFit."""
 
@@ -65,6 +56,8 @@ class FitResult:
         self.status = "ok"
         self.noise_coeffs = None
         self.noise_resids = {}
+        self.fac = None     # the design-matrix normalisation of the step (Fitter.fac)
+        self.step = None    # the parameter step, timing columns (par units)
 
 
 class BatchOutcome:
@@ -104,7 +97,7 @@ class BatchFit:
 
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
                  layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None,
-                 wideband=False):
+                 wideband=False, want_fac=False):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
         are bare parameter tables of already-uploaded pulsars, e.g. grid points).
 
@@ -114,6 +107,7 @@ class BatchFit:
         (GLSFitter) or "glsstate" (GLSState, the downhill GLS fitter)."""
         self.items = list(items) if items is not None else None
         self.mode = mode
+        self.want_fac = bool(want_fac)  # read the step's normalisation back (Fitter.fac)
         self.threshold = threshold
         self.degeneracy_style = degeneracy_style or mode
         self.degenerate = None  # per instance: dropped directions of the last SVD-path step
@@ -265,12 +259,35 @@ class BatchFit:
             res.errors = er[d][:nc].copy()
             res.cov = cov[d].copy()
             res.noise_coeffs = dp[d][nc:lay.K].copy()
+            res.step = dp[d][:nc].copy()
             res.labels = list(lay.columns)
             if self.items is not None:
                 m = self.items[k][0]
                 for j, name in enumerate(lay.columns):
                     if name != "Offset":
                         m[name].uncertainty = float(res.errors[j])
+
+    def _fac_into(self, results):
+        """The normalisation of the last step's design matrix per instance (the reference's
+        ``fac`` / ``norm``, utils.py:2879 normalize_designmatrix, zero norm -> 1): WLS, the
+        column norms of the whitened M (fitter.py:1320-1343); GLS, the column norms of
+        [M | noise bases] (fitter.py:2164-2176), with the ECORR quantisation columns
+        (sqrt of each epoch's TOA count) after the timing columns and before the Fourier
+        bases, the reference's noise_model_designmatrix order.  From the device Gram
+        (pint_debug_gram: its diagonal, and the unweighted column sums of squares)."""
+        if not self.want_fac:
+            return
+        for (G, colsq), k, lay in zip(self.s.debug_gram(), self.idx, self.layouts):
+            nc = len(lay.columns)
+            if self.gls:
+                f = np.sqrt(np.asarray(colsq[:lay.K], dtype=np.float64))
+                if lay.nep > 0:
+                    ep = np.sqrt(np.diff(np.asarray(lay.ep_ptr)).astype(np.float64))
+                    f = np.concatenate([f[:nc], ep, f[nc:]])
+            else:
+                f = np.sqrt(np.diag(G)[:nc].astype(np.float64))
+            f[f == 0] = 1.0
+            results[k].fac = f
 
     def _noise_into(self, results):
         """Noise realisations of the last step (GLS only)."""
@@ -294,6 +311,7 @@ class BatchFit:
             self._step()
             if outputs:
                 self._errors_into(results)
+                self._fac_into(results)
                 self._noise_into(results)
             self.s.apply_step(np.ones(self.ninst))
         self._eval(False)
@@ -404,6 +422,7 @@ class BatchFit:
         if outputs:
             results = [FitResult() for _ in range(self.n0)]
             self._errors_into(results)
+            self._fac_into(results)
             self._noise_into(results)
         self.s.eval(want_M=False)
         c2, _ = self._chi2_now()
@@ -424,16 +443,55 @@ class BatchFit:
 # ----------------------------------------------------------------------------------
 # single-model fitters (reference API)
 # ----------------------------------------------------------------------------------
+class FitState:
+    """The state a fit ended at (the reference's ModelState, fitter.py:908-979, as far as a
+    finished fit exposes it: DownhillFitter.current_state, fitter.py:1075): the model and its
+    residuals, chi2, the step's design-matrix normalisation ``fac``, the step, the fitted
+    columns and their covariance.  The device computed all of it; nothing is re-evaluated."""
+
+    def __init__(self, fitter, model, resids, res):
+        self.fitter = fitter
+        self.model = model
+        self.resids = resids
+        self.chi2 = res.chi2
+        self.fac = res.fac
+        self.norm = res.fac
+        self.params = list(res.labels) if getattr(res, "labels", None) is not None else []
+        self.step = res.step
+        self.noise_ampls = res.noise_coeffs
+        self.parameter_covariance_matrix = (CovarianceMatrix(res.cov, res.labels)
+                                            if res.cov is not None else None)
+
+    @property
+    def covariance_matrix(self):
+        warnings.warn("This parameter is deprecated.  Use `parameter_covariance_matrix` instead of "
+                      "`covariance_matrix`", DeprecationWarning)
+        return self.parameter_covariance_matrix
+
+
 class Fitter:
     def __init__(self, toas, model, track_mode=None, residuals=None):
         self.toas = toas
         self.model_init = model
         self.track_mode = track_mode
         self.model = copy.deepcopy(model)
-        self.resids_init = residuals
+        self._resids_init = residuals
         self.resids = None
         self.converged = False
         self.method = None
+        self.is_wideband = getattr(self, "is_wideband", False)
+
+    @property
+    def resids_init(self):
+        """The pre-fit residuals (fitter.py:214 computes them at construction; here on first
+        use, from the initial model)."""
+        if self._resids_init is None:
+            self._resids_init = self.make_resids(self.model_init)
+        return self._resids_init
+
+    @resids_init.setter
+    def resids_init(self, r):
+        self._resids_init = r
 
     @classmethod
     def auto(cls, toas, model, downhill=True, track_mode=None, residuals=None, **kwargs):
@@ -449,6 +507,12 @@ class Fitter:
     def update_resids(self):
         self.resids = self.make_resids(self.model)
 
+    def reset_model(self):
+        """fitter.py:557: back to the initial model."""
+        self.model = copy.deepcopy(self.model_init)
+        self.update_resids()
+        self.fitresult = []
+
     def get_designmatrix(self):
         return self.model.designmatrix(self.toas)
 
@@ -456,7 +520,7 @@ class Fitter:
         from .residuals import Residuals
         wideband = getattr(self, "is_wideband", False)
         bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style,
-                      track_mode=self.track_mode, wideband=wideband)
+                      track_mode=self.track_mode, wideband=wideband, want_fac=True)
         self.resids = None
         try:
             res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
@@ -468,14 +532,72 @@ class Fitter:
         finally:
             bf.close()
         self.fitresult = res
-        self.errors = res.errors
-        self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
-        self.converged = res.converged
+        self._set_outputs(res)
         if self.resids is None:
             self.update_resids()
         if mode == "gls" and noise and not wideband:
             self.resids.noise_resids = res.noise_resids
+            self.resids.norm = res.fac  # fitter.py:2268-2282 sets resids.norm beside noise_resids
+        if not plain:
+            self.current_state = FitState(self, self.model, self.resids, res)
         return res
+
+    def _set_outputs(self, res):
+        """fitter.py:2231-2252 / :1076-1085: errors, the labelled covariance and correlation
+        matrices of the fitted columns, and the step's normalisation ``fac``."""
+        self.errors = res.errors
+        self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
+        self.parameter_correlation_matrix = self.parameter_covariance_matrix.to_correlation_matrix()
+        self.converged = res.converged
+        if not isinstance(self, DownhillFitter):  # DownhillFitter.fac is current_state.fac
+            self.fac = res.fac
+
+    # -- the reference Fitter's reporting API (fitter.py:348-620, :807-890) ------------
+    def _get_corr_cov_matrix(self, matrix_type, with_phase, pretty_print, prec, usecolor):
+        if not hasattr(self, f"parameter_{matrix_type}_matrix"):
+            raise AttributeError(f"You must run .fit_toas() before accessing the {matrix_type} matrix")
+        cm = getattr(self, f"parameter_{matrix_type}_matrix")
+        if not pretty_print:
+            return cm.prettyprint(prec=prec, offset=with_phase)
+        print(cm.prettyprint(prec=prec, offset=with_phase, usecolor=usecolor))
+
+    def get_parameter_covariance_matrix(self, with_phase=False, pretty_print=False, prec=3):
+        """fitter.py:592."""
+        return self._get_corr_cov_matrix("covariance", with_phase, pretty_print, prec, False)
+
+    def get_parameter_correlation_matrix(self, with_phase=False, pretty_print=False, prec=3, usecolor=True):
+        """fitter.py:605."""
+        return self._get_corr_cov_matrix("correlation", with_phase, pretty_print, prec, usecolor)
+
+    @property
+    def covariance_matrix(self):
+        warnings.warn("This parameter is deprecated. Use `parameter_covariance_matrix` instead of "
+                      "`covariance_matrix`", DeprecationWarning)
+        return self.parameter_covariance_matrix
+
+    def get_params_dict(self, which="free", kind="value"):
+        """fitter.py:807 (values, or uncertainties with kind="uncertainty")."""
+        names = self.model.free_params if which == "free" else self.model.params
+        if kind == "uncertainty":
+            return {n: self.model[n].uncertainty for n in names}
+        return self.model.get_params_dict(which=which)
+
+    def set_param_uncertainties(self, fitp):
+        """fitter.py:874."""
+        for k, v in fitp.items():
+            self.model[k].uncertainty = v
+
+    def get_summary(self, nodmx=False):
+        """fitter.py:348-472: fit quality and a prefit/postfit parameter table.  The layout
+        (header lines, column widths, the uncertainties package's shorthand ``value(unc)``
+        for fitted parameters) is the reference's; angles print as sexagesimal strings and
+        the derived-parameter block (derived_quantities.py, out of scope) is omitted."""
+        from .summary import fitter_summary
+        return fitter_summary(self, nodmx=nodmx)
+
+    def print_summary(self):
+        """fitter.py:502."""
+        print(self.get_summary())
 
     def update_model(self, chi2=None):
         """fitter.py:530-555: START/FINISH/NTOA (and EPHEM/CLOCK when the TOAs carry them),
@@ -513,6 +635,10 @@ class Fitter:
 
 
 class WLSFitter(Fitter):
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        super().__init__(toas, model, track_mode, residuals)
+        self.method = "weighted_least_square"  # fitter.py:1963
+
     def fit_toas(self, maxiter=1, threshold=None, debug=False):
         if self.model.has_correlated_errors:
             pass  # the reference WLSFitter ignores correlated noise
@@ -522,6 +648,10 @@ class WLSFitter(Fitter):
 
 
 class GLSFitter(Fitter):
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        super().__init__(toas, model, track_mode, residuals)
+        self.method = "generalized_least_square"  # fitter.py:2102
+
     def fit_toas(self, maxiter=1, threshold=0, full_cov=False, debug=False):
         """fitter.py:2104.  full_cov=True: the reference forms the dense N x N covariance
         C = N + U Phi U^T, Cholesky-factors it and solves M^T C^-1 M with the timing columns
@@ -571,16 +701,14 @@ class WidebandTOAFitter(Fitter):
         fitter.py:2546-2552); full_cov=True solves the same system (Woodbury identity)."""
         self.model.validate()
         bf = BatchFit([(self.model, self.toas)], mode="gls", threshold=threshold, degeneracy_style="gls",
-                      track_mode=self.track_mode, wideband=True)
+                      track_mode=self.track_mode, wideband=True, want_fac=True)
         try:
             res = bf.fit_plain(maxiter=maxiter)[0]
             chi2 = float(bf.last_chi2_lin[0])
         finally:
             bf.close()
         self.fitresult = res
-        self.errors = res.errors
-        self.parameter_covariance_matrix = CovarianceMatrix(res.cov, res.labels)
-        self.converged = res.converged
+        self._set_outputs(res)
         self.update_resids()
         self.update_model(chi2)
         return chi2
@@ -588,6 +716,15 @@ class WidebandTOAFitter(Fitter):
 
 class DownhillFitter(Fitter):
     mode = "wls"
+
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        super().__init__(toas, model, track_mode, residuals)
+        self.method = "downhill_checked"  # fitter.py:997
+
+    @property
+    def fac(self):
+        """fitter.py:1207: the normalisation of the best state's step."""
+        return self.current_state.fac
 
     def fit_toas(self, maxiter=20, noise_fit_niter=2, required_chi2_decrease=1e-2, max_chi2_increase=1e-2,
                  min_lambda=1e-3, noisefit_method="Newton-CG", compute_noise_uncertainties=True, debug=False,
@@ -677,7 +814,12 @@ class DownhillWLSFitter(DownhillFitter):
         if model.has_correlated_errors:
             raise CorrelatedErrors(model)
         super().__init__(toas, model, track_mode, residuals)
+        self.method = "downhill_wls"  # fitter.py:1392
 
 
 class DownhillGLSFitter(DownhillFitter):
     mode = "gls"
+
+    def __init__(self, toas, model, track_mode=None, residuals=None):
+        super().__init__(toas, model, track_mode, residuals)
+        self.method = "downhill_gls"  # fitter.py:1545

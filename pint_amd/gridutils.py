@@ -11,6 +11,7 @@ rank, and the chi2 blocks are all-gathered over RCCL -- the only collective.
 from __future__ import annotations
 
 import copy
+import os
 from typing import List, Sequence
 
 import numpy as np
@@ -59,8 +60,10 @@ def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
     world = dist.get_world_size()
     buf = torch.full((per,), float("nan"), dtype=torch.float64)
     buf[: len(local)] = torch.from_numpy(np.ascontiguousarray(local, dtype=np.float64))
-    if dist.get_backend() == "nccl":
-        buf = buf.cuda()
+    if dist.get_backend() == "nccl":  # this rank's GPU (LOCAL_RANK), not whatever device is current
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        buf = buf.to(dev)
     gl = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(gl, buf)
     return torch.cat([g.cpu() for g in gl]).numpy()[:npts]

@@ -16,6 +16,7 @@ That gather is the only collective; there is no data-path communication.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional, Sequence
 
 import numpy as np
@@ -71,7 +72,11 @@ def gather_rows(local: np.ndarray, counts: Sequence[int], dist) -> np.ndarray:
     if len(local):
         buf[: len(local)] = torch.from_numpy(np.ascontiguousarray(local, dtype=np.float64))
     if dist.get_backend() == "nccl":
-        buf = buf.cuda()
+        # this rank's own GPU (LOCAL_RANK), whatever device is current: a collective over
+        # buffers that all landed on cuda:0 hangs or fails in RCCL
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        buf = buf.to(dev)
     gl = [torch.empty_like(buf) for _ in range(dist.get_world_size())]
     dist.all_gather(gl, buf)
     return np.concatenate([g.cpu().numpy()[:c] for g, c in zip(gl, counts)])

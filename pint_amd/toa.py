@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import os
+import warnings
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -225,6 +226,33 @@ def _bipm_choice(include_bipm, model):
     return False
 
 
+_NO_CLOCK_SITES = {"barycenter", "geocenter", "spacecraft", "ssb", "stl_geo"}
+
+
+def _warn_missing_clocks(obs, clock_files):
+    """The reference applies each topocentric site's clock files by default and warns when
+    they are missing (observatory/topo_obs.py clock_corrections); here clock files are only
+    applied when passed, so topocentric TOAs without any for their site warn the same way
+    (residuals of real observatory data then differ from the reference's at the us level)."""
+    from .observatory import get_observatory_name
+    have = set()
+    for k in (clock_files or {}):
+        try:
+            have.add(get_observatory_name(k))
+        except KeyError:
+            have.add(str(k))
+    for site in sorted(set(obs)):
+        try:
+            canon = get_observatory_name(site)
+        except KeyError:
+            canon = str(site)
+        if canon.lower() in _NO_CLOCK_SITES or canon in have:
+            continue
+        warnings.warn(f"No clock corrections found for observatory {canon}: topocentric TOAs are prepared "
+                      "without site clock corrections (pass clock_files={site: path} to apply them)",
+                      UserWarning)
+
+
 def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, include_pn=True,
              clock_files=None) -> TOAs:
     """get_TOAs for a tim file (toa.py:109-330) without PINT/astropy: read (pint_amd.tim),
@@ -249,6 +277,7 @@ def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, i
     obs = [r.obs for r in recs]
     flags = [dict(r.flags) for r in recs]
     corr = np.array([float(f.get("to", 0.0)) for f in flags])
+    _warn_missing_clocks(obs, clock_files)
     if clock_files:
         from .clock import site_corrections
         corr = corr + site_corrections(clock_files, obs, day + frac)

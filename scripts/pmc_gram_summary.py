@@ -44,7 +44,8 @@ def main(out, workload, *dirs):
         if "SQ_INSTS_VALU" in m and m.get("SQ_INSTS_MFMA"):
             m["valu_per_mfma"] = m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"]
         res[base] = m
-    json.dump({"workload": workload, "note": __doc__, "kernels": res}, open(out, "w"), indent=1)
+    json.dump({"workload": workload, "workload_key": workload.split(" ")[0], "note": __doc__, "kernels": res},
+              open(out, "w"), indent=1)
     for k, m in res.items():
         if m.get("mfma_busy_frac"):
             print(f"{k:24s} MFMA busy {m['mfma_busy_frac']:.3f}  MFMA {m.get('mfma_gflop', 0):.4g} GFLOP/step")

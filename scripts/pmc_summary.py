@@ -50,7 +50,7 @@ def main(fetch_csv, write_csv, out, workload):
         parts = [k for k in kern if k.startswith(grp + "<")]
         if parts:
             kern[grp] = {x: sum(kern[k][x] for k in parts) for x in ("fetch_bytes", "write_bytes", "hbm_bytes")}
-    json.dump({"workload": workload, "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1, KiB->bytes",
+    json.dump({"workload": workload, "workload_key": workload.split(" ")[0], "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1, KiB->bytes",
                "kernels": kern}, open(out, "w"), indent=1)
 
 

@@ -1,0 +1,114 @@
+"""The fitter outputs the drop-in boundary promises beside the fitted model (SURVEY.md
+§8(b)): ``fac`` (fitter.py:1343, :1455, :2176), ``current_state`` (:1075),
+``parameter_correlation_matrix`` (:1083, :2063, :2250) and ``get_summary`` /
+``print_summary`` (:348, :502), against the reference's own arrays where the stage
+fixtures hold them (tests/golden/<name>_stage.npz: its GLSFitter's ``norm`` and ``xvar``)."""
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, load
+
+pytestmark = pytest.mark.gpu
+
+
+def stage(name):
+    import os
+    return dict(np.load(os.path.join(GOLDEN, name + "_stage.npz"), allow_pickle=False))
+
+
+@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855"])
+def test_gls_fac_and_correlation(name):
+    """GLSFitter.fac = the reference's norm (every column of [M | noise bases], the ECORR
+    quantisation columns included): 1e-12 relative.  The correlation matrix of the timing
+    columns against the reference's xvar: 1e-9 on the PTA fixtures; the ill-conditioned
+    J0740 (cond 7e12) / B1855 (3e11) systems to their solvers' rounding (test_gpu_stage)."""
+    from pint_amd import GLSFitter
+    model, toas, z, meta = load(name)
+    st = stage(name)
+    f = GLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    fac = np.asarray(f.fac)
+    assert fac.shape == st["norm"].shape, (fac.shape, st["norm"].shape)
+    rel = np.max(np.abs(fac / st["norm"] - 1))
+    print(f"{name}: fac max rel {rel:.2e}")
+    assert rel < 1e-12
+    assert f.resids.norm is f.fac or np.array_equal(f.resids.norm, f.fac)
+    nc = len(f.parameter_covariance_matrix.labels)
+    xv = st["xvar_tr"][:nc, :nc]
+    e = np.sqrt(np.diag(xv))
+    cref = xv / np.outer(e, e)
+    corr = f.parameter_correlation_matrix.matrix
+    assert f.parameter_correlation_matrix.labels == f.parameter_covariance_matrix.labels
+    assert np.allclose(np.diag(corr), 1.0, rtol=0, atol=1e-14)
+    d = np.max(np.abs(corr - cref))
+    print(f"{name}: correlation max abs diff {d:.2e}")
+    assert d < {"j0740": 5e-3, "b1855": 5e-3}.get(name, 1e-9)
+    txt = f.get_parameter_correlation_matrix(usecolor=False)
+    assert "Parameter correlation matrix" in txt and "Offset" not in txt.splitlines()[2]
+
+
+def test_wls_fac():
+    """WLSFitter.fac: column norms of the whitened design matrix (fitter.py:1320-1343),
+    against the device design matrix and uncertainties, and the covariance's labels."""
+    from pint_amd import WLSFitter
+    model, toas, z, meta = load("ngc6440e")
+    f = WLSFitter(toas, model)
+    M, params, _ = f.model_init.designmatrix(toas)
+    f.fit_toas(maxiter=1)
+    sig = f.resids.get_data_error() * 1e-6
+    ref = np.sqrt(np.sum((M / sig[:, None]) ** 2, axis=0))
+    assert np.max(np.abs(np.asarray(f.fac) / ref - 1)) < 1e-12
+    assert f.parameter_covariance_matrix.labels == list(params)
+
+
+@pytest.mark.parametrize("name", ["pta_iso", "ecorr_phoff"])
+def test_downhill_current_state(name):
+    """DownhillFitter.current_state (fitter.py:1075): the best state's model, residuals,
+    chi2, normalisation and covariance; DownhillFitter.fac is its fac (:1207)."""
+    from pint_amd import DownhillGLSFitter
+    from pint_amd.fitter import MaxiterReached, StepProblem
+    model, toas, z, meta = load(name)
+    f = DownhillGLSFitter(toas, model)
+    try:
+        f.fit_toas(maxiter=10)
+    except (MaxiterReached, StepProblem):
+        pass
+    cs = f.current_state
+    assert cs.model is f.model and cs.resids is f.resids
+    assert cs.chi2 == f.resids.chi2
+    assert f.fac is cs.fac
+    assert cs.params == f.parameter_covariance_matrix.labels
+    assert np.array_equal(cs.parameter_covariance_matrix.matrix, f.parameter_covariance_matrix.matrix)
+    nc = len(cs.params)
+    assert len(cs.fac) >= nc and np.all(np.asarray(cs.fac) > 0)
+    corr = f.parameter_correlation_matrix.matrix
+    cov = f.parameter_covariance_matrix.matrix
+    e = np.sqrt(np.diag(cov))
+    assert np.allclose(corr, cov / np.outer(e, e), rtol=1e-14, atol=1e-15)
+
+
+def test_get_summary():
+    """get_summary / print_summary (fitter.py:348-502): the reference's header lines and a
+    prefit / postfit row per parameter, fitted ones as value(uncertainty)."""
+    from pint_amd import GLSFitter
+    from pint_amd.summary import shorthand
+    model, toas, z, meta = load("pta_iso")
+    f = GLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    s = f.get_summary()
+    lines = s.splitlines()
+    assert lines[0] == (f"Fitted model using generalized_least_square method with {len(f.model.free_params)} "
+                        f"free parameters to {toas.ntoas} TOAs")
+    assert lines[1].startswith("Prefit residuals Wrms = ") and "Postfit residuals Wrms = " in lines[1]
+    assert lines[2] == (f"Chisq = {f.resids.chi2:.3f} for {f.resids.dof} d.o.f. for reduced Chisq of "
+                        f"{f.resids.reduced_chi2:.3f}")
+    rows = {l.split()[0]: l for l in lines[6:] if l.strip()}
+    for p in f.model.free_params:
+        par = f.model[p]
+        if par.kind in ("hourangle", "degangle"):
+            assert "+/-" in rows[p], rows[p]
+        else:
+            assert shorthand(par.value, par.uncertainty) in rows[p], (p, rows[p])
+    assert "CHI2" in rows
+    nd = f.get_summary(nodmx=True)
+    assert not any(l.startswith("DMX") for l in nd.splitlines())

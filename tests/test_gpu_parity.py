@@ -759,3 +759,79 @@ def test_deferred_covariance_matches_in_kernel(name, monkeypatch):
     assert covs[0].shape == covs[1].shape
     assert np.all(np.isfinite(covs[1]))
     assert np.array_equal(covs[0], covs[1]), np.max(np.abs(covs[0] - covs[1]))
+
+
+@pytest.mark.gpu
+def test_pipelined_lazy_steps_match_synchronous():
+    """The bench's configuration: >= 16 instances in lazy mode, the covariance
+    deferred to k_cov_dmx on the copy stream, steps pipelined two deep (step_end /
+    check_step), the noise realisations read inside the step.  Each step's outputs --
+    steps, errors, covariances, noise realisations, post-fit chi2 -- equal bit for bit those
+    of a synchronous session with the in-kernel covariance (PINT_COV_DEFER=0) fed the same
+    parameter tables."""
+    from pint_amd import simulation as sim
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = sim.make_pta(ntoas=1500, indices=list(range(18)))
+    nsteps = 3
+
+    def session(lazy):
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        tabs = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
+        s.set_instances(list(zip(lays, tabs)))
+        if lazy:
+            s.set_lazy(True)
+        else:
+            s.set_cov_defer(0)
+        return s, np.concatenate(tabs)
+
+    s0, t0 = session(False)
+    ref, tables = [], [t0]
+    for k in range(nsteps):
+        s0.set_tables(tables[k])
+        s0.eval(want_M=Session.FIT)
+        s0.fit_step(1)
+        dp, er, cov, _ = s0.read_step()
+        nz = s0.noise_resids()
+        s0.apply_step(np.full(len(items), 0.5))
+        tables.append(s0.read_tables_flat())
+        s0.eval(want_M=False)
+        ref.append((dp, er, cov, nz, s0.chi2_gls().copy()))
+    s0.close()
+
+    s1, _ = session(True)
+    got, prev = [None] * nsteps, None
+
+    def grab(k, out):
+        (dp, er, cov, _), nz, c2 = out
+        got[k] = ([d.copy() for d in dp], [e.copy() for e in er], [c.copy() for c in cov],
+                  [{kk: v.copy() for kk, v in d.items()} for d in nz], np.array(c2, copy=True))
+
+    for k in range(nsteps):
+        s1.set_tables(tables[k])
+        s1.eval(want_M=Session.FIT)
+        s1.fit_step(1)
+        o = s1.read_step()
+        nz = s1.noise_resids()
+        s1.apply_step(np.full(len(items), 0.5))
+        s1.eval(want_M=False)
+        c2 = s1.chi2_gls()
+        slot = s1.step_end()
+        if prev is not None:
+            s1.check_step(prev[0])
+            grab(k - 1, prev[1])
+        prev = (slot, (o, nz, c2))
+    s1.check_step(prev[0])
+    grab(nsteps - 1, prev[1])
+    s1.close()
+    for k in range(nsteps):
+        dp0, er0, cov0, nz0, c20 = ref[k]
+        dp1, er1, cov1, nz1, c21 = got[k]
+        for i in range(len(items)):
+            assert np.array_equal(dp0[i], dp1[i]), (k, i)
+            assert np.array_equal(er0[i], er1[i]), (k, i)
+            assert np.all(np.isfinite(cov1[i])) and np.array_equal(cov0[i], cov1[i]), (k, i)
+            assert nz0[i].keys() == nz1[i].keys() and "pl_red_noise" in nz1[i]
+            for comp in nz0[i]:
+                assert np.array_equal(nz0[i][comp], nz1[i][comp]), (k, i, comp)
+        assert np.array_equal(c20, c21), k

@@ -132,8 +132,7 @@ def test_gpu_wideband_fit():
 def test_gpu_wideband_downhill():
     """WidebandDownhillFitter on the device (the wideband GLS step + the combined chi2 in the
     line search) against the reference's: status, chi2 at the end-to-end floor, parameters
-    within the Downhill bar of tests/test_gpu_parity.py::test_downhill_gls (5e-2 sigma: the
-    best-iterate choice follows each side's own chi2 rounding)."""
+    within 2e-4 sigma (10x the 2e-5 sigma measured on MI355X)."""
     from golden_util import load
     from pint_amd import WidebandDownhillFitter
     from pint_amd.fitter import MaxiterReached, StepProblem
@@ -149,4 +148,23 @@ def test_gpu_wideband_downhill():
     ref = _ref_pars(meta, "wbdown_params")
     worst = max(abs(float((LD(f.model[p].value) - ref[p]) / LD(meta["wbdown_errors"][p]))) for p in ref)
     print(f"wideband downhill: chi2 {f.resids.chi2:.6f} ref {meta['wbdown_chi2']:.6f}, worst {worst:.2e} sigma")
-    assert worst < 5e-2, worst
+    assert worst < 2e-4, worst
+
+
+@pytest.mark.gpu
+def test_gpu_wideband_fit_too_many_dm_columns():
+    """k_wb_gram carries at most 8 free DM-type columns (DM Taylor terms + DMJUMPs); a model
+    with more is refused (PINT_E_INVALID) instead of fitting the extra columns without their
+    DM rows."""
+    from golden_util import load
+    from pint_amd import WidebandTOAFitter, get_model
+    from pint_amd._lib import PintError
+    model, toas, z, meta = load("wb_dd")
+    text = open(os.path.join(GOLDEN, "wb_dd.par")).read()
+    # 7 more free DMJUMPs on MJD ranges holding TOAs: DM, DM1, DM2 + 8 DMJUMPs = 11 columns
+    extra = "".join(f"DMJUMP mjd {53000 + 400 * k} {53300 + 400 * k} 0.0 1\n" for k in range(1, 8))
+    m2 = get_model(text + extra)
+    m2.free_params = list(model.free_params) + [p for p in m2.params if p.startswith("DMJUMP")
+                                                and p not in model.free_params]
+    with pytest.raises((PintError, ValueError), match="DM-type columns"):
+        WidebandTOAFitter(toas, m2).fit_toas(maxiter=1)
