@@ -185,6 +185,11 @@ int pint_apply_step(pint_ctx *ctx, const double *lambda_);
  * the current residuals, per instance. */
 int pint_chi2_gls(pint_ctx *ctx, double *chi2);
 
+/* WLS chi2 (residuals.py:638-667 _calc_wls_chi2: sum (r / sigma_scaled)^2) of the current
+ * residuals, per instance -- e.g. of residuals replaced by pint_debug_set_resids (the
+ * residual pass reports its own through pint_read_resids). */
+int pint_chi2_wls(pint_ctx *ctx, double *chi2);
+
 /* ECORR epochs of pulsar `psr` (replaces EcorrNoise.ecorr_basis_weight_pair,
  * noise_model.py:385-427 + get_ecorr_epochs :808): nep epochs, TOA index lists in CSR form
  * (ep_ptr[nep+1], ep_idx[ep_ptr[nep]]) and the prior variance phi_e = ECORR^2 in s^2.

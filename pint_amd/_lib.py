@@ -69,7 +69,8 @@ def lib():
     L.pint_device_count.restype = C.c_int
     L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
     L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
-    for fn in ("pint_get_tables", "pint_set_tables", "pint_read_designmatrix", "pint_chi2_gls", "pint_last_timing"):
+    for fn in ("pint_get_tables", "pint_set_tables", "pint_read_designmatrix", "pint_chi2_gls", "pint_chi2_wls",
+               "pint_last_timing"):
         getattr(L, fn).argtypes = [vp, dptr]
     L.pint_eval.argtypes = [vp, C.c_int]
     L.pint_fit_step.argtypes = [vp, C.c_int]
@@ -121,7 +122,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_vgram_layout", "pint_lognorm", "pint_solve_eig", "pint_step_end", "pint_check_step",
             "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
-            "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids"]
+            "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids", "pint_chi2_wls"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

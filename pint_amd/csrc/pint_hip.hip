@@ -3128,6 +3128,25 @@ __global__ __launch_bounds__(PREP_T) void k_apply(const PsrDev* __restrict__ psr
     prep_one(psrs[I.psr].spec, P, S.tstride, ic + inst);
 }
 
+// k_chi2w: the WLS chi2 sum_i (r_i / sigma_i)^2 of the current time residuals of every
+// instance (residuals.py:638-667 _calc_wls_chi2), one workgroup per instance, wave-shuffle
+// reductions in a fixed order (deterministic); pint_chi2_wls, for residuals replaced by
+// pint_debug_set_resids / pint_set_resids (the residual pass computes its own chi2).
+__global__ __launch_bounds__(256) void k_chi2w(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                               const double* __restrict__ rtime, double* __restrict__ chi2) {
+    __shared__ double sh[4];
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const double* r = rtime + (I.roff - blockIdx.x);
+    double a = 0.0;
+    for (int i = threadIdx.x; i < I.n; i += 256) {
+        const double x = r[i] * Pd.isig[i];
+        a += x * x;
+    }
+    a = block_sum<4>(a, sh);
+    if (threadIdx.x == 0) chi2[blockIdx.x] = a;
+}
+
 // ---------------------------------------------------------------------------------
 // Noise realisations of the last fit step (fitter.py:2270-2282 GLSFitter, :1582-1605
 // DownhillGLSFitter: noise_resids[comp] = M[:, comp] @ xhat[comp] with M, xhat normalised,
@@ -4812,6 +4831,19 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
                        stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm);
     HIPCHK(hipGetLastError());
     record(ctx, 11);
+    HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+// WLS chi2 of the current residuals, per instance (k_chi2w); the chi2 that pint_read_resids
+// reports comes from the residual pass itself, this one from whatever d_rt holds now.
+int pint_chi2_wls(pint_ctx* ctx, double* chi2) {
+    if (!ctx || ctx->ninst <= 0 || !chi2) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    hipLaunchKernelGGL(k_chi2w, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt,
+                       ctx->d_chi2g);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;

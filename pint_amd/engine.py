@@ -696,6 +696,12 @@ class Session:
         self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
         return c if self.lazy else c.copy()
 
+    def chi2_wls(self):
+        """WLS chi2 of the current residuals per instance (pint_chi2_wls)."""
+        c = self._pin("chi2w", len(self.inst_layout))
+        self._check(self.L.pint_chi2_wls(self.ctx, L.ptr(c)))
+        return c if self.lazy else c.copy()
+
     def solve_eig(self, mode, thresholds):
         """SVD path of the fitters on the last fit_step's Gram (k_eig): replaces the step
         outputs; returns, per instance, the dropped directions (list of arrays over the

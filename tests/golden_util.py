@@ -11,7 +11,7 @@ PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "
         "ecorr_fit": "ecorr_fit.par", "white_mjd": "white_mjd.par", "ell1h_h3": "ell1h_h3.par",
         "ell1h_h4": "ell1h_h4.par", "ell1h_stig": "ell1h_stig.par", "pta_bt": "pta_bt.par",
         "pta_dmn": "pta_dmn.par", "pta_ddk": "pta_ddk.par", "pta_ddk_nk": "pta_ddk_nk.par",
-        "wb_dd": "wb_dd.par"}
+        "wb_dd": "wb_dd.par", "c5_iso": "c5_iso.par", "c5_ell1": "c5_ell1.par", "c5_dd": "c5_dd.par"}
 
 
 def load(name):
@@ -33,3 +33,13 @@ def load(name):
 def ref_value(meta, key, p):
     v = meta[key][p]
     return np.longdouble(v[0]) + np.longdouble(v[1])
+
+
+def downhill_bar(name, p, floor=1e-3):
+    """Per-parameter Downhill bar (sigma units): 2x the reference's own spread when its
+    residuals are perturbed at the 5 ps longdouble floor (tests/golden/downhill_spread.json,
+    oracle/refgen/gen_downhill_spread.py), at least `floor` (1e-3 sigma)."""
+    d = json.load(open(os.path.join(GOLDEN, "downhill_spread.json")))
+    if name not in d:
+        return floor
+    return max(floor, 2.0 * d[name]["max_dev_sigma"].get(p, 0.0))

@@ -147,8 +147,37 @@ def test_stage_gram_step(name):
     print(f"{name}: solver rounding: reference cho_solve {e_ref:.2e} sigma, device {e_dev:.2e} sigma; "
           f"Gram difference propagated {e_in:.2e} sigma")
     assert e_dev <= max(1e-9, 3 * e_ref), (e_dev, e_ref)
+    # the covariance decomposed the same way: each side's inverse against the longdouble
+    # inverse of the system it was given (the reference's cho_solve(c, I) of its mtcm, the
+    # device's Cholesky inverse of the device Gram), in units of sigma_i sigma_j
+    ncol = len(lay.columns)
+    Xref = ld_inverse(Aph)[:ncol, :ncol] / np.outer(norm_ref[:ncol], norm_ref[:ncol])
+    Xdev = ld_inverse(Ad)[:ncol, :ncol] * np.outer(inv[:ncol], inv[:ncol])
+    ee = np.outer(eref[:ncol], eref[:ncol])
+    c_ref = float(np.max(np.abs(cref - Xref) / ee))
+    c_dev = float(np.max(np.abs(cov - Xdev) / ee))
+    c_in = float(np.max(np.abs(Xdev - Xref) / ee))
+    print(f"{name}: covariance rounding: reference {c_ref:.2e}, device {c_dev:.2e}; Gram difference "
+          f"propagated {c_in:.2e} (sigma_i sigma_j)")
+    assert c_dev <= max(1e-9, 3 * c_ref), (c_dev, c_ref)
     assert de.max() <= 1e-3 and dc.max() <= 5e-3
     bf.close()
+
+
+def ld_inverse(A):
+    """Gauss-Jordan inverse with partial pivoting in longdouble."""
+    A = np.array(A, dtype=np.longdouble)
+    n = len(A)
+    M = np.concatenate([A, np.eye(n, dtype=np.longdouble)], axis=1)
+    for k in range(n):
+        p = k + int(np.argmax(np.abs(M[k:, k])))
+        if p != k:
+            M[[k, p]] = M[[p, k]]
+        M[k] /= M[k, k]
+        f = M[:, k].copy()
+        f[k] = 0
+        M -= np.outer(f, M[k])
+    return M[:, n:]
 
 
 def ld_solve(A, b):

@@ -6,7 +6,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN
+from golden_util import GOLDEN, downhill_bar
 
 import pint_oracle as O
 
@@ -213,13 +213,13 @@ def test_downhill_gls(name):
     assert status == meta["down_status"]
     assert abs(chi2 / meta["down_chi2"] - 1) < 5e-6
     # Near convergence a Gauss-Newton step in a nonlinear direction (DD SINI/M2) moves the
-    # parameters by ~1% sigma while chi2 changes by ~1e-4, below the ~1e-3 chi2 noise of
-    # the reference's own longdouble residuals: which iterate is "best" is then decided by
-    # rounding, so the converged solutions agree to 0.05 sigma, not 1e-3 sigma.
+    # parameters by ~1% sigma while chi2 changes by ~1e-4: which iterate is "best" is then
+    # decided by rounding.  Bar: 1e-3 sigma, or 2x the reference's own spread under 5 ps
+    # residual perturbations (downhill_spread.json) where that is larger.
     ref = _ref_pars(meta, "down_params")
     for j, p in _timing_cols(st["names"]):
         sig = meta["down_errors"][p]
-        assert abs(float(best.values[p] - ref[p])) < 5e-2 * sig, p
+        assert abs(float(best.values[p] - ref[p])) < downhill_bar(name, p) * sig, p
         assert abs(st["errs"][j] / sig - 1) < 1e-2, p
 
 
