@@ -137,17 +137,16 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
     lays = [s.add(build_layout(m, t)) for m, t in items]
     tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
     s.set_instances(list(zip(lays, tabs0)))
-    flat0 = np.concatenate(tabs0)
-    ones = np.ones(len(lays))
+    s.save_tables()        # the initial models, resident in HBM like the TOAs
     s.set_lazy(True)
 
     def step():
-        s.set_tables(flat0)
+        s.restore_tables()     # every step fits from the initial models (device->device copy)
         s.eval(want_M=Session.FIT)
         s.fit_step(1)
         out = s.read_step()    # steps, errors, timing covariance -> host (fit outputs)
         nz = s.noise_resids()  # noise realisations -> host (fitter.py:2269-2282, full_cov=False)
-        s.apply_step(ones)
+        s.apply_step_uniform(1.0)
         s.eval(want_M=False)
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
         return out, nz, c2

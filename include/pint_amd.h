@@ -180,6 +180,15 @@ int pint_read_step(pint_ctx *ctx, double *dpars, double *errs, double *cov, doub
 /* tables += lambda[k] * dpars (double-double add): fitter.py:957 take_step_model and
  * :2073-2080 the longdouble parameter update. */
 int pint_apply_step(pint_ctx *ctx, const double *lambda_);
+/* The same with one lambda for every instance (GLSFitter / WLSFitter take the full step,
+ * fitter.py:2254-2263); a kernel argument, no host->device copy. */
+int pint_apply_step_uniform(pint_ctx *ctx, double lambda_);
+
+/* Device-resident parameter tables: pint_save_tables snapshots the batch's current tables
+ * on the device, pint_restore_tables copies the snapshot back (device->device on the
+ * stream), e.g. to start repeated fits from the same initial models without an upload. */
+int pint_save_tables(pint_ctx *ctx);
+int pint_restore_tables(pint_ctx *ctx);
 
 /* GLS chi2 (Woodbury, residuals.py:567 _calc_gls_chi2 + utils.py:3074 woodbury_dot) of
  * the current residuals, per instance. */

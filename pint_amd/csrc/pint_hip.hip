@@ -208,11 +208,21 @@ __device__ __forceinline__ void prep_one(const pint_spec_t* Sg, const double* Pg
     }
 }
 
+// k_prep: the per-instance constants of the tables; with tables0 (pint_restore_tables
+// pending) the instance's table is first put back from the device snapshot, in the same
+// launch (the constants are formed from the snapshot, which is what the table then holds)
 __global__ __launch_bounds__(PREP_T) void k_prep(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                 const double* __restrict__ tables, InstConst* __restrict__ ic) {
+                                                 double* __restrict__ tables, const double* __restrict__ tables0,
+                                                 InstConst* __restrict__ ic) {
     const InstDev I = insts[blockIdx.x];
     const PsrDev& Pd = psrs[I.psr];
-    prep_one(Pd.spec, tables + I.toff, Pd.spec->tstride, ic + blockIdx.x);
+    const int ts = Pd.spec->tstride;
+    if (tables0) {
+        for (int i = threadIdx.x; i < ts; i += PREP_T) tables[I.toff + i] = tables0[I.toff + i];
+        prep_one(Pd.spec, tables0 + I.toff, ts, ic + blockIdx.x);
+        return;
+    }
+    prep_one(Pd.spec, tables + I.toff, ts, ic + blockIdx.x);
 }
 
 template <int WANT_M, int BIN>
@@ -3111,16 +3121,17 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
 // default 1024-thread budget of 128 VGPRs spilled 252 B/lane into its serial chain)
 __global__ __launch_bounds__(PREP_T) void k_apply(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts, double* __restrict__ tables,
                         const double* __restrict__ dpars, const double* __restrict__ lam,
-                        InstConst* __restrict__ ic) {
+                        InstConst* __restrict__ ic, double lam_u) {
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const pint_spec_t& S = *psrs[I.psr].spec;
     double* P = tables + I.toff;
+    const double li = lam ? lam[inst] : lam_u;  // per instance, or one lambda for the batch
     for (int c = threadIdx.x; c < S.ncol; c += blockDim.x) {
         int o = S.col_toff[c];
         if (o < 0) continue;
-        if (lam[inst] == 0.0) continue;  // decided instances: a non-finite step must not touch them
-        dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam[inst] * dpars[I.coff + c]);
+        if (li == 0.0) continue;  // decided instances: a non-finite step must not touch them
+        dd v = dd_add_d(dd_make(P[o], P[o + 1]), li * dpars[I.coff + c]);
         P[o] = v.hi;
         P[o + 1] = v.lo;
     }
@@ -3160,35 +3171,61 @@ __global__ __launch_bounds__(256) void k_chi2w(const PsrDev* __restrict__ psrs, 
 __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ dpars, double* __restrict__ out,
                                                    int dm, const double* __restrict__ dfac) {
+    __shared__ double sa[256];  // the component's amplitudes (a_k, b_k), staged once per block
     const int inst = blockIdx.y;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= I.n) return;
-    const double* a = dpars + I.coff + S.ncol;
+    // block-uniform bounds (readfirstlane: the spec is read through a generic pointer)
+    const int ncol = __builtin_amdgcn_readfirstlane(S.ncol), nred = __builtin_amdgcn_readfirstlane(S.nred);
+    const int dmn0 = __builtin_amdgcn_readfirstlane(S.dmn0);
+    const int k0 = dm ? dmn0 : 0, k1 = dm ? nred : dmn0;
+    const double* a = dpars + I.coff + ncol;
     double v = 0.0;
-    const int k0 = dm ? S.dmn0 : 0, k1 = dm ? S.nred : S.dmn0;
-    if (!dm && k1 > 0) {
+    if (!dm && k1 > 0 && k1 <= 128) {
         // PLRedNoise block: harmonics 1..dmn0 of f_1 = red_freq[0] (get_rednoise_freqs is
         // linspace(1/T, nmodes/T)), by rotations of the row's e^{i theta} (k_redbase) instead
-        // of a double-double reduction and a sincos per harmonic
-        const double c1 = Pd.red_cs[4 * i], s1 = Pd.red_cs[4 * i + 1];
-        double cs = c1, sn = s1;
-        for (int k = 0; k < k1; k++) {
-            v += a[2 * k] * sn + a[2 * k + 1] * cs;
-            rot(cs, sn, c1, s1);
+        // of a double-double reduction and a sincos per harmonic; four independent chains
+        // (harmonics j + 1 + 4m, j < 4, stepped by e^{4 i theta}) for instruction-level
+        // parallelism
+        for (int k = threadIdx.x; k < 2 * k1; k += 256) sa[k] = a[k];
+        __syncthreads();
+        if (i >= I.n) return;
+        const double4_t z = ((gptr<double4_t>)Pd.red_cs)[i];
+        const double c1 = z[0], s1 = z[1];
+        double cz[4], sz[4];
+        cz[0] = c1;
+        sz[0] = s1;
+#pragma unroll
+        for (int j = 1; j < 4; j++) {
+            cz[j] = cz[j - 1];
+            sz[j] = sz[j - 1];
+            rot(cz[j], sz[j], c1, s1);
         }
-    } else if (k1 > k0) {
-        const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
-        for (int k = k0; k < k1; k++) {
-            const dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
-            const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
-            double sn, cs;
-            sincos(TWO_PI * fr, &sn, &cs);
-            v += a[2 * k] * sn + a[2 * k + 1] * cs;
+        double c4 = cz[3], s4 = sz[3];  // e^{4 i theta}
+        double vj[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int m = 0; m < k1; m += 4) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (m + j < k1) vj[j] += sa[2 * (m + j)] * sz[j] + sa[2 * (m + j) + 1] * cz[j];
+                rot(cz[j], sz[j], c4, s4);
+            }
         }
-        if (dm) v *= dfac[I.ooff + i];
+        v = (vj[0] + vj[1]) + (vj[2] + vj[3]);
+    } else {
+        if (i >= I.n) return;
+        if (k1 > k0) {
+            const dd ts = dd_mul_d(dd_make(Pd.tdb_hi[i], Pd.tdb_lo[i]), DAYSEC);
+            for (int k = k0; k < k1; k++) {
+                const dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[nred + k]));
+                const double fr = dd_to_d(dd_sub(x, dd_floor(x)));
+                double sn, cs;
+                sincos(TWO_PI * fr, &sn, &cs);
+                v += a[2 * k] * sn + a[2 * k + 1] * cs;
+            }
+            if (dm) v *= dfac[I.ooff + i];
+        }
     }
     out[I.roff - inst + i] = v;
 }
@@ -3452,6 +3489,10 @@ struct pint_ctx {
     size_t nz_cap = 0;
     double* d_noise = nullptr;  // pint_noise_resids: red and ECORR realisations (2 tot_out)
     long noise_cap = 0;
+    double* d_tables0 = nullptr;  // pint_save_tables snapshot
+    long tables0_cap = 0;
+    bool restore_pending = false;  // pint_restore_tables not yet carried out (k_prep does it)
+    double* chi2_dst = nullptr;    // lazy pint_chi2_gls: the host buffer of its deferred copy
     hipEvent_t ev_noise = nullptr;
 };
 
@@ -3639,9 +3680,11 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
-                   (void**)&ctx->d_xw, (void**)&ctx->d_noise};
+                   (void**)&ctx->d_xw, (void**)&ctx->d_noise, (void**)&ctx->d_tables0};
     for (auto p : ps) dfree(*p);
     ctx->noise_cap = 0;
+    ctx->tables0_cap = 0;
+    ctx->restore_pending = false;
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
     ctx->graph_exec = nullptr;
@@ -4221,7 +4264,19 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     return PINT_OK;
 }
 
+static int flush_restore(pint_ctx* ctx);
+
+// a lazy pint_chi2_gls copy not yet enqueued: on the kernel stream, in order
+static int flush_chi2(pint_ctx* ctx) {
+    if (!ctx->chi2_dst) return PINT_OK;
+    double* dst = ctx->chi2_dst;
+    ctx->chi2_dst = nullptr;
+    HIPCHK(hipMemcpyAsync(dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    return PINT_OK;
+}
+
 int pint_get_tables(pint_ctx* ctx, double* out) {
+    if (flush_restore(ctx)) return PINT_E_HIP;
     HIPCHK(hipMemcpyAsync(out, ctx->d_tables, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -4229,6 +4284,7 @@ int pint_get_tables(pint_ctx* ctx, double* out) {
 
 int pint_set_tables(pint_ctx* ctx, const double* tables) {
     ctx->ic_valid = false;
+    ctx->restore_pending = false;  // overwritten anyway
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -4260,8 +4316,11 @@ static void update_timings(pint_ctx* ctx) {
 
 static int decode_status(pint_ctx* ctx, int st);
 
+static int flush_chi2(pint_ctx* ctx);
+
 static int check_status(pint_ctx* ctx) {
     int st = 0;
+    if (flush_chi2(ctx)) return PINT_E_HIP;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -4296,7 +4355,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     record(ctx, want_M ? 2 : 0);
     if (!ctx->ic_valid) {  // k_apply refreshes them itself
         hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_tables, ctx->d_ic);
+                           ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
+        ctx->restore_pending = false;
         HIPCHK(hipGetLastError());
         ctx->ic_valid = true;
     }
@@ -4403,6 +4463,7 @@ int pint_set_wideband(pint_ctx* ctx, int psr, const double* pp_dm, const double*
 
 int pint_dm_resids(pint_ctx* ctx, int subtract_mean, int use_weighted_mean, double* resid_out, double* chi2_out) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    if (flush_restore(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
     if (ctx->tot_out > ctx->dmr_cap) {
         if (ctx->d_dmr) hipFree(ctx->d_dmr);
@@ -4444,6 +4505,7 @@ int pint_read_designmatrix(pint_ctx* ctx, double* M) {
 // Gram + solve for every instance; requires pint_eval(want_M=1) on the current state.
 int pint_fit_step(pint_ctx* ctx, int mode) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    if (flush_restore(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
     if (ctx->wbfit) {
         // k_wb_gram carries at most WB_MAXC free DM-type columns (DM Taylor terms + DMJUMPs):
@@ -4466,6 +4528,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
+        if (ctx->copy_pending) {  // the copy stream's noise realisations read esum / eD
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
+            ctx->copy_pending = false;
+        }
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
         HIPCHK(hipGetLastError());
@@ -4796,19 +4862,75 @@ void pint_host_free(void* p) {
 }
 
 int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
+    if (!ctx || ctx->ninst <= 0 || !lambda_) return PINT_E_INVALID;
+    if (flush_restore(ctx)) return PINT_E_HIP;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
-                       ctx->d_dpars, ctx->d_lam, ctx->d_ic);
+                       ctx->d_dpars, ctx->d_lam, ctx->d_ic, 0.0);
     HIPCHK(hipGetLastError());
     ctx->ic_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
+// The same step with one lambda for every instance (GLSFitter / WLSFitter take the full
+// step, fitter.py:2254-2263): a kernel argument, no host->device copy.
+int pint_apply_step_uniform(pint_ctx* ctx, double lambda_) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    if (flush_restore(ctx)) return PINT_E_HIP;
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
+    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
+                       ctx->d_dpars, (const double*)nullptr, ctx->d_ic, lambda_);
+    HIPCHK(hipGetLastError());
+    ctx->ic_valid = true;
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+// Parameter tables resident on the device: pint_save_tables snapshots the current tables,
+// pint_restore_tables puts the snapshot back (a device copy on the stream), e.g. to start
+// every fit of a benchmark loop from the same initial models without a host->device upload.
+int pint_save_tables(pint_ctx* ctx) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    if (flush_restore(ctx)) return PINT_E_HIP;
+    hipSetDevice(ctx->device);
+    if (ctx->tot_table > ctx->tables0_cap) {
+        dfree((void*&)ctx->d_tables0);
+        HIPCHK(cmalloc((void**)&ctx->d_tables0, sizeof(double) * ctx->tot_table));
+        ctx->tables0_cap = ctx->tot_table;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->d_tables0, ctx->d_tables, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
+int pint_restore_tables(pint_ctx* ctx) {
+    if (!ctx || ctx->ninst <= 0 || !ctx->d_tables0 || ctx->tables0_cap < ctx->tot_table) {
+        if (ctx) ctx->err = "pint_restore_tables: no snapshot of this batch (pint_save_tables)";
+        return PINT_E_INVALID;
+    }
+    ctx->ic_valid = false;
+    if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
+    // deferred: the next pint_eval's k_prep copies the snapshot back as it forms the
+    // per-instance constants (one launch less); every other reader of the tables flushes it
+    ctx->restore_pending = true;
+    return PINT_OK;
+}
+
+static int flush_restore(pint_ctx* ctx) {
+    if (!ctx->restore_pending) return PINT_OK;
+    ctx->restore_pending = false;
+    HIPCHK(hipMemcpyAsync(ctx->d_tables, ctx->d_tables0, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    return PINT_OK;
+}
+
 // Woodbury GLS chi2 of the current residuals; requires a previous pint_fit_step(mode=1)
 // (Sigma factor) and the red-noise columns of the last design matrix.
 int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
+    if (flush_chi2(ctx)) return PINT_E_HIP;
     int R = 0;
     for (auto& I : ctx->inst) R = 2 * ctx->psrs[I.psr].spec.nred > R ? 2 * ctx->psrs[I.psr].spec.nred : R;
     int stride = R + 2;
@@ -4831,6 +4953,12 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
                        stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm);
     HIPCHK(hipGetLastError());
     record(ctx, 11);
+    if (ctx->lazy && !ctx->capturing) {
+        // the copy is deferred to pint_step_end (the copy stream, after the step's end event:
+        // no event of its own on the kernel stream) or pint_check; valid after either
+        ctx->chi2_dst = chi2;
+        return PINT_OK;
+    }
     HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -4840,6 +4968,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
 // reports comes from the residual pass itself, this one from whatever d_rt holds now.
 int pint_chi2_wls(pint_ctx* ctx, double* chi2) {
     if (!ctx || ctx->ninst <= 0 || !chi2) return PINT_E_INVALID;
+    if (flush_chi2(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
     hipLaunchKernelGGL(k_chi2w, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt,
                        ctx->d_chi2g);
@@ -4975,10 +5104,18 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
     ctx->sigma_pending = false;
     const int s = ctx->slot;
-    ctx->cdone_rec[s] = ctx->copy_pending;
-    if (ctx->copy_pending) HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
-    HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    // the step's kernels end at ev_done; its status word goes to the host on the copy stream
+    // after them (off the kernel stream), and ev_cdone covers it and the step's output copies
     HIPCHK(hipEventRecord(ctx->ev_done[s], ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_done[s], 0));
+    if (ctx->chi2_dst) {  // the step's deferred chi2 copy (pint_chi2_gls, lazy)
+        HIPCHK(hipMemcpyAsync(ctx->chi2_dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost,
+                              ctx->cstream));
+        ctx->chi2_dst = nullptr;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->cstream));
+    HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
+    ctx->cdone_rec[s] = true;
     ctx->slot = s ^ 1;
     ctx->d_status = ctx->d_status_slots + ctx->slot;
     ctx->ev = ctx->ev_slot[ctx->slot];
@@ -5073,22 +5210,24 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     double* de = ctx->d_noise + std::max<long>(1, ctx->tot_out);
     int maxn = 1;
     for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
+    // lazy: the kernels and the copies run on the copy stream after the solve (ev_solved, no
+    // new event on the kernel stream): they read dpars and the ECORR epoch sums, which the
+    // next fit step overwrites only after waiting for ev_copied
+    hipStream_t st = ctx->stream;
+    if (ctx->lazy) {
+        st = ctx->cstream;
+        HIPCHK(hipStreamWaitEvent(st, ctx->ev_solved, 0));
+    }
     if (red)
-        hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+        hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, st, ctx->d_psrs,
                            ctx->d_inst, ctx->d_dpars, dr, 0, ctx->d_dfac);
     if (ecorr) {
-        HIPCHK(hipMemsetAsync(de, 0, sizeof(double) * ctx->tot_out, ctx->stream));
+        HIPCHK(hipMemsetAsync(de, 0, sizeof(double) * ctx->tot_out, st));
         if (ctx->max_nep > 0)
-            hipLaunchKernelGGL(k_noise_ecorr, dim3(ctx->max_nep, ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs,
+            hipLaunchKernelGGL(k_noise_ecorr, dim3(ctx->max_nep, ctx->ninst), dim3(64), 0, st, ctx->d_psrs,
                                ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, de);
     }
     if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids: launch failed"; return PINT_E_HIP; }
-    hipStream_t st = ctx->stream;
-    if (ctx->lazy) {
-        HIPCHK(hipEventRecord(ctx->ev_noise, ctx->stream));
-        HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_noise, 0));
-        st = ctx->cstream;
-    }
     if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
     if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
     if (ctx->lazy) {

@@ -483,6 +483,18 @@ class Session:
             self._keep.append(lam)
         self._check(self.L.pint_apply_step(self.ctx, L.ptr(lam)))
 
+    def apply_step_uniform(self, lam=1.0):
+        """tables += lam * step for every instance (one lambda: a kernel argument)."""
+        self._check(self.L.pint_apply_step_uniform(self.ctx, float(lam)))
+
+    def save_tables(self):
+        """Snapshot the batch's parameter tables on the device (pint_save_tables)."""
+        self._check(self.L.pint_save_tables(self.ctx))
+
+    def restore_tables(self):
+        """Put the device snapshot back (a device->device copy, pint_restore_tables)."""
+        self._check(self.L.pint_restore_tables(self.ctx))
+
     # -- HIP graphs ---------------------------------------------------------------------
     def capture(self, fn):
         """Capture the launches fn() enqueues (lazy mode) into a HIP graph; returns fn()'s

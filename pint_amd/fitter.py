@@ -313,7 +313,7 @@ class BatchFit:
                 self._errors_into(results)
                 self._fac_into(results)
                 self._noise_into(results)
-            self.s.apply_step(np.ones(self.ninst))
+            self.s.apply_step_uniform(1.0)
         self._eval(False)
         c2, _ = self._chi2_now()
         if not outputs:

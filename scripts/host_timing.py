@@ -17,20 +17,20 @@ s = Session()
 lays = [s.add(build_layout(sp["model"], t)) for sp, t in zip(specs, toas)]
 tabs = [pack_table(l, sp["model"]) for l, sp in zip(lays, specs)]
 s.set_instances(list(zip(lays, tabs)))
-flat = np.concatenate(tabs)
-ones = np.ones(len(lays))
+s.save_tables()
 s.set_lazy(True)
 s.set_timing_mask(1 << 6)
-names = ["set_tables", "eval_M", "fit_step", "read_step", "apply", "eval", "chi2_gls", "step_end", "check_step"]
+names = ["restore", "eval_M", "fit_step", "read_step", "noise", "apply", "eval", "chi2_gls", "step_end", "check_step"]
 acc = {n: [] for n in names}
 prev = None
 for it in range(30):
     T = [time.perf_counter()]
-    s.set_tables(flat); T.append(time.perf_counter())
+    s.restore_tables(); T.append(time.perf_counter())
     s.eval(want_M=Session.FIT); T.append(time.perf_counter())
     s.fit_step(1); T.append(time.perf_counter())
     s.read_step(); T.append(time.perf_counter())
-    s.apply_step(ones); T.append(time.perf_counter())
+    s.noise_resids(); T.append(time.perf_counter())
+    s.apply_step_uniform(1.0); T.append(time.perf_counter())
     s.eval(want_M=False); T.append(time.perf_counter())
     s.chi2_gls(); T.append(time.perf_counter())
     cur = s.step_end(); T.append(time.perf_counter())
@@ -42,5 +42,8 @@ for it in range(30):
         for n, a, b in zip(names, T[:-1], T[1:]):
             acc[n].append((b - a) * 1e6)
 s.check_step(prev)
+tot = 0.0
 for n in names:
+    tot += np.median(acc[n])
     print(f"{n:12s} median {np.median(acc[n]):8.1f} us  max {np.max(acc[n]):8.1f}")
+print(f"sum of medians {tot:.1f} us")

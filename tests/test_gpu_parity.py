@@ -842,3 +842,38 @@ def test_pipelined_lazy_steps_match_synchronous():
             for comp in nz0[i]:
                 assert np.array_equal(nz0[i][comp], nz1[i][comp]), (k, i, comp)
         assert np.array_equal(c20, c21), k
+
+
+@pytest.mark.gpu
+def test_resident_tables_and_uniform_step():
+    """pint_save_tables / pint_restore_tables (device-resident initial models) and
+    pint_apply_step_uniform give bit for bit what an upload of the same tables and
+    pint_apply_step with a lambda array give: tables after the step, residual chi2."""
+    from pint_amd import simulation as sim
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = sim.make_pta(ntoas=1200, indices=list(range(4)))
+    outs = []
+    for resident in (False, True):
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        tabs = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
+        s.set_instances(list(zip(lays, tabs)))
+        flat0 = np.concatenate(tabs)
+        if resident:
+            s.save_tables()
+            s.set_tables(flat0 * 0.0 + 1.0)  # overwrite, then restore the snapshot
+            s.restore_tables()
+        else:
+            s.set_tables(flat0)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        if resident:
+            s.apply_step_uniform(0.75)
+        else:
+            s.apply_step(np.full(len(items), 0.75))
+        tab = s.read_tables_flat()
+        s.eval(want_M=False)
+        outs.append((tab, s.chi2_gls().copy()))
+        s.close()
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
