@@ -263,6 +263,10 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * Every HIP timing event costs device time (~5 us each), so a timed run enables only the
  * slots it reports. */
 #define PINT_OPT_TIMING_MASK 3
+/* PINT_OPT_TIMING_EVERY k (default 1): the Gram kernels' timing events (slot 6) ride on
+ * every k-th pint_fit_step only; the other steps carry no events.  The slot then reads 0
+ * after an unsampled step. */
+#define PINT_OPT_TIMING_EVERY 8
 /* PINT_OPT_REFINE = 1 (default): a normal-equations solve whose condition estimate
  * max diag(A) * max diag(A^-1) exceeds 1e8 gets one pass of iterative refinement with a
  * double-double residual (the explicit L^-1 of the blocked solves otherwise loses ~cond(L)

@@ -54,11 +54,24 @@ struct PmState {
     double p[3], v1[3], tl1;
 };
 
+// the trigonometric values pm_setup starts from: cos/sin of ra, dec, ra2 = ra + pmr and
+// dec2 = dec + pmd (independent: k_prep forms them on separate lanes, pm_setup_trig)
+struct PmTrig {
+    double cra, sra, cdec, sdec, cra2, sra2, cdec2, sdec2;
+};
+
+PD void pm_setup_trig(double pmr, double pmd, double px, const PmTrig& T, PmState& st);
+
 PD void pm_setup(double ra, double dec, double pmr, double pmd, double px, PmState& st) {
+    const double ra2 = ra + pmr, dec2 = dec + pmd;
+    const PmTrig T = {cos(ra), sin(ra), cos(dec), sin(dec), cos(ra2), sin(ra2), cos(dec2), sin(dec2)};
+    pm_setup_trig(pmr, pmd, px, T, st);
+}
+
+PD void pm_setup_trig(double pmr, double pmd, double px, const PmTrig& T, PmState& st) {
     // pmsafe: override parallax (PXMIN 5e-7 arcsec, F = 326)
-    double a1[3] = {cos(ra) * cos(dec), sin(ra) * cos(dec), sin(dec)};
-    double ra2 = ra + pmr, dec2 = dec + pmd;
-    double b1[3] = {cos(ra2) * cos(dec2), sin(ra2) * cos(dec2), sin(dec2)};
+    double a1[3] = {T.cra * T.cdec, T.sra * T.cdec, T.sdec};
+    double b1[3] = {T.cra2 * T.cdec2, T.sra2 * T.cdec2, T.sdec2};
     double cx = a1[1] * b1[2] - a1[2] * b1[1];
     double cy = a1[2] * b1[0] - a1[0] * b1[2];
     double cz = a1[0] * b1[1] - a1[1] * b1[0];
@@ -73,7 +86,7 @@ PD void pm_setup(double ra, double dec, double pmr, double pmd, double px, PmSta
     double w = px1a >= 1e-7 ? px1a : 1e-7;
     double r = DR2AS / w;
     double rad = pmr / DJY, decd = pmd / DJY;
-    double st_ = sin(ra), ct = cos(ra), sp = sin(dec), cp = cos(dec);
+    double st_ = T.sra, ct = T.cra, sp = T.sdec, cp = T.cdec;
     double rcp = r * cp;
     double x = rcp * ct, y = rcp * st_;
     double rpd = r * decd;
@@ -221,6 +234,74 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
     double pmra_c = v[0] * era[0] + v[1] * era[1] + v[2] * era[2];
     double pmdec = v[0] * edec[0] + v[1] * edec[1] + v[2] * edec[2];
     pm_setup(ra, dec, pmra_c / cos(dec), pmdec, 1e-3 /* 1 kpc dummy */, C.pm);
+    C.has_pm = 1;
+}
+
+// inst_setup by the 64 lanes of one wave (k_prep, k_apply): the equatorial astrometry's
+// independent transcendental calls -- cos/sin of RA and DEC, the double-double 1/PB, then
+// cos/sin of the proper-motion-displaced RA and DEC -- on separate lanes, exchanged through
+// `sx` (LDS, >= 8 doubles); lane 0 finishes (pmsafe's atan2, starpv's iteration).  The same
+// expressions as inst_setup, so the same values; ecliptic models run inst_setup on lane 0.
+// Every lane of the wave must call it; C is written by lane 0.
+PD void inst_setup_wave(const pint_spec_t& S, const double* P, InstConst& C, double* sx, int lane) {
+    if (S.astrometry != 1) {
+        if (lane == 0) inst_setup(S, P, C);
+        return;
+    }
+    const double lon = pval(P, S.o_lon), lat = pval(P, S.o_lat);
+    const double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
+    const double pmb = S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0;
+    const double ra = lon * HA_RAD, dec = lat * DEG_RAD;
+    if (lane == 0) {
+        sx[0] = cos(ra);
+        sx[1] = sin(ra);
+    } else if (lane == 1) {
+        sx[2] = cos(dec);
+        sx[3] = sin(dec);
+    } else if (lane == 2 && S.binary && S.o_bin[PINT_B_PB] >= 0) {
+        dd ipb = dd_div(dd_make(1.0), dd_mul_d(pdd(P, S.o_bin[PINT_B_PB]), DAYSEC));
+        sx[4] = ipb.hi;
+        sx[5] = ipb.lo;
+    }
+    __syncthreads();
+    const bool pm = !(pml == 0.0 && pmb == 0.0);
+    const double cd = sx[2];
+    const double pmr = pml * MAS_RAD / cd, pmd = pmb * MAS_RAD;
+    if (pm) {
+        if (lane == 0) {
+            const double ra2 = ra + pmr;
+            sx[8] = cos(ra2);
+            sx[9] = sin(ra2);
+        } else if (lane == 1) {
+            const double dec2 = dec + pmd;
+            sx[10] = cos(dec2);
+            sx[11] = sin(dec2);
+        }
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    C.F0 = pval(P, S.o_F);
+    C.iF0 = 1.0 / C.F0;
+    C.has_pm = 0;
+    C.posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
+    C.ipb_hi = C.ipb_lo = 0.0;
+    if (S.binary && S.o_bin[PINT_B_PB] >= 0) {
+        C.ipb_hi = sx[4];
+        C.ipb_lo = sx[5];
+    }
+    C.plon = ra;  // lon * HA_RAD
+    C.plat = dec;
+    C.cplat = sx[2];
+    C.splat = sx[3];
+    C.cplon = sx[0];
+    C.splon = sx[1];
+    C.L0[0] = sx[0] * sx[2];
+    C.L0[1] = sx[1] * sx[2];
+    C.L0[2] = sx[3];
+    if (!pm) return;
+    const double px_as = (S.o_px >= 0 ? pval(P, S.o_px) : 0.0) * 1e-3;
+    const PmTrig T = {sx[0], sx[1], sx[2], sx[3], sx[8], sx[9], sx[10], sx[11]};
+    pm_setup_trig(pmr, pmd, px_as, T, C.pm);
     C.has_pm = 1;
 }
 

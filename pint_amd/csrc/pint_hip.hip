@@ -28,6 +28,17 @@ using namespace pint;
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
+// e^{i theta} rotation: (c, s) <- (c, s) * (c1, s1)
+__device__ __forceinline__ void rot(double& c, double& s, double c1, double s1) {
+    const double cn = c * c1 - s * s1;
+    s = s * c1 + c * s1;
+    c = cn;
+}
+
+// a pointer in the global address space (loads through it are global_load, not flat_load)
+template <typename T>
+using gptr = const T __attribute__((address_space(1)))*;
+
 // ---------------------------------------------------------------------------------
 // device-side descriptors
 // ---------------------------------------------------------------------------------
@@ -201,11 +212,12 @@ __device__ __forceinline__ void prep_one(const pint_spec_t* Sg, const double* Pg
     if (staged)
         for (int i = threadIdx.x; i < tstride; i += blockDim.x) sP[i] = Pg[i];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        InstConst C;
-        inst_setup(*reinterpret_cast<const pint_spec_t*>(sS), staged ? sP : Pg, C);
-        *out = C;
-    }
+    // the wave's lanes share the independent transcendental calls (inst_setup_wave)
+    __shared__ double sx[16];
+    __shared__ InstConst sC;
+    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(sS), staged ? sP : Pg, sC, sx, threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x == 0) *out = sC;
 }
 
 // k_prep: the per-instance constants of the tables; with tables0 (pint_restore_tables
@@ -405,11 +417,22 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     }
 }
 
+// k_resid2 with wtile: the Woodbury dot products of the post-fit chi2 (k_wdot's F^T W r and
+// 1^T W r, residuals.py:567-589 via utils.py:3074) come out of the same pass.  The PLRedNoise
+// basis is the harmonic series e^{i k theta} (k_redbase), and e^{i (a + 8b) theta} =
+// e^{i a theta} e^{i 8b theta}: one 16x16 v_mfma_f64_16x16x4f64 tile D = A^T B per block with
+// A = w r [cos a theta | sin a theta] and B = [cos 8b theta | sin 8b theta] (a, b < 8) holds
+// every sum_i w_i r_i e^{i k theta_i}, k < 64 (k_rsum combines: cos k = D[a][b] - D[8+a][8+b],
+// sin k = D[8+a][b] + D[a][8+b]; 1^T W r = D[0][0]).  Wave w of the block holds rows r0 + 64w
+// + 256j + lane (j < 4): four contiguous 64-row chunks, staged one at a time in the wave's own
+// LDS columns and contracted by 16 k-steps of 4 rows.
+constexpr int WT_CS = 66;  // k_resid2 tile staging: column stride (doubles), 64 rows + 2
 __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const int* __restrict__ rblk_inst, const double* __restrict__ ftay,
                                                    double* __restrict__ rtime, double* __restrict__ rphase,
-                                                   double* __restrict__ rpart) {
+                                                   double* __restrict__ rpart, double* __restrict__ wtile) {
     __shared__ double sh[RES_BT / 64];
+    extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS: A (columns 0-15), B (16-31)
     const int ii = rblk_inst[blockIdx.x];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -430,17 +453,70 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
         b = block_sum<RES_BT / 64>(b, sh);
         mean = a / b;
     }
+    const bool tile = wtile != nullptr;
+    const bool harm = tile && __builtin_amdgcn_readfirstlane(S.nred) > 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};  // independent chains
+    typedef double __attribute__((address_space(3))) ldsd;
+    ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS);
     double c2 = 0.0;
-    for (int i = r0 + threadIdx.x; i < r1; i += RES_BT) {
-        double p = rphase[oo + i] - mean;
-        rphase[oo + i] = p;
-        double rt = p / ftay[ro + i];  // calc_time_resids (residuals.py:483-538)
-        rtime[oo + i] = rt;
-        double z = rt * Pd.isig[i];
-        c2 += z * z;
+#pragma unroll 1
+    for (int j = 0; j < RES_RB / RES_BT; j++) {
+        const int i = r0 + threadIdx.x + j * RES_BT;
+        double wr = 0.0;
+        if (i < r1) {
+            double p = rphase[oo + i] - mean;
+            rphase[oo + i] = p;
+            double rt = p / ftay[ro + i];  // calc_time_resids (residuals.py:483-538)
+            rtime[oo + i] = rt;
+            const double is = Pd.isig[i];
+            double z = rt * is;
+            c2 += z * z;
+            wr = z * is;
+        }
+        if (tile) {  // (block-uniform)
+            double c1 = 1.0, s1 = 0.0, c8 = 1.0, s8 = 0.0;
+            if (harm && i < r1) {
+                const double4_t zz = ((gptr<double4_t>)Pd.red_cs)[i];
+                c1 = zz[0];
+                s1 = zz[1];
+                c8 = zz[2];
+                s8 = zz[3];
+            }
+            double ca = wr, sa = 0.0, cb = 1.0, sb = 0.0;
+#pragma unroll
+            for (int a = 0; a < 8; a++) {
+                X[a * WT_CS + lane] = ca;
+                X[(8 + a) * WT_CS + lane] = sa;
+                X[(16 + a) * WT_CS + lane] = cb;
+                X[(24 + a) * WT_CS + lane] = sb;
+                rot(ca, sa, c1, s1);
+                rot(cb, sb, c8, s8);
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's stores before its reads
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int ks = 0; ks < 16; ks++) {
+                const int row = 4 * ks + (lane >> 4);
+                const double av = X[(lane & 15) * WT_CS + row], bv = X[(16 + (lane & 15)) * WT_CS + row];
+                acc[ks & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ks & 3], 0, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
     }
     c2 = block_sum<RES_BT / 64>(c2, sh);
     if (threadIdx.x == 0) rpart[3 * blockIdx.x + 2] = c2;
+    if (tile) {
+        // the waves' tiles summed in a fixed order through LDS (acc[q]: D[4q + lane/16][lane%16])
+        __syncthreads();
+        double* red = xs;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            red[wave * 256 + (4 * q + (lane >> 4)) * 16 + (lane & 15)] = (acc[0][q] + acc[1][q]) + (acc[2][q] + acc[3][q]);
+        __syncthreads();
+        for (int e = threadIdx.x; e < 256; e += RES_BT)
+            wtile[(long)blockIdx.x * 256 + e] = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
+    }
 }
 
 // _calc_wls_chi2 (residuals.py:638-667): one wave per instance sums its blocks' chi2
@@ -846,11 +922,6 @@ __device__ __forceinline__ void dd_sincos_cyc(dd x, double* s, double* c) {
     sincos(TWO_PI * fr, s, c);
 }
 
-__device__ __forceinline__ void rot(double& c, double& s, double c1, double s1) {
-    const double cn = c * c1 - s * s1;
-    s = s * c1 + c * s1;
-    c = cn;
-}
 
 // e^{i k theta} from e^{i theta} by binary powering (k >= 0)
 __device__ __forceinline__ void cpow(double c1, double s1, int k, double& c, double& s) {
@@ -888,9 +959,6 @@ __device__ __forceinline__ int vsel(bool p, int a, int b) {
     return r;
 }
 
-// a pointer in the global address space (loads through it are global_load, not flat_load)
-template <typename T>
-using gptr = const T __attribute__((address_space(1)))*;
 
 // (experiment) per-workgroup phase timestamps of k_gram_v
 __device__ unsigned long long g_gvts[4096 * 5];
@@ -3031,9 +3099,11 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 const double* __restrict__ esum, const double* __restrict__ eD,
                                                 const double* __restrict__ eW, const double* __restrict__ wpart,
                                                 int nsplit, int stride, double* __restrict__ ecs,
-                                                double* __restrict__ chi2, double* __restrict__ lognorm) {
+                                                double* __restrict__ chi2, double* __restrict__ lognorm,
+                                                const double* __restrict__ wtile, const double* __restrict__ chi2w) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
+    __shared__ double Dt[256], wloc[130];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -3042,6 +3112,27 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     const double* ri = rtime + (I.roff - inst);
     double* d = lds;  // Kn
     const double* wp = wpart + (long)inst * nsplit * stride;
+    if (wtile) {
+        // the dots from k_resid2's trig tiles (one per residual block of the instance, summed
+        // in block order): F_j^T W r (sin, cos of harmonic h + 1 at 2h, 2h + 1), r^T W r (the
+        // residual pass's chi2) at R, 1^T W r = D[0][0] at R + 1 -- k_wdot's layout, one split
+        double v = 0.0;
+        for (int k = 0; k < I.nrb; k++) v += wtile[(long)(I.rb0 + k) * 256 + threadIdx.x];
+        Dt[threadIdx.x] = v;
+        __syncthreads();
+        for (int h = threadIdx.x; h < R / 2; h += blockDim.x) {
+            const int k = h + 1, a = k & 7, b = k >> 3;
+            wloc[2 * h] = Dt[(8 + a) * 16 + b] + Dt[a * 16 + 8 + b];      // sum w r sin(k theta)
+            wloc[2 * h + 1] = Dt[a * 16 + b] - Dt[(8 + a) * 16 + 8 + b];  // sum w r cos(k theta)
+        }
+        if (threadIdx.x == 0) {
+            wloc[R] = chi2w[inst];
+            wloc[R + 1] = Dt[0];
+        }
+        __syncthreads();
+        wp = wloc;
+        nsplit = 1;
+    }
     double rwr = 0.0, rw1 = 0.0;
     if (threadIdx.x == 0) {
         for (int q = 0; q < nsplit; q++) {
@@ -3426,6 +3517,8 @@ struct pint_ctx {
     bool ic_valid = false;  // per-instance constants (k_prep) current for the tables
     bool no_events = false; // PINT_NO_EVENTS=1: no per-kernel timing events (their cost)
     int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
+    int timing_every = 1;   // PINT_OPT_TIMING_EVERY: Gram events on every k-th fit step
+    long gram_calls = 0;
     hipGraph_t graph = nullptr;          // a captured launch sequence (pint_capture_*)
     hipGraphExec_t graph_exec = nullptr;
     bool capturing = false;
@@ -3493,6 +3586,10 @@ struct pint_ctx {
     long tables0_cap = 0;
     bool restore_pending = false;  // pint_restore_tables not yet carried out (k_prep does it)
     double* chi2_dst = nullptr;    // lazy pint_chi2_gls: the host buffer of its deferred copy
+    bool wfuse = false;            // the batch takes the fused Woodbury dots (k_resid2 tiles)
+    bool wtile_valid = false;      // d_wpart holds the current residuals' dots (one split)
+    double* d_wtile = nullptr;     // k_resid2's per-block trig tiles (256 per residual block)
+    int wstride = 0;
     hipEvent_t ev_noise = nullptr;
 };
 
@@ -3680,11 +3777,13 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
-                   (void**)&ctx->d_xw, (void**)&ctx->d_noise, (void**)&ctx->d_tables0};
+                   (void**)&ctx->d_xw, (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
+                   (void**)&ctx->d_wtile};
     for (auto p : ps) dfree(*p);
     ctx->noise_cap = 0;
     ctx->tables0_cap = 0;
     ctx->restore_pending = false;
+    ctx->wfuse = ctx->wtile_valid = false;
     if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
     if (ctx->graph) hipGraphDestroy(ctx->graph);
     ctx->graph_exec = nullptr;
@@ -4217,6 +4316,29 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     if (!rbi.empty())
         HIPCHK(hipMemcpy(ctx->d_rblk_inst, rbi.data(), sizeof(int) * rbi.size(), hipMemcpyHostToDevice));
     HIPCHK(cmalloc((void**)&ctx->d_rpart, sizeof(double) * 3 * std::max<size_t>(1, rbi.size())));
+    // the post-fit Woodbury dots fused into the residual pass (k_resid2 tiles, k_rsum): every
+    // instance's noise basis a PLRedNoise harmonic series of < 64 modes (no PLDMNoise)
+    {
+        bool fuse = true;
+        int R = 0;
+        for (int k = 0; k < ninst; k++) {
+            const pint_spec_t& sp = ctx->psrs[inst_psr[k]].spec;
+            R = std::max(R, 2 * sp.nred);
+            if (sp.dmn0 < sp.nred || sp.nred > 63) fuse = false;
+        }
+        ctx->wfuse = fuse && !rbi.empty();
+        ctx->wtile_valid = false;
+        if (ctx->wfuse) {
+            HIPCHK(cmalloc((void**)&ctx->d_wtile, sizeof(double) * 256 * rbi.size()));
+            const size_t need = (size_t)ninst * (R + 2);
+            if (need > ctx->wpart_cap) {
+                dfree((void*&)ctx->d_wpart);
+                HIPCHK(cmalloc((void**)&ctx->d_wpart, sizeof(double) * need));
+                ctx->wpart_cap = need;
+            }
+            ctx->wstride = R + 2;
+        }
+    }
 
     HIPCHK(cmalloc((void**)&ctx->d_tables, sizeof(double) * toff));
     HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
@@ -4303,7 +4425,7 @@ static void record(pint_ctx* ctx, int i, hipStream_t st = nullptr) {
     ctx->rec[i] = true;
 }
 
-static void update_timings(pint_ctx* ctx) {
+static void update_timings(pint_ctx* ctx, bool zero_missing = false) {
     const auto& pairs = kTimingPairs;
     for (int k = 0; k < pint_ctx::NMS; k++) {
         if (!((ctx->timing_mask >> k) & 1)) continue;
@@ -4311,6 +4433,8 @@ static void update_timings(pint_ctx* ctx) {
         if (ctx->rec[pairs[k][0]] && ctx->rec[pairs[k][1]] &&
             hipEventElapsedTime(&t, ctx->ev[pairs[k][0]], ctx->ev[pairs[k][1]]) == hipSuccess)
             ctx->ms[k] = t;
+        else if (zero_missing)
+            ctx->ms[k] = 0.0f;  // not recorded in this step (e.g. an unsampled Gram, PINT_OPT_TIMING_EVERY)
     }
 }
 
@@ -4420,9 +4544,15 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     if (ctx->nrblk > 0) {
         hipLaunchKernelGGL(k_resid1, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_rblk_inst, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
-        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart);
+        // without the design matrix (the post-fit evaluation a GLS chi2 follows): the Woodbury
+        // dot products come with the residual pass (k_resid2 tiles, k_rsum)
+        const bool wt = ctx->wfuse && want_M == 0;
+        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0,
+                           ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
+                           wt ? ctx->d_wtile : nullptr);
         hipLaunchKernelGGL(k_rsum, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_inst, ctx->d_rpart, ctx->d_chi2);
+        ctx->wtile_valid = wt;
     }
     HIPCHK(hipGetLastError());
     record(ctx, 5);
@@ -4559,10 +4689,15 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     // Gram-kernel timing: when the whole Gram is k_gram_v launches, the slot's start/stop
     // events ride on the first/last dispatch packet (hipExtLaunchKernel) instead of marker
     // packets between kernels, which cost the stream ~10 us each
-    const bool gram_t = !ctx->no_events && ((ctx->timing_mask >> 6) & 1);
+    // PINT_OPT_TIMING_EVERY k: the Gram events ride on every k-th fit step only (each event
+    // pair still costs the stream a few us; the average over the sampled launches is the
+    // kernel's time)
+    const bool sampled = ctx->timing_every <= 1 || (ctx->gram_calls++ % ctx->timing_every) == 0;
+    const bool gram_t = !ctx->no_events && ((ctx->timing_mask >> 6) & 1) && sampled;
     const bool ext_t = gram_t && vgp && (cmp ? ctx->kp_groups_c : ctx->kp_groups).empty() &&
                        !ctx->kp_groups_v.empty();
-    if (!ext_t) record(ctx, 12);
+    const bool gram_mark = sampled && !ext_t;  // marker-packet events (the other Gram paths)
+    if (gram_mark) record(ctx, 12);
     {
         // instances are launched in groups of equal tiles-per-wave T (template parameter);
         // per-instance tile counts are recomputed in-kernel from their own Kp.
@@ -4638,11 +4773,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
 #undef PINT_GRAMV
         }
         if (ext_t) ctx->rec[12] = ctx->rec[13] = true;
-        else record(ctx, 13);
+        else if (gram_mark) record(ctx, 13);
         hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->nsplit, ctx->d_TSp, ctx->d_TS);
         HIPCHK(hipGetLastError());
-    } else {
+    } else if (gram_mark) {
         record(ctx, 13);
     }
     HIPCHK(hipGetLastError());
@@ -4935,6 +5070,10 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     for (auto& I : ctx->inst) R = 2 * ctx->psrs[I.psr].spec.nred > R ? 2 * ctx->psrs[I.psr].spec.nred : R;
     int stride = R + 2;
     int nsw = ctx->nsplit;  // same N-split as the Gram (fills the CUs)
+    if (ctx->wtile_valid) {  // the residual pass formed the dots (k_resid2 tiles -> k_rsum)
+        nsw = 1;
+        stride = ctx->wstride;
+    }
     size_t need = (size_t)ctx->ninst * nsw * stride;
     if (need > ctx->wpart_cap) {
         if (ctx->capturing) { ctx->err = "pint_chi2_gls: first call inside a graph capture"; return PINT_E_INVALID; }
@@ -4944,13 +5083,16 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     }
     record(ctx, 10);
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
-    hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
-                       ctx->d_rt, nsw, stride, ctx->m_compact, ctx->d_wpart);
-    HIPCHK(hipGetLastError());
+    if (!ctx->wtile_valid) {
+        hipLaunchKernelGGL(k_wdot, dim3(nsw, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_M,
+                           ctx->d_rt, nsw, stride, ctx->m_compact, ctx->d_wpart);
+        HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_wsolve, dim3(ctx->ninst), dim3(256), sizeof(double) * ((R + 1) + (R + 1) * (R + 2) / 2),
                        ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
-                       stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm);
+                       stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm,
+                       ctx->wtile_valid ? (const double*)ctx->d_wtile : nullptr, (const double*)ctx->d_chi2);
     HIPCHK(hipGetLastError());
     record(ctx, 11);
     if (ctx->lazy && !ctx->capturing) {
@@ -4997,6 +5139,12 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
         return PINT_OK;
     }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_TIMING_EVERY) {
+        if (value < 1) return PINT_E_INVALID;
+        ctx->timing_every = value;
+        ctx->gram_calls = 0;
+        return PINT_OK;
+    }
     if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {
         ctx->timing_mask = value & 0xff;
@@ -5120,7 +5268,8 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     ctx->d_status = ctx->d_status_slots + ctx->slot;
     ctx->ev = ctx->ev_slot[ctx->slot];
     ctx->rec = ctx->rec_slot[ctx->slot];
-    for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec[k] = false;
+    // (the new slot's event flags still belong to its previous step, which the caller checks
+    // next: pint_check_step reads and clears them)
     *slot = s;
     return PINT_OK;
 }
@@ -5140,7 +5289,8 @@ int pint_check_step(pint_ctx* ctx, int s) {
     bool* rec = ctx->rec;
     ctx->ev = ctx->ev_slot[s];
     ctx->rec = ctx->rec_slot[s];
-    update_timings(ctx);
+    update_timings(ctx, true);  // this step's timings (0 where it recorded none)
+    for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec[k] = false;
     ctx->ev = ev;
     ctx->rec = rec;
     return decode_status(ctx, st);
@@ -5293,6 +5443,7 @@ int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
     hipSetDevice(ctx->device);
     HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->wtile_valid = false;  // the fused Woodbury dots were those of the replaced residuals
     return PINT_OK;
 }
 
@@ -5304,6 +5455,7 @@ int pint_set_resids(pint_ctx* ctx, const double* time_resid) { return pint_debug
 int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !sigma_s) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    ctx->wtile_valid = false;  // new weights: the fused Woodbury dots are stale
     PsrHost& ph = ctx->psrs[psr];
     const int n = ph.n;
     std::vector<double> is(n);

@@ -618,6 +618,11 @@ class Session:
         """Timing slots of timing() whose HIP events are recorded (each costs device time)."""
         self._check(self.L.pint_set_option(self.ctx, 3, int(mask)))
 
+    def set_timing_every(self, k=1):
+        """Gram timing events on every k-th fit step only (PINT_OPT_TIMING_EVERY); timing()
+        then reads 0 in slot 6 after an unsampled step."""
+        self._check(self.L.pint_set_option(self.ctx, 8, int(k)))
+
     def set_refine(self, on=True):
         """Iterative refinement of ill-conditioned solves (PINT_OPT_REFINE, default on)."""
         self._check(self.L.pint_set_option(self.ctx, 4, 1 if on else 0))

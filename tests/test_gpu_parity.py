@@ -877,3 +877,32 @@ def test_resident_tables_and_uniform_step():
         s.close()
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("names", [("pta_iso", "pta_ell1", "pta_dd"), ("b1855",), ("j0740", "pta_iso"),
+                                   ("ecorr_phoff",)])
+def test_fused_woodbury_dots_match_wdot(names):
+    """The post-fit Woodbury dot products formed inside the residual pass (k_resid2's trig
+    tiles, k_rsum) give the GLS chi2 and log-normalisation of k_wdot's (the same residuals
+    re-entered, which takes the k_wdot path) to rounding."""
+    from pint_amd.engine import Session
+    from pint_amd.fitter import BatchFit
+    items = [load(n)[:2] for n in names]
+    bf = BatchFit(items, mode="gls")
+    s = bf.s
+    s.eval(want_M=Session.FIT)
+    s.fit_step(1)
+    s.apply_step_uniform(1.0)
+    s.eval(want_M=False)
+    c_fused = s.chi2_gls().copy()
+    l_fused = s.lognorm(1)
+    tr, _, _ = s.read_resids()
+    s.debug_set_resids(tr)
+    c_wdot = s.chi2_gls().copy()
+    l_wdot = s.lognorm(1)
+    bf.close()
+    rel = np.abs(c_fused / c_wdot - 1)
+    print(names, "fused vs k_wdot chi2", rel)
+    assert np.all(rel < 1e-12), rel
+    assert np.allclose(l_fused, l_wdot, rtol=1e-13, atol=0)
