@@ -237,6 +237,15 @@ __global__ __launch_bounds__(PREP_T) void k_prep(const PsrDev* __restrict__ psrs
     prep_one(Pd.spec, tables + I.toff, ts, ic + blockIdx.x);
 }
 
+constexpr int EVAL_MAXTAB = 512;  // doubles of a parameter table staged in LDS (larger ones read in place)
+constexpr int EVAL_MAXRUN = 64;   // column runs staged in LDS
+struct EvalLds {
+    pint_spec_t S;
+    InstConst C;
+    ColRun R[EVAL_MAXRUN];
+    double P[EVAL_MAXTAB];
+};
+
 template <int WANT_M, int BIN>
 __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                            const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
@@ -245,15 +254,36 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
                                            double* __restrict__ ftay, double* __restrict__ delay_out,
                                            double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
                                            int write_red, int* __restrict__ status, int* __restrict__ istatus,
-                                           double* __restrict__ dfac) {
+                                           double* __restrict__ dfac, EvalLds& L) {
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
-    const pint_spec_t& S = *Pd.spec;
+    // the block's instance -- model structure, parameter table, per-instance constants and
+    // column runs -- staged in LDS: every row reads them, and an LDS read returns in a
+    // fraction of a global (cache) load's latency and needs no address registers
+    const int ts = Pd.spec->tstride, nrun = Pd.nrun;
+    const bool stP = ts <= EVAL_MAXTAB, stR = nrun <= EVAL_MAXRUN;
+    {
+        const int* sg = reinterpret_cast<const int*>(Pd.spec);
+        int* sd = reinterpret_cast<int*>(&L.S);
+        for (int k = threadIdx.x; k < (int)(sizeof(pint_spec_t) / 4); k += blockDim.x) sd[k] = sg[k];
+        const int* cg = reinterpret_cast<const int*>(ic + ii);
+        int* cd = reinterpret_cast<int*>(&L.C);
+        for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cg[k];
+        if (stP)
+            for (int k = threadIdx.x; k < ts; k += blockDim.x) L.P[k] = tables[I.toff + k];
+        if (stR) {
+            const int* rg = reinterpret_cast<const int*>(Pd.runs);
+            int* rd = reinterpret_cast<int*>(L.R);
+            for (int k = threadIdx.x; k < nrun * (int)(sizeof(ColRun) / 4); k += blockDim.x) rd[k] = rg[k];
+        }
+    }
+    __syncthreads();
+    const pint_spec_t& S = L.S;
     const unsigned r = (unsigned)(blk_row0[b] + threadIdx.x);
     const int n = I.n;
     if (r > (unsigned)n) return;
-    const double* P = tables + I.toff;
+    const double* P = stP ? L.P : tables + I.toff;
     ToaRow t;
     t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
     t.freq = Pd.freq[r];
@@ -271,7 +301,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
     const bool rowM = WANT_M && r < (unsigned)n;
     const bool cmp = WANT_M && compact && Pd.dsplit;
-    eval_toa<BIN>(S, P, ic[ii], t, o, rowM ? Mb : nullptr, r, n, Pd.runs, Pd.nrun, cmp);
+    eval_toa<BIN>(S, P, L.C, t, o, rowM ? Mb : nullptr, r, n, stR ? L.R : Pd.runs, nrun, cmp);
     if (rowM && cmp) dmxv[I.ooff + r] = o.dmc;
     if (o.status) {  // the batch's status word and this instance's own (pint_inst_status)
         atomicOr(status, 1 << o.status);
@@ -314,8 +344,9 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
                                               int write_red, int* __restrict__ status, int* __restrict__ istatus,
                                               double* __restrict__ dfac) {
+    __shared__ EvalLds L;
     eval_block<WANT_M, BIN>(blockIdx.x, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                            Mout, dmxv, compact, write_red, status, istatus, dfac);
+                            Mout, dmxv, compact, write_red, status, istatus, dfac, L);
 }
 
 // k_eval_mix: all binary models in one launch (heaviest first: DD, ELL1, isolated blocks),
@@ -333,15 +364,16 @@ __device__ __forceinline__ void eval_mix_body(const PsrDev* __restrict__ psrs, c
                                                   double* __restrict__ dfac) {
     const int n2 = off3 - off2, n1 = off2 - off1;
     const int b = blockIdx.x;
+    __shared__ EvalLds L;
     if (b < n2)
         eval_block<WANT_M, 2>(off2 + b, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus, dfac);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac, L);
     else if (b < n2 + n1)
         eval_block<WANT_M, 1>(off1 + b - n2, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay,
-                              delay_out, Mout, dmxv, compact, write_red, status, istatus, dfac);
+                              delay_out, Mout, dmxv, compact, write_red, status, istatus, dfac, L);
     else
         eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus, dfac);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac, L);
 }
 #define PINT_EVAL_MIX_ARGS                                                                                      \
     const PsrDev *__restrict__ psrs, const InstDev *__restrict__ insts, const int *__restrict__ blk_inst,        \
@@ -3481,7 +3513,6 @@ struct pint_ctx {
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;   // copy stream: fit outputs -> host, overlapped with compute
     hipEvent_t ev_solved = nullptr, ev_copied = nullptr;
-    bool copy_pending = false;
     hipStream_t sstream = nullptr;   // side stream: the Woodbury Sigma factor (k_sigma)
     hipEvent_t ev_gram = nullptr, ev_sigma = nullptr;
     bool sigma_pending = false;
@@ -3586,12 +3617,31 @@ struct pint_ctx {
     long tables0_cap = 0;
     bool restore_pending = false;  // pint_restore_tables not yet carried out (k_prep does it)
     double* chi2_dst = nullptr;    // lazy pint_chi2_gls: the host buffer of its deferred copy
+    // fit outputs the copy stream reads, one set per pipeline slot: a step's solve writes its
+    // slot's set while the copies of the previous step (the other slot) may still run, so the
+    // solve need not wait for them (copy_pend[slot]: copies of that slot's set in flight)
+    double *d_dpars_s[2] = {nullptr, nullptr}, *d_errs_s[2] = {nullptr, nullptr}, *d_cov_s[2] = {nullptr, nullptr};
+    double *d_chi2lin_s[2] = {nullptr, nullptr}, *d_xw_s[2] = {nullptr, nullptr}, *d_chi2g_s[2] = {nullptr, nullptr};
+    bool copy_pend[2] = {false, false};
+    int out_slot = -1;
     bool wfuse = false;            // the batch takes the fused Woodbury dots (k_resid2 tiles)
     bool wtile_valid = false;      // d_wpart holds the current residuals' dots (one split)
     double* d_wtile = nullptr;     // k_resid2's per-block trig tiles (256 per residual block)
     int wstride = 0;
     hipEvent_t ev_noise = nullptr;
 };
+
+// Point the context's fit-output buffers at pipeline slot sl's set.
+static void select_out_slot(pint_ctx* ctx, int sl) {
+    if (ctx->out_slot == sl) return;
+    ctx->out_slot = sl;
+    ctx->d_dpars = ctx->d_dpars_s[sl];
+    ctx->d_errs = ctx->d_errs_s[sl];
+    ctx->d_cov = ctx->d_cov_s[sl];
+    ctx->d_chi2lin = ctx->d_chi2lin_s[sl];
+    ctx->d_xw = ctx->d_xw_s[sl];
+    ctx->d_chi2g = ctx->d_chi2g_s[sl];
+}
 
 // Per-instance buffers (eval rows, design matrices, Gram partials: tens of GB for a large
 // grid batch) go through a process-wide cache per device: hipMalloc/hipFree of that much
@@ -3769,17 +3819,21 @@ static void free_instances(pint_ctx* ctx) {
     void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2, (void**)&ctx->d_istatus, (void**)&ctx->d_rscr,
-                   (void**)&ctx->d_chi2lin, (void**)&ctx->d_G, (void**)&ctx->d_colsq, (void**)&ctx->d_work,
-                   (void**)&ctx->d_dpars, (void**)&ctx->d_errs, (void**)&ctx->d_cov, (void**)&ctx->d_sigL,
-                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g, (void**)&ctx->d_lognorm, (void**)&ctx->d_eigw,
+                   (void**)&ctx->d_chi2lin_s[0], (void**)&ctx->d_chi2lin_s[1], (void**)&ctx->d_G, (void**)&ctx->d_colsq,
+                   (void**)&ctx->d_work, (void**)&ctx->d_dpars_s[0], (void**)&ctx->d_dpars_s[1], (void**)&ctx->d_errs_s[0],
+                   (void**)&ctx->d_errs_s[1], (void**)&ctx->d_cov_s[0], (void**)&ctx->d_cov_s[1], (void**)&ctx->d_sigL,
+                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g_s[0], (void**)&ctx->d_chi2g_s[1], (void**)&ctx->d_lognorm,
+                   (void**)&ctx->d_eigw,
                    (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
-                   (void**)&ctx->d_xw, (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
+                   (void**)&ctx->d_xw_s[0], (void**)&ctx->d_xw_s[1], (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
                    (void**)&ctx->d_wtile};
     for (auto p : ps) dfree(*p);
+    ctx->d_dpars = ctx->d_errs = ctx->d_cov = ctx->d_chi2lin = ctx->d_xw = ctx->d_chi2g = nullptr;
+    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
     ctx->noise_cap = 0;
     ctx->tables0_cap = 0;
     ctx->restore_pending = false;
@@ -4304,7 +4358,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
     HIPCHK(cmalloc((void**)&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
     HIPCHK(cmalloc((void**)&ctx->d_BFp, sizeof(double) * std::max<long>(1, vboff)));
-    if (xwoff > 0 && xwoff <= (1L << 28)) HIPCHK(cmalloc((void**)&ctx->d_xw, sizeof(double) * xwoff));
+    if (xwoff > 0 && xwoff <= (1L << 28)) {
+        HIPCHK(cmalloc((void**)&ctx->d_xw_s[0], sizeof(double) * xwoff));
+        HIPCHK(cmalloc((void**)&ctx->d_xw_s[1], sizeof(double) * xwoff));
+    }
     HIPCHK(cmalloc((void**)&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_blk_inst, sizeof(int) * bi.size()));
@@ -4353,19 +4410,26 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_istatus, sizeof(int) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_rscr, sizeof(double) * RSCR * (size_t)ninst));
     HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ninst, ctx->stream));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2g, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2g_s[0], sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2g_s[1], sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_lognorm, sizeof(double) * ninst));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2lin, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2lin_s[0], sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_chi2lin_s[1], sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_G, sizeof(double) * goff));
     HIPCHK(cmalloc((void**)&ctx->d_colsq, sizeof(double) * coff * nsplit));
     HIPCHK(cmalloc((void**)&ctx->d_work, sizeof(double) * soff));
-    HIPCHK(cmalloc((void**)&ctx->d_cov, sizeof(double) * (cvoff > 0 ? cvoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_cov_s[0], sizeof(double) * (cvoff > 0 ? cvoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_cov_s[1], sizeof(double) * (cvoff > 0 ? cvoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_sigL, sizeof(double) * soff));
-    HIPCHK(cmalloc((void**)&ctx->d_dpars, sizeof(double) * coff));
-    HIPCHK(cmalloc((void**)&ctx->d_errs, sizeof(double) * coff));
-    // the per-instance slot past the last column (K+1 stride) is never written by a solve
-    HIPCHK(hipMemsetAsync(ctx->d_dpars, 0, sizeof(double) * coff, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->d_errs, 0, sizeof(double) * coff, ctx->stream));
+    for (int sl = 0; sl < 2; sl++) {
+        HIPCHK(cmalloc((void**)&ctx->d_dpars_s[sl], sizeof(double) * coff));
+        HIPCHK(cmalloc((void**)&ctx->d_errs_s[sl], sizeof(double) * coff));
+        // the per-instance slot past the last column (K+1 stride) is never written by a solve
+        HIPCHK(hipMemsetAsync(ctx->d_dpars_s[sl], 0, sizeof(double) * coff, ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->d_errs_s[sl], 0, sizeof(double) * coff, ctx->stream));
+    }
+    ctx->out_slot = -1;
+    select_out_slot(ctx, ctx->slot);
     HIPCHK(cmalloc((void**)&ctx->d_lam, sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
@@ -4446,6 +4510,7 @@ static int check_status(pint_ctx* ctx) {
     int st = 0;
     if (flush_chi2(ctx)) return PINT_E_HIP;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
+    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -4658,9 +4723,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
-        if (ctx->copy_pending) {  // the copy stream's noise realisations read esum / eD
+        if (ctx->copy_pend[0] || ctx->copy_pend[1]) {  // the copy stream's noise realisations read esum / eD
             HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
-            ctx->copy_pending = false;
+            ctx->copy_pend[0] = ctx->copy_pend[1] = false;
         }
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
@@ -4862,9 +4927,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
         }
     }
-    if (ctx->copy_pending) {  // the previous step's outputs may still be in flight to the host
-        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
-        ctx->copy_pending = false;
+    if (ctx->copy_pend[ctx->slot]) {  // this slot's outputs may still be in flight to the host
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));  // (the latest copies: covers them)
+        ctx->copy_pend[0] = ctx->copy_pend[1] = false;
     }
     ctx->cov_pending = false;
     if (skip) {
@@ -4979,7 +5044,7 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
     if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, st));
     if (ctx->lazy) {
         HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
-        ctx->copy_pending = true;
+        ctx->copy_pend[ctx->slot] = true;
         return PINT_OK;
     }
     HIPCHK(hipStreamSynchronize(st));
@@ -5163,8 +5228,9 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
 // frozen at capture: replays re-run the same batch on whatever the buffers hold.
 static void join_side_streams(pint_ctx* ctx) {
     if (ctx->sigma_pending) hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0);
-    if (ctx->copy_pending) hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0);
-    ctx->sigma_pending = ctx->copy_pending = false;
+    if (ctx->copy_pend[0] || ctx->copy_pend[1]) hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0);
+    ctx->sigma_pending = false;
+    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
 }
 
 int pint_capture_begin(pint_ctx* ctx) {
@@ -5174,7 +5240,8 @@ int pint_capture_begin(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->cstream));
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->sigma_pending = ctx->copy_pending = false;
+    ctx->sigma_pending = false;
+    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
     HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
     ctx->capturing = true;
     return PINT_OK;
@@ -5268,6 +5335,7 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     ctx->d_status = ctx->d_status_slots + ctx->slot;
     ctx->ev = ctx->ev_slot[ctx->slot];
     ctx->rec = ctx->rec_slot[ctx->slot];
+    select_out_slot(ctx, ctx->slot);  // the next step's fit outputs (read them before step_end)
     // (the new slot's event flags still belong to its previous step, which the caller checks
     // next: pint_check_step reads and clears them)
     *slot = s;
@@ -5280,6 +5348,7 @@ int pint_check_step(pint_ctx* ctx, int s) {
     HIPCHK(hipEventSynchronize(ctx->ev_done[s]));
     if (ctx->cdone_rec[s]) HIPCHK(hipEventSynchronize(ctx->ev_cdone[s]));
     ctx->cdone_rec[s] = false;
+    ctx->copy_pend[s] = false;  // its output copies are complete
     const int st = ctx->h_status[s];
     if (st) {
         ctx->h_status[s] = 0;
@@ -5382,7 +5451,7 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
     if (ctx->lazy) {
         HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
-        ctx->copy_pending = true;
+        ctx->copy_pend[ctx->slot] = true;
         return PINT_OK;
     }
     HIPCHK(hipStreamSynchronize(st));
