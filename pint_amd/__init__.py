@@ -12,6 +12,6 @@ from .residuals import Residuals, WidebandDMResiduals, WidebandTOAResiduals  # n
 from .fitter import (Fitter, WLSFitter, GLSFitter, DownhillWLSFitter, DownhillGLSFitter, WidebandTOAFitter,  # noqa: F401
                      WidebandDownhillFitter,  # noqa: F401
                      MaxiterReached, StepProblem, InvalidModelParameters, CorrelatedErrors)
-from .gridutils import grid_chisq  # noqa: F401
+from .gridutils import grid_chisq, grid_chisq_derived, tuple_chisq, tuple_chisq_derived  # noqa: F401
 
 __version__ = "0.1.0"

@@ -1,4 +1,5 @@
-"""grid_chisq (reference gridutils.py:166-389) on the GPU.
+"""grid_chisq, grid_chisq_derived, tuple_chisq and tuple_chisq_derived (reference
+gridutils.py:166-966) on the GPU.
 
 Every grid point is one parameter-table instance; all points of a rank are fitted by one
 batched launch sequence (BatchFit).  Semantics follow the reference's *parallel* path
@@ -141,19 +142,22 @@ def point_tables(lay, base_table, parnames, flat, c0, c1):
     return tabs
 
 
-def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
-               executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
-    """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
-    Returns (chi2 array of meshgrid shape, dict of meshgrid-shaped extra parameter arrays).
-    `executor`, `ncpu`, `chunksize` are accepted for API compatibility: the points run as one
-    GPU batch per rank instead of a process pool.  With torch.distributed initialised, rank
-    r fits the r-th contiguous block of the flattened meshgrid and the blocks are
-    all-gathered, so every rank returns the whole grid."""
+def _as_ld(v):
+    """A grid coordinate as longdouble: plain numbers, numpy arrays, or anything carrying a
+    `.value` in the parameter's own unit (the reference passes astropy Quantities)."""
+    return np.asarray(getattr(v, "value", v), dtype=np.longdouble)
+
+
+def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
+                extraparnames: Sequence[str], fitargs):
+    """Fit every point of `flat` (one longdouble array of values per parameter in
+    `parnames`, all of one length) with `parnames` frozen; returns the flat chi2 array and a
+    dict of flat extra-parameter arrays, every rank holding all points.  The shared body of
+    the four grid entry points (gridutils.py:166/:392/:588/:773, parallel path: a cold
+    start from the input fitter's model at every point, gridutils.py:72)."""
     from .engine import pack_table
     mode, down = _fit_kind(ftr)
-    out, flat = grid_points(parvalues)
-    shape = out[0].shape
-    npts = flat[0].size
+    npts = int(flat[0].size) if len(flat) else 0
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     per, lo, hi = shard_range(npts, rank, world)
@@ -186,8 +190,61 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     # (gridutils.py:107-110 reads them outside the try); a point taken out of the batch as
     # invalid has none (NaN, final_tables_flat)
     chi2_all = gather_blocks(chi2, per, npts, dist)
-    extra_all = {e: gather_blocks(extra[e], per, npts, dist).reshape(shape) for e in extraparnames}
-    return chi2_all.reshape(shape), extra_all
+    extra_all = {e: gather_blocks(extra[e], per, npts, dist) for e in extraparnames}
+    return chi2_all, extra_all
+
+
+def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
+               executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
+    """chi2 over the meshgrid of `parvalues` with `parnames` frozen (gridutils.py:166).
+    Returns (chi2 array of meshgrid shape, dict of meshgrid-shaped extra parameter arrays).
+    `executor`, `ncpu`, `chunksize` are accepted for API compatibility: the points run as one
+    GPU batch per rank instead of a process pool.  With torch.distributed initialised, rank
+    r fits the r-th contiguous block of the flattened meshgrid and the blocks are
+    all-gathered, so every rank returns the whole grid."""
+    out, flat = grid_points(parvalues)
+    shape = out[0].shape
+    chi2, extra = _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
+    return chi2.reshape(shape), {e: v.reshape(shape) for e, v in extra.items()}
+
+
+def grid_chisq_derived(ftr, parnames: Sequence[str], parfuncs: Sequence, gridvalues: Sequence,
+                       extraparnames: List[str] = [], executor=None, ncpu=None, chunksize=1,
+                       printprogress=False, **fitargs):
+    """chi2 over the meshgrid of `gridvalues`, each point's fitted parameters `parnames` set to
+    `parfuncs[j](*grid)` (gridutils.py:392-585): e.g. a grid in (F0, tau) fitting F0 and
+    F1 = -F0 / 2 tau.  Returns (chi2 of meshgrid shape, [parameter value arrays of meshgrid
+    shape, one per parfunc], dict of meshgrid-shaped extras).  The functions see longdouble
+    meshgrids; the extras follow the reference's parallel path (one array entry per point --
+    its serial path keeps only the last point's value, gridutils.py:580-581)."""
+    grid = np.meshgrid(*[_as_ld(v) for v in gridvalues])
+    shape = grid[0].shape
+    out = [np.broadcast_to(np.asarray(f(*grid)), shape) for f in parfuncs]
+    flat = [_as_ld(o).reshape(-1) for o in out]
+    chi2, extra = _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
+    return chi2.reshape(shape), out, {e: v.reshape(shape) for e, v in extra.items()}
+
+
+def tuple_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames: List[str] = [],
+                executor=None, ncpu=None, chunksize=1, printprogress=False, **fitargs):
+    """chi2 at each tuple of `parvalues` (one value per name of `parnames`, any set of points:
+    gridutils.py:588-770).  Returns (chi2 of length len(parvalues), dict of extra-parameter
+    arrays of that length).  Multi-GPU: the list is split into contiguous blocks, one per
+    rank, exactly like the flattened meshgrid of grid_chisq."""
+    flat = [_as_ld([pv[j] for pv in parvalues]).reshape(-1) for j in range(len(parnames))]
+    return _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
+
+
+def tuple_chisq_derived(ftr, parnames: Sequence[str], parfuncs: Sequence, parvalues: Sequence,
+                        extraparnames: List[str] = [], executor=None, ncpu=None, chunksize=1,
+                        printprogress=False, **fitargs):
+    """chi2 at each tuple of `parvalues`, the fitted parameters `parnames` set to
+    `[f(*tuple) for f in parfuncs]` (gridutils.py:773-966).  Returns (chi2, the list of
+    per-point parameter value lists, dict of extras)."""
+    out = [[f(*pv) for f in parfuncs] for pv in parvalues]
+    flat = [_as_ld([o[j] for o in out]).reshape(-1) for j in range(len(parnames))]
+    chi2, extra = _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
+    return chi2, out, extra
 
 
 def best_point(chi2, parnames: Sequence[str], parvalues: Sequence):

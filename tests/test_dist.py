@@ -101,6 +101,69 @@ def test_grid_chisq_two_ranks_gloo():
     assert np.isnan(want).any() and not np.isnan(want).all()
 
 
+_FUNCS = (lambda x, y: x, lambda x, y: -x / 2 / y)
+
+
+def _tuple_args():
+    f, (g0, g1) = _grid_args()
+    pts = list(zip(g0[[0, 3, 1, 4, 2, 2, 0]], g1[[4, 0, 3, 1, 2, 0, 1]]))   # 7 points: blocks 4 + 3
+    tau = -g0[2] / (2 * g1[[0, 1, 2, 3, 4, 2, 1]])
+    dpts = list(zip(g0[[0, 1, 2, 3, 4, 0, 1]], tau))
+    return f, pts, dpts
+
+
+def _tuple_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    import pint_amd.gridutils as gu
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _stub_grid(gu)
+        f, pts, dpts = _tuple_args()
+        c2, ex = gu.tuple_chisq(f, ("F0", "F1"), pts, extraparnames=["DM"])
+        d2, out, dex = gu.tuple_chisq_derived(f, ("F0", "F1"), _FUNCS, dpts, extraparnames=["DM"])
+        g0 = np.unique([p[0] for p in dpts])
+        gd, gout, gex = gu.grid_chisq_derived(f, ("F0", "F1"), _FUNCS, (g0, np.unique([p[1] for p in dpts])))
+        q.put((rank, (c2, ex["DM"], d2, dex["DM"], gd)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tuple_chisq_two_ranks_gloo():
+    """tuple_chisq / tuple_chisq_derived / grid_chisq_derived (gridutils.py:588/:773/:392)
+    split into contiguous per-rank blocks and all-gathered: every rank returns exactly the
+    one-process result, in list order."""
+    out = _spawn(_tuple_worker)
+    import pint_amd.gridutils as gu
+    _stub_grid(gu)
+    f, pts, dpts = _tuple_args()
+    want, wex = gu.tuple_chisq(f, ("F0", "F1"), pts, extraparnames=["DM"])
+    assert want.shape == (7,) and wex["DM"].shape == (7,)
+    # a tuple list is the same fit as the grid points it names
+    for k, (x, y) in enumerate(pts):
+        one, _ = gu.grid_chisq(f, ("F0", "F1"), (np.array([x]), np.array([y])))
+        np.testing.assert_array_equal(one.reshape(-1), want[k:k + 1])
+    dwant, dout, dwex = gu.tuple_chisq_derived(f, ("F0", "F1"), _FUNCS, dpts, extraparnames=["DM"])
+    assert len(dout) == 7 and all(len(o) == 2 for o in dout)
+    for (x, y), o in zip(dpts, dout):
+        assert o[0] == x and o[1] == -x / 2 / y
+    g0 = np.unique([p[0] for p in dpts])
+    gt = np.unique([p[1] for p in dpts])
+    gwant, gout, _ = gu.grid_chisq_derived(f, ("F0", "F1"), _FUNCS, (g0, gt))
+    assert gwant.shape == (len(gt), len(g0)) and gout[1].shape == gwant.shape
+    G0, GT = np.meshgrid(g0, gt)
+    np.testing.assert_array_equal(gout[1], -G0 / 2 / GT)
+    for rank, (c2, dm, d2, ddm, gd) in out.items():
+        np.testing.assert_array_equal(c2, want)
+        np.testing.assert_array_equal(dm, wex["DM"])
+        np.testing.assert_array_equal(d2, dwant)
+        np.testing.assert_array_equal(ddm, dwex["DM"])
+        np.testing.assert_array_equal(gd, gwant)
+    assert np.isnan(want).any() and not np.isnan(want).all()
+
+
 # ---- PTA sharding -------------------------------------------------------------------------
 def test_lpt_shard_properties():
     from pint_amd.pta import lpt_shard

@@ -6,11 +6,12 @@ longdouble rounding), design matrix 1e-9 relative per column, fitted parameters 
 sigma, chi2 1e-9 relative stage-wise (the end-to-end chi2 floor is documented in
 tests/test_oracle_golden.py::test_gls_fit)."""
 import copy
+import os
 
 import numpy as np
 import pytest
 
-from golden_util import downhill_bar, load, ref_value
+from golden_util import GOLDEN, downhill_bar, load, ref_value
 
 import pint_oracle as O
 
@@ -228,6 +229,48 @@ def test_grid_chisq_ngc():
     finally:
         gridutils.GRID_MAX_POINTS = old
     assert np.allclose(c2c, c2, rtol=1e-12, atol=0)
+
+
+def _ld(z, k):
+    return z[k + "_hi"].astype(np.longdouble) + z[k + "_lo"]
+
+
+def test_grid_tuple_variants_ngc():
+    """grid_chisq_derived / tuple_chisq / tuple_chisq_derived (gridutils.py:392/:588/:773)
+    against the reference's parallel-path outputs (oracle/refgen/gen_tuple.py): chi2 at
+    rtol 1e-7 (the grid_chisq bar), the fitted extra DM within 1e-3 sigma, the derived
+    F1 = -F0/2tau values to the longdouble ulp."""
+    from pint_amd import WLSFitter
+    from pint_amd.gridutils import grid_chisq_derived, tuple_chisq, tuple_chisq_derived
+    model, toas, _, meta = load("ngc6440e")
+    z = np.load(os.path.join(GOLDEN, "grid_tuple.npz"))
+    f = WLSFitter(toas, model)
+    f.fit_toas(maxiter=1)
+    sdm = meta["wls_errors"]["DM"]
+    funcs = (lambda x, y: x, lambda x, y: -x / 2 / y)
+
+    c2, out, ex = grid_chisq_derived(f, ("F0", "F1"), funcs, (_ld(z, "gd_F0"), _ld(z, "gd_tau")),
+                                     extraparnames=["DM"])
+    assert c2.shape == z["gd_chi2"].shape == out[1].shape == ex["DM"].shape
+    np.testing.assert_allclose(c2, z["gd_chi2"], rtol=1e-7, atol=0)
+    d = np.abs(out[1].astype(np.longdouble) / _ld(z, "gd_out_F1") - 1)
+    assert float(d.max()) < 4 * np.finfo(np.longdouble).eps
+    assert float(np.max(np.abs(ex["DM"] - z["gd_DM_hi"]))) < 1e-3 * sdm
+
+    pts = list(zip(_ld(z, "tp_F0"), _ld(z, "tp_F1")))
+    c2, ex = tuple_chisq(f, ("F0", "F1"), pts, extraparnames=["DM"])
+    assert c2.shape == (len(pts),)
+    np.testing.assert_allclose(c2, z["tp_chi2"], rtol=1e-7, atol=0)
+    assert float(np.max(np.abs(ex["DM"] - z["tp_DM_hi"]))) < 1e-3 * sdm
+
+    pts = list(zip(_ld(z, "td_F0"), _ld(z, "td_tau")))
+    c2, out, ex = tuple_chisq_derived(f, ("F0", "F1"), funcs, pts, extraparnames=["DM"])
+    np.testing.assert_allclose(c2, z["td_chi2"], rtol=1e-7, atol=0)
+    f1 = np.array([o[1] for o in out], dtype=np.longdouble)
+    assert float(np.max(np.abs(f1 / _ld(z, "td_out_F1") - 1))) < 4 * np.finfo(np.longdouble).eps
+    assert float(np.max(np.abs(ex["DM"] - z["td_DM_hi"]))) < 1e-3 * sdm
+    # the model the fitter holds is untouched by the grids (gridutils.py:383-386 restore)
+    assert not f.model["F0"].frozen and not f.model["F1"].frozen
 
 
 # ---- seeded perturbations against the oracle --------------------------------------------
