@@ -57,6 +57,9 @@ typedef struct {
     const uint32_t *flags;          /* n+1 bit0: barycentric obs, bit1: all ssb_obs_pos != 0 */
     const uint64_t *jump_mask;      /* n+1 bit k: JUMP k selects this TOA               */
     const int32_t *dmx_a, *dmx_b;   /* n+1 DMX bin indices (-1 none; two allow overlap) */
+    const double *planet_km;        /* (n+1)*15 obs_<planet>_pos for jupiter, saturn, venus,
+                                       uranus, neptune (toa.py:2403-2433); read only when
+                                       spec.shapiro == 2, may be NULL otherwise             */
 } pint_toas_t;
 
 /* ---- model structure ------------------------------------------------------------ */
@@ -83,7 +86,8 @@ enum { PINT_BIN_NONE = 0, PINT_BIN_ELL1 = 1, PINT_BIN_DD = 2, PINT_BIN_ELL1H = 3
 typedef struct {
     int32_t nf;             /* spin terms F0..F{nf-1}                                   */
     int32_t astrometry;     /* 0 none, 1 equatorial (RAJ/DECJ), 2 ecliptic (ELONG/ELAT) */
-    int32_t shapiro;        /* SolarSystemShapiro present (sun only)                    */
+    int32_t shapiro;        /* SolarSystemShapiro: 0 absent, 1 the Sun, 2 the Sun and the
+                               PLANET_SHAPIRO planets (solar_system_shapiro.py:105-117)    */
     int32_t ndm;            /* DispersionDM taylor terms (0 = component absent)         */
     int32_t ndmx;           /* DMX bins                                                 */
     int32_t binary;         /* PINT_BIN_*: 0 none, 1 ELL1, 2 DD, 3 ELL1H, 4 BT, 5 DDK   */

@@ -37,6 +37,10 @@ C_KMS = 299792.458
 AU_KM = 149597870.7
 KPC_KM = 3.0856775814913674e16
 TSUN = 4.92549094830932e-06
+# M_sun / M_planet of the PLANET_SHAPIRO planets (pint/__init__.py:84-90), summation order of
+# solar_system_shapiro.py:112
+PLANETS = (("jupiter", 1047.3486), ("saturn", 3497.898), ("venus", 408523.71), ("uranus", 22902.98),
+           ("neptune", 19412.24))
 DMCONST = 4149.377593360996
 DAYSEC = 86400.0
 DJY = 365.25
@@ -121,10 +125,13 @@ def _rows(toas: dict, tzr: bool):
     """Concatenate TOA rows and the TZR row (as the product does) -> dict of arrays."""
     keys = ["tdb_hi", "tdb_lo", "freq_mhz", "ssb_obs_pos_km", "ssb_obs_vel_kms", "obs_sun_pos_km", "mjd_float",
             "is_bary", "delta_pulse_number"]
+    keys = keys + [f"obs_{pl}_pos_km" for pl, _ in PLANETS if f"obs_{pl}_pos_km" in toas]
     out = {}
     for k in keys:
         a = np.asarray(toas[k])
-        if tzr:
+        if tzr and k not in toas["tzr"] and k.startswith("obs_") and k != "obs_sun_pos_km":
+            a = np.concatenate([a, np.zeros((1, 3))])   # a barycentric TZR TOA carries no planets
+        elif tzr:
             b = np.asarray(toas["tzr"][k], dtype=a.dtype).reshape((1,) + a.shape[1:])
             a = np.concatenate([a, b])
         out[k] = a
@@ -166,6 +173,9 @@ def toas_from_fixture(z: dict, meta: dict) -> dict:
     d = {k: np.asarray(z[k]) for k in ("tdb_hi", "tdb_lo", "freq_mhz", "err_us", "ssb_obs_pos_km",
                                        "ssb_obs_vel_kms", "obs_sun_pos_km", "mjd_float", "is_bary",
                                        "delta_pulse_number")}
+    for pl, _ in PLANETS:
+        if f"obs_{pl}_pos_km" in z:
+            d[f"obs_{pl}_pos_km"] = np.asarray(z[f"obs_{pl}_pos_km"])
     if "pulse_number" in z:
         d["pulse_number"] = np.asarray(z["pulse_number"])
     d["flags"] = meta.get("flag_columns", {})
@@ -823,6 +833,12 @@ def evaluate(om: OModel, toas: dict, with_tzr=True):
         r = np.linalg.norm(sun, axis=1)
         rct = (sun * L).sum(1)
         d = np.where(nb, -2.0 * TSUN * np.log((r - rct) / AU_KM), 0.0)
+        if om.v("PLANET_SHAPIRO"):
+            # solar_system_shapiro.py:110-117: each planet's term added in this order
+            for pl, ratio in PLANETS:
+                pp = R[f"obs_{pl}_pos_km"]
+                rp = np.linalg.norm(pp, axis=1)
+                d = d + np.where(nb, -2.0 * (TSUN / ratio) * np.log((rp - (pp * L).sum(1)) / AU_KM), 0.0)
         out["shapiro"] = d
         delay += d
     bfreq = R["freq_mhz"] * (1.0 - (vel * L).sum(1) / C_KMS) if astro else R["freq_mhz"]

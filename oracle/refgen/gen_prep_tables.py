@@ -17,6 +17,12 @@ astropy 4.3.1, pyerfa 2.0.0, ephem="builtin", IERS-B bundled with astropy):
 * earth          : erfa.epv00 barycentric Earth position (km) / velocity (km/s) at TDB,
                    0.25-day grid (6-point Lagrange: < 2 cm)
 * sun            : Sun barycentric position/velocity (epv00 pvb - pvh), 1-day grid
+* venus, jupiter, saturn, uranus, neptune
+                 : barycentric positions (km) as astropy 4.3's builtin
+                   get_body_barycentric_posvel forms them (erfa.plan94 heliocentric + the
+                   Sun's epv00 barycentric vector) for compute_posvels(planets=True)
+                   (toa.py:2403-2433); Venus on a 1-day grid, the outer planets on 4 days
+                   (6-point Lagrange: < 10 m, checked below)
 Usage: run_ref.sh gen_prep_tables.py
 """
 import os
@@ -30,6 +36,15 @@ REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 AU_KM = 149597870.7
 DAYSEC = 86400.0
 M0, M1 = 49900.0, 60600.0
+
+
+def planet_bary_km(mjd, idx):
+    """astropy 4.3 _get_body_barycentric_posvel for ephemeris 'builtin': erfa.plan94
+    heliocentric position plus the Sun's barycentric one (epv00 pvb - pvh), au -> km."""
+    j1 = np.full_like(mjd, 2400000.5)
+    pvh, pvb = erfa.epv00(j1, mjd)
+    pl = erfa.plan94(j1, mjd, idx)
+    return (pl["p"] + pvb["p"] - pvh["p"]) * AU_KM
 
 
 def main():
@@ -79,10 +94,30 @@ def main():
     g1 = np.arange(M0, M1 + 1e-9, 1.0)
     pvh1, pvb1 = erfa.epv00(np.full_like(g1, 2400000.5), g1)
     sun = np.column_stack([(pvb1["p"] - pvh1["p"]) * AU_KM, (pvb1["v"] - pvh1["v"]) * AU_KM / DAYSEC])
+    planets = {}
+    for name, idx, step in (("venus", 2, 1.0), ("jupiter", 5, 4.0), ("saturn", 6, 4.0), ("uranus", 7, 4.0),
+                            ("neptune", 8, 4.0)):
+        gp = np.arange(M0, M1 + 1e-9, step)
+        planets[name] = planet_bary_km(gp, idx)
+        planets[name + "_t0"], planets[name + "_dt"] = M0, step
+        # 6-point Lagrange (nodes i-2..i+3, as pint_amd.prep._lagrange6) at random epochs
+        tt = rng.uniform(M0 + 3 * step, M1 - 4 * step, 300)
+        xg = (tt - M0) / step
+        i = np.floor(xg).astype(int)
+        uu = xg - i
+        est = 0.0
+        for k in range(-2, 4):
+            w = np.ones_like(uu)
+            for m in range(-2, 4):
+                if m != k:
+                    w = w * (uu - m) / (k - m)
+            est = est + w[:, None] * planets[name][i + k]
+        err = np.max(np.abs(est - planet_bary_km(tt, idx)))
+        assert err < 1e-2, (name, err)
     out = os.path.join(REPO, "pint_amd", "data", "prep_tables.npz")
     np.savez_compressed(out, leap=leap, iers=iers_tab, cip_t0=M0, cip_dt=0.5, cip=np.column_stack([x, y, s]),
                         dtdb_t0=M0, dtdb_dt=0.5, dtdb=np.column_stack([G, C, S, B]),
-                        earth_t0=M0, earth_dt=0.25, earth=earth, sun_t0=M0, sun_dt=1.0, sun=sun,
+                        earth_t0=M0, earth_dt=0.25, earth=earth, sun_t0=M0, sun_dt=1.0, sun=sun, **planets,
                         source=np.array("astropy 4.3.1 / pyerfa 2.0.0 (ephem builtin, IERS-B), "
                                         "oracle/refgen/gen_prep_tables.py"))
     print("wrote", out, os.path.getsize(out), "iers", iers_tab[0, 0], iers_tab[-1, 0], file=sys.stderr)

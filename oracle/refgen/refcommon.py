@@ -76,6 +76,9 @@ def pack_toas(toas, model=None):
         out["delta_pulse_number"] = np.asarray(t["delta_pulse_number"], dtype=np.float64)
     else:
         out["delta_pulse_number"] = np.zeros(len(t))
+    for pl in ("jupiter", "saturn", "venus", "uranus", "neptune", "earth"):   # planets=True (toa.py:2403)
+        if f"obs_{pl}_pos" in t.colnames:
+            out[f"obs_{pl}_pos_km"] = np.asarray(t[f"obs_{pl}_pos"].quantity.to_value(u.km), dtype=np.float64)
     if "ssb_obs_vel_ecl" in t.colnames:
         out["ssb_obs_vel_ecl_kms"] = np.asarray(t["ssb_obs_vel_ecl"].quantity.to_value(u.km / u.s),
                                                 dtype=np.float64)

@@ -13,6 +13,10 @@ constexpr double C_KMS = 299792.458;              // c, km/s
 constexpr double AU_KM = 149597870.7;             // astropy au
 constexpr double KPC_KM = 3.0856775814913674e16;  // 1 kpc in km
 constexpr double TSUN = 4.92549094830932e-06;     // GM_sun/c^3 (s), pint/__init__.py:80
+// GM/c^3 of jupiter, saturn, venus, uranus, neptune: Tsun / (M_sun / M_planet) rounded once,
+// as pint/__init__.py:84-90 forms them
+__device__ __constant__ const double TPLANET[5] = {TSUN / 1047.3486, TSUN / 3497.898, TSUN / 408523.71, TSUN / 22902.98,
+                               TSUN / 19412.24};
 constexpr double DMCONST = 4149.377593360996;     // 1/2.41e-4 MHz^2 s cm^3/pc, :68
 constexpr double DAYSEC = 86400.0;
 constexpr double DJY = 365.25;
@@ -954,6 +958,7 @@ struct ToaRow {
     dd tdb;
     double freq;
     double pos[3], vel[3], sun[3];
+    const double* planet;  // 15: observatory -> jupiter, saturn, venus, uranus, neptune (km), or null
     uint32_t flags;
     uint64_t jmask;
     int dmx_a, dmx_b;
@@ -1026,11 +1031,22 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
             delay += d;
         }
     }
-    // ---- solar system Shapiro (solar_system_shapiro.py:59-124), sun only ----
+    // ---- solar system Shapiro (solar_system_shapiro.py:59-124): the Sun, and with
+    //      PLANET_SHAPIRO (shapiro == 2) the five planets of :112 summed in that order ----
     if (S.shapiro && !is_bary) {
         double rs = sqrt(t.sun[0] * t.sun[0] + t.sun[1] * t.sun[1] + t.sun[2] * t.sun[2]);
         double rct = t.sun[0] * L[0] + t.sun[1] * L[1] + t.sun[2] * L[2];
-        delay += -2.0 * TSUN * log((rs - rct) * INV_AU_KM);
+        double ds = -2.0 * TSUN * log((rs - rct) * INV_AU_KM);
+        if (S.shapiro == 2) {
+#pragma unroll 1
+            for (int q = 0; q < 5; q++) {
+                const double x = t.planet[3 * q], y = t.planet[3 * q + 1], z = t.planet[3 * q + 2];
+                const double rp = sqrt(x * x + y * y + z * z);
+                const double rcp = x * L[0] + y * L[1] + z * L[2];
+                ds += -2.0 * TPLANET[q] * log((rp - rcp) * INV_AU_KM);
+            }
+        }
+        delay += ds;
     }
     // ---- barycentric radio frequency (astrometry.py:359-364) ----
     double bfreq = t.freq;

@@ -44,6 +44,7 @@ using gptr = const T __attribute__((address_space(1)))*;
 // ---------------------------------------------------------------------------------
 struct PsrDev {
     const double *tdb_hi, *tdb_lo, *freq, *sigma, *isig, *pos, *vel, *sun, *pn, *dpn;
+    const double* planet;    // (n+1) x 15 observatory -> planet vectors (spec shapiro == 2), else null
     const uint32_t* flags;
     const uint64_t* jmask;
     const int32_t *dmx_a, *dmx_b;
@@ -293,6 +294,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
         t.vel[k] = Pd.vel[3 * r + k];
         t.sun[k] = Pd.sun[3 * r + k];
     }
+    t.planet = S.shapiro == 2 ? Pd.planet + 15 * r : nullptr;
     t.flags = Pd.flags[r];
     t.jmask = Pd.jmask[r];
     t.dmx_a = Pd.dmx_a[r];
@@ -3926,6 +3928,10 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->pos_km, 3 * (n + 1), d.pos);
     rc |= upload(ctx, ph, t->vel_kms, 3 * (n + 1), d.vel);
     rc |= upload(ctx, ph, t->sun_km, 3 * (n + 1), d.sun);
+    if (spec->shapiro == 2) {
+        if (!t->planet_km) { ctx->err = "PLANET_SHAPIRO needs the planet positions (planet_km)"; return -PINT_E_INVALID; }
+        rc |= upload(ctx, ph, t->planet_km, (size_t)15 * (n + 1), d.planet);
+    }
     rc |= upload(ctx, ph, t->pulse_number, n, d.pn);
     rc |= upload(ctx, ph, t->delta_pn, n + 1, d.dpn);
     rc |= upload(ctx, ph, t->flags, n + 1, d.flags);

@@ -112,7 +112,9 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.o_px = place("PX")
         if model.POSEPOCH.value is not None:
             spec.o_POSEPOCH = place("POSEPOCH")
-        spec.shapiro = 1 if "SolarSystemShapiro" in model.components else 0
+        spec.shapiro = 0
+        if "SolarSystemShapiro" in model.components:
+            spec.shapiro = 2 if ("PLANET_SHAPIRO" in model and model.PLANET_SHAPIRO.value) else 1
         if ak == 2:
             spec.obliquity = OBLIQUITY[str(model.ECL.value or "IERS2010")]
     dms = model.dm_terms()
@@ -337,11 +339,39 @@ def pack_toas(lay: PulsarLayout):
                 db[i] = j
             else:
                 raise NotImplementedError("more than two overlapping DMX bins on one TOA")
-    keep = [tdb_hi, tdb_lo, freq, sigma_s, pos, vel, sun, pn, dpn, flags, jm, da, db]
+    planet = None
+    if lay.spec.shapiro == 2:
+        planet = planet_rows(toas, tz, is_bary)
+    keep = [tdb_hi, tdb_lo, freq, sigma_s, pos, vel, sun, pn, dpn, flags, jm, da, db, planet]
     t = L.ToasT(n, L.ptr(tdb_hi), L.ptr(tdb_lo), L.ptr(freq), L.ptr(sigma_s), L.ptr(pos), L.ptr(vel), L.ptr(sun),
                 L.ptr(pn), L.ptr(dpn), L.ptr(flags, C.c_uint32), L.ptr(jm, C.c_uint64), L.ptr(da, C.c_int32),
-                L.ptr(db, C.c_int32))
+                L.ptr(db, C.c_int32), L.ptr(planet) if planet is not None else None)
     return t, keep
+
+
+SHAPIRO_PLANETS = ("jupiter", "saturn", "venus", "uranus", "neptune")   # solar_system_shapiro.py:112
+
+
+def planet_rows(toas, tz, is_bary) -> np.ndarray:
+    """(n+1, 15) observatory -> planet vectors (km) of the TOAs and the TZR TOA for
+    PLANET_SHAPIRO; like the reference (solar_system_shapiro.py:118-122) missing columns are
+    a KeyError naming planets=True.  A barycentric TZR TOA needs none (its Shapiro delay is
+    not evaluated, :100)."""
+    cols = []
+    for pl in SHAPIRO_PLANETS:
+        k = f"obs_{pl}_pos_km"
+        if k not in toas.arrays:
+            raise KeyError("Planet positions not found when trying to compute Solar System Shapiro delay. "
+                           "Make sure that you include `planets=True` in your `get_TOAs()` call, or use "
+                           "`get_model_and_toas()`.")
+        if k in tz:
+            b = np.asarray(tz[k], dtype=np.float64).reshape(1, 3)
+        elif is_bary[-1]:
+            b = np.zeros((1, 3))
+        else:
+            raise KeyError(f"the TZR TOA has no {k} (prepare it with planets=True)")
+        cols.append(np.concatenate([np.asarray(toas.arrays[k], dtype=np.float64), b]))
+    return np.ascontiguousarray(np.concatenate(cols, axis=1))
 
 
 def make_tzr_row(model, toas) -> dict:

@@ -149,6 +149,15 @@ def sun_posvel(tdb: np.ndarray):
     return _posvel("sun", tdb)
 
 
+PLANETS = ("jupiter", "saturn", "venus", "uranus", "neptune")   # solar_system_shapiro.py:112
+
+
+def planet_pos(name: str, tdb: np.ndarray) -> np.ndarray:
+    """objPosVel_wrt_SSB(name, tdb, "builtin").pos (km): astropy's builtin planets (erfa.plan94
+    heliocentric + the Sun's barycentric vector), tabulated."""
+    return _lagrange6(name, tdb)
+
+
 # ---------------------------------------------------------------------------------------
 # Earth orientation (astropy 4.3 EarthLocation.get_gcrs_posvel via CIRS)
 # ---------------------------------------------------------------------------------------
@@ -262,11 +271,13 @@ def _geodetic_args(itrf_m):
 # ---------------------------------------------------------------------------------------
 # the whole preparation
 # ---------------------------------------------------------------------------------------
-def prepare(day: np.ndarray, frac: np.ndarray, obs: Sequence[str], corr_s: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
+def prepare(day: np.ndarray, frac: np.ndarray, obs: Sequence[str], corr_s: Optional[np.ndarray] = None,
+            planets: bool = False) -> Dict[str, np.ndarray]:
     """Per-TOA boundary columns (pint_amd.toa FIELDS) for MJD (day, fraction) in each site's
     time scale (UTC for observatories and the geocenter, TDB for the barycenter), after
     adding clock corrections corr_s (s): tdb_hi/lo, mjd_float, ssb_obs_pos/vel, obs_sun_pos,
-    is_bary."""
+    is_bary; with planets=True also obs_<planet>_pos for the Shapiro planets and the Earth
+    (toa.py:2403-2433: the body's barycentric position minus the observatory's)."""
     n = len(day)
     day = np.asarray(day, dtype=np.float64)
     frac = np.asarray(frac, dtype=np.float64)
@@ -304,5 +315,11 @@ def prepare(day: np.ndarray, frac: np.ndarray, obs: Sequence[str], corr_s: Optio
     sp, _ = sun_posvel(tdb.astype(np.float64))
     hi = tdb.astype(np.float64)
     lo = (tdb - LD(hi)).astype(np.float64)
-    return {"tdb_hi": hi, "tdb_lo": lo, "mjd_float": mjd_float, "ssb_obs_pos_km": pos, "ssb_obs_vel_kms": vel,
-            "obs_sun_pos_km": sp - pos, "is_bary": is_bary}
+    out = {"tdb_hi": hi, "tdb_lo": lo, "mjd_float": mjd_float, "ssb_obs_pos_km": pos, "ssb_obs_vel_kms": vel,
+           "obs_sun_pos_km": sp - pos, "is_bary": is_bary}
+    if planets:
+        tf = tdb.astype(np.float64)
+        for pl in PLANETS:
+            out[f"obs_{pl}_pos_km"] = planet_pos(pl, tf) - pos
+        out["obs_earth_pos_km"] = earth_posvel(tf)[0] - pos
+    return out

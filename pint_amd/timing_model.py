@@ -180,8 +180,6 @@ class TimingModel:
             if len(self.dm_terms()) > 1 and any(self[n].value for n in self.dm_terms()[1:]):
                 if self.DMEPOCH.value is None:
                     self.DMEPOCH.value = LD(self.PEPOCH.value)  # dispersion_model.py:197
-        if "PLANET_SHAPIRO" in self and self.PLANET_SHAPIRO.value:
-            raise NotImplementedError("PLANET_SHAPIRO Y is outside the supported hot path")
         if "NE_SW" in self and self.NE_SW.value:
             raise NotImplementedError("solar-wind dispersion (NE_SW != 0) is outside the supported hot path")
         if "CORRECT_TROPOSPHERE" in self and self.CORRECT_TROPOSPHERE.value:

@@ -22,6 +22,8 @@ import numpy as np
 
 FIELDS = ["tdb_hi", "tdb_lo", "freq_mhz", "err_us", "ssb_obs_pos_km", "ssb_obs_vel_kms", "obs_sun_pos_km",
           "mjd_float", "is_bary", "delta_pulse_number"]
+# compute_posvels(planets=True) columns (toa.py:96 all_planets, :2403-2433)
+PLANET_FIELDS = [f"obs_{p}_pos_km" for p in ("jupiter", "saturn", "venus", "uranus", "neptune", "earth")]
 
 
 class TOAs:
@@ -50,6 +52,11 @@ class TOAs:
         self._uid = id(self)
 
     # -- reference-like accessors ------------------------------------------------------
+    @property
+    def planets(self) -> bool:
+        """Planet positions present (toa.py:1336 TOAs.planets / compute_posvels(planets=True))."""
+        return all(k in self.arrays for k in PLANET_FIELDS)
+
     @property
     def ntoas(self) -> int:
         return len(self.arrays["tdb_hi"])
@@ -182,7 +189,7 @@ class TOAs:
 
 
 def from_arrays_with_tzr(z: Dict[str, np.ndarray], flag_columns=None, name="", obs_names=None) -> TOAs:
-    arrays = {k: np.asarray(z[k]) for k in z if not k.startswith("tzr_") and (k in FIELDS or k in (
+    arrays = {k: np.asarray(z[k]) for k in z if not k.startswith("tzr_") and (k in FIELDS or k in PLANET_FIELDS or k in (
         "pulse_number", "ssb_obs_vel_ecl_kms"))}
     tzr = None
     if "tzr_tdb_hi" in z:
@@ -264,10 +271,8 @@ def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, i
     from .tim import read_tim
     ephem = _ephem_choice(ephem, model)
     _bipm_choice(include_bipm, model)
-    if planets is None:
+    if planets is None:   # toa.py:226-231: the model's PLANET_SHAPIRO decides
         planets = bool(model is not None and "PLANET_SHAPIRO" in model and model.PLANET_SHAPIRO.value)
-    if planets:
-        raise NotImplementedError("planet positions are outside the supported hot path (PLANET_SHAPIRO)")
     recs, commands = read_tim(timfile)
     if not recs:
         raise ValueError("No TOAs found!")
@@ -284,7 +289,7 @@ def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, i
     for f, c in zip(flags, corr):
         if c != 0:
             f["clkcorr"] = str(c)
-    cols = prep.prepare(day, frac, obs, corr)
+    cols = prep.prepare(day, frac, obs, corr, planets=bool(planets))
     cols["freq_mhz"] = np.array([r.freq_mhz for r in recs], dtype=np.float64)
     cols["err_us"] = np.array([r.error_us for r in recs], dtype=np.float64)
     # phase_columns_from_flags (toa.py:1959-1983)
@@ -303,7 +308,7 @@ def load_tim(timfile, model=None, ephem=None, include_bipm=None, planets=None, i
     t.ephem = ephem
     t.clock = "TT(TAI)"
     t.commands = commands
-    t.prepared = {"ephem": ephem, "include_bipm": False, "clock_files": clock_files}
+    t.prepared = {"ephem": ephem, "include_bipm": False, "clock_files": clock_files, "planets": bool(planets)}
     return t
 
 
@@ -322,7 +327,8 @@ def tzr_row(model, prepared) -> dict:
     if prepared.get("clock_files"):
         from .clock import site_corrections
         corr = site_corrections(prepared["clock_files"], [site], np.array([day + frac]))
-    cols = prep.prepare(np.array([day]), np.array([frac]), [site], corr)
+    # the TZR TOA is prepared with the TOAs' planets choice (absolute_phase.py:118)
+    cols = prep.prepare(np.array([day]), np.array([frac]), [site], corr, planets=prepared.get("planets", False))
     cols["freq_mhz"] = np.array([fr])
     cols["delta_pulse_number"] = np.zeros(1)
     cols["flags"] = {}
