@@ -60,6 +60,9 @@ typedef struct {
     const double *planet_km;        /* (n+1)*15 obs_<planet>_pos for jupiter, saturn, venus,
                                        uranus, neptune (toa.py:2403-2433); read only when
                                        spec.shapiro == 2, may be NULL otherwise             */
+    const int32_t *dmx_x;           /* DMX bins beyond a TOA's first two (any number may overlap,
+                                       dispersion_model.py:659-678): n+2 offsets into this array,
+                                       then the bin indices; NULL when no TOA has more than two */
 } pint_toas_t;
 
 /* ---- model structure ------------------------------------------------------------ */

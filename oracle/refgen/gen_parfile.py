@@ -21,7 +21,8 @@ PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "
         "ell1h_h3": "ell1h_h3.par", "ell1h_h4": "ell1h_h4.par", "ell1h_stig": "ell1h_stig.par",
         "pta_bt": "pta_bt.par", "pta_dmn": "pta_dmn.par", "pta_ddk": "pta_ddk.par", "pta_ddk_nk": "pta_ddk_nk.par", "wb_dd": "wb_dd.par",
         "c5_iso": "c5_iso.par", "c5_ell1": "c5_ell1.par", "c5_dd": "c5_dd.par",
-        "planet_ngc": "planet_ngc.par", "planet_b1855": "planet_b1855.par"}
+        "planet_ngc": "planet_ngc.par", "planet_b1855": "planet_b1855.par",
+        "dmx_overlap": "dmx_overlap.par"}
 
 
 

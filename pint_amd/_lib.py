@@ -29,7 +29,8 @@ class ToasT(C.Structure):
     _fields_ = [("n", C.c_int32), ("tdb_hi", dptr), ("tdb_lo", dptr), ("freq_mhz", dptr), ("sigma_s", dptr),
                 ("pos_km", dptr), ("vel_kms", dptr), ("sun_km", dptr), ("pulse_number", dptr), ("delta_pn", dptr),
                 ("flags", C.POINTER(C.c_uint32)), ("jump_mask", C.POINTER(C.c_uint64)),
-                ("dmx_a", C.POINTER(C.c_int32)), ("dmx_b", C.POINTER(C.c_int32)), ("planet_km", dptr)]
+                ("dmx_a", C.POINTER(C.c_int32)), ("dmx_b", C.POINTER(C.c_int32)), ("planet_km", dptr),
+                ("dmx_x", C.POINTER(C.c_int32))]
 
 
 class SpecT(C.Structure):

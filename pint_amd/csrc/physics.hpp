@@ -962,6 +962,8 @@ struct ToaRow {
     uint32_t flags;
     uint64_t jmask;
     int dmx_a, dmx_b;
+    const int32_t* dmx_x;  // PsrDev::dmx_x (bins beyond the first two), entries [dmx_x0, dmx_x1)
+    int dmx_x0, dmx_x1;
 };
 
 struct EvalOut {
@@ -1075,6 +1077,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         double dmx = 0.0;
         if (t.dmx_a >= 0) dmx += pval(P, S.o_DMX + 2 * t.dmx_a);
         if (t.dmx_b >= 0) dmx += pval(P, S.o_DMX + 2 * t.dmx_b);
+        for (int k = t.dmx_x0; k < t.dmx_x1; k++) dmx += pval(P, S.o_DMX + 2 * t.dmx_x[k]);
         delay += dmx * DMCONST * inv_f2;
     }
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
@@ -1197,7 +1200,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
             case PINT_COL_DMX:  // d_dm_d_DMX (:684): 1 on the bin's TOAs
                 for (int j = 0; j < R.cnt; j++, colp += ld) {
                     const int idx = R.idx0 + j;
-                    colp[r] = (t.dmx_a == idx || t.dmx_b == idx) ? dmc : 0.0;
+                    bool in = t.dmx_a == idx || t.dmx_b == idx;
+                    for (int k = t.dmx_x0; k < t.dmx_x1; k++) in |= t.dmx_x[k] == idx;
+                    colp[r] = in ? dmc : 0.0;
                 }
                 break;
             case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103): logf^(k+1)

@@ -48,6 +48,7 @@ struct PsrDev {
     const uint32_t* flags;
     const uint64_t* jmask;
     const int32_t *dmx_a, *dmx_b;
+    const int32_t* dmx_x;    // bins beyond the first two: n+2 offsets, then indices (null: none)
     const pint_spec_t* spec;
     const double* red_freq;  // 2 nred: the frequencies as double-double, hi[nred] then lo[nred]
     const double* red_phi;   // 2*nred
@@ -299,6 +300,9 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     t.jmask = Pd.jmask[r];
     t.dmx_a = Pd.dmx_a[r];
     t.dmx_b = Pd.dmx_b[r];
+    t.dmx_x = Pd.dmx_x;
+    t.dmx_x0 = Pd.dmx_x ? Pd.dmx_x[r] : 0;
+    t.dmx_x1 = Pd.dmx_x ? Pd.dmx_x[r + 1] : 0;
     EvalOut o;
     double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
     const bool rowM = WANT_M && r < (unsigned)n;
@@ -1459,6 +1463,8 @@ __global__ __launch_bounds__(DMR_T) void k_dm_resid(const PsrDev* __restrict__ p
             const int a = Pd.dmx_a[i], b = Pd.dmx_b[i];
             if (a >= 0) dm += pval(P, S.o_DMX + 2 * a);
             if (b >= 0) dm += pval(P, S.o_DMX + 2 * b);
+            if (Pd.dmx_x)
+                for (int k = Pd.dmx_x[i]; k < Pd.dmx_x[i + 1]; k++) dm += pval(P, S.o_DMX + 2 * Pd.dmx_x[k]);
         }
         if (S.ndmjump > 0) {
             const uint64_t m = Pd.dmjmask[i];
@@ -1513,6 +1519,8 @@ __device__ __forceinline__ void wb_row(const PsrDev& Pd, const pint_spec_t& S, c
         const int a = Pd.dmx_a[i], b = Pd.dmx_b[i];
         if (a >= 0) dm += pval(P, S.o_DMX + 2 * a);
         if (b >= 0) dm += pval(P, S.o_DMX + 2 * b);
+        if (Pd.dmx_x)
+            for (int k = Pd.dmx_x[i]; k < Pd.dmx_x[i + 1]; k++) dm += pval(P, S.o_DMX + 2 * Pd.dmx_x[k]);
     }
     if (S.ndmjump > 0) {
         const uint64_t m = Pd.dmjmask[i];
@@ -3938,6 +3946,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->jump_mask, n + 1, d.jmask);
     rc |= upload(ctx, ph, t->dmx_a, n + 1, d.dmx_a);
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
+    if (t->dmx_x) rc |= upload(ctx, ph, t->dmx_x, (size_t)t->dmx_x[n + 1], d.dmx_x);
     rc |= upload(ctx, ph, red_freq, (size_t)2 * spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)4 * n, d.red_cs);
@@ -3971,12 +3980,16 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
             }
         bool ok = ndc >= 8;
         std::vector<std::vector<int>> lists(ndc);
+        auto colof = [&](int bin) { return bin >= 0 && bin < spec->ndmx ? colOfBin[bin] : -1; };
         for (int i = 0; ok && i < n; i++) {
-            const int a = t->dmx_a[i] >= 0 && t->dmx_a[i] < spec->ndmx ? colOfBin[t->dmx_a[i]] : -1;
-            const int b = t->dmx_b[i] >= 0 && t->dmx_b[i] < spec->ndmx ? colOfBin[t->dmx_b[i]] : -1;
-            if (a >= 0 && b >= 0) ok = false;
-            else if (a >= 0) lists[a].push_back(i);
-            else if (b >= 0) lists[b].push_back(i);
+            int c = -1, nfree = 0;
+            for (int bin : {t->dmx_a[i], t->dmx_b[i]})
+                if (colof(bin) >= 0) { c = colof(bin); nfree++; }
+            if (t->dmx_x)
+                for (int k = t->dmx_x[i]; k < t->dmx_x[i + 1]; k++)
+                    if (colof(t->dmx_x[k]) >= 0) { c = colof(t->dmx_x[k]); nfree++; }
+            if (nfree > 1) ok = false;
+            else if (c >= 0) lists[c].push_back(i);
         }
         std::vector<int32_t> cmap(K + 1), dptr(ndc + 1, 0), didx;
         int kd = 0, ad = 0;

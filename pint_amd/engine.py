@@ -325,6 +325,7 @@ def pack_toas(lay: PulsarLayout):
             jm[n] |= np.uint64(1) << np.uint64(k)
     da = np.full(n + 1, -1, dtype=np.int32)
     db = np.full(n + 1, -1, dtype=np.int32)
+    extra = {}
     mjdf = np.concatenate([np.asarray(A["mjd_float"], dtype=np.float64),
                            np.asarray(tz.get("mjd_float", [0.0]), dtype=np.float64).reshape(1)])
     for j, name in enumerate(model.dmx_params()):
@@ -337,15 +338,28 @@ def pack_toas(lay: PulsarLayout):
                 da[i] = j
             elif db[i] < 0:
                 db[i] = j
-            else:
-                raise NotImplementedError("more than two overlapping DMX bins on one TOA")
+            else:   # a third (fourth, ...) overlapping bin: the CSR overflow below
+                extra.setdefault(int(i), []).append(j)
+    dmx_x = None
+    if extra:
+        # n+2 offsets into the same array, then the bin indices in parameter order (the
+        # reference sums every selecting bin, dispersion_model.py:672-677)
+        cnt = np.zeros(n + 1, dtype=np.int64)
+        for i, js in extra.items():
+            cnt[i] = len(js)
+        off = (n + 2) + np.concatenate([[0], np.cumsum(cnt)])
+        dmx_x = np.empty(int(off[-1]), dtype=np.int32)
+        dmx_x[:n + 2] = off
+        for i, js in extra.items():
+            dmx_x[off[i]:off[i + 1]] = js
     planet = None
     if lay.spec.shapiro == 2:
         planet = planet_rows(toas, tz, is_bary)
-    keep = [tdb_hi, tdb_lo, freq, sigma_s, pos, vel, sun, pn, dpn, flags, jm, da, db, planet]
+    keep = [tdb_hi, tdb_lo, freq, sigma_s, pos, vel, sun, pn, dpn, flags, jm, da, db, planet, dmx_x]
     t = L.ToasT(n, L.ptr(tdb_hi), L.ptr(tdb_lo), L.ptr(freq), L.ptr(sigma_s), L.ptr(pos), L.ptr(vel), L.ptr(sun),
                 L.ptr(pn), L.ptr(dpn), L.ptr(flags, C.c_uint32), L.ptr(jm, C.c_uint64), L.ptr(da, C.c_int32),
-                L.ptr(db, C.c_int32), L.ptr(planet) if planet is not None else None)
+                L.ptr(db, C.c_int32), L.ptr(planet) if planet is not None else None,
+                L.ptr(dmx_x, C.c_int32) if dmx_x is not None else None)
     return t, keep
 
 
