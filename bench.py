@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--grid", type=int, default=256, help="grid side for the chi2-grid leg (0 = skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--weak", type=int, default=1, help="also time a 68 x N pulsar PTA over the N ranks (N > 1)")
+    ap.add_argument("--c2", type=int, default=256, help="B1855 (C2) fits per batched step (0 = skip the C2 leg)")
     ap.add_argument("--j0740", type=int, default=256,
                     help="(M2, SINI) grid side of the C3/C4 J0740 legs (0 = skip)")
     args = ap.parse_args()
@@ -105,6 +106,7 @@ def main():
     roof = leg["roofline"]
     grid = grid_leg(args.grid, dist, barrier, max_over_ranks) if args.grid > 0 else None
     j0740 = j0740_legs(args.j0740, dist, barrier, max_over_ranks) if args.j0740 > 0 else None
+    c2 = c2_leg(args.c2, 20, 3, world, barrier, max_over_ranks) if args.c2 > 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(leg["items"])
@@ -120,7 +122,8 @@ def main():
                           "npsr": args.npsr, "ntoas": args.ntoas,
                           "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
                           "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
-               "roofline": roof, "pta_weak": weak, "grid": grid, "j0740": j0740, "cpu_baseline": cpu}
+               "roofline": roof, "pta_weak": weak, "grid": grid, "j0740": j0740, "c2": c2,
+               "cpu_baseline": cpu}
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
@@ -138,6 +141,20 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
     lays = [s.add(build_layout(m, t)) for m, t in items]
     tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
     s.set_instances(list(zip(lays, tabs0)))
+    dt, kt_gram, n_gram, step = timed_steps(s, args.steps, args.warmup, barrier, max_over_ranks)
+    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays))}
+    if profile:
+        out["roofline"] = roofline(s, lays, kt_gram / max(1, n_gram), step, args)
+        out["roofline"]["gram_event_launches"] = int(n_gram)
+    s.close()
+    return out
+
+
+def timed_steps(s, steps, warmup, barrier, max_over_ranks):
+    """Time `steps` fit steps of the Session's batch (warm-up first), pipelined two deep; one
+    step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.  Returns
+    (max-over-ranks seconds, summed Gram event time of the sampled steps, their count, step)."""
+    from pint_amd.engine import Session
     s.save_tables()        # the initial models, resident in HBM like the TOAs
     s.set_lazy(True)
 
@@ -153,8 +170,9 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
         return out, nz, c2
 
     # timed region: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop on
-    # its first/last dispatch packet), on every GRAM_EVERY-th step: each event pair still
-    # costs the stream a few us, so the Gram's time is the average over the sampled launches
+    # its first/last dispatch packet, or marker packets on the other Gram paths), on every
+    # GRAM_EVERY-th step: each event pair still costs the stream a few us, so the Gram's time
+    # is the average over the sampled launches
     s.set_timing_mask(1 << SLOT_GRAM)
     s.set_timing_every(GRAM_EVERY)
 
@@ -176,17 +194,48 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
             kt, nk = kt + t, nk + (t > 0)
         return kt, nk
 
-    run(args.warmup)
+    run(warmup)
     barrier()
     t0 = time.perf_counter()
-    kt_gram, n_gram = run(args.steps)
+    kt, nk = run(steps)
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays))}
-    if profile:
-        out["roofline"] = roofline(s, lays, kt_gram / max(1, n_gram), step, args)
-        out["roofline"]["gram_event_launches"] = int(n_gram)
+    return dt, kt, nk, step
+
+
+def c2_leg(batch, steps, warmup, world, barrier, max_over_ranks):
+    """C2: B1855+09 NANOGrav 9-yr (4005 TOAs, DD, 72 DMX, 235 ECORR epochs,
+    PLRedNoise; prepared here from its tim file) -- one GLSFitter.fit_toas(maxiter=1)
+    end to end (host included, the reference's unit), and `batch` fits of it as one batched
+    step (compact layout with the ECORR elimination, k_ecorr_dmx) on every rank."""
+    import copy
+    from pint_amd import GLSFitter
+    from pint_amd.engine import Session, build_layout, pack_table
+    from pint_amd.toa import get_model_and_toas
+    g = os.path.join(ROOT, "tests", "golden")
+    model, toas = get_model_and_toas(os.path.join(g, "B1855+09_NANOGrav_9yv1.gls.par"),
+                                     os.path.join(g, "B1855+09_NANOGrav_9yv1.tim.gz"), ephem="builtin",
+                                     include_bipm=False)
+    out = {"workload": f"B1855+09 9-yr, {toas.ntoas} TOAs, {len(model.free_params)} free parameters (C2)"}
+    dts = []
+    for rep in range(4):  # the first fit is the warm-up
+        f = GLSFitter(toas, copy.deepcopy(model))
+        t0 = time.perf_counter()
+        f.fit_toas(maxiter=1)
+        dts.append(time.perf_counter() - t0)
+    dt = float(np.median(dts[1:]))
+    out["single_fit"] = {"metric": "GLSFitter fits/sec (maxiter=1, one fit, host included)",
+                         "value": round(1.0 / dt, 3), "seconds": round(dt, 4), "chi2": float(f.resids.chi2)}
+    s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
+    lay = s.add(build_layout(model, toas))
+    s.set_instances([(lay, pack_table(lay, model))] * batch)
+    layout = s.fit_layout(lay)
+    dtb, kt, nk, _ = timed_steps(s, steps, warmup, barrier, max_over_ranks)
     s.close()
+    out["batched"] = {"metric": f"GLS fits/sec, {batch} B1855 fits per batched step on each of {world} rank(s)",
+                      "unit": "fits/s", "value": round(batch * world * steps / dtb, 1), "ms_per_step": round(dtb / steps * 1e3, 4),
+                      "gram_ms": round(kt / max(1, nk), 4), "compact_layout": bool(layout[0]),
+                      "gram_cols": layout[1], "dmx_cols": layout[2]}
     return out
 
 

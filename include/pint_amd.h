@@ -210,14 +210,18 @@ int pint_chi2_wls(pint_ctx *ctx, double *chi2);
  * noise_model.py:385-427 + get_ecorr_epochs :808): nep epochs, TOA index lists in CSR form
  * (ep_ptr[nep+1], ep_idx[ep_ptr[nep]]) and the prior variance phi_e = ECORR^2 in s^2.
  * The quantisation block is eliminated by a Schur complement on the device (its normal
- * matrix block is diagonal), so it adds no Gram columns.  Call before pint_set_instances. */
+ * matrix block is diagonal), so it adds no Gram columns; on the compact layout each epoch
+ * then couples to at most one DMX column (else the pulsar takes the full layout).  Call
+ * before pint_set_instances. */
 int pint_set_ecorr(pint_ctx *ctx, int psr, int nep, const int32_t *ep_ptr, const int32_t *ep_idx,
                    const double *ep_phi);
 
 /* Fit layout of pulsar `psr` (no reference counterpart; for benchmarks/tests):
  * out4 = {compact, Gram columns excl. residual, sparse DMX columns, padded Gram width}.
  * compact = 1 when the DMX columns are kept out of M and the dense Gram (>= 8 free DMX
- * columns, no TOA in two free bins, no ECORR): pint_eval(ctx, 2) then writes the compact
+ * columns, no TOA in two free bins, no TOA in two ECORR epochs, every ECORR epoch's TOAs in at
+ * most one free bin -- its elimination then keeps the DMX block diagonal, k_ecorr_dmx):
+ * pint_eval(ctx, 2) then writes the compact
  * design matrix, and pint_fit_step forms their Gram rows as bin sums. */
 int pint_fit_layout(pint_ctx *ctx, int psr, int32_t *out4);
 /* The k_gram_v layout of a pulsar in the current batch: (on the vg path (+2 with the

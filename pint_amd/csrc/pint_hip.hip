@@ -58,6 +58,11 @@ struct PsrDev {
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
     const int32_t* toa_ep;   // n: the ECORR epoch of each TOA (-1: none)
+    // compact layout with ECORR: every epoch's TOAs lie in at most one DMX column, so the
+    // epoch block couples to one bin and its elimination keeps the DMX block diagonal
+    const int32_t* ep_bin;   // nep: the DMX column of each epoch's TOAs (-1: none)
+    const int32_t* bep_ptr;  // ndc+1: CSR of the epochs of each DMX column
+    const int32_t* bep_idx;
     // white-noise classes for noise-parameter fits (pint_set_noise_classes): TOAs grouped by
     // the set of EFAC/EQUAD masks selecting them, CSR; raw TOA errors (us)
     const int32_t *cls_ptr, *cls_idx, *toa_cls;
@@ -78,7 +83,8 @@ struct PsrDev {
     const int32_t* drow;     // n: DMX column of each TOA (-1: none)
     const int32_t* dorig;    // Kd: original column of each compact dense column
     const int32_t* xorig;    // ndc: original column of each DMX column
-    int dsplit;              // compact layout applies (>= 8 DMX columns, no ECORR, no overlapping bins)
+    int dsplit;              // compact layout applies (>= 8 DMX columns, no overlapping bins, every ECORR
+                             // epoch within one DMX column)
     int dcontig;             // every DMX column's TOAs are one contiguous row range (k_gram fuses the bin sums)
     int ndc, Kd, Kpd, red0c; // DMX columns; compact width (excl. residual), padded, first red column
     int n;
@@ -591,16 +597,20 @@ __host__ __device__ constexpr int gram_q(int T) { return (gram_maxkp(T) * gram_c
 // W_e = sum w_i, D_e = W_e + 1/phi_e.  The quantisation-matrix block of the GLS normal
 // matrix is diagonal (disjoint epochs), so eliminating it is the rank-nep update
 // G' = G - sum_e s_e s_e^T / D_e, folded into k_gram as nep extra rows of weight -1/D_e.
+// Compact layout: s_e over the dense compact columns (stride Kpd), and the epoch's DMX entry
+// c_e = sum_{i in e} w_i x_i of its one bin (ep_bin) into eC (k_ecorr_dmx reduces DD, Sd).
 __global__ __launch_bounds__(256) void k_ecorr(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                const double* __restrict__ M, const double* __restrict__ rtime,
                                                double* __restrict__ esum, double* __restrict__ eD,
-                                               double* __restrict__ eW) {
+                                               double* __restrict__ eW, int compact, const double* __restrict__ dmxv,
+                                               double* __restrict__ eC) {
     const int inst = blockIdx.y;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (e >= Pd.nep) return;
-    const int n = I.n, K = I.K, Kp = I.Kp;
+    const bool cmp = compact && Pd.dsplit;
+    const int n = I.n, K = cmp ? Pd.Kd : I.K, Kp = cmp ? Pd.Kpd : I.Kp;
     const double* Mi = M + I.moff;
     const double* ri = rtime + (I.roff - inst);
     const int a = Pd.ep_ptr[e], b = Pd.ep_ptr[e + 1];
@@ -625,7 +635,64 @@ __global__ __launch_bounds__(256) void k_ecorr(const PsrDev* __restrict__ psrs, 
         }
         eW[I.epoff + e] = W;
         eD[I.epoff + e] = W + 1.0 / Pd.ep_phi[e];
+        if (cmp) {
+            double c = 0.0;
+            if (Pd.ep_bin[e] >= 0) {
+                const double* xv = dmxv + I.ooff;
+                for (int k = a; k < b; k++) {
+                    const int i = Pd.ep_idx[k];
+                    if (Pd.drow[i] >= 0) c += xv[i] / (Pd.sigma[i] * Pd.sigma[i]);
+                }
+            }
+            eC[I.epoff + e] = c;
+        }
     }
+}
+
+// k_ecorr_dmx: the ECORR elimination's share of the DMX rows in the compact layout.  With
+// every epoch in one DMX column a(e), eliminating the epochs leaves the DMX block diagonal:
+//   DD[a] -= sum_{e: a(e)=a} c_e^2 / D_e,   Sd[a][c] -= sum_{e: a(e)=a} c_e s_e[c] / D_e
+// (c over the dense compact columns and the residual).  One wave per (DMX column,
+// instance), lanes over columns; epochs summed in index order (deterministic).
+__global__ __launch_bounds__(64) void k_ecorr_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                  const double* __restrict__ esum, const double* __restrict__ eD,
+                                                  const double* __restrict__ eC, double* __restrict__ Sd,
+                                                  double* __restrict__ DD) {
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    const int a = blockIdx.x, lane = threadIdx.x;
+    if (!Pd.dsplit || Pd.nep == 0 || a >= Pd.ndc) return;
+    const int k0 = Pd.bep_ptr[a], k1 = Pd.bep_ptr[a + 1];
+    if (k0 == k1) return;
+    const int Kd = Pd.Kd, Kpd = Pd.Kpd;
+    double* out = Sd + I.sdoff + (long)a * Kpd;
+    for (int c = lane; c <= Kd; c += 64) {
+        double acc = 0.0;
+        for (int k = k0; k < k1; k++) {
+            const int e = Pd.bep_idx[k];
+            acc += eC[I.epoff + e] * esum[I.eoff + (long)e * Kpd + c] / eD[I.epoff + e];
+        }
+        out[c] -= acc;
+    }
+    if (lane == 0) {
+        double d = 0.0;
+        for (int k = k0; k < k1; k++) {
+            const int e = Pd.bep_idx[k];
+            const double ce = eC[I.epoff + e];
+            d += ce * ce / eD[I.epoff + e];
+        }
+        DD[I.ddoff + a] -= d;
+    }
+}
+
+// s_e of original column j (j = K: the residual) whatever the layout: the compact layout's
+// dense columns through cmap, its DMX columns as the epoch's bin entry c_e
+__device__ __forceinline__ double esum_col(const PsrDev& Pd, const InstDev& I, const double* esum,
+                                           const double* eC, bool cmp, int e, int j) {
+    if (!cmp) return esum[I.eoff + (long)e * I.Kp + j];
+    const int c = Pd.cmap[j];
+    if (c >= 0) return esum[I.eoff + (long)e * Pd.Kpd + c];
+    return Pd.ep_bin[e] == -c - 1 ? eC[I.epoff + e] : 0.0;
 }
 
 // k_gram: FP64 MFMA Gram of the whitened rows [T | r] / sigma, one 16-wave workgroup per
@@ -3142,7 +3209,8 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 const double* __restrict__ eW, const double* __restrict__ wpart,
                                                 int nsplit, int stride, double* __restrict__ ecs,
                                                 double* __restrict__ chi2, double* __restrict__ lognorm,
-                                                const double* __restrict__ wtile, const double* __restrict__ chi2w) {
+                                                const double* __restrict__ wtile, const double* __restrict__ chi2w,
+                                                int compact) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
     __shared__ double Dt[256], wloc[130];
@@ -3201,10 +3269,14 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     erwr = block_sum<4>(erwr, sh);
     erw1 = block_sum<4>(erw1, sh);
     __syncthreads();  // ce visible
+    // the Fourier columns of the epoch sums: after the timing columns (full layout) or at
+    // red0c of the compact dense columns
+    const bool ecmp = compact && Pd.dsplit;
+    const int es = ecmp ? Pd.Kpd : I.Kp, ef = ecmp ? Pd.red0c : S.ncol;
     for (int j = threadIdx.x; j < R; j += blockDim.x) {
         double v = 0.0;
         for (int q = 0; q < nsplit; q++) v += wp[(long)q * stride + j];
-        for (int e = 0; e < nep; e++) v -= Ei[(long)e * I.Kp + S.ncol + j] * ce[e];
+        for (int e = 0; e < nep; e++) v -= Ei[(long)e * es + ef + j] * ce[e];
         d[j] = v;
     }
     if (threadIdx.x == 0) d[R] = S.wb_noones ? 0.0 : rw1 - erw1;  // the ones column's entry
@@ -3365,18 +3437,19 @@ __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ ps
 
 __global__ __launch_bounds__(64) void k_noise_ecorr(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                     const double* __restrict__ dpars, const double* __restrict__ esum,
-                                                    const double* __restrict__ eD, double* __restrict__ out) {
+                                                    const double* __restrict__ eD, double* __restrict__ out,
+                                                    int compact, const double* __restrict__ eC) {
     const int inst = blockIdx.y, e = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     if (e >= Pd.nep) return;
+    const bool cmp = compact && Pd.dsplit;
     const int K = I.K;
-    const double* se = esum + I.eoff + (long)e * I.Kp;
     const double* x = dpars + I.coff;
     double t = 0.0;
-    for (int c = threadIdx.x; c < K; c += 64) t += se[c] * x[c];
+    for (int c = threadIdx.x; c < K; c += 64) t += esum_col(Pd, I, esum, eC, cmp, e, c) * x[c];
     t = wave_sum(t);
-    const double ce = (se[K] - t) / eD[I.epoff + e];
+    const double ce = (esum_col(Pd, I, esum, eC, cmp, e, K) - t) / eD[I.epoff + e];
     double* o = out + (I.roff - inst);
     for (int k = Pd.ep_ptr[e] + threadIdx.x; k < Pd.ep_ptr[e + 1]; k += 64) o[Pd.ep_idx[k]] = ce;
 }
@@ -3487,7 +3560,7 @@ __global__ __launch_bounds__(256) void k_debug_gram(const PsrDev* __restrict__ p
                                                     const double* __restrict__ DD, const double* __restrict__ DCS,
                                                     const double* __restrict__ esum, const double* __restrict__ eD,
                                                     int pre_ecorr, const long* __restrict__ ooff,
-                                                    double* __restrict__ out) {
+                                                    double* __restrict__ out, const double* __restrict__ eC) {
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -3500,7 +3573,7 @@ __global__ __launch_bounds__(256) void k_debug_gram(const PsrDev* __restrict__ p
         const int i = (int)(e / W), j = (int)(e % W);
         double v = g(i, j);
         for (int q = 0; q < nep; q++)
-            v += esum[I.eoff + (long)q * I.Kp + i] * esum[I.eoff + (long)q * I.Kp + j] / eD[I.epoff + q];
+            v += esum_col(Pd, I, esum, eC, cmp, q, i) * esum_col(Pd, I, esum, eC, cmp, q, j) / eD[I.epoff + q];
         o[e] = v;
     }
     for (int j = threadIdx.x; j < I.K; j += blockDim.x) o[(long)W * W + j] = colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j);
@@ -3582,6 +3655,7 @@ struct pint_ctx {
     double *d_G = nullptr, *d_colsq = nullptr, *d_work = nullptr, *d_dpars = nullptr, *d_errs = nullptr;
     double *d_cov = nullptr, *d_sigL = nullptr, *d_lam = nullptr, *d_chi2g = nullptr;
     double *d_esum = nullptr, *d_eD = nullptr, *d_eW = nullptr, *d_ecs = nullptr, *d_wpart = nullptr;
+    double* d_eC = nullptr;  // compact layout: each epoch's DMX entry c_e (k_ecorr)
     double* d_lognorm = nullptr;  // per instance: logdet(C)/2 of the last pint_chi2_gls
     double *d_eigw = nullptr, *d_degv = nullptr;  // k_eig scratch and dropped directions
     int* d_ndeg = nullptr;
@@ -3835,7 +3909,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g_s[0], (void**)&ctx->d_chi2g_s[1], (void**)&ctx->d_lognorm,
                    (void**)&ctx->d_eigw,
                    (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
-                   (void**)&ctx->d_eW, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
+                   (void**)&ctx->d_eW, (void**)&ctx->d_eC, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
@@ -4108,7 +4182,36 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
     }
     if (rc) return PINT_E_HIP;
     ph.dev.nep = nep;
-    ph.dev.dsplit = 0;  // the ECORR Schur rows span every column: keep the full layout
+    if (ph.dev.dsplit) {
+        // the compact layout stays when no TOA is in two epochs and each epoch's TOAs lie in at
+        // most one DMX column (the epoch-by-DMX block then has one entry per epoch); otherwise
+        // the Schur rows couple DMX columns: the full layout
+        const int ndc = ph.dev.ndc;
+        std::vector<int32_t> eb(nep, -1), bptr(ndc + 1, 0), bidx;
+        bool ok = !ph.dev.ep_overlap;
+        for (int e = 0; ok && e < nep; e++)
+            for (int k = ep_ptr[e]; k < ep_ptr[e + 1]; k++) {
+                const int a = ph.drow_host[ep_idx[k]];
+                if (a < 0) continue;
+                if (eb[e] >= 0 && eb[e] != a) { ok = false; break; }
+                eb[e] = a;
+            }
+        if (ok) {
+            std::vector<std::vector<int32_t>> lists(ndc);
+            for (int e = 0; e < nep; e++)
+                if (eb[e] >= 0) lists[eb[e]].push_back(e);
+            for (int a = 0; a < ndc; a++) {
+                bptr[a + 1] = bptr[a] + (int)lists[a].size();
+                bidx.insert(bidx.end(), lists[a].begin(), lists[a].end());
+            }
+            rc |= upload(ctx, ph, eb.data(), eb.size(), ph.dev.ep_bin);
+            rc |= upload(ctx, ph, bptr.data(), bptr.size(), ph.dev.bep_ptr);
+            rc |= upload(ctx, ph, bidx.data(), bidx.size(), ph.dev.bep_idx);
+            if (rc) return PINT_E_HIP;
+        } else {
+            ph.dev.dsplit = 0;
+        }
+    }
     return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
 }
 
@@ -4453,6 +4556,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
+    HIPCHK(cmalloc((void**)&ctx->d_eC, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_ecs, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_ic, sizeof(InstConst) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_dmxv, sizeof(double) * (out > 0 ? out : 1)));
@@ -4747,7 +4851,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             ctx->copy_pend[0] = ctx->copy_pend[1] = false;
         }
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
-                           ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW);
+                           ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->m_compact,
+                           ctx->d_dmxv, ctx->d_eC);
         HIPCHK(hipGetLastError());
     }
     const int cmp = ctx->m_compact;
@@ -4767,6 +4872,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         if (any_gather) {
             hipLaunchKernelGGL(k_dmx, dim3(ctx->max_ndc, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                                ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+            HIPCHK(hipGetLastError());
+        }
+        if (mode == 1 && ctx->max_nep > 0) {  // the ECORR elimination's share of the DMX rows
+            hipLaunchKernelGGL(k_ecorr_dmx, dim3(ctx->max_ndc, ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_esum, ctx->d_eD, ctx->d_eC, ctx->d_Sd, ctx->d_DD);
             HIPCHK(hipGetLastError());
         }
     }
@@ -5176,7 +5286,8 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
                        ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
                        stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm,
-                       ctx->wtile_valid ? (const double*)ctx->d_wtile : nullptr, (const double*)ctx->d_chi2);
+                       ctx->wtile_valid ? (const double*)ctx->d_wtile : nullptr, (const double*)ctx->d_chi2,
+                       ctx->m_compact);
     HIPCHK(hipGetLastError());
     record(ctx, 11);
     if (ctx->lazy && !ctx->capturing) {
@@ -5463,7 +5574,7 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
         HIPCHK(hipMemsetAsync(de, 0, sizeof(double) * ctx->tot_out, st));
         if (ctx->max_nep > 0)
             hipLaunchKernelGGL(k_noise_ecorr, dim3(ctx->max_nep, ctx->ninst), dim3(64), 0, st, ctx->d_psrs,
-                               ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, de);
+                               ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, de, ctx->m_compact, ctx->d_eC);
     }
     if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids: launch failed"; return PINT_E_HIP; }
     if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
@@ -5514,7 +5625,7 @@ int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
     HIPCHK(hipMemcpy(doff, off.data(), sizeof(long) * ctx->ninst, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_debug_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
                        ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_esum,
-                       ctx->d_eD, pre_ecorr && ctx->max_nep > 0, doff, d);
+                       ctx->d_eD, pre_ecorr && ctx->max_nep > 0, doff, d, ctx->d_eC);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, sizeof(double) * off[ctx->ninst], hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -77,6 +77,8 @@ def test_stage_gram_step(name):
     st = stage(name)
     bf, G, colsq, dp, er, cov, _ = device_stage(name, z["res_time"])
     lay = bf.layouts[0]
+    if name == "b1855":  # 72 DMX bins + 235 ECORR epochs on the compact layout (k_ecorr_dmx)
+        assert bf.s.fit_layout(lay)[0] == 1
     tr = st["cols_tr"]
     K = lay.K
     assert K == len(tr), (K, len(tr))
@@ -275,6 +277,45 @@ def test_fitter_noise_resids_and_update_model(name):
     # two longdouble/double-double evaluations (tests/test_oracle_golden.py::test_gls_fit)
     assert abs(f.model.TRES.value / um["TRES"] - 1) < 1e-5
     assert f.model.DMDATA.value is False
+
+
+def test_compact_ecorr_matches_full_layout():
+    """B1855 (72 DMX bins, 235 ECORR epochs): the compact layout (DMX as bin sums, the ECORR
+    elimination's DMX share in k_ecorr_dmx) and the full layout (DMX columns in M) solve the
+    same normal equations: step, errors, covariance, GLS chi2 and the ECORR realisations agree
+    to rounding."""
+    from pint_amd.engine import Session
+    from pint_amd.fitter import BatchFit
+    model, toas, z, meta = load("b1855")
+    out = {}
+    for key, want in (("compact", Session.FIT), ("full", True)):
+        bf = BatchFit([(model, toas)], mode="gls")
+        s = bf.s
+        s.eval(want_M=want)
+        assert s.fit_layout(bf.layouts[0])[0] == 1
+        s.debug_set_resids([z["res_time"]])
+        s.fit_step(1)
+        dp, er, cov, _ = s.read_step()
+        nr = s.noise_resids()[0]
+        c2 = s.chi2_gls()[0]
+        G, _ = s.debug_gram(pre_ecorr=True)[0]
+        K = bf.layouts[0].K
+        out[key] = (dp[0][:K], er[0][:K], cov[0], nr, c2, G)
+        bf.close()
+    dc, ec, cc, nc, c2c, Gc = out["compact"]
+    df, ef, cf, nf, c2f, Gf = out["full"]
+    d = np.sqrt(np.diag(Gf)[:K])
+    print(f"b1855 compact vs full: gram {np.max(np.abs(Gc - Gf)[:K, :K] / np.outer(d, d)):.1e} "
+          f"step {np.max(np.abs(dc - df) / ef):.1e} errs {np.max(np.abs(ec / ef - 1)):.1e} "
+          f"chi2 {abs(c2c / c2f - 1):.1e}")
+    assert np.max(np.abs(Gc - Gf)[:K, :K] / np.outer(d, d)) < 1e-12
+    # B1855's normal matrix has cond ~3e11: the two layouts' solves round differently
+    assert np.max(np.abs(dc - df) / ef) < 1e-6
+    assert np.max(np.abs(ec / ef - 1)) < 1e-6
+    assert np.max(np.abs(cc - cf) / np.outer(ef[:len(cc)], ef[:len(cc)])) < 1e-6
+    assert abs(c2c / c2f - 1) < 1e-9
+    for k in nf:
+        assert np.max(np.abs(nc[k] - nf[k])) <= 1e-6 * np.max(np.abs(nf[k])) + 1e-15, k
 
 
 def test_full_cov_matches_rank_reduced():
