@@ -309,10 +309,12 @@ def test_compact_ecorr_matches_full_layout():
           f"step {np.max(np.abs(dc - df) / ef):.1e} errs {np.max(np.abs(ec / ef - 1)):.1e} "
           f"chi2 {abs(c2c / c2f - 1):.1e}")
     assert np.max(np.abs(Gc - Gf)[:K, :K] / np.outer(d, d)) < 1e-12
-    # B1855's normal matrix has cond ~3e11: the two layouts' solves round differently
-    assert np.max(np.abs(dc - df) / ef) < 1e-6
-    assert np.max(np.abs(ec / ef - 1)) < 1e-6
-    assert np.max(np.abs(cc - cf) / np.outer(ef[:len(cc)], ef[:len(cc)])) < 1e-6
+    # the Grams agree to rounding, but B1855's normal matrix has cond ~3e11: the two layouts'
+    # solves (k_solve_dmx on the DMX-eliminated system, k_solve_blk on the full one) differ by
+    # ~cond x eps (measured 1.1e-5 sigma in the step, 1.2e-5 in the errors)
+    assert np.max(np.abs(dc - df) / ef) < 1e-4
+    assert np.max(np.abs(ec / ef - 1)) < 1e-4
+    assert np.max(np.abs(cc - cf) / np.outer(ef[:len(cc)], ef[:len(cc)])) < 1e-4
     assert abs(c2c / c2f - 1) < 1e-9
     for k in nf:
         assert np.max(np.abs(nc[k] - nf[k])) <= 1e-6 * np.max(np.abs(nf[k])) + 1e-15, k
