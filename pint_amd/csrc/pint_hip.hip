@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include "physics.hpp"
 
@@ -88,6 +89,7 @@ struct PsrDev {
     const int32_t* dptr;     // ndc+1: CSR of the TOAs of each DMX column
     const int32_t* didx;
     const int32_t* drow;     // n: DMX column of each TOA (-1: none)
+    const int32_t* dslot;    // n: its k_gram_v slot, drow % vns (-1: none); vg pulsars only
     const int32_t* dorig;    // Kd: original column of each compact dense column
     const int32_t* xorig;    // ndc: original column of each DMX column
     int dsplit;              // compact layout applies (>= 8 DMX columns, no overlapping bins, every ECORR
@@ -1265,7 +1267,6 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     double csq[QL];  // sums of squares of this wave's timing columns (lanes = rows)
 #pragma unroll
     for (int q = 0; q < QL; q++) csq[q] = 0.0;
-    const bool w0 = wave == 0;
     int sp0 = -1, sp1 = -1;  // per buffer: the slot column of this lane's row of two chunks ago
     double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, c8_n = 1.0, s8_n = 0.0;
     double st[QL] = {};
@@ -1275,7 +1276,17 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     int cur0 = -1, cur1 = -1;   // VB: bins held by the even / odd half of accB (wave-uniform)
     double4_t accB = {0, 0, 0, 0};
     double* const vbase = BFp + I.vboff + ((long)split * GW + wave) * NS * 128;
-    auto load = [&](long c0) {  // the next chunk's row data -> registers (clamped rows)
+    // Every staging / MFMA lambda takes the wave index as a compile-time constant W (the
+    // chunk loop is instantiated once per wave and dispatched on the uniform wave id): the
+    // wave's LDS columns and trig harmonics are then constants -- immediate offsets, no
+    // runtime selects in the powers e^{i a theta}, fewer scalar registers (no SGPR spills).
+    // With NTC - NTR >= 4 every harmonic h < 32 has a column inside the tile (f0 = 16 NTR):
+    // the harmonics past nred are staged unconditionally into padding columns that the
+    // epilogue never stores.
+    constexpr bool FULLH = NTC - NTR >= 4;
+    int sl_n = -1;  // the staged row's DMX slot (dslot; wave 0)
+    auto load = [&](auto Wc, long c0) {  // the next chunk's row data -> registers (clamped rows)
+        constexpr int W = decltype(Wc)::value;
         long row = c0 + lane;
         if (VB) {  // c0 = i0 + 16 c
             const long rel = (c0 - i0) + (long)(lane >> 4) * QV + (lane & 15);
@@ -1287,9 +1298,15 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
         // (global-address-space loads: through generic pointers they would be flat loads,
         // which also count against lgkmcnt, so every LDS wait would wait for them too)
         w_n = ok_n ? ((gptr<double>)Pd.isig)[row] : 0.0;  // rows past the split weigh 0
-        r_n = ri[row];
-        x_n = xv[row];
-        d_n = ((gptr<int>)Pd.drow)[row];
+        if (W == 0) {
+            r_n = ri[row];
+            x_n = xv[row];
+            sl_n = ((gptr<int>)Pd.dslot)[row];
+        }
+        if (VB) {
+            d_n = ((gptr<int>)Pd.drow)[row];
+            if (W != 0) x_n = xv[row];
+        }
         const double4_t z = ((gptr<double4_t>)Pd.red_cs)[row];
         c1_n = z[0];
         s1_n = z[1];
@@ -1297,39 +1314,38 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
         s8_n = z[3];
 #pragma unroll
         for (int q = 0; q < QL; q++) {
-            const int c = wave + GW * q;
+            const int c = W + GW * q;
             if (c < r0) st[q] = ok_n ? Mi[(long)c * n + row] : 0.0;  // uniform guard
         }
     };
     // LDS stores through a 32-bit (address space 3) pointer: column index x CS + lane
     typedef double __attribute__((address_space(3))) ldsd;
     auto put = [&](ldsd* Ts, int colidx, double v) { Ts[colidx * CS + lane] = v; };
-    auto stage = [&](double* Tsg, int& sp) {  // registers -> whitened row block in LDS
+    auto stage = [&](auto Wc, double* Tsg, int& sp) {  // registers -> whitened row block in LDS
+        constexpr int W = decltype(Wc)::value;
         ldsd* Ts = (ldsd*)Tsg;
         const double iw = w_n;
 #pragma unroll
         for (int q = 0; q < QL; q++) {
-            const int c = wave + GW * q;
+            const int c = W + GW * q;
             if (c < r0) {  // uniform guard (scalar branch)
                 put(Ts, c, st[q] * iw);
                 csq[q] += st[q] * st[q];  // 0 past the split
             }
         }
-        {  // residual and DMX slot entry (wave 0's share)
-            const int sl = (ok_n && d_n >= 0) ? d_n % NS : -1;
-            if (w0) {
-                put(Ts, r0, r_n * iw);
-                put(Ts, vsel(sp >= 0, s0 + sp, DUM), 0.0);
-                put(Ts, vsel(sl >= 0, s0 + sl, DUM), x_n * iw);
-            }
+        if (W == 0) {  // residual and DMX slot entry (wave 0's share)
+            const int sl = ok_n ? sl_n : -1;
+            put(Ts, r0, r_n * iw);
+            put(Ts, vsel(sp >= 0, s0 + sp, DUM), 0.0);
+            put(Ts, vsel(sl >= 0, s0 + sl, DUM), x_n * iw);
             sp = sl;
-            binc = (ok_n && d_n >= 0) ? d_n : -1;
         }
+        if (VB) binc = (ok_n && d_n >= 0) ? d_n : -1;
 #pragma unroll
         for (int j = 0; j < TA; j++) {
-            // trig blocks: harmonic a of A and 8a of B, a = wave + GW j (weighted: the
-            // rotations below are linear, so they carry the weight along)
-            const int a = wave + GW * j;
+            // trig blocks: harmonic a of A and 8a of B, a = W + GW j (weighted: the rotations
+            // below are linear, so they carry the weight along)
+            const int a = W + GW * j;
             double ca, sa, cb, sb;
             cpow_u8(c1_n, s1_n, a, ca, sa);
             cpow_u8(c8_n, s8_n, a, cb, sb);
@@ -1356,7 +1372,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
 #pragma unroll
             for (int u = 0; u < HMAX; u++) {
                 const int h = a + 8 * u;  // harmonic h + 1 -> columns f0 + 2h (sin), +1 (cos)
-                if (h < nred) {           // uniform guard
+                if (FULLH || h < nred) {  // uniform guard
                     put(Ts, f0 + 2 * h, s);
                     put(Ts, f0 + 2 * h + 1, c);
                 }
@@ -1364,14 +1380,15 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
             }
         }
     };
-    auto mfma = [&](const double* Ts) {
+    auto mfma = [&](auto Wc, const double* Ts) {
+        constexpr int W = decltype(Wc)::value;
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
             // the row offset of this k-step is laundered through an empty asm so the
             // compiler cannot pair reads of consecutive k-steps (4 doubles apart) into
             // ds_read2_b64: that form is serviced as 16-lane groups banked mod 32, where the
             // column stride CS = 66 puts lanes c and c + 8 on one bank (2-way conflict)
-            int roff = (wave * KS + ks) * 4;
+            int roff = (W * KS + ks) * 4;
             asm volatile("" : "+v"(roff));
             const double* Tr = Ts + (lane & 15) * CS + (lane >> 4) + roff;
             double a[NTR], b[NTC];
@@ -1397,51 +1414,64 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
         }
     };
     const long nch = i1 > i0 ? (i1 - i0 + CH - 1) / CH : 0;
-    if (nch > 0) load(i0);  // in flight while the buffers are zeroed
-    for (int k = tid; k < GVB * Kpt * CS; k += NTH) lds[k] = 0.0;  // slot and padding columns stay 0
-    __syncthreads();
-    if constexpr (GVB == 2) {
-        if (nch > 0) {
-            stage(Tb0, sp0);
-            load(i0 + CH);
-        }
+    auto chunks = [&](auto Wc) {
+        constexpr int W = decltype(Wc)::value;
+        if (nch > 0) load(Wc, i0);  // in flight while the buffers are zeroed
+        // the slot columns start at 0 (a row writes its own slot entry and clears the previous
+        // one); every other column is rewritten each chunk or is padding the epilogue skips
+        for (int bf = 0; bf < GVB; bf++)
+            for (int k = tid; k < NS * CS; k += NTH) lds[bf * Kpt * CS + s0 * CS + k] = 0.0;
         __syncthreads();
-        GVTS(1);
-        for (long c = 0; c < nch; c++) {
-            const bool odd = c & 1;
-            // chunk c+1 into the other buffer (past the last chunk: rows with iw = 0, never read)
-            int sp = odd ? sp0 : sp1;
-            if (!(dbg & 4)) stage(odd ? Tb0 : Tb1, sp);
-            if (odd) sp0 = sp;
-            else sp1 = sp;
-            if (!(dbg & 1)) load(i0 + (c + 2) * CH);
-            if (!(dbg & 2)) mfma(odd ? Tb1 : Tb0);
-            __syncthreads();
-        }
-    } else {
-        // one buffer, two workgroups per CU: one's staging and barriers fill the other's gaps
-        GVTS(1);
-        const long CHS = VB ? 16 : CH;  // row step of a chunk (VB: per quarter)
-        for (long c = 0; c < nch; c++) {
-            if (!(dbg & 4)) stage(Tb0, sp0);
-            if (!(dbg & 1)) load(i0 + (c + 1) * CHS);  // past the last chunk: clamped, unused
-            __syncthreads();
-            if (VB) {
-                // the bins of the wave's 16 rows (staging lanes 16 wave ..): the first and the
-                // last row with a bin (bins are contiguous row ranges; the host admits <= 2 per
-                // group, of distinct parity)
-                const unsigned long long m = __ballot(binc >= 0);
-                const unsigned mw = (unsigned)((m >> (16 * wave)) & 0xffffull);
-                if (mw != 0u) {
-                    const int lf = 16 * wave + __builtin_ctz(mw), ll = 16 * wave + 31 - __builtin_clz(mw);
-                    const int bf = __builtin_amdgcn_readlane(binc, lf), bl = __builtin_amdgcn_readlane(binc, ll);
-                    VB_ENTER(bf);
-                    VB_ENTER(bl);
-                }
+        if constexpr (GVB == 2) {
+            if (nch > 0) {
+                stage(Wc, Tb0, sp0);
+                load(Wc, i0 + CH);
             }
-            if (!(dbg & 2)) mfma(Tb0);
             __syncthreads();
+            GVTS(1);
+            for (long c = 0; c < nch; c++) {
+                const bool odd = c & 1;
+                // chunk c+1 into the other buffer (past the last chunk: rows with iw = 0, never read)
+                int sp = odd ? sp0 : sp1;
+                if (!(dbg & 4)) stage(Wc, odd ? Tb0 : Tb1, sp);
+                if (odd) sp0 = sp;
+                else sp1 = sp;
+                if (!(dbg & 1)) load(Wc, i0 + (c + 2) * CH);
+                if (!(dbg & 2)) mfma(Wc, odd ? Tb1 : Tb0);
+                __syncthreads();
+            }
+        } else {
+            // one buffer, two workgroups per CU: one's staging and barriers fill the other's gaps
+            GVTS(1);
+            const long CHS = VB ? 16 : CH;  // row step of a chunk (VB: per quarter)
+            for (long c = 0; c < nch; c++) {
+                if (!(dbg & 4)) stage(Wc, Tb0, sp0);
+                if (!(dbg & 1)) load(Wc, i0 + (c + 1) * CHS);  // past the last chunk: clamped, unused
+                __syncthreads();
+                if (VB) {
+                    // the bins of the wave's 16 rows (staging lanes 16 W ..): the first and the
+                    // last row with a bin (bins are contiguous row ranges; the host admits <= 2
+                    // per group, of distinct parity)
+                    const unsigned long long m = __ballot(binc >= 0);
+                    const unsigned mw = (unsigned)((m >> (16 * W)) & 0xffffull);
+                    if (mw != 0u) {
+                        const int lf = 16 * W + __builtin_ctz(mw), ll = 16 * W + 31 - __builtin_clz(mw);
+                        const int bf = __builtin_amdgcn_readlane(binc, lf), bl = __builtin_amdgcn_readlane(binc, ll);
+                        VB_ENTER(bf);
+                        VB_ENTER(bl);
+                    }
+                }
+                if (!(dbg & 2)) mfma(Wc, Tb0);
+                __syncthreads();
+            }
         }
+    };
+    static_assert(GW == 4, "k_gram_v: the chunk loop is dispatched over four waves");
+    switch (wave) {
+        case 0: chunks(std::integral_constant<int, 0>{}); break;
+        case 1: chunks(std::integral_constant<int, 1>{}); break;
+        case 2: chunks(std::integral_constant<int, 2>{}); break;
+        default: chunks(std::integral_constant<int, 3>{}); break;
     }
     if (VB) {
         if (cur0 >= 0) vb_flush(accB, vbase + (long)(cur0 % NS) * 128, 0, lane);
@@ -1465,27 +1495,39 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     auto cidx = [&](int p) { return p < r0 ? p : (p == r0 ? Kd : r0 + (p - f0)); };
     constexpr int TG = NT < VTG ? NT : VTG;
     double* red = lds;  // [GW][TG][256] (the host sizes LDS for it)
-    int k = 0;
+    // only the tiles the MFMAs formed (the all-slot row tiles' skipped tiles hold nothing to
+    // store): groups of TG, every thread reducing element tid of each tile of the group; the
+    // tile coordinates are compile-time constants after unrolling
+    constexpr int NKEPT = [] {
+        int c = 0;
+        for (int ti = 0; ti < NTR; ti++)
+            for (int tj = ti; tj < NTC; tj++)
+                if (!(ti >= NTR - NSK && (tj < NTR || VB))) c++;
+        return c;
+    }();
+    int gti[TG], gtj[TG];
+    int k = 0, g = 0, kept = 0;
 #pragma unroll
     for (int ti = 0; ti < NTR; ti++) {
 #pragma unroll
         for (int tj = ti; tj < NTC; tj++, k++) {
-            const int g = k % TG;
+            if (ti >= NTR - NSK && (tj < NTR || VB)) continue;
             if (g == 0) __syncthreads();  // the previous group's (or the MFMAs') readers are done
 #pragma unroll
             for (int q = 0; q < 4; q++) red[((wave * TG + g) * 4 + q) * 64 + lane] = acc[k][q];
-            if (g == TG - 1 || k == NT - 1) {
+            gti[g] = ti;
+            gtj[g] = tj;
+            kept++;
+            if (g == TG - 1 || kept == NKEPT) {
                 __syncthreads();
-                const int kbase = k - g;
-                for (int e = tid; e < (g + 1) * 256; e += NTH) {
-                    const int gg = e >> 8, q = (e >> 6) & 3, ln = e & 63;
+                const int q = (tid >> 6) & 3, ln = tid & 63;  // NTH = 256: one element per thread
+#pragma unroll
+                for (int gg = 0; gg < TG; gg++) {
+                    if (gg > g) break;
                     double v = 0.0;
 #pragma unroll
                     for (int w = 0; w < GW; w++) v += red[((w * TG + gg) * 4 + q) * 64 + ln];
-                    int tt = kbase + gg, r_ = 0;  // tile (r_, r_ + tt) of the row-major list
-                    while (tt >= NTC - r_) { tt -= NTC - r_; r_++; }
-                    const int tJ_ = r_ + tt;
-                    const int pr = r_ * 16 + (ln >> 4) + 4 * q, pc = tJ_ * 16 + (ln & 15);
+                    const int pr = gti[gg] * 16 + (ln >> 4) + 4 * q, pc = gtj[gg] * 16 + (ln & 15);
                     if (pr > pc || pc >= Wv) continue;
                     const bool rs = pr >= s0, cs = pc >= s0 && pc < f0;
                     if (!rs && !cs) {
@@ -1500,6 +1542,9 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                         Sp[(long)(pr - s0) * SW + cidx(pc)] = v;            // DMX x F (VB: binned)
                     }
                 }
+                g = 0;
+            } else {
+                g++;
             }
         }
     }
@@ -3654,6 +3699,7 @@ struct PsrHost {
     pint_spec_t spec;
     std::vector<int> dlo, dhi;  // row range of each DMX column's bin (compact layout)
     std::vector<int> drow_host; // DMX column of each TOA (-1: none), compact layout
+    int dslot_ns = 0;           // vns the uploaded dslot was formed with (0: none)
     std::vector<void*> bufs;
     int n, K;
 };
@@ -4367,6 +4413,12 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 d.vg = 1;
                 d.vns = ns;
                 d.vkp = kpv;
+                if (ph.dslot_ns != ns) {  // the rows' slots, so k_gram_v does no modulo
+                    std::vector<int32_t> sl(ph.n);
+                    for (int i = 0; i < ph.n; i++) sl[i] = ph.drow_host[i] >= 0 ? ph.drow_host[i] % ns : -1;
+                    if (upload(ctx, ph, sl.data(), sl.size(), d.dslot)) return PINT_E_HIP;
+                    ph.dslot_ns = ns;
+                }
                 break;
             }
         }
