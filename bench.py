@@ -245,14 +245,15 @@ def roofline(s, lays, kt_gram, step, args):
     k_gram_v (FP64 MFMA):
       alg_flops   useful flops of the normal matrix it forms, per TOA row: 2 x [(P+1)(P+2)/2
                   ([T|r]^T W [T|r], upper) + (P+1) R ([T|r]^T W F) + (P+2) (the row's DMX bin
-                  entry against [T|r] and itself) + R (DMX x F) + 2 (2 nred + 1) (the weighted
-                  trig sums C_m, S_m that give F^T W F)], P = compact timing columns, R = 2 nred;
+                  entry against [T|r] and itself) + R (DMX x F)], P = compact timing columns,
+                  R = 2 nred (F^T W F comes from the weighted trig sums, which depend on the
+                  TOAs and sigma only: formed once per pulsar by k_trigw, not per launch);
       exec_flops  the MFMAs it issues, counted exactly as the kernel loops them: per N-split
-                  ceil(rows / 64) chunks x 16 k-steps x (NT + 1) tiles x 2048 flop (NT = the
+                  ceil(rows / 64) chunks x 16 k-steps x NT tiles x 2048 flop (NT = the
                   [T|r|slots] x [T|r|slots|F] upper tiles less the all-slot (DD-only) tiles the
-                  kernel skips, + the trig tile; with the binned DMX x F tile (PINT_OPT_VBIN) the
-                  all-slot row tiles go entirely and the binned tile comes); equals the PMC
-                  SQ_INSTS_MFMA x 2048 of the profile (profiles/pmc_gram_r02.json).
+                  kernel skips; with the binned DMX x F tile (PINT_OPT_VBIN) the all-slot row
+                  tiles go entirely and the binned tile comes); equals the PMC SQ_INSTS_MFMA x
+                  2048 of the profile (profiles/pmc_gram_rNN.json).
     achieved = alg_flops / event time; exec_TFLOP/s beside it."""
     from pint_amd.pta import fit_cost  # noqa: F401
     nsplit = s.nsplit()
@@ -264,10 +265,10 @@ def roofline(s, lays, kt_gram, step, args):
         vb = bool(vg & 2)  # binned DMX x F tile: the all-slot row tiles go, one binned tile comes
         n, R, nred = l.n, 2 * l.nred, l.nred
         P = r0
-        alg += 2.0 * n * ((P + 1) * (P + 2) / 2 + (P + 1) * R + (P + 2) + R + 2 * (2 * nred + 1))
+        alg += 2.0 * n * ((P + 1) * (P + 2) / 2 + (P + 1) * R + (P + 2) + R)
         ntr, ntc = (r0 + 1 + ns) // 16, kpv // 16
         nsk = ntr - (r0 + 1 + 15) // 16  # trailing all-slot row tiles: their DD-only tiles are skipped
-        nt = 1 + (1 if vb else 0)  # the trig tile (+ the binned tile)
+        nt = 1 if vb else 0        # the binned tile
         for ti in range(ntr):      # as the kernel's loop skips them (gram_v_body)
             nt += sum(1 for tj in range(ti, ntc) if not (ti >= ntr - nsk and (tj < ntr or vb)))
         per = -(-n // nsplit)

@@ -62,6 +62,8 @@ struct PsrDev {
     const double* red_phi;   // 2*nred
     const double* red_cs;    // n x 4: (cos, sin) of theta and of 8 theta, theta = 2 pi t f_1 (k_redbase)
     const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trigu)
+    const double* trigW;     // 2 x 64: C_m, S_m = sum_i w_i (cos, sin) m theta_i, w = 1/sigma^2 (k_trigw):
+                             // TOA-only at fixed sigma, formed at upload and by pint_set_sigma
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
     const double* ep_phi;    // nep prior variances (s^2)
@@ -1245,11 +1247,11 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     const int s0 = r0 + 1, f0 = r0 + 1 + NS, Wv = f0 + (Kd - r0);  // slot / Fourier / end columns
     // Kpv == 16 NTC and f0 == 16 NTR (the launch groups instances by both)
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
-    // trig blocks past Kpv: A = [cos a theta | sin a theta]/sigma (a < 8), B = [cos 8b theta |
-    // sin 8b theta]/sigma (b < 8): the tile A^T B holds every C_m, S_m (weighted), m = a + 8b
-    // < 64 -- F^T W F (k_greduce).  The unweighted sums for the Fourier column norms depend
-    // on the TOAs only (PsrDev::trigU, formed at upload).  DUM: the write-only dummy column.
-    const int tA = Kpv, tB = Kpv + 16, DUM = Kpv + 32, tX = Kpv + 33, Kpt = Kpv + (VB ? 49 : 33);
+    // past Kpv (VB): the trig block A = [cos a theta | sin a theta]/sigma (a < 8) and the
+    // binned block B'' (tX).  F^T W F comes from the weighted trig sums C_m, S_m, which depend
+    // on the TOAs and sigma only (PsrDev::trigW, k_trigw); the unweighted sums for the Fourier
+    // column norms likewise (PsrDev::trigU).  DUM: the write-only dummy column.
+    const int tA = Kpv, DUM = Kpv + 16, tX = Kpv + 17, Kpt = Kpv + (VB ? 33 : 17);
     double* const Tb0 = lds;
     double* const Tb1 = lds + (GVB - 1) * Kpt * CS;
     long i0, i1;
@@ -1261,7 +1263,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     const double* xv = dmxv + I.ooff;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    double4_t acc[NT], accW = {0, 0, 0, 0};
+    double4_t acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
     double csq[QL];  // sums of squares of this wave's timing columns (lanes = rows)
@@ -1346,16 +1348,17 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
             // trig blocks: harmonic a of A and 8a of B, a = W + GW j (weighted: the rotations
             // below are linear, so they carry the weight along)
             const int a = W + GW * j;
-            double ca, sa, cb, sb;
+            double ca, sa;
             cpow_u8(c1_n, s1_n, a, ca, sa);
-            cpow_u8(c8_n, s8_n, a, cb, sb);
             ca *= iw;
             sa *= iw;
-            put(Ts, tA + a, ca);
-            put(Ts, tA + 8 + a, sa);
-            put(Ts, tB + a, cb * iw);
-            put(Ts, tB + 8 + a, sb * iw);
+            if (VB) {  // the trig block A of the binned tile
+                put(Ts, tA + a, ca);
+                put(Ts, tA + 8 + a, sa);
+            }
             if (VB && j == 0) {
+                double cb, sb;
+                cpow_u8(c8_n, s8_n, a, cb, sb);
                 // B'' = x [cos 8a theta | sin 8a theta]/sigma (a < 4) in the 8 columns of the
                 // row's bin parity, zeros in the other 8
                 const bool odd = (d_n & 1) != 0;
@@ -1407,10 +1410,9 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[k], 0, 0, 0);
                 }
             }
-            // trig tile, unconditional (zero in LDS without red noise)
-            const double ta = Tr[tA * CS];
-            accW = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, Tr[tB * CS], accW, 0, 0, 0);
-            if (VB) accB = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, Tr[tX * CS], accB, 0, 0, 0);
+            // binned DMX x F tile (the weighted trig sums of F^T W F are formed once per pulsar,
+            // k_trigw: TOA and sigma only)
+            if (VB) accB = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], Tr[tX * CS], accB, 0, 0, 0);
         }
     };
     const long nch = i1 > i0 ? (i1 - i0 + CH - 1) / CH : 0;
@@ -1546,28 +1548,6 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
             } else {
                 g++;
             }
-        }
-    }
-    if (nred > 0) {  // trig tile: sum over the waves, then C, S of m = a + 8b
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 4; q++) red[(wave * 4 + q) * 64 + lane] = accW[q];
-        __syncthreads();
-        double* tsum = red + GW * 256;  // [256]
-        for (int e = tid; e < 256; e += NTH) {
-            double v = 0.0;
-#pragma unroll
-            for (int w = 0; w < GW; w++) v += red[w * 256 + e];
-            tsum[e] = v;
-        }
-        __syncthreads();
-        // tile element (i, j) at ((i >> 2) * 64 + (i & 3) * 16 + j) (f64 MFMA C/D layout)
-        auto tix = [](int i, int j) { return ((i >> 2) << 6) + ((i & 3) << 4) + j; };
-        double* out = TSp + ((long)I.self * nsplit + split) * (4 * VTRIG);
-        for (int m = tid; m < VTRIG; m += NTH) {
-            const int a = m & 7, b = m >> 3;
-            out[m] = tsum[tix(a, b)] - tsum[tix(8 + a, 8 + b)];          // C_m
-            out[VTRIG + m] = tsum[tix(8 + a, b)] + tsum[tix(a, 8 + b)];  // S_m
         }
     }
     GVTS(3);
@@ -1854,6 +1834,26 @@ __global__ __launch_bounds__(128) void k_trigu(const double* __restrict__ cs, in
     }
     part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
 }
+// k_trigw: the weighted sums C_m = sum_i w_i cos m theta_i, S_m = sum_i w_i sin m theta_i (m <
+// 64, w = 1/sigma^2) that give the Gram's F^T W F block (k_greduce's product-to-sum
+// identities); e^{i m theta} = e^{i a theta} e^{i 8b theta} (m = a + 8b) from the row's
+// e^{i theta} and e^{i 8 theta} (k_redbase), as k_gram_v formed them before they moved here.
+// They depend on the TOAs and sigma only, so they are formed at upload and when the
+// uncertainties change (pint_set_sigma), not in every fit step; summed by k_trigu_sum.
+__global__ __launch_bounds__(128) void k_trigw(const double* __restrict__ cs, const double* __restrict__ isig, int n,
+                                               double* __restrict__ part) {
+    const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
+    const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);
+    double acc = 0.0;
+    for (int i = i0; i < i1; i++) {
+        double ca, sa, cb, sb;
+        cpow(cs[4 * i], cs[4 * i + 1], m & 7, ca, sa);
+        cpow(cs[4 * i + 2], cs[4 * i + 3], m >> 3, cb, sb);
+        const double w = isig[i] * isig[i];
+        acc += kind ? w * (sa * cb + ca * sb) : w * (ca * cb - sa * sb);
+    }
+    part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
+}
 __global__ __launch_bounds__(256) void k_trigu_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
     __shared__ double sh[4];
     double acc = 0.0;
@@ -1871,6 +1871,10 @@ __global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, c
     const int m = threadIdx.x, nb = nsplit;
     if (m >= 2 * VTRIG) {  // unweighted sums: TOA-only, formed at upload (k_trigu)
         TS[(long)I.self * 4 * VTRIG + m] = Pd.trigU[m - 2 * VTRIG];
+        return;
+    }
+    if (Pd.trigW) {  // weighted sums: TOA and sigma only, formed at upload / pint_set_sigma (k_trigw)
+        TS[(long)I.self * 4 * VTRIG + m] = Pd.trigW[m];
         return;
     }
     const double* p = TSp + (long)I.self * nsplit * (4 * VTRIG) + m;
@@ -3939,6 +3943,20 @@ extern "C" void pint_release_cache(void) {
     hipSetDevice(cur);
 }
 
+// the weighted trig sums of a pulsar with red noise (PsrDev::trigW) from its current isig
+static int form_trigw(pint_ctx* ctx, const PsrDev& d, int n) {
+    if (!d.trigW || !d.red_cs || n <= 0) return 0;
+    const int nb = (n + TRIGU_R - 1) / TRIGU_R;
+    double* part = nullptr;
+    HIPCHK(hipMalloc((void**)&part, sizeof(double) * 128 * std::max(1, nb)));
+    hipLaunchKernelGGL(k_trigw, dim3(nb), dim3(128), 0, ctx->stream, d.red_cs, d.isig, n, part);
+    hipLaunchKernelGGL(k_trigu_sum, dim3(128), dim3(256), 0, ctx->stream, part, nb, (double*)d.trigW);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipFree(part));
+    return 0;
+}
+
 template <typename T>
 static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const T*& dst) {
     void* p = nullptr;
@@ -4143,6 +4161,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         HIPCHK(hipGetLastError());
     }
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
+    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
     if (!rc && spec->nred > 0) {
         const int nb = (n + TRIGU_R - 1) / TRIGU_R;
         double* part = nullptr;
@@ -4152,6 +4171,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(ctx->stream));
         HIPCHK(hipFree(part));
+        if (form_trigw(ctx, d, n)) return PINT_E_HIP;
     }
     {
         // compact fit layout: DMX columns out of M when there are enough of them and no TOA
@@ -5049,7 +5069,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             hipEvent_t e0 = (ext_t && gi == 0) ? ctx->ev[12] : nullptr;
             hipEvent_t e1 = (ext_t && gi + 1 == ctx->kp_groups_v.size()) ? ctx->ev[13] : nullptr;
             dim3 grid(ctx->nsplit, kg.count);
-            const size_t lds = sizeof(double) * std::max<size_t>((size_t)GVB * (kg.maxKp + (ctx->vb_on && kg.maxKp <= 96 ? 49 : 33)) * (VCH + 2),
+            const size_t lds = sizeof(double) * std::max<size_t>((size_t)GVB * (kg.maxKp + (ctx->vb_on && kg.maxKp <= 96 ? 33 : 17)) * (VCH + 2),
                                                                  std::max(GW * VTG * 256, GW * 256 + 256));
 #define PINT_GRAMV(R_, C_)                                                                                       \
             if (ctx->vb_on && C_ <= 6)                                                                               \
@@ -5788,6 +5808,7 @@ int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
     HIPCHK(hipMemcpyAsync((void*)ph.dev.sigma, sigma_s, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync((void*)ph.dev.isig, is.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (ph.spec.nred > 0 && form_trigw(ctx, ph.dev, n)) return PINT_E_HIP;  // the F^T W F sums of the new weights
     ph.dev.logsig = ls;
     ph.dev.sumw = sw;
     return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;
