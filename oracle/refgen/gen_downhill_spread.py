@@ -12,6 +12,9 @@ the TOAs themselves is below tdbld's longdouble resolution (0.5 ns at MJD 5e4) -
 records, per fitted parameter, max |p_perturbed - p_unperturbed| / sigma.
 tests/test_gpu_parity.py::test_downhill_gls sets its per-parameter bar from it.
 
+wb_dd runs WidebandDownhillFitter (fitter.py:1812-1895) the same way; its TOA residuals
+(WidebandTOAResiduals.toa) are the perturbed ones.
+
 Usage: oracle/refenv/run_ref.sh oracle/refgen/gen_downhill_spread.py [name ...]
 Writes tests/golden/downhill_spread.json.
 """
@@ -33,8 +36,8 @@ NREP = 8
 SIGMA_S = 5e-12
 
 
-def fit(model, toas):
-    f = pfit.DownhillGLSFitter(toas, copy.deepcopy(model))
+def fit(model, toas, cls=pfit.DownhillGLSFitter):
+    f = cls(toas, copy.deepcopy(model))
     try:
         f.fit_toas(maxiter=10)
         status = "converged"
@@ -46,8 +49,14 @@ def fit(model, toas):
 
 
 def spread(name):
-    model, toas = rebuild(name)
-    v0, e0, s0, c0 = fit(model, toas)
+    cls = pfit.DownhillGLSFitter
+    if name == "wb_dd":  # WidebandDownhillFitter; the TOA part of its residuals is perturbed
+        import gen_wideband
+        _, model, toas = gen_wideband.build()
+        cls = pfit.WidebandDownhillFitter
+    else:
+        model, toas = rebuild(name)
+    v0, e0, s0, c0 = fit(model, toas, cls)
     worst = {p: 0.0 for p in v0}
     statuses, chi2s = [], []
     orig = pres.Residuals.calc_time_resids
@@ -59,7 +68,7 @@ def spread(name):
                 return orig(self, *a, **k) + delta * u.s
 
             pres.Residuals.calc_time_resids = calc
-            v, e, s, c = fit(model, toas)
+            v, e, s, c = fit(model, toas, cls)
             statuses.append(s)
             chi2s.append(c / c0 - 1)
             for p in v0:

@@ -31,8 +31,8 @@ DMEQUAD mjd 53000 55000 0.0002
 """
 
 
-def main():
-    register_clockless_sites()
+def build():
+    """(par text, model, TOAs) of wb_dd (seeded: the same TOAs on every call)."""
     np.random.seed(21)
     par = pta_par(21, "DD") + EXTRA
     model = get_model(io.StringIO(par))
@@ -41,6 +41,12 @@ def main():
                                     include_bipm=False, multi_freqs_in_epoch=False, wideband=True,
                                     wideband_dm_error=2e-4 * u.pc / u.cm ** 3)
     model.find_empty_masks(ts, freeze=True)
+    return par, model, ts
+
+
+def main():
+    register_clockless_sites()
+    par, model, ts = build()
     with open(f"{GOLDEN}/wb_dd.par", "w") as f:
         f.write(par)
     arr, flags = pack_toas(ts)

@@ -1205,18 +1205,19 @@ __device__ __forceinline__ void vb_flush(double4_t& acc, double* __restrict__ ds
 #pragma unroll
     for (int q = 0; q < 4; q++) acc[q] = mine ? 0.0 : acc[q];
 }
-// VB: bin b enters the accumulator half of its parity; a half holding another bin is flushed
+// VB: bin b enters the accumulator half of its parity; a half holding another bin is flushed.
+// cur0/cur1 are updated by selects, not by stores in two branches: the branch form was merged
+// into a parity-indexed private array (scratch), whose reload waited on vmcnt(0) -- i.e. on the
+// next chunk's prefetch -- in every chunk
 #define VB_ENTER(b)                                                                                  \
     do {                                                                                             \
         const int b_ = (b);                                                                          \
-        if (b_ & 1) {                                                                                \
-            if (cur1 != b_) {                                                                        \
-                if (cur1 >= 0) vb_flush(accB, vbase + (long)(cur1 % NS) * 128, 1, lane);            \
-                cur1 = b_;                                                                           \
-            }                                                                                        \
-        } else if (cur0 != b_) {                                                                     \
-            if (cur0 >= 0) vb_flush(accB, vbase + (long)(cur0 % NS) * 128, 0, lane);                 \
-            cur0 = b_;                                                                               \
+        const int p_ = b_ & 1;                                                                       \
+        const int c_ = p_ ? cur1 : cur0;                                                             \
+        if (c_ != b_) {                                                                              \
+            if (c_ >= 0) vb_flush(accB, vbase + (long)(c_ % NS) * 128, p_, lane);                    \
+            cur1 = __builtin_amdgcn_readfirstlane(p_ ? b_ : cur1);                                   \
+            cur0 = __builtin_amdgcn_readfirstlane(p_ ? cur0 : b_);                                   \
         }                                                                                            \
     } while (0)
 

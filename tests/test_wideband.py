@@ -131,9 +131,12 @@ def test_gpu_wideband_fit():
 @pytest.mark.gpu
 def test_gpu_wideband_downhill():
     """WidebandDownhillFitter on the device (the wideband GLS step + the combined chi2 in the
-    line search) against the reference's: status, chi2 at the end-to-end floor, parameters
-    within 2e-4 sigma (10x the 2e-5 sigma measured on MI355X)."""
-    from golden_util import load
+    line search) against the reference's: status, chi2 at the end-to-end floor, and per
+    parameter 2e-4 sigma or 2x the reference's own spread when its TOA residuals are perturbed
+    at the 5 ps floor, where that is larger (downhill_spread.json["wb_dd"]: the nearly
+    degenerate M2 / SINI pair and the orbital parameters move the reference's accepted iterate
+    by up to 1.2e-3 sigma; the device measured 1.16e-3 sigma, SINI)."""
+    from golden_util import load, downhill_bar
     from pint_amd import WidebandDownhillFitter
     from pint_amd.fitter import MaxiterReached, StepProblem
     model, toas, z, meta = load("wb_dd")
@@ -146,9 +149,11 @@ def test_gpu_wideband_downhill():
     assert status == meta["wbdown_status"]
     assert abs(f.resids.chi2 / meta["wbdown_chi2"] - 1) < 5e-6, (f.resids.chi2, meta["wbdown_chi2"])
     ref = _ref_pars(meta, "wbdown_params")
-    worst = max(abs(float((LD(f.model[p].value) - ref[p]) / LD(meta["wbdown_errors"][p]))) for p in ref)
-    print(f"wideband downhill: chi2 {f.resids.chi2:.6f} ref {meta['wbdown_chi2']:.6f}, worst {worst:.2e} sigma")
-    assert worst < 2e-4, worst
+    dev = {p: abs(float((LD(f.model[p].value) - ref[p]) / LD(meta["wbdown_errors"][p]))) for p in ref}
+    p_w = max(dev, key=dev.get)
+    print(f"wideband downhill: chi2 {f.resids.chi2:.6f} ref {meta['wbdown_chi2']:.6f}, worst {dev[p_w]:.2e} sigma ({p_w})")
+    for p, d in dev.items():
+        assert d < downhill_bar("wb_dd", p, floor=2e-4), (p, d, downhill_bar("wb_dd", p, floor=2e-4))
 
 
 @pytest.mark.gpu
