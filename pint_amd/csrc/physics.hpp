@@ -81,10 +81,14 @@ PD void pm_setup_trig(double pmr, double pmd, double px, const PmTrig& T, PmStat
     double cz = a1[0] * b1[1] - a1[1] * b1[0];
     double ss = sqrt(cx * cx + cy * cy + cz * cz);
     double cs = a1[0] * b1[0] + a1[1] * b1[1] + a1[2] * b1[2];
-    double pm = (ss != 0.0 || cs != 0.0) ? atan2(ss, cs) : 0.0;
     double px1a = px;
-    pm *= 326.0;
-    if (px1a < pm) px1a = pm;
+    // the separation pm = atan2(ss, cs) only enters as max(px, 326 pm); with cs > 0,
+    // atan2(ss, cs) = atan(ss / cs) <= ss / cs, so when 326 ss / cs (with a rounding margin)
+    // stays below px the override cannot apply and the atan2 chain is skipped
+    if ((ss != 0.0 || cs != 0.0) && !(cs > 0.0 && 326.0 * (ss / cs) * (1.0 + 1e-12) < px1a)) {
+        const double pm = 326.0 * atan2(ss, cs);
+        if (px1a < pm) px1a = pm;
+    }
     if (px1a < 5e-7) px1a = 5e-7;
     // starpv (rv = 0)
     double w = px1a >= 1e-7 ? px1a : 1e-7;
@@ -267,23 +271,33 @@ PD void inst_setup_wave(const pint_spec_t& S, const double* P, InstConst& C, dou
         sx[4] = ipb.hi;
         sx[5] = ipb.lo;
     }
-    __syncthreads();
     const bool pm = !(pml == 0.0 && pmb == 0.0);
-    const double cd = sx[2];
-    const double pmr = pml * MAS_RAD / cd, pmd = pmb * MAS_RAD;
-    if (pm) {
-        if (lane == 0) {
-            const double ra2 = ra + pmr;
-            sx[8] = cos(ra2);
-            sx[9] = sin(ra2);
-        } else if (lane == 1) {
-            const double dec2 = dec + pmd;
-            sx[10] = cos(dec2);
-            sx[11] = sin(dec2);
-        }
+    const double pmd = pmb * MAS_RAD;
+    if (pm && lane == 3) {  // dec2 does not depend on the other trig values: same phase
+        const double dec2 = dec + pmd;
+        sx[10] = cos(dec2);
+        sx[11] = sin(dec2);
     }
     __syncthreads();
     if (lane != 0) return;
+    const double cd = sx[2];
+    const double pmr = pml * MAS_RAD / cd;
+    if (pm) {
+        // cos/sin of ra2 = fl(ra + pmr) by angle addition from ra's: d = ra2 - ra is exact
+        // (Sterbenz) and small, its sine and cosine are short Taylor series (a direct sincos
+        // would need a second dependent transcendental phase); a large d takes sincos
+        const double ra2 = ra + pmr, d = ra2 - ra;
+        if (fabs(d) < 1e-2) {
+            const double d2 = d * d;
+            const double sd = d * (1.0 - d2 * (1.0 / 6.0 - d2 * (1.0 / 120.0 - d2 * (1.0 / 5040.0))));
+            const double cdl = 1.0 - d2 * (0.5 - d2 * (1.0 / 24.0 - d2 * (1.0 / 720.0 - d2 * (1.0 / 40320.0))));
+            sx[8] = sx[0] * cdl - sx[1] * sd;
+            sx[9] = sx[1] * cdl + sx[0] * sd;
+        } else {
+            sx[8] = cos(ra2);
+            sx[9] = sin(ra2);
+        }
+    }
     C.F0 = pval(P, S.o_F);
     C.iF0 = 1.0 / C.F0;
     C.has_pm = 0;

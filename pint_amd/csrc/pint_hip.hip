@@ -1863,37 +1863,9 @@ __global__ __launch_bounds__(256) void k_trigu_sum(const double* __restrict__ pa
     if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
-// k_tsum: k_gram_v's per-split trig-sum partials of an instance summed in a fixed order
-__global__ __launch_bounds__(256) void k_tsum(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                              int nsplit, const double* __restrict__ TSp, double* __restrict__ TS) {
-    const InstDev I = insts[blockIdx.x];
-    const PsrDev& Pd = psrs[I.psr];
-    if (!Pd.vg) return;
-    const int m = threadIdx.x, nb = nsplit;
-    if (m >= 2 * VTRIG) {  // unweighted sums: TOA-only, formed at upload (k_trigu)
-        TS[(long)I.self * 4 * VTRIG + m] = Pd.trigU[m - 2 * VTRIG];
-        return;
-    }
-    if (Pd.trigW) {  // weighted sums: TOA and sigma only, formed at upload / pint_set_sigma (k_trigw)
-        TS[(long)I.self * 4 * VTRIG + m] = Pd.trigW[m];
-        return;
-    }
-    const double* p = TSp + (long)I.self * nsplit * (4 * VTRIG) + m;
-    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-    int x = 0;
-    for (; x + 3 < nb; x += 4) {
-        v0 += p[(long)x * 4 * VTRIG];
-        v1 += p[(long)(x + 1) * 4 * VTRIG];
-        v2 += p[(long)(x + 2) * 4 * VTRIG];
-        v3 += p[(long)(x + 3) * 4 * VTRIG];
-    }
-    for (; x < nb; x++) v0 += p[(long)x * 4 * VTRIG];
-    TS[(long)I.self * 4 * VTRIG + m] = (v0 + v1) + (v2 + v3);
-}
-
 // Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
 // triangle only, in a fixed order (deterministic), and the column sums of squares.
-// vg instances: the Fourier block F^T W F from the trig sums TS (k_gram_v + k_tsum) by the
+// vg instances: the Fourier block F^T W F from the pulsar's weighted trig sums (trigW) by the
 // product-to-sum identities (a, b = harmonics 1..nred), and past block nbg the DMX bin
 // rows Sd, DD, DCS from k_gram_v's slot partials of the N-splits the bin's rows fall in:
 //   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
@@ -1973,7 +1945,7 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
             if (vg && (j > Kc)) {
                 G[e] = 0.0;  // padding
             } else if (vg && i >= r0 && j < Kc) {
-                const double* C = TS + (long)I.self * 4 * VTRIG;
+                const double* C = Pd.trigW;  // C_m, S_m (k_trigw: TOA and sigma only)
                 const double* Sn = C + VTRIG;
                 const int ha = (i - r0) / 2 + 1, sa = (i - r0) & 1;  // 0 sin, 1 cos
                 const int hb = (j - r0) / 2 + 1, sb = (j - r0) & 1;
@@ -1995,7 +1967,7 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
     if (e < Kc) {
         double* cs = colsq + (I.coff + e) * nsplit;
         if (vg && e >= r0) {  // Fourier column: sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2
-            const double* U = TS + (long)I.self * 4 * VTRIG + 2 * VTRIG;
+            const double* U = Pd.trigU;  // U_m (k_trigu: TOA only)
             const int h = (int)(e - r0) / 2 + 1;
             cs[0] = 0.5 * (U[0] + (((e - r0) & 1) ? U[2 * h] : -U[2 * h]));
         } else {
@@ -3320,8 +3292,8 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 const double* __restrict__ eW, const double* __restrict__ wpart,
                                                 int nsplit, int stride, double* __restrict__ ecs,
                                                 double* __restrict__ chi2, double* __restrict__ lognorm,
-                                                const double* __restrict__ wtile, const double* __restrict__ chi2w,
-                                                int compact) {
+                                                const double* __restrict__ wtile, const double* __restrict__ rpart,
+                                                double* __restrict__ chi2w, int compact) {
     extern __shared__ double lds[];
     __shared__ double sh[8];
     __shared__ double Dt[256], wloc[130];
@@ -3334,6 +3306,18 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     double* d = lds;  // Kn
     const double* wp = wpart + (long)inst * nsplit * stride;
     if (wtile) {
+        // r^T W r: the residual pass's chi2 partials of the instance summed exactly as k_rsum
+        // does (wave 0, same order: the same bits), stored as the residuals' chi2 (k_rsum is
+        // then not launched for this pass)
+        if (threadIdx.x < 64) {
+            double t = 0.0;
+            for (int k = threadIdx.x; k < I.nrb; k += 64) t += rpart[3 * (I.rb0 + k) + 2];
+            t = wave_sum(t);
+            if (threadIdx.x == 0) {
+                chi2w[inst] = t;
+                wloc[R] = t;
+            }
+        }
         // the dots from k_resid2's trig tiles (one per residual block of the instance, summed
         // in block order): F_j^T W r (sin, cos of harmonic h + 1 at 2h, 2h + 1), r^T W r (the
         // residual pass's chi2) at R, 1^T W r = D[0][0] at R + 1 -- k_wdot's layout, one split
@@ -3346,10 +3330,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
             wloc[2 * h] = Dt[(8 + a) * 16 + b] + Dt[a * 16 + 8 + b];      // sum w r sin(k theta)
             wloc[2 * h + 1] = Dt[a * 16 + b] - Dt[(8 + a) * 16 + 8 + b];  // sum w r cos(k theta)
         }
-        if (threadIdx.x == 0) {
-            wloc[R] = chi2w[inst];
-            wloc[R + 1] = Dt[0];
-        }
+        if (threadIdx.x == 0) wloc[R + 1] = Dt[0];
         __syncthreads();
         wp = wloc;
         nsplit = 1;
@@ -3819,6 +3800,7 @@ struct pint_ctx {
     long tables0_cap = 0;
     bool restore_pending = false;  // pint_restore_tables not yet carried out (k_prep does it)
     double* chi2_dst = nullptr;    // lazy pint_chi2_gls: the host buffer of its deferred copy
+    bool chi2_pending = false;     // d_chi2 not yet summed from the last residual pass's partials
     // fit outputs the copy stream reads, one set per pipeline slot: a step's solve writes its
     // slot's set while the copies of the previous step (the other slot) may still run, so the
     // solve need not wait for them (copy_pend[slot]: copies of that slot's set in flight)
@@ -4879,7 +4861,9 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                            ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
                            wt ? ctx->d_wtile : nullptr);
-        hipLaunchKernelGGL(k_rsum, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_inst, ctx->d_rpart, ctx->d_chi2);
+        // the chi2 partials are summed when the chi2 is read (pint_read_resids) or by k_wsolve,
+        // which needs them anyway: no launch of its own in a fit step
+        ctx->chi2_pending = true;
         ctx->wtile_valid = wt;
     }
     HIPCHK(hipGetLastError());
@@ -4891,6 +4875,11 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 }
 
 int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, double* chi2) {
+    if (chi2 && ctx->chi2_pending) {
+        hipLaunchKernelGGL(k_rsum, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_inst, ctx->d_rpart, ctx->d_chi2);
+        HIPCHK(hipGetLastError());
+        ctx->chi2_pending = false;
+    }
     if (time_resid) HIPCHK(hipMemcpyAsync(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (phase_resid) HIPCHK(hipMemcpyAsync(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (chi2) HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
@@ -5108,9 +5097,6 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         }
         if (ext_t) ctx->rec[12] = ctx->rec[13] = true;
         else if (gram_mark) record(ctx, 13);
-        hipLaunchKernelGGL(k_tsum, dim3(ctx->ninst), dim3(4 * VTRIG), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->nsplit, ctx->d_TSp, ctx->d_TS);
-        HIPCHK(hipGetLastError());
     } else if (gram_mark) {
         record(ctx, 13);
     }
@@ -5426,9 +5412,10 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
                        ctx->stream, ctx->d_psrs,
                        ctx->d_inst, ctx->d_rt, ctx->d_sigL, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_wpart, nsw,
                        stride, ctx->d_ecs, ctx->d_chi2g, ctx->d_lognorm,
-                       ctx->wtile_valid ? (const double*)ctx->d_wtile : nullptr, (const double*)ctx->d_chi2,
-                       ctx->m_compact);
+                       ctx->wtile_valid ? (const double*)ctx->d_wtile : nullptr, (const double*)ctx->d_rpart,
+                       ctx->d_chi2, ctx->m_compact);
     HIPCHK(hipGetLastError());
+    if (ctx->wtile_valid) ctx->chi2_pending = false;  // k_wsolve stored the residuals' chi2
     record(ctx, 11);
     if (ctx->lazy && !ctx->capturing) {
         // the copy is deferred to pint_step_end (the copy stream, after the step's end event:

@@ -1,0 +1,48 @@
+"""Per-step kernel timeline from a rocprofv3 kernel trace of the bench (PTA leg only):
+    python scripts/step_timeline.py gpurun_out/profq/run_kernel_trace.csv
+Finds the steady-state steps (one k_gram_v group launch per step), and prints for the median
+step each dispatch's start offset, duration and the idle gap before it (queue 0 = the main
+stream; the copy-stream kernels are listed with their stream)."""
+import csv
+import sys
+from collections import defaultdict
+
+import numpy as np
+
+
+def short(name):
+    n = name.split("(")[0]
+    return n.replace("void ", "")[:40]
+
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+ks = []
+for r in rows:
+    ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+               r.get("Queue_Id", r.get("Stream_Id", "?"))))
+ks.sort()
+# steps start at each k_prep whose table reset precedes the evaluation with M
+starts = [i for i, k in enumerate(ks) if k[2].startswith("k_prep")]
+steps = []
+for a, b in zip(starts, starts[1:]):
+    seg = ks[a:b]
+    if any(k[2].startswith("k_gram_v") for k in seg):
+        steps.append(seg)
+steps = steps[len(steps) // 3:]  # steady state
+dur = [s[-1][1] - s[0][0] for s in steps]
+med = steps[int(np.argsort(dur)[len(dur) // 2])]
+print(f"{len(steps)} steady steps; span median {np.median(dur) / 1e3:.1f} us (min {min(dur) / 1e3:.1f})")
+t0 = med[0][0]
+prev_end = defaultdict(lambda: t0)
+tot = defaultdict(float)
+for s, e, n, q in med:
+    gap = s - prev_end[q]
+    print(f"  q{q:>3} +{(s - t0) / 1e3:7.1f} us  {(e - s) / 1e3:6.1f} us  gap {gap / 1e3:5.1f}  {n}")
+    prev_end[q] = e
+# per-kernel average over the steady steps
+for st in steps:
+    for s, e, n, q in st:
+        tot[n] += (e - s) / 1e3 / len(steps)
+print("per-step kernel time (avg over steady steps):")
+for n, v in sorted(tot.items(), key=lambda kv: -kv[1]):
+    print(f"  {v:7.1f} us  {n}")
