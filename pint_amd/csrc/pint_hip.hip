@@ -1870,78 +1870,84 @@ __global__ __launch_bounds__(256) void k_trigu_sum(const double* __restrict__ pa
 // rows Sd, DD, DCS from k_gram_v's slot partials of the N-splits the bin's rows fall in:
 //   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
 //   sin a cos b = (S_a+b + S_a-b)/2     (S_-k = -S_k),
-__global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                 int nsplit, int nparts, int compact, int nbg,
-                                                 double* __restrict__ Gpart, double* __restrict__ colsq,
-                                                 const double* __restrict__ TS, const double* __restrict__ Sdp,
-                                                 const double* __restrict__ dmxv, double* __restrict__ Sd,
-                                                 double* __restrict__ DD, double* __restrict__ DCS,
-                                                 const double* __restrict__ BFp, int vb) {
-    const InstDev I = insts[blockIdx.y];
-    const PsrDev& Pd = psrs[I.psr];
-    const bool cmp = compact && Pd.dsplit;
+struct GredArgs {
+    int nsplit, nparts, compact, vb;
+    double* Gpart;
+    double* colsq;
+    const double* Sdp;
+    const double* dmxv;
+    double* Sd;
+    double* DD;
+    double* DCS;
+    const double* BFp;
+};
+
+// DMX bin a of a vg instance (one wave, lane = lane index): its row Sd (DMX x [T|r|F], from
+// the slot partials or the binned VB partials of the N-splits the bin's rows fall in), DD
+// and DCS.  Wave-uniform: only wave-level reductions.
+__device__ __forceinline__ void gred_bin(const InstDev& I, const PsrDev& Pd, const GredArgs& g, int a, int lane) {
+    const int Kp = Pd.Kpd, Kc = Pd.Kd, r0 = Pd.red0c, nsplit = g.nsplit;
+    const int SW = Kc + 3;
+    const int cnt = Pd.dptr[a + 1] - Pd.dptr[a];
+    const long lo = cnt > 0 ? Pd.didx[Pd.dptr[a]] : 0, hi = lo + cnt;
+    long per = (I.n + nsplit - 1) / nsplit;
+    per = (per + 3) / 4 * 4;
+    const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
+    const double* part = g.Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
+    for (int c = lane; c <= Kc; c += 64) {
+        double v = 0.0;
+        if (g.vb && Pd.vb && c >= r0 && c < Kc) {
+            // binned DMX x F (k_gram_v VB): the 16x8 blocks D of the (split, wave) quarters
+            // the bin's rows touch; harmonic k = a_ + 8 cc: cos = D[a_][cc] - D[8+a_][4+cc],
+            // sin = D[8+a_][cc] + D[a_][4+cc]; column r0 + 2h is sin((h+1) theta), +1 cos
+            const int h = (c - r0) >> 1, k = h + 1, a_ = k & 7, cc = k >> 3;
+            const bool isin = ((c - r0) & 1) == 0;
+            const int e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
+            const int e1 = isin ? a_ * 8 + 4 + cc : (8 + a_) * 8 + 4 + cc;
+            const double sg = isin ? 1.0 : -1.0;
+            for (int q = q0; q <= q1; q++) {
+                const long s0_ = (long)q * per, s1_ = min((long)I.n, s0_ + per), len = s1_ - s0_;
+                const long QV = (len + VCH - 1) / VCH * 16;
+                for (int w = 0; w < GW; w++) {
+                    const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
+                    if (w0 >= w1 || hi <= w0 || lo >= w1) continue;  // no row of the bin here
+                    const double* D = g.BFp + I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
+                    v += D[e0] + sg * D[e1];
+                }
+            }
+        } else {
+            for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
+        }
+        g.Sd[I.sdoff + (long)a * Kp + c] = v;
+    }
+    // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
+    // square norm is the bin's only DMX x DMX entry: k_gram_v skips those tiles)
+    double q2 = 0.0, qw = 0.0;
+    for (long i = lo + lane; i < hi; i += 64) {
+        const double xx = g.dmxv[I.ooff + i], xw = xx * Pd.isig[i];
+        q2 += xx * xx;
+        qw += xw * xw;
+    }
+    q2 = wave_sum(q2);
+    qw = wave_sum(qw);
+    if (lane == 0) {
+        g.DCS[I.ddoff + a] = q2;
+        g.DD[I.ddoff + a] = qw;
+    }
+}
+
+// element e of an instance's Gram (slot 0 <- sum of the N-split partials, upper triangle;
+// vg: F^T W F from the trig sums, padding zero) and, for e < Kc, the column sum of squares
+__device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, const GredArgs& g, long e) {
+    const bool cmp = g.compact && Pd.dsplit;
     const bool vg = cmp && Pd.vg;
     const int Kp = cmp ? Pd.Kpd : I.Kp, Kc = cmp ? Pd.Kd : I.K;
     const int r0 = Pd.red0c;
-    if ((int)blockIdx.x >= nbg) {  // DMX bins of a vg instance (one per wave): slot partials
-        const int lane = threadIdx.x & 63;
-        const int a = (blockIdx.x - nbg) * 4 + (threadIdx.x >> 6);
-        if (!vg || a >= Pd.ndc) return;  // wave-uniform: only wave-level reductions below
-        const int SW = Kc + 3;
-        const int cnt = Pd.dptr[a + 1] - Pd.dptr[a];
-        const long lo = cnt > 0 ? Pd.didx[Pd.dptr[a]] : 0, hi = lo + cnt;
-        long per = (I.n + nsplit - 1) / nsplit;
-        per = (per + 3) / 4 * 4;
-        const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
-        const double* part = Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
-        for (int c = lane; c <= Kc; c += 64) {
-            double v = 0.0;
-            if (vb && Pd.vb && c >= r0 && c < Kc) {
-                // binned DMX x F (k_gram_v VB): the 16x8 blocks D of the (split, wave) quarters
-                // the bin's rows touch; harmonic k = a_ + 8 cc: cos = D[a_][cc] - D[8+a_][4+cc],
-                // sin = D[8+a_][cc] + D[a_][4+cc]; column r0 + 2h is sin((h+1) theta), +1 cos
-                const int h = (c - r0) >> 1, k = h + 1, a_ = k & 7, cc = k >> 3;
-                const bool isin = ((c - r0) & 1) == 0;
-                const int e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
-                const int e1 = isin ? a_ * 8 + 4 + cc : (8 + a_) * 8 + 4 + cc;
-                const double sg = isin ? 1.0 : -1.0;
-                for (int q = q0; q <= q1; q++) {
-                    const long s0_ = (long)q * per, s1_ = min((long)I.n, s0_ + per), len = s1_ - s0_;
-                    const long QV = (len + VCH - 1) / VCH * 16;
-                    for (int w = 0; w < GW; w++) {
-                        const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
-                        if (w0 >= w1 || hi <= w0 || lo >= w1) continue;  // no row of the bin here
-                        const double* D = BFp + I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
-                        v += D[e0] + sg * D[e1];
-                    }
-                }
-            } else {
-                for (int q = q0; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
-            }
-            Sd[I.sdoff + (long)a * Kp + c] = v;
-        }
-        // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
-        // square norm is the bin's only DMX x DMX entry: k_gram_v skips those tiles)
-        double q2 = 0.0, qw = 0.0;
-        for (long i = lo + lane; i < hi; i += 64) {
-            const double xx = dmxv[I.ooff + i], xw = xx * Pd.isig[i];
-            q2 += xx * xx;
-            qw += xw * xw;
-        }
-        q2 = wave_sum(q2);
-        qw = wave_sum(qw);
-        if (lane == 0) {
-            DCS[I.ddoff + a] = q2;
-            DD[I.ddoff + a] = qw;
-        }
-        return;
-    }
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long KK = (long)Kp * Kp;
     if (e < KK) {
         const int i = (int)(e / Kp), j = (int)(e % Kp);
         if (i <= j) {
-            double* G = Gpart + I.goff;
+            double* G = g.Gpart + I.goff;
             if (vg && (j > Kc)) {
                 G[e] = 0.0;  // padding
             } else if (vg && i >= r0 && j < Kc) {
@@ -1959,23 +1965,44 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
                 G[e] = v;
             } else {
                 double sacc = G[e];
-                for (int q = 1; q < nparts; q++) sacc += G[(long)q * KK + e];
+                for (int q = 1; q < g.nparts; q++) sacc += G[(long)q * KK + e];
                 G[e] = sacc;
             }
         }
     }
     if (e < Kc) {
-        double* cs = colsq + (I.coff + e) * nsplit;
+        double* cs = g.colsq + (I.coff + e) * g.nsplit;
         if (vg && e >= r0) {  // Fourier column: sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2
             const double* U = Pd.trigU;  // U_m (k_trigu: TOA only)
             const int h = (int)(e - r0) / 2 + 1;
             cs[0] = 0.5 * (U[0] + (((e - r0) & 1) ? U[2 * h] : -U[2 * h]));
         } else {
             double v = cs[0];
-            for (int q = 1; q < nsplit; q++) v += cs[q];
+            for (int q = 1; q < g.nsplit; q++) v += cs[q];
             cs[0] = v;
         }
     }
+}
+
+// Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
+// triangle only, in a fixed order (deterministic), and the column sums of squares.
+// vg instances: the Fourier block F^T W F from the pulsar's weighted trig sums (trigW) by the
+// product-to-sum identities (a, b = harmonics 1..nred), and past block nbg the DMX bin
+// rows Sd, DD, DCS from k_gram_v's slot partials of the N-splits the bin's rows fall in:
+//   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
+//   sin a cos b = (S_a+b + S_a-b)/2     (S_-k = -S_k),
+__global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                 int nbg, GredArgs g) {
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    const bool vg = g.compact && Pd.dsplit && Pd.vg;
+    if ((int)blockIdx.x >= nbg) {  // DMX bins of a vg instance (one per wave)
+        const int a = (blockIdx.x - nbg) * 4 + (threadIdx.x >> 6);
+        if (!vg || a >= Pd.ndc) return;  // wave-uniform
+        gred_bin(I, Pd, g, a, threadIdx.x & 63);
+        return;
+    }
+    gred_elem(I, Pd, g, (long)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2379,6 +2406,25 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
     return true;
 }
 
+// U^T W U entry (i, j) of U = [F, 1] (F: sin, cos of harmonics 1..R/2 at 2h, 2h + 1; the ones
+// column at R) from the weighted trig sums C_m = sum w cos m theta, S_m (trigW):
+//   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
+//   sin a cos b = (S_a+b + S_a-b)/2,  1 sin b = S_b,  1 cos b = C_b,  1 1 = C_0
+__device__ __forceinline__ double trig_uwu(const double* C, int i, int j, int R) {
+    const double* Sn = C + VTRIG;
+    if (i > j) { const int t = i; i = j; j = t; }
+    if (i == R) return C[0];
+    const int ha = i / 2 + 1, sa = i & 1;
+    if (j == R) return sa ? C[ha] : Sn[ha];
+    const int hb = j / 2 + 1, sb = j & 1;
+    const int dm = ha > hb ? ha - hb : hb - ha, sm = ha + hb;
+    const double sd = ha >= hb ? Sn[ha - hb] : -Sn[hb - ha];
+    if (sa == 0 && sb == 0) return 0.5 * (C[dm] - C[sm]);
+    if (sa == 1 && sb == 1) return 0.5 * (C[dm] + C[sm]);
+    if (sa == 0) return 0.5 * (Sn[sm] + sd);
+    return 0.5 * (Sn[sm] - sd);
+}
+
 // Woodbury Sigma = diag(1/Phi) + U^T N^-1 U, U = [F, 1] (ones = F0 * Offset column), from
 // the (ECORR Schur-reduced) Gram; factored with blk_cholinv in the LDS region A and its
 // X = L^-1 stored packed lower (incl. diagonal) to Xout for k_wsolve (residuals.py:567-589).
@@ -2400,7 +2446,10 @@ __device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& 
             if (S.wb_noones && (gi == R || gj == R)) {
                 v = (gi == gj) ? 1.0 : 0.0;  // no ones column (PHOFF free): a decoupled unit row
             } else {
-                v = G(ci, cj) * si * sj;
+                // vg: U^T W U from the pulsar's weighted trig sums (U's ones column is the
+                // constant column itself, not F0 x the Offset column of M): F^T W F by the
+                // product-to-sum identities, 1^T W F_h = S_h / C_h, 1^T W 1 = C_0
+                v = Pd.vg ? trig_uwu(Pd.trigW, gi, gj, R) : G(ci, cj) * si * sj;
                 if (gi == gj) v += (gi < R) ? 1.0 / Pd.red_phi[gi] : 1e-40;
             }
         } else {
@@ -5101,26 +5150,6 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         record(ctx, 13);
     }
     HIPCHK(hipGetLastError());
-    if (nparts > 1 || vgp) {
-        int maxKp = 16;
-        for (auto& I : ctx->inst) {
-            const PsrDev& pd = ctx->psrs[I.psr].dev;
-            maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : I.Kp);
-        }
-        const int nbg = (maxKp * maxKp + 255) / 256;
-        record(ctx, 14);
-        hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? (ctx->max_ndc + 3) / 4 : 0), ctx->ninst), dim3(256), 0, ctx->stream,
-                           ctx->d_psrs, ctx->d_inst, ctx->nsplit, nparts, cmp, nbg, ctx->d_G, ctx->d_colsq, ctx->d_TS,
-                           ctx->d_Sdp, ctx->d_dmxv, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_BFp, ctx->vb_on);
-        HIPCHK(hipGetLastError());
-        record(ctx, 15);
-    }
-    if (ctx->wbfit && cmp) {  // WidebandTOAFitter: the DM rows join the normal equations
-        hipLaunchKernelGGL(k_wb_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_tables, ctx->nsplit, ctx->d_G, ctx->d_colsq, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
-        HIPCHK(hipGetLastError());
-    }
-    record(ctx, 7);
     // solve plan: the DMX-eliminated solve (k_solve_dmx) for compact-layout instances when
     // every such instance fits its LDS budget; the others (and everything in the full
     // layout) go to the blocked MFMA solve, or the column-by-column one beyond its budget.
@@ -5152,7 +5181,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     const int skip = ndmx_inst > 0 ? 1 : 0;
     // Woodbury Sigma factor: in k_solve_dmx's grid when every instance is solved there, else
     // on the side stream, concurrent with the per-instance solve
-    int do_sigma = 0, fuse_sigma = 0;
+    int do_sigma = 0, fuse_sigma = 0, side_sigma = 0, nbs_sig = 0;
     size_t lds_s = 0;
     if (mode == 1) {
         int kn = 0;
@@ -5161,27 +5190,48 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             const PsrHost& ph = ctx->psrs[I.psr];
             if (ph.spec.nred > 0 || ph.dev.nep > 0) { any = true; kn = std::max(kn, 2 * ph.spec.nred + 1); }
         }
-        const int nbs = (kn + 15) / 16;
-        lds_s = sizeof(double) * (size_t)nbs * (nbs + 1) / 2 * 256;
-        if (any && nbs <= BS_MAXNB && ctx->blocked_solve && skip && Ks == 0) {
-            fuse_sigma = 1;
-        } else if (any && nbs <= BS_MAXNB && ctx->blocked_solve) {
-            HIPCHK(hipEventRecord(ctx->ev_gram, ctx->stream));
-            HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
-            if (nbs <= 5)
-                hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
-                                   ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
-            else
-                hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
-                                   ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
-                                   ctx->d_status);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
-            ctx->sigma_pending = true;
-        } else if (any) {
-            do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
-        }
+        nbs_sig = (kn + 15) / 16;
+        lds_s = sizeof(double) * (size_t)nbs_sig * (nbs_sig + 1) / 2 * 256;
+        if (any && nbs_sig <= BS_MAXNB && ctx->blocked_solve && skip && Ks == 0) fuse_sigma = 1;
+        else if (any && nbs_sig <= BS_MAXNB && ctx->blocked_solve) side_sigma = 1;
+        else if (any) do_sigma = 1;  // the column-by-column solve factors it (beyond the blocked LDS budget)
     }
+    GredArgs gra{ctx->nsplit, nparts, cmp, ctx->vb_on, ctx->d_G, ctx->d_colsq, ctx->d_Sdp, ctx->d_dmxv,
+                 ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_BFp};
+    if (nparts > 1 || vgp) {
+        int maxKp = 16;
+        for (auto& I : ctx->inst) {
+            const PsrDev& pd = ctx->psrs[I.psr].dev;
+            maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : I.Kp);
+        }
+        const int nbg = (maxKp * maxKp + 255) / 256;
+        record(ctx, 14);
+        hipLaunchKernelGGL(k_greduce, dim3(nbg + (vgp ? (ctx->max_ndc + 3) / 4 : 0), ctx->ninst), dim3(256), 0, ctx->stream,
+                           ctx->d_psrs, ctx->d_inst, nbg, gra);
+        HIPCHK(hipGetLastError());
+        record(ctx, 15);
+    }
+    if (ctx->wbfit && cmp) {  // WidebandTOAFitter: the DM rows join the normal equations
+        hipLaunchKernelGGL(k_wb_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->nsplit, ctx->d_G, ctx->d_colsq, ctx->d_Sd, ctx->d_DD, ctx->d_DCS);
+        HIPCHK(hipGetLastError());
+    }
+    record(ctx, 7);
+    if (side_sigma) {
+        HIPCHK(hipEventRecord(ctx->ev_gram, ctx->stream));
+        HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
+        if (nbs_sig <= 5)
+            hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
+        else
+            hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
+                               ctx->d_status);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
+        ctx->sigma_pending = true;
+    }
+    hipEvent_t solved_ev = nullptr;  // ev_solved on the solve's dispatch packet (else a marker)
     if (ctx->copy_pend[ctx->slot]) {  // this slot's outputs may still be in flight to the host
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));  // (the latest copies: covers them)
         ctx->copy_pend[0] = ctx->copy_pend[1] = false;
@@ -5190,11 +5240,16 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (skip) {
         // deferred covariance for batches (a single fit would pay a launch on its read instead)
         double* xw = (ctx->d_xw && (ctx->cov_defer == 2 || (ctx->cov_defer == 1 && ctx->ninst >= 16))) ? ctx->d_xw : nullptr;
-        hipLaunchKernelGGL(k_solve_dmx<16>, dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
-                           fuse_sigma ? std::max(lds_x, lds_s) : lds_x, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_Sd, ctx->d_DD, ctx->d_DCS,
-                           ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                           fuse_sigma, ctx->refine, xw);
+        // when it is the last solve kernel, ev_solved rides on its dispatch packet (a separate
+        // event record is a marker packet between kernels: ~6-10 us of idle stream, measured)
+        solved_ev = Ks == 0 ? ctx->ev_solved : nullptr;
+        hipExtLaunchKernelGGL((k_solve_dmx<16>), dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
+                              (uint32_t)(fuse_sigma ? std::max(lds_x, lds_s) : lds_x), ctx->stream, nullptr, solved_ev, 0u,
+                              (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_tables,
+                              (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
+                              (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
+                              ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
+                              fuse_sigma, ctx->refine, xw);
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -5231,7 +5286,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     HIPCHK(hipGetLastError());
     record(ctx, 8);
-    HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
+    if (!solved_ev) HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
     if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
     update_timings(ctx);
