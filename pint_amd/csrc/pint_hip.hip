@@ -3762,6 +3762,7 @@ struct pint_ctx {
     int vgram = 1;       // PINT_OPT_VGRAM
     int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
     int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
+    int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
     int n_vg = 0;        // instances on the k_gram_v path
@@ -4041,6 +4042,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
     ctx->cov_defer = getenv("PINT_COV_DEFER") ? atoi(getenv("PINT_COV_DEFER")) : 1;  // 0 off, 1 batches, 2 always
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
+    ctx->gv_pair = getenv("PINT_GV_PAIR") ? atoi(getenv("PINT_GV_PAIR")) : 1;
     hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
     hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
     for (int sl = 0; sl < 2; sl++) {
@@ -4619,16 +4621,29 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 const PsrDev& pd = ctx->psrs[ctx->inst[k].psr].dev;
                 const int ntr = (pd.red0c + 1 + pd.vns) / 16, ntc = pd.vkp / 16;
                 const int nsk = ntr - (pd.red0c + 1 + 15) / 16;
-                int t = 1 + (pd.vb ? 1 : 0);
+                int t = pd.vb ? 1 : 0;
                 for (int ti = 0; ti < ntr; ti++)
                     for (int tj = ti; tj < ntc; tj++)
                         if (!(ti >= ntr - nsk && (tj < ntr || pd.vb))) t++;
-                return (long)t * ctx->inst[k].n;
+                // MFMA tiles per k-step, and the timing columns loaded and staged (measured on
+                // the bench PTA: ~4 columns cost one tile)
+                return (long)(4 * t + pd.red0c + 1) * ctx->inst[k].n;
             };
             std::vector<long> ck(ninst, 0);
             for (auto& b : bucket) {
                 for (int k : b) ck[k] = cost(k);
                 std::stable_sort(b.begin(), b.end(), [&](int x, int y) { return ck[x] > ck[y]; });
+                // two k_gram_v workgroups share a CU, and the dispatcher gives workgroup w and
+                // w + ncu (roughly) the same CU in the first resident round: pair the heaviest
+                // instances (first ncu workgroups) with the lightest (next ncu), then the rest
+                // heaviest first (PINT_GV_PAIR=0: plain heaviest-first order)
+                const int k1 = ncu / std::max(1, nsplit);
+                if (ctx->gv_pair && k1 > 0 && (int)b.size() > 2 * k1) {
+                    std::vector<int> o(b.begin(), b.begin() + k1);
+                    o.insert(o.end(), b.rbegin(), b.rbegin() + k1);
+                    o.insert(o.end(), b.begin() + k1, b.end() - k1);
+                    b.swap(o);
+                }
             }
         }
         for (int T = 1; T <= maxT; T++) {
