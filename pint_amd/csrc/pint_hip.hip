@@ -4481,6 +4481,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
         if (d.vg && ctx->vbin && d.vkp <= 96 && d.vns >= 16) {
             // VB (binned DMX x F): the 16 rows a wave takes from one chunk (split sp, quarter w,
             // rows i0 + w QV + 16 c ..) hold at most two bins, of distinct parity (drow)
+            // (a pulsar that fails it leaves the vg path: with an all-slot row tile k_gram_v
+            // takes the binned body, so vg without VB is not a layout the kernel knows)
             const std::vector<int>& dr = ph.drow_host;
             for (int sp = 0; d.vg && sp < nsplit; sp++) {
                 const long i0 = std::min<long>((long)sp * per, ph.n), i1 = std::min<long>(i0 + per, ph.n);
