@@ -1094,6 +1094,17 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         for (int k = t.dmx_x0; k < t.dmx_x1; k++) dmx += pval(P, S.o_DMX + 2 * t.dmx_x[k]);
         delay += dmx * DMCONST * inv_f2;
     }
+    // ---- FD (frequency_dependent.py:70-101): formed here, added after the binary delay (the
+    //      sum keeps the reference's order) so that the binary columns can be written as soon
+    //      as the binary state exists ----
+    double logf = 0.0;  // used by FD and its columns only
+    double fd = 0.0;
+    if (S.nfd > 0) {
+        logf = log(bfreq * 1e-3);
+        if (!isfinite(logf)) logf = 0.0;
+        for (int k = S.nfd; k >= 1; k--) fd = fd * logf + pval(P, S.o_FD + 2 * (k - 1));
+        fd *= logf;
+    }
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
     BinState B;
     B.status = 0;
@@ -1119,20 +1130,35 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         delay += B.delay;
         if (B.status) o.status = B.status;
     }
-    // ---- FD (frequency_dependent.py:70-101) ----
-    double logf = 0.0;  // used by FD and its columns only
-    if (S.nfd > 0) {
-        logf = log(bfreq * 1e-3);
-        if (!isfinite(logf)) logf = 0.0;
-        double fd = 0.0;
-        for (int k = S.nfd; k >= 1; k--) fd = fd * logf + pval(P, S.o_FD + 2 * (k - 1));
-        fd *= logf;
-        delay += fd;
-    }
+    if (S.nfd > 0) delay += fd;
     o.delay = delay;
-    // ---- spindown phase (spindown.py:124-155) + jumps (jump.py:119-136) ----
     dd dt0 = dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_PEPOCH)), DAYSEC);
     dd dt = dd_add_d(dt0, -delay);
+    double dtd = dd_to_d(dt);
+    o.fdt = spin_freq(S, P, dtd);
+    o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
+    const double chain = o.fdt * C.iF0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+    // ---- the binary columns of the design-matrix row, while the binary state is live (it
+    //      then dies: ~80 doubles fewer in registers through the phase and the other columns) ----
+    if (Mb && BIN != 0) {
+        Ell1Grad eg;
+        if (BIN == 1 || BIN == 3) ell1_grad<BIN == 3>(B, eg);
+        for (int u = 0; u < nrun; u++) {
+            const ColRun R = runs[u];
+            if (R.kind != PINT_COL_BIN) continue;
+            double* colp = Mb + (long)(compact ? R.dcol0 : R.col0) * ld;
+            for (int j = 0; j < R.cnt; j++, colp += ld) {
+                const int pid = S.col_index[R.col0 + j];
+                double d = 0.0;
+                if (BIN == 1 || BIN == 3) d = ell1_deriv(B, eg, pid);
+                if (BIN == 2) d = ddm_deriv(B, pid);
+                if (BIN == 4) d = bt_deriv(B, pid);
+                if (BIN == 5) d = ddm_deriv<true>(B, pid);
+                colp[r] = chain * d * bin_unit_factor(pid);
+            }
+        }
+    }
+    // ---- spindown phase (spindown.py:124-155) + jumps (jump.py:119-136) ----
     dd ph = spin_phase(S, P, dt);
     if (S.njump > 0 && t.jmask) {
         dd F0 = pdd(P, S.o_F);
@@ -1143,13 +1169,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     // (row ld = n)
     if (S.o_PHOFF >= 0 && r < (unsigned)ld) ph = dd_sub(ph, pdd(P, S.o_PHOFF));
     o.phase = ph;
-    double dtd = dd_to_d(dt);
-    o.fdt = spin_freq(S, P, dtd);
-    o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
     if (!Mb) return;
     // ---- design matrix row (timing_model.py:2073-2175) ----
-    const double F0 = C.F0, iF0 = C.iF0;
-    const double chain = o.fdt * iF0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+    const double iF0 = C.iF0;
     // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities), once per TOA
     double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
     if (S.astrometry) {
@@ -1177,8 +1199,6 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         // d_delay_astrometry_d_PX (astrometry.py:219-249)
         gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
     }
-    Ell1Grad eg;
-    if (BIN == 1 || BIN == 3) ell1_grad<BIN == 3>(B, eg);
     const double dmc = chain * DMCONST * inv_f2;
     o.dmc = dmc;
     for (int u = 0; u < nrun; u++) {
@@ -1227,16 +1247,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
                     colp[r] = chain * v;
                 }
             } break;
-            case PINT_COL_BIN:
-                for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    const int pid = S.col_index[R.col0 + j];
-                    double d = 0.0;
-                    if (BIN == 1 || BIN == 3) d = ell1_deriv(B, eg, pid);
-                    if (BIN == 2) d = ddm_deriv(B, pid);
-                    if (BIN == 4) d = bt_deriv(B, pid);
-                    if (BIN == 5) d = ddm_deriv<true>(B, pid);
-                    colp[r] = chain * d * bin_unit_factor(pid);
-                }
+            case PINT_COL_BIN:  // written with the binary state above
+                if (BIN == 0)
+                    for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
                 break;
             default:
                 for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
