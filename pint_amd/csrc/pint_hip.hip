@@ -3354,6 +3354,16 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     const double* ri = rtime + (I.roff - inst);
     double* d = lds;  // Kn
     const double* wp = wpart + (long)inst * nsplit * stride;
+    // the packed inverse factor of Sigma (from the solve) staged in LDS first, with coalesced
+    // loads that are in flight while the dot products below are summed; with no noise basis
+    // Sigma is the 1x1 [1e-40 + 1^T N^-1 1], which the solves do not factor
+    const bool nobasis = (R == 0 && Pd.nep == 0);
+    double* Xs = d + Kn;  // Kn (Kn + 1) / 2
+    {
+        const double* X = sigL + I.soff;
+        const int nX = nobasis ? 0 : Kn * (Kn + 1) / 2;
+        for (int e = threadIdx.x; e < nX; e += blockDim.x) Xs[e] = X[e];
+    }
     if (wtile) {
         // r^T W r: the residual pass's chi2 partials of the instance summed exactly as k_rsum
         // does (wave 0, same order: the same bits), stored as the residuals' chi2 (k_rsum is
@@ -3428,16 +3438,8 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     }
     if (threadIdx.x == 0) d[R] = S.wb_noones ? 0.0 : rw1 - erw1;  // the ones column's entry
     __syncthreads();
-    // y = L^-1 d with the explicit inverse factor from k_solve (row dot products); with no
-    // noise basis Sigma is the 1x1 [1e-40 + 1^T N^-1 1], which the solves do not factor
-    const bool nobasis = (R == 0 && nep == 0);
+    // y = L^-1 d with the explicit inverse factor (staged above), four lanes per row
     const double x00 = S.wb_noones ? 1.0 : 1.0 / sqrt(1e-40 + Pd.sumw);
-    const double* X = sigL + I.soff;
-    // the packed factor staged in LDS with coalesced loads, then four lanes per row
-    double* Xs = d + Kn;  // Kn (Kn + 1) / 2
-    const int nX = nobasis ? 0 : Kn * (Kn + 1) / 2;
-    for (int e = threadIdx.x; e < nX; e += blockDim.x) Xs[e] = X[e];
-    __syncthreads();
     double q = 0.0;
     for (int i0 = 0; i0 < Kn; i0 += blockDim.x / 4) {
         const int i = i0 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
