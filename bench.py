@@ -59,12 +59,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a box with fewer GPUs than ranks (not the measured
+    # configuration): PINT_BENCH_SHARE_GPU=1 maps rank r to GPU r mod (GPUs), and
+    # PINT_BENCH_BACKEND=gloo carries the collectives on the host (RCCL refuses two ranks on
+    # one GPU).  The driver's N-GPU runs use neither.
+    backend = os.environ.get("PINT_BENCH_BACKEND", "nccl")
+    if world > 1 and os.environ.get("PINT_BENCH_SHARE_GPU") == "1":
+        import torch
+        local = local % max(1, torch.cuda.device_count())
+        os.environ["LOCAL_RANK"] = str(local)
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
 
     def barrier():
         if dist is not None:
@@ -76,7 +85,7 @@ def main():
         if dist is None:
             return v
         import torch
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        t = torch.tensor([v], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
