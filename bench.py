@@ -5,7 +5,7 @@ One *step* = one GLSFitter.fit_toas(maxiter=1) (fitter.py:2104) of every pulsar 
 shard, batched in one launch sequence per GPU: design matrix + residuals (k_eval/k_resid),
 Gram on FP64 MFMA (k_gram_v), Cholesky/solve/covariance (k_solve_dmx; iterative refinement
 where the condition estimate asks for it), double-double parameter update (k_apply), post-fit residuals and Woodbury
-chi2 (k_wdot/k_wsolve), with the fit outputs (steps, errors, covariances, chi2) copied back
+chi2 (k_resid2's trig tiles + k_wsolve), with the fit outputs (steps, errors, covariances, chi2) copied back
 to the host on a copy stream, overlapped with the kernels.
 
 Sharding (pint_amd.pta): the pulsars are assigned to ranks by
