@@ -54,6 +54,11 @@ def main():
     ap.add_argument("--c2", type=int, default=256, help="B1855 (C2) fits per batched step (0 = skip the C2 leg)")
     ap.add_argument("--j0740", type=int, default=256,
                     help="(M2, SINI) grid side of the C3/C4 J0740 legs (0 = skip)")
+    ap.add_argument("--emulate-world", default="2,4,8",
+                    help="N=1 only: time every rank's LPT shard of the PTA for these world sizes on this "
+                         "GPU, one after the other (predicted_strong; '' = skip)")
+    ap.add_argument("--cold-start", type=int, default=1,
+                    help="N=1 only: upload + first fit of the PTA in a fresh session (cold_start)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +118,11 @@ def main():
                 "pulsars_per_rank": [len(s) for s in sh2]}
 
     roof = leg["roofline"]
+    cold = cold_start(leg["items"], rank) if (world == 1 and args.cold_start) else None
+    emu = None
+    if world == 1 and args.emulate_world:
+        emu = emulate_world(leg["items"], costs, [int(x) for x in args.emulate_world.split(",") if x],
+                            args, fits_per_s, leg["dt"] / args.steps)
     grid = grid_leg(args.grid, dist, barrier, max_over_ranks) if args.grid > 0 else None
     j0740 = j0740_legs(args.j0740, dist, barrier, max_over_ranks) if args.j0740 > 0 else None
     c2 = c2_leg(args.c2, 20, 3, world, barrier, max_over_ranks) if args.c2 > 0 else None
@@ -131,7 +141,8 @@ def main():
                           "npsr": args.npsr, "ntoas": args.ntoas,
                           "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
                           "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
-               "roofline": roof, "pta_weak": weak, "grid": grid, "j0740": j0740, "c2": c2,
+               "roofline": roof, "pta_weak": weak, "predicted_strong": emu, "cold_start": cold,
+               "grid": grid, "j0740": j0740, "c2": c2,
                "cpu_baseline": cpu}
         print(json.dumps(out))
     if dist is not None:
@@ -156,6 +167,78 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
         out["roofline"] = roofline(s, lays, kt_gram / max(1, n_gram), step, args)
         out["roofline"]["gram_event_launches"] = int(n_gram)
     s.close()
+    return out
+
+
+def emulate_world(items, costs, worlds, args, value1, step1):
+    """Predicted strong scaling of the headline metric on this one GPU: for each world size N,
+    every rank's LPT shard (pint_amd.pta.lpt_shard, the assignment bench.py uses at N ranks)
+    is uploaded into its own session and timed for the same K steps, one shard after the
+    other; the predicted N-GPU step is the slowest shard's (the max-over-ranks the N-rank run
+    takes).  Host-side enqueue runs on this one process as it would on each rank."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    from pint_amd.pta import lpt_shard
+
+    def nobarrier():
+        pass
+
+    steps, warm = max(20, args.steps // 2), max(3, args.warmup // 2)
+    out = {"method": ("each rank's LPT shard timed alone on this GPU (same step as the headline), "
+                      f"{steps} steps after {warm} warm-up; predicted value = npsr / max over shards"),
+           "n1": {"value": round(value1, 3), "ms_per_step": round(step1 * 1e3, 4)}}
+    for nw in worlds:
+        if nw <= 1:
+            continue
+        per = []
+        for sh in lpt_shard(costs, nw):
+            if not sh:
+                per.append(0.0)
+                continue
+            s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
+            sub = [items[i] for i in sh]
+            lays = [s.add(build_layout(m, t)) for m, t in sub]
+            s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, sub)])
+            dt, _, _, _ = timed_steps(s, steps, warm, nobarrier, lambda v: v)
+            s.close()
+            per.append(dt / steps)
+        mx = max(per)
+        out[f"n{nw}"] = {"value": round(len(items) / mx, 3), "ms_per_step": round(mx * 1e3, 4),
+                         "ms_per_shard": [round(p * 1e3, 4) for p in per],
+                         "pulsars_per_rank": [len(sh) for sh in lpt_shard(costs, nw)],
+                         "speedup_vs_n1": round(step1 / mx, 3)}
+        log(f"[emulate {nw}] shards {[round(p * 1e3, 3) for p in per]} ms -> {len(items) / mx:.0f} fits/s")
+    return out
+
+
+def cold_start(items, rank):
+    """Cold start of the PTA (the library already loaded): a fresh session, every pulsar's
+    host packing and upload (incl. the per-pulsar set-up kernels), then the first
+    GLSFitter.fit_toas(maxiter=1) step of all pulsars, synchronously.  Wall times."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    t0 = time.perf_counter()
+    s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
+    lays = [build_layout(m, t) for m, t in items]
+    t1 = time.perf_counter()
+    for l in lays:
+        s.add(l)
+    s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+    s.check()
+    t2 = time.perf_counter()
+    s.eval(want_M=Session.FIT)
+    s.fit_step(1)
+    s.read_step()
+    s.noise_resids()
+    s.apply_step_uniform(1.0)
+    s.eval(want_M=False)
+    s.chi2_gls()
+    s.check()
+    t3 = time.perf_counter()
+    s.close()
+    out = {"pulsars": len(items), "layout_ms": round((t1 - t0) * 1e3, 2), "upload_ms": round((t2 - t1) * 1e3, 2),
+           "first_fit_ms": round((t3 - t2) * 1e3, 3), "cold_start_ms": round((t3 - t0) * 1e3, 2),
+           "note": "wall, host included: host layouts, upload (TOA columns + per-pulsar set-up kernels), "
+                   "first synchronous fit step"}
+    log(f"[rank {rank}] cold start {out}")
     return out
 
 

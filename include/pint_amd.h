@@ -352,6 +352,13 @@ int pint_debug_read(pint_ctx *ctx, int which, double *out);
 int pint_debug_gram(pint_ctx *ctx, int pre_ecorr, double *out);
 int pint_debug_set_resids(pint_ctx *ctx, const double *time_resid);
 
+/* The normalisation of the last pint_fit_step's design matrix, the reference fitters' `fac`
+ * / `norm` squared (utils.py:2879 normalize_designmatrix; fitter.py:1320-1343 WLS,
+ * fitter.py:2164-2176 GLS): per instance K_i values at the same K_i+1 stride as
+ * pint_read_step's dpars.  mode 1: the unweighted column sums of squares of [M | F];
+ * mode 0: the diagonal of the whitened normal matrix M^T N^-1 M.  Synchronous. */
+int pint_read_norms(pint_ctx *ctx, int mode, double *out);
+
 /* Per-instance status bits (1 << PINT_E_*) raised by evaluations since the last call, one
  * int32 per instance; reading clears them.  The batch status returned by pint_eval/
  * pint_check names the first error of any instance; this names the instances, so one

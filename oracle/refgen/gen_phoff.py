@@ -7,6 +7,10 @@
 * ecorr_phoff : the same with ECORR and no time-correlated noise, four frequencies per epoch:
                 the ECORR-only Sherman-Morrison chi2 (residuals.py:591-636, dispatch
                 :705-709) and its log-normalisation, GLSFitter.
+* phoff_red   : PhaseOffset with PHOFF frozen and PLRedNoise (+ the template's DMX): no
+                Offset column in the fit, and the Woodbury chi2 appends the ones column with
+                Phi = 1e40 (residuals.py:583-585) -- GLSFitter, DownhillGLSFitter.
+* phoff_ecorr : the same with ECORR as well (four frequencies per epoch).
 N = 600 TOAs each.  Usage: run_ref.sh gen_phoff.py [name ...]
 """
 import io
@@ -30,14 +34,22 @@ def par_phoff(seed, ecorr):
     return "\n".join(lines) + "\n"
 
 
-def gen(name, seed, ecorr, fit):
+def par_frozen(seed, ecorr):
+    lines = pta_par(seed, "").splitlines()  # keeps the template's PLRedNoise
+    lines.append("PHOFF 0.05")              # frozen
+    if ecorr:
+        lines.append("ECORR -f fake 0.8")
+    return "\n".join(lines) + "\n"
+
+
+def gen(name, seed, ecorr, fit, frozen=False):
     np.random.seed(seed)
-    par = par_phoff(seed, ecorr)
+    par = par_frozen(seed, ecorr) if frozen else par_phoff(seed, ecorr)
     model = get_model(io.StringIO(par))
     ts = sim.make_fake_toas_uniform(53000, 56652, 600, model,
                                     freq=np.array([800, 1200, 1600, 2000]) * u.MHz,
                                     obs="geocenter", error=0.5 * u.us, add_noise=True,
-                                    add_correlated_noise=ecorr, include_bipm=False,
+                                    add_correlated_noise=ecorr or frozen, include_bipm=False,
                                     multi_freqs_in_epoch=ecorr, flags={"f": "fake"})
     model.find_empty_masks(ts, freeze=True)
     if ecorr:
@@ -56,3 +68,7 @@ if __name__ == "__main__":
         gen("wls_phoff", 5, False, "wls")
     if "ecorr_phoff" in which:
         gen("ecorr_phoff", 6, True, "gls")
+    if "phoff_red" in which:
+        gen("phoff_red", 7, False, "gls", frozen=True)
+    if "phoff_ecorr" in which:
+        gen("phoff_ecorr", 8, True, "gls", frozen=True)

@@ -60,9 +60,9 @@ struct PsrDev {
     const pint_spec_t* spec;
     const double* red_freq;  // 2 nred: the frequencies as double-double, hi[nred] then lo[nred]
     const double* red_phi;   // 2*nred
-    const double* red_cs;    // n x 4: (cos, sin) of theta and of 8 theta, theta = 2 pi t f_1 (k_redbase)
-    const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trigu)
-    const double* trigW;     // 2 x 64: C_m, S_m = sum_i w_i (cos, sin) m theta_i, w = 1/sigma^2 (k_trigw):
+    const double* red_cs;    // n x 4: (cos, sin) of theta and of 8 theta, theta = 2 pi t f_1 (k_trig_setup)
+    const double* trigU;     // 2 x 64: U_m = sum_i cos m theta_i, V_m = sum_i sin m theta_i (k_trig_setup)
+    const double* trigW;     // 2 x 64: C_m, S_m = sum_i w_i (cos, sin) m theta_i, w = 1/sigma^2 (k_trig_setup):
                              // TOA-only at fixed sigma, formed at upload and by pint_set_sigma
     const int32_t* ep_ptr;   // ECORR epochs, CSR (nep+1)
     const int32_t* ep_idx;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
 
 // k_resid2 with wtile: the Woodbury dot products of the post-fit chi2 (k_wdot's F^T W r and
 // 1^T W r, residuals.py:567-589 via utils.py:3074) come out of the same pass.  The PLRedNoise
-// basis is the harmonic series e^{i k theta} (k_redbase), and e^{i (a + 8b) theta} =
+// basis is the harmonic series e^{i k theta} (k_trig_setup), and e^{i (a + 8b) theta} =
 // e^{i a theta} e^{i 8b theta}: one 16x16 v_mfma_f64_16x16x4f64 tile D = A^T B per block with
 // A = w r [cos a theta | sin a theta] and B = [cos 8b theta | sin 8b theta] (a, b < 8) holds
 // every sum_i w_i r_i e^{i k theta_i}, k < 64 (k_rsum combines: cos k = D[a][b] - D[8+a][8+b],
@@ -1069,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_dmx_rows(const PsrDev* __restrict__ psr
 // The PLRedNoise basis (noise_model.py:861-880, frequencies :847-858) is a harmonic
 // series: F[:,2h] = sin((h+1) theta_i), F[:,2h+1] = cos((h+1) theta_i), theta_i =
 // 2 pi t_i f_1, t = tdbld * 86400 s, f_k = k f_1.  Hence
-//  - F is generated in the kernel by rotations of the per-TOA fundamental (k_redbase),
+//  - F is generated in the kernel by rotations of the per-TOA fundamental (k_trig_setup),
 //    never stored in M;
 //  - its Gram block F^T W F follows from the weighted trig sums C_m = sum_i w_i cos(m
 //    theta_i), S_m = sum_i w_i sin(m theta_i), m <= 2 nred, by the product-to-sum
@@ -1166,7 +1166,7 @@ __device__ __forceinline__ void cpow_u8(double c1, double s1, int k, double& c, 
 // (column-major, stride VCH+2), one row per lane: wave w stages the timing columns w, w + GW,
 // ..., the trig-block harmonics a = w, w + GW (A: e^{i a theta}, B: e^{i 8a theta}) and from
 // each A harmonic the Fourier harmonics a + 1 + 8u, by short powers and rotations of the row's
-// e^{i theta}, e^{i 8 theta} (k_redbase) that carry the weight along; the residual and the
+// e^{i theta}, e^{i 8 theta} (k_trig_setup) that carry the weight along; the residual and the
 // row's DMX slot entry (the slot block is zero except one entry per row, so only the previous
 // and the new entry of the row are rewritten) come with wave 0's share.  Each wave then takes
 // 16 rows of the chunk (four 4-row k-steps) and accumulates ALL the tiles (row tiles < ntr x
@@ -1250,7 +1250,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     const int SW = Kd + 3;  // Sdp row: compact columns 0..Kd, DD (+1 spare)
     // past Kpv (VB): the trig block A = [cos a theta | sin a theta]/sigma (a < 8) and the
     // binned block B'' (tX).  F^T W F comes from the weighted trig sums C_m, S_m, which depend
-    // on the TOAs and sigma only (PsrDev::trigW, k_trigw); the unweighted sums for the Fourier
+    // on the TOAs and sigma only (PsrDev::trigW, k_trig_setup); the unweighted sums for the Fourier
     // column norms likewise (PsrDev::trigU).  DUM: the write-only dummy column.
     const int tA = Kpv, DUM = Kpv + 16, tX = Kpv + 17, Kpt = Kpv + (VB ? 33 : 17);
     double* const Tb0 = lds;
@@ -1412,7 +1412,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
                 }
             }
             // binned DMX x F tile (the weighted trig sums of F^T W F are formed once per pulsar,
-            // k_trigw: TOA and sigma only)
+            // k_trig_setup: TOA and sigma only)
             if (VB) accB = __builtin_amdgcn_mfma_f64_16x16x4f64(Tr[tA * CS], Tr[tX * CS], accB, 0, 0, 0);
         }
     };
@@ -1800,67 +1800,124 @@ __global__ __launch_bounds__(256) void k_wb_gram(const PsrDev* __restrict__ psrs
     }
 }
 
-// k_redbase: the fundamental of the PLRedNoise basis per TOA, (cos, sin)(2 pi t_i f_1)
-// with the phase t_i f_1 reduced in double-double; computed once at pint_add_pulsar
-// (TOA-only data, like tdb).  Harmonic m is reached by rotations of it.
-__global__ void k_redbase(const double* __restrict__ tdb_hi, const double* __restrict__ tdb_lo, int n, double f1,
-                          double f1_lo, double* __restrict__ cs) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const dd x = dd_mul(dd_mul_d(dd_make(tdb_hi[i], tdb_lo[i]), DAYSEC), dd_make(f1, f1_lo));
-    double s, c, s8, c8;
-    dd_sincos_cyc(x, &s, &c);
-    dd_sincos_cyc(dd_make(8.0 * x.hi, 8.0 * x.lo), &s8, &c8);  // 8 theta: exact scaling of the dd phase
-    cs[4 * i] = c;
-    cs[4 * i + 1] = s;
-    cs[4 * i + 2] = c8;
-    cs[4 * i + 3] = s8;
+// k_trig_setup + k_trig_sum: the per-pulsar red-noise set-up of every pulsar of an upload in
+// two launches (instead of k_redbase, k_trigu, k_trigu_sum, k_trigw, k_trigu_sum per pulsar).
+// A job is one pulsar (or, from pint_set_sigma, one pulsar's weighted sums only); a block
+// takes TRIG_RB rows of one job, one row per thread per pass:
+//   * with `base`, the row's e^{i theta}, e^{i 8 theta} (theta = 2 pi t f_1, dd phase;
+//     k_redbase's arithmetic) written to red_cs, else read from it;
+//   * A = [cos a theta | sin a theta], B = [cos 8b theta | sin 8b theta] (a, b < 8, by
+//     rotations) staged per wave in LDS, and two 16x16 MFMA tiles accumulated: A^T B
+//     (unweighted) and A^T (w B) (w = 1/sigma^2);
+// the block's two tiles (the waves' tiles summed in a fixed order) go to its partial slot.
+// k_trig_sum adds a job's block partials in block order (deterministic) and forms, with
+// e^{i(a + 8b) theta} = e^{i a theta} e^{i 8b theta},
+//   U_m = T[a][b] - T[8+a][8+b],  V_m = T[8+a][b] + T[a][8+b]   (m = a + 8b)
+// of the unweighted tile into trigU (cos, sin sums, TOA only) and of the weighted one into
+// trigW (C_m, S_m).
+constexpr int TRIG_RB = 1024;  // rows per block (4 per thread)
+struct TrigJob {
+    const double* tdb_hi;
+    const double* tdb_lo;
+    const double* isig;
+    double* cs;      // red_cs (4 per row)
+    double* trigU;   // nullptr: weighted sums only
+    double* trigW;
+    double f1, f1_lo;
+    int n, b0, nb, base;
+};
+
+__global__ __launch_bounds__(256) void k_trig_setup(const TrigJob* __restrict__ jobs, int njob,
+                                                    double* __restrict__ part) {
+    extern __shared__ double xs[];  // per wave 48 * WT_CS: A (0-15), B (16-31), w B (32-47)
+    int lo = 0, hi = njob - 1;      // the block's job (jobs sorted by b0)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].b0 <= (int)blockIdx.x) lo = mid;
+        else hi = mid - 1;
+    }
+    const TrigJob J = jobs[lo];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r0 = ((int)blockIdx.x - J.b0) * TRIG_RB;
+    typedef double __attribute__((address_space(3))) ldsd;
+    ldsd* X = (ldsd*)(xs + wave * 48 * WT_CS);
+    double4_t au[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, aw[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll 1
+    for (int j = 0; j < TRIG_RB / 256; j++) {
+        const int i = r0 + (int)threadIdx.x + j * 256;
+        double c1 = 1.0, s1 = 0.0, c8 = 1.0, s8 = 0.0, w = 0.0, a0 = 0.0;
+        if (i < J.n) {
+            if (J.base) {
+                const dd x = dd_mul(dd_mul_d(dd_make(J.tdb_hi[i], J.tdb_lo[i]), DAYSEC), dd_make(J.f1, J.f1_lo));
+                dd_sincos_cyc(x, &s1, &c1);
+                dd_sincos_cyc(dd_make(8.0 * x.hi, 8.0 * x.lo), &s8, &c8);  // 8 theta: exact scaling of the dd phase
+                J.cs[4 * i] = c1;
+                J.cs[4 * i + 1] = s1;
+                J.cs[4 * i + 2] = c8;
+                J.cs[4 * i + 3] = s8;
+            } else {
+                const double4_t zz = ((gptr<double4_t>)J.cs)[i];
+                c1 = zz[0];
+                s1 = zz[1];
+                c8 = zz[2];
+                s8 = zz[3];
+            }
+            w = J.isig[i] * J.isig[i];
+            a0 = 1.0;
+        }
+        double ca = a0, sa = 0.0, cb = 1.0, sb = 0.0;
+#pragma unroll
+        for (int a = 0; a < 8; a++) {
+            X[a * WT_CS + lane] = ca;
+            X[(8 + a) * WT_CS + lane] = sa;
+            X[(16 + a) * WT_CS + lane] = cb;
+            X[(24 + a) * WT_CS + lane] = sb;
+            X[(32 + a) * WT_CS + lane] = w * cb;
+            X[(40 + a) * WT_CS + lane] = w * sb;
+            rot(ca, sa, c1, s1);
+            rot(cb, sb, c8, s8);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's stores before its reads
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int ks = 0; ks < 16; ks++) {
+            const int row = 4 * ks + (lane >> 4);
+            const double av = X[(lane & 15) * WT_CS + row];
+            const double bv = X[(16 + (lane & 15)) * WT_CS + row], bw = X[(32 + (lane & 15)) * WT_CS + row];
+            au[ks & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, au[ks & 1], 0, 0, 0);
+            aw[ks & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bw, aw[ks & 1], 0, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    double* red = xs;  // the waves' tiles summed in a fixed order (acc[q]: D[4q + lane/16][lane%16])
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = (4 * q + (lane >> 4)) * 16 + (lane & 15);
+        red[wave * 512 + e] = au[0][q] + au[1][q];
+        red[wave * 512 + 256 + e] = aw[0][q] + aw[1][q];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 512; e += 256)
+        part[(long)blockIdx.x * 512 + e] = (red[e] + red[512 + e]) + (red[1024 + e] + red[1536 + e]);
 }
 
-// k_trigu: the unweighted trig sums U_m, V_m (m < 64) over the pulsar's TOAs, from which
-// k_greduce forms the Fourier column norms (sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2).
-// They depend on the TOAs only, so they are formed once at upload: grid = row blocks of
-// TRIGU_R rows (short, so the grid fills the chip), thread m (cos) / 64 + m (sin) per block;
-// k_trigu_sum then adds the block partials of each sum, one workgroup per sum, in a fixed
-// tree order (deterministic).
-constexpr int TRIGU_R = 16;
-__global__ __launch_bounds__(128) void k_trigu(const double* __restrict__ cs, int n, double* __restrict__ part) {
-    const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
-    const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);
-    double acc = 0.0;
-    for (int i = i0; i < i1; i++) {
-        double c, sn;
-        cpow(cs[4 * i], cs[4 * i + 1], m, c, sn);
-        acc += kind ? sn : c;
+__global__ __launch_bounds__(256) void k_trig_sum(const TrigJob* __restrict__ jobs, const double* __restrict__ part) {
+    __shared__ double T[512];
+    const TrigJob J = jobs[blockIdx.x];
+    for (int e = threadIdx.x; e < 512; e += 256) {
+        double v = 0.0;
+        for (int b = 0; b < J.nb; b++) v += part[(long)(J.b0 + b) * 512 + e];
+        T[e] = v;
     }
-    part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
-}
-// k_trigw: the weighted sums C_m = sum_i w_i cos m theta_i, S_m = sum_i w_i sin m theta_i (m <
-// 64, w = 1/sigma^2) that give the Gram's F^T W F block (k_greduce's product-to-sum
-// identities); e^{i m theta} = e^{i a theta} e^{i 8b theta} (m = a + 8b) from the row's
-// e^{i theta} and e^{i 8 theta} (k_redbase), as k_gram_v formed them before they moved here.
-// They depend on the TOAs and sigma only, so they are formed at upload and when the
-// uncertainties change (pint_set_sigma), not in every fit step; summed by k_trigu_sum.
-__global__ __launch_bounds__(128) void k_trigw(const double* __restrict__ cs, const double* __restrict__ isig, int n,
-                                               double* __restrict__ part) {
-    const int m = threadIdx.x & 63, kind = threadIdx.x >> 6;
-    const int i0 = blockIdx.x * TRIGU_R, i1 = min(n, i0 + TRIGU_R);
-    double acc = 0.0;
-    for (int i = i0; i < i1; i++) {
-        double ca, sa, cb, sb;
-        cpow(cs[4 * i], cs[4 * i + 1], m & 7, ca, sa);
-        cpow(cs[4 * i + 2], cs[4 * i + 3], m >> 3, cb, sb);
-        const double w = isig[i] * isig[i];
-        acc += kind ? w * (sa * cb + ca * sb) : w * (ca * cb - sa * sb);
+    __syncthreads();
+    const int m = threadIdx.x & 63, a = m & 7, b = m >> 3, kind = threadIdx.x >> 6;  // kind 0 U, 1 W
+    if (kind < 2 && (kind == 1 || J.trigU)) {
+        const double* D = T + kind * 256;
+        double* o = kind ? J.trigW : J.trigU;
+        o[m] = D[a * 16 + b] - D[(8 + a) * 16 + 8 + b];
+        o[VTRIG + m] = D[(8 + a) * 16 + b] + D[a * 16 + 8 + b];
     }
-    part[(long)blockIdx.x * 128 + threadIdx.x] = acc;
-}
-__global__ __launch_bounds__(256) void k_trigu_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
-    __shared__ double sh[4];
-    double acc = 0.0;
-    for (int b = threadIdx.x; b < nb; b += 256) acc += part[(long)b * 128 + blockIdx.x];
-    acc = block_sum<4>(acc, sh);
-    if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
 // Sum the Gram partials of every N-split (+ the ECORR Schur slot) into slot 0, upper
@@ -1951,7 +2008,7 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
             if (vg && (j > Kc)) {
                 G[e] = 0.0;  // padding
             } else if (vg && i >= r0 && j < Kc) {
-                const double* C = Pd.trigW;  // C_m, S_m (k_trigw: TOA and sigma only)
+                const double* C = Pd.trigW;  // C_m, S_m (k_trig_setup: TOA and sigma only)
                 const double* Sn = C + VTRIG;
                 const int ha = (i - r0) / 2 + 1, sa = (i - r0) & 1;  // 0 sin, 1 cos
                 const int hb = (j - r0) / 2 + 1, sb = (j - r0) & 1;
@@ -1973,7 +2030,7 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
     if (e < Kc) {
         double* cs = g.colsq + (I.coff + e) * g.nsplit;
         if (vg && e >= r0) {  // Fourier column: sum sin^2 = (N - U_2h)/2, cos^2 = (N + U_2h)/2
-            const double* U = Pd.trigU;  // U_m (k_trigu: TOA only)
+            const double* U = Pd.trigU;  // U_m (k_trig_setup: TOA only)
             const int h = (int)(e - r0) / 2 + 1;
             cs[0] = 0.5 * (U[0] + (((e - r0) & 1) ? U[2 * h] : -U[2 * h]));
         } else {
@@ -2003,6 +2060,41 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
         return;
     }
     gred_elem(I, Pd, g, (long)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// PhaseOffset with a frozen PHOFF: the fit has no Offset column, yet the Woodbury chi2
+// appends the ones column with Phi = 1e40 (residuals.py:583-585).  Its row of Sigma cannot
+// come from the Gram (no column of M is the ones column), so k_onesrow forms it per instance
+// before the solve: 1^T W~ F_j and 1^T W~ 1 (W~: ECORR eliminated, as the Gram is), the
+// Fourier part from the pulsar's weighted trig sums (F_2h = sin (h+1) theta, F_2h+1 = cos;
+// PLRedNoise modes only: the host refuses PLDMNoise here) and the ECORR Schur term from
+// k_ecorr's epoch sums.  vg instances take the same row from trig_uwu (no ECORR there).
+__device__ __forceinline__ bool ones_virtual(const pint_spec_t& S) { return S.o_PHOFF >= 0 && !S.wb_noones; }
+
+__global__ __launch_bounds__(64) void k_onesrow(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                const double* __restrict__ esum, const double* __restrict__ eD,
+                                                const double* __restrict__ eW, const double* __restrict__ eC,
+                                                int compact, double* __restrict__ ones) {
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    if (!ones_virtual(S) || !(S.nred > 0 || Pd.nep > 0)) return;
+    const bool cmp = compact && Pd.dsplit;
+    const int R = 2 * S.nred;
+    for (int j = threadIdx.x; j <= R; j += 64) {
+        double v;
+        if (j < R) {
+            const int h = j / 2 + 1;
+            v = (j & 1) ? Pd.trigW[h] : Pd.trigW[VTRIG + h];
+        } else {
+            v = Pd.sumw;
+        }
+        for (int e = 0; e < Pd.nep; e++) {
+            const double w = eW[I.epoff + e];
+            v -= w * (j < R ? esum_col(Pd, I, esum, eC, cmp, e, S.ncol + j) : w) / eD[I.epoff + e];
+        }
+        ones[I.coff + j] = v;
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -2088,7 +2180,8 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
                                                    double* __restrict__ work, double* __restrict__ dpars,
                                                    double* __restrict__ errs, double* __restrict__ cov,
                                                    double* __restrict__ chi2lin, double* __restrict__ sigL,
-                                                   int* __restrict__ status, int skip_dsplit, int do_sigma) {
+                                                   int* __restrict__ status, int skip_dsplit, int do_sigma,
+                                                   const double* __restrict__ ones) {
     extern __shared__ double lds[];
     __shared__ double sh[SOLVE_T / 64];
     const int inst = blockIdx.x;
@@ -2199,6 +2292,8 @@ __global__ __launch_bounds__(SOLVE_T) void k_solve(const PsrDev* __restrict__ ps
             double v;
             if (S.wb_noones && (i == R || j == R)) {
                 v = (i == j) ? 1.0 : 0.0;  // no ones column: a decoupled unit row
+            } else if (ones && ones_virtual(S) && (i == R || j == R)) {
+                v = ones[I.coff + (i == R ? j : i)] + (i == j ? 1e-40 : 0.0);  // k_onesrow (no Offset column)
             } else {
                 v = G(ci, cj) * si * sj;
                 if (i == j) v += (i < R) ? 1.0 / Pd.red_phi[i] : 1e-40;
@@ -2328,13 +2423,18 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
 #pragma unroll
         for (int c = j + 1; c < 16; c++) a[c] -= a[j] * rdlane(a[j], c);
     }
-    double x[16];
+    // X = L^-1 by forward substitution, lane r its column r, in axpy order: once x[u] is
+    // known every later row subtracts its term, so the dependent chain is two operations
+    // per row instead of a t-term dot product per row (the same subtraction order, u
+    // ascending, hence the same rounding)
+    double x[16], s[16];
 #pragma unroll
-    for (int t = 0; t < 16; t++) {
-        double s = (r == t) ? 1.0 : 0.0;
+    for (int t = 0; t < 16; t++) s[t] = (r == t) ? 1.0 : 0.0;
 #pragma unroll
-        for (int u = 0; u < t; u++) s -= rdlane(a[u], t) * x[u];
-        x[t] = s * ril[t];
+    for (int u = 0; u < 16; u++) {
+        x[u] = s[u] * ril[u];
+#pragma unroll
+        for (int t = u + 1; t < 16; t++) s[t] -= rdlane(a[u], t) * x[u];
     }
     if (lane < 16) {
 #pragma unroll
@@ -2430,7 +2530,7 @@ __device__ __forceinline__ double trig_uwu(const double* C, int i, int j, int R)
 // X = L^-1 stored packed lower (incl. diagonal) to Xout for k_wsolve (residuals.py:567-589).
 template <int NW>
 __device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& Pd, const pint_spec_t& S, double F0, double* A,
-                               int wave, int lane, int* sflag, double* Xout) {
+                               int wave, int lane, int* sflag, double* Xout, const double* ones) {
     const int ncol = S.ncol, R = 2 * S.nred, Kn = R + 1;
     const int nbs = (Kn + 15) >> 4;
     const int tid = threadIdx.x;
@@ -2445,6 +2545,8 @@ __device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& 
             const double si = (gi < R) ? 1.0 : F0, sj = (gj < R) ? 1.0 : F0;
             if (S.wb_noones && (gi == R || gj == R)) {
                 v = (gi == gj) ? 1.0 : 0.0;  // no ones column (PHOFF free): a decoupled unit row
+            } else if (!Pd.vg && ones && ones_virtual(S) && (gi == R || gj == R)) {
+                v = ones[gi == R ? gj : gi] + (gi == gj ? 1e-40 : 0.0);  // k_onesrow (no Offset column)
             } else {
                 // vg: U^T W U from the pulsar's weighted trig sums (U's ones column is the
                 // constant column itself, not F0 x the Offset column of M): F^T W F by the
@@ -2697,7 +2799,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
                                                        int* __restrict__ status, int fuse_sigma, int refine,
-                                                       double* __restrict__ xw) {
+                                                       double* __restrict__ xw, const double* __restrict__ ones) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -2713,7 +2815,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const GramView G = gram_view(Pd, I, Gpart, Pd.dsplit != 0, Sd, DD);
-        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff))
+        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff,
+                                ones ? ones + I.coff : nullptr))
             if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
         return;
     }
@@ -3230,7 +3333,7 @@ __global__ __launch_bounds__(NW * 64) void k_sigma(const PsrDev* __restrict__ ps
                                                    const double* __restrict__ tables, const double* __restrict__ Gpart,
                                                    int compact, const double* __restrict__ Sd,
                                                    const double* __restrict__ DD, double* __restrict__ sigL,
-                                                   int* __restrict__ status) {
+                                                   int* __restrict__ status, const double* __restrict__ ones) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     const InstDev I = insts[blockIdx.x];
@@ -3242,7 +3345,8 @@ __global__ __launch_bounds__(NW * 64) void k_sigma(const PsrDev* __restrict__ ps
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const GramView G = gram_view(Pd, I, Gpart, compact && Pd.dsplit, Sd, DD);
-    if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff)) {
+    if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff,
+                            ones ? ones + I.coff : nullptr)) {
         if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
     }
 }
@@ -3273,7 +3377,7 @@ __global__ __launch_bounds__(256) void k_wdot(const PsrDev* __restrict__ psrs, c
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* out = wpart + ((long)inst * nsplit + split) * stride;
     if (compact && Pd.dsplit && Pd.vg) {
-        // Fourier columns generated per row by rotations of the fundamental (k_redbase):
+        // Fourier columns generated per row by rotations of the fundamental (k_trig_setup):
         // wave w takes harmonics 8w .. 8w+7; wave 0 also accumulates r^T W r and 1^T W r
         const int h0 = 8 * wave;
         const bool act = h0 < S.nred;
@@ -3539,7 +3643,7 @@ __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ ps
     double v = 0.0;
     if (!dm && k1 > 0 && k1 <= 128) {
         // PLRedNoise block: harmonics 1..dmn0 of f_1 = red_freq[0] (get_rednoise_freqs is
-        // linspace(1/T, nmodes/T)), by rotations of the row's e^{i theta} (k_redbase) instead
+        // linspace(1/T, nmodes/T)), by rotations of the row's e^{i theta} (k_trig_setup) instead
         // of a double-double reduction and a sincos per harmonic; four independent chains
         // (harmonics j + 1 + 4m, j < 4, stepped by e^{4 i theta}) for instruction-level
         // parallelism
@@ -3728,6 +3832,23 @@ __global__ __launch_bounds__(256) void k_debug_gram(const PsrDev* __restrict__ p
     for (int j = threadIdx.x; j < I.K; j += blockDim.x) o[(long)W * W + j] = colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j);
 }
 
+// The design-matrix normalisation of the last pint_fit_step (pint_read_norms): per instance
+// its K column norms squared in the fitter's original column order -- mode 1 (GLS) the
+// unweighted column sums of squares of [M | F] (fitter.py:2164-2176 normalize_designmatrix),
+// mode 0 (WLS) the whitened Gram's diagonal, the timing columns (fitter.py:1320-1343).
+__global__ __launch_bounds__(64) void k_norms(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                              const double* __restrict__ Gpart, const double* __restrict__ colsq,
+                                              int nsplit, int compact, const double* __restrict__ Sd,
+                                              const double* __restrict__ DD, const double* __restrict__ DCS, int mode,
+                                              double* __restrict__ out) {
+    const InstDev I = insts[blockIdx.x];
+    const PsrDev& Pd = psrs[I.psr];
+    const bool cmp = compact && Pd.dsplit;
+    const GramView g = gram_view(Pd, I, Gpart, cmp, Sd, DD);
+    for (int j = threadIdx.x; j < I.K; j += blockDim.x)
+        out[I.coff + j] = mode == 1 ? colsq_of(Pd, I, colsq, nsplit, cmp, DCS, j) : g(j, j);
+}
+
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
@@ -3739,6 +3860,7 @@ struct PsrHost {
     int dslot_ns = 0;           // vns the uploaded dslot was formed with (0: none)
     std::vector<void*> bufs;
     int n, K;
+    double f1 = 0.0, f1_lo = 0.0;  // the red-noise fundamental (dd), k_trig_setup
 };
 
 struct pint_ctx {
@@ -3751,6 +3873,7 @@ struct pint_ctx {
     bool sigma_pending = false;
     std::string err;
     std::vector<PsrHost> psrs;
+    std::vector<int> setup_pending;  // pulsars whose red-noise set-up (k_trig_setup) is not run yet
     PsrDev* d_psrs = nullptr;
     int npsr_dev = 0;
     // instances
@@ -3863,6 +3986,8 @@ struct pint_ctx {
     bool wfuse = false;            // the batch takes the fused Woodbury dots (k_resid2 tiles)
     bool wtile_valid = false;      // d_wpart holds the current residuals' dots (one split)
     double* d_wtile = nullptr;     // k_resid2's per-block trig tiles (256 per residual block)
+    double* d_norms = nullptr;     // pint_read_norms: per-instance K vectors (coff)
+    double* d_ones = nullptr;      // k_onesrow: the Woodbury ones row without an Offset column (coff)
     int wstride = 0;
     hipEvent_t ev_noise = nullptr;
 };
@@ -3978,18 +4103,62 @@ extern "C" void pint_release_cache(void) {
     hipSetDevice(cur);
 }
 
-// the weighted trig sums of a pulsar with red noise (PsrDev::trigW) from its current isig
-static int form_trigw(pint_ctx* ctx, const PsrDev& d, int n) {
-    if (!d.trigW || !d.red_cs || n <= 0) return 0;
-    const int nb = (n + TRIGU_R - 1) / TRIGU_R;
-    double* part = nullptr;
-    HIPCHK(hipMalloc((void**)&part, sizeof(double) * 128 * std::max(1, nb)));
-    hipLaunchKernelGGL(k_trigw, dim3(nb), dim3(128), 0, ctx->stream, d.red_cs, d.isig, n, part);
-    hipLaunchKernelGGL(k_trigu_sum, dim3(128), dim3(256), 0, ctx->stream, part, nb, (double*)d.trigW);
+// k_trig_setup + k_trig_sum over a list of jobs (one sync at the end)
+static int run_trig_jobs(pint_ctx* ctx, std::vector<TrigJob>& jobs) {
+    if (jobs.empty()) return 0;
+    int nb = 0;
+    for (auto& J : jobs) {
+        J.b0 = nb;
+        J.nb = (J.n + TRIG_RB - 1) / TRIG_RB;
+        nb += J.nb;
+    }
+    void *part = nullptr, *dj = nullptr;
+    HIPCHK(cmalloc(&part, sizeof(double) * 512 * (size_t)std::max(1, nb)));
+    HIPCHK(cmalloc(&dj, sizeof(TrigJob) * jobs.size()));
+    HIPCHK(hipMemcpyAsync(dj, jobs.data(), sizeof(TrigJob) * jobs.size(), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_trig_setup, dim3(nb), dim3(256), sizeof(double) * 4 * 48 * WT_CS, ctx->stream,
+                       (const TrigJob*)dj, (int)jobs.size(), (double*)part);
+    hipLaunchKernelGGL(k_trig_sum, dim3((unsigned)jobs.size()), dim3(256), 0, ctx->stream, (const TrigJob*)dj,
+                       (const double*)part);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipFree(part));
+    dfree(part);
+    dfree(dj);
     return 0;
+}
+
+static TrigJob trig_job(const PsrHost& ph, bool base) {
+    const PsrDev& d = ph.dev;
+    TrigJob J{};
+    J.tdb_hi = d.tdb_hi;
+    J.tdb_lo = d.tdb_lo;
+    J.isig = d.isig;
+    J.cs = (double*)d.red_cs;
+    J.trigU = base ? (double*)d.trigU : nullptr;
+    J.trigW = (double*)d.trigW;
+    J.f1 = ph.f1;
+    J.f1_lo = ph.f1_lo;
+    J.n = ph.n;
+    J.base = base ? 1 : 0;
+    return J;
+}
+
+// the red-noise set-up of every pulsar added since the last flush, batched: e^{i theta},
+// e^{i 8 theta} per TOA and the trig sums U_m, V_m, C_m, S_m (k_trig_setup + k_trig_sum)
+static int flush_setup(pint_ctx* ctx) {
+    if (ctx->setup_pending.empty()) return 0;
+    std::vector<TrigJob> jobs;
+    for (int p : ctx->setup_pending) jobs.push_back(trig_job(ctx->psrs[p], true));
+    ctx->setup_pending.clear();
+    return run_trig_jobs(ctx, jobs);
+}
+
+// the weighted trig sums of a pulsar with red noise (PsrDev::trigW) from its current isig
+static int form_trigw(pint_ctx* ctx, const PsrHost& ph) {
+    if (!ph.dev.trigW || !ph.dev.red_cs || ph.n <= 0) return 0;
+    if (flush_setup(ctx)) return 1;  // red_cs first
+    std::vector<TrigJob> jobs{trig_job(ph, false)};
+    return run_trig_jobs(ctx, jobs);
 }
 
 template <typename T>
@@ -4081,7 +4250,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
                    (void**)&ctx->d_xw_s[0], (void**)&ctx->d_xw_s[1], (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
-                   (void**)&ctx->d_wtile};
+                   (void**)&ctx->d_wtile, (void**)&ctx->d_norms, (void**)&ctx->d_ones};
     for (auto p : ps) dfree(*p);
     ctx->d_dpars = ctx->d_errs = ctx->d_cov = ctx->d_chi2lin = ctx->d_xw = ctx->d_chi2g = nullptr;
     ctx->copy_pend[0] = ctx->copy_pend[1] = false;
@@ -4187,27 +4356,25 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     rc |= upload(ctx, ph, t->jump_mask, n + 1, d.jmask);
     rc |= upload(ctx, ph, t->dmx_a, n + 1, d.dmx_a);
     rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
-    if (t->dmx_x) rc |= upload(ctx, ph, t->dmx_x, (size_t)t->dmx_x[n + 1], d.dmx_x);
+    if (t->dmx_x) {
+        // the CSR overflow of the DMX bin ids: n+2 non-decreasing offsets starting at n+2,
+        // then bin indices in [0, ndmx) (the kernels index the table with them unchecked)
+        const int32_t* x = t->dmx_x;
+        bool ok = x[0] == n + 2;
+        for (int i = 0; ok && i <= n; i++) ok = x[i + 1] >= x[i];
+        for (int k = ok ? n + 2 : 0; ok && k < x[n + 1]; k++) ok = x[k] >= 0 && x[k] < spec->ndmx;
+        if (!ok) { ctx->err = "dmx_x: malformed DMX overflow CSR (offsets or bin indices)"; return -PINT_E_INVALID; }
+        rc |= upload(ctx, ph, t->dmx_x, (size_t)x[n + 1], d.dmx_x);
+    }
     rc |= upload(ctx, ph, red_freq, (size_t)2 * spec->nred, d.red_freq);
     rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)4 * n, d.red_cs);
-    if (!rc && spec->nred > 0) {
-        hipLaunchKernelGGL(k_redbase, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, d.tdb_hi, d.tdb_lo, n,
-                           red_freq[0], red_freq[spec->nred], (double*)d.red_cs);
-        HIPCHK(hipGetLastError());
-    }
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
     rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
-    if (!rc && spec->nred > 0) {
-        const int nb = (n + TRIGU_R - 1) / TRIGU_R;
-        double* part = nullptr;
-        HIPCHK(hipMalloc((void**)&part, sizeof(double) * 128 * std::max(1, nb)));
-        hipLaunchKernelGGL(k_trigu, dim3(nb), dim3(128), 0, ctx->stream, d.red_cs, n, part);
-        hipLaunchKernelGGL(k_trigu_sum, dim3(128), dim3(256), 0, ctx->stream, part, nb, (double*)d.trigU);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        HIPCHK(hipFree(part));
-        if (form_trigw(ctx, d, n)) return PINT_E_HIP;
+    const bool trig_setup = spec->nred > 0;  // red_cs and the trig sums: flush_setup, batched
+    if (trig_setup) {
+        ph.f1 = red_freq[0];
+        ph.f1_lo = red_freq[spec->nred];
     }
     {
         // compact fit layout: DMX columns out of M when there are enough of them and no TOA
@@ -4297,6 +4464,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
     d.K = K;
     d.Kp = Kp;
     ctx->psrs.push_back(ph);
+    if (trig_setup) ctx->setup_pending.push_back((int)ctx->psrs.size() - 1);
     if (refresh_psrs(ctx)) return -PINT_E_HIP;
     return (int)ctx->psrs.size() - 1;
 }
@@ -4387,6 +4555,7 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
 int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (flush_setup(ctx)) return PINT_E_HIP;  // the uploads' red-noise set-up, one batch
     free_instances(ctx);
     ctx->inst.resize(ninst);
     long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0, eoff = 0, epoff = 0;
@@ -4743,6 +4912,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     ctx->out_slot = -1;
     select_out_slot(ctx, ctx->slot);
     HIPCHK(cmalloc((void**)&ctx->d_lam, sizeof(double) * ninst));
+    HIPCHK(cmalloc((void**)&ctx->d_norms, sizeof(double) * coff));
+    HIPCHK(cmalloc((void**)&ctx->d_ones, sizeof(double) * coff));
     HIPCHK(cmalloc((void**)&ctx->d_esum, sizeof(double) * (eoff > 0 ? eoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_eD, sizeof(double) * (epoff > 0 ? epoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_eW, sizeof(double) * (epoff > 0 ? epoff : 1)));
@@ -5054,6 +5225,19 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     const int cmp = ctx->m_compact;
     const bool vgp = cmp && ctx->n_vg > 0;  // k_gram_v path for the vg instances
+    // PhaseOffset with a frozen PHOFF and correlated noise: the Woodbury ones row (k_onesrow)
+    const double* ones = nullptr;
+    if (mode == 1) {
+        for (auto& I : ctx->inst) {
+            const PsrHost& ph = ctx->psrs[I.psr];
+            if (ph.spec.o_PHOFF >= 0 && !ph.spec.wb_noones && (ph.spec.nred > 0 || ph.dev.nep > 0)) ones = ctx->d_ones;
+        }
+        if (ones) {
+            hipLaunchKernelGGL(k_onesrow, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_eC, cmp, ctx->d_ones);
+            HIPCHK(hipGetLastError());
+        }
+    }
     if (cmp && ctx->max_ndc > 0 && ctx->any_dmx_rows) {
         int maxKd = 0;
         bool any_gather = false;
@@ -5241,11 +5425,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->ev_gram, 0));
         if (nbs_sig <= 5)
             hipLaunchKernelGGL(k_sigma<4>, dim3(ctx->ninst), dim3(256), lds_s, ctx->sstream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status);
+                               ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL, ctx->d_status, ones);
         else
             hipLaunchKernelGGL(k_sigma<16>, dim3(ctx->ninst), dim3(1024), lds_s, ctx->sstream, ctx->d_psrs,
                                ctx->d_inst, ctx->d_tables, ctx->d_G, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_sigL,
-                               ctx->d_status);
+                               ctx->d_status, ones);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
         ctx->sigma_pending = true;
@@ -5268,7 +5452,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                               (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
                               (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
                               ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                              fuse_sigma, ctx->refine, xw);
+                              fuse_sigma, ctx->refine, xw, ones);
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -5296,7 +5480,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         hipLaunchKernelGGL(k_solve, dim3(ctx->ninst), dim3(SOLVE_T), lds_s, ctx->stream, ctx->d_psrs, ctx->d_inst,
                            ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, nparts, mode, cmp, ctx->d_Sd, ctx->d_DD,
                            ctx->d_DCS, ctx->d_work, ctx->d_dpars,
-                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, do_sigma);
+                           ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, do_sigma, ones);
     }
     if (do_sigma && !(nbx > BS_MAXNB || !ctx->blocked_solve)) {
         // Sigma too large for k_sigma but the main solve went to the blocked kernels
@@ -5810,6 +5994,20 @@ int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
 
 // Parity introspection: the assembled normal matrix of the last pint_fit_step (see
 // k_debug_gram); out holds (K_i+1)^2 + K_i doubles per instance, concatenated.
+// The normalisation of the last pint_fit_step's design matrix (k_norms): per instance K
+// values at the instance's K+1-stride offset (read_step's layout), squared column norms.
+int pint_read_norms(pint_ctx* ctx, int mode, double* out) {
+    if (!ctx || ctx->ninst <= 0 || !out || (mode != 0 && mode != 1)) return PINT_E_INVALID;
+    if (ctx->lazy) { ctx->err = "pint_read_norms is synchronous (lazy mode is on)"; return PINT_E_INVALID; }
+    hipSetDevice(ctx->device);
+    hipLaunchKernelGGL(k_norms, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
+                       ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, mode, ctx->d_norms);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, ctx->d_norms, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PINT_OK;
+}
+
 int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
     if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
@@ -5870,7 +6068,7 @@ int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
     HIPCHK(hipMemcpyAsync((void*)ph.dev.sigma, sigma_s, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync((void*)ph.dev.isig, is.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (ph.spec.nred > 0 && form_trigw(ctx, ph.dev, n)) return PINT_E_HIP;  // the F^T W F sums of the new weights
+    if (ph.spec.nred > 0 && form_trigw(ctx, ph)) return PINT_E_HIP;  // the F^T W F sums of the new weights
     ph.dev.logsig = ls;
     ph.dev.sumw = sw;
     return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK;

@@ -100,9 +100,11 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.o_PHOFF = place("PHOFF")
     phoff_free = has_phoff and "PHOFF" in model.free_params
     spec.wb_noones = 1 if phoff_free else 0
-    if has_phoff and not phoff_free and use_gls_basis and model.has_correlated_errors:
-        # the Woodbury chi2 then appends a column of ones the fit layout does not carry
-        raise NotImplementedError("PhaseOffset with a frozen PHOFF and correlated noise "
+    if has_phoff and not phoff_free and use_gls_basis and "PLDMNoise" in model.components:
+        # the Woodbury chi2 then appends a column of ones the fit layout does not carry; its
+        # row of Sigma is formed from the weighted trig sums (k_onesrow), which cover the
+        # PLRedNoise harmonics and ECORR but not PLDMNoise's (1400 MHz / f)^2-scaled modes
+        raise NotImplementedError("PhaseOffset with a frozen PHOFF and PLDMNoise "
                                   "(residuals.py:583-585 ones column) is not supported")
     ak = model.astrometry_kind
     spec.astrometry = ak
@@ -846,6 +848,15 @@ class Session:
             out.append(d)
         return out
 
+    def read_norms(self, mode):
+        """Per instance the K squared column norms of the last fit_step's design matrix
+        (pint_read_norms): mode 1 the unweighted sums of squares of [M | F], mode 0 the
+        whitened Gram's diagonal."""
+        kk = [l.K + 1 for l in self.inst_layout]
+        out = np.empty(sum(kk))
+        self._check(self.L.pint_read_norms(self.ctx, int(mode), L.ptr(out)))
+        return [x[:l.K] for x, l in zip(self._split(out, kk), self.inst_layout)]
+
     def debug_gram(self, pre_ecorr=False):
         """Stage-wise parity introspection: per instance (G, colsq) of the last fit_step, G the
         unnormalised (K+1)^2 normal matrix [M | r]^T N^-1 [M | r] (ECORR eliminated, or
@@ -913,6 +924,58 @@ class Session:
 def release_cache():
     """Hand the device-buffer cache back to the HIP runtime (pint_release_cache)."""
     L.lib().pint_release_cache()
+
+
+# -- resident uploads (reference-API single fits and residuals) ------------------------
+# The last few (TOAs, model structure) uploads stay on the device with their Session, like
+# the TOAs of a serving process: a fit or Residuals of the same TOAs and model structure
+# re-binds one parameter table instead of packing and uploading the TOAs again.  An entry is
+# reused only when every parameter outside the device table (noise values, DMX ranges,
+# masks, TZR, ...) is unchanged, the frozen set and the components are the same and the
+# TOA object is the same object; anything else re-uploads.
+RESIDENT_MAX = 4
+_RESIDENT: "Dict[tuple, tuple]" = {}
+
+
+def _structure_sig(model, lay):
+    offs = lay.offsets
+    return (tuple(model.components), model.binary, tuple(model.free_params),
+            tuple((n, (model[n].value is None) if n in offs else str(model[n].value), bool(model[n].frozen))
+                  for n in model.params))
+
+
+def resident(model, toas, tag=None, track_mode=None, subtract_mean=True, use_weighted_mean=True,
+             use_gls_basis=True):
+    """(Session, PulsarLayout) of the resident upload of (model structure, toas), creating
+    it (and evicting the least recently used entry beyond RESIDENT_MAX) when needed.  The
+    Session belongs to the cache: callers must not close it."""
+    key = (id(toas), toas.ntoas, tag, track_mode, bool(subtract_mean), bool(use_weighted_mean), bool(use_gls_basis))
+    ent = _RESIDENT.pop(key, None)
+    if ent is not None:
+        s, lay, t0, sig = ent
+        if t0 is toas and model.binary != "ELL1H" and _structure_sig(model, lay) == sig:
+            model.validate()
+            _RESIDENT[key] = ent  # most recently used last
+            return s, lay
+        s.close()
+    s = Session()
+    try:
+        lay = s.add(build_layout(model, toas, track_mode=track_mode, subtract_mean=subtract_mean,
+                                 use_weighted_mean=use_weighted_mean, use_gls_basis=use_gls_basis))
+    except Exception:
+        s.close()
+        raise
+    _RESIDENT[key] = (s, lay, toas, _structure_sig(model, lay))
+    while len(_RESIDENT) > RESIDENT_MAX:
+        old = next(iter(_RESIDENT))
+        _RESIDENT.pop(old)[0].close()
+    return s, lay
+
+
+def drop_resident():
+    """Close every resident upload's Session."""
+    while _RESIDENT:
+        _RESIDENT.pop(next(iter(_RESIDENT)))[0].close()
 
 
 # -- convenience single-model evaluations (used by TimingModel methods) ----------------

@@ -97,7 +97,7 @@ class BatchFit:
 
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
                  layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None,
-                 wideband=False, want_fac=False):
+                 wideband=False, want_fac=False, fac_style=None, own_session=None):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
         are bare parameter tables of already-uploaded pulsars, e.g. grid points).
 
@@ -108,6 +108,9 @@ class BatchFit:
         self.items = list(items) if items is not None else None
         self.mode = mode
         self.want_fac = bool(want_fac)  # read the step's normalisation back (Fitter.fac)
+        self.fac_style = fac_style      # None | "timing" | "wbstate" (_fac_into)
+        # a Session passed in belongs to the caller (a resident upload, a grid session)
+        self.own_session = (session is None) if own_session is None else bool(own_session)
         self.threshold = threshold
         self.degeneracy_style = degeneracy_style or mode
         self.degenerate = None  # per instance: dropped directions of the last SVD-path step
@@ -187,10 +190,12 @@ class BatchFit:
 
     # -- helpers ------------------------------------------------------------------------
     def _chi2_now(self):
-        c2 = self.s.read_chi2()
-        if any(self.use_gls_chi2):
-            cg = self.s.chi2_gls()
-            c2 = np.where(self.use_gls_chi2, cg, c2)
+        if all(self.use_gls_chi2):
+            c2 = self.s.chi2_gls()
+        else:
+            c2 = self.s.read_chi2()
+            if any(self.use_gls_chi2):
+                c2 = np.where(self.use_gls_chi2, self.s.chi2_gls(), c2)
         if self.wideband:  # WidebandTOAResiduals.chi2 = the TOA chi2 + the DM chi2 (residuals.py:1206)
             c2 = c2 + self.s.dm_resids()[1]
         return c2, None
@@ -273,19 +278,27 @@ class BatchFit:
         column norms of the whitened M (fitter.py:1320-1343); GLS, the column norms of
         [M | noise bases] (fitter.py:2164-2176), with the ECORR quantisation columns
         (sqrt of each epoch's TOA count) after the timing columns and before the Fourier
-        bases, the reference's noise_model_designmatrix order.  From the device Gram
-        (pint_debug_gram: its diagonal, and the unweighted column sums of squares)."""
+        bases, the reference's noise_model_designmatrix order.  From the device
+        (pint_read_norms: the Gram's diagonal, or the unweighted column sums of squares).
+        fac_style "timing": the timing columns only (GLSFitter full_cov=True appends no
+        noise basis, fitter.py:2166); "wbstate": WidebandState's norm[ntmpar:] = 1 with
+        ntmpar = free parameters + 1 (fitter.py:1652-1657)."""
         if not self.want_fac:
             return
-        for (G, colsq), k, lay in zip(self.s.debug_gram(), self.idx, self.layouts):
+        for nq, k, lay in zip(self.s.read_norms(1 if self.gls else 0), self.idx, self.layouts):
             nc = len(lay.columns)
             if self.gls:
-                f = np.sqrt(np.asarray(colsq[:lay.K], dtype=np.float64))
+                f = np.sqrt(np.asarray(nq[:lay.K], dtype=np.float64))
                 if lay.nep > 0:
                     ep = np.sqrt(np.diff(np.asarray(lay.ep_ptr)).astype(np.float64))
                     f = np.concatenate([f[:nc], ep, f[nc:]])
+                if self.fac_style == "timing":
+                    f = f[:nc]
+                elif self.fac_style == "wbstate":
+                    m = self.items[k][0] if self.items is not None else lay.model
+                    f[len(m.free_params) + 1:] = 1.0
             else:
-                f = np.sqrt(np.diag(G)[:nc].astype(np.float64))
+                f = np.sqrt(np.asarray(nq[:nc], dtype=np.float64))
             f[f == 0] = 1.0
             results[k].fac = f
 
@@ -349,18 +362,28 @@ class BatchFit:
         """The reference's per-fitter control flow (fitter.py:1015-1095), applied to every
         instance at once: a lambda-halving line search on each instance's chi2, with the
         best state tracked per instance.  Decisions are vectorised over instances; each
-        trial is one batched eval + chi2 of all undecided instances.  A trial state whose
-        evaluation fails (invalid parameters) is a rejected trial of that instance only."""
+        trial is one batched eval + chi2 of all instances.  A trial state whose evaluation
+        fails (invalid parameters) is a rejected trial of that instance only.
+
+        The states stay on the device: the current states are a device snapshot of the
+        tables (pint_save_tables), a trial is snapshot + lambda x step (pint_restore_tables,
+        k_apply), and an instance that has accepted its step keeps that lambda in the
+        following trials of the same iteration, so that after the last trial the tables hold
+        every instance's new current state.  Only the chi2 of a trial crosses to the host.
+        A state better than an instance's best is always an accepted one (its chi2 is below
+        the current state's), so the best tables are read back at most once per iteration."""
         self._step()                                     # step of the initial state (drops invalid ones)
         n = self.ninst
-        cur_tab = self.s.read_tables_flat()
+        single = n == 1
+        self.s.save_tables()                             # the current states
+        best_tab = self.s.read_tables_flat()
         sizes = np.array([l.tstride for l in self.layouts])
         ent = np.repeat(np.arange(n), sizes)             # instance of every table entry
         self._eval(False)
         cur_chi2, _ = self._chi2_now()
         cur_chi2 = np.array(cur_chi2, dtype=np.float64)
         best_chi2 = cur_chi2.copy()
-        best_tab = cur_tab.copy()
+        best_cur = np.ones(n, dtype=bool)                # the best state is the current one
         active = np.ones(n, dtype=bool)
         converged = np.zeros(n, dtype=bool)
         exc = np.zeros(n, dtype=bool)
@@ -369,10 +392,16 @@ class BatchFit:
                 break
             lam = np.ones(n)
             decided = ~active
+            acc_lam = np.zeros(n)                        # the lambda an instance ends the iteration at
             dec = np.zeros(n)
+            newbest = np.zeros(n, dtype=bool)
             while not decided.all():
-                self.s.set_tables(cur_tab)
-                self.s.apply_step(np.where(decided, 0.0, lam))
+                self.s.restore_tables()
+                applied = np.where(decided, acc_lam, lam)
+                if single:
+                    self.s.apply_step_uniform(float(applied[0]))
+                else:
+                    self.s.apply_step(applied)
                 bad = np.zeros(n, dtype=bool)
                 try:
                     self.s.eval(want_M=False)
@@ -384,14 +413,12 @@ class BatchFit:
                         raise
                 new_chi2, _ = self._chi2_now()
                 new_chi2 = np.where(bad, np.nan, np.array(new_chi2, dtype=np.float64))
-                new_tab = self.s.read_tables_flat()
                 und = ~decided
                 d = cur_chi2 - new_chi2
                 ok = np.isfinite(new_chi2)
                 better = und & ok & (new_chi2 < best_chi2)          # fitter.py:1046-1049
                 best_chi2[better] = new_chi2[better]
-                sel = better[ent]
-                best_tab[sel] = new_tab[sel]
+                newbest |= better
                 bad = und & (~ok | (d < -max_chi2_increase))         # :1050-1062 halve lambda
                 lam[bad] /= 2
                 gone = bad & (lam < min_lambda)                      # :1058 StepProblem
@@ -399,23 +426,37 @@ class BatchFit:
                 decided |= gone
                 dec[gone] = 0.0
                 good = und & ~bad                                    # :1063-1067 accept
-                sel = good[ent]
-                cur_tab[sel] = new_tab[sel]
+                acc_lam[good] = lam[good]
                 cur_chi2[good] = new_chi2[good]
                 dec[good] = d[good]
                 decided |= good
+                best_cur[good] = better[good]
+            # the tables hold every instance's last trial; its new current state is the
+            # accepted lambda (0 after a failed search): re-applied only where they differ,
+            # then the snapshot the next iteration's trials start from
+            if not np.array_equal(applied, acc_lam):
+                self.s.restore_tables()
+                if single:
+                    self.s.apply_step_uniform(float(acc_lam[0]))
+                else:
+                    self.s.apply_step(acc_lam)
+            self.s.save_tables()
+            if newbest.any():
+                tab = self.s.read_tables_flat()
+                sel = newbest[ent]
+                best_tab[sel] = tab[sel]
             done = active & exc
             conv = active & ~exc & (-max_chi2_increase <= dec) & (dec < required_chi2_decrease) & (lam == 1)
             converged |= conv                                        # :1076-1085
             active &= ~(done | conv)
             if active.any() and it < maxiter - 1:
-                self.s.set_tables(cur_tab)
                 # step at the new current states (inactive ones are ignored); every current
                 # state has been evaluated, so nothing can be dropped here
                 if self._step() is not None:
                     raise RuntimeError("a downhill state evaluated before failed its re-evaluation")
         # best state -> model, residuals; covariance from a step at the best state
-        self.s.set_tables(best_tab)
+        if not best_cur.all():
+            self.s.set_tables(best_tab)
         if self._step() is not None:
             raise RuntimeError("a downhill best state evaluated before failed its re-evaluation")
         results = None
@@ -437,7 +478,8 @@ class BatchFit:
         return self._finish(results)
 
     def close(self):
-        self.s.close()
+        if self.own_session:
+            self.s.close()
 
 
 # ----------------------------------------------------------------------------------
@@ -516,11 +558,17 @@ class Fitter:
     def get_designmatrix(self):
         return self.model.designmatrix(self.toas)
 
-    def _run(self, mode, plain=True, threshold=None, style=None, noise=True, **kw):
+    def _run(self, mode, plain=True, threshold=None, style=None, noise=True, fac_style=None, **kw):
+        from .engine import resident
         from .residuals import Residuals
         wideband = getattr(self, "is_wideband", False)
-        bf = BatchFit([(self.model, self.toas)], mode=mode, threshold=threshold, degeneracy_style=style,
-                      track_mode=self.track_mode, wideband=wideband, want_fac=True)
+        # the resident upload of these TOAs and this model structure (engine.resident): a
+        # refit, the next Downhill fit or a Residuals of the result re-binds one table
+        s, lay = resident(self.model, self.toas, tag="wb" if wideband else None, track_mode=self.track_mode,
+                          use_gls_basis=mode == "gls")
+        bf = BatchFit([(self.model, self.toas)], mode=mode, session=s, layouts=[lay], threshold=threshold,
+                      degeneracy_style=style, track_mode=self.track_mode, wideband=wideband, want_fac=True,
+                      fac_style=fac_style)
         self.resids = None
         try:
             res = bf.fit_plain(**kw)[0] if plain else bf.fit_downhill(**kw)[0]
@@ -662,7 +710,7 @@ class GLSFitter(Fitter):
         noise realisations (fitter.py:2268)."""
         self.full_cov = full_cov
         res = self._run("gls", plain=True, maxiter=maxiter, threshold=threshold, style="gls",
-                        noise=not full_cov)
+                        noise=not full_cov, fac_style="timing" if full_cov else None)
         self.update_model(res.chi2)
         return res.chi2
 
@@ -770,7 +818,8 @@ class DownhillFitter(Fitter):
             threshold = 0.0
         res = self._run(self.mode, plain=False, maxiter=maxiter, required_chi2_decrease=required_chi2_decrease,
                         max_chi2_increase=max_chi2_increase, min_lambda=min_lambda,
-                        threshold=threshold, style="wls" if self.mode == "wls" else "glsstate")
+                        threshold=threshold, style="wls" if self.mode == "wls" else "glsstate",
+                        fac_style="wbstate" if getattr(self, "is_wideband", False) else None)
         self.update_model(res.chi2)
         if res.status == "StepProblem":
             raise StepProblem("Unable to improve chi2 even with very small steps")

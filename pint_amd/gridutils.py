@@ -55,7 +55,8 @@ def shard_range(npts: int, rank: int, world: int):
 def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
     """All-gather every rank's chi2 block (NaN-padded to `per`) -> the full flat array.
     Over RCCL when the process group is nccl, gloo on CPU."""
-    if dist is None or dist.get_world_size() == 1:
+    from . import pta
+    if dist is None or (dist.get_world_size() == 1 and not pta.FORCE_COLLECTIVE):
         return local
     import torch
     world = dist.get_world_size()
@@ -219,7 +220,9 @@ def grid_chisq_derived(ftr, parnames: Sequence[str], parfuncs: Sequence, gridval
     its serial path keeps only the last point's value, gridutils.py:580-581)."""
     grid = np.meshgrid(*[_as_ld(v) for v in gridvalues])
     shape = grid[0].shape
-    out = [np.broadcast_to(np.asarray(f(*grid)), shape) for f in parfuncs]
+    # writable arrays of meshgrid shape (a parfunc returning a scalar broadcasts to a copy,
+    # not to a read-only stride-0 view)
+    out = [np.array(np.broadcast_to(np.asarray(f(*grid)), shape)) for f in parfuncs]
     flat = [_as_ld(o).reshape(-1) for o in out]
     chi2, extra = _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
     return chi2.reshape(shape), out, {e: v.reshape(shape) for e, v in extra.items()}

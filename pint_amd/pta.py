@@ -21,6 +21,10 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
+# Run the gathers through the process group even at world size 1 (tests: the RCCL branch
+# executes on one GPU before a multi-GPU node ever sees it).
+FORCE_COLLECTIVE = False
+
 STATUS_CODES = {"ok": 0, "converged": 1, "MaxiterReached": 2, "StepProblem": 3, "InvalidModelParameters": 4}
 STATUS_NAMES = {v: k for k, v in STATUS_CODES.items()}
 
@@ -63,7 +67,7 @@ def _dist():
 def gather_rows(local: np.ndarray, counts: Sequence[int], dist) -> np.ndarray:
     """All-gather each rank's (counts[r], W) float64 block; returns the rank-ordered
     concatenation (sum(counts), W) on every rank.  RCCL for an nccl group, gloo on CPU."""
-    if dist is None or dist.get_world_size() == 1:
+    if dist is None or (dist.get_world_size() == 1 and not FORCE_COLLECTIVE):
         return local
     import torch
     W = local.shape[1]

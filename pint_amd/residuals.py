@@ -12,7 +12,7 @@ import collections
 import numpy as np
 
 from . import _lib as L
-from .engine import Session, build_layout, pack_table
+from .engine import Session, build_layout, pack_table, resident
 
 
 class Residuals:
@@ -42,31 +42,29 @@ class Residuals:
             self.update()
 
     def update(self):
-        s = Session()
-        try:
-            lay = s.add(build_layout(self.model, self.toas, track_mode=self._track_mode_arg,
-                                     subtract_mean=self.subtract_mean, use_weighted_mean=self.use_weighted_mean))
-            self.track_mode = lay.track_mode
-            s.set_instances([(lay, pack_table(lay))])
-            corr = self.model.has_correlated_errors and (lay.nred > 0 or lay.nep > 0)
-            s.eval(want_M=Session.FIT if corr else False)
-            tr, pr, c2 = s.read_resids()
-            self.time_resids = tr[0]
-            self.phase_resids = pr[0]
-            self._sigma_us = lay.sigma_us
-            if corr:
-                try:  # the step only provides the Woodbury factor; a degenerate timing solve is irrelevant
-                    s.fit_step(1)
-                except L.PintError as e:
-                    if e.code != L.PINT_E_NOT_PD:
-                        raise
-                self._chi2 = float(s.chi2_gls()[0])
-            else:
-                self._chi2 = float(c2[0])
-            ln_kind = 1 if corr else (2 if self.model.has_correlated_errors else 0)
-            self._lognorm = float(s.lognorm(ln_kind)[0])
-        finally:
-            s.close()
+        # the resident upload of these TOAs and this model structure (engine.resident): a
+        # Residuals of a fitted model re-binds one parameter table
+        s, lay = resident(self.model, self.toas, track_mode=self._track_mode_arg,
+                          subtract_mean=self.subtract_mean, use_weighted_mean=self.use_weighted_mean)
+        self.track_mode = lay.track_mode
+        s.set_instances([(lay, pack_table(lay, self.model))])
+        corr = self.model.has_correlated_errors and (lay.nred > 0 or lay.nep > 0)
+        s.eval(want_M=Session.FIT if corr else False)
+        tr, pr, c2 = s.read_resids()
+        self.time_resids = tr[0]
+        self.phase_resids = pr[0]
+        self._sigma_us = lay.sigma_us
+        if corr:
+            try:  # the step only provides the Woodbury factor; a degenerate timing solve is irrelevant
+                s.fit_step(1)
+            except L.PintError as e:
+                if e.code != L.PINT_E_NOT_PD:
+                    raise
+            self._chi2 = float(s.chi2_gls()[0])
+        else:
+            self._chi2 = float(c2[0])
+        ln_kind = 1 if corr else (2 if self.model.has_correlated_errors else 0)
+        self._lognorm = float(s.lognorm(ln_kind)[0])
 
     @classmethod
     def _from_batch(cls, toas, model, bf, d, chi2, track_mode=None):

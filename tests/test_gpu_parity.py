@@ -18,9 +18,10 @@ import pint_oracle as O
 pytestmark = pytest.mark.gpu
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise",
-         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk"]
+         "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk",
+         "phoff_red", "phoff_ecorr"]
 GLS_NAMES = ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ecorr_fit", "ell1h_h3", "ell1h_h4",
-             "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk"]
+             "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red", "phoff_ecorr"]
 
 
 @pytest.fixture(scope="module", params=NAMES)
@@ -173,7 +174,7 @@ def test_gls_fit(name):
     assert np.max(np.abs(f.resids.time_resids - z["gls_post_resid"])) < 2e-10
 
 
-@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff"])
+@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr"])
 def test_downhill_gls(name):
     from pint_amd import DownhillGLSFitter
     from pint_amd.fitter import MaxiterReached, StepProblem
@@ -481,6 +482,7 @@ def _fit_once_paths(items, vgram, vbin=True):
     c2 = s.chi2_gls()
     out = [(dp[k], er[k], cov[k], cl[k], c2[k]) for k in range(len(items))]
     bf.close()
+    s.close()
     return nvg, out
 
 
