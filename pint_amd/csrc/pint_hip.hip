@@ -2021,9 +2021,17 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
                 else v = 0.5 * (Sn[sm] - sd);               // cos a sin b
                 G[e] = v;
             } else {
-                double sacc = G[e];
-                for (int q = 1; q < g.nparts; q++) sacc += G[(long)q * KK + e];
-                G[e] = sacc;
+                // eight independent chains (eight partial loads in flight; a single chain
+                // issued one load per add and waited on each: a 195-split single pulsar
+                // took 127 us), combined in a fixed tree order (deterministic)
+                double a[8] = {G[e], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                int q = 1;
+                for (; q + 8 <= g.nparts; q += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) a[u] += G[(long)(q + u) * KK + e];
+                }
+                for (; q < g.nparts; q++) a[0] += G[(long)q * KK + e];
+                G[e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
             }
         }
     }
@@ -2034,9 +2042,14 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
             const int h = (int)(e - r0) / 2 + 1;
             cs[0] = 0.5 * (U[0] + (((e - r0) & 1) ? U[2 * h] : -U[2 * h]));
         } else {
-            double v = cs[0];
-            for (int q = 1; q < g.nsplit; q++) v += cs[q];
-            cs[0] = v;
+            double a[4] = {cs[0], 0.0, 0.0, 0.0};
+            int q = 1;
+            for (; q + 4 <= g.nsplit; q += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) a[u] += cs[q + u];
+            }
+            for (; q < g.nsplit; q++) a[0] += cs[q];
+            cs[0] = (a[0] + a[1]) + (a[2] + a[3]);
         }
     }
 }
@@ -4590,6 +4603,10 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                  d.red0c + 1 <= VMAXR0) ? 1 : 0;
     }
     const long slots = (long)ncu * (2 * nvgc > ninst ? GWG : 1);
+    // A batch too small to fill the chip even at the finest split (a single fit, a few
+    // pulsars) is latency-bound: splits of 128 rows leave each workgroup two chunks while
+    // k_greduce sums hundreds of partials per Gram element.  Keep >= 512 rows per split there.
+    if ((long)ninst * maxsplit < slots) maxsplit = std::max(1, std::min(maxsplit, (maxN + 511) / 512));
     // (smallest split count within 3% of the best makespan: each split adds a partial
     // Gram that k_greduce must sum)
     double best = 1e30;

@@ -404,6 +404,30 @@ def make_tzr_row(model, toas) -> dict:
             "delta_pulse_number": np.zeros(1), "flags": {}}
 
 
+class SplitView:
+    """Per-instance views of one flat output buffer (list-like: len, indexing, iteration),
+    formed on access: a batched step hands out its outputs without building one array
+    object per instance (host time per step), and the pinned buffer behind it is filled by
+    the device copies."""
+
+    def __init__(self, flat, offsets, shapes=None):
+        self.flat, self.off, self.shapes = flat, offsets, shapes
+
+    def __len__(self):
+        return len(self.off) - 1
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self[i] for i in range(*k.indices(len(self)))]
+        if k < 0:
+            k += len(self)
+        v = self.flat[self.off[k]:self.off[k + 1]]
+        return v.reshape(self.shapes[k]) if self.shapes is not None else v
+
+    def __iter__(self):
+        return (self[k] for k in range(len(self)))
+
+
 class Session:
     """A pint_ctx with uploaded pulsars and a batch of instances."""
 
@@ -505,6 +529,14 @@ class Session:
         self._check(self.L.pint_set_instances(self.ctx, len(ids), L.ptr(ids, C.c_int32), L.ptr(tabs)))
         self.inst_layout = lays
         self.ntab = len(tabs)
+        # per-instance output offsets (read_step, noise_resids), formed once per batch
+        kk = np.array([l.K + 1 for l in lays], dtype=np.int64)
+        nc = np.array([len(l.columns) for l in lays], dtype=np.int64)
+        nn = np.array([l.n for l in lays], dtype=np.int64)
+        self._off_k = np.concatenate([[0], np.cumsum(kk)])
+        self._off_cov = np.concatenate([[0], np.cumsum(nc * nc)])
+        self._cov_shapes = [(int(c), int(c)) for c in nc]
+        self._off_n = np.concatenate([[0], np.cumsum(nn)])
 
     # -- launches -------------------------------------------------------------------
     FIT = 2  # want_M for a fit step: compact layout (DMX columns as bin sums)
@@ -727,23 +759,19 @@ class Session:
         self._check(rc)
 
     def read_step(self, want_cov=True):
-        kk = [l.K + 1 for l in self.inst_layout]
-        nc = [len(l.columns) for l in self.inst_layout]
-        dp = self._pin("dp", sum(kk))
-        er = self._pin("er", sum(kk))
-        cov = self._pin("cov", sum(c * c for c in nc)) if want_cov else None
-        cl = self._pin("cl", len(kk))
+        """(steps, errors, covariances, linearised chi2) of the last fit_step: per-instance
+        views (SplitView) of the K+1 step / error vectors and the timing covariance."""
+        ok = self._off_k
+        dp = self._pin("dp", ok[-1])
+        er = self._pin("er", ok[-1])
+        cov = self._pin("cov", self._off_cov[-1]) if want_cov else None
+        cl = self._pin("cl", len(ok) - 1)
         self._check(self.L.pint_read_step(self.ctx, L.ptr(dp), L.ptr(er), L.ptr(cov), L.ptr(cl)))
         if not self.lazy:  # synchronous call: hand out private copies of the pinned buffers
             dp, er, cl = dp.copy(), er.copy(), cl.copy()
             cov = cov.copy() if want_cov else None
-        covs = []
-        if want_cov:
-            o = 0
-            for c in nc:
-                covs.append(cov[o:o + c * c].reshape(c, c))
-                o += c * c
-        return self._split(dp, kk), self._split(er, kk), covs, cl
+        covs = SplitView(cov, self._off_cov, self._cov_shapes) if want_cov else []
+        return SplitView(dp, ok), SplitView(er, ok), covs, cl
 
     def read_tables(self):
         return self._split(self.read_tables_flat(), [l.tstride for l in self.inst_layout])
@@ -819,17 +847,7 @@ class Session:
             ec = np.empty(sum(n)) if anyec else None
         self._check(self.L.pint_noise_resids(self.ctx, L.ptr(red), L.ptr(ec)))
         if self.lazy:
-            out = []
-            o = 0
-            for lay, k in zip(self.inst_layout, n):
-                d = {}
-                if anyec and "EcorrNoise" in lay.model.components:
-                    d["ecorr_noise"] = ec[o:o + k]
-                if anyred and lay.spec.dmn0 > 0:
-                    d["pl_red_noise"] = red[o:o + k]
-                out.append(d)
-                o += k
-            return out
+            return _NoiseViews(self.inst_layout, self._off_n, red if anyred else None, ec if anyec else None)
         red = red if red is not None else np.zeros(sum(n))
         ec = ec if ec is not None else np.zeros(sum(n))
         anydm = any(l.spec.dmn0 < l.nred for l in self.inst_layout)
@@ -926,6 +944,27 @@ def release_cache():
     L.lib().pint_release_cache()
 
 
+class _NoiseViews(SplitView):
+    """Per-instance {component: n-array} views of the noise realisations (lazy sessions)."""
+
+    def __init__(self, lays, off, red, ec):
+        super().__init__(None, off)
+        self.lays, self.red, self.ec = lays, red, ec
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self[i] for i in range(*k.indices(len(self)))]
+        if k < 0:
+            k += len(self)
+        lay, a, b = self.lays[k], self.off[k], self.off[k + 1]
+        d = {}
+        if self.ec is not None and "EcorrNoise" in lay.model.components:
+            d["ecorr_noise"] = self.ec[a:b]
+        if self.red is not None and lay.spec.dmn0 > 0:
+            d["pl_red_noise"] = self.red[a:b]
+        return d
+
+
 # -- resident uploads (reference-API single fits and residuals) ------------------------
 # The last few (TOAs, model structure) uploads stay on the device with their Session, like
 # the TOAs of a serving process: a fit or Residuals of the same TOAs and model structure
@@ -938,10 +977,11 @@ _RESIDENT: "Dict[tuple, tuple]" = {}
 
 
 def _structure_sig(model, lay):
+    # the values themselves (scalars compared with ==; a NaN never matches, so it re-uploads)
+    # (the parameter dict's insertion order and the components fix the column order)
     offs = lay.offsets
-    return (tuple(model.components), model.binary, tuple(model.free_params),
-            tuple((n, (model[n].value is None) if n in offs else str(model[n].value), bool(model[n].frozen))
-                  for n in model.params))
+    return (tuple(model.components), model.binary,
+            tuple((n, (p.value is None) if n in offs else p.value, p.frozen) for n, p in model._params.items()))
 
 
 def resident(model, toas, tag=None, track_mode=None, subtract_mean=True, use_weighted_mean=True,

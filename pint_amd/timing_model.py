@@ -73,11 +73,21 @@ class TimingModel:
     def add_param(self, p: Param):
         self._params[p.name] = p
         self.components.setdefault(p.component or "TimingModel", []).append(p.name)
+        object.__setattr__(self, "_order", None)
 
     @property
     def params(self) -> List[str]:
         """Parameter order: top level, astrometry, spindown, remaining components
-        (timing_model.py:614-652)."""
+        (timing_model.py:614-652).  Cached until the next add_param (the fitters ask for
+        it, and for free_params, several times per fit)."""
+        cached = self.__dict__.get("_order")
+        if cached is not None and cached[0] == len(self._params):
+            return list(cached[1])
+        order = self._params_order()
+        object.__setattr__(self, "_order", (len(self._params), tuple(order)))
+        return order
+
+    def _params_order(self) -> List[str]:
         top = [n for n, p in self._params.items() if p.component in ("", "TimingModel")]
         astro = [n for n, p in self._params.items() if p.component.startswith("Astrometry")]
         spin = [n for n, p in self._params.items() if p.component == "Spindown"]

@@ -46,3 +46,27 @@ def downhill_bar(name, p, floor=1e-3):
     if name not in d:
         return floor
     return max(floor, 2.0 * d[name]["max_dev_sigma"].get(p, 0.0))
+
+
+_SPREAD = None
+
+
+def rms_ps(a, b) -> float:
+    """rms of the difference of two time-residual arrays (s), in ps."""
+    return float(np.sqrt(np.mean((np.asarray(a, dtype=np.float64) - np.asarray(b, dtype=np.float64)) ** 2)) * 1e12)
+
+
+def chi2_bar(name, kind, resid_rms_ps, floor=1e-9):
+    """End-to-end relative chi2 bar of fixture `name` (kind "pre": the pre-fit Residuals chi2,
+    "fit": the GLSFitter / WLSFitter fit_toas(maxiter=1) chi2, "down": the DownhillGLSFitter
+    chi2): 2x the reference's own chi2 spread when its time residuals move by as much as the
+    residuals under test differ from the reference's.  tests/golden/fit_spread.json
+    (oracle/refgen/gen_fit_spread.py) holds max |chi2 / chi2_0 - 1| of the reference under fixed
+    per-TOA N(0, 5 ps) and N(0, 30 ps) residual shifts; the bar scales the larger per-ps rate
+    to the measured rms difference `resid_rms_ps` (at least the 5 ps longdouble floor)."""
+    global _SPREAD
+    if _SPREAD is None:
+        _SPREAD = json.load(open(os.path.join(GOLDEN, "fit_spread.json")))
+    d = _SPREAD[name]
+    per_ps = max(d["5ps"][kind] / 5.0, d["30ps"][kind] / 30.0)
+    return max(floor, 2.0 * per_ps * max(float(resid_rms_ps), 5.0))

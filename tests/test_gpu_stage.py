@@ -23,7 +23,7 @@ import copy
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN, load, ref_value
+from golden_util import GOLDEN, chi2_bar, load, ref_value, rms_ps
 
 pytestmark = pytest.mark.gpu
 
@@ -271,8 +271,10 @@ def test_fitter_noise_resids_and_update_model(name):
     um = dict(zip([str(x) for x in st["update_model_keys"]], st["update_model_vals"]))
     assert f.model.NTOA.value == int(um["NTOA"])
     assert float(f.model.START.value) == um["START"] and float(f.model.FINISH.value) == um["FINISH"]
-    assert abs(f.model.CHI2.value / um["CHI2"] - 1) < 5e-6
-    assert abs(f.model.CHI2R.value / um["CHI2R"] - 1) < 5e-6
+    # end-to-end: 2x the reference's chi2 spread at the measured post-fit residual rms
+    bar = chi2_bar(name, "fit", rms_ps(f.resids.time_resids, st["post_resid"]) if "post_resid" in st else 30.0)
+    assert abs(f.model.CHI2.value / um["CHI2"] - 1) < bar
+    assert abs(f.model.CHI2R.value / um["CHI2R"] - 1) < bar
     # TRES is the weighted rms of the post-fit residuals: end-to-end, so at the ~ps floor of
     # two longdouble/double-double evaluations (tests/test_oracle_golden.py::test_gls_fit)
     assert abs(f.model.TRES.value / um["TRES"] - 1) < 1e-5
@@ -354,8 +356,10 @@ def test_downhill_gls_j0740():
         s = meta["down_errors"][p]
         d = float((np.longdouble(f.model[p].value) - ref_value(meta, "down_params", p)) / np.longdouble(s))
         worst = max(worst, abs(d))
-    print(f"j0740 downhill: chi2 rel {rel:.2e}, worst param {worst:.2e} sigma")
-    assert rel < 5e-6
+    from pint_amd import Residuals
+    bar = chi2_bar("j0740", "down", rms_ps(Residuals(toas, model).time_resids, z["res_time"]))
+    print(f"j0740 downhill: chi2 rel {rel:.2e} (bar {bar:.1e}), worst param {worst:.2e} sigma")
+    assert rel < bar
     assert worst < 1e-3
 
 
@@ -378,8 +382,11 @@ def test_grid_m2_sini_j0740():
     pb_ref = st["grid_PB_parallel_hi"] + st["grid_PB_parallel_lo"]
     dpb = np.max(np.abs(ex["PB"] - pb_ref))
     print(f"j0740 (M2,SINI) grid: chi2 max rel {rel:.2e}; PB max abs {dpb:.2e} d")
-    # each point's chi2 is a post-fit chi2: end-to-end, so at the floor of test_gls_fit (5e-6)
-    assert rel < 5e-6
+    # each point's chi2 is a post-fit chi2: end-to-end, so at the floor of test_gls_fit (2x
+    # the reference's fit chi2 spread at the measured residual rms, golden_util.chi2_bar)
+    from pint_amd import Residuals
+    m0 = load("j0740")[0]  # the fixture's own model (model above holds the grid's base values)
+    assert rel < chi2_bar("j0740", "fit", rms_ps(Residuals(toas, m0).time_resids, z["res_time"]))
     assert np.unravel_index(np.argmin(c2), c2.shape) == np.unravel_index(np.argmin(ref), ref.shape)
     # serial (warm start) and parallel (cold start) differ in the reference itself
     print("reference serial vs parallel:", np.max(np.abs(st["grid_chi2_serial"] / ref - 1)))
