@@ -373,7 +373,9 @@ int pint_inst_status(pint_ctx *ctx, int32_t *out);
  * DownhillGLSFitter.fit_toas (:1582-1605) set it. */
 int pint_noise_resids(pint_ctx *ctx, double *red, double *ecorr);
 /* The PLDMNoise realisation of the same step (its modes times (1400 MHz / f_bary)^2), n_i per
- * instance: Residuals.noise_resids["pl_DM_noise"] (zeros for pulsars without PLDMNoise). */
+ * instance: Residuals.noise_resids["pl_DM_noise"] (zeros for pulsars without PLDMNoise).  In
+ * lazy mode it is enqueued on the copy stream like pint_noise_resids (dm valid after
+ * pint_check / pint_check_step; the next evaluation with M waits for it). */
 int pint_noise_resids_dm(pint_ctx *ctx, double *dm);
 
 /* Device time (ms, HIP events on the streams the kernels run on) of the last launches, 8

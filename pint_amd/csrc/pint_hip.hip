@@ -3995,6 +3995,7 @@ struct pint_ctx {
     double *d_dpars_s[2] = {nullptr, nullptr}, *d_errs_s[2] = {nullptr, nullptr}, *d_cov_s[2] = {nullptr, nullptr};
     double *d_chi2lin_s[2] = {nullptr, nullptr}, *d_xw_s[2] = {nullptr, nullptr}, *d_chi2g_s[2] = {nullptr, nullptr};
     bool copy_pend[2] = {false, false};
+    bool dm_noise_pend = false;  // a copy-stream PLDMNoise realisation still reads d_dfac (lazy)
     int out_slot = -1;
     bool wfuse = false;            // the batch takes the fused Woodbury dots (k_resid2 tiles)
     bool wtile_valid = false;      // d_wpart holds the current residuals' dots (one split)
@@ -5041,6 +5042,10 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         write_red = ctx->red_valid[want_M == 2] ? 0 : 1;
         ctx->red_valid[want_M == 2] = 1;
         ctx->red_valid[want_M != 2] = 0;  // the other layout's red columns get overwritten
+        if (ctx->dm_noise_pend) {  // the evaluation with M rewrites the DM-noise scale d_dfac
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
+            ctx->dm_noise_pend = false;
+        }
     }
     record(ctx, want_M ? 2 : 0);
     if (!ctx->ic_valid) {  // k_apply refreshes them itself
@@ -5950,7 +5955,7 @@ int pint_inst_status(pint_ctx* ctx, int32_t* out) {
 int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
-    const long need = 2 * std::max<long>(1, ctx->tot_out);
+    const long need = 3 * std::max<long>(1, ctx->tot_out);  // red, ECORR, DM noise
     if (need > ctx->noise_cap) {
         if (ctx->capturing) { ctx->err = "pint_noise_resids: first call inside a graph capture"; return PINT_E_INVALID; }
         dfree((void*&)ctx->d_noise);
@@ -5993,20 +5998,35 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
 int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
     if (!ctx || ctx->ninst <= 0 || !dm) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
-    double* d = nullptr;
-    HIPCHK(hipMalloc(&d, sizeof(double) * std::max<long>(1, ctx->tot_out)));
+    const long need = 3 * std::max<long>(1, ctx->tot_out);
+    if (need > ctx->noise_cap) {
+        if (ctx->capturing) { ctx->err = "pint_noise_resids_dm: first call inside a graph capture"; return PINT_E_INVALID; }
+        dfree((void*&)ctx->d_noise);
+        HIPCHK(cmalloc((void**)&ctx->d_noise, sizeof(double) * need));
+        ctx->noise_cap = need;
+    }
+    double* d = ctx->d_noise + 2 * std::max<long>(1, ctx->tot_out);
     int maxn = 1;
     for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
-    hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
+    // lazy: on the copy stream after the solve, like pint_noise_resids; the next evaluation
+    // with M (which rewrites the per-TOA DM-noise scale d_dfac) waits for it
+    hipStream_t st = ctx->stream;
+    if (ctx->lazy) {
+        st = ctx->cstream;
+        HIPCHK(hipStreamWaitEvent(st, ctx->ev_solved, 0));
+    }
+    hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, st, ctx->d_psrs,
                        ctx->d_inst, ctx->d_dpars, d, 1, ctx->d_dfac);
-    int rc = PINT_OK;
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(dm, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-        rc = PINT_E_HIP;
-    hipStreamSynchronize(ctx->stream);
-    hipFree(d);
-    if (rc) ctx->err = "pint_noise_resids_dm: HIP error";
-    return rc;
+    if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids_dm: launch failed"; return PINT_E_HIP; }
+    HIPCHK(hipMemcpyAsync(dm, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
+    if (ctx->lazy) {
+        HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
+        ctx->copy_pend[ctx->slot] = true;
+        ctx->dm_noise_pend = true;
+        return PINT_OK;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return PINT_OK;
 }
 
 // Parity introspection: the assembled normal matrix of the last pint_fit_step (see

@@ -835,8 +835,7 @@ class Session:
         n = [l.n for l in self.inst_layout]
         anyred = any(l.spec.dmn0 > 0 for l in self.inst_layout)
         anyec = any("EcorrNoise" in l.model.components for l in self.inst_layout)
-        if self.lazy and any(l.spec.dmn0 < l.nred for l in self.inst_layout):
-            raise NotImplementedError("lazy noise_resids: PLDMNoise realisations need a synchronous session")
+        anydm = any(l.spec.dmn0 < l.nred for l in self.inst_layout)
         if self.lazy:
             # enqueued (kernels after the solve, copies on the copy stream into pinned
             # buffers): the arrays handed out are complete after check()/check_step()
@@ -847,10 +846,13 @@ class Session:
             ec = np.empty(sum(n)) if anyec else None
         self._check(self.L.pint_noise_resids(self.ctx, L.ptr(red), L.ptr(ec)))
         if self.lazy:
-            return _NoiseViews(self.inst_layout, self._off_n, red if anyred else None, ec if anyec else None)
+            dm = None
+            if anydm:  # PLDMNoise: enqueued on the copy stream as well (pint_noise_resids_dm)
+                dm = self._pin("noise_dm", sum(n))
+                self._check(self.L.pint_noise_resids_dm(self.ctx, L.ptr(dm)))
+            return _NoiseViews(self.inst_layout, self._off_n, red if anyred else None, ec if anyec else None, dm)
         red = red if red is not None else np.zeros(sum(n))
         ec = ec if ec is not None else np.zeros(sum(n))
-        anydm = any(l.spec.dmn0 < l.nred for l in self.inst_layout)
         dm = np.zeros(sum(n))
         if anydm:
             self._check(self.L.pint_noise_resids_dm(self.ctx, L.ptr(dm)))
@@ -947,9 +949,9 @@ def release_cache():
 class _NoiseViews(SplitView):
     """Per-instance {component: n-array} views of the noise realisations (lazy sessions)."""
 
-    def __init__(self, lays, off, red, ec):
+    def __init__(self, lays, off, red, ec, dm=None):
         super().__init__(None, off)
-        self.lays, self.red, self.ec = lays, red, ec
+        self.lays, self.red, self.ec, self.dm = lays, red, ec, dm
 
     def __getitem__(self, k):
         if isinstance(k, slice):
@@ -962,6 +964,8 @@ class _NoiseViews(SplitView):
             d["ecorr_noise"] = self.ec[a:b]
         if self.red is not None and lay.spec.dmn0 > 0:
             d["pl_red_noise"] = self.red[a:b]
+        if self.dm is not None and lay.spec.dmn0 < lay.nred:
+            d["pl_DM_noise"] = self.dm[a:b]
         return d
 
 

@@ -176,6 +176,9 @@ def test_gls_fit(name):
         # has cond 7e12 (B1855 with the dense ECORR block 1e16, 3e11 after elimination),
         # so its weakest-determined errors agree with the reference's LAPACK to ~1e-3
         # (measured on MI355X, scripts/diag/downhill_margin.py: J0740 JUMP1 1.3e-3, B1855 T0 1.2e-4)
+        # (bars between each fixture's solver floor and its 1e-13 Gram-precision floor,
+        # tests/golden/cov_floor.json: J0740 2.8e-5 .. 0.13, B1855 1.1e-5 .. 0.018; the PTA
+        # fixtures' Gram floor is <= 9e-10, so 1e-5 is their solver/rounding allowance)
         etol = {"j0740": 3e-3, "b1855": 5e-4}.get(name, 1e-5)
         assert abs(f.model[p].uncertainty / s - 1) < etol, (p, f.model[p].uncertainty / s - 1)
     assert worst < 1e-3, worst
@@ -806,6 +809,51 @@ def test_pldm_noise_resids():
         err = np.max(np.abs(f.resids.noise_resids[comp] - v)) / np.max(np.abs(v))
         # end to end, the realisations carry the step's conditioning (cf. TOL_NOISE, test_gpu_stage.py)
         assert err < 1e-4, (comp, err)
+
+
+def test_pldm_noise_resids_lazy_pipelined():
+    """PLDMNoise realisations in a lazy, pipelined session (the bench's step shape: the
+    realisations enqueued on the copy stream, pint_noise_resids_dm) equal the synchronous
+    session's bit for bit, over two steps in flight, with a PLRedNoise-only pulsar beside."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load("pta_dmn")[:2], load("pta_iso")[:2]]
+
+    def fresh():
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        return s
+
+    s0 = fresh()
+    s0.eval(want_M=Session.FIT)
+    s0.fit_step(1)
+    want = s0.noise_resids()
+    s0.close()
+    s = fresh()
+    s.save_tables()
+    s.set_lazy(True)
+    got, prev = [], None
+    for _ in range(3):
+        s.restore_tables()
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        nz = s.noise_resids()
+        s.apply_step_uniform(1.0)
+        s.eval(want_M=False)
+        slot = s.step_end()
+        if prev is not None:
+            s.check_step(prev[0])
+            got.append([{k: v.copy() for k, v in d.items()} for d in prev[1]])
+        prev = (slot, nz)
+    s.check_step(prev[0])
+    got.append([{k: v.copy() for k, v in d.items()} for d in prev[1]])
+    s.close()
+    assert set(want[0]) == {"pl_red_noise", "pl_DM_noise"} and "pl_DM_noise" not in want[1]
+    for g in got:
+        for k in range(2):
+            assert set(g[k]) == set(want[k])
+            for comp in want[k]:
+                assert np.array_equal(g[k][comp], want[k][comp]), comp
 
 
 @pytest.mark.gpu

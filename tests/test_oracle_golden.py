@@ -251,3 +251,17 @@ def test_lnlikelihood(fx):
     ref = meta["res_lnlikelihood"]
     # chi2/2 carries the oracle-vs-reference residual floor (<= 1.2e-6 relative, pta_ell1)
     assert abs(ll - ref) <= 1e-6 * abs(meta["res_chi2"]) + 1e-9 * abs(ref), (ll, ref)
+
+
+def test_covariance_floors_bracket_the_bars():
+    """tests/golden/cov_floor.json (oracle/cov_floor.py, from the reference's recorded normal
+    matrices): the GPU tests' uncertainty / correlation bars of the ill-conditioned fixtures
+    lie between the reference's own solver error and the spread a 1e-13 Gram difference
+    implies; the well-conditioned PTA fixtures' whole floor is far below their 1e-5 bar."""
+    d = json.load(open(os.path.join(GOLDEN, "cov_floor.json")))
+    for name, (ebar, cbar) in {"j0740": (3e-3, 5e-3), "b1855": (5e-4, 5e-3)}.items():
+        f = d[name]
+        assert 2 * f["solver_err_rel"] < ebar < f["gram_err_rel"], (name, f)
+        assert 2 * f["solver_corr_abs"] < cbar, (name, f)
+    for name in ("pta_iso", "pta_ell1", "pta_dd"):
+        assert d[name]["solver_err_rel"] + d[name]["gram_err_rel"] < 1e-8
