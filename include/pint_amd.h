@@ -169,7 +169,8 @@ int pint_eval(pint_ctx *ctx, int want_M);  /* want_M: 0 none, 1 full, 2 fit layo
 
 /* Copy results to caller buffers (any pointer may be NULL).  Residual rows are n_i per
  * instance, eval rows n_i+1 (last = TZR TOA), design matrices n_i x K_i column-major
- * with K_i = ncol + 2*nred. */
+ * with K_i = ncol + 2*nred.  pint_read_resids in lazy mode only enqueues its copies (pinned
+ * buffers, valid after pint_check). */
 int pint_read_resids(pint_ctx *ctx, double *time_resid, double *phase_resid, double *chi2_wls);
 int pint_read_eval(pint_ctx *ctx, double *phase_hi, double *phase_lo, double *ftaylor, double *delay);
 int pint_read_designmatrix(pint_ctx *ctx, double *M);

@@ -5144,7 +5144,7 @@ int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, dou
     if (time_resid) HIPCHK(hipMemcpyAsync(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (phase_resid) HIPCHK(hipMemcpyAsync(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
     if (chi2) HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));  // lazy: valid after pint_check
     return PINT_OK;
 }
 

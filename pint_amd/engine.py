@@ -653,8 +653,9 @@ class Session:
         return self._split(r, n), c2
 
     def read_chi2(self):
-        """WLS chi2 per instance only (no residual rows copied back)."""
-        c2 = np.empty(len(self.inst_layout))
+        """WLS chi2 per instance only (no residual rows copied back); lazy: a pinned buffer
+        that is complete after check()."""
+        c2 = self._pin("chi2r", len(self.inst_layout)) if self.lazy else np.empty(len(self.inst_layout))
         self._check(self.L.pint_read_resids(self.ctx, None, None, L.ptr(c2)))
         return c2
 
@@ -731,9 +732,11 @@ class Session:
         return int(self.L.pint_query(self.ctx, 2))
 
     def check(self):
-        self._check(self.L.pint_check(self.ctx))
-        self._inflight.clear()
-        self._keep.clear()
+        try:
+            self._check(self.L.pint_check(self.ctx))
+        finally:  # synchronised either way: the staging buffers are free again
+            self._inflight.clear()
+            self._keep.clear()
 
     # -- pipelined steps (lazy mode) ------------------------------------------------
     def step_end(self) -> int:

@@ -190,15 +190,23 @@ class BatchFit:
 
     # -- helpers ------------------------------------------------------------------------
     def _chi2_now(self):
-        if all(self.use_gls_chi2):
-            c2 = self.s.chi2_gls()
-        else:
-            c2 = self.s.read_chi2()
-            if any(self.use_gls_chi2):
-                c2 = np.where(self.use_gls_chi2, self.s.chi2_gls(), c2)
+        c2, _ = self._chi2_enqueue()()
         if self.wideband:  # WidebandTOAResiduals.chi2 = the TOA chi2 + the DM chi2 (residuals.py:1206)
             c2 = c2 + self.s.dm_resids()[1]
         return c2, None
+
+    def _chi2_enqueue(self):
+        """Enqueue the chi2 reads of the current residuals; returns a function giving the
+        per-instance chi2 (after check() in lazy mode, where the reads land in pinned
+        buffers)."""
+        if all(self.use_gls_chi2):
+            cg = self.s.chi2_gls()
+            return lambda: (np.array(cg, dtype=np.float64), None)
+        cw = self.s.read_chi2()
+        cg = self.s.chi2_gls() if any(self.use_gls_chi2) else None
+        if cg is None:
+            return lambda: (np.array(cw, dtype=np.float64), None)
+        return lambda: (np.where(self.use_gls_chi2, cg, cw), None)
 
     def _step(self):
         keep = self._eval(Session.FIT)
@@ -396,22 +404,38 @@ class BatchFit:
             dec = np.zeros(n)
             newbest = np.zeros(n, dtype=bool)
             while not decided.all():
-                self.s.restore_tables()
-                applied = np.where(decided, acc_lam, lam)
-                if single:
-                    self.s.apply_step_uniform(float(applied[0]))
-                else:
-                    self.s.apply_step(applied)
-                bad = np.zeros(n, dtype=bool)
+                # one trial: enqueued lazily (restore, lambda x step, evaluation, chi2) and
+                # synchronised once; an instance whose evaluation raised a status is a rejected
+                # trial (wideband: the DM chi2 read is synchronous, so the trial is too)
+                lazy = not self.wideband
+                if lazy:
+                    self.s.set_lazy(True)
                 try:
-                    self.s.eval(want_M=False)
-                except L.PintError as e:
-                    if e.code not in self.EVAL_ERRORS:
-                        raise
-                    bad = self.s.inst_status() != 0
-                    if not bad.any():
-                        raise
-                new_chi2, _ = self._chi2_now()
+                    self.s.restore_tables()
+                    applied = np.where(decided, acc_lam, lam)
+                    if single:
+                        self.s.apply_step_uniform(float(applied[0]))
+                    else:
+                        self.s.apply_step(applied)
+                    bad = np.zeros(n, dtype=bool)
+                    try:
+                        self.s.eval(want_M=False)
+                        if lazy:
+                            got = self._chi2_enqueue()
+                            self.s.check()
+                            new_chi2, _ = got()
+                        else:
+                            new_chi2, _ = self._chi2_now()
+                    except L.PintError as e:
+                        if e.code not in self.EVAL_ERRORS:
+                            raise
+                        bad = self.s.inst_status() != 0
+                        if not bad.any():
+                            raise
+                        new_chi2, _ = got() if lazy else self._chi2_now()
+                finally:
+                    if lazy:
+                        self.s.set_lazy(False)
                 new_chi2 = np.where(bad, np.nan, np.array(new_chi2, dtype=np.float64))
                 und = ~decided
                 d = cur_chi2 - new_chi2
