@@ -8,10 +8,13 @@ device's double-double -- give time residuals that differ by a few to a few tens
 such residuals moves with them, by an amount that depends on the fixture (TOA errors, count,
 correlated noise).  This script measures that for the reference itself: every time residual
 it computes (Residuals.calc_time_resids, residuals.py:483) is shifted by a fixed per-TOA
-N(0, sigma_p) draw (seeds 1..NREP; sigma_p = 5 ps, the longdouble floor, and 30 ps, the
-residual tests' rms bar), and the pre-fit Residuals chi2, the GLSFitter / WLSFitter
-fit_toas(maxiter=1) chi2 and (for the Downhill fixtures) the DownhillGLSFitter chi2 are
-recorded as max |chi2 / chi2_0 - 1|.
+pattern of rms sigma_p (5 ps, the longdouble floor, and 30 ps, the residual tests' rms bar),
+and the pre-fit Residuals chi2, the GLSFitter / WLSFitter fit_toas(maxiter=1) chi2 and (for
+the Downhill fixtures) the DownhillGLSFitter chi2 are recorded as max |chi2 / chi2_0 - 1|.
+The patterns are NREP independent N(0, sigma_p) draws and, because two evaluations' residual
+differences are not independent per TOA (they follow the TOA epoch and frequency), four
+structured ones of the same rms: sinusoids in time over the data span, a third of it and one
+year (random phase), and a dispersive (1400 MHz / f)^2 pattern with zero weighted mean.
 
 The (model, TOAs) of each fixture are rebuilt by its own generator (gen_synth, gen_phoff,
 gen_stage.rebuild), whose capture() is intercepted, and checked bit-for-bit against the
@@ -128,6 +131,22 @@ def check_same(name, toas):
     assert np.array_equal(np.asarray(toas.table["tdbld"], dtype=np.float64), base["tdb_hi"]), f"{name}: TOAs differ"
 
 
+def patterns(toas):
+    """Unit-rms residual shift patterns: NREP N(0, 1) draws, then the structured ones."""
+    out = [np.random.default_rng(rep).normal(0.0, 1.0, toas.ntoas) for rep in range(1, NREP + 1)]
+    t = np.asarray(toas.table["tdbld"], dtype=np.float64)
+    span = max(t.max() - t.min(), 1.0)
+    rng = np.random.default_rng(100)
+    for per in (span, span / 3.0, 365.25):
+        p = np.sin(2 * np.pi * (t - t.min()) / per + rng.uniform(0, 2 * np.pi))
+        out.append(p / np.sqrt(np.mean(p * p)))
+    f = np.asarray(toas.table["freq"].to_value(u.MHz), dtype=np.float64)
+    p = (1400.0 / np.where(np.isfinite(f) & (f > 0), f, 1400.0)) ** 2
+    p = p - np.mean(p)
+    out.append(p / np.sqrt(np.mean(p * p)) if np.any(p) else out[0])
+    return out
+
+
 def measure(model, toas, fit, down):
     fcls = pfit.GLSFitter if fit == "gls" else pfit.WLSFitter
     keys = ("pre", "fit", "down", "post")
@@ -164,8 +183,8 @@ def measure(model, toas, fit, down):
     try:
         for key, sig in LEVELS.items():
             worst = {k: (0.0 if v is not None else None) for k, v in zip(keys, base)}
-            for rep in range(1, NREP + 1):
-                shift = np.random.default_rng(rep).normal(0.0, sig, toas.ntoas) * u.s
+            for rep, pat in enumerate(patterns(toas), start=1):
+                shift = pat * sig * u.s
 
                 def calc(self, *a, **k):
                     return orig(self, *a, **k) + shift

@@ -1105,6 +1105,36 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         for (int k = S.nfd; k >= 1; k--) fd = fd * logf + pval(P, S.o_FD + 2 * (k - 1));
         fd *= logf;
     }
+    // ---- astrometric design-matrix geometry (astrometry.py:186-212 get_d_delay_quantities),
+    //      formed here without the chain factor so that the TOA's position, velocity and Sun
+    //      vectors and the pulsar direction die before the binary state is set up (the
+    //      binary columns are written while that state is live: the register peak) ----
+    double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
+    if (Mb && S.astrometry) {
+        // Earth direction angles (era, edec) of the SSB->observatory vector enter only as
+        // cos(edec) sin(plon - era), cos(edec) cos(plon - era) and sin(edec): formed from
+        // the vector itself, cos(edec) cos(era) = x/r etc. (no atan2/sin/cos per TOA)
+        double u[3] = {t.pos[0], t.pos[1], t.pos[2]};
+        if (S.astrometry == 2) {
+            // earth ecliptic lon/lat via ICRS->PulsarEcliptic (astrometry.py:1034-1055)
+            double ue[3] = {u[0], u[1], u[2]};
+            icrs_to_ecl(S.obliquity, ue, u);
+        }
+        const double r_km = sqrt(rr);
+        const double ir = r_km > 0.0 ? 1.0 / r_km : 0.0;
+        const double ced_sdl = (C.splon * u[0] - C.cplon * u[1]) * ir;
+        const double ced_cdl = (C.cplon * u[0] + C.splon * u[1]) * ir;
+        const double sed = u[2] * ir;
+        const double te_s = S.o_POSEPOCH >= 0 ? dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC)) : 0.0;
+        const double rc = r_km * INV_C_KMS;
+        // d_delay_astrometry_d_RAJ / _ELONG, _DECJ / _ELAT, PM partials x te (astrometry.py:536-627, 1067-1170)
+        gLON = rc * (ced_sdl * C.cplat) * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
+        gLAT = rc * (ced_cdl * C.splat - sed * C.cplat) * DEG_RAD;
+        gPMLON = rc * ced_sdl * te_s * MASYR_RADS;
+        gPMLAT = rc * (ced_cdl * C.splat - C.cplat * sed) * te_s * MASYR_RADS;
+        // d_delay_astrometry_d_PX (astrometry.py:219-249)
+        gPX = 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
+    }
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
     BinState B;
     B.status = 0;
@@ -1172,33 +1202,12 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     if (!Mb) return;
     // ---- design matrix row (timing_model.py:2073-2175) ----
     const double iF0 = C.iF0;
-    // astrometric geometry (astrometry.py:186-212 get_d_delay_quantities), once per TOA
-    double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
-    if (S.astrometry) {
-        // Earth direction angles (era, edec) of the SSB->observatory vector enter only as
-        // cos(edec) sin(plon - era), cos(edec) cos(plon - era) and sin(edec): formed from
-        // the vector itself, cos(edec) cos(era) = x/r etc. (no atan2/sin/cos per TOA)
-        double u[3] = {t.pos[0], t.pos[1], t.pos[2]};
-        if (S.astrometry == 2) {
-            // earth ecliptic lon/lat via ICRS->PulsarEcliptic (astrometry.py:1034-1055)
-            double ue[3] = {u[0], u[1], u[2]};
-            icrs_to_ecl(S.obliquity, ue, u);
-        }
-        const double r_km = sqrt(rr);
-        const double ir = r_km > 0.0 ? 1.0 / r_km : 0.0;
-        const double ced_sdl = (C.splon * u[0] - C.cplon * u[1]) * ir;
-        const double ced_cdl = (C.cplon * u[0] + C.splon * u[1]) * ir;
-        const double sed = u[2] * ir;
-        const double te_s = S.o_POSEPOCH >= 0 ? dd_to_d(dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_POSEPOCH)), DAYSEC)) : 0.0;
-        const double rc = chain * r_km * INV_C_KMS;
-        // d_delay_astrometry_d_RAJ / _ELONG, _DECJ / _ELAT, PM partials x te (astrometry.py:536-627, 1067-1170)
-        gLON = rc * (ced_sdl * C.cplat) * (S.astrometry == 1 ? HA_RAD : DEG_RAD);
-        gLAT = rc * (ced_cdl * C.splat - sed * C.cplat) * DEG_RAD;
-        gPMLON = rc * ced_sdl * te_s * MASYR_RADS;
-        gPMLAT = rc * (ced_cdl * C.splat - C.cplat * sed) * te_s * MASYR_RADS;
-        // d_delay_astrometry_d_PX (astrometry.py:219-249)
-        gPX = chain * 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
-    }
+    // the astrometric geometry formed above, times the chain factor
+    gLON *= chain;
+    gLAT *= chain;
+    gPMLON *= chain;
+    gPMLAT *= chain;
+    gPX *= chain;
     const double dmc = chain * DMCONST * inv_f2;
     o.dmc = dmc;
     for (int u = 0; u < nrun; u++) {

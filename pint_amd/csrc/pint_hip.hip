@@ -2440,14 +2440,15 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     // known every later row subtracts its term, so the dependent chain is two operations
     // per row instead of a t-term dot product per row (the same subtraction order, u
     // ascending, hence the same rounding)
-    double x[16], s[16];
+    // (x[u] overwrites s[u] in place: s[u] is dead once x[u] is formed)
+    double x[16];
 #pragma unroll
-    for (int t = 0; t < 16; t++) s[t] = (r == t) ? 1.0 : 0.0;
+    for (int t = 0; t < 16; t++) x[t] = (r == t) ? 1.0 : 0.0;
 #pragma unroll
     for (int u = 0; u < 16; u++) {
-        x[u] = s[u] * ril[u];
+        x[u] *= ril[u];
 #pragma unroll
-        for (int t = u + 1; t < 16; t++) s[t] -= rdlane(a[u], t) * x[u];
+        for (int t = u + 1; t < 16; t++) x[t] -= rdlane(a[u], t) * x[u];
     }
     if (lane < 16) {
 #pragma unroll
@@ -2892,29 +2893,62 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     }
     __syncthreads();
     // ---- build S = A_dd, U = A_dx D^-1/2, b_d ----
-    for (int e = tid; e < nblkS * 256; e += NW * 64) {
-        int Ib, Jb;
-        tri_decode(e >> 8, Ib, Jb);
-        const int r = e & 15, c = (e >> 4) & 15;
-        const int gi = Ib * 16 + r, gj = Jb * 16 + c;
-        double v;
-        if (gi < Kd && gj < Kd) {
-            const double ni = ind[gi], nj = ind[gj];
-            v = Gd(gi, gj) * (ni * nj);
-            if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
-        } else {
-            v = (gi == gj) ? 1.0 : 0.0;
+    // (each thread's Gram and DMX-row loads issued together, SB at a time, before their LDS
+    // stores: one global-load latency per round instead of one per element)
+    constexpr int SB = 8;
+    for (int e0 = tid; e0 < nblkS * 256; e0 += NW * 64 * SB) {
+        double g[SB];
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int e = e0 + u * NW * 64;
+            g[u] = 0.0;
+            if (e < nblkS * 256) {
+                int Ib, Jb;
+                tri_decode(e >> 8, Ib, Jb);
+                const int gi = Ib * 16 + (e & 15), gj = Jb * 16 + ((e >> 4) & 15);
+                if (gi < Kd && gj < Kd) g[u] = Gd(gi, gj);
+            }
         }
-        A[((e >> 8) << 8) + swz(r, c)] = v;
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int e = e0 + u * NW * 64;
+            if (e >= nblkS * 256) break;
+            int Ib, Jb;
+            tri_decode(e >> 8, Ib, Jb);
+            const int r = e & 15, c = (e >> 4) & 15;
+            const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+            double v;
+            if (gi < Kd && gj < Kd) {
+                const double ni = ind[gi], nj = ind[gj];
+                v = g[u] * (ni * nj);
+                if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
+            } else {
+                v = (gi == gj) ? 1.0 : 0.0;
+            }
+            A[((e >> 8) << 8) + swz(r, c)] = v;
+        }
     }
     __syncthreads();
-    for (int e = tid; e < nbd * nbk * 256; e += NW * 64) {
-        const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
-        const int r = e & 15, c = (e >> 4) & 15;
-        const int gi = Ib * 16 + r, a = kb * 16 + c;
-        double v = 0.0;
-        if (gi < Kd && a < ndc) v = Sdi[(long)a * Kp + gi] * (ind[gi] * inx[a]) * isd[a];
-        A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = v;
+    for (int e0 = tid; e0 < nbd * nbk * 256; e0 += NW * 64 * SB) {
+        double g[SB];
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int e = e0 + u * NW * 64;
+            const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+            const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
+            g[u] = (e < nbd * nbk * 256 && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int e = e0 + u * NW * 64;
+            if (e >= nbd * nbk * 256) break;
+            const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+            const int r = e & 15, c = (e >> 4) & 15;
+            const int gi = Ib * 16 + r, a = kb * 16 + c;
+            double v = 0.0;
+            if (gi < Kd && a < ndc) v = g[u] * (ind[gi] * inx[a]) * isd[a];
+            A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = v;
+        }
     }
     for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) * ind[c] : 0.0;
     const double rwr = Gd(Kres, Kres);

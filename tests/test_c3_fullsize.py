@@ -31,8 +31,10 @@ def _bar(meta, key, floor):
 
 
 def test_fixture_takes_the_bench_c3_path(fx):
-    """Same compact layout, vg path and binned-tile choice as the bench's 50k-TOA C3 pulsar
-    (bench.py j0740_data), in one session (one N-split for both)."""
+    """Same compact layout, vg path, binned-tile choice and k_gram_v instantiation <NTR, NTC>
+    as the bench's 50k-TOA C3 pulsar (bench.py j0740_data), in one session (one N-split for
+    both).  The column counts differ by the empty masks each TOA set freezes (the 10k
+    reference TOAs leave 50 DMX bins and one more timing column free, the 50k ones 54)."""
     import sys
     import os
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -50,9 +52,10 @@ def test_fixture_takes_the_bench_c3_path(fx):
     finally:
         s.close()
     print(f"fixture fit_layout {ff} vgram {vf}; bench {fb} {vb}")
-    assert ff[:3] == fb[:3]                       # compact, Gram columns, DMX columns
-    assert (vf[0], vf[3]) == (vb[0], vb[3])       # vg (+ binned tile) flags, compact timing columns
-    assert vf[0] & 1
+    assert ff[0] == fb[0] == 1                    # compact fit layout
+    assert vf[0] == vb[0] and vf[0] & 1           # vg path, binned-tile flag
+    inst = [((v[3] + 1 + v[1]) // 16, v[2] // 16) for v in (vf, vb)]
+    assert inst[0] == inst[1], inst               # the same k_gram_v<NTR, NTC, VB> instantiation
 
 
 def test_gls_fit_10k(fx):
