@@ -140,7 +140,7 @@ def patterns(toas):
     for per in (span, span / 3.0, 365.25):
         p = np.sin(2 * np.pi * (t - t.min()) / per + rng.uniform(0, 2 * np.pi))
         out.append(p / np.sqrt(np.mean(p * p)))
-    f = np.asarray(toas.table["freq"].to_value(u.MHz), dtype=np.float64)
+    f = np.asarray(toas.get_freqs().to_value(u.MHz), dtype=np.float64)
     p = (1400.0 / np.where(np.isfinite(f) & (f > 0), f, 1400.0)) ** 2
     p = p - np.mean(p)
     out.append(p / np.sqrt(np.mean(p * p)) if np.any(p) else out[0])

@@ -2420,35 +2420,43 @@ __device__ double block_max(double v, double* sh) {
 // r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
 // the block is overwritten by L^-1 (zeros above the diagonal).  Returns false if not
 // positive definite.
+// 1/sqrt(d) as v_rsq_f64 + two Newton steps: within 1 ulp like the library rsqrt (max 0.993
+// vs 0.987 ulp over 1e6 pivots in (1e-8, 4]) at 52 instead of 67 cycles of dependent latency
+// (bench/rsq_probe.hip); the Cholesky pivot chain is serial, so the latency is what counts
+__device__ __forceinline__ double rsq2(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
+    return __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
+}
+
 __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
-    double a[16], ril[16];
+    // Cholesky (lane r holds row r) and X = L^-1 (lane r its column r) in one pass: pivot j's
+    // column L[c][j] is broadcast once (v_readlane) and used by both the trailing update of A
+    // and the forward substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the
+    // same operations and rounding as a separate substitution after the factorisation, with
+    // half the lane reads)
+    double a[16], x[16];
 #pragma unroll
-    for (int c = 0; c < 16; c++) a[c] = Akk[swz(r, c)];
+    for (int c = 0; c < 16; c++) {
+        a[c] = Akk[swz(r, c)];
+        x[c] = (r == c) ? 1.0 : 0.0;
+    }
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
-        const double il = rsqrt(djj);
-        ril[j] = il;
+        const double il = rsq2(djj);
         a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
+        x[j] *= il;
 #pragma unroll
-        for (int c = j + 1; c < 16; c++) a[c] -= a[j] * rdlane(a[j], c);
-    }
-    // X = L^-1 by forward substitution, lane r its column r, in axpy order: once x[u] is
-    // known every later row subtracts its term, so the dependent chain is two operations
-    // per row instead of a t-term dot product per row (the same subtraction order, u
-    // ascending, hence the same rounding)
-    // (x[u] overwrites s[u] in place: s[u] is dead once x[u] is formed)
-    double x[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) x[t] = (r == t) ? 1.0 : 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-        x[u] *= ril[u];
-#pragma unroll
-        for (int t = u + 1; t < 16; t++) x[t] -= rdlane(a[u], t) * x[u];
+        for (int c = j + 1; c < 16; c++) {
+            const double Lcj = rdlane(a[j], c);
+            a[c] -= a[j] * Lcj;
+            x[c] -= Lcj * x[j];
+        }
     }
     if (lane < 16) {
 #pragma unroll
@@ -2868,6 +2876,31 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
     TS(0);
+    // ---- loads first: each thread's Gram (S) and DMX-row (U) elements are issued before the
+    //      norms and held in registers across them, so building S and U costs one global-load
+    //      latency instead of one per phase (systems larger than RS / RU elements per thread
+    //      load the rest in the tail loops) ----
+    constexpr int RS = 4, RU = 12;
+    const int nS = nblkS * 256, nU = nbd * nbk * 256;
+    double gS[RS], gU[RU];
+#pragma unroll
+    for (int u = 0; u < RS; u++) {
+        const int e = tid + u * NW * 64;
+        gS[u] = 0.0;
+        if (e < nS) {
+            int Ib, Jb;
+            tri_decode(e >> 8, Ib, Jb);
+            const int gi = Ib * 16 + (e & 15), gj = Jb * 16 + ((e >> 4) & 15);
+            if (gi < Kd && gj < Kd) gS[u] = Gd(gi, gj);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+        const int e = tid + u * NW * 64;
+        const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+        const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
+        gU[u] = (e < nU && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
+    }
     // ---- column norms (utils.py:2879: zero norm -> 1), b_x, D (normalised) ----
     for (int c = tid; c < nbd * 16; c += NW * 64) {
         double v = 1.0;
@@ -2893,62 +2926,43 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     }
     __syncthreads();
     // ---- build S = A_dd, U = A_dx D^-1/2, b_d ----
-    // (each thread's Gram and DMX-row loads issued together, SB at a time, before their LDS
-    // stores: one global-load latency per round instead of one per element)
-    constexpr int SB = 8;
-    for (int e0 = tid; e0 < nblkS * 256; e0 += NW * 64 * SB) {
-        double g[SB];
-#pragma unroll
-        for (int u = 0; u < SB; u++) {
-            const int e = e0 + u * NW * 64;
-            g[u] = 0.0;
-            if (e < nblkS * 256) {
-                int Ib, Jb;
-                tri_decode(e >> 8, Ib, Jb);
-                const int gi = Ib * 16 + (e & 15), gj = Jb * 16 + ((e >> 4) & 15);
-                if (gi < Kd && gj < Kd) g[u] = Gd(gi, gj);
-            }
+    auto put_S = [&](int e, double g) {
+        int Ib, Jb;
+        tri_decode(e >> 8, Ib, Jb);
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+        double v;
+        if (gi < Kd && gj < Kd) {
+            const double ni = ind[gi], nj = ind[gj];
+            v = g * (ni * nj);
+            if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
+        } else {
+            v = (gi == gj) ? 1.0 : 0.0;
         }
+        A[((e >> 8) << 8) + swz(r, c)] = v;
+    };
+    auto put_U = [&](int e, double g) {
+        const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+        const int r = e & 15, c = (e >> 4) & 15;
+        const int gi = Ib * 16 + r, a = kb * 16 + c;
+        A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = (gi < Kd && a < ndc) ? g * (ind[gi] * inx[a]) * isd[a] : 0.0;
+    };
 #pragma unroll
-        for (int u = 0; u < SB; u++) {
-            const int e = e0 + u * NW * 64;
-            if (e >= nblkS * 256) break;
-            int Ib, Jb;
-            tri_decode(e >> 8, Ib, Jb);
-            const int r = e & 15, c = (e >> 4) & 15;
-            const int gi = Ib * 16 + r, gj = Jb * 16 + c;
-            double v;
-            if (gi < Kd && gj < Kd) {
-                const double ni = ind[gi], nj = ind[gj];
-                v = g[u] * (ni * nj);
-                if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
-            } else {
-                v = (gi == gj) ? 1.0 : 0.0;
-            }
-            A[((e >> 8) << 8) + swz(r, c)] = v;
-        }
+    for (int u = 0; u < RS; u++)
+        if (tid + u * NW * 64 < nS) put_S(tid + u * NW * 64, gS[u]);
+    for (int e = tid + RS * NW * 64; e < nS; e += NW * 64) {  // tail
+        int Ib, Jb;
+        tri_decode(e >> 8, Ib, Jb);
+        const int gi = Ib * 16 + (e & 15), gj = Jb * 16 + ((e >> 4) & 15);
+        put_S(e, (gi < Kd && gj < Kd) ? Gd(gi, gj) : 0.0);
     }
-    __syncthreads();
-    for (int e0 = tid; e0 < nbd * nbk * 256; e0 += NW * 64 * SB) {
-        double g[SB];
 #pragma unroll
-        for (int u = 0; u < SB; u++) {
-            const int e = e0 + u * NW * 64;
-            const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
-            const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
-            g[u] = (e < nbd * nbk * 256 && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < SB; u++) {
-            const int e = e0 + u * NW * 64;
-            if (e >= nbd * nbk * 256) break;
-            const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
-            const int r = e & 15, c = (e >> 4) & 15;
-            const int gi = Ib * 16 + r, a = kb * 16 + c;
-            double v = 0.0;
-            if (gi < Kd && a < ndc) v = g[u] * (ind[gi] * inx[a]) * isd[a];
-            A[ublk(Ib, kb, nbk, nblkS) + swz(r, c)] = v;
-        }
+    for (int u = 0; u < RU; u++)
+        if (tid + u * NW * 64 < nU) put_U(tid + u * NW * 64, gU[u]);
+    for (int e = tid + RU * NW * 64; e < nU; e += NW * 64) {  // tail
+        const int blk = e >> 8, Ib = blk / nbk, kb = blk % nbk;
+        const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
+        put_U(e, (gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0);
     }
     for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) * ind[c] : 0.0;
     const double rwr = Gd(Kres, Kres);
@@ -3921,6 +3935,7 @@ struct pint_ctx {
     std::string err;
     std::vector<PsrHost> psrs;
     std::vector<int> setup_pending;  // pulsars whose red-noise set-up (k_trig_setup) is not run yet
+    bool psrs_dirty = false;         // d_psrs lags ctx->psrs (pulsars added since the last refresh)
     PsrDev* d_psrs = nullptr;
     int npsr_dev = 0;
     // instances
@@ -4222,7 +4237,33 @@ static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const 
     return 0;
 }
 
+// A pulsar's upload staged on the host: every array at a 256-byte aligned offset of one
+// buffer, then one device allocation and one copy (instead of an allocation and a
+// synchronous copy per array); the recorded pointer fields are set at commit.
+struct Arena {
+    std::vector<char> host;
+    std::vector<std::pair<size_t, const void**>> fix;
+    template <typename T>
+    int add(const T* src, size_t count, const T*& dst) {
+        const size_t off = (host.size() + 255) & ~(size_t)255;
+        const size_t bytes = std::max(count * sizeof(T), sizeof(T));
+        host.resize(off + bytes, 0);
+        if (src && count) memcpy(host.data() + off, src, count * sizeof(T));
+        fix.push_back({off, reinterpret_cast<const void**>(&dst)});
+        return 0;
+    }
+    int commit(pint_ctx* ctx, PsrHost& ph) {
+        void* p = nullptr;
+        HIPCHK(hipMalloc(&p, std::max<size_t>(host.size(), 256)));
+        HIPCHK(hipMemcpy(p, host.data(), host.size(), hipMemcpyHostToDevice));
+        ph.bufs.push_back(p);
+        for (auto& f : fix) *f.second = static_cast<const void*>(static_cast<char*>(p) + f.first);
+        return 0;
+    }
+};
+
 static int refresh_psrs(pint_ctx* ctx) {
+    ctx->psrs_dirty = false;
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
     ctx->d_psrs = nullptr;
     std::vector<PsrDev> all;
@@ -4368,16 +4409,17 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         return -PINT_E_INVALID;
     }
     PsrHost ph;
+    Arena ar;  // every array of the pulsar staged on the host, one allocation and one copy
     ph.spec = *spec;
     ph.n = n;
     ph.K = K;
     PsrDev& d = ph.dev;
     memset(&d, 0, sizeof(d));
     int rc = 0;
-    rc |= upload(ctx, ph, t->tdb_hi, n + 1, d.tdb_hi);
-    rc |= upload(ctx, ph, t->tdb_lo, n + 1, d.tdb_lo);
-    rc |= upload(ctx, ph, t->freq_mhz, n + 1, d.freq);
-    rc |= upload(ctx, ph, t->sigma_s, n, d.sigma);
+    rc |= ar.add(t->tdb_hi, n + 1, d.tdb_hi);
+    rc |= ar.add(t->tdb_lo, n + 1, d.tdb_lo);
+    rc |= ar.add(t->freq_mhz, n + 1, d.freq);
+    rc |= ar.add(t->sigma_s, n, d.sigma);
     {
         std::vector<double> is(n);
         double ls = 0.0, sw = 0.0;
@@ -4389,21 +4431,21 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         }
         d.logsig = ls;
         d.sumw = sw;
-        rc |= upload(ctx, ph, is.data(), n, d.isig);
+        rc |= ar.add(is.data(), n, d.isig);
     }
-    rc |= upload(ctx, ph, t->pos_km, 3 * (n + 1), d.pos);
-    rc |= upload(ctx, ph, t->vel_kms, 3 * (n + 1), d.vel);
-    rc |= upload(ctx, ph, t->sun_km, 3 * (n + 1), d.sun);
+    rc |= ar.add(t->pos_km, 3 * (n + 1), d.pos);
+    rc |= ar.add(t->vel_kms, 3 * (n + 1), d.vel);
+    rc |= ar.add(t->sun_km, 3 * (n + 1), d.sun);
     if (spec->shapiro == 2) {
         if (!t->planet_km) { ctx->err = "PLANET_SHAPIRO needs the planet positions (planet_km)"; return -PINT_E_INVALID; }
-        rc |= upload(ctx, ph, t->planet_km, (size_t)15 * (n + 1), d.planet);
+        rc |= ar.add(t->planet_km, (size_t)15 * (n + 1), d.planet);
     }
-    rc |= upload(ctx, ph, t->pulse_number, n, d.pn);
-    rc |= upload(ctx, ph, t->delta_pn, n + 1, d.dpn);
-    rc |= upload(ctx, ph, t->flags, n + 1, d.flags);
-    rc |= upload(ctx, ph, t->jump_mask, n + 1, d.jmask);
-    rc |= upload(ctx, ph, t->dmx_a, n + 1, d.dmx_a);
-    rc |= upload(ctx, ph, t->dmx_b, n + 1, d.dmx_b);
+    rc |= ar.add(t->pulse_number, n, d.pn);
+    rc |= ar.add(t->delta_pn, n + 1, d.dpn);
+    rc |= ar.add(t->flags, n + 1, d.flags);
+    rc |= ar.add(t->jump_mask, n + 1, d.jmask);
+    rc |= ar.add(t->dmx_a, n + 1, d.dmx_a);
+    rc |= ar.add(t->dmx_b, n + 1, d.dmx_b);
     if (t->dmx_x) {
         // the CSR overflow of the DMX bin ids: n+2 non-decreasing offsets starting at n+2,
         // then bin indices in [0, ndmx) (the kernels index the table with them unchecked)
@@ -4412,13 +4454,13 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         for (int i = 0; ok && i <= n; i++) ok = x[i + 1] >= x[i];
         for (int k = ok ? n + 2 : 0; ok && k < x[n + 1]; k++) ok = x[k] >= 0 && x[k] < spec->ndmx;
         if (!ok) { ctx->err = "dmx_x: malformed DMX overflow CSR (offsets or bin indices)"; return -PINT_E_INVALID; }
-        rc |= upload(ctx, ph, t->dmx_x, (size_t)x[n + 1], d.dmx_x);
+        rc |= ar.add(t->dmx_x, (size_t)x[n + 1], d.dmx_x);
     }
-    rc |= upload(ctx, ph, red_freq, (size_t)2 * spec->nred, d.red_freq);
-    rc |= upload(ctx, ph, red_phi, (size_t)2 * spec->nred, d.red_phi);
-    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)4 * n, d.red_cs);
-    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
-    rc |= upload(ctx, ph, (const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
+    rc |= ar.add(red_freq, (size_t)2 * spec->nred, d.red_freq);
+    rc |= ar.add(red_phi, (size_t)2 * spec->nred, d.red_phi);
+    rc |= ar.add((const double*)nullptr, (size_t)4 * n, d.red_cs);
+    rc |= ar.add((const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
+    rc |= ar.add((const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
     const bool trig_setup = spec->nred > 0;  // red_cs and the trig sums: flush_setup, batched
     if (trig_setup) {
         ph.f1 = red_freq[0];
@@ -4467,7 +4509,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
                 if (k > 0 && lists[a][k] != lists[a][k - 1] + 1) contig = false;
             }
         }
-        rc |= upload(ctx, ph, drow.data(), drow.size(), d.drow);
+        rc |= ar.add(drow.data(), drow.size(), d.drow);
         ph.drow_host.assign(drow.begin(), drow.end());
         ph.dlo.assign(ndc, 0);
         ph.dhi.assign(ndc, 0);
@@ -4485,12 +4527,12 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
                 if (cmap[c] >= 0) dorig[cmap[c]] = c;
                 else xorig[-cmap[c] - 1] = c;
             }
-            rc |= upload(ctx, ph, dorig.data(), dorig.size(), d.dorig);
-            rc |= upload(ctx, ph, xorig.data(), xorig.size(), d.xorig);
+            rc |= ar.add(dorig.data(), dorig.size(), d.dorig);
+            rc |= ar.add(xorig.data(), xorig.size(), d.xorig);
         }
-        rc |= upload(ctx, ph, cmap.data(), cmap.size(), d.cmap);
-        rc |= upload(ctx, ph, dptr.data(), dptr.size(), d.dptr);
-        rc |= upload(ctx, ph, didx.data(), didx.size(), d.didx);
+        rc |= ar.add(cmap.data(), cmap.size(), d.cmap);
+        rc |= ar.add(dptr.data(), dptr.size(), d.dptr);
+        rc |= ar.add(didx.data(), didx.size(), d.didx);
         // design-matrix column runs: same kind, consecutive indices (BIN: same kind only)
         std::vector<ColRun> runs;
         for (int c = 0; c < ncol; c++) {
@@ -4501,19 +4543,19 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
             }
             runs.push_back(ColRun{k, c, 1, ix, k == PINT_COL_DMX ? -1 : cmap[c], {0, 0, 0}});
         }
-        rc |= upload(ctx, ph, runs.data(), runs.size(), d.runs);
+        rc |= ar.add(runs.data(), runs.size(), d.runs);
         d.nrun = (int)runs.size();
     }
     const pint_spec_t* sp = nullptr;
-    rc |= upload(ctx, ph, spec, 1, sp);
-    if (rc) return -PINT_E_HIP;
+    rc |= ar.add(spec, 1, sp);
+    if (rc || ar.commit(ctx, ph)) return -PINT_E_HIP;
     d.spec = sp;
     d.n = n;
     d.K = K;
     d.Kp = Kp;
     ctx->psrs.push_back(ph);
     if (trig_setup) ctx->setup_pending.push_back((int)ctx->psrs.size() - 1);
-    if (refresh_psrs(ctx)) return -PINT_E_HIP;
+    ctx->psrs_dirty = true;  // the device descriptor array is rebuilt once, at pint_set_instances
     return (int)ctx->psrs.size() - 1;
 }
 
@@ -4603,6 +4645,7 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
 int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (ctx->psrs_dirty && refresh_psrs(ctx)) return PINT_E_HIP;
     if (flush_setup(ctx)) return PINT_E_HIP;  // the uploads' red-noise set-up, one batch
     free_instances(ctx);
     ctx->inst.resize(ninst);
@@ -4662,31 +4705,59 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     // vg compact path (k_gram_v): contiguous DMX bins, no ECORR, nred <= 31, <= 47
     // timing columns; the DMX slots fill the [T | r] row tiles (+16 if needed) such that the
     // bins of every N-split are distinct mod vns; LDS width <= VMAXKP
+    auto vg_ok = [&](const PsrHost& ph) {
+        const PsrDev& d = ph.dev;
+        return ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
+               ph.spec.dmn0 >= ph.spec.nred &&  // PLDMNoise: stored, per-TOA scaled basis
+               d.red0c + 1 <= VMAXR0;
+    };
+    auto slots_ok = [&](const PsrHost& ph, int ntr) {  // bins of every split distinct mod ns
+        const PsrDev& d = ph.dev;
+        const int wt = d.red0c + 1, R = d.Kd - d.red0c;
+        const int ns = 16 * ntr - wt, kpv = (16 * ntr + R + 15) / 16 * 16;
+        if (ns < 1 || kpv > VMAXKP) return false;
+        long per = (ph.n + nsplit - 1) / nsplit;
+        per = (per + 3) / 4 * 4;
+        for (int sp = 0; sp < nsplit; sp++) {
+            const long i0 = sp * per, i1 = std::min<long>(i0 + per, ph.n);
+            std::vector<char> seen(ns, 0);
+            for (int a = 0; a < d.ndc; a++) {
+                if (ph.dhi[a] <= ph.dlo[a] || ph.dlo[a] >= i1 || ph.dhi[a] <= i0) continue;
+                if (seen[a % ns]) return false;
+                seen[a % ns] = 1;
+            }
+        }
+        return true;
+    };
+    // A batch whose Gram workgroups fit one resident round (a few pulsars: the per-rank shard
+    // of a PTA over several GPUs) is latency-bound, and every distinct k_gram_v tile shape is
+    // a launch of its own, in sequence: there all vg pulsars take the largest row-tile count
+    // any of them needs (more padding MFMAs, one launch)
+    int force_ntr = 0;
+    if ((long)ninst * nsplit <= slots) {
+        std::vector<char> inb(ctx->psrs.size(), 0);
+        for (int k = 0; k < ninst; k++) inb[inst_psr[k]] = 1;
+        for (size_t p = 0; p < ctx->psrs.size(); p++) {
+            const PsrHost& ph = ctx->psrs[p];
+            if (!inb[p] || !vg_ok(ph)) continue;
+            const int wt = ph.dev.red0c + 1;
+            for (int ntr = (wt + 15) / 16; ntr <= std::min(3, (wt + 15) / 16 + 2); ntr++)
+                if (slots_ok(ph, ntr)) { force_ntr = std::max(force_ntr, ntr); break; }
+        }
+    }
     for (auto& ph : ctx->psrs) {
         PsrDev& d = ph.dev;
         d.vg = 0;
         d.vb = 0;
-        if (!(ctx->vgram && d.dsplit && d.dcontig && d.nep == 0 && ph.spec.nred <= VTRIG / 2 - 1 &&
-              ph.spec.dmn0 >= ph.spec.nred &&  // PLDMNoise: stored, per-TOA scaled basis
-              d.red0c + 1 <= VMAXR0))
-            continue;
+        if (!vg_ok(ph)) continue;
         long per = (ph.n + nsplit - 1) / nsplit;
         per = (per + 3) / 4 * 4;
         const int wt = d.red0c + 1, R = d.Kd - d.red0c;
-        for (int ntr = (wt + 15) / 16; ntr <= std::min(3, (wt + 15) / 16 + 2); ntr++) {
+        const int ntr0 = std::max((wt + 15) / 16, std::min(3, force_ntr));
+        for (int ntr = ntr0; ntr <= std::min(3, (wt + 15) / 16 + 2); ntr++) {
             const int ns = 16 * ntr - wt, kpv = (16 * ntr + R + 15) / 16 * 16;
-            if (ns < 1 || kpv > VMAXKP) continue;
-            bool ok = true;
-            for (int sp = 0; ok && sp < nsplit; sp++) {
-                const long i0 = sp * per, i1 = std::min<long>(i0 + per, ph.n);
-                std::vector<char> seen(ns, 0);
-                for (int a = 0; ok && a < d.ndc; a++) {
-                    if (ph.dhi[a] <= ph.dlo[a] || ph.dlo[a] >= i1 || ph.dhi[a] <= i0) continue;
-                    if (seen[a % ns]) ok = false;
-                    seen[a % ns] = 1;
-                }
-            }
-            if (ok) {
+            if (!slots_ok(ph, ntr)) continue;
+            {
                 d.vg = 1;
                 d.vns = ns;
                 d.vkp = kpv;
@@ -5498,7 +5569,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     ctx->cov_pending = false;
     if (skip) {
         // deferred covariance for batches (a single fit would pay a launch on its read instead)
-        double* xw = (ctx->d_xw && (ctx->cov_defer == 2 || (ctx->cov_defer == 1 && ctx->ninst >= 16))) ? ctx->d_xw : nullptr;
+        // (and in lazy, pipelined steps of any size: the read runs k_cov_dmx on the copy stream,
+        // beside the next kernels, so a small batch's solve does not carry it either)
+        double* xw = (ctx->d_xw && (ctx->cov_defer == 2 || (ctx->cov_defer == 1 && (ctx->ninst >= 16 || ctx->lazy))))
+                         ? ctx->d_xw : nullptr;
         // when it is the last solve kernel, ev_solved rides on its dispatch packet (a separate
         // event record is a marker packet between kernels: ~6-10 us of idle stream, measured)
         solved_ev = Ks == 0 ? ctx->ev_solved : nullptr;

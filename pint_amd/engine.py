@@ -335,13 +335,13 @@ def pack_toas(lay: PulsarLayout):
         r1 = float(model["DMXR1_" + tag].value)
         r2 = float(model["DMXR2_" + tag].value)
         sel = np.where((mjdf >= r1) & (mjdf <= r2))[0]  # toa_select.py:101 inclusive
-        for i in sel:
-            if da[i] < 0:
-                da[i] = j
-            elif db[i] < 0:
-                db[i] = j
-            else:   # a third (fourth, ...) overlapping bin: the CSR overflow below
-                extra.setdefault(int(i), []).append(j)
+        fa = da[sel] < 0            # (bins in parameter order: a TOA's first free slot)
+        da[sel[fa]] = j
+        rest = sel[~fa]
+        fb = db[rest] < 0
+        db[rest[fb]] = j
+        for i in rest[~fb]:         # a third (fourth, ...) overlapping bin: the CSR overflow below
+            extra.setdefault(int(i), []).append(j)
     dmx_x = None
     if extra:
         # n+2 offsets into the same array, then the bin indices in parameter order (the

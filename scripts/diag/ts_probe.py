@@ -3,7 +3,8 @@ sys.path.insert(0, os.getcwd())
 from pint_amd.engine import Session, build_layout, pack_table
 from pint_amd import simulation as sim
 from pint_amd.timing_model import get_model
-items = sim.make_pta(ntoas=10000, indices=list(range(68)))
+NPSR = int(sys.argv[1]) if len(sys.argv) > 1 else 68
+items = sim.make_pta(ntoas=10000, indices=list(range(NPSR)))
 s = Session(0)
 lays = [s.add(build_layout(m, t)) for m, t in items]
 s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
