@@ -1,0 +1,210 @@
+// The 16x16 diagonal-block factor of the blocked Cholesky (k_solve_dmx's diag_factor): one
+// wave factors a symmetric positive-definite 16x16 block held in LDS and overwrites it with
+// L^-1.  Variants:
+//   0  as in pint_hip.hip (row per lane, readlane broadcasts; the compiler hoists the
+//      readlanes of several pivots and spills SGPRs to VGPR lanes),
+//   1  the same arithmetic with a scheduling barrier after each pivot (no cross-pivot
+//      hoisting: the broadcasts of one pivot live in SGPRs at a time),
+//   2  variant 1 with one Newton step on v_rsq_f64 instead of two,
+//   3  the pivot column broadcast through LDS (VGPR operands), 4: that with one Newton step.
+// Prints the max error of L^-1 against a long-double Cholesky inverse on the host (relative
+// to max |L^-1|) and the cycles per factor (s_memtime, 64 dependent factors in one wave).
+// Build: hipcc --offload-arch=gfx950 -O3 bench/diag_probe.hip -o build/diag_probe
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+__device__ __forceinline__ double rdlane(double v, int l) {
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ int swz(int r, int c) { return (c << 4) + (r ^ (c & 14)); }
+
+template <int NEWTON>
+__device__ __forceinline__ double rsqn(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+#pragma unroll
+    for (int k = 0; k < NEWTON; k++) y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
+    return y;
+}
+
+template <int V>
+__device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
+    const int r = lane & 15;
+    double a[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        a[c] = Akk[swz(r, c)];
+        x[c] = (r == c) ? 1.0 : 0.0;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const double djj = rdlane(a[j], j);
+        ok = ok && (djj > 0.0);
+        const double il = V == 2 ? rsqn<1>(djj) : rsqn<2>(djj);
+        a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
+        x[j] *= il;
+#pragma unroll
+        for (int c = j + 1; c < 16; c++) {
+            const double Lcj = rdlane(a[j], c);
+            a[c] -= a[j] * Lcj;
+            x[c] -= Lcj * x[j];
+        }
+        if (V >= 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+    }
+    return ok;
+}
+
+// variant 3: the scaled pivot column goes through LDS (one ds_write by lanes 0..15, then
+// uniform-address reads: every lane gets L_cj in VGPRs, no SGPR broadcasts)
+template <int NEWTON>
+__device__ __forceinline__ bool diag_factor_lds(double* Akk, double* colbuf, int lane) {
+    const int r = lane & 15;
+    double a[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        a[c] = Akk[swz(r, c)];
+        x[c] = (r == c) ? 1.0 : 0.0;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const double djj = rdlane(a[j], j);
+        ok = ok && (djj > 0.0);
+        const double il = rsqn<NEWTON>(djj);
+        a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
+        x[j] *= il;
+        typedef __attribute__((address_space(3))) double ldsd;
+        typedef double dv2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(3))) dv2 ldsd2;
+        if (lane < 16) ((ldsd*)colbuf)[lane] = a[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double Lc[16];
+#pragma unroll
+        for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
+            const dv2 v = ((ldsd2*)colbuf)[c2];
+            Lc[2 * c2] = v.x;
+            Lc[2 * c2 + 1] = v.y;
+        }
+#pragma unroll
+        for (int c = j + 1; c < 16; c++) {
+            a[c] -= a[j] * Lc[c];
+            x[c] -= Lc[c] * x[j];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+    }
+    return ok;
+}
+
+template <int V>
+__device__ __forceinline__ bool factor_v(double* Akk, double* colbuf, int lane) {
+    if constexpr (V >= 3) return diag_factor_lds<V == 3 ? 2 : 1>(Akk, colbuf, lane);
+    else return diag_factor<V>(Akk, lane);
+}
+
+template <int V>
+__global__ __launch_bounds__(64) void k_diag(const double* __restrict__ in, double* __restrict__ out,
+                                             long long* __restrict__ cyc, int reps) {
+    __shared__ double blk[256];
+    __shared__ double colbuf[16];
+    const int lane = threadIdx.x;
+    for (int e = lane; e < 256; e += 64) blk[e] = in[e];
+    __syncthreads();
+    bool ok = factor_v<V>(blk, colbuf, lane);
+    __syncthreads();
+    for (int e = lane; e < 256; e += 64) out[e] = blk[e];
+    // timing: reps dependent factors of the same block (restaged from registers each time)
+    __syncthreads();
+    for (int e = lane; e < 256; e += 64) blk[e] = in[e];
+    __syncthreads();
+    long long t0 = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < reps; k++) {
+        ok &= factor_v<V>(blk, colbuf, lane);
+        __syncthreads();
+        for (int e = lane; e < 256; e += 64) blk[e] = in[e] + (ok ? 0.0 : 1.0) * blk[e];
+        __syncthreads();
+    }
+    long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) cyc[0] = (t1 - t0) / reps;
+}
+
+int main() {
+    // a normalised SPD block like the solve's: unit-ish diagonal, correlated off-diagonals
+    std::vector<double> A(256), M(256);
+    unsigned long long s = 88172645463325252ull;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (double)(s >> 11) / 9007199254740992.0 - 0.5; };
+    for (int i = 0; i < 16; i++)
+        for (int k = 0; k < 24; k++) M[i * 16 + (k % 16)] += rnd();
+    std::vector<long double> S(256, 0.0L);
+    for (int i = 0; i < 16; i++)
+        for (int j = 0; j < 16; j++) {
+            long double v = (i == j) ? 0.05L : 0.0L;
+            for (int k = 0; k < 16; k++) v += (long double)M[i * 16 + k] * M[j * 16 + k];
+            S[i * 16 + j] = v;
+        }
+    for (int i = 0; i < 16; i++)
+        for (int j = 0; j < 16; j++) A[((j << 4) + (i ^ (j & 14)))] = (double)S[i * 16 + j];
+    // host: L (long double) from the double input, then L^-1
+    std::vector<long double> L(256, 0.0L), X(256, 0.0L);
+    for (int i = 0; i < 16; i++)
+        for (int j = 0; j < 16; j++) S[i * 16 + j] = (long double)A[((j << 4) + (i ^ (j & 14)))];
+    for (int j = 0; j < 16; j++) {
+        long double d = S[j * 16 + j];
+        for (int k = 0; k < j; k++) d -= L[j * 16 + k] * L[j * 16 + k];
+        L[j * 16 + j] = sqrtl(d);
+        for (int i = j + 1; i < 16; i++) {
+            long double v = S[i * 16 + j];
+            for (int k = 0; k < j; k++) v -= L[i * 16 + k] * L[j * 16 + k];
+            L[i * 16 + j] = v / L[j * 16 + j];
+        }
+    }
+    for (int c = 0; c < 16; c++)
+        for (int i = 0; i < 16; i++) {
+            long double v = (i == c) ? 1.0L : 0.0L;
+            for (int k = 0; k < i; k++) v -= L[i * 16 + k] * X[k * 16 + c];
+            X[i * 16 + c] = v / L[i * 16 + i];
+        }
+    long double xmax = 0;
+    for (auto v : X) xmax = fmaxl(xmax, fabsl(v));
+    double *din, *dout;
+    long long* dc;
+    hipMalloc(&din, 256 * 8);
+    hipMalloc(&dout, 256 * 8);
+    hipMalloc(&dc, 8);
+    hipMemcpy(din, A.data(), 256 * 8, hipMemcpyHostToDevice);
+    for (int v = 0; v < 5; v++) {
+        if (v == 0) hipLaunchKernelGGL(k_diag<0>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 1) hipLaunchKernelGGL(k_diag<1>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 2) hipLaunchKernelGGL(k_diag<2>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 3) hipLaunchKernelGGL(k_diag<3>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 4) hipLaunchKernelGGL(k_diag<4>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        std::vector<double> o(256);
+        long long c;
+        hipMemcpy(o.data(), dout, 256 * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+        long double err = 0;
+        for (int i = 0; i < 16; i++)
+            for (int j = 0; j < 16; j++) {
+                const long double ref = j <= i ? X[i * 16 + j] : 0.0L;
+                err = fmaxl(err, fabsl((long double)o[(j << 4) + (i ^ (j & 14))] - ref));
+            }
+        printf("variant %d: max |X - X_ref| / max|X| = %.3Le, %lld cycles per factor (s_memtime)\n", v,
+               err / xmax, c);
+    }
+    return 0;
+}

@@ -129,7 +129,7 @@ struct InstDev {
     long ddoff;
     long vgoff;  // k_gram_v DMX slot partials offset (nsplit * vns * (Kd+3))
     long vboff;  // k_gram_v binned DMX x Fourier partials offset (nsplit * GW * vns * 128)
-    long xwoff;  // k_solve_dmx -> k_cov_dmx export offset (X, W blocks and the scalings)
+    long xwoff;  // k_solve_dmx -> k_cov_dmx export offset (X, U blocks and the scalings)
     int self;    // index of this instance in the batch
     int nrb;     // k_resid row blocks of this instance (RES_RB rows each)
     long rb0;    // first k_resid row block
@@ -2812,6 +2812,24 @@ __device__ __forceinline__ void cov_dmx_blocks(const double* A, const double* in
     }
 }
 
+// W = X U in place of U (X = L_S^-1 in the lower blocks of A, U in the nbd x nbk U blocks):
+// (block row Ib, block column kb) pairs in rounds of NW waves, block rows descending: a
+// round's products have read their U blocks before its W blocks are stored, and a later
+// round (smaller or equal Ib, other pairs) never reads a block stored earlier
+template <int NW>
+__device__ __forceinline__ void w_from_xu(double* A, int nbd, int nbk, int nblkS, int wave, int lane) {
+    const int npair = nbd * nbk;
+    for (int r = 0; r < npair; r += NW) {
+        const int p = r + wave, Ib = nbd - 1 - p / nbk, kb = p % nbk;
+        double4_t acc = {0, 0, 0, 0};
+        if (p < npair)
+            for (int Jb = 0; Jb <= Ib; Jb++)
+                bmma<false, true>(acc, A + lblk(Ib, Jb), A + ublk(Jb, kb, nbk, nblkS), lane, false);
+        __syncthreads();
+        if (p < npair) bstore(A + ublk(Ib, kb, nbk, nblkS), acc, lane, 1.0);
+    }
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
@@ -3004,7 +3022,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         return;
     }
     TS(3);
-    // ---- y = X b'_d ; W = X U (in place, wave per U block column, block rows descending) ----
+    // ---- y = X b'_d ----
     const int g0 = tid >> 2, sub = tid & 3;
     for (int g = g0; g < nbd * 16; g += NW * 16) {
         double sy = 0.0;
@@ -3013,24 +3031,14 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sy += __shfl_xor(sy, 2, 64);
         if (sub == 0) yv[g] = sy;
     }
-    {
-        // (block row Ib, block column kb) pairs in rounds of NW, block rows descending: a
-        // round's products have read their U blocks before its W blocks are stored, and a
-        // later round (smaller or equal Ib, other pairs) never reads a block stored earlier
-        const int npair = nbd * nbk;
-        for (int r = 0; r < npair; r += NW) {
-            const int p = r + wave, Ib = nbd - 1 - p / nbk, kb = p % nbk;
-            double4_t acc = {0, 0, 0, 0};
-            if (p < npair)
-                for (int Jb = 0; Jb <= Ib; Jb++)
-                    bmma<false, true>(acc, A + lblk(Ib, Jb), A + ublk(Jb, kb, nbk, nblkS), lane, false);
-            __syncthreads();
-            if (p < npair) bstore(A + ublk(Ib, kb, nbk, nblkS), acc, lane, 1.0);
-        }
-    }
+    // deferred covariance (xw): W = X U, the DMX errors and the covariance blocks are formed by
+    // k_cov_dmx at the read, off the step's critical path; the step needs only
+    // z = W^T y = U^T X^T y = U^T x_d, so U stays in LDS as it is
+    const bool defer = xw != nullptr;
+    if (!defer) w_from_xu<NW>(A, nbd, nbk, nblkS, wave, lane);  // W = X U in place of U
     __syncthreads();
     TS(4);
-    // ---- x_d = X^T y, z = W^T y, x_x = D^-1 b_x - D^-1/2 z ; errors ----
+    // ---- x_d = X^T y ; errors of the dense columns ----
     double amax = 0.0, vmax = 0.0;  // max diag(A) and max diag(A^-1): the condition estimate
     for (int g = g0; g < Kd; g += NW * 16) {
         double s1 = 0.0, se = 0.0;
@@ -3050,22 +3058,28 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             amax = fmax(amax, Gd(g, g) * (ind[g] * ind[g]));
         }
     }
+    if (defer) __syncthreads();  // x_d visible: z = U^T x_d below
+    // ---- z = W^T y (= U^T x_d when deferred), x_x = D^-1 b_x - D^-1/2 z ; DMX errors ----
     for (int a = g0; a < ndc; a += NW * 16) {
         double sz = 0.0, sw = 0.0;
         for (int rr = sub; rr < nbd * 16; rr += 4) {
             const double w = A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
-            sz += w * yv[rr];
+            sz += w * (defer ? (rr < Kd ? xd[rr] : 0.0) : yv[rr]);
             sw += w * w;
         }
         sz += __shfl_xor(sz, 1, 64);
         sz += __shfl_xor(sz, 2, 64);
-        sw += __shfl_xor(sw, 1, 64);
-        sw += __shfl_xor(sw, 2, 64);
+        if (!defer) {
+            sw += __shfl_xor(sw, 1, 64);
+            sw += __shfl_xor(sw, 2, 64);
+        }
         if (sub == 0) {
             const double d = Dn[a];
             xx[a] = bx[a] / d - sz * isd[a];
-            errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / d + sw / d) * inx[a];
-            vmax = fmax(vmax, (1.0 + sw) / d);
+            // deferred: the DMX errors come from k_cov_dmx (they need W); diag(A^-1) >= 1/d
+            // keeps the condition estimate a lower bound
+            if (!defer) errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / d + sw / d) * inx[a];
+            vmax = fmax(vmax, defer ? 1.0 / d : (1.0 + sw) / d);
             amax = fmax(amax, d);
         }
     }
@@ -3076,8 +3090,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     __syncthreads();
     // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
     // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
-    // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y).  The explicit L^-1 loses ~cond(L) digits that
-    // LAPACK's triangular solves keep (cho_solve, fitter.py:2197) ----
+    // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y, W^T y = U^T dx_d when deferred).  The explicit
+    // L^-1 loses ~cond(L) digits that LAPACK's triangular solves keep (cho_solve,
+    // fitter.py:2197) ----
     auto Ad = [&](int i, int j) {
         double v = Gd(i, j) * (ind[i] * ind[j]);
         if (i == j && mode == 1 && i >= red0) v += (ind[i] * ind[i]) / Pd.red_phi[i - red0];
@@ -3129,12 +3144,17 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             for (int rr = g + sub; rr < nbd * 16; rr += 4) s1 += A[lblk(rr >> 4, g >> 4) + swz(rr & 15, g & 15)] * yv[rr];
             s1 += __shfl_xor(s1, 1, 64);
             s1 += __shfl_xor(s1, 2, 64);
-            if (sub == 0) xd[g] += s1;
+            if (sub == 0) {
+                xd[g] += s1;
+                rd[g] = s1;  // dx_d (rd is consumed): U^T dx_d below when deferred
+            }
         }
+        if (defer) __syncthreads();
         for (int a = g0; a < ndc; a += NW * 16) {
             double sz = 0.0;
             for (int rr = sub; rr < nbd * 16; rr += 4)
-                sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * yv[rr];
+                sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] *
+                      (defer ? (rr < Kd ? rd[rr] : 0.0) : yv[rr]);
             sz += __shfl_xor(sz, 1, 64);
             sz += __shfl_xor(sz, 2, 64);
             if (sub == 0) xx[a] += rx[a] / Dn[a] - sz * isd[a];
@@ -3156,7 +3176,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
     TS(5);
     // ---- covariance of the timing parameters ----
-    if (xw) {  // deferred to k_cov_dmx (several workgroups per instance, at the read)
+    if (xw) {  // deferred to k_cov_dmx (several workgroups per instance, at the read): X, U
         double* o = xw + I.xwoff;
         const int na = (nblkS + nbd * nbk) * 256;
         for (int e = tid; e < na; e += NW * 64) o[e] = A[e];
@@ -3172,13 +3192,15 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     TS(6);
 }
 
-// k_cov_dmx: the covariance blocks of k_solve_dmx, COV_WG workgroups per instance, each
-// staging the instance's X, W and scalings (d_xw) in LDS; launched by pint_read_step when
-// the covariance is read (on the copy stream, off the fit step's critical path)
+// k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred
+// solves export X, U and the scalings to d_xw); COV_WG workgroups per instance, each staging
+// the instance's export in LDS and forming W itself; launched by pint_read_step when the
+// errors or the covariance are read (on the copy stream, off the fit step's critical path)
 constexpr int COV_WG = 3;
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                     const double* __restrict__ xw, int mode, double* __restrict__ cov) {
+                                                     const double* __restrict__ xw, int mode, double* __restrict__ cov,
+                                                     double* __restrict__ errs) {
     extern __shared__ double lds[];
     const InstDev I = insts[blockIdx.x];
     const PsrDev& Pd = psrs[I.psr];
@@ -3196,8 +3218,24 @@ __global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ 
     const double* inx = ind + nbd * 16;
     const double* isd = inx + nbk * 16;
     const double* Dn = isd + nbk * 16;
-    cov_dmx_blocks(lds, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, Pd.spec->ncol, red0, ndc, nbd, nbk, nblkS,
-                   blockIdx.y * NW + wave, gridDim.y * NW, lane);
+    w_from_xu<NW>(lds, nbd, nbk, nblkS, wave, lane);
+    __syncthreads();
+    if (blockIdx.y == 0 && errs) {  // DMX errors: C_xx's diagonal D^-1 + D^-1 |W_a|^2
+        const int g0 = threadIdx.x >> 2, sub = threadIdx.x & 3;
+        for (int a = g0; a < ndc; a += NW * 16) {
+            double sw = 0.0;
+            for (int rr = sub; rr < nbd * 16; rr += 4) {
+                const double w = lds[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
+                sw += w * w;
+            }
+            sw += __shfl_xor(sw, 1, 64);
+            sw += __shfl_xor(sw, 2, 64);
+            if (sub == 0) errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / Dn[a] + sw / Dn[a]) * inx[a];
+        }
+    }
+    if (cov)
+        cov_dmx_blocks(lds, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, Pd.spec->ncol, red0, ndc, nbd, nbk, nblkS,
+                       blockIdx.y * NW + wave, gridDim.y * NW, lane);
 }
 
 // ---------------------------------------------------------------------------------
@@ -3958,7 +3996,7 @@ struct pint_ctx {
     double* d_Sdp = nullptr;                    // k_gram_v DMX slot partials
     double* d_BFp = nullptr;                    // k_gram_v binned DMX x Fourier partials (VB)
     int vb_on = 0;                              // the batch's vg instances use VB
-    double* d_xw = nullptr;     // k_solve_dmx's X, W and scalings for the deferred covariance
+    double* d_xw = nullptr;     // k_solve_dmx's X, U and scalings for the deferred W, DMX errors and covariance
     int cov_defer = 1;          // PINT_COV_DEFER: the DMX-eliminated covariance in k_cov_dmx (0 never,
                                 // 1 batches of >= 16 instances, 2 always)
     bool cov_pending = false;   // d_cov of the last solve not formed yet (k_cov_dmx at the read)
@@ -5675,11 +5713,12 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
     // follow; the caller's buffers (pinned: pint_host_alloc) are valid after pint_check().
     hipStream_t st = ctx->lazy ? ctx->cstream : ctx->stream;
     if (ctx->lazy) HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_solved, 0));
-    if (cov && ctx->cov_pending) {  // the DMX-eliminated solve's covariance blocks
-        hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ctx->ninst, COV_WG), dim3(1024), ctx->cov_lds, st, ctx->d_psrs,
-                           ctx->d_inst, ctx->d_xw, ctx->cov_mode, ctx->d_cov);
+    if ((cov || errs) && ctx->cov_pending) {  // the DMX-eliminated solve's W, DMX errors, covariance
+        hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ctx->ninst, cov ? COV_WG : 1), dim3(1024), ctx->cov_lds, st,
+                           ctx->d_psrs, ctx->d_inst, ctx->d_xw, ctx->cov_mode, cov ? ctx->d_cov : nullptr,
+                           ctx->d_errs);
         HIPCHK(hipGetLastError());
-        ctx->cov_pending = false;
+        ctx->cov_pending = cov == nullptr;  // errors only: a later read of the covariance re-runs it
     }
     if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
     if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
