@@ -57,6 +57,9 @@ def main():
     ap.add_argument("--emulate-world", default="2,4,8",
                     help="N=1 only: time every rank's LPT shard of the PTA for these world sizes on this "
                          "GPU, one after the other (predicted_strong; '' = skip)")
+    ap.add_argument("--graph", default="0", choices=["0", "1", "auto"],
+                    help="step launches: 0 enqueued from the host, 1 one HIP-graph replay per step, auto the "
+                         "faster of the two on a short trial (every rank makes the same choice)")
     ap.add_argument("--cold-start", type=int, default=1,
                     help="N=1 only: upload + first fit of the PTA in a fresh session (cold_start)")
     args = ap.parse_args()
@@ -140,6 +143,7 @@ def main():
                                       f"realisations (the {args.npsr}-pulsar PTA, LPT-sharded over {world} rank(s))",
                           "npsr": args.npsr, "ntoas": args.ntoas,
                           "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
+                          "launch": leg["launch"],
                           "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
                "roofline": roof, "pta_weak": weak, "predicted_strong": emu, "cold_start": cold,
                "grid": grid, "j0740": j0740, "c2": c2,
@@ -161,8 +165,9 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
     lays = [s.add(build_layout(m, t)) for m, t in items]
     tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
     s.set_instances(list(zip(lays, tabs0)))
-    dt, kt_gram, n_gram, step = timed_steps(s, args.steps, args.warmup, barrier, max_over_ranks)
-    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays))}
+    dt, kt_gram, n_gram, step, launch = timed_steps(s, args.steps, args.warmup, barrier, max_over_ranks,
+                                                    graph=args.graph)
+    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays)), "launch": launch}
     if profile:
         out["roofline"] = roofline(s, lays, kt_gram / max(1, n_gram), step, args)
         out["roofline"]["gram_event_launches"] = int(n_gram)
@@ -189,22 +194,24 @@ def emulate_world(items, costs, worlds, args, value1, step1):
     for nw in worlds:
         if nw <= 1:
             continue
-        per = []
+        per, modes = [], []
         for sh in lpt_shard(costs, nw):
             if not sh:
                 per.append(0.0)
+                modes.append(None)
                 continue
             s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
             sub = [items[i] for i in sh]
             lays = [s.add(build_layout(m, t)) for m, t in sub]
             s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, sub)])
-            dt, _, _, _ = timed_steps(s, steps, warm, nobarrier, lambda v: v)
+            dt, _, _, _, launch = timed_steps(s, steps, warm, nobarrier, lambda v: v, graph=args.graph)
             s.close()
             per.append(dt / steps)
+            modes.append(launch)
         mx = max(per)
         out[f"n{nw}"] = {"value": round(len(items) / mx, 3), "ms_per_step": round(mx * 1e3, 4),
                          "ms_per_shard": [round(p * 1e3, 4) for p in per],
-                         "pulsars_per_rank": [len(sh) for sh in lpt_shard(costs, nw)],
+                         "pulsars_per_rank": [len(sh) for sh in lpt_shard(costs, nw)], "launch": modes,
                          "speedup_vs_n1": round(step1 / mx, 3)}
         log(f"[emulate {nw}] shards {[round(p * 1e3, 3) for p in per]} ms -> {len(items) / mx:.0f} fits/s")
     return out
@@ -225,10 +232,9 @@ def cold_start(items, rank):
     s.check()
     t2 = time.perf_counter()
     s.eval(want_M=Session.FIT)
-    s.fit_step(1)
+    s.fit_step_apply(1, 1.0)
     s.read_step()
     s.noise_resids()
-    s.apply_step_uniform(1.0)
     s.eval(want_M=False)
     s.chi2_gls()
     s.check()
@@ -242,10 +248,16 @@ def cold_start(items, rank):
     return out
 
 
-def timed_steps(s, steps, warmup, barrier, max_over_ranks):
+def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto"):
     """Time `steps` fit steps of the Session's batch (warm-up first), pipelined two deep; one
-    step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.  Returns
-    (max-over-ranks seconds, summed Gram event time of the sampled steps, their count, step)."""
+    step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.
+
+    graph: 0 enqueue every launch of every step from the host; 1 capture the step once per
+    pipeline slot into a HIP graph and replay it (the same kernels, copies and outputs, one
+    host launch per step); "auto" times a short run of each after the warm-up and keeps the
+    faster (a small batch's step is shorter than its ~20 host launches take to enqueue).
+    Returns (max-over-ranks seconds, summed Gram event time of the sampled steps, their
+    count, step, launch mode)."""
     from pint_amd.engine import Session
     s.save_tables()        # the initial models, resident in HBM like the TOAs
     s.set_lazy(True)
@@ -253,27 +265,28 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks):
     def step():
         s.restore_tables()     # every step fits from the initial models (device->device copy)
         s.eval(want_M=Session.FIT)
-        s.fit_step(1)
+        s.fit_step_apply(1, 1.0)  # the GLS step and the full-step update (fused into the solve)
         out = s.read_step()    # steps, errors, timing covariance -> host (fit outputs)
         nz = s.noise_resids()  # noise realisations -> host (fitter.py:2269-2282, full_cov=False)
-        s.apply_step_uniform(1.0)
         s.eval(want_M=False)
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
         return out, nz, c2
 
-    # timed region: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop on
+    # Gram timing: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop on
     # its first/last dispatch packet, or marker packets on the other Gram paths), on every
-    # GRAM_EVERY-th step: each event pair still costs the stream a few us, so the Gram's time
-    # is the average over the sampled launches
+    # GRAM_EVERY-th enqueued step: each event pair still costs the stream a few us, so the
+    # Gram's time is the average over the sampled launches.  Graph replays carry no events:
+    # their Gram time comes from enqueued steps timed after the graph run.
     s.set_timing_mask(1 << SLOT_GRAM)
     s.set_timing_every(GRAM_EVERY)
 
-    def run(nsteps):
-        """nsteps steps pipelined two deep (Session.step_end / check_step); returns the
-        summed Gram-kernel event time of the sampled steps and their count."""
+    def run(nsteps, launch):
+        """nsteps steps pipelined two deep (Session.step_end / check_step); launch() enqueues
+        one step.  Returns the summed Gram-kernel event time of the sampled steps and their
+        count."""
         kt, nk, prev = 0.0, 0, None
         for _ in range(nsteps):
-            step()
+            launch()
             cur = s.step_end()
             if prev is not None:
                 s.check_step(prev)
@@ -286,13 +299,33 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks):
             kt, nk = kt + t, nk + (t > 0)
         return kt, nk
 
-    run(warmup)
+    run(warmup, step)
+    use_graph = False
+    if graph in (1, "1", "auto"):
+        s.set_timing_mask(0)
+        for _ in range(2):  # one graph per pipeline slot
+            s.capture(step)
+            s.check_step(s.step_end())
+        if graph == "auto":
+            ntry = max(10, min(50, steps // 2))
+            t0 = time.perf_counter()
+            run(ntry, step)
+            t_direct = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            run(ntry, s.replay)
+            t_graph = time.perf_counter() - t0
+            use_graph = max_over_ranks(t_graph - t_direct) < 0.0  # the same choice on every rank
+        else:
+            use_graph = True
+        s.set_timing_mask(1 << SLOT_GRAM)
     barrier()
     t0 = time.perf_counter()
-    kt, nk = run(steps)
+    kt, nk = run(steps, s.replay if use_graph else step)
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    return dt, kt, nk, step
+    if use_graph:
+        kt, nk = run(max(2 * GRAM_EVERY, steps // 4), step)
+    return dt, kt, nk, step, ("hip-graph" if use_graph else "direct")
 
 
 def c2_leg(batch, steps, warmup, world, barrier, max_over_ranks):
@@ -322,12 +355,12 @@ def c2_leg(batch, steps, warmup, world, barrier, max_over_ranks):
     lay = s.add(build_layout(model, toas))
     s.set_instances([(lay, pack_table(lay, model))] * batch)
     layout = s.fit_layout(lay)
-    dtb, kt, nk, _ = timed_steps(s, steps, warmup, barrier, max_over_ranks)
+    dtb, kt, nk, _, launch = timed_steps(s, steps, warmup, barrier, max_over_ranks)
     s.close()
     out["batched"] = {"metric": f"GLS fits/sec, {batch} B1855 fits per batched step on each of {world} rank(s)",
                       "unit": "fits/s", "value": round(batch * world * steps / dtb, 1), "ms_per_step": round(dtb / steps * 1e3, 4),
                       "gram_ms": round(kt / max(1, nk), 4), "compact_layout": bool(layout[0]),
-                      "gram_cols": layout[1], "dmx_cols": layout[2]}
+                      "gram_cols": layout[1], "dmx_cols": layout[2], "launch": launch}
     return out
 
 

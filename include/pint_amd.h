@@ -191,6 +191,12 @@ int pint_apply_step(pint_ctx *ctx, const double *lambda_);
 /* The same with one lambda for every instance (GLSFitter / WLSFitter take the full step,
  * fitter.py:2254-2263); a kernel argument, no host->device copy. */
 int pint_apply_step_uniform(pint_ctx *ctx, double lambda_);
+/* pint_fit_step followed by pint_apply_step_uniform(lambda_) (GLSFitter.fit_toas's step and
+ * full-step update, fitter.py:2164-2263): when every instance takes the DMX-eliminated solve
+ * on the generated-Fourier path the update and the new tables' per-instance constants are
+ * formed at the end of the solve kernel, saving the apply launch.  pint_read_step and
+ * pint_noise_resids read the step, not the tables, and may follow it. */
+int pint_fit_step_apply(pint_ctx *ctx, int mode, double lambda_);
 
 /* Device-resident parameter tables: pint_save_tables snapshots the batch's current tables
  * on the device, pint_restore_tables copies the snapshot back (device->device on the
@@ -325,7 +331,10 @@ int pint_lognorm(pint_ctx *ctx, int gls, double *out);
  * caller's pinned buffers, the side-stream work) becomes one graph; pint_graph_launch
  * replays it with one launch.  Device buffers and host pointers are fixed at capture, so a
  * replay re-runs the same batch on whatever those buffers hold (e.g. new parameter tables
- * written into the same pinned buffer).  pint_set_instances discards the graph. */
+ * written into the same pinned buffer).  One graph per pipeline slot (pint_step_end): a
+ * capture belongs to the slot current at pint_capture_end (its outputs, status word and
+ * pinned buffers), and pint_graph_launch replays the current slot's graph, so captured steps
+ * pipeline two deep like enqueued ones.  pint_set_instances discards the graphs. */
 int pint_capture_begin(pint_ctx *ctx);
 int pint_capture_end(pint_ctx *ctx);
 int pint_graph_launch(pint_ctx *ctx);

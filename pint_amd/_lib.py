@@ -80,6 +80,7 @@ def lib():
     L.pint_read_step.argtypes = [vp, dptr, dptr, dptr, dptr]
     L.pint_apply_step.argtypes = [vp, dptr]
     L.pint_apply_step_uniform.argtypes = [vp, C.c_double]
+    L.pint_fit_step_apply.argtypes = [vp, C.c_int, C.c_double]
     L.pint_save_tables.argtypes = [vp]
     L.pint_restore_tables.argtypes = [vp]
     L.pint_sync.argtypes = [vp]
@@ -128,7 +129,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
             "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids", "pint_chi2_wls",
-            "pint_apply_step_uniform", "pint_save_tables", "pint_restore_tables", "pint_read_norms"]
+            "pint_apply_step_uniform", "pint_fit_step_apply", "pint_save_tables", "pint_restore_tables", "pint_read_norms"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -265,6 +265,14 @@ struct EvalLds {
     double P[EVAL_MAXTAB];
 };
 
+// restore targets of an evaluation that reads the parameter snapshot (pint_restore_tables): the
+// first block of each instance writes the snapshot's table and constants back (k_prep's work
+// on the restore path, without its launch); null otherwise
+struct EvalRestore {
+    double* tables;
+    InstConst* ic;
+};
+
 template <int WANT_M, int BIN>
 __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                            const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
@@ -273,7 +281,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
                                            double* __restrict__ ftay, double* __restrict__ delay_out,
                                            double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
                                            int write_red, int* __restrict__ status, int* __restrict__ istatus,
-                                           double* __restrict__ dfac, EvalLds& L) {
+                                           double* __restrict__ dfac, EvalLds& L, EvalRestore rs) {
     int ii = blk_inst[b];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -298,6 +306,12 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
         }
     }
     __syncthreads();
+    if (rs.tables && blk_row0[b] == 0) {  // the instance's first block puts the snapshot back
+        for (int k = threadIdx.x; k < ts; k += blockDim.x) rs.tables[I.toff + k] = stP ? L.P[k] : tables[I.toff + k];
+        const int* cs = reinterpret_cast<const int*>(&L.C);
+        int* cd = reinterpret_cast<int*>(rs.ic + ii);
+        for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cs[k];
+    }
     const pint_spec_t& S = L.S;
     const unsigned r = (unsigned)(blk_row0[b] + threadIdx.x);
     const int n = I.n;
@@ -366,10 +380,10 @@ __global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, c
                                               double* __restrict__ ftay, double* __restrict__ delay_out,
                                               double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
                                               int write_red, int* __restrict__ status, int* __restrict__ istatus,
-                                              double* __restrict__ dfac) {
+                                              double* __restrict__ dfac, EvalRestore rs) {
     __shared__ EvalLds L;
     eval_block<WANT_M, BIN>(blockIdx.x, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                            Mout, dmxv, compact, write_red, status, istatus, dfac, L);
+                            Mout, dmxv, compact, write_red, status, istatus, dfac, L, rs);
 }
 
 // k_eval_mix: all binary models in one launch (heaviest first: DD, ELL1, isolated blocks),
@@ -384,19 +398,19 @@ __device__ __forceinline__ void eval_mix_body(const PsrDev* __restrict__ psrs, c
                                                   double* __restrict__ ftay, double* __restrict__ delay_out,
                                                   double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
                                                   int write_red, int* __restrict__ status, int* __restrict__ istatus,
-                                                  double* __restrict__ dfac) {
+                                                  double* __restrict__ dfac, EvalRestore rs) {
     const int n2 = off3 - off2, n1 = off2 - off1;
     const int b = blockIdx.x;
     __shared__ EvalLds L;
     if (b < n2)
         eval_block<WANT_M, 2>(off2 + b, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus, dfac, L);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac, L, rs);
     else if (b < n2 + n1)
         eval_block<WANT_M, 1>(off1 + b - n2, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay,
-                              delay_out, Mout, dmxv, compact, write_red, status, istatus, dfac, L);
+                              delay_out, Mout, dmxv, compact, write_red, status, istatus, dfac, L, rs);
     else
         eval_block<WANT_M, 0>(b - n2 - n1, psrs, insts, blk_inst, blk_row0, tables, ic, ph_hi, ph_lo, ftay, delay_out,
-                              Mout, dmxv, compact, write_red, status, istatus, dfac, L);
+                              Mout, dmxv, compact, write_red, status, istatus, dfac, L, rs);
 }
 #define PINT_EVAL_MIX_ARGS                                                                                      \
     const PsrDev *__restrict__ psrs, const InstDev *__restrict__ insts, const int *__restrict__ blk_inst,        \
@@ -404,10 +418,10 @@ __device__ __forceinline__ void eval_mix_body(const PsrDev* __restrict__ psrs, c
         const InstConst *__restrict__ ic, double *__restrict__ ph_hi, double *__restrict__ ph_lo,               \
         double *__restrict__ ftay, double *__restrict__ delay_out, double *__restrict__ Mout,                   \
         double *__restrict__ dmxv, int compact, int write_red, int *__restrict__ status,                        \
-        int *__restrict__ istatus, double *__restrict__ dfac
+        int *__restrict__ istatus, double *__restrict__ dfac, EvalRestore rs
 #define PINT_EVAL_MIX_PASS                                                                                      \
     psrs, insts, blk_inst, blk_row0, off1, off2, off3, tables, ic, ph_hi, ph_lo, ftay, delay_out, Mout, dmxv,  \
-        compact, write_red, status, istatus, dfac
+        compact, write_red, status, istatus, dfac, rs
 template <int WANT_M>
 __global__ __launch_bounds__(256) void k_eval_mix(PINT_EVAL_MIX_ARGS) {
     eval_mix_body<WANT_M>(PINT_EVAL_MIX_PASS);
@@ -448,17 +462,34 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     dd d0 = dd_make(0.0);
     if (!S.track_pn && S.subtract_mean) d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
     double sw = 0.0, swx = 0.0;
-    for (int i = r0 + threadIdx.x; i < r1; i += RES_BT) {
-        dd d = dd_add_d(dd_sub(dd_make(ph_hi[ro + i], ph_lo[ro + i]), tz), Pd.dpn[i]);
+    // the thread's four rows: every load issued before the arithmetic (one load latency per
+    // block, not one per row: a small batch's pass is latency-bound)
+    constexpr int RPT = RES_RB / RES_BT;
+    double lh[RPT], ll[RPT], lp[RPT], lpn[RPT], lw[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+        const int i = r0 + threadIdx.x + u * RES_BT;
+        const bool in = i < r1;
+        lh[u] = in ? ph_hi[ro + i] : 0.0;
+        ll[u] = in ? ph_lo[ro + i] : 0.0;
+        lp[u] = in ? Pd.dpn[i] : 0.0;
+        lpn[u] = (in && S.track_pn) ? Pd.pn[i] : 0.0;
+        lw[u] = (in && S.weighted_mean) ? Pd.isig[i] : 1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+        const int i = r0 + threadIdx.x + u * RES_BT;
+        if (i >= r1) break;
+        dd d = dd_add_d(dd_sub(dd_make(lh[u], ll[u]), tz), lp[u]);
         double full;
         if (S.track_pn) {
-            full = dd_to_d(dd_add_d(d, -Pd.pn[i]));
+            full = dd_to_d(dd_add_d(d, -lpn[u]));
         } else {
             dd x = dd_sub(d, d0);
             full = dd_to_d(dd_sub(x, dd_round_half_up(x)));
         }
         rphase[oo + i] = full;
-        double w = S.weighted_mean ? Pd.isig[i] * Pd.isig[i] : 1.0;
+        double w = S.weighted_mean ? lw[u] * lw[u] : 1.0;
         sw += w;
         swx += w * full;
     }
@@ -515,29 +546,35 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     typedef double __attribute__((address_space(3))) ldsd;
     ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS);
     double c2 = 0.0;
-#pragma unroll 1
-    for (int j = 0; j < RES_RB / RES_BT; j++) {
+    // the thread's four rows loaded up front (one load latency per block, not one per row)
+    constexpr int RPT = RES_RB / RES_BT;
+    double lr[RPT], lf[RPT], ls[RPT];
+    double4_t lz[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+        const int i = r0 + threadIdx.x + j * RES_BT;
+        const bool in = i < r1;
+        lr[j] = in ? rphase[oo + i] : 0.0;
+        lf[j] = in ? ftay[ro + i] : 1.0;
+        ls[j] = in ? Pd.isig[i] : 0.0;
+        lz[j] = (harm && in) ? ((gptr<double4_t>)Pd.red_cs)[i] : double4_t{1.0, 0.0, 1.0, 0.0};
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
         const int i = r0 + threadIdx.x + j * RES_BT;
         double wr = 0.0;
         if (i < r1) {
-            double p = rphase[oo + i] - mean;
+            double p = lr[j] - mean;
             rphase[oo + i] = p;
-            double rt = p / ftay[ro + i];  // calc_time_resids (residuals.py:483-538)
+            double rt = p / lf[j];  // calc_time_resids (residuals.py:483-538)
             rtime[oo + i] = rt;
-            const double is = Pd.isig[i];
+            const double is = ls[j];
             double z = rt * is;
             c2 += z * z;
             wr = z * is;
         }
         if (tile) {  // (block-uniform)
-            double c1 = 1.0, s1 = 0.0, c8 = 1.0, s8 = 0.0;
-            if (harm && i < r1) {
-                const double4_t zz = ((gptr<double4_t>)Pd.red_cs)[i];
-                c1 = zz[0];
-                s1 = zz[1];
-                c8 = zz[2];
-                s8 = zz[3];
-            }
+            const double c1 = lz[j][0], s1 = lz[j][1], c8 = lz[j][2], s8 = lz[j][3];
             double ca = wr, sa = 0.0, cb = 1.0, sb = 0.0;
 #pragma unroll
             for (int a = 0; a < 8; a++) {
@@ -2420,23 +2457,31 @@ __device__ double block_max(double v, double* sh) {
 // r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
 // the block is overwritten by L^-1 (zeros above the diagonal).  Returns false if not
 // positive definite.
-// 1/sqrt(d) as v_rsq_f64 + two Newton steps: within 1 ulp like the library rsqrt (max 0.993
-// vs 0.987 ulp over 1e6 pivots in (1e-8, 4]) at 52 instead of 67 cycles of dependent latency
-// (bench/rsq_probe.hip); the Cholesky pivot chain is serial, so the latency is what counts
-__device__ __forceinline__ double rsq2(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
-    return __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
+// 1/sqrt(d) as v_rsq_f64 + one Newton step: the hardware estimate alone is off by up to 2.4e8
+// ulp, one step brings it to <= 19 ulp (4e-15 relative; two steps: 0.99 ulp at 14 more
+// cycles of dependent latency per pivot, bench/rsq_probe.hip).  A pivot's 4e-15 scales its
+// column of L and of L^-1 alike, a backward error of the order of the factorisation's own
+// rounding (~n eps); the ill-conditioned solves are refined against the Gram in dd anyway
+__device__ __forceinline__ double rsq1(double d) {
+    const double y = __builtin_amdgcn_rsq(d);
+    return __builtin_fma(y, __builtin_fma(-(0.5 * d) * y, y, 0.5), y);
 }
 
 __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
     // Cholesky (lane r holds row r) and X = L^-1 (lane r its column r) in one pass: pivot j's
-    // column L[c][j] is broadcast once (v_readlane) and used by both the trailing update of A
-    // and the forward substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the
-    // same operations and rounding as a separate substitution after the factorisation, with
-    // half the lane reads)
+    // scaled column L[.][j] goes through LDS (lanes 0..15 write it, every lane reads it back
+    // with uniform-address loads) and is used by both the trailing update of A and the forward
+    // substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the same operations and
+    // rounding as a separate substitution after the factorisation).  Broadcasting it with
+    // v_readlane instead put every L[c][j] in an SGPR pair and the compiler, hoisting them
+    // across pivots, spilled SGPRs to VGPR lanes: 1356 instructions against 914 per block,
+    // 8278 against 5958 s_memtime units per factor (with the one-step rsqrt;
+    // bench/diag_probe.hip)
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) double ldsd;
+    typedef __attribute__((address_space(3))) dv2 ldsd2;
+    __shared__ double colbuf[16];
     double a[16], x[16];
 #pragma unroll
     for (int c = 0; c < 16; c++) {
@@ -2448,15 +2493,26 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     for (int j = 0; j < 16; j++) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
-        const double il = rsq2(djj);
+        const double il = rsq1(djj);
         a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
         x[j] *= il;
+        if (lane < 16) ((ldsd*)colbuf)[lane] = a[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double Lc[16];
+#pragma unroll
+        for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
+            const dv2 v = ((ldsd2*)colbuf)[c2];
+            Lc[2 * c2] = v.x;
+            Lc[2 * c2 + 1] = v.y;
+        }
 #pragma unroll
         for (int c = j + 1; c < 16; c++) {
-            const double Lcj = rdlane(a[j], c);
-            a[c] -= a[j] * Lcj;
-            x[c] -= Lcj * x[j];
+            a[c] -= a[j] * Lc[c];
+            x[c] -= Lc[c] * x[j];
         }
+        __builtin_amdgcn_wave_barrier();  // the next pivot's column store after these reads
     }
     if (lane < 16) {
 #pragma unroll
@@ -2830,6 +2886,64 @@ __device__ __forceinline__ void w_from_xu(double* A, int nbd, int nbk, int nblkS
     }
 }
 
+// the DMX parameters' errors: sqrt of C_xx's diagonal D^-1 + D^-1 |W_a|^2 (normalised), a lane
+// quad per DMX column (W in the U blocks of A)
+template <int NW>
+__device__ __forceinline__ void dmx_errors(const double* A, const double* inx, const double* Dn, const PsrDev& Pd,
+                                           double* __restrict__ errs, int ndc, int nbd, int nbk, int nblkS) {
+    const int g0 = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    for (int a = g0; a < ndc; a += NW * 16) {
+        double sw = 0.0;
+        for (int rr = sub; rr < nbd * 16; rr += 4) {
+            const double w = A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
+            sw += w * w;
+        }
+        sw += __shfl_xor(sw, 1, 64);
+        sw += __shfl_xor(sw, 2, 64);
+        if (sub == 0) errs[Pd.xorig[a]] = sqrt(1.0 / Dn[a] + sw / Dn[a]) * inx[a];
+    }
+}
+
+// pint_fit_step_apply: k_apply's work at the end of the solve -- tables += lam * step (dd,
+// timing columns, Offset skipped) and the instance's constants of the updated table -- so a
+// GLS step (lambda 1) needs no separate apply launch.  Every thread of the workgroup calls it
+// (inst_setup_wave synchronises the block); the dynamic LDS (free after the solve's exports)
+// stages the spec header, the table, the lanes' exchange slots and the constants
+template <int NW>
+__device__ __forceinline__ void solve_apply_tail(const PsrDev& Pd, const InstDev& I, int inst, const double* dpars,
+                                                 double* __restrict__ tables, InstConst* __restrict__ ic, double lam,
+                                                 double* lds) {
+    const pint_spec_t& Sg = *Pd.spec;
+    const int tid = threadIdx.x, ncol = Sg.ncol, ts = Sg.tstride;
+    double* P = tables + I.toff;
+    __syncthreads();  // dpars of every thread written; the solve's LDS free
+    for (int c = tid; c < ncol; c += NW * 64) {
+        const int o = Sg.col_toff[c];
+        if (o < 0 || lam == 0.0) continue;
+        const dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam * dpars[I.coff + c]);
+        P[o] = v.hi;
+        P[o + 1] = v.lo;
+    }
+    __syncthreads();
+    double* sS = lds;
+    double* sP = sS + PREP_HDR;
+    double* sx = sP + ts;
+    InstConst* sC = reinterpret_cast<InstConst*>(sx + 16);
+    const double* hg = reinterpret_cast<const double*>(&Sg);
+    for (int i = tid; i < PREP_HDR; i += NW * 64) sS[i] = hg[i];
+    for (int i = tid; i < ts; i += NW * 64) sP[i] = P[i];
+    __syncthreads();
+    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(sS), sP, *sC, sx, tid);
+    __syncthreads();
+    const int* cs = reinterpret_cast<const int*>(sC);
+    int* cd = reinterpret_cast<int*>(ic + inst);
+    for (int k = tid; k < (int)(sizeof(InstConst) / 4); k += NW * 64) cd[k] = cs[k];
+}
+// dynamic LDS (bytes) solve_apply_tail needs for a table of tstride doubles
+static inline size_t apply_tail_lds(int tstride) {
+    return sizeof(double) * ((size_t)PREP_HDR + tstride + 16) + sizeof(InstConst) + 16;
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
@@ -2839,7 +2953,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        double* __restrict__ errs, double* __restrict__ cov,
                                                        double* __restrict__ chi2lin, double* __restrict__ sigL,
                                                        int* __restrict__ status, int fuse_sigma, int refine,
-                                                       double* __restrict__ xw, const double* __restrict__ ones) {
+                                                       double* __restrict__ xw, const double* __restrict__ ones,
+                                                       double* __restrict__ apply_tables, InstConst* __restrict__ apply_ic,
+                                                       double apply_lam) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[NW];
@@ -3031,11 +3147,10 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sy += __shfl_xor(sy, 2, 64);
         if (sub == 0) yv[g] = sy;
     }
-    // deferred covariance (xw): W = X U, the DMX errors and the covariance blocks are formed by
-    // k_cov_dmx at the read, off the step's critical path; the step needs only
-    // z = W^T y = U^T X^T y = U^T x_d, so U stays in LDS as it is
-    const bool defer = xw != nullptr;
-    if (!defer) w_from_xu<NW>(A, nbd, nbk, nblkS, wave, lane);  // W = X U in place of U
+    // the step needs only z = W^T y = U^T X^T y = U^T x_d, so U stays in LDS as it is: W = X U
+    // (for the DMX errors and the covariance) is formed after the step, here or -- deferred
+    // solves (xw) -- by k_cov_dmx at the read, off the step's critical path; both orders give
+    // the same bits
     __syncthreads();
     TS(4);
     // ---- x_d = X^T y ; errors of the dense columns ----
@@ -3058,28 +3173,19 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             amax = fmax(amax, Gd(g, g) * (ind[g] * ind[g]));
         }
     }
-    if (defer) __syncthreads();  // x_d visible: z = U^T x_d below
-    // ---- z = W^T y (= U^T x_d when deferred), x_x = D^-1 b_x - D^-1/2 z ; DMX errors ----
+    __syncthreads();  // x_d visible: z = U^T x_d below
+    // ---- z = U^T x_d, x_x = D^-1 b_x - D^-1/2 z ----
     for (int a = g0; a < ndc; a += NW * 16) {
-        double sz = 0.0, sw = 0.0;
-        for (int rr = sub; rr < nbd * 16; rr += 4) {
-            const double w = A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
-            sz += w * (defer ? (rr < Kd ? xd[rr] : 0.0) : yv[rr]);
-            sw += w * w;
-        }
+        double sz = 0.0;
+        for (int rr = sub; rr < Kd; rr += 4) sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * xd[rr];
         sz += __shfl_xor(sz, 1, 64);
         sz += __shfl_xor(sz, 2, 64);
-        if (!defer) {
-            sw += __shfl_xor(sw, 1, 64);
-            sw += __shfl_xor(sw, 2, 64);
-        }
         if (sub == 0) {
             const double d = Dn[a];
             xx[a] = bx[a] / d - sz * isd[a];
-            // deferred: the DMX errors come from k_cov_dmx (they need W); diag(A^-1) >= 1/d
-            // keeps the condition estimate a lower bound
-            if (!defer) errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / d + sw / d) * inx[a];
-            vmax = fmax(vmax, defer ? 1.0 / d : (1.0 + sw) / d);
+            // the DMX entries of diag(A^-1) are (1 + |W_a|^2) / d >= 1 / d: the estimate stays a
+            // lower bound without W
+            vmax = fmax(vmax, 1.0 / d);
             amax = fmax(amax, d);
         }
     }
@@ -3090,7 +3196,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     __syncthreads();
     // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
     // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
-    // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y, W^T y = U^T dx_d when deferred).  The explicit
+    // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y with W^T y = U^T dx_d).  The explicit
     // L^-1 loses ~cond(L) digits that LAPACK's triangular solves keep (cho_solve,
     // fitter.py:2197) ----
     auto Ad = [&](int i, int j) {
@@ -3146,15 +3252,13 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             s1 += __shfl_xor(s1, 2, 64);
             if (sub == 0) {
                 xd[g] += s1;
-                rd[g] = s1;  // dx_d (rd is consumed): U^T dx_d below when deferred
+                rd[g] = s1;  // dx_d (rd is consumed): U^T dx_d below
             }
         }
-        if (defer) __syncthreads();
+        __syncthreads();
         for (int a = g0; a < ndc; a += NW * 16) {
             double sz = 0.0;
-            for (int rr = sub; rr < nbd * 16; rr += 4)
-                sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] *
-                      (defer ? (rr < Kd ? rd[rr] : 0.0) : yv[rr]);
+            for (int rr = sub; rr < Kd; rr += 4) sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * rd[rr];
             sz += __shfl_xor(sz, 1, 64);
             sz += __shfl_xor(sz, 2, 64);
             if (sub == 0) xx[a] += rx[a] / Dn[a] - sz * isd[a];
@@ -3186,10 +3290,16 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             o[na + nbd * 16 + nbk * 16 + e] = isd[e];
             o[na + nbd * 16 + 2 * nbk * 16 + e] = Dn[e];
         }
-        return;
+    } else {
+        // in the kernel: W = X U in place of U, the DMX errors (C_xx's diagonal D^-1 + D^-1
+        // |W_a|^2) and the covariance blocks, as k_cov_dmx forms them
+        w_from_xu<NW>(A, nbd, nbk, nblkS, wave, lane);
+        __syncthreads();
+        dmx_errors<NW>(A, inx, Dn, Pd, errs + I.coff, ndc, nbd, nbk, nblkS);
+        cov_dmx_blocks(A, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, ncol, red0, ndc, nbd, nbk, nblkS, wave, NW, lane);
     }
-    cov_dmx_blocks(A, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, ncol, red0, ndc, nbd, nbk, nblkS, wave, NW, lane);
     TS(6);
+    if (apply_tables) solve_apply_tail<NW>(Pd, I, inst, dpars, apply_tables, apply_ic, apply_lam, lds);
 }
 
 // k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred
@@ -3220,19 +3330,7 @@ __global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ 
     const double* Dn = isd + nbk * 16;
     w_from_xu<NW>(lds, nbd, nbk, nblkS, wave, lane);
     __syncthreads();
-    if (blockIdx.y == 0 && errs) {  // DMX errors: C_xx's diagonal D^-1 + D^-1 |W_a|^2
-        const int g0 = threadIdx.x >> 2, sub = threadIdx.x & 3;
-        for (int a = g0; a < ndc; a += NW * 16) {
-            double sw = 0.0;
-            for (int rr = sub; rr < nbd * 16; rr += 4) {
-                const double w = lds[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)];
-                sw += w * w;
-            }
-            sw += __shfl_xor(sw, 1, 64);
-            sw += __shfl_xor(sw, 2, 64);
-            if (sub == 0) errs[I.coff + Pd.xorig[a]] = sqrt(1.0 / Dn[a] + sw / Dn[a]) * inx[a];
-        }
-    }
+    if (blockIdx.y == 0 && errs) dmx_errors<NW>(lds, inx, Dn, Pd, errs + I.coff, ndc, nbd, nbk, nblkS);
     if (cov)
         cov_dmx_blocks(lds, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, Pd.spec->ncol, red0, ndc, nbd, nbk, nblkS,
                        blockIdx.y * NW + wave, gridDim.y * NW, lane);
@@ -3583,9 +3681,16 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
         // the dots from k_resid2's trig tiles (one per residual block of the instance, summed
         // in block order): F_j^T W r (sin, cos of harmonic h + 1 at 2h, 2h + 1), r^T W r (the
         // residual pass's chi2) at R, 1^T W r = D[0][0] at R + 1 -- k_wdot's layout, one split
-        double v = 0.0;
-        for (int k = 0; k < I.nrb; k++) v += wtile[(long)(I.rb0 + k) * 256 + threadIdx.x];
-        Dt[threadIdx.x] = v;
+        // the instance's block tiles summed in block order in four interleaved chains (four
+        // loads in flight instead of one dependent load per block), combined in a fixed order
+        double v4[4] = {0.0, 0.0, 0.0, 0.0};
+        int k = 0;
+        for (; k + 4 <= I.nrb; k += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) v4[u] += wtile[(long)(I.rb0 + k + u) * 256 + threadIdx.x];
+        }
+        for (; k < I.nrb; k++) v4[0] += wtile[(long)(I.rb0 + k) * 256 + threadIdx.x];
+        Dt[threadIdx.x] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
         __syncthreads();
         for (int h = threadIdx.x; h < R / 2; h += blockDim.x) {
             const int k = h + 1, a = k & 7, b = k >> 3;
@@ -4007,8 +4112,8 @@ struct pint_ctx {
     int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
     int timing_every = 1;   // PINT_OPT_TIMING_EVERY: Gram events on every k-th fit step
     long gram_calls = 0;
-    hipGraph_t graph = nullptr;          // a captured launch sequence (pint_capture_*)
-    hipGraphExec_t graph_exec = nullptr;
+    hipGraph_t graph_s[2] = {nullptr, nullptr};          // a captured launch sequence per pipeline
+    hipGraphExec_t graph_exec_s[2] = {nullptr, nullptr};  // slot (pint_capture_*, pint_graph_launch)
     bool capturing = false;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
@@ -4036,6 +4141,11 @@ struct pint_ctx {
     size_t eig_cap = 0;
     int degv_cap = 0;
     InstConst* d_ic = nullptr;  // per-instance constants (k_prep)
+    InstConst* d_ic0 = nullptr; // the constants of the table snapshot (pint_save_tables)
+    bool apply_req = false;     // pint_fit_step_apply: fuse the apply into the solve if possible
+    bool apply_done = false;    //   ... and it was fused
+    double apply_lam = 1.0;
+    bool ic0_valid = false;
     double *d_dmxv = nullptr, *d_Sd = nullptr, *d_DD = nullptr, *d_DCS = nullptr;  // sparse-DMX layout
     double* d_dfac = nullptr;  // PLDMNoise basis scale per TOA row (only with PLDMNoise pulsars)
     int max_ndc = 0;
@@ -4328,9 +4438,15 @@ pint_ctx* pint_ctx_create(int device) {
     }
     hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
-    hipEventCreateWithFlags(&ctx->ev_solved, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ctx->ev_copied, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ctx->ev_noise, hipEventDisableTiming);
+    // the cross-stream events are waited on by the device (and ev_done by the host only for
+    // completion: everything the host reads comes through copies covered by ev_cdone), so they
+    // release to device scope: the default system-scope release writes back the caches and
+    // idled the stream ~4-8 us at each such event, measured (PINT_EV_SYSTEM=1 restores it)
+    const unsigned evf = hipEventDisableTiming |
+                         ((getenv("PINT_EV_SYSTEM") && atoi(getenv("PINT_EV_SYSTEM"))) ? 0u : hipEventReleaseToDevice);
+    hipEventCreateWithFlags(&ctx->ev_solved, evf);
+    hipEventCreateWithFlags(&ctx->ev_copied, evf);
+    hipEventCreateWithFlags(&ctx->ev_noise, evf);
     // PINT_SERIAL=1 (profiling aid): side-stream kernels run on the main stream, so
     // rocprof's per-kernel durations are not inflated by concurrent kernels
     if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
@@ -4341,11 +4457,11 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->cov_defer = getenv("PINT_COV_DEFER") ? atoi(getenv("PINT_COV_DEFER")) : 1;  // 0 off, 1 batches, 2 always
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     ctx->gv_pair = getenv("PINT_GV_PAIR") ? atoi(getenv("PINT_GV_PAIR")) : 1;
-    hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ctx->ev_sigma, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ctx->ev_gram, evf);
+    hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < 2; sl++) {
         for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev_slot[sl][i]);
-        hipEventCreateWithFlags(&ctx->ev_done[sl], hipEventDisableTiming);
+        hipEventCreateWithFlags(&ctx->ev_done[sl], evf);
         hipEventCreateWithFlags(&ctx->ev_cdone[sl], hipEventDisableTiming);
     }
     hipMalloc(&ctx->d_status_slots, 2 * sizeof(int));
@@ -4372,7 +4488,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_lam, (void**)&ctx->d_chi2g_s[0], (void**)&ctx->d_chi2g_s[1], (void**)&ctx->d_lognorm,
                    (void**)&ctx->d_eigw,
                    (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
-                   (void**)&ctx->d_eW, (void**)&ctx->d_eC, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic,
+                   (void**)&ctx->d_eW, (void**)&ctx->d_eC, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic, (void**)&ctx->d_ic0,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
@@ -4383,12 +4499,15 @@ static void free_instances(pint_ctx* ctx) {
     ctx->copy_pend[0] = ctx->copy_pend[1] = false;
     ctx->noise_cap = 0;
     ctx->tables0_cap = 0;
+    ctx->ic0_valid = false;
     ctx->restore_pending = false;
     ctx->wfuse = ctx->wtile_valid = false;
-    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
-    if (ctx->graph) hipGraphDestroy(ctx->graph);
-    ctx->graph_exec = nullptr;
-    ctx->graph = nullptr;
+    for (int k = 0; k < 2; k++) {
+        if (ctx->graph_exec_s[k]) hipGraphExecDestroy(ctx->graph_exec_s[k]);
+        if (ctx->graph_s[k]) hipGraphDestroy(ctx->graph_s[k]);
+        ctx->graph_exec_s[k] = nullptr;
+        ctx->graph_s[k] = nullptr;
+    }
     ctx->ninst = 0;
     ctx->wpart_cap = 0;
     ctx->eig_cap = 0;
@@ -5125,7 +5244,7 @@ int pint_set_tables(pint_ctx* ctx, const double* tables) {
 static const int kTimingPairs[pint_ctx::NMS][2] = {{0, 1}, {4, 5}, {6, 7}, {7, 8}, {2, 3}, {10, 11}, {12, 13}, {14, 15}};
 
 static void record(pint_ctx* ctx, int i, hipStream_t st = nullptr) {
-    if (ctx->no_events) return;
+    if (ctx->no_events || ctx->capturing) return;  // no timing events inside a graph
     bool on = false;  // only the events of the enabled timing slots (each costs device time)
     for (int k = 0; k < pint_ctx::NMS; k++)
         if ((ctx->timing_mask >> k) & 1) on |= kTimingPairs[k][0] == i || kTimingPairs[k][1] == i;
@@ -5191,11 +5310,22 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         }
     }
     record(ctx, want_M ? 2 : 0);
-    if (!ctx->ic_valid) {  // k_apply refreshes them itself
-        hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
+    const double* tabs = ctx->d_tables;
+    const InstConst* icp = ctx->d_ic;
+    EvalRestore rs{nullptr, nullptr};
+    if (!ctx->ic_valid) {  // (k_apply refreshes them itself)
+        if (ctx->restore_pending && ctx->ic0_valid) {
+            // restore: the evaluation reads the snapshot and its constants (pint_save_tables) and
+            // each instance's first block writes them back -- no k_prep launch in a refit step
+            tabs = ctx->d_tables0;
+            icp = ctx->d_ic0;
+            rs = EvalRestore{ctx->d_tables, ctx->d_ic};
+        } else {
+            hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
+            HIPCHK(hipGetLastError());
+        }
         ctx->restore_pending = false;
-        HIPCHK(hipGetLastError());
         ctx->ic_valid = true;
     }
     const bool mix = (ctx->eval_merge >> (want_M ? 1 : 0)) & 1;
@@ -5203,18 +5333,18 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 #define PINT_EVAL_MIX(WM)                                                                                      \
         hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
-                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac)
+                           tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs)
         if (want_M && ctx->eval_wpe == 3) {
             hipLaunchKernelGGL((k_eval_mix_w<1, 3>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],
-                               ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
-                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac);
+                               tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
+                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs);
         } else if (want_M && ctx->eval_wpe == 4) {
             hipLaunchKernelGGL((k_eval_mix_w<1, 4>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],
-                               ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
-                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac);
+                               tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
+                               ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs);
         } else if (want_M) PINT_EVAL_MIX(1); else PINT_EVAL_MIX(0);
 #undef PINT_EVAL_MIX
         HIPCHK(hipGetLastError());
@@ -5229,8 +5359,8 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         const int* br = ctx->d_blk_row0 + ctx->blk_off[t];
 #define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
         hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
-                           ctx->d_tables, ctx->d_ic, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
-                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac)
+                           tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
+                           ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs)
         if (want_M) {
             switch (t) {
                 case 0: PINT_EVAL_LAUNCH(1, 0); break;
@@ -5433,7 +5563,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     // pair still costs the stream a few us; the average over the sampled launches is the
     // kernel's time)
     const bool sampled = ctx->timing_every <= 1 || (ctx->gram_calls++ % ctx->timing_every) == 0;
-    const bool gram_t = !ctx->no_events && ((ctx->timing_mask >> 6) & 1) && sampled;
+    const bool gram_t = !ctx->no_events && !ctx->capturing && ((ctx->timing_mask >> 6) & 1) && sampled;
     const bool ext_t = gram_t && vgp && (cmp ? ctx->kp_groups_c : ctx->kp_groups).empty() &&
                        !ctx->kp_groups_v.empty();
     const bool gram_mark = sampled && !ext_t;  // marker-packet events (the other Gram paths)
@@ -5537,7 +5667,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             if (blk > SD_MAXBLK || nbd > 17 || nbs > BS_MAXNB) dmx_ok = false;
             lds_x = std::max(lds_x, sizeof(double) * ((size_t)std::max(blk, nbs * (nbs + 1) / 2) * 256 +
                                                       (size_t)(5 * nbd + 6 * nbk) * 16));
-            if (lds_x > 160 * 1024) dmx_ok = false;
+            if (lds_x > 160 * 1024 - 512) dmx_ok = false;  // (the kernel's static LDS beside it)
         } else {
             Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
         }
@@ -5613,14 +5743,36 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                          ? ctx->d_xw : nullptr;
         // when it is the last solve kernel, ev_solved rides on its dispatch packet (a separate
         // event record is a marker packet between kernels: ~6-10 us of idle stream, measured)
-        solved_ev = Ks == 0 ? ctx->ev_solved : nullptr;
+        // (in a graph capture: a plain event record, the cross-stream edge of the capture)
+        solved_ev = (Ks == 0 && !ctx->capturing) ? ctx->ev_solved : nullptr;
+        // pint_fit_step_apply: the apply at the end of the solve when every instance is solved
+        // here on the generated-Fourier path (whose Woodbury Sigma does not read F0 from the
+        // table the apply rewrites)
+        double* apply_tab = nullptr;
+        InstConst* apply_ic = nullptr;
+        size_t lds_dyn = fuse_sigma ? std::max(lds_x, lds_s) : lds_x;
+        if (ctx->apply_req && Ks == 0 && !side_sigma && !do_sigma) {
+            bool ok = true;
+            int maxts = 0;
+            for (auto& I : ctx->inst) {
+                const PsrHost& ph = ctx->psrs[I.psr];
+                ok = ok && cmp && ph.dev.dsplit && ph.dev.vg;
+                maxts = std::max(maxts, ph.spec.tstride);
+            }
+            if (ok && apply_tail_lds(maxts) <= 160 * 1024 - 512) {
+                apply_tab = ctx->d_tables;
+                apply_ic = ctx->d_ic;
+                lds_dyn = std::max(lds_dyn, apply_tail_lds(maxts));
+                ctx->apply_done = true;
+            }
+        }
         hipExtLaunchKernelGGL((k_solve_dmx<16>), dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
-                              (uint32_t)(fuse_sigma ? std::max(lds_x, lds_s) : lds_x), ctx->stream, nullptr, solved_ev, 0u,
+                              (uint32_t)lds_dyn, ctx->stream, nullptr, solved_ev, 0u,
                               (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_tables,
                               (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
                               (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
                               ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                              fuse_sigma, ctx->refine, xw, ones);
+                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam);
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -5770,6 +5922,27 @@ int pint_apply_step_uniform(pint_ctx* ctx, double lambda_) {
     return PINT_OK;
 }
 
+// A fit step followed by tables += lambda * step (pint_fit_step + pint_apply_step_uniform):
+// when every instance takes the DMX-eliminated solve on the generated-Fourier path, the
+// apply and the new table's per-instance constants are formed at the end of the solve
+// kernel (solve_apply_tail) instead of in a k_apply launch.  The step's outputs (pint_read_step,
+// pint_noise_resids) read the step, not the tables, so they may follow.
+int pint_fit_step_apply(pint_ctx* ctx, int mode, double lambda_) {
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    ctx->apply_req = true;
+    ctx->apply_lam = lambda_;
+    ctx->apply_done = false;
+    const int rc = pint_fit_step(ctx, mode);
+    ctx->apply_req = false;
+    if (rc != PINT_OK) return rc;
+    if (ctx->apply_done) {
+        ctx->apply_done = false;
+        ctx->ic_valid = true;
+        return PINT_OK;
+    }
+    return pint_apply_step_uniform(ctx, lambda_);
+}
+
 // Parameter tables resident on the device: pint_save_tables snapshots the current tables,
 // pint_restore_tables puts the snapshot back (a device copy on the stream), e.g. to start
 // every fit of a benchmark loop from the same initial models without a host->device upload.
@@ -5784,6 +5957,12 @@ int pint_save_tables(pint_ctx* ctx) {
     }
     HIPCHK(hipMemcpyAsync(ctx->d_tables0, ctx->d_tables, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToDevice,
                           ctx->stream));
+    // the snapshot's per-instance constants, so a restore needs no k_prep (pint_eval)
+    if (!ctx->d_ic0) HIPCHK(cmalloc((void**)&ctx->d_ic0, sizeof(InstConst) * ctx->ninst));
+    hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                       ctx->d_tables0, (const double*)nullptr, ctx->d_ic0);
+    HIPCHK(hipGetLastError());
+    ctx->ic0_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -5937,19 +6116,23 @@ int pint_capture_end(pint_ctx* ctx) {
     ctx->capturing = false;
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamEndCapture(ctx->stream, &g));
-    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
-    if (ctx->graph) hipGraphDestroy(ctx->graph);
-    ctx->graph = g;
-    ctx->graph_exec = nullptr;
-    HIPCHK(hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0));
+    const int s = ctx->slot;  // the graph writes this slot's outputs, status word and pinned buffers
+    if (ctx->graph_exec_s[s]) hipGraphExecDestroy(ctx->graph_exec_s[s]);
+    if (ctx->graph_s[s]) hipGraphDestroy(ctx->graph_s[s]);
+    ctx->graph_s[s] = g;
+    ctx->graph_exec_s[s] = nullptr;
+    HIPCHK(hipGraphInstantiate(&ctx->graph_exec_s[s], g, nullptr, nullptr, 0));
     return PINT_OK;
 }
 
 int pint_graph_launch(pint_ctx* ctx) {
-    if (!ctx || !ctx->graph_exec) return PINT_E_INVALID;
+    if (!ctx || !ctx->graph_exec_s[ctx->slot]) {
+        if (ctx) ctx->err = "pint_graph_launch: no graph captured for this pipeline slot";
+        return PINT_E_INVALID;
+    }
     hipSetDevice(ctx->device);
     join_side_streams(ctx);
-    HIPCHK(hipGraphLaunch(ctx->graph_exec, ctx->stream));
+    HIPCHK(hipGraphLaunch(ctx->graph_exec_s[ctx->slot], ctx->stream));
     return PINT_OK;
 }
 

@@ -549,6 +549,12 @@ class Session:
     def fit_step(self, mode):
         self._check(self.L.pint_fit_step(self.ctx, int(mode)))
 
+    def fit_step_apply(self, mode, lam=1.0):
+        """fit_step(mode) then apply_step_uniform(lam) (pint_fit_step_apply: fused into the
+        solve kernel when every instance allows it).  read_step / noise_resids may follow:
+        they read the step, not the tables."""
+        self._check(self.L.pint_fit_step_apply(self.ctx, int(mode), float(lam)))
+
     def apply_step(self, lam):
         lam = np.broadcast_to(np.asarray(lam, dtype=np.float64), (len(self.inst_layout),))
         if self.lazy and "lambda" not in self._inflight:

@@ -606,6 +606,113 @@ def test_graph_replay_matches_direct():
     s.close()
 
 
+def test_pipelined_graph_steps_match_enqueued():
+    """The bench's step (restore the initial tables, evaluate with M, GLS fit, read the fit
+    outputs and the noise realisations, apply, evaluate, GLS chi2) captured once per pipeline
+    slot and replayed two deep (pint_graph_launch + step_end / check_step) gives the same
+    outputs, bit for bit, as the same step enqueued launch by launch -- including the
+    deferred W = XU / DMX errors / covariance of k_cov_dmx on the copy stream."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+    s = Session()
+    lays = [s.add(build_layout(m, t)) for m, t in items]
+    s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+    s.save_tables()
+    s.set_lazy(True)
+    s.set_timing_mask(0)
+
+    def step():
+        s.restore_tables()
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        out = s.read_step()
+        nz = s.noise_resids()
+        s.apply_step_uniform(1.0)
+        s.eval(want_M=False)
+        return out, nz, s.chi2_gls()
+
+    def snap(res):
+        (dp, er, cov, cl), nz, c2 = res
+        return ([x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov]
+                + [cl.copy(), c2.copy()] + [np.asarray(v).copy() for k in range(len(lays)) for v in nz[k].values()])
+
+    want = []
+    for _ in range(2):  # enqueued, one slot each
+        r = step()
+        s.check_step(s.step_end())
+        want.append(snap(r))
+    caps = {}
+    for _ in range(2):
+        slot = s._slot
+        caps[slot] = s.capture(step)
+        s.check_step(s.step_end())
+    got, prev = [], None
+    for k in range(4):
+        slot = s._slot
+        s.replay()
+        cur = s.step_end()
+        if prev is not None:
+            s.check_step(prev[0])
+            got.append(snap(caps[prev[1]]))
+        prev = (cur, slot)
+    s.check_step(prev[0])
+    got.append(snap(caps[prev[1]]))
+    for g in got:
+        assert len(g) == len(want[0])
+        for x, y in zip(want[0], g):
+            assert np.array_equal(x, y)
+    s.close()
+
+
+def test_fit_step_apply_matches_separate_apply():
+    """pint_fit_step_apply (the full-step update and the new tables' constants formed at the
+    end of the solve kernel) gives the same tables, step outputs, noise realisations and
+    post-fit GLS chi2, bit for bit, as pint_fit_step followed by the k_apply launch, lazy or
+    not; a step from the restored snapshot (the evaluation reads the snapshot and its saved
+    constants, no k_prep launch) repeats the first step exactly."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+
+    def run(fused, lazy):
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.save_tables()
+        if lazy:
+            s.set_lazy(True)
+        res = []
+        for _ in range(2):  # the second step starts from the restored snapshot
+            s.restore_tables()
+            s.eval(want_M=Session.FIT)
+            if fused:
+                s.fit_step_apply(1, 1.0)
+            else:
+                s.fit_step(1)
+            dp, er, cov, cl = s.read_step()
+            nz = s.noise_resids()
+            if not fused:
+                s.apply_step_uniform(1.0)
+            s.eval(want_M=False)
+            c2 = s.chi2_gls()
+            if lazy:
+                s.check()
+            res.append([x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov] +
+                       [np.array(cl, copy=True), np.array(c2, copy=True), s.read_tables_flat()] +
+                       [np.asarray(v).copy() for k in range(len(lays)) for v in nz[k].values()])
+        s.close()
+        return res
+
+    base = run(False, False)
+    for fused, lazy in ((True, False), (True, True), (False, True)):
+        got = run(fused, lazy)
+        for a, b in zip(base, got):
+            assert len(a) == len(b)
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), (fused, lazy)
+    for x, y in zip(base[0], base[1]):  # the second step, from the restored snapshot, repeats the first
+        assert np.array_equal(x, y)
+
+
 def test_pipelined_steps_match_synchronous():
     """Steps pipelined two deep (Session.step_end / check_step: step k+1 enqueued before the
     host waits for step k, per-slot pinned outputs and status words) give bit-identical
