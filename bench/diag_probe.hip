@@ -6,7 +6,10 @@
 //   1  the same arithmetic with a scheduling barrier after each pivot (no cross-pivot
 //      hoisting: the broadcasts of one pivot live in SGPRs at a time),
 //   2  variant 1 with one Newton step on v_rsq_f64 instead of two,
-//   3  the pivot column broadcast through LDS (VGPR operands), 4: that with one Newton step.
+//   3  the pivot column broadcast through LDS (VGPR operands), 4: that with one Newton step,
+//   5  variant 3 with a scheduling barrier after each pivot,
+//   6  two waves: the factorisation (readlane) and the inverse (LDS columns) one pivot apart.
+// The kernel is compiled with the 1024-thread register budget of the solves (128 VGPRs).
 // Prints the max error of L^-1 against a long-double Cholesky inverse on the host (relative
 // to max |L^-1|) and the cycles per factor (s_memtime, 64 dependent factors in one wave).
 // Build: hipcc --offload-arch=gfx950 -O3 bench/diag_probe.hip -o build/diag_probe
@@ -66,7 +69,7 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
 
 // variant 3: the scaled pivot column goes through LDS (one ds_write by lanes 0..15, then
 // uniform-address reads: every lane gets L_cj in VGPRs, no SGPR broadcasts)
-template <int NEWTON>
+template <int NEWTON, bool SB = false>
 __device__ __forceinline__ bool diag_factor_lds(double* Akk, double* colbuf, int lane) {
     const int r = lane & 15;
     double a[16], x[16];
@@ -87,9 +90,7 @@ __device__ __forceinline__ bool diag_factor_lds(double* Akk, double* colbuf, int
         typedef double dv2 __attribute__((ext_vector_type(2)));
         typedef __attribute__((address_space(3))) dv2 ldsd2;
         if (lane < 16) ((ldsd*)colbuf)[lane] = a[j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         double Lc[16];
 #pragma unroll
         for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
@@ -103,6 +104,7 @@ __device__ __forceinline__ bool diag_factor_lds(double* Akk, double* colbuf, int
             x[c] -= Lc[c] * x[j];
         }
         __builtin_amdgcn_wave_barrier();
+        if (SB) __builtin_amdgcn_sched_barrier(0);
     }
     if (lane < 16) {
 #pragma unroll
@@ -111,18 +113,100 @@ __device__ __forceinline__ bool diag_factor_lds(double* Akk, double* colbuf, int
     return ok;
 }
 
+// variant 6: two waves.  Wave 0 factors (lane r holds row r of A, readlane broadcasts of the
+// scaled pivot column, as variant 1 without the x updates) and publishes each scaled column
+// L[.][j] in LDS with a counter; wave 1 forms X = L^-1 (lane r holds column r of X) from the
+// published columns as they arrive (uniform-address LDS loads), one pivot behind.
+__device__ __forceinline__ bool diag_factor2(double* Akk, double* colbuf, volatile int* cnt, int wave, int lane) {
+    const int r = lane & 15;
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) double ldsd;
+    typedef __attribute__((address_space(3))) dv2 ldsd2;
+    bool ok = true;
+    if (wave == 0) {
+        double a[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) a[c] = Akk[swz(r, c)];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const double djj = rdlane(a[j], j);
+            ok = ok && (djj > 0.0);
+            const double il = rsqn<2>(djj);
+            a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
+            if (lane < 16) ((ldsd*)colbuf)[16 * j + lane] = a[j];
+            colbuf[256 + j] = il;  // (uniform) the pivot's 1/L_jj for wave 1
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) *cnt = j + 1;
+#pragma unroll
+            for (int c = j + 1; c < 16; c++) {
+                const double Lcj = rdlane(a[j], c);
+                a[c] -= a[j] * Lcj;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else if (wave == 1) {
+        double x[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) x[c] = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            while (*cnt < j + 1) __builtin_amdgcn_s_sleep(1);
+            __asm__ volatile("" ::: "memory");
+            const double il = colbuf[256 + j];
+            x[j] *= il;
+            double Lc[16];
+#pragma unroll
+            for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
+                const dv2 v = ((ldsd2*)colbuf)[8 * j + c2];
+                Lc[2 * c2] = v.x;
+                Lc[2 * c2 + 1] = v.y;
+            }
+#pragma unroll
+            for (int c = j + 1; c < 16; c++) x[c] -= Lc[c] * x[j];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane < 16) {
+#pragma unroll
+            for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+        }
+    }
+    return ok;
+}
+
 template <int V>
 __device__ __forceinline__ bool factor_v(double* Akk, double* colbuf, int lane) {
-    if constexpr (V >= 3) return diag_factor_lds<V == 3 ? 2 : 1>(Akk, colbuf, lane);
+    if constexpr (V >= 5) return diag_factor_lds<2, true>(Akk, colbuf, lane);
+    else if constexpr (V >= 3) return diag_factor_lds<V == 3 ? 2 : 1>(Akk, colbuf, lane);
     else return diag_factor<V>(Akk, lane);
 }
 
 template <int V>
-__global__ __launch_bounds__(64) void k_diag(const double* __restrict__ in, double* __restrict__ out,
+__global__ __launch_bounds__(1024) void k_diag(const double* __restrict__ in, double* __restrict__ out,
                                              long long* __restrict__ cyc, int reps) {
     __shared__ double blk[256];
-    __shared__ double colbuf[16];
-    const int lane = threadIdx.x;
+    __shared__ double colbuf[16 * 16 + 16];
+    __shared__ int cnt;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if constexpr (V == 6) {  // two waves (128 threads); the other variants run on one
+        for (int e = threadIdx.x; e < 256; e += blockDim.x) blk[e] = in[e];
+        if (threadIdx.x == 0) cnt = 0;
+        __syncthreads();
+        bool ok6 = diag_factor2(blk, colbuf, &cnt, wave, lane);
+        __syncthreads();
+        for (int e = threadIdx.x; e < 256; e += blockDim.x) out[e] = blk[e];
+        __syncthreads();
+        long long t0 = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < reps; k++) {
+            for (int e = threadIdx.x; e < 256; e += blockDim.x) blk[e] = in[e] + (ok6 ? 0.0 : 1.0) * blk[e];
+            if (threadIdx.x == 0) cnt = 0;
+            __syncthreads();
+            ok6 &= diag_factor2(blk, colbuf, &cnt, wave, lane);
+            __syncthreads();
+        }
+        long long t1 = __builtin_amdgcn_s_memtime();
+        if (threadIdx.x == 0) cyc[0] = (t1 - t0) / reps;
+        return;
+    }
     for (int e = lane; e < 256; e += 64) blk[e] = in[e];
     __syncthreads();
     bool ok = factor_v<V>(blk, colbuf, lane);
@@ -187,12 +271,14 @@ int main() {
     hipMalloc(&dout, 256 * 8);
     hipMalloc(&dc, 8);
     hipMemcpy(din, A.data(), 256 * 8, hipMemcpyHostToDevice);
-    for (int v = 0; v < 5; v++) {
+    for (int v = 0; v < 7; v++) {
         if (v == 0) hipLaunchKernelGGL(k_diag<0>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 1) hipLaunchKernelGGL(k_diag<1>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 2) hipLaunchKernelGGL(k_diag<2>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 3) hipLaunchKernelGGL(k_diag<3>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 4) hipLaunchKernelGGL(k_diag<4>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 5) hipLaunchKernelGGL(k_diag<5>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 6) hipLaunchKernelGGL(k_diag<6>, dim3(1), dim3(128), 0, 0, din, dout, dc, 64);
         std::vector<double> o(256);
         long long c;
         hipMemcpy(o.data(), dout, 256 * 8, hipMemcpyDeviceToHost);

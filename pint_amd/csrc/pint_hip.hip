@@ -2063,6 +2063,16 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
                 // took 127 us), combined in a fixed tree order (deterministic)
                 double a[8] = {G[e], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 int q = 1;
+                // 32 partial loads in flight per round (a small batch has ~56 splits: one
+                // dependent load round per 8 partials was the kernel's latency), summed into
+                // the same eight chains in the same order
+                for (; q + 32 <= g.nparts; q += 32) {
+                    double t[32];
+#pragma unroll
+                    for (int u = 0; u < 32; u++) t[u] = G[(long)(q + u) * KK + e];
+#pragma unroll
+                    for (int u = 0; u < 32; u++) a[u & 7] += t[u];
+                }
                 for (; q + 8 <= g.nparts; q += 8) {
 #pragma unroll
                     for (int u = 0; u < 8; u++) a[u] += G[(long)(q + u) * KK + e];
@@ -2081,6 +2091,13 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
         } else {
             double a[4] = {cs[0], 0.0, 0.0, 0.0};
             int q = 1;
+            for (; q + 32 <= g.nsplit; q += 32) {  // (as above: same chains, same order)
+                double t[32];
+#pragma unroll
+                for (int u = 0; u < 32; u++) t[u] = cs[q + u];
+#pragma unroll
+                for (int u = 0; u < 32; u++) a[u & 3] += t[u];
+            }
             for (; q + 4 <= g.nsplit; q += 4) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) a[u] += cs[q + u];
@@ -2457,31 +2474,23 @@ __device__ double block_max(double v, double* sh) {
 // r, readlane broadcasts), then its inverse column by column (lane c solves L x = e_c);
 // the block is overwritten by L^-1 (zeros above the diagonal).  Returns false if not
 // positive definite.
-// 1/sqrt(d) as v_rsq_f64 + one Newton step: the hardware estimate alone is off by up to 2.4e8
-// ulp, one step brings it to <= 19 ulp (4e-15 relative; two steps: 0.99 ulp at 14 more
-// cycles of dependent latency per pivot, bench/rsq_probe.hip).  A pivot's 4e-15 scales its
-// column of L and of L^-1 alike, a backward error of the order of the factorisation's own
-// rounding (~n eps); the ill-conditioned solves are refined against the Gram in dd anyway
-__device__ __forceinline__ double rsq1(double d) {
-    const double y = __builtin_amdgcn_rsq(d);
-    return __builtin_fma(y, __builtin_fma(-(0.5 * d) * y, y, 0.5), y);
+// 1/sqrt(d) as v_rsq_f64 + two Newton steps: within 1 ulp like the library rsqrt (max 0.993
+// vs 0.987 ulp over 1e6 pivots in (1e-8, 4]) at 52 instead of 67 cycles of dependent latency
+// (bench/rsq_probe.hip); the Cholesky pivot chain is serial, so the latency is what counts
+__device__ __forceinline__ double rsq2(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
+    return __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
 }
 
 __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
     // Cholesky (lane r holds row r) and X = L^-1 (lane r its column r) in one pass: pivot j's
-    // scaled column L[.][j] goes through LDS (lanes 0..15 write it, every lane reads it back
-    // with uniform-address loads) and is used by both the trailing update of A and the forward
-    // substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the same operations and
-    // rounding as a separate substitution after the factorisation).  Broadcasting it with
-    // v_readlane instead put every L[c][j] in an SGPR pair and the compiler, hoisting them
-    // across pivots, spilled SGPRs to VGPR lanes: 1356 instructions against 914 per block,
-    // 8278 against 5958 s_memtime units per factor (with the one-step rsqrt;
-    // bench/diag_probe.hip)
-    typedef double dv2 __attribute__((ext_vector_type(2)));
-    typedef __attribute__((address_space(3))) double ldsd;
-    typedef __attribute__((address_space(3))) dv2 ldsd2;
-    __shared__ double colbuf[16];
+    // column L[c][j] is broadcast once (v_readlane) and used by both the trailing update of A
+    // and the forward substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the
+    // same operations and rounding as a separate substitution after the factorisation, with
+    // half the lane reads)
     double a[16], x[16];
 #pragma unroll
     for (int c = 0; c < 16; c++) {
@@ -2493,26 +2502,15 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     for (int j = 0; j < 16; j++) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
-        const double il = rsq1(djj);
+        const double il = rsq2(djj);
         a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
         x[j] *= il;
-        if (lane < 16) ((ldsd*)colbuf)[lane] = a[j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        double Lc[16];
-#pragma unroll
-        for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
-            const dv2 v = ((ldsd2*)colbuf)[c2];
-            Lc[2 * c2] = v.x;
-            Lc[2 * c2 + 1] = v.y;
-        }
 #pragma unroll
         for (int c = j + 1; c < 16; c++) {
-            a[c] -= a[j] * Lc[c];
-            x[c] -= Lc[c] * x[j];
+            const double Lcj = rdlane(a[j], c);
+            a[c] -= a[j] * Lcj;
+            x[c] -= Lcj * x[j];
         }
-        __builtin_amdgcn_wave_barrier();  // the next pivot's column store after these reads
     }
     if (lane < 16) {
 #pragma unroll
@@ -2520,6 +2518,13 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     }
     return ok;
 }
+
+// (Tried in round 4: broadcasting L[.][j] through LDS instead of v_readlane -- 914 instead of
+// 1356 instructions and 21 % faster alone (bench/diag_probe.hip), but its VGPR operands do not
+// fit the solves' 128-VGPR budget (1024-thread workgroups): 1 KiB/lane of scratch, the solve
+// 59 -> 152 us; the same with the inverse on a second wave fed through LDS (variant 6) spilled
+// as well.  The readlane form keeps the broadcasts in SGPRs.  A one-step rsqrt (19 ulp)
+// moved J0740's unrefined covariance by 1.3e-3 of its scale: also dropped.)
 
 __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+1)/2 + j, j <= i
     int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
@@ -2904,44 +2909,45 @@ __device__ __forceinline__ void dmx_errors(const double* A, const double* inx, c
     }
 }
 
-// pint_fit_step_apply: k_apply's work at the end of the solve -- tables += lam * step (dd,
-// timing columns, Offset skipped) and the instance's constants of the updated table -- so a
-// GLS step (lambda 1) needs no separate apply launch.  Every thread of the workgroup calls it
-// (inst_setup_wave synchronises the block); the dynamic LDS (free after the solve's exports)
-// stages the spec header, the table, the lanes' exchange slots and the constants
+// pint_fit_step_apply: k_apply's work inside the solve -- tables += lam * step (dd, timing
+// columns, Offset skipped) and the instance's constants of the updated table -- so a GLS step
+// (lambda 1) needs no apply launch.  The spec header and the table are staged in LDS beyond
+// the solve's own data when the kernel starts (their loads overlap the build), each step
+// element updates its table entry where it is written (LDS and HBM), and after the solve every
+// thread calls inst_setup_wave (which synchronises the block) on the staged copy: no global
+// round trip after the step.  The staging region: PREP_HDR + tstride + 16 doubles, then the
+// constants
+static inline size_t apply_tail_lds(int tstride) {
+    return sizeof(double) * ((size_t)PREP_HDR + tstride + 16) + sizeof(InstConst) + 16;
+}
 template <int NW>
-__device__ __forceinline__ void solve_apply_tail(const PsrDev& Pd, const InstDev& I, int inst, const double* dpars,
-                                                 double* __restrict__ tables, InstConst* __restrict__ ic, double lam,
-                                                 double* lds) {
-    const pint_spec_t& Sg = *Pd.spec;
-    const int tid = threadIdx.x, ncol = Sg.ncol, ts = Sg.tstride;
-    double* P = tables + I.toff;
-    __syncthreads();  // dpars of every thread written; the solve's LDS free
-    for (int c = tid; c < ncol; c += NW * 64) {
-        const int o = Sg.col_toff[c];
-        if (o < 0 || lam == 0.0) continue;
-        const dd v = dd_add_d(dd_make(P[o], P[o + 1]), lam * dpars[I.coff + c]);
-        P[o] = v.hi;
-        P[o + 1] = v.lo;
-    }
-    __syncthreads();
-    double* sS = lds;
-    double* sP = sS + PREP_HDR;
-    double* sx = sP + ts;
+__device__ __forceinline__ void apply_stage(const PsrDev& Pd, const InstDev& I, const double* tables, double* tail) {
+    const double* hg = reinterpret_cast<const double*>(Pd.spec);
+    const int ts = Pd.spec->tstride;
+    const double* P = tables + I.toff;
+    for (int i = threadIdx.x; i < PREP_HDR; i += NW * 64) tail[i] = hg[i];
+    for (int i = threadIdx.x; i < ts; i += NW * 64) tail[PREP_HDR + i] = P[i];
+}
+// column c's step dp: the staged (LDS) and the HBM table entry += lam * dp in double-double
+__device__ __forceinline__ void apply_col(const pint_spec_t& Sg, double* __restrict__ P, double* tailP, int c, double dp,
+                                          double lam) {
+    const int o = Sg.col_toff[c];
+    if (o < 0 || lam == 0.0) return;
+    const dd v = dd_add_d(dd_make(tailP[o], tailP[o + 1]), lam * dp);
+    tailP[o] = v.hi;
+    tailP[o + 1] = v.lo;
+    P[o] = v.hi;
+    P[o + 1] = v.lo;
+}
+__device__ __forceinline__ void apply_setup(int inst, double* tail, int ts, InstConst* __restrict__ ic) {
+    __syncthreads();  // every column's update in the staged table
+    double* sx = tail + PREP_HDR + ts;
     InstConst* sC = reinterpret_cast<InstConst*>(sx + 16);
-    const double* hg = reinterpret_cast<const double*>(&Sg);
-    for (int i = tid; i < PREP_HDR; i += NW * 64) sS[i] = hg[i];
-    for (int i = tid; i < ts; i += NW * 64) sP[i] = P[i];
-    __syncthreads();
-    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(sS), sP, *sC, sx, tid);
+    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(tail), tail + PREP_HDR, *sC, sx, threadIdx.x);
     __syncthreads();
     const int* cs = reinterpret_cast<const int*>(sC);
     int* cd = reinterpret_cast<int*>(ic + inst);
-    for (int k = tid; k < (int)(sizeof(InstConst) / 4); k += NW * 64) cd[k] = cs[k];
-}
-// dynamic LDS (bytes) solve_apply_tail needs for a table of tstride doubles
-static inline size_t apply_tail_lds(int tstride) {
-    return sizeof(double) * ((size_t)PREP_HDR + tstride + 16) + sizeof(InstConst) + 16;
+    for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cs[k];
 }
 
 template <int NW>
@@ -2998,6 +3004,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     double* xx = xd + nbd * 16;                       // nbk*16: normalised x_x
     double* rd = xx + nbk * 16;                       // nbd*16: residual r_d
     double* rx = rd + nbd * 16;                       // nbk*16: residual r_x
+    double* tail = rx + nbk * 16;                     // pint_fit_step_apply: spec header, table, setup
     const double* Gp = Gpart + I.goff;
     const double* Sdi = Sd + I.sdoff;
     auto Gd = [&](int i, int j) {  // dense compact Gram (upper storage)
@@ -3010,6 +3017,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
     TS(0);
+    if (apply_tables) apply_stage<NW>(Pd, I, apply_tables, tail);
     // ---- loads first: each thread's Gram (S) and DMX-row (U) elements are issued before the
     //      norms and held in registers across them, so building S and U costs one global-load
     //      latency instead of one per phase (systems larger than RS / RU elements per thread
@@ -3268,13 +3276,18 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     TS(21);
     // ---- steps (par units), chi2lin = r^T W r - b . x ----
     double bx_dot = 0.0;
+    double* Papp = apply_tables ? apply_tables + I.toff : nullptr;
     for (int g = tid; g < Kd; g += NW * 64) {
-        dpars[I.coff + Pd.dorig[g]] = xd[g] * ind[g];
+        const double v = xd[g] * ind[g];
+        dpars[I.coff + Pd.dorig[g]] = v;
         bx_dot += Gd(g, Kres) * ind[g] * xd[g];
+        if (Papp && Pd.dorig[g] < ncol) apply_col(S, Papp, tail + PREP_HDR, Pd.dorig[g], v, apply_lam);
     }
     for (int a = tid; a < ndc; a += NW * 64) {
-        dpars[I.coff + Pd.xorig[a]] = xx[a] * inx[a];
+        const double v = xx[a] * inx[a];
+        dpars[I.coff + Pd.xorig[a]] = v;
         bx_dot += bx[a] * xx[a];
+        if (Papp) apply_col(S, Papp, tail + PREP_HDR, Pd.xorig[a], v, apply_lam);
     }
     bx_dot = block_sum<NW>(bx_dot, sh);
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
@@ -3299,7 +3312,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         cov_dmx_blocks(A, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, ncol, red0, ndc, nbd, nbk, nblkS, wave, NW, lane);
     }
     TS(6);
-    if (apply_tables) solve_apply_tail<NW>(Pd, I, inst, dpars, apply_tables, apply_ic, apply_lam, lds);
+    if (apply_tables) apply_setup(inst, tail, S.tstride, apply_ic);
 }
 
 // k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred
@@ -5335,7 +5348,11 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
                            tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
                            ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs)
-        if (want_M && ctx->eval_wpe == 3) {
+        // the 3-waves/SIMD register budget (spills) pays when the blocks fill the SIMDs more
+        // than twice; a small batch (<= 2 waves per SIMD) runs the unconstrained build (203
+        // VGPRs, no spills) at its own occupancy
+        const bool small = ctx->nblk <= 2 * 256;
+        if (want_M && ctx->eval_wpe == 3 && !small) {
             hipLaunchKernelGGL((k_eval_mix_w<1, 3>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],
                                tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M,
@@ -5759,10 +5776,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 ok = ok && cmp && ph.dev.dsplit && ph.dev.vg;
                 maxts = std::max(maxts, ph.spec.tstride);
             }
-            if (ok && apply_tail_lds(maxts) <= 160 * 1024 - 512) {
+            // the staging region follows each instance's own solve data (lds_x bounds it)
+            if (ok && lds_x + apply_tail_lds(maxts) <= 160 * 1024 - 512) {
                 apply_tab = ctx->d_tables;
                 apply_ic = ctx->d_ic;
-                lds_dyn = std::max(lds_dyn, apply_tail_lds(maxts));
+                lds_dyn = std::max(lds_dyn, lds_x + apply_tail_lds(maxts));
                 ctx->apply_done = true;
             }
         }

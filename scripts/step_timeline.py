@@ -21,8 +21,16 @@ for r in rows:
     ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                r.get("Queue_Id", r.get("Stream_Id", "?"))))
 ks.sort()
-# steps start at each k_prep whose table reset precedes the evaluation with M
-starts = [i for i, k in enumerate(ks) if k[2].startswith("k_prep")]
+# steps start at the table reset (k_prep) or, when the restore is folded into it (round 4),
+# at the evaluation with M
+def _is_start(name):
+    return name.startswith("k_prep") or name.startswith("k_eval_mix_w<1") or name.startswith("k_eval_mix<1")
+
+
+starts = []
+for i, k in enumerate(ks):
+    if _is_start(k[2]) and not (starts and ks[starts[-1]][2].startswith("k_prep") and i == starts[-1] + 1):
+        starts.append(i)
 steps = []
 for a, b in zip(starts, starts[1:]):
     seg = ks[a:b]
