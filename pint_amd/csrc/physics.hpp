@@ -250,7 +250,7 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
 // cos/sin of the proper-motion-displaced RA and DEC -- on separate lanes, exchanged through
 // `sx` (LDS, >= 8 doubles); lane 0 finishes (pmsafe's atan2, starpv's iteration).  The same
 // expressions as inst_setup, so the same values; ecliptic models run inst_setup on lane 0.
-// Every lane of the wave must call it; C is written by lane 0.
+// Every lane of the block's first wave must call it (lane = threadIdx.x); C is written by lane 0.
 PD void inst_setup_wave(const pint_spec_t& S, const double* P, InstConst& C, double* sx, int lane) {
     if (S.astrometry != 1) {
         if (lane == 0) inst_setup(S, P, C);
@@ -278,7 +278,11 @@ PD void inst_setup_wave(const pint_spec_t& S, const double* P, InstConst& C, dou
         sx[10] = cos(dec2);
         sx[11] = sin(dec2);
     }
-    __syncthreads();
+    // the exchange is within wave 0 (lanes 0..3 write, lane 0 reads): a wave-level barrier,
+    // so a caller may run it on one wave while the block's other waves do other work
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane != 0) return;
     const double cd = sx[2];
     const double pmr = pml * MAS_RAD / cd;

@@ -2454,6 +2454,30 @@ __device__ __forceinline__ dd dd_wave_sum(dd s) {  // sum over the 64 lanes of a
     for (int o = 32; o >= 1; o >>= 1) s = dd_add(s, dd_make(__shfl_xor(s.hi, o, 64), __shfl_xor(s.lo, o, 64)));
     return s;
 }
+// the block maxima of two values with one pair of barriers (sh: 2 NW doubles)
+template <int NW>
+__device__ void block_max2(double* v, double* sh) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        v[0] = fmax(v[0], __shfl_xor(v[0], o, 64));
+        v[1] = fmax(v[1], __shfl_xor(v[1], o, 64));
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) {
+        sh[w] = v[0];
+        sh[NW + w] = v[1];
+    }
+    __syncthreads();
+    double a = sh[0], b = sh[NW];
+#pragma unroll
+    for (int i = 1; i < NW; i++) {
+        a = fmax(a, sh[i]);
+        b = fmax(b, sh[NW + i]);
+    }
+    v[0] = a;
+    v[1] = b;
+}
 constexpr int REFINE_PASSES = 1;
 constexpr double REFINE_KAPPA = 1e8;  // refine when the condition estimate exceeds this
 template <int NW>
@@ -2939,15 +2963,21 @@ __device__ __forceinline__ void apply_col(const pint_spec_t& Sg, double* __restr
     P[o] = v.hi;
     P[o + 1] = v.lo;
 }
-__device__ __forceinline__ void apply_setup(int inst, double* tail, int ts, InstConst* __restrict__ ic) {
-    __syncthreads();  // every column's update in the staged table
+// wave 0 only (the other waves export the solve meanwhile); the staged table complete (the
+// caller's block barrier after the step writes)
+// (not inlined: the setup's code stays out of the solve's hot loops -- inlined it grew the
+// kernel by ~10k instructions and its register spills)
+__device__ __attribute__((noinline)) void apply_setup(int inst, double* tail, int ts, InstConst* __restrict__ ic) {
     double* sx = tail + PREP_HDR + ts;
     InstConst* sC = reinterpret_cast<InstConst*>(sx + 16);
-    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(tail), tail + PREP_HDR, *sC, sx, threadIdx.x);
-    __syncthreads();
+    const int lane = threadIdx.x;
+    inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(tail), tail + PREP_HDR, *sC, sx, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int* cs = reinterpret_cast<const int*>(sC);
     int* cd = reinterpret_cast<int*>(ic + inst);
-    for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cs[k];
+    for (int k = lane; k < (int)(sizeof(InstConst) / 4); k += 64) cd[k] = cs[k];
 }
 
 template <int NW>
@@ -2964,7 +2994,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        double apply_lam) {
     extern __shared__ double lds[];
     __shared__ int sflag;
-    __shared__ double sh[NW];
+    __shared__ double sh[2 * NW];  // block_sum / block_max2
     if (fuse_sigma && (int)blockIdx.x >= (int)gridDim.x / 2) {
         // the Woodbury Sigma factor (k_sigma's work) in the second half of the grid, so it
         // runs concurrently with the solves without a second stream
@@ -3068,6 +3098,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     }
     __syncthreads();
     // ---- build S = A_dd, U = A_dx D^-1/2, b_d ----
+    // the normalised Gram diagonal, for the condition estimate's max diag(A), parked in rd
+    // (the refinement's residual, unused until then) instead of a register held across the
+    // register-hungry Cholesky
     auto put_S = [&](int e, double g) {
         int Ib, Jb;
         tri_decode(e >> 8, Ib, Jb);
@@ -3077,6 +3110,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         if (gi < Kd && gj < Kd) {
             const double ni = ind[gi], nj = ind[gj];
             v = g * (ni * nj);
+            if (gi == gj) rd[gi] = v;
             if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
         } else {
             v = (gi == gj) ? 1.0 : 0.0;
@@ -3161,34 +3195,37 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     // the same bits
     __syncthreads();
     TS(4);
-    // ---- x_d = X^T y ; errors of the dense columns ----
-    double amax = 0.0, vmax = 0.0;  // max diag(A) and max diag(A^-1): the condition estimate
-    for (int g = g0; g < Kd; g += NW * 16) {
+    // ---- x_d = X^T y ; errors of the dense columns (8 lanes per column: one round of
+    //      groups, ~10-long chains instead of ~20 with lane quads) ----
+    double vmax = 0.0, amax = 0.0;  // max diag(A^-1), max diag(A) (from the build, in rd)
+    const int h0 = tid >> 3, hs = tid & 7;
+    for (int g = h0; g < Kd; g += NW * 8) {
         double s1 = 0.0, se = 0.0;
-        for (int rr = g + sub; rr < nbd * 16; rr += 4) {
+        for (int rr = g + hs; rr < nbd * 16; rr += 8) {
             const double x = A[lblk(rr >> 4, g >> 4) + swz(rr & 15, g & 15)];
             s1 += x * yv[rr];
             se += x * x;
         }
-        s1 += __shfl_xor(s1, 1, 64);
-        s1 += __shfl_xor(s1, 2, 64);
-        se += __shfl_xor(se, 1, 64);
-        se += __shfl_xor(se, 2, 64);
-        if (sub == 0) {
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            se += __shfl_xor(se, o, 64);
+        }
+        if (hs == 0) {
             xd[g] = s1;
             errs[I.coff + Pd.dorig[g]] = sqrt(se) * ind[g];
             vmax = fmax(vmax, se);
-            amax = fmax(amax, Gd(g, g) * (ind[g] * ind[g]));
+            amax = fmax(amax, rd[g]);
         }
     }
     __syncthreads();  // x_d visible: z = U^T x_d below
     // ---- z = U^T x_d, x_x = D^-1 b_x - D^-1/2 z ----
-    for (int a = g0; a < ndc; a += NW * 16) {
+    for (int a = h0; a < ndc; a += NW * 8) {
         double sz = 0.0;
-        for (int rr = sub; rr < Kd; rr += 4) sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * xd[rr];
-        sz += __shfl_xor(sz, 1, 64);
-        sz += __shfl_xor(sz, 2, 64);
-        if (sub == 0) {
+        for (int rr = hs; rr < Kd; rr += 8) sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * xd[rr];
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) sz += __shfl_xor(sz, o, 64);
+        if (hs == 0) {
             const double d = Dn[a];
             xx[a] = bx[a] / d - sz * isd[a];
             // the DMX entries of diag(A^-1) are (1 + |W_a|^2) / d >= 1 / d: the estimate stays a
@@ -3200,7 +3237,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     // refine only where the solve can lose digits: kappa >= max diag(A) max diag(A^-1)
     // (a lower bound of cond(A)); measured, the unrefined error is ~1e-17 kappa sigma
     // (PTA pulsars kappa 1e5..1e7: <= 3e-12 sigma; J0740 7e12: 8e-5 sigma)
-    const bool do_ref = refine && block_max<NW>(amax, sh) * block_max<NW>(vmax, sh) > REFINE_KAPPA;
+    double am_vm[2] = {amax, vmax};
+    block_max2<NW>(am_vm, sh);
+    const bool do_ref = refine && am_vm[0] * am_vm[1] > REFINE_KAPPA;
     __syncthreads();
     // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
     // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
@@ -3289,19 +3328,25 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         bx_dot += bx[a] * xx[a];
         if (Papp) apply_col(S, Papp, tail + PREP_HDR, Pd.xorig[a], v, apply_lam);
     }
-    bx_dot = block_sum<NW>(bx_dot, sh);
+    bx_dot = block_sum<NW>(bx_dot, sh);  // (its barriers also complete the staged table's updates)
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
     TS(5);
+    // pint_fit_step_apply: the updated table's constants on wave 0, beside the export
+    const bool setup_w0 = apply_tables && xw;
+    if (setup_w0 && wave == 0) apply_setup(inst, tail, S.tstride, apply_ic);
     // ---- covariance of the timing parameters ----
     if (xw) {  // deferred to k_cov_dmx (several workgroups per instance, at the read): X, U
         double* o = xw + I.xwoff;
         const int na = (nblkS + nbd * nbk) * 256;
-        for (int e = tid; e < na; e += NW * 64) o[e] = A[e];
-        for (int e = tid; e < nbd * 16; e += NW * 64) o[na + e] = ind[e];
-        for (int e = tid; e < nbk * 16; e += NW * 64) {
-            o[na + nbd * 16 + e] = inx[e];
-            o[na + nbd * 16 + nbk * 16 + e] = isd[e];
-            o[na + nbd * 16 + 2 * nbk * 16 + e] = Dn[e];
+        const int t0 = setup_w0 ? tid - 64 : tid, ts_ = setup_w0 ? (NW - 1) * 64 : NW * 64;
+        if (t0 >= 0) {
+            for (int e = t0; e < na; e += ts_) o[e] = A[e];
+            for (int e = t0; e < nbd * 16; e += ts_) o[na + e] = ind[e];
+            for (int e = t0; e < nbk * 16; e += ts_) {
+                o[na + nbd * 16 + e] = inx[e];
+                o[na + nbd * 16 + nbk * 16 + e] = isd[e];
+                o[na + nbd * 16 + 2 * nbk * 16 + e] = Dn[e];
+            }
         }
     } else {
         // in the kernel: W = X U in place of U, the DMX errors (C_xx's diagonal D^-1 + D^-1
@@ -3312,7 +3357,10 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         cov_dmx_blocks(A, ind, inx, isd, Dn, Pd, cov + (long)I.cvoff, ncol, red0, ndc, nbd, nbk, nblkS, wave, NW, lane);
     }
     TS(6);
-    if (apply_tables) apply_setup(inst, tail, S.tstride, apply_ic);
+    if (apply_tables && !setup_w0) {
+        __syncthreads();  // (the covariance blocks read A, not the staged table; kept simple)
+        if (wave == 0) apply_setup(inst, tail, S.tstride, apply_ic);
+    }
 }
 
 // k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred

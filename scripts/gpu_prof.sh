@@ -7,12 +7,16 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0"
+# the 68-pulsar PTA step only: no emulated shards, no cold start (their launches would mix
+# other batch sizes into the per-kernel figures)
+B="python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --grid 64 --j0740 0 --c2 0 --cpu-baseline 0 > gpurun_out/prof.log 2>&1 || exit $?
+    python3 bench.py --steps 10 --warmup 2 --grid 64 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 \
+    > gpurun_out/prof.log 2>&1 || exit $?
 # C2 (B1855 x 256 batched fits) on its own trace: its kernels share names with the PTA's
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c2 -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --npsr 4 --grid 0 --j0740 0 --cpu-baseline 0 > gpurun_out/prof_c2.log 2>&1 || exit $?
+    python3 bench.py --steps 2 --warmup 1 --npsr 4 --grid 0 --j0740 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 \
+    > gpurun_out/prof_c2.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $B > gpurun_out/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- $B > gpurun_out/pmc_write.log 2>&1 || exit $?
 export PINT_SERIAL=1
