@@ -523,19 +523,28 @@ class Session:
         if tables.ndim != 2 or tables.shape[1] != lay.tstride:
             raise ValueError(f"tables must be (ninst, {lay.tstride}), got {tables.shape}")
         ids = np.full(tables.shape[0], lay.psr_id, dtype=np.int32)
-        self._set(ids, tables.ravel(), [lay] * tables.shape[0])
+        self._set(ids, tables.ravel(), [lay] * tables.shape[0], uniform=True)
 
-    def _set(self, ids, tabs, lays):
+    def _set(self, ids, tabs, lays, uniform=False):
         self._check(self.L.pint_set_instances(self.ctx, len(ids), L.ptr(ids, C.c_int32), L.ptr(tabs)))
         self.inst_layout = lays
         self.ntab = len(tabs)
-        # per-instance output offsets (read_step, noise_resids), formed once per batch
-        kk = np.array([l.K + 1 for l in lays], dtype=np.int64)
-        nc = np.array([len(l.columns) for l in lays], dtype=np.int64)
-        nn = np.array([l.n for l in lays], dtype=np.int64)
+        # per-instance output offsets (read_step, noise_resids), formed once per batch (one
+        # layout for every instance -- grid points -- without a Python loop over them: a
+        # 256 x 256 grid's loops took ~15 ms of its ~25 ms)
+        if uniform and lays:
+            n = len(lays)
+            kk = np.full(n, lays[0].K + 1, dtype=np.int64)
+            nc = np.full(n, len(lays[0].columns), dtype=np.int64)
+            nn = np.full(n, lays[0].n, dtype=np.int64)
+            self._cov_shapes = [(int(nc[0]), int(nc[0]))] * n
+        else:
+            kk = np.array([l.K + 1 for l in lays], dtype=np.int64)
+            nc = np.array([len(l.columns) for l in lays], dtype=np.int64)
+            nn = np.array([l.n for l in lays], dtype=np.int64)
+            self._cov_shapes = [(int(c), int(c)) for c in nc]
         self._off_k = np.concatenate([[0], np.cumsum(kk)])
         self._off_cov = np.concatenate([[0], np.cumsum(nc * nc)])
-        self._cov_shapes = [(int(c), int(c)) for c in nc]
         self._off_n = np.concatenate([[0], np.cumsum(nn)])
 
     # -- launches -------------------------------------------------------------------

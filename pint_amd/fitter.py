@@ -133,7 +133,8 @@ class BatchFit:
         self.idx = np.arange(self.n0)                 # device instance -> original index
         self.failed = np.zeros(self.n0, dtype=bool)  # original instances taken out of the batch
         self.tables0 = tables
-        self.grid_like = isinstance(tables, np.ndarray) and tables.ndim == 2 and all(l is layouts[0] for l in layouts)
+        self.grid_like = (isinstance(tables, np.ndarray) and tables.ndim == 2 and len(layouts) > 0
+                          and len(set(map(id, layouts))) == 1)  # one layout object (C-level scan)
         self.layouts0 = list(layouts)
         self._bind(list(layouts), tables)
         # wideband (WidebandTOAFitter / WidebandDownhillFitter): the DM rows join every fit
@@ -154,7 +155,10 @@ class BatchFit:
         else:
             self.s.set_instances(list(zip(layouts, tables)))
         self.ninst = len(layouts)
-        self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in layouts]
+        if self.grid_like and layouts:
+            self.use_gls_chi2 = [self.gls and (layouts[0].nred > 0 or layouts[0].nep > 0)] * len(layouts)
+        else:
+            self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in layouts]
 
     def _drop(self, bad):
         """Take the device instances flagged in `bad` out of the batch (their current tables
