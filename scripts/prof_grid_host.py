@@ -13,7 +13,7 @@ f.fit_toas(maxiter=1)
 F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
 g0 = F0 + np.linspace(-3, 3, side) * np.longdouble(f.model.F0.uncertainty)
 g1 = F1 + np.linspace(-3, 3, side) * np.longdouble(f.model.F1.uncertainty)
-for rep in range(3):
+for rep in range(int(sys.argv[2]) if len(sys.argv) > 2 else 3):
     t0 = time.perf_counter()
     grid_chisq(f, ("F0", "F1"), (g0, g1))
     print("grid", side, "rep", rep, round(time.perf_counter() - t0, 4), flush=True)
@@ -21,4 +21,4 @@ pr = cProfile.Profile()
 pr.enable()
 grid_chisq(f, ("F0", "F1"), (g0, g1))
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
