@@ -246,8 +246,8 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
 }
 
 // inst_setup by the 64 lanes of one wave (k_prep, k_apply): the equatorial astrometry's
-// independent transcendental calls -- cos/sin of RA and DEC, the double-double 1/PB, then
-// cos/sin of the proper-motion-displaced RA and DEC -- on separate lanes, exchanged through
+// independent transcendental calls -- cos/sin of RA, DEC and the proper-motion-displaced DEC,
+// the double-double 1/PB -- on separate lanes, exchanged through
 // `sx` (LDS, >= 8 doubles); lane 0 finishes (pmsafe's atan2, starpv's iteration).  The same
 // expressions as inst_setup, so the same values; ecliptic models run inst_setup on lane 0.
 // Every lane of the block's first wave must call it (lane = threadIdx.x); C is written by lane 0.
@@ -260,23 +260,26 @@ PD void inst_setup_wave(const pint_spec_t& S, const double* P, InstConst& C, dou
     const double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
     const double pmb = S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0;
     const double ra = lon * HA_RAD, dec = lat * DEG_RAD;
-    if (lane == 0) {
-        sx[0] = cos(ra);
-        sx[1] = sin(ra);
-    } else if (lane == 1) {
-        sx[2] = cos(dec);
-        sx[3] = sin(dec);
-    } else if (lane == 2 && S.binary && S.o_bin[PINT_B_PB] >= 0) {
+    const bool pm = !(pml == 0.0 && pmb == 0.0);
+    const double pmd = pmb * MAS_RAD;
+    // one cos and one sin per lane, of a per-lane angle (lane 0: RA, 1: DEC, 2: dec2 = DEC +
+    // pmd, which does not depend on the other trig values): the calls are not divergent, so
+    // the wave runs each once instead of once per lane's branch
+    {
+        const double ang = lane == 0 ? ra : (lane == 1 ? dec : dec + pmd);
+        const double c = cos(ang), sn = sin(ang);
+        if (lane < 2) {
+            sx[2 * lane] = c;
+            sx[2 * lane + 1] = sn;
+        } else if (lane == 2 && pm) {
+            sx[10] = c;
+            sx[11] = sn;
+        }
+    }
+    if (lane == 3 && S.binary && S.o_bin[PINT_B_PB] >= 0) {
         dd ipb = dd_div(dd_make(1.0), dd_mul_d(pdd(P, S.o_bin[PINT_B_PB]), DAYSEC));
         sx[4] = ipb.hi;
         sx[5] = ipb.lo;
-    }
-    const bool pm = !(pml == 0.0 && pmb == 0.0);
-    const double pmd = pmb * MAS_RAD;
-    if (pm && lane == 3) {  // dec2 does not depend on the other trig values: same phase
-        const double dec2 = dec + pmd;
-        sx[10] = cos(dec2);
-        sx[11] = sin(dec2);
     }
     // the exchange is within wave 0 (lanes 0..3 write, lane 0 reads): a wave-level barrier,
     // so a caller may run it on one wave while the block's other waves do other work

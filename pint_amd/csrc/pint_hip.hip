@@ -2952,10 +2952,9 @@ __device__ __forceinline__ void apply_stage(const PsrDev& Pd, const InstDev& I, 
     for (int i = threadIdx.x; i < PREP_HDR; i += NW * 64) tail[i] = hg[i];
     for (int i = threadIdx.x; i < ts; i += NW * 64) tail[PREP_HDR + i] = P[i];
 }
-// column c's step dp: the staged (LDS) and the HBM table entry += lam * dp in double-double
-__device__ __forceinline__ void apply_col(const pint_spec_t& Sg, double* __restrict__ P, double* tailP, int c, double dp,
-                                          double lam) {
-    const int o = Sg.col_toff[c];
+// a column's step dp: the staged (LDS) and the HBM table entry o (the column's col_toff)
+// += lam * dp in double-double
+__device__ __forceinline__ void apply_col(double* __restrict__ P, double* tailP, int o, double dp, double lam) {
     if (o < 0 || lam == 0.0) return;
     const dd v = dd_add_d(dd_make(tailP[o], tailP[o + 1]), lam * dp);
     tailP[o] = v.hi;
@@ -2971,7 +2970,9 @@ __device__ __attribute__((noinline)) void apply_setup(int inst, double* tail, in
     double* sx = tail + PREP_HDR + ts;
     InstConst* sC = reinterpret_cast<InstConst*>(sx + 16);
     const int lane = threadIdx.x;
+    TS(22);
     inst_setup_wave(*reinterpret_cast<const pint_spec_t*>(tail), tail + PREP_HDR, *sC, sx, lane);
+    TS(23);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -3180,6 +3181,15 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         return;
     }
     TS(3);
+    // the steps' and errors' bookkeeping loads (original column indices, b_d's Gram entry),
+    // issued here so their latency passes under y and x_d (one column per thread: Kd, ndc
+    // <= 16 BS_MAXNB <= NW 64)
+    static_assert(16 * BS_MAXNB <= NW * 64, "k_solve_dmx: one dense / DMX column per thread");
+    const int h0 = tid >> 3, hs = tid & 7;
+    const int od_t = tid < Kd ? Pd.dorig[tid] : 0;       // the step loop's column (g = tid)
+    const int ox_t = tid < ndc ? Pd.xorig[tid] : 0;      // ... and DMX column (a = tid)
+    const double gb_t = tid < Kd ? Gd(tid, Kres) : 0.0;
+    const int od_h = h0 < Kd ? Pd.dorig[h0] : 0;         // the x_d loop's column (g = h0)
     // ---- y = X b'_d ----
     const int g0 = tid >> 2, sub = tid & 3;
     for (int g = g0; g < nbd * 16; g += NW * 16) {
@@ -3189,6 +3199,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         sy += __shfl_xor(sy, 2, 64);
         if (sub == 0) yv[g] = sy;
     }
+    // the table offsets of the step loop's columns (pint_fit_step_apply)
+    const int to_d = (apply_tables && tid < Kd && od_t < ncol) ? S.col_toff[od_t] : -1;
+    const int to_x = (apply_tables && tid < ndc) ? S.col_toff[ox_t] : -1;
     // the step needs only z = W^T y = U^T X^T y = U^T x_d, so U stays in LDS as it is: W = X U
     // (for the DMX errors and the covariance) is formed after the step, here or -- deferred
     // solves (xw) -- by k_cov_dmx at the read, off the step's critical path; both orders give
@@ -3198,7 +3211,6 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     // ---- x_d = X^T y ; errors of the dense columns (8 lanes per column: one round of
     //      groups, ~10-long chains instead of ~20 with lane quads) ----
     double vmax = 0.0, amax = 0.0;  // max diag(A^-1), max diag(A) (from the build, in rd)
-    const int h0 = tid >> 3, hs = tid & 7;
     for (int g = h0; g < Kd; g += NW * 8) {
         double s1 = 0.0, se = 0.0;
         for (int rr = g + hs; rr < nbd * 16; rr += 8) {
@@ -3213,34 +3225,53 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         }
         if (hs == 0) {
             xd[g] = s1;
-            errs[I.coff + Pd.dorig[g]] = sqrt(se) * ind[g];
+            errs[I.coff + od_h] = sqrt(se) * ind[g];  // (g = h0: one round of groups)
             vmax = fmax(vmax, se);
             amax = fmax(amax, rd[g]);
         }
     }
-    __syncthreads();  // x_d visible: z = U^T x_d below
+    // the DMX entries of diag(A^-1) are (1 + |W_a|^2) / d >= 1 / d: the estimate stays a
+    // lower bound without W.  Both maxima are reduced here, over the barrier x_d needs anyway
+    for (int a = tid; a < ndc; a += NW * 64) {
+        const double d = Dn[a];
+        vmax = fmax(vmax, 1.0 / d);
+        amax = fmax(amax, d);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
+        amax = fmax(amax, __shfl_xor(amax, o, 64));
+    }
+    if (lane == 0) {
+        sh[wave] = amax;
+        sh[NW + wave] = vmax;
+    }
+    __syncthreads();  // x_d and the maxima visible: z = U^T x_d below
+    TS(25);
+    {
+        double a_ = sh[0], b_ = sh[NW];
+#pragma unroll
+        for (int i = 1; i < NW; i++) {
+            a_ = fmax(a_, sh[i]);
+            b_ = fmax(b_, sh[NW + i]);
+        }
+        amax = a_;
+        vmax = b_;
+    }
     // ---- z = U^T x_d, x_x = D^-1 b_x - D^-1/2 z ----
     for (int a = h0; a < ndc; a += NW * 8) {
         double sz = 0.0;
         for (int rr = hs; rr < Kd; rr += 8) sz += A[ublk(rr >> 4, a >> 4, nbk, nblkS) + swz(rr & 15, a & 15)] * xd[rr];
 #pragma unroll
         for (int o = 1; o < 8; o <<= 1) sz += __shfl_xor(sz, o, 64);
-        if (hs == 0) {
-            const double d = Dn[a];
-            xx[a] = bx[a] / d - sz * isd[a];
-            // the DMX entries of diag(A^-1) are (1 + |W_a|^2) / d >= 1 / d: the estimate stays a
-            // lower bound without W
-            vmax = fmax(vmax, 1.0 / d);
-            amax = fmax(amax, d);
-        }
+        if (hs == 0) xx[a] = bx[a] / Dn[a] - sz * isd[a];
     }
     // refine only where the solve can lose digits: kappa >= max diag(A) max diag(A^-1)
     // (a lower bound of cond(A)); measured, the unrefined error is ~1e-17 kappa sigma
     // (PTA pulsars kappa 1e5..1e7: <= 3e-12 sigma; J0740 7e12: 8e-5 sigma)
-    double am_vm[2] = {amax, vmax};
-    block_max2<NW>(am_vm, sh);
-    const bool do_ref = refine && am_vm[0] * am_vm[1] > REFINE_KAPPA;
-    __syncthreads();
+    const bool do_ref = refine && amax * vmax > REFINE_KAPPA;
+    TS(26);
+    __syncthreads();  // x_x visible (and the maxima read before block_sum reuses sh)
     // ---- iterative refinement: r = b - A x with A from the Gram in global memory (dd
     // residual), then the same Schur solve of r (b'' = r_d - A_dx D^-1 r_x, y = X b'', dx_d =
     // X^T y, dx_x = D^-1 r_x - D^-1/2 W^T y with W^T y = U^T dx_d).  The explicit
@@ -3316,17 +3347,21 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     // ---- steps (par units), chi2lin = r^T W r - b . x ----
     double bx_dot = 0.0;
     double* Papp = apply_tables ? apply_tables + I.toff : nullptr;
-    for (int g = tid; g < Kd; g += NW * 64) {
+    // (one column per thread; the column indices, their table offsets and b_d's Gram entry
+    // loaded before)
+    if (tid < Kd) {
+        const int g = tid;
         const double v = xd[g] * ind[g];
-        dpars[I.coff + Pd.dorig[g]] = v;
-        bx_dot += Gd(g, Kres) * ind[g] * xd[g];
-        if (Papp && Pd.dorig[g] < ncol) apply_col(S, Papp, tail + PREP_HDR, Pd.dorig[g], v, apply_lam);
+        dpars[I.coff + od_t] = v;
+        bx_dot += gb_t * ind[g] * xd[g];
+        if (Papp && od_t < ncol) apply_col(Papp, tail + PREP_HDR, to_d, v, apply_lam);
     }
-    for (int a = tid; a < ndc; a += NW * 64) {
+    if (tid < ndc) {
+        const int a = tid;
         const double v = xx[a] * inx[a];
-        dpars[I.coff + Pd.xorig[a]] = v;
+        dpars[I.coff + ox_t] = v;
         bx_dot += bx[a] * xx[a];
-        if (Papp) apply_col(S, Papp, tail + PREP_HDR, Pd.xorig[a], v, apply_lam);
+        if (Papp) apply_col(Papp, tail + PREP_HDR, to_x, v, apply_lam);
     }
     bx_dot = block_sum<NW>(bx_dot, sh);  // (its barriers also complete the staged table's updates)
     if (tid == 0) chi2lin[inst] = rwr - bx_dot;
@@ -3348,6 +3383,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                 o[na + nbd * 16 + 2 * nbk * 16 + e] = Dn[e];
             }
         }
+        if (blockIdx.x == 0 && tid == 64) g_ts[24] = __builtin_amdgcn_s_memrealtime();  // (ts probe)
     } else {
         // in the kernel: W = X U in place of U, the DMX errors (C_xx's diagonal D^-1 + D^-1
         // |W_a|^2) and the covariance blocks, as k_cov_dmx forms them
