@@ -210,6 +210,27 @@ __device__ double block_sum(double v, double* sh) {
     for (int i = 0; i < NW; i++) t += sh[i];
     return t;
 }
+// block_sum of V values at once (one barrier pair; each value reduced in block_sum's order,
+// so the same bits); sh holds V * NW doubles
+template <int NW, int V>
+__device__ void block_sums(double* v, double* sh) {
+#pragma unroll
+    for (int k = 0; k < V; k++) v[k] = wave_sum(v[k]);
+    int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) {
+#pragma unroll
+        for (int k = 0; k < V; k++) sh[k * NW + w] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < V; k++) {
+        double t = 0.0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) t += sh[k * NW + i];
+        v[k] = t;
+    }
+}
 
 // ---------------------------------------------------------------------------------
 // k_eval: one thread per TOA row (row n = TZR TOA)
@@ -444,11 +465,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 // accumulates chi2 partials, which k_rsum adds per instance.
 constexpr int RES_BT = 256;
 constexpr int RES_RB = 1024;  // rows per block (4 per thread)
+constexpr int RES_RPT = RES_RB / RES_BT;  // rows per thread
 __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const int* __restrict__ rblk_inst,
                                                    const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
                                                    double* __restrict__ rphase, double* __restrict__ rpart) {
-    __shared__ double sh[RES_BT / 64];
+    __shared__ double sh[2 * (RES_BT / 64)];
     const int ii = rblk_inst[blockIdx.x];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
@@ -462,12 +484,11 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     dd d0 = dd_make(0.0);
     if (!S.track_pn && S.subtract_mean) d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
     double sw = 0.0, swx = 0.0;
-    // the thread's four rows: every load issued before the arithmetic (one load latency per
+    // the thread's RES_RPT rows: every load issued before the arithmetic (one load latency per
     // block, not one per row: a small batch's pass is latency-bound)
-    constexpr int RPT = RES_RB / RES_BT;
-    double lh[RPT], ll[RPT], lp[RPT], lpn[RPT], lw[RPT];
+    double lh[RES_RPT], ll[RES_RPT], lp[RES_RPT], lpn[RES_RPT], lw[RES_RPT];
 #pragma unroll
-    for (int u = 0; u < RPT; u++) {
+    for (int u = 0; u < RES_RPT; u++) {
         const int i = r0 + threadIdx.x + u * RES_BT;
         const bool in = i < r1;
         lh[u] = in ? ph_hi[ro + i] : 0.0;
@@ -477,7 +498,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
         lw[u] = (in && S.weighted_mean) ? Pd.isig[i] : 1.0;
     }
 #pragma unroll
-    for (int u = 0; u < RPT; u++) {
+    for (int u = 0; u < RES_RPT; u++) {
         const int i = r0 + threadIdx.x + u * RES_BT;
         if (i >= r1) break;
         dd d = dd_add_d(dd_sub(dd_make(lh[u], ll[u]), tz), lp[u]);
@@ -494,8 +515,10 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
         swx += w * full;
     }
     if (S.subtract_mean) {
-        swx = block_sum<RES_BT / 64>(swx, sh);
-        sw = block_sum<RES_BT / 64>(sw, sh);
+        double v[2] = {swx, sw};
+        block_sums<RES_BT / 64, 2>(v, sh);
+        swx = v[0];
+        sw = v[1];
         if (threadIdx.x == 0) {
             rpart[3 * blockIdx.x] = sw;
             rpart[3 * blockIdx.x + 1] = swx;
@@ -517,7 +540,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
                                                    const int* __restrict__ rblk_inst, const double* __restrict__ ftay,
                                                    double* __restrict__ rtime, double* __restrict__ rphase,
                                                    double* __restrict__ rpart, double* __restrict__ wtile) {
-    __shared__ double sh[RES_BT / 64];
+    __shared__ double sh[2 * (RES_BT / 64)];
     extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS: A (columns 0-15), B (16-31)
     const int ii = rblk_inst[blockIdx.x];
     const InstDev I = insts[ii];
@@ -528,30 +551,15 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     const long oo = I.roff - ii;
     const int r0 = (int)(blockIdx.x - I.rb0) * RES_RB;
     const int r1 = min(n, r0 + RES_RB);
-    double mean = 0.0;
-    if (S.subtract_mean) {  // residuals.py:314-425 weighted mean (utils.py:2002), fixed tree order
-        double a = 0.0, b = 0.0;
-        for (int k = threadIdx.x; k < I.nrb; k += RES_BT) {
-            b += rpart[3 * (I.rb0 + k)];
-            a += rpart[3 * (I.rb0 + k) + 1];
-        }
-        a = block_sum<RES_BT / 64>(a, sh);
-        b = block_sum<RES_BT / 64>(b, sh);
-        mean = a / b;
-    }
     const bool tile = wtile != nullptr;
     const bool harm = tile && __builtin_amdgcn_readfirstlane(S.nred) > 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};  // independent chains
-    typedef double __attribute__((address_space(3))) ldsd;
-    ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS);
-    double c2 = 0.0;
-    // the thread's four rows loaded up front (one load latency per block, not one per row)
-    constexpr int RPT = RES_RB / RES_BT;
-    double lr[RPT], lf[RPT], ls[RPT];
-    double4_t lz[RPT];
+    // the thread's RES_RPT rows loaded up front (one load latency per block, not one per row),
+    // before the weighted mean's partial sums and barriers, so the two latencies overlap
+    double lr[RES_RPT], lf[RES_RPT], ls[RES_RPT];
+    double4_t lz[RES_RPT];
 #pragma unroll
-    for (int j = 0; j < RPT; j++) {
+    for (int j = 0; j < RES_RPT; j++) {
         const int i = r0 + threadIdx.x + j * RES_BT;
         const bool in = i < r1;
         lr[j] = in ? rphase[oo + i] : 0.0;
@@ -559,8 +567,23 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
         ls[j] = in ? Pd.isig[i] : 0.0;
         lz[j] = (harm && in) ? ((gptr<double4_t>)Pd.red_cs)[i] : double4_t{1.0, 0.0, 1.0, 0.0};
     }
+    double mean = 0.0;
+    if (S.subtract_mean) {  // residuals.py:314-425 weighted mean (utils.py:2002), fixed tree order
+        double a = 0.0, b = 0.0;
+        for (int k = threadIdx.x; k < I.nrb; k += RES_BT) {
+            b += rpart[3 * (I.rb0 + k)];
+            a += rpart[3 * (I.rb0 + k) + 1];
+        }
+        double v[2] = {a, b};
+        block_sums<RES_BT / 64, 2>(v, sh);
+        mean = v[0] / v[1];
+    }
+    double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};  // independent chains
+    typedef double __attribute__((address_space(3))) ldsd;
+    ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS);
+    double c2 = 0.0;
 #pragma unroll
-    for (int j = 0; j < RPT; j++) {
+    for (int j = 0; j < RES_RPT; j++) {
         const int i = r0 + threadIdx.x + j * RES_BT;
         double wr = 0.0;
         if (i < r1) {
@@ -3742,7 +3765,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 const double* __restrict__ wtile, const double* __restrict__ rpart,
                                                 double* __restrict__ chi2w, int compact) {
     extern __shared__ double lds[];
-    __shared__ double sh[8];
+    __shared__ double sh[12];  // block_sums<4, 3>
     __shared__ double Dt[256], wloc[130];
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
@@ -3810,6 +3833,20 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     const int nep = Pd.nep;
     const double* Ei = esum + I.eoff;
     double* ce = ecs + I.epoff;
+    // log-normalisation of the likelihood, logdet(C)/2 (residuals.py:567-589 via
+    // utils.py:3074 woodbury_dot): logdet C = logdet N + logdet Phi + logdet Sigma, Phi =
+    // [phi_red, phi_ecorr, 1e40]; with the ECORR block eliminated, logdet Sigma =
+    // sum_e log D_e + logdet Sigma' and Sigma' = L L^T (X = L^-1 holds 1/L_jj on its diagonal).
+    // Its inputs are ready at launch: formed here, off the dot products' chain, and reduced
+    // with the ECORR sums
+    const double x00 = S.wb_noones ? 1.0 : 1.0 / sqrt(1e-40 + Pd.sumw);
+    double ld = 0.0;
+    {
+        const double* X = sigL + I.soff;
+        for (int e = threadIdx.x; e < nep; e += blockDim.x) ld += log(Pd.ep_phi[e]) + log(eD[I.epoff + e]);
+        for (int k = threadIdx.x; k < R; k += blockDim.x) ld += log(Pd.red_phi[k]);
+        for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(nobasis ? x00 : X[tri(j, j)]);
+    }
     double erwr = 0.0, erw1 = 0.0;
     for (int e = threadIdx.x; e < nep; e += blockDim.x) {
         double c = 0.0;
@@ -3822,9 +3859,13 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
         erw1 += eW[I.epoff + e] * c / De;
         ce[e] = c / De;
     }
-    erwr = block_sum<4>(erwr, sh);
-    erw1 = block_sum<4>(erw1, sh);
-    __syncthreads();  // ce visible
+    {
+        double v[3] = {erwr, erw1, ld};
+        block_sums<4, 3>(v, sh);  // (its barriers also make ce visible)
+        erwr = v[0];
+        erw1 = v[1];
+        ld = v[2];
+    }
     // the Fourier columns of the epoch sums: after the timing columns (full layout) or at
     // red0c of the compact dense columns
     const bool ecmp = compact && Pd.dsplit;
@@ -3844,7 +3885,6 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     if (threadIdx.x == 0) d[R] = S.wb_noones ? 0.0 : rw1 - erw1;  // the ones column's entry
     __syncthreads();
     // y = L^-1 d with the explicit inverse factor (staged above), four lanes per row
-    const double x00 = S.wb_noones ? 1.0 : 1.0 / sqrt(1e-40 + Pd.sumw);
     double q = 0.0;
     for (int i0 = 0; i0 < Kn; i0 += blockDim.x / 4) {
         const int i = i0 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
@@ -3859,15 +3899,6 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
         if (sub == 0 && i < Kn) q += s * s;
     }
     q = block_sum<4>(q, sh);
-    // log-normalisation of the likelihood, logdet(C)/2 (residuals.py:567-589 via
-    // utils.py:3074 woodbury_dot): logdet C = logdet N + logdet Phi + logdet Sigma, Phi =
-    // [phi_red, phi_ecorr, 1e40]; with the ECORR block eliminated, logdet Sigma =
-    // sum_e log D_e + logdet Sigma' and Sigma' = L L^T (X = L^-1 holds 1/L_jj on its diagonal)
-    double ld = 0.0;
-    for (int e = threadIdx.x; e < nep; e += blockDim.x) ld += log(Pd.ep_phi[e]) + log(eD[I.epoff + e]);
-    for (int k = threadIdx.x; k < R; k += blockDim.x) ld += log(Pd.red_phi[k]);
-    for (int j = threadIdx.x; j < Kn; j += blockDim.x) ld -= 2.0 * log(nobasis ? x00 : Xs[tri(j, j)]);
-    ld = block_sum<4>(ld, sh);
     if (threadIdx.x == 0) {
         chi2[inst] = (rwr - erwr) - q;
         lognorm[inst] = 0.5 * (ld + 2.0 * Pd.logsig + (S.wb_noones ? 0.0 : log(1e40)));
@@ -4022,7 +4053,7 @@ __global__ __launch_bounds__(256) void k_noise_lnl(const PsrDev* __restrict__ ps
                                                   const double* __restrict__ qf, const double* __restrict__ epw,
                                                   double* __restrict__ epsv, double* __restrict__ out,
                                                   double* __restrict__ clsg, double* __restrict__ epg) {
-    __shared__ double sh[4];
+    __shared__ double sh[32];  // block_sums<4, 8>
     const int inst = blockIdx.x;
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
@@ -4075,21 +4106,22 @@ __global__ __launch_bounds__(256) void k_noise_lnl(const PsrDev* __restrict__ ps
             A += g * N;
             B += g;
         }
-        A = block_sum<4>(A, sh);
-        B = block_sum<4>(B, sh);
+        {
+            double v[2] = {A, B};
+            block_sums<4, 2>(v, sh);
+            A = v[0];
+            B = v[1];
+        }
         if (threadIdx.x == 0 && kind < 2) {
             clsg[2 * (q0 + c)] = A;
             clsg[2 * (q0 + c) + 1] = B;
         }
     }
-    t1 = block_sum<4>(t1, sh);
-    t2 = block_sum<4>(t2, sh);
-    S = block_sum<4>(S, sh);
-    V = block_sum<4>(V, sh);
-    ec = block_sum<4>(ec, sh);
-    el = block_sum<4>(el, sh);
-    ea = block_sum<4>(ea, sh);
-    eb = block_sum<4>(eb, sh);
+    {
+        double v[8] = {t1, t2, S, V, ec, el, ea, eb};
+        block_sums<4, 8>(v, sh);  // (one barrier pair for the eight sums, the same bits)
+        t1 = v[0]; t2 = v[1]; S = v[2]; V = v[3]; ec = v[4]; el = v[5]; ea = v[6]; eb = v[7];
+    }
     if (threadIdx.x == 0) {
         double chi2 = t1 - ec, ln = 0.5 * (t2 + el);
         if (kind == 2) {
@@ -5487,15 +5519,16 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     record(ctx, want_M ? 3 : 1);
     record(ctx, 4);
     if (ctx->nrblk > 0) {
-        hipLaunchKernelGGL(k_resid1, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_rblk_inst, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
         // without the design matrix (the post-fit evaluation a GLS chi2 follows): the Woodbury
         // dot products come with the residual pass (k_resid2 tiles, k_rsum)
         const bool wt = ctx->wfuse && want_M == 0;
-        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0,
-                           ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
-                           wt ? ctx->d_wtile : nullptr);
+        const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
+        // (256-row blocks for small batches were measured: resid1 faster, resid2 and k_wsolve's
+        // longer tile sums slower, the step ~1.4 us slower at 9 pulsars)
+        hipLaunchKernelGGL(k_resid1, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_rblk_inst, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
+        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart, wt ? ctx->d_wtile : nullptr);
         // the chi2 partials are summed when the chi2 is read (pint_read_resids) or by k_wsolve,
         // which needs them anyway: no launch of its own in a fit step
         ctx->chi2_pending = true;

