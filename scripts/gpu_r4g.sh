@@ -10,10 +10,10 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
 rc=$?
 tail -4 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 200 python3 scripts/diag/ts_probe.py 9 > gpurun_out/ts9.txt 2>&1 || exit $?
-tail -4 gpurun_out/ts9.txt
+timeout -k 10 200 python3 scripts/diag/ts_probe.py 9 apply > gpurun_out/ts9.txt 2>&1 || exit $?
+tail -6 gpurun_out/ts9.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof9 -o run -- \
-    python3 bench.py --npsr 9 --steps 30 --warmup 5 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world '' --cold-start 0 \
+    python3 bench.py --npsr 9 --steps 30 --warmup 5 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 \
     > gpurun_out/prof9.log 2>&1 || exit $?
 python3 scripts/step_timeline.py gpurun_out/prof9/run_kernel_trace.csv > gpurun_out/timeline9.txt 2>&1 || true
 head -40 gpurun_out/timeline9.txt
