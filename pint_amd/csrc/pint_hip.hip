@@ -3097,6 +3097,9 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
         gU[u] = (e < nU && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
     }
+    // b_d's Gram entries and r^T W r with them (one column per thread), not after the barrier
+    const double gb_pre = tid < Kd ? Gd(tid, Kres) : 0.0;
+    const double rwr = Gd(Kres, Kres);
     // ---- column norms (utils.py:2879: zero norm -> 1), b_x, D (normalised) ----
     for (int c = tid; c < nbd * 16; c += NW * 64) {
         double v = 1.0;
@@ -3164,8 +3167,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
         put_U(e, (gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0);
     }
-    for (int c = tid; c < nbd * 16; c += NW * 64) bd[c] = c < Kd ? Gd(c, Kres) * ind[c] : 0.0;
-    const double rwr = Gd(Kres, Kres);
+    if (tid < nbd * 16) bd[tid] = tid < Kd ? gb_pre * ind[tid] : 0.0;
     __syncthreads();
     TS(1);
     // ---- S -= U U^T (lower blocks), b'_d = b_d - U D^-1/2 b_x ----
@@ -3177,7 +3179,11 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             bmma<false, false>(acc, A + ublk(Ib, k, nbk, nblkS), A + ublk(Jb, k, nbk, nblkS), lane, true);
         bstore(A + lblk(Ib, Jb), acc, lane, 1.0);
     }
+    TS(27);
+    if (blockIdx.x == 0 && tid == 14 * 64) g_ts[29] = __builtin_amdgcn_s_memrealtime();  // (ts probe: wave 14)
     {
+        // (8 lanes per row counted from the idle last wave, two chains each, measured no
+        // faster: the phase is bound by the CU's MFMA issue, 15 blocks x 32 MFMAs on 4 SIMDs)
         const int g0 = tid >> 2, sub = tid & 3;
         double bnew = 0.0;
         for (int c = g0; c < nbd * 16; c += NW * 16) {
@@ -3188,6 +3194,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
             sacc += __shfl_xor(sacc, 2, 64);
             bnew = bd[c] - sacc;
         }
+        TS(28);
         __syncthreads();
         if (sub == 0 && g0 < nbd * 16) bd[g0] = bnew;  // NW*16 >= nbd*16 groups
     }

@@ -23,6 +23,7 @@ for it in range(3):
     print("  chol: diag0 %.2f barrier %.2f panel0 %.2f trail0 %.2f | rest-of-chol %.2f | inv step1 %.2f rest %.2f" % tuple(np.diff(np.concatenate([[out[2]], out[10:17]]))))
     print("  refine: residual %.2f b'' %.2f y %.2f update %.2f | steps %.2f" % tuple(np.diff(np.concatenate([[out[17]], out[18:22], [out[5]]]))))
     if APPLY:
+        print("  S -= UU^T: MFMA wave 0 %.2f wave 14 %.2f | b' (wave 0) %.2f | phase %.2f" % (out[27] - out[1], out[29] - out[1], out[28] - out[27], out[2] - out[1]))
         print("  x phase: x_d %.2f z %.2f max+refine %.2f steps %.2f" % (out[25] - out[4], out[26] - out[25], out[21] - out[26], out[5] - out[21]))
         print("  tail: steps->setup start %.2f setup %.2f | export end (wave 1) %.2f after the steps" % (out[22] - out[5], out[23] - out[22], out[24] - out[5]))
     if APPLY:
