@@ -2584,6 +2584,10 @@ __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+
 // Blocked Cholesky + in-place inverse of the nb x nb block lower matrix A in LDS:
 // afterwards A holds X = L^-1.  Needs NW >= nb - 1.  Returns false (uniformly) if A is
 // not positive definite.
+// (Tried in round 4: forming X's block row k - 1 on the waves off wave 0's SIMD while wave 0
+// factors diagonal block k -- the same operations, stored after the step's barrier -- removed
+// the row loop below (3.3 -> 0.1 us) but the accumulators held across the barrier doubled the
+// diagonal factor (3.7 -> 7.2 us per block, register pressure): dropped.)
 template <int NW>
 __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
     for (int k = 0; k < nb; k++) {
