@@ -2585,9 +2585,10 @@ __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+
 // afterwards A holds X = L^-1.  Needs NW >= nb - 1.  Returns false (uniformly) if A is
 // not positive definite.
 // (Tried in round 4: forming X's block row k - 1 on the waves off wave 0's SIMD while wave 0
-// factors diagonal block k -- the same operations, stored after the step's barrier -- removed
-// the row loop below (3.3 -> 0.1 us) but the accumulators held across the barrier doubled the
-// diagonal factor (3.7 -> 7.2 us per block, register pressure): dropped.)
+// factors diagonal block k, or X's block row k on the waves the trailing update leaves idle --
+// the same operations, stored after a barrier -- removed the row loop below (3.3 -> 0.1 us)
+// but either way the diagonal factor doubled (3.7 -> 6.9-7.2 us per block, also at k = 0
+// where no row is formed: the register allocation of the loop): dropped.)
 template <int NW>
 __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
     for (int k = 0; k < nb; k++) {
