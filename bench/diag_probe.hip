@@ -8,7 +8,8 @@
 //   2  variant 1 with one Newton step on v_rsq_f64 instead of two,
 //   3  the pivot column broadcast through LDS (VGPR operands), 4: that with one Newton step,
 //   5  variant 3 with a scheduling barrier after each pivot,
-//   6  two waves: the factorisation (readlane) and the inverse (LDS columns) one pivot apart.
+//   6  two waves: the factorisation (readlane) and the inverse (LDS columns) one pivot apart,
+//   7  variant 0 with the lane index opaque per pivot (no hoisted lane-mask SGPR pairs).
 // The kernel is compiled with the 1024-thread register budget of the solves (128 VGPRs).
 // Prints the max error of L^-1 against a long-double Cholesky inverse on the host (relative
 // to max |L^-1|) and the cycles per factor (s_memtime, 64 dependent factors in one wave).
@@ -59,6 +60,40 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
             x[c] -= Lcj * x[j];
         }
         if (V >= 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+    }
+    return ok;
+}
+
+// variant 7: as variant 0, with the lane's row index made opaque in every pivot, so the
+// compiler cannot hoist the sixteen pivots' lane-mask compares (SGPR pairs kept live, spilled
+// to VGPR lanes); for lane r == j the scaled pivot a[j] * il is djj * il exactly
+__device__ __forceinline__ bool diag_factor_c4(double* Akk, int lane) {
+    int r = lane & 15;
+    double a[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        a[c] = Akk[swz(r, c)];
+        x[c] = (r == c) ? 1.0 : 0.0;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        __asm__ volatile("" : "+v"(r));
+        const double djj = rdlane(a[j], j);
+        ok = ok && (djj > 0.0);
+        const double il = rsqn<2>(djj);
+        a[j] = (r >= j) ? a[j] * il : 0.0;
+        x[j] *= il;
+#pragma unroll
+        for (int c = j + 1; c < 16; c++) {
+            const double Lcj = rdlane(a[j], c);
+            a[c] -= a[j] * Lcj;
+            x[c] -= Lcj * x[j];
+        }
     }
     if (lane < 16) {
 #pragma unroll
@@ -175,7 +210,8 @@ __device__ __forceinline__ bool diag_factor2(double* Akk, double* colbuf, volati
 
 template <int V>
 __device__ __forceinline__ bool factor_v(double* Akk, double* colbuf, int lane) {
-    if constexpr (V >= 5) return diag_factor_lds<2, true>(Akk, colbuf, lane);
+    if constexpr (V == 7) return diag_factor_c4(Akk, lane);
+    else if constexpr (V >= 5) return diag_factor_lds<2, true>(Akk, colbuf, lane);
     else if constexpr (V >= 3) return diag_factor_lds<V == 3 ? 2 : 1>(Akk, colbuf, lane);
     else return diag_factor<V>(Akk, lane);
 }
@@ -271,7 +307,7 @@ int main() {
     hipMalloc(&dout, 256 * 8);
     hipMalloc(&dc, 8);
     hipMemcpy(din, A.data(), 256 * 8, hipMemcpyHostToDevice);
-    for (int v = 0; v < 7; v++) {
+    for (int v = 0; v < 8; v++) {
         if (v == 0) hipLaunchKernelGGL(k_diag<0>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 1) hipLaunchKernelGGL(k_diag<1>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 2) hipLaunchKernelGGL(k_diag<2>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
@@ -279,6 +315,7 @@ int main() {
         if (v == 4) hipLaunchKernelGGL(k_diag<4>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 5) hipLaunchKernelGGL(k_diag<5>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 6) hipLaunchKernelGGL(k_diag<6>, dim3(1), dim3(128), 0, 0, din, dout, dc, 64);
+        if (v == 7) hipLaunchKernelGGL(k_diag<7>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         std::vector<double> o(256);
         long long c;
         hipMemcpy(o.data(), dout, 256 * 8, hipMemcpyDeviceToHost);
