@@ -2566,7 +2566,9 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     return ok;
 }
 
-// (Tried in round 4: broadcasting L[.][j] through LDS instead of v_readlane -- 914 instead of
+// (Tried in round 4: a scheduling barrier after each pivot -- 11 % fewer cycles in
+// bench/diag_probe.hip (7506 vs 8413), no change inside the solve (3.6 us per block).
+// Broadcasting L[.][j] through LDS instead of v_readlane -- 914 instead of
 // 1356 instructions and 21 % faster alone (bench/diag_probe.hip), but its VGPR operands do not
 // fit the solves' 128-VGPR budget (1024-thread workgroups): 1 KiB/lane of scratch, the solve
 // 59 -> 152 us; the same with the inverse on a second wave fed through LDS (variant 6) spilled
