@@ -39,7 +39,7 @@ import gen_synth
 
 NREP = 4
 LEVELS = {"5ps": 5e-12, "30ps": 3e-11}
-DOWNHILL = {"pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr", "j0740"}
+DOWNHILL = {"pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr", "phoff_dmn", "j0740"}
 
 _GRAB = {}
 
@@ -55,7 +55,8 @@ SYNTH = {"pta_iso": (1, ""), "pta_ell1": (2, "ELL1"), "pta_dd": (3, "DD"), "pta_
          "pta_ddk": (16, "DDK"), "pta_ddk_nk": (17, "DDK_NK"), "ell1h_h3": (11, "ELL1H_H3"),
          "ell1h_h4": (12, "ELL1H_H4"), "ell1h_stig": (13, "ELL1H_STIG")}
 PHOFF = {"wls_phoff": (5, False, "wls", False), "ecorr_phoff": (6, True, "gls", False),
-         "phoff_red": (7, False, "gls", True), "phoff_ecorr": (8, True, "gls", True)}
+         "phoff_red": (7, False, "gls", True), "phoff_ecorr": (8, True, "gls", True),
+         "phoff_dmn": (9, False, "gls", True)}
 
 
 def rebuild(name):
@@ -70,7 +71,7 @@ def rebuild(name):
         gen_synth.gen_j0740()
     elif name in PHOFF:
         seed, ecorr, fit, frozen = PHOFF[name]
-        gen_phoff.gen(name, seed, ecorr, fit, frozen=frozen)
+        gen_phoff.gen(name, seed, ecorr, fit, frozen=frozen, dmn=name == "phoff_dmn")
     elif name == "b1855":
         from gen_stage import rebuild as stage_rebuild
         m, t = stage_rebuild("b1855")

@@ -11,6 +11,8 @@
                 Offset column in the fit, and the Woodbury chi2 appends the ones column with
                 Phi = 1e40 (residuals.py:583-585) -- GLSFitter, DownhillGLSFitter.
 * phoff_ecorr : the same with ECORR as well (four frequencies per epoch).
+* phoff_dmn   : phoff_red with PLDMNoise beside PLRedNoise: the ones column's row of Sigma
+                then includes the DM modes' (1400 MHz / f)^2-scaled weighted sums.
 N = 600 TOAs each.  Usage: run_ref.sh gen_phoff.py [name ...]
 """
 import io
@@ -34,17 +36,19 @@ def par_phoff(seed, ecorr):
     return "\n".join(lines) + "\n"
 
 
-def par_frozen(seed, ecorr):
+def par_frozen(seed, ecorr, dmn=False):
     lines = pta_par(seed, "").splitlines()  # keeps the template's PLRedNoise
     lines.append("PHOFF 0.05")              # frozen
     if ecorr:
         lines.append("ECORR -f fake 0.8")
+    if dmn:  # PLDMNoise (noise_model.py:443), as pta_dmn
+        lines += ["TNDMAMP -13.2", "TNDMGAM 2.8", "TNDMC 20"]
     return "\n".join(lines) + "\n"
 
 
-def gen(name, seed, ecorr, fit, frozen=False):
+def gen(name, seed, ecorr, fit, frozen=False, dmn=False):
     np.random.seed(seed)
-    par = par_frozen(seed, ecorr) if frozen else par_phoff(seed, ecorr)
+    par = par_frozen(seed, ecorr, dmn) if frozen else par_phoff(seed, ecorr)
     model = get_model(io.StringIO(par))
     ts = sim.make_fake_toas_uniform(53000, 56652, 600, model,
                                     freq=np.array([800, 1200, 1600, 2000]) * u.MHz,
@@ -72,3 +76,5 @@ if __name__ == "__main__":
         gen("phoff_red", 7, False, "gls", frozen=True)
     if "phoff_ecorr" in which:
         gen("phoff_ecorr", 8, True, "gls", frozen=True)
+    if "phoff_dmn" in which:
+        gen("phoff_dmn", 9, False, "gls", frozen=True, dmn=True)

@@ -2156,22 +2156,43 @@ __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs
 // appends the ones column with Phi = 1e40 (residuals.py:583-585).  Its row of Sigma cannot
 // come from the Gram (no column of M is the ones column), so k_onesrow forms it per instance
 // before the solve: 1^T W~ F_j and 1^T W~ 1 (W~: ECORR eliminated, as the Gram is), the
-// Fourier part from the pulsar's weighted trig sums (F_2h = sin (h+1) theta, F_2h+1 = cos;
-// PLRedNoise modes only: the host refuses PLDMNoise here) and the ECORR Schur term from
-// k_ecorr's epoch sums.  vg instances take the same row from trig_uwu (no ECORR there).
+// PLRedNoise part from the pulsar's weighted trig sums (F_2h = sin (h+1) theta, F_2h+1 =
+// cos), the PLDMNoise modes' (their (1400 MHz / f)^2 scale per TOA has no trig-sum form) as
+// weighted sums of their stored columns of M, and the ECORR Schur term from k_ecorr's epoch
+// sums.  vg instances take the same row from trig_uwu (no ECORR, no PLDMNoise there).
 __device__ __forceinline__ bool ones_virtual(const pint_spec_t& S) { return S.o_PHOFF >= 0 && !S.wb_noones; }
 
 __global__ __launch_bounds__(64) void k_onesrow(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                 const double* __restrict__ esum, const double* __restrict__ eD,
                                                 const double* __restrict__ eW, const double* __restrict__ eC,
-                                                int compact, double* __restrict__ ones) {
+                                                int compact, const double* __restrict__ M, double* __restrict__ ones) {
     const InstDev I = insts[blockIdx.x];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
     if (!ones_virtual(S) || !(S.nred > 0 || Pd.nep > 0)) return;
     const bool cmp = compact && Pd.dsplit;
-    const int R = 2 * S.nred;
+    const int R = 2 * S.nred, jd = 2 * S.dmn0;  // columns >= jd (< R): PLDMNoise modes
+    if (jd < R) {  // sum_i w_i F_ij over the stored DM-noise columns, in a fixed order
+        const int n = I.n;
+        const double* Fb = M + I.moff + (long)(cmp ? Pd.red0c : S.ncol) * n;
+        for (int j = jd; j < R; j++) {
+            double acc = 0.0;
+            for (int i = threadIdx.x; i < n; i += 64) {
+                const double is = Pd.isig[i];
+                acc += Fb[(long)j * n + i] * (is * is);
+            }
+            acc = wave_sum(acc);
+            if (threadIdx.x == 0) {
+                for (int e = 0; e < Pd.nep; e++) {
+                    const double w = eW[I.epoff + e];
+                    acc -= w * esum_col(Pd, I, esum, eC, cmp, e, S.ncol + j) / eD[I.epoff + e];
+                }
+                ones[I.coff + j] = acc;
+            }
+        }
+    }
     for (int j = threadIdx.x; j <= R; j += 64) {
+        if (j >= jd && j < R) continue;  // (above)
         double v;
         if (j < R) {
             const int h = j / 2 + 1;
@@ -5679,7 +5700,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         }
         if (ones) {
             hipLaunchKernelGGL(k_onesrow, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_eC, cmp, ctx->d_ones);
+                               ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->d_eC, cmp, ctx->d_M, ctx->d_ones);
             HIPCHK(hipGetLastError());
         }
     }

@@ -100,12 +100,9 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         spec.o_PHOFF = place("PHOFF")
     phoff_free = has_phoff and "PHOFF" in model.free_params
     spec.wb_noones = 1 if phoff_free else 0
-    if has_phoff and not phoff_free and use_gls_basis and "PLDMNoise" in model.components:
-        # the Woodbury chi2 then appends a column of ones the fit layout does not carry; its
-        # row of Sigma is formed from the weighted trig sums (k_onesrow), which cover the
-        # PLRedNoise harmonics and ECORR but not PLDMNoise's (1400 MHz / f)^2-scaled modes
-        raise NotImplementedError("PhaseOffset with a frozen PHOFF and PLDMNoise "
-                                  "(residuals.py:583-585 ones column) is not supported")
+    # (a frozen PHOFF with correlated noise: the Woodbury chi2 appends a column of ones the fit
+    # layout does not carry; k_onesrow forms its row of Sigma -- PLRedNoise from the weighted
+    # trig sums, PLDMNoise from the stored basis columns, ECORR from the epoch sums)
     ak = model.astrometry_kind
     spec.astrometry = ak
     if ak:

@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise",
          "white_mjd", "ecorr_fit", "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk",
-         "phoff_red", "phoff_ecorr"]
+         "phoff_red", "phoff_ecorr", "phoff_dmn"]
 GLS_NAMES = ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ecorr_fit", "ell1h_h3", "ell1h_h4",
-             "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red", "phoff_ecorr"]
+             "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red", "phoff_ecorr", "phoff_dmn"]
 
 
 @pytest.fixture(scope="module", params=NAMES)
@@ -188,7 +188,8 @@ def test_gls_fit(name):
     assert np.max(np.abs(f.resids.time_resids - z["gls_post_resid"])) < 2e-10
 
 
-@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr"])
+@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr",
+                                  "phoff_dmn"])
 def test_downhill_gls(name):
     from pint_amd import DownhillGLSFitter
     from pint_amd.fitter import MaxiterReached, StepProblem

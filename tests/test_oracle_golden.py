@@ -12,7 +12,7 @@ import pint_oracle as O
 
 NAMES = ["ngc6440e", "b1855", "j0740", "pta_iso", "pta_ell1", "pta_dd", "wls_phoff", "ecorr_phoff", "wls_noise", "white_mjd", "ecorr_fit",
          "ell1h_h3", "ell1h_h4", "ell1h_stig", "pta_bt",
-         "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red", "phoff_ecorr"]
+         "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red", "phoff_ecorr", "phoff_dmn"]
 DELAY_MAP = {"delay_solar_system_geometric_delay": "geometric", "delay_solar_system_shapiro_delay": "shapiro",
              "delay_constant_dispersion_delay": "dm", "delay_DMX_dispersion_delay": "dmx",
              "delay_binarymodel_delay": "binary", "delay_FD_delay": "fd", "delay_total": "delay"}
@@ -173,7 +173,7 @@ def test_wls_fit_phoff():
 
 @pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "j0740", "b1855", "ecorr_phoff", "ell1h_h3", "ell1h_h4",
                                   "ell1h_stig", "pta_bt", "pta_dmn", "pta_ddk", "pta_ddk_nk", "phoff_red",
-                                  "phoff_ecorr"])
+                                  "phoff_ecorr", "phoff_dmn"])
 def test_gls_fit(name):
     om, toas, z, meta = fixture(name)
     om2, st, chi2 = O.fit_once(om, toas, gls=True)
@@ -211,7 +211,8 @@ def test_downhill_wls():
         assert abs(st["errs"][j] / sig - 1) < 1e-6, p
 
 
-@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr"])
+@pytest.mark.parametrize("name", ["pta_iso", "pta_ell1", "pta_dd", "ecorr_phoff", "phoff_red", "phoff_ecorr",
+                                  "phoff_dmn"])
 def test_downhill_gls(name):
     om, toas, z, meta = fixture(name)
     best, status, st, chi2 = O.downhill_fit(om, toas, gls=True, maxiter=10)
