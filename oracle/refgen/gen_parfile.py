@@ -22,7 +22,8 @@ PARS = {"ngc6440e": "NGC6440E.par", "b1855": "B1855+09_NANOGrav_9yv1.gls.par", "
         "pta_bt": "pta_bt.par", "pta_dmn": "pta_dmn.par", "pta_ddk": "pta_ddk.par", "pta_ddk_nk": "pta_ddk_nk.par", "wb_dd": "wb_dd.par",
         "c5_iso": "c5_iso.par", "c5_ell1": "c5_ell1.par", "c5_dd": "c5_dd.par",
         "planet_ngc": "planet_ngc.par", "planet_b1855": "planet_b1855.par",
-        "dmx_overlap": "dmx_overlap.par", "phoff_red": "phoff_red.par", "phoff_ecorr": "phoff_ecorr.par"}
+        "dmx_overlap": "dmx_overlap.par", "phoff_red": "phoff_red.par", "phoff_ecorr": "phoff_ecorr.par",
+        "phoff_dmn": "phoff_dmn.par"}
 
 
 
