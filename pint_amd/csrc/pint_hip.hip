@@ -4600,6 +4600,8 @@ pint_ctx* pint_ctx_create(int device) {
         ctx->err = "hipSetDevice failed";
         return ctx;
     }
+    // (stream priorities -- the kernel stream highest, the copy stream lowest -- measured no
+    // different in round 4: 0.376-0.384 vs 0.380-0.387 ms per 68-pulsar step)
     hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
     // the cross-stream events are waited on by the device (and ev_done by the host only for
