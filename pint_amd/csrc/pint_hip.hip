@@ -3458,7 +3458,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
 }
 
 // k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred
-// solves export X, U and the scalings to d_xw); up to COV_WG workgroups per instance, each staging
+// solves export X, U and the scalings to d_xw); COV_WG workgroups per instance, each staging
 // the instance's export in LDS and forming W itself; launched by pint_read_step when the
 // errors or the covariance are read (on the copy stream, off the fit step's critical path)
 constexpr int COV_WG = 3;
@@ -6042,11 +6042,11 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
     hipStream_t st = ctx->lazy ? ctx->cstream : ctx->stream;
     if (ctx->lazy) HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_solved, 0));
     if ((cov || errs) && ctx->cov_pending) {  // the DMX-eliminated solve's W, DMX errors, covariance
-        // at most ~half the CUs: in a pipelined step this runs beside the next step's evaluation
-        // with M, which it slowed by 7 % on the 68-pulsar PTA at 3 workgroups per instance (204
-        // CUs; 1 per instance: 0.376-0.386 vs 0.406-0.410 ms per step), while a small batch's
-        // copy stream wants the 3 (9-34 pulsars: 1-2 us per step better)
-        const int cov_wg = std::max(1, std::min(COV_WG, 128 / std::max(1, ctx->ninst)));
+        // (round 4: capping it at ~half the CUs, beside the next pipelined step's evaluation,
+        // looked 7 % faster in one A/B sweep and not at all in a second -- the 68-pulsar step is
+        // bimodal run to run on one box, 0.38 or 0.41 ms; PINT_COV_WG sets a fixed count)
+        static const int cov_env = getenv("PINT_COV_WG") ? atoi(getenv("PINT_COV_WG")) : 0;
+        const int cov_wg = cov_env > 0 ? cov_env : COV_WG;
         hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ctx->ninst, cov ? cov_wg : 1), dim3(1024), ctx->cov_lds, st,
                            ctx->d_psrs, ctx->d_inst, ctx->d_xw, ctx->cov_mode, cov ? ctx->d_cov : nullptr,
                            ctx->d_errs);
