@@ -49,6 +49,38 @@ class PintError(RuntimeError):
 
 
 _lib = None
+HIP_RUNTIME = None  # the libamdhip64 this process shares with torch (None: the system one)
+
+
+def _share_torch_hip_runtime():
+    """One HIP runtime per process, whatever is loaded first.
+
+    libpint_hip.so needs libamdhip64.so.7 (RUNPATH /opt/rocm/lib).  The ROCm torch wheel
+    ships its own libamdhip64 + libhsa-runtime64 (soname libamdhip64.so.7 as well, loaded
+    through libtorch_hip's NEEDED "libamdhip64.so" and RPATH $ORIGIN).  If this library
+    loads first, the later `import torch` cannot match "libamdhip64.so" against the loaded
+    soname and maps the wheel's copy beside it: two HIP/HSA runtimes in one process, and
+    torch's sees no device (torch.cuda.is_available() False; the RCCL process group of
+    pta.gather_rows / gridutils.gather_blocks then cannot start).  Loading the wheel's
+    runtime first (by path, without importing torch) makes libpint_hip.so's NEEDED resolve
+    to it by soname, and torch's own later load to the same file (same inode): one runtime
+    either way.  PINT_HIP_RUNTIME=system keeps /opt/rocm's (for processes without torch)."""
+    global HIP_RUNTIME
+    if os.environ.get("PINT_HIP_RUNTIME", "torch") == "system":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            HIP_RUNTIME = p
+            return
 
 
 def lib():
@@ -58,6 +90,7 @@ def lib():
         return _lib
     if not os.path.exists(LIBPATH):
         raise RuntimeError(f"HIP extension missing: {LIBPATH} (run __graft_entry__.build())")
+    _share_torch_hip_runtime()
     L = C.CDLL(LIBPATH)
     vp = C.c_void_p
     L.pint_ctx_create.restype = vp

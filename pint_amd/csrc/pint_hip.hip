@@ -3059,7 +3059,16 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const GramView G = gram_view(Pd, I, Gpart, Pd.dsplit != 0, Sd, DD);
-        if (!woodbury_sigma<NW>(G, Pd, S, pval(tables + I.toff, S.o_F), lds, wave, lane, &sflag, sigL + (long)I.soff,
+        // F0 scales the stored Offset column only (not on the vg path, whose ones column
+        // comes from the trig sums).  With the fused apply the other half of this grid
+        // rewrites the tables, so F0 must not be read then: the host fuses only all-vg
+        // batches, and an instance that breaks that invariant fails here instead of racing.
+        if (apply_tables && !Pd.vg) {
+            if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
+            return;
+        }
+        const double F0 = Pd.vg ? 0.0 : pval(tables + I.toff, S.o_F);
+        if (!woodbury_sigma<NW>(G, Pd, S, F0, lds, wave, lane, &sflag, sigL + (long)I.soff,
                                 ones ? ones + I.coff : nullptr))
             if (threadIdx.x == 0) atomicOr(status, 1 << PINT_E_SIGMA);
         return;

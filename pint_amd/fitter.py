@@ -422,6 +422,7 @@ class BatchFit:
                     else:
                         self.s.apply_step(applied)
                     bad = np.zeros(n, dtype=bool)
+                    got = None  # this trial's enqueued chi2 (never a previous trial's)
                     try:
                         self.s.eval(want_M=False)
                         if lazy:
@@ -433,10 +434,15 @@ class BatchFit:
                     except L.PintError as e:
                         if e.code not in self.EVAL_ERRORS:
                             raise
+                        if lazy:  # status and chi2 read synchronously from here on
+                            self.s.set_lazy(False)
+                            lazy = False
                         bad = self.s.inst_status() != 0
                         if not bad.any():
                             raise
-                        new_chi2, _ = got() if lazy else self._chi2_now()
+                        # the chi2 enqueued before the error (check() has synchronised it),
+                        # else recomputed synchronously
+                        new_chi2, _ = got() if got is not None else self._chi2_now()
                 finally:
                     if lazy:
                         self.s.set_lazy(False)

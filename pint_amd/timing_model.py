@@ -74,6 +74,7 @@ class TimingModel:
         self._params[p.name] = p
         self.components.setdefault(p.component or "TimingModel", []).append(p.name)
         object.__setattr__(self, "_order", None)
+        object.__setattr__(self, "_names", {})
 
     @property
     def params(self) -> List[str]:
@@ -149,13 +150,29 @@ class TimingModel:
             return 2
         return 0
 
+    def _names_of(self, key, build):
+        """Name lists derived from the parameter set alone, cached until the next add_param
+        (parameters are never removed): build_layout / validate ask for them many times per
+        upload, and a regex pass over ~250 parameters each time dominated the host layout."""
+        cache = self.__dict__.get("_names")
+        if cache is None or cache.get("_n") != len(self._params):  # (a shallow copy shares _params)
+            cache = {"_n": len(self._params)}
+            object.__setattr__(self, "_names", cache)
+        hit = cache.get(key)
+        if hit is None:
+            hit = cache[key] = tuple(build())
+        return list(hit)
+
     def prefix_list(self, prefix_rx: str) -> List[str]:
-        out = []
-        for n, p in self._params.items():
-            m = re.match(prefix_rx, n)
-            if m:
-                out.append((int(m.group(1)), n))
-        return [n for _, n in sorted(out)]
+        def build():
+            rx = re.compile(prefix_rx)
+            out = []
+            for n in self._params:
+                m = rx.match(n)
+                if m:
+                    out.append((int(m.group(1)), n))
+            return [n for _, n in sorted(out)]
+        return self._names_of(("prefix", prefix_rx), build)
 
     def spin_terms(self) -> List[str]:
         return self.prefix_list(r"^F(\d+)$")
@@ -170,7 +187,10 @@ class TimingModel:
         return self.prefix_list(r"^FD(\d+)$")
 
     def mask_params(self, base: str) -> List[str]:
-        return [n for n, p in self._params.items() if p.kind == "mask" and re.match(rf"^{base}\d+$", n)]
+        def build():
+            rx = re.compile(rf"^{base}\d+$")
+            return [n for n, p in self._params.items() if p.kind == "mask" and rx.match(n)]
+        return self._names_of(("mask", base), build)
 
     # -- validation (the parts of Component.validate that matter on the hot path) -----
     def validate(self):

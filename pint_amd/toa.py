@@ -171,16 +171,12 @@ class TOAs:
             return np.array([], dtype=int)
         if len(key_value) == 2:
             raise NotImplementedError("range selection on a flag column")
-        return np.where(self._flag_array(k, col) == key_value[0])[0]
-
-    def _flag_array(self, k, col):
-        """The flag column as a numpy string array (cached per column object)."""
-        cache = self.__dict__.setdefault("_flag_np", {})
-        hit = cache.get(k)
-        if hit is None or hit[0] is not col or len(hit[1]) != len(col):
-            hit = (col, np.asarray(["" if c is None else str(c) for c in col]))
-            cache[k] = hit
-        return hit[1]
+        # each entry compared with == as the reference's selector does (an object array keeps
+        # None and non-string values as they are); built per call, so an in-place edit of
+        # the column is always seen
+        arr = np.empty(len(col), dtype=object)
+        arr[:] = col
+        return np.where(arr == key_value[0])[0]
 
     # -- persistence -----------------------------------------------------------------
     def save(self, path: str):

@@ -49,6 +49,7 @@ def downhill_bar(name, p, floor=1e-3):
 
 
 _SPREAD = None
+SPREAD_MAX_PS = 30.0  # the largest residual shift oracle/refgen/gen_fit_spread.py measured
 
 
 def rms_ps(a, b) -> float:
@@ -63,10 +64,16 @@ def chi2_bar(name, kind, resid_rms_ps, floor=1e-9):
     residuals under test differ from the reference's.  tests/golden/fit_spread.json
     (oracle/refgen/gen_fit_spread.py) holds max |chi2 / chi2_0 - 1| of the reference under fixed
     per-TOA N(0, 5 ps) and N(0, 30 ps) residual shifts; the bar scales the larger per-ps rate
-    to the measured rms difference `resid_rms_ps` (at least the 5 ps longdouble floor)."""
+    to the measured rms difference `resid_rms_ps` (at least the 5 ps longdouble floor).
+
+    The spread is calibrated over 5-30 ps of residual difference, so a measured rms above
+    SPREAD_MAX_PS fails here: a residual drift must fail the test, not widen its own bar."""
     global _SPREAD
     if _SPREAD is None:
         _SPREAD = json.load(open(os.path.join(GOLDEN, "fit_spread.json")))
+    assert float(resid_rms_ps) <= SPREAD_MAX_PS, (
+        f"{name}/{kind}: residuals differ from the reference's by {float(resid_rms_ps):.1f} ps rms, beyond the "
+        f"{SPREAD_MAX_PS:g} ps the chi2 spread was calibrated over")
     d = _SPREAD[name]
     per_ps = max(d["5ps"][kind] / 5.0, d["30ps"][kind] / 30.0)
     return max(floor, 2.0 * per_ps * max(float(resid_rms_ps), 5.0))

@@ -83,3 +83,45 @@ def test_overlap_device_parity():
         d = float((LD(f.model[p].value) - ref_value(meta, "wls_params", p)) / LD(s))
         assert abs(d) < 1e-3, (p, d)
         assert abs(f.model[p].uncertainty / s - 1) < 1e-6, p
+
+
+@pytest.mark.parametrize("case", ["touching", "disjoint", "shuffled", "gaps_and_pairs", "nested"])
+def test_pack_bin_assignment_matches_the_per_bin_rule(case):
+    """pack_toas assigns bins by two sorted searches when the ranges are sorted with
+    non-decreasing ends and no TOA lies in more than two bins (the PTA's consecutive bins
+    share their endpoints); anything else takes the per-bin pass.  Both must give every TOA
+    its selecting bins in parameter order (toa_select.py:101, inclusive)."""
+    from pint_amd.engine import build_layout, pack_toas
+    model, toas, z, meta = load("dmx_overlap")
+    names = model.dmx_params()
+    mjd = np.concatenate([toas.get_mjds(), np.atleast_1d(toas.tzr["mjd_float"])])
+    rng = np.random.default_rng(7)
+    lo, hi = float(mjd[:-1].min()), float(mjd[:-1].max())
+    m = len(names)
+    edges = np.linspace(lo - 1, hi + 1, m + 1)
+    r1, r2 = edges[:-1].copy(), edges[1:].copy()
+    if case == "touching":     # a TOA exactly on a shared endpoint is in both bins
+        k = np.arange(1, m)   # each inner edge moved onto the nearest TOA
+        r2[k - 1] = r1[k] = np.sort(mjd[np.argmin(np.abs(mjd[:-1, None] - edges[None, k]), axis=0)])
+    elif case == "disjoint":
+        r2 -= 1e-3
+    elif case == "shuffled":   # parameter order != time order
+        p = rng.permutation(m)
+        r1, r2 = r1[p], r2[p]
+    elif case == "gaps_and_pairs":
+        r1[::2] += 0.3 * (r2[::2] - r1[::2])
+        r2[1::2] = r2[1::2] + 0.5 * (edges[1] - edges[0])  # overlaps the next bin: pairs of bins
+    else:                      # one bin inside another: the per-bin pass
+        r1[1], r2[1] = r1[0] + 0.1, r2[0] - 0.1
+    for nm, a, b in zip(names, r1, r2):
+        model["DMXR1_" + nm[4:]].value = LD(a)
+        model["DMXR2_" + nm[4:]].value = LD(b)
+    t, keep = pack_toas(build_layout(model, toas))
+    da, db, x = keep[11], keep[12], keep[14]
+    if case == "touching":
+        assert (db >= 0).sum() >= 1  # some TOA sits on a shared endpoint
+    for i in range(len(mjd)):
+        want = [j for j, nm in enumerate(names)
+                if float(model["DMXR1_" + nm[4:]].value) <= mjd[i] <= float(model["DMXR2_" + nm[4:]].value)]
+        got = [b for b in (da[i], db[i]) if b >= 0] + (list(x[x[i]:x[i + 1]]) if x is not None else [])
+        assert got == want, (case, i, got, want)

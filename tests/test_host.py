@@ -114,6 +114,22 @@ def test_library_exports_header_symbols():
     assert lib.pint_device_count() >= 0 or True  # callable without a GPU (returns 0 / error)
 
 
+def test_one_hip_runtime_whatever_loads_first():
+    """libpint_hip.so loaded before `import torch` must not leave two HIP/HSA runtimes in the
+    process (torch's would then see no device and the RCCL gathers could not start)."""
+    _lib_path()
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from pint_amd import _lib; _lib.lib()\n"
+            "import torch\n"
+            "m = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "h = {l.split()[-1] for l in open('/proc/self/maps') if 'libhsa-runtime64' in l}\n"
+            "print(len(m), len(h))\n") % ROOT
+    env = dict(os.environ)
+    env.pop("PINT_HIP_RUNTIME", None)
+    out = subprocess.run([sys.executable, "-c", code], check=True, capture_output=True, text=True, env=env)
+    assert out.stdout.split() == ["1", "1"], out.stdout
+
+
 def test_struct_layout_matches_header():
     """ctypes mirrors (pint_amd/_lib.py) == the C header layout (compiled with gcc)."""
     from pint_amd import _lib

@@ -31,8 +31,15 @@ def nccl_group():
     import torch
     import torch.distributed as dist
     from pint_amd import pta
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+    from pint_amd import _lib
+    ndev = _lib.lib().pint_device_count()
+    if ndev <= 0:
+        pytest.skip("no GPU visible to libpint_hip")
+    # the library sees a device, so torch must too: a False here is a second HIP runtime in
+    # the process (pint_amd._lib._share_torch_hip_runtime), never a reason to skip
+    maps = sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln})
+    assert torch.cuda.is_available(), (f"libpint_hip sees {ndev} device(s) but torch sees "
+                                       f"{torch.cuda.device_count()}; HIP runtimes mapped: {maps}")
     os.environ.setdefault("LOCAL_RANK", "0")
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", world_size=1, rank=0)
     pta.FORCE_COLLECTIVE = True
