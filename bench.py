@@ -263,8 +263,8 @@ def cold_start(items, rank):
 
 
 def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pass=True):
-    """Time `steps` fit steps of the Session's batch (warm-up first), pipelined two deep; one
-    step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.
+    """Time `steps` fit steps of the Session's batch (warm-up first), pipelined L.NSLOT deep;
+    one step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.
 
     graph: 0 enqueue every launch of every step from the host; 1 capture the step once per
     pipeline slot into a HIP graph and replay it (the same kernels, copies and outputs, one
@@ -272,11 +272,14 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
     faster (a small batch's step is shorter than its ~20 host launches take to enqueue).
     Returns (max-over-ranks seconds, summed Gram event time of the sampled steps, their
     count, step, launch mode)."""
+    from collections import deque
+    from pint_amd import _lib as L
     from pint_amd.engine import Session
     s.save_tables()        # the initial models, resident in HBM like the TOAs
     s.set_lazy(True)
 
-    def step():
+    def step_calls():
+        """The step as separate library calls (the graph capture records these)."""
         s.restore_tables()     # every step fits from the initial models (device->device copy)
         s.eval(want_M=Session.FIT)
         s.fit_step_apply(1, 1.0)  # the GLS step and the full-step update (fused into the solve)
@@ -285,6 +288,15 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
         s.eval(want_M=False)
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
         return out, nz, c2
+
+    def step():
+        """The same step enqueued by one call (pint_fit_step_enqueue, closes the step);
+        returns its slot."""
+        return s.fit_step_enqueue(restore=True, lam=1.0)[0]
+
+    def replay():
+        s.replay()
+        return s.step_end()
 
     # Gram timing: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop on
     # its first/last dispatch packet, or marker packets on the other Gram paths), on every
@@ -295,30 +307,43 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
     s.set_timing_every(GRAM_EVERY)
 
     def run(nsteps, launch):
-        """nsteps steps pipelined two deep (Session.step_end / check_step); launch() enqueues
-        one step.  Returns the summed Gram-kernel event time of the sampled steps and their
-        count."""
-        kt, nk, prev = 0.0, 0, None
-        for _ in range(nsteps):
-            launch()
-            cur = s.step_end()
-            if prev is not None:
-                s.check_step(prev)
-                t = s.timing()[SLOT_GRAM]
-                kt, nk = kt + t, nk + (t > 0)
-            prev = cur
-        if prev is not None:
-            s.check_step(prev)
+        """nsteps steps pipelined L.NSLOT deep: before a step is enqueued, the step that last
+        used its slot is checked (Session.check_step), so the device holds up to NSLOT - 1
+        queued steps while the host enqueues the next; launch() enqueues and closes one
+        step and returns its slot.  Returns the summed Gram-kernel event time of the
+        sampled steps and their count."""
+        kt, nk, pend = 0.0, 0, deque()
+        trace = [] if os.environ.get("PINT_BENCH_TRACE") else None
+
+        def check_one():
+            nonlocal kt, nk
+            s.check_step(pend.popleft())
             t = s.timing()[SLOT_GRAM]
             kt, nk = kt + t, nk + (t > 0)
+
+        for _ in range(nsteps):
+            if len(pend) >= L.NSLOT:
+                if trace is not None:
+                    trace.append(("w", time.perf_counter()))
+                check_one()
+            if trace is not None:
+                trace.append(("l", time.perf_counter()))
+            pend.append(launch())
+        while pend:
+            check_one()
+        if trace is not None and len(trace) > 2:
+            d = [(trace[i + 1][1] - trace[i][1], i, trace[i][0]) for i in range(len(trace) - 1)]
+            big = sorted(d, reverse=True)[:4]
+            log(f"[trace] {nsteps} steps: largest host intervals (ms, index, after) "
+                f"{[(round(x * 1e3, 3), i, k) for x, i, k in big]}; median {np.median([x for x, _, _ in d]) * 1e3:.3f}")
         return kt, nk
 
     run(warmup, step)
     use_graph = False
     if graph in (1, "1", "auto"):
         s.set_timing_mask(0)
-        for _ in range(2):  # one graph per pipeline slot
-            s.capture(step)
+        for _ in range(L.NSLOT):  # one graph per pipeline slot
+            s.capture(step_calls)
             s.check_step(s.step_end())
         if graph == "auto":
             ntry = max(10, min(50, steps // 2))
@@ -326,16 +351,29 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
             run(ntry, step)
             t_direct = time.perf_counter() - t0
             t0 = time.perf_counter()
-            run(ntry, s.replay)
+            run(ntry, replay)
             t_graph = time.perf_counter() - t0
             use_graph = max_over_ranks(t_graph - t_direct) < 0.0  # the same choice on every rank
         else:
             use_graph = True
-    barrier()
-    t0 = time.perf_counter()
-    run(steps, s.replay if use_graph else step)
-    barrier()
-    dt = max_over_ranks(time.perf_counter() - t0)
+    # Python's cyclic GC: a full collection traverses every host object -- the TOA tables and
+    # flag lists of the whole PTA -- and took ~7 ms whenever it fell inside the timed steps
+    # (a 20-step run: 0.40 or 0.73 ms per step by where it fell).  Collected once here and
+    # frozen (the objects alive now are never traversed again), no collection in the timed
+    # steps; a compiled host would have no such pause.
+    import gc
+    gc.collect()
+    gc.freeze()
+    gc.disable()
+    try:
+        barrier()
+        t0 = time.perf_counter()
+        run(steps, replay if use_graph else step)
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+    finally:
+        gc.enable()
+        gc.unfreeze()
     # the Gram kernel's time: the same step with its events, after the timed region
     kt, nk = 0.0, 0
     if gram_pass:
@@ -435,8 +473,7 @@ def roofline(s, lays, kt_gram, step, args):
     kt = np.zeros(8)
     nprof = 3
     for _ in range(nprof):
-        step()
-        s.check()
+        s.check_step(step())  # (one step in flight: its events alone on the streams)
         kt += s.timing()
     kt /= nprof
     names = ["k_eval", "k_resid", "gram_span", "k_solve", "k_eval_M", "k_woodbury", "k_gram", "k_greduce"]

@@ -158,6 +158,17 @@ int pint_add_pulsar(pint_ctx *ctx, const pint_toas_t *toas, const pint_spec_t *s
  * dd pairs in par-file units).  Replaces the parameter state of a TimingModel
  * (parameter.py values) for a whole batch. */
 int pint_set_instances(pint_ctx *ctx, int ninst, const int32_t *inst_psr, const double *tables);
+
+/* A grid of npts instances of pulsar psr (gridutils.py:166 grid_chisq, :392, :588, :773 -- the
+ * reference forms one model copy per point, gridutils.py:72): each point's table is `base`
+ * (tstride doubles) with nvar (hi, lo) entries replaced, formed on the device from the base
+ * table and the grid axes.  Variable j (table offset var_toff[j]) of point k takes the pair
+ * vals_j[((k0 + k) / var_stride[j]) % var_size[j]], vals_j = the var_size[j] (hi, lo) pairs
+ * of variable j in `vals` (the variables' pairs concatenated): a meshgrid's axis, or every
+ * point's own value (stride 1).  k0: the global index of the first point (a rank's block).
+ * Otherwise as pint_set_instances. */
+int pint_set_grid(pint_ctx *ctx, int psr, int npts, const double *base, int nvar, const int32_t *var_toff,
+                  const int64_t *var_stride, const int64_t *var_size, const double *vals, int64_t k0);
 int pint_get_tables(pint_ctx *ctx, double *tables_out);
 int pint_set_tables(pint_ctx *ctx, const double *tables);
 
@@ -262,12 +273,26 @@ int pint_check(pint_ctx *ctx);
 
 /* Pipelined steps (replaces the per-step pint_check of a lazy-mode loop; no reference
  * counterpart -- the reference's fitters are synchronous).  pint_step_end closes the work
- * enqueued since the previous step_end and returns its slot (0/1) in *slot; launches
- * after it go to the other slot (own status word, timing events).  pint_check_step waits
- * for that step only and returns its status, so the host enqueues step k+1 while the
- * device runs step k.  At most two steps in flight: check slot s before ending the step
- * after the next.  Pinned output buffers must be per slot. */
+ * enqueued since the previous step_end and returns its slot (0 .. PINT_NSLOT-1) in *slot;
+ * launches after it go to the next slot (own status word, timing events, fit-output
+ * buffers).  pint_check_step waits for that step only and returns its status, so the host
+ * enqueues the next steps while the device runs step k.  At most PINT_NSLOT steps in
+ * flight: check slot s before ending the step that reuses it.  Pinned output buffers must
+ * be per slot.  In lazy mode pint_read_step / pint_noise_resids(_dm) put their copy-stream
+ * work behind the step's last kernel (at pint_step_end or pint_check), not behind the
+ * solve. */
+#define PINT_NSLOT 3
 int pint_step_end(pint_ctx *ctx, int *slot);
+/* One GLSFitter.fit_toas(maxiter=1) step of every instance (fitter.py:2164-2289: the GLS
+ * step, full_cov=False noise realisations :2269-2282, the post-fit chi2 it returns) enqueued
+ * by a single call, lazy mode only: [pint_restore_tables when restore], pint_eval(2),
+ * pint_fit_step_apply(mode = 1, lambda_), pint_read_step(dpars, errs, cov, chi2lin),
+ * pint_noise_resids(noise_red, noise_ecorr), pint_noise_resids_dm(noise_dm), pint_eval(0),
+ * pint_chi2_gls(chi2), pint_step_end(slot).  NULL outputs are skipped; pinned buffers
+ * (pint_host_alloc), complete after pint_check_step(*slot). */
+int pint_fit_step_enqueue(pint_ctx *ctx, int restore, int mode, double lambda_, double *dpars, double *errs,
+                          double *cov, double *chi2lin, double *noise_red, double *noise_ecorr, double *noise_dm,
+                          double *chi2, int *slot);
 int pint_check_step(pint_ctx *ctx, int slot);
 /* Engine options (no reference counterpart): PINT_OPT_BLOCKED_SOLVE = 1 (default) solves
  * the normal equations with the blocked FP64-MFMA kernel, 0 with the column-by-column
@@ -306,6 +331,11 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * stream) instead of inside the solve: 0 never, 1 for batches of >= 16 instances, 2 always.
  * Same values bit for bit; takes effect at the next pint_fit_step. */
 #define PINT_OPT_COV_DEFER 7
+/* PINT_OPT_SCHUR = 1 (default): for deferred solves (PINT_OPT_COV_DEFER) the DMX-eliminated
+ * solve's build phase -- column norms, S = A_dd, U = A_dx D^-1/2, S -= U U^T, b'_d -- runs as
+ * k_schur, one workgroup per (block of S, instance), before the one-workgroup-per-instance
+ * solve; 0 keeps it inside the solve.  Same operations in the same order: same bits. */
+#define PINT_OPT_SCHUR 9
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

@@ -15,6 +15,7 @@ LIBPATH = os.environ.get("PINT_LIB") or os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
 EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
+NSLOT = 3       # PINT_NSLOT: pipeline slots (pint_step_end / pint_check_step)
 B_NPAR = 27
 BIN_NONE, BIN_ELL1, BIN_DD, BIN_ELL1H, BIN_BT, BIN_DDK = range(6)
 
@@ -103,6 +104,8 @@ def lib():
     L.pint_device_count.restype = C.c_int
     L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
     L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
+    L.pint_set_grid.argtypes = [vp, C.c_int, C.c_int, dptr, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                C.POINTER(C.c_int64), dptr, C.c_int64]
     for fn in ("pint_get_tables", "pint_set_tables", "pint_read_designmatrix", "pint_chi2_gls", "pint_chi2_wls",
                "pint_last_timing"):
         getattr(L, fn).argtypes = [vp, dptr]
@@ -134,6 +137,7 @@ def lib():
     L.pint_set_ecorr.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dptr]
     L.pint_check.argtypes = [vp]
     L.pint_step_end.argtypes = [vp, C.POINTER(C.c_int)]
+    L.pint_fit_step_enqueue.argtypes = [vp, C.c_int, C.c_int, C.c_double] + [dptr] * 8 + [C.POINTER(C.c_int)]
     L.pint_check_step.argtypes = [vp, C.c_int]
     L.pint_inst_status.argtypes = [vp, C.POINTER(C.c_int32)]
     L.pint_noise_resids.argtypes = [vp, dptr, dptr]
@@ -162,7 +166,8 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_inst_status", "pint_noise_resids", "pint_debug_gram", "pint_debug_set_resids",
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
             "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids", "pint_chi2_wls",
-            "pint_apply_step_uniform", "pint_fit_step_apply", "pint_save_tables", "pint_restore_tables", "pint_read_norms"]
+            "pint_apply_step_uniform", "pint_fit_step_apply", "pint_save_tables", "pint_restore_tables", "pint_read_norms",
+            "pint_fit_step_enqueue", "pint_set_grid"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

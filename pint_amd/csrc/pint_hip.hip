@@ -23,6 +23,7 @@
 #include <map>
 #include <type_traits>
 #include <mutex>
+#include <functional>
 #include "physics.hpp"
 
 using namespace pint;
@@ -3032,6 +3033,191 @@ __device__ __attribute__((noinline)) void apply_setup(int inst, double* tail, in
     for (int k = lane; k < (int)(sizeof(InstConst) / 4); k += 64) cd[k] = cs[k];
 }
 
+// k_schur: k_solve_dmx's build phase for deferred solves (xw), spread over the chip -- the
+// norms (utils.py:2879), S = A_dd and U = A_dx D^-1/2 normalised, S -= U U^T and b'_d = b_d -
+// U D^-1/2 b_x -- one 256-thread workgroup per (lower block of S, instance), each staging the
+// U block rows it needs in LDS.  At 9 pulsars the same work inside the one-workgroup-per-
+// instance solve took ~16 us of its ~63 (profiles: solve phases, round 4).  The operations
+// and their order are the solve's own (wave 0 runs the block's MFMA chain in k order, b'_d
+// by the same lane quads), so the solve that loads the result gives the same bits.
+// Output per instance at xw + xwoff: the S' blocks and U blocks in the solve's LDS layout,
+// then ind (nbd*16), inx, isd, Dn (nbk*16 each) -- k_cov_dmx's export layout -- then b'_d
+// (nbd*16), b_x (nbk*16) and the normalised Gram diagonal rd (nbd*16).
+constexpr int SCHUR_T = 256;
+__global__ __launch_bounds__(SCHUR_T) void k_schur(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ Gpart, const double* __restrict__ colsq,
+                                                   int nsplit, int mode, const double* __restrict__ Sd,
+                                                   const double* __restrict__ DD, const double* __restrict__ DCS,
+                                                   double* __restrict__ xw) {
+    extern __shared__ double lds[];
+    const InstDev I = insts[blockIdx.y];
+    const PsrDev& Pd = psrs[I.psr];
+    if (!Pd.dsplit) return;
+    const int ndc = Pd.ndc, Kp = Pd.Kpd, Kres = Pd.Kd;
+    const int Kd = (mode == 0) ? Pd.red0c : Pd.Kd;
+    const int red0 = Pd.red0c;
+    const int nbd = (Kd + 15) >> 4, nbk = (ndc + 15) >> 4;
+    const int nblkS = nbd * (nbd + 1) / 2;
+    const int p = blockIdx.x;
+    if (p >= nblkS) return;
+    int Ib, Jb;
+    tri_decode(p, Ib, Jb);
+    const bool diag = Ib == Jb;
+    const double* Gp = Gpart + I.goff;
+    const double* Sdi = Sd + I.sdoff;
+    auto Gd = [&](int i, int j) {
+        if (i > j) { int t = i; i = j; j = t; }
+        return Gp[(long)i * Kp + j];
+    };
+    double* uI = lds;                               // nbk blocks: U(Ib, k)
+    double* uJ = diag ? uI : uI + nbk * 256;        // nbk blocks: U(Jb, k)
+    double* inx = uI + (diag ? 1 : 2) * nbk * 256;  // nbk*16
+    double* isd = inx + nbk * 16;                   // nbk*16
+    double* Dn = isd + nbk * 16;                    // nbk*16
+    double* bx = Dn + nbk * 16;                     // nbk*16
+    double* indI = bx + nbk * 16;                   // 16: rows of Ib
+    double* indJ = indI + 16;                       // 16: rows of Jb
+    const int tid = threadIdx.x, lane = tid & 63;
+    // ---- every global load of the workgroup issued first (one load latency, not one per
+    //      phase): the DMX norms' inputs, the two row blocks' column norms, the U elements,
+    //      the S block's Gram entries and b_d's ----
+    constexpr int URB = 8;  // U elements per thread and row block held in registers (nbk <= 8)
+    const int nrow = diag ? 1 : 2;
+    double gU[2][URB];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int u = 0; u < URB; u++) {
+            const int e = tid + u * SCHUR_T, r = e & 15, a = e >> 4;
+            const int gi = (t == 0 ? Ib : Jb) * 16 + r;
+            gU[t][u] = (t < nrow && e < nbk * 256 && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
+        }
+    double gD = 0.0, gC = 0.0, gB = 0.0, gN = 0.0, gS[4] = {0, 0, 0, 0}, gb = 0.0;
+    if (tid < nbk * 16 && tid < ndc) {
+        gD = DD[I.ddoff + tid];
+        gC = mode == 0 ? gD : DCS[I.ddoff + tid];
+        gB = Sdi[(long)tid * Kp + Kres];
+    }
+    if (tid >= 128 && tid < 160) {
+        const int c = ((tid - 128) < 16 ? Ib : Jb) * 16 + ((tid - 128) & 15);
+        if (c < Kd) gN = mode == 0 ? Gd(c, c) : colsq[(I.coff + c) * nsplit];
+    }
+    if (tid < 64) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int gi = Ib * 16 + (lane >> 4) + 4 * q, gj = Jb * 16 + (lane & 15);
+            if (gi < Kd && gj < Kd) gS[q] = Gd(gi, gj);
+        }
+    } else if (diag && tid < 128) {
+        const int c = Ib * 16 + ((tid - 64) >> 2);
+        if (c < Kd) gb = Gd(c, Kres);
+    }
+    // ---- norms (the solve's formulas) ----
+    for (int a = tid; a < nbk * 16; a += SCHUR_T) {
+        double d = 1.0, b = 0.0, na = 1.0;
+        if (a < ndc) {
+            const double dd_ = a == tid ? gD : DD[I.ddoff + a];
+            na = sqrt(a == tid ? gC : (mode == 0 ? dd_ : DCS[I.ddoff + a]));
+            na = na == 0.0 ? 1.0 : na;
+            d = dd_ / (na * na);
+            b = (a == tid ? gB : Sdi[(long)a * Kp + Kres]) / na;
+        }
+        inx[a] = 1.0 / na;
+        Dn[a] = d;
+        isd[a] = 1.0 / sqrt(d);
+        bx[a] = b;
+    }
+    if (tid >= 128 && tid < 160) {
+        const int k = tid - 128, c = (k < 16 ? Ib : Jb) * 16 + (k & 15);
+        double v = 1.0;
+        if (c < Kd) {
+            v = sqrt(gN);
+            v = v == 0.0 ? 1.0 : v;
+        }
+        (k < 16 ? indI : indJ)[k & 15] = 1.0 / v;
+    }
+    __syncthreads();
+    // ---- U block rows Ib (and Jb), scaled: U[gi][a] = A_dx[gi][a] ind[gi] inx[a] isd[a] ----
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        if (t >= nrow) break;
+        const double* ind = t == 0 ? indI : indJ;
+        double* u = t == 0 ? uI : uJ;
+        const int B = t == 0 ? Ib : Jb;
+#pragma unroll
+        for (int uu = 0; uu < URB; uu++) {
+            const int e = tid + uu * SCHUR_T, r = e & 15, a = e >> 4;
+            if (e < nbk * 256) {
+                const int gi = B * 16 + r;
+                u[((a >> 4) << 8) + swz(r, a & 15)] = (gi < Kd && a < ndc) ? gU[t][uu] * (ind[r] * inx[a]) * isd[a] : 0.0;
+            }
+        }
+        for (int e = tid + URB * SCHUR_T; e < nbk * 256; e += SCHUR_T) {  // (nbk > URB: the tail)
+            const int r = e & 15, a = e >> 4, gi = B * 16 + r;
+            const double g = (gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
+            u[((a >> 4) << 8) + swz(r, a & 15)] = (gi < Kd && a < ndc) ? g * (ind[r] * inx[a]) * isd[a] : 0.0;
+        }
+    }
+    __syncthreads();
+    double* o = xw + I.xwoff;
+    const int na = (nblkS + nbd * nbk) * 256;
+    double* o_ind = o + na;
+    double* o_inx = o_ind + nbd * 16;
+    double* o_isd = o_inx + nbk * 16;
+    double* o_Dn = o_isd + nbk * 16;
+    double* o_bd = o_Dn + nbk * 16;
+    double* o_bx = o_bd + nbd * 16;
+    double* o_rd = o_bx + nbk * 16;
+    if (tid < 64) {
+        // the S block (the solve's put_S) and S -= sum_k U(Ib,k) U(Jb,k)^T in k order
+        double4_t acc;
+        const int c = lane & 15;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = (lane >> 4) + 4 * q;
+            const int gi = Ib * 16 + r, gj = Jb * 16 + c;
+            double v;
+            if (gi < Kd && gj < Kd) {
+                const double ni = indI[r], nj = indJ[c];
+                v = gS[q] * (ni * nj);
+                if (gi == gj) o_rd[gi] = v;
+                if (gi == gj && mode == 1 && gi >= red0) v += (ni * ni) / Pd.red_phi[gi - red0];
+            } else {
+                v = (gi == gj) ? 1.0 : 0.0;
+            }
+            acc[q] = v;
+        }
+        for (int k = 0; k < nbk; k++) bmma<false, false>(acc, uI + k * 256, uJ + k * 256, lane, true);
+        double* So = o + ((long)p << 8);
+#pragma unroll
+        for (int q = 0; q < 4; q++) So[swz((lane >> 4) + 4 * q, lane & 15)] = acc[q];
+    } else if (diag && tid < 128) {
+        // b'_d of the block's rows, by the solve's lane quads: b_d - sum_a U[c][a] (b_x[a] isd[a])
+        const int l = tid - 64, cr = l >> 2, sub = l & 3;
+        const int c = Ib * 16 + cr;
+        double sacc = 0.0;
+        for (int a = sub; a < ndc; a += 4) sacc += uI[((a >> 4) << 8) + swz(cr, a & 15)] * (bx[a] * isd[a]);
+        sacc += __shfl_xor(sacc, 1, 64);
+        sacc += __shfl_xor(sacc, 2, 64);
+        const double bd = c < Kd ? gb * indI[cr] : 0.0;
+        if (sub == 0) o_bd[c] = bd - sacc;
+    } else if (diag) {
+        // the block row's U blocks and norms; workgroup 0 the DMX vectors
+        const int t0 = tid - 128;
+        for (int e = t0; e < nbk * 256; e += SCHUR_T - 128) o[ublk(Ib, e >> 8, nbk, nblkS) + (e & 255)] = uI[e];
+        if (t0 < 16) o_ind[Ib * 16 + t0] = indI[t0];
+        if (p == 0)
+            for (int a = t0; a < nbk * 16; a += SCHUR_T - 128) {
+                o_inx[a] = inx[a];
+                o_isd[a] = isd[a];
+                o_Dn[a] = Dn[a];
+                o_bx[a] = bx[a];
+            }
+    }
+}
+static inline size_t schur_lds(int nbk) { return sizeof(double) * ((size_t)2 * nbk * 256 + 4 * nbk * 16 + 32); }
+static inline long schur_xw_extra(long nbd, long nbk) { return (2 * nbd + nbk) * 16; }
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
@@ -3043,7 +3229,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        int* __restrict__ status, int fuse_sigma, int refine,
                                                        double* __restrict__ xw, const double* __restrict__ ones,
                                                        double* __restrict__ apply_tables, InstConst* __restrict__ apply_ic,
-                                                       double apply_lam) {
+                                                       double apply_lam, int pre) {
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[2 * NW];  // block_sum / block_max2
@@ -3109,6 +3295,27 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     if (tid == 0) sflag = 0;
     TS(0);
     if (apply_tables) apply_stage<NW>(Pd, I, apply_tables, tail);
+    const double rwr = Gd(Kres, Kres);
+    if (pre) {
+        // k_schur formed S' = S - U U^T, U, the norms and b'_d in xw (its layout): load them
+        const double* o = xw + I.xwoff;
+        const int na = (nblkS + nbd * nbk) * 256;
+        for (int e = tid; e < na; e += NW * 64) A[e] = o[e];
+        const double* v = o + na;
+        for (int e = tid; e < nbd * 16; e += NW * 64) {
+            ind[e] = v[e];
+            bd[e] = v[nbd * 16 + 3 * nbk * 16 + e];
+            rd[e] = v[2 * nbd * 16 + 4 * nbk * 16 + e];
+        }
+        for (int e = tid; e < nbk * 16; e += NW * 64) {
+            inx[e] = v[nbd * 16 + e];
+            isd[e] = v[nbd * 16 + nbk * 16 + e];
+            Dn[e] = v[nbd * 16 + 2 * nbk * 16 + e];
+            bx[e] = v[2 * nbd * 16 + 3 * nbk * 16 + e];
+        }
+        __syncthreads();
+        TS(1);
+    } else {
     // ---- loads first: each thread's Gram (S) and DMX-row (U) elements are issued before the
     //      norms and held in registers across them, so building S and U costs one global-load
     //      latency instead of one per phase (systems larger than RS / RU elements per thread
@@ -3134,9 +3341,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         const int gi = Ib * 16 + (e & 15), a = kb * 16 + ((e >> 4) & 15);
         gU[u] = (e < nU && gi < Kd && a < ndc) ? Sdi[(long)a * Kp + gi] : 0.0;
     }
-    // b_d's Gram entries and r^T W r with them (one column per thread), not after the barrier
+    // b_d's Gram entries (one column per thread), not after the barrier
     const double gb_pre = tid < Kd ? Gd(tid, Kres) : 0.0;
-    const double rwr = Gd(Kres, Kres);
     // ---- column norms (utils.py:2879: zero norm -> 1), b_x, D (normalised) ----
     for (int c = tid; c < nbd * 16; c += NW * 64) {
         double v = 1.0;
@@ -3236,6 +3442,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         if (sub == 0 && g0 < nbd * 16) bd[g0] = bnew;  // NW*16 >= nbd*16 groups
     }
     __syncthreads();
+    }  // (build)
     TS(2);
     if (!blk_cholinv<NW>(A, nbd, wave, lane, &sflag)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
@@ -3439,9 +3646,12 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     // ---- covariance of the timing parameters ----
     if (xw) {  // deferred to k_cov_dmx (several workgroups per instance, at the read): X, U
         double* o = xw + I.xwoff;
-        const int na = (nblkS + nbd * nbk) * 256;
+        // (after k_schur the U blocks and the scalings are in xw already: X alone)
+        const int na = pre ? nblkS * 256 : (nblkS + nbd * nbk) * 256;
         const int t0 = setup_w0 ? tid - 64 : tid, ts_ = setup_w0 ? (NW - 1) * 64 : NW * 64;
-        if (t0 >= 0) {
+        if (t0 >= 0 && pre) {
+            for (int e = t0; e < na; e += ts_) o[e] = A[e];
+        } else if (t0 >= 0) {
             for (int e = t0; e < na; e += ts_) o[e] = A[e];
             for (int e = t0; e < nbd * 16; e += ts_) o[na + e] = ind[e];
             for (int e = t0; e < nbk * 16; e += ts_) {
@@ -3464,6 +3674,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         __syncthreads();  // (the covariance blocks read A, not the staged table; kept simple)
         if (wave == 0) apply_setup(inst, tail, S.tstride, apply_ic);
     }
+    TS(7);
 }
 
 // k_cov_dmx: W = X U, the DMX errors and the covariance blocks of k_solve_dmx (deferred
@@ -4261,11 +4472,14 @@ struct pint_ctx {
     InstDev* d_inst_sorted = nullptr;   // instances grouped by k_gram T (full layout)
     InstDev* d_inst_sorted_c = nullptr; // ... compact layout
     InstDev* d_inst_sorted_v = nullptr; // ... compact layout, generated Fourier basis (k_gram_v)
+    bool sorted_alias[3] = {false, false, false};  // a launch order equal to d_inst's: d_inst itself
+    double* d_gridspec = nullptr;       // pint_set_grid: the base table and the grid axes
     std::vector<KpGroup> kp_groups, kp_groups_c, kp_groups_v;
     int vgram = 1;       // PINT_OPT_VGRAM
     int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
     int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
     int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
+    int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
     int n_vg = 0;        // instances on the k_gram_v path
@@ -4285,8 +4499,9 @@ struct pint_ctx {
     int timing_mask = 0xff; // PINT_OPT_TIMING_MASK: timing slots whose events are recorded
     int timing_every = 1;   // PINT_OPT_TIMING_EVERY: Gram events on every k-th fit step
     long gram_calls = 0;
-    hipGraph_t graph_s[2] = {nullptr, nullptr};          // a captured launch sequence per pipeline
-    hipGraphExec_t graph_exec_s[2] = {nullptr, nullptr};  // slot (pint_capture_*, pint_graph_launch)
+    static constexpr int NSLOT = PINT_NSLOT;  // pipeline slots (pint_step_end / pint_check_step)
+    hipGraph_t graph_s[NSLOT] = {};          // a captured launch sequence per pipeline
+    hipGraphExec_t graph_exec_s[NSLOT] = {};  // slot (pint_capture_*, pint_graph_launch)
     bool capturing = false;
     int* d_blk_inst = nullptr;
     int* d_blk_row0 = nullptr;
@@ -4337,17 +4552,17 @@ struct pint_ctx {
     // reduction, 7/8 solve, 10/11 Woodbury chi2, 12/13 the Gram kernels alone, 14/15 k_greduce
     // (side stream)
     static constexpr int NEV = 16, NMS = 8;
-    // pipelined steps (pint_step_end / pint_check_step): two slots, each with its own timing
+    // pipelined steps (pint_step_end / pint_check_step): NSLOT slots, each with its own timing
     // events, status word and end-of-step event; non-pipelined use stays in slot 0
     int slot = 0;
-    hipEvent_t ev_slot[2][NEV];
-    bool rec_slot[2][NEV] = {{false}};
+    hipEvent_t ev_slot[NSLOT][NEV];
+    bool rec_slot[NSLOT][NEV] = {{false}};
     hipEvent_t* ev = ev_slot[0];  // the current slot's events
     bool* rec = rec_slot[0];
-    hipEvent_t ev_done[2] = {nullptr, nullptr};
-    hipEvent_t ev_cdone[2] = {nullptr, nullptr};  // the step's output copies (copy stream)
-    bool cdone_rec[2] = {false, false};
-    int* d_status_slots = nullptr;  // 2 status words on the device
+    hipEvent_t ev_done[NSLOT] = {};
+    hipEvent_t ev_cdone[NSLOT] = {};  // the step's output copies (copy stream)
+    bool cdone_rec[NSLOT] = {};
+    int* d_status_slots = nullptr;  // NSLOT status words on the device
     int* h_status = nullptr;        // their pinned host mirrors
     float ms[NMS] = {0, 0, 0, 0, 0, 0, 0, 0};
     double* d_nz = nullptr;  // pint_noise_lnlike scratch (parameters, epoch sums, outputs)
@@ -4362,9 +4577,9 @@ struct pint_ctx {
     // fit outputs the copy stream reads, one set per pipeline slot: a step's solve writes its
     // slot's set while the copies of the previous step (the other slot) may still run, so the
     // solve need not wait for them (copy_pend[slot]: copies of that slot's set in flight)
-    double *d_dpars_s[2] = {nullptr, nullptr}, *d_errs_s[2] = {nullptr, nullptr}, *d_cov_s[2] = {nullptr, nullptr};
-    double *d_chi2lin_s[2] = {nullptr, nullptr}, *d_xw_s[2] = {nullptr, nullptr}, *d_chi2g_s[2] = {nullptr, nullptr};
-    bool copy_pend[2] = {false, false};
+    double *d_dpars_s[NSLOT] = {}, *d_errs_s[NSLOT] = {}, *d_cov_s[NSLOT] = {};
+    double *d_chi2lin_s[NSLOT] = {}, *d_xw_s[NSLOT] = {}, *d_chi2g_s[NSLOT] = {};
+    bool copy_pend[NSLOT] = {};
     bool dm_noise_pend = false;  // a copy-stream PLDMNoise realisation still reads d_dfac (lazy)
     int out_slot = -1;
     bool wfuse = false;            // the batch takes the fused Woodbury dots (k_resid2 tiles)
@@ -4374,7 +4589,45 @@ struct pint_ctx {
     double* d_ones = nullptr;      // k_onesrow: the Woodbury ones row without an Offset column (coff)
     int wstride = 0;
     hipEvent_t ev_noise = nullptr;
+    // lazy copy-stream work of the current step (pint_read_step's k_cov_dmx and copies, the
+    // noise realisations): enqueued at the step's end (pint_step_end, after ev_done) or at
+    // pint_check, behind the kernel stream's last kernel -- so no cross-stream event sits
+    // inside the step (the solve's dispatch carried ev_solved: ~5 us of idle stream after it)
+    std::vector<std::function<int()>> cq;
+    // (Tried: holding a closed step's cq back until the next step's solve starts -- an event
+    // on k_schur's dispatch -- so its kernels and blit copies run beside the one-workgroup-
+    // per-instance solve: the event cost a ~6 us gap and the copy-stream workgroups slowed the
+    // solve itself, 0.226 vs 0.193 ms per 9-pulsar step; dropped.)
 };
+
+static bool any_copy_pend(const pint_ctx* ctx) {
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++)
+        if (ctx->copy_pend[sl]) return true;
+    return false;
+}
+static void clear_copy_pend(pint_ctx* ctx) {
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) ctx->copy_pend[sl] = false;
+}
+// enqueue the deferred copy-stream work behind `after` (an event just recorded on the kernel
+// stream); ev_copied then covers it, and copy_pend marks the current slot's outputs in flight
+static int flush_cq(pint_ctx* ctx, hipEvent_t after) {
+    if (ctx->cq.empty()) return PINT_OK;
+    HIPCHK(hipStreamWaitEvent(ctx->cstream, after, 0));
+    std::vector<std::function<int()>> ops;
+    ops.swap(ctx->cq);
+    for (auto& op : ops)
+        if (int rc = op()) return rc;
+    HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
+    ctx->copy_pend[ctx->slot] = true;
+    return PINT_OK;
+}
+// ... behind everything enqueued on the kernel stream so far (a marker event): before a launch
+// rewrites what the deferred work reads (a second fit step in the same slot, the DM-noise scale)
+static int flush_cq_now(pint_ctx* ctx) {
+    if (ctx->cq.empty()) return PINT_OK;
+    HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
+    return flush_cq(ctx, ctx->ev_solved);
+}
 
 // Point the context's fit-output buffers at pipeline slot sl's set.
 static void select_out_slot(pint_ctx* ctx, int sl) {
@@ -4583,6 +4836,31 @@ struct Arena {
     }
 };
 
+extern "C" {
+static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables);
+}
+
+// pint_set_grid: tables[k] = base with each grid variable's (hi, lo) pair set (see there)
+__global__ __launch_bounds__(256) void k_grid_tables(const double* __restrict__ spec, int ts, int nvar, int npts,
+                                                     long k0, double* __restrict__ tables) {
+    const long total = (long)npts * ts;
+    const double* hdr = spec + ts;
+    const double* vals = hdr + 4 * nvar;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+        const long k = e / ts;
+        const int i = (int)(e - k * ts);
+        double v = spec[i];
+        for (int j = 0; j < nvar; j++) {
+            const int o = (int)hdr[4 * j];
+            if (i != o && i != o + 1) continue;
+            const long st = (long)hdr[4 * j + 1], sz = (long)hdr[4 * j + 2], vo = (long)hdr[4 * j + 3];
+            const long q = ((k0 + k) / st) % sz;
+            v = vals[2 * (vo + q) + (i - o)];
+        }
+        tables[e] = v;
+    }
+}
+
 static int refresh_psrs(pint_ctx* ctx) {
     ctx->psrs_dirty = false;
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
@@ -4632,18 +4910,20 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->cov_defer = getenv("PINT_COV_DEFER") ? atoi(getenv("PINT_COV_DEFER")) : 1;  // 0 off, 1 batches, 2 always
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     ctx->gv_pair = getenv("PINT_GV_PAIR") ? atoi(getenv("PINT_GV_PAIR")) : 1;
+    ctx->schur = getenv("PINT_SCHUR") ? atoi(getenv("PINT_SCHUR")) : 1;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
-    for (int sl = 0; sl < 2; sl++) {
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
         for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev_slot[sl][i]);
         hipEventCreateWithFlags(&ctx->ev_done[sl], evf);
         hipEventCreateWithFlags(&ctx->ev_cdone[sl], hipEventDisableTiming);
     }
-    hipMalloc(&ctx->d_status_slots, 2 * sizeof(int));
-    hipMemset(ctx->d_status_slots, 0, 2 * sizeof(int));
+    hipMalloc(&ctx->d_status_slots, pint_ctx::NSLOT * sizeof(int));
+    hipMemset(ctx->d_status_slots, 0, pint_ctx::NSLOT * sizeof(int));
     ctx->d_status = ctx->d_status_slots;
-    hipHostMalloc(&ctx->h_status, 2 * sizeof(int), hipHostMallocDefault);
-    if (ctx->h_status) ctx->h_status[0] = ctx->h_status[1] = 0;
+    hipHostMalloc(&ctx->h_status, pint_ctx::NSLOT * sizeof(int), hipHostMallocDefault);
+    if (ctx->h_status)
+        for (int sl = 0; sl < pint_ctx::NSLOT; sl++) ctx->h_status[sl] = 0;
     return ctx;
 }
 
@@ -4654,30 +4934,40 @@ static void free_instances(pint_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
+    InstDev** sorted[3] = {&ctx->d_inst_sorted, &ctx->d_inst_sorted_c, &ctx->d_inst_sorted_v};
+    for (int l = 0; l < 3; l++) {  // (aliases of d_inst: freed once, below)
+        if (ctx->sorted_alias[l]) *sorted[l] = nullptr;
+        ctx->sorted_alias[l] = false;
+    }
+    dfree((void*&)ctx->d_gridspec);
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
+        void** pss[] = {(void**)&ctx->d_chi2lin_s[sl], (void**)&ctx->d_dpars_s[sl], (void**)&ctx->d_errs_s[sl],
+                        (void**)&ctx->d_cov_s[sl], (void**)&ctx->d_chi2g_s[sl], (void**)&ctx->d_xw_s[sl]};
+        for (auto p : pss) dfree(*p);
+    }
     void** ps[] = {(void**)&ctx->d_inst, (void**)&ctx->d_inst_sorted, (void**)&ctx->d_blk_inst, (void**)&ctx->d_blk_row0, (void**)&ctx->d_tables,
                    (void**)&ctx->d_phhi, (void**)&ctx->d_phlo, (void**)&ctx->d_ftay, (void**)&ctx->d_delay,
                    (void**)&ctx->d_M, (void**)&ctx->d_rt, (void**)&ctx->d_rp, (void**)&ctx->d_chi2, (void**)&ctx->d_istatus, (void**)&ctx->d_rscr,
-                   (void**)&ctx->d_chi2lin_s[0], (void**)&ctx->d_chi2lin_s[1], (void**)&ctx->d_G, (void**)&ctx->d_colsq,
-                   (void**)&ctx->d_work, (void**)&ctx->d_dpars_s[0], (void**)&ctx->d_dpars_s[1], (void**)&ctx->d_errs_s[0],
-                   (void**)&ctx->d_errs_s[1], (void**)&ctx->d_cov_s[0], (void**)&ctx->d_cov_s[1], (void**)&ctx->d_sigL,
-                   (void**)&ctx->d_lam, (void**)&ctx->d_chi2g_s[0], (void**)&ctx->d_chi2g_s[1], (void**)&ctx->d_lognorm,
+                   (void**)&ctx->d_G, (void**)&ctx->d_colsq,
+                   (void**)&ctx->d_work, (void**)&ctx->d_sigL,
+                   (void**)&ctx->d_lam, (void**)&ctx->d_lognorm,
                    (void**)&ctx->d_eigw,
                    (void**)&ctx->d_degv, (void**)&ctx->d_ndeg, (void**)&ctx->d_esum, (void**)&ctx->d_eD,
                    (void**)&ctx->d_eW, (void**)&ctx->d_eC, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic, (void**)&ctx->d_ic0,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
                    (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
-                   (void**)&ctx->d_xw_s[0], (void**)&ctx->d_xw_s[1], (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
+                   (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
                    (void**)&ctx->d_wtile, (void**)&ctx->d_norms, (void**)&ctx->d_ones};
     for (auto p : ps) dfree(*p);
     ctx->d_dpars = ctx->d_errs = ctx->d_cov = ctx->d_chi2lin = ctx->d_xw = ctx->d_chi2g = nullptr;
-    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+    clear_copy_pend(ctx);
     ctx->noise_cap = 0;
     ctx->tables0_cap = 0;
     ctx->ic0_valid = false;
     ctx->restore_pending = false;
     ctx->wfuse = ctx->wtile_valid = false;
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < pint_ctx::NSLOT; k++) {
         if (ctx->graph_exec_s[k]) hipGraphExecDestroy(ctx->graph_exec_s[k]);
         if (ctx->graph_s[k]) hipGraphDestroy(ctx->graph_s[k]);
         ctx->graph_exec_s[k] = nullptr;
@@ -4692,6 +4982,7 @@ static void free_instances(pint_ctx* ctx) {
 void pint_ctx_destroy(pint_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
+    ctx->cq.clear();  // deferred reads never enqueued: their host buffers are not filled
     hipStreamSynchronize(ctx->stream);
     free_instances(ctx);
     for (auto& p : ctx->psrs) {
@@ -4703,7 +4994,7 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->d_nz) hipFree(ctx->d_nz);
     if (ctx->d_status_slots) hipFree(ctx->d_status_slots);
     if (ctx->h_status) hipHostFree(ctx->h_status);
-    for (int sl = 0; sl < 2; sl++) {
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
         for (int i = 0; i < pint_ctx::NEV; i++) hipEventDestroy(ctx->ev_slot[sl][i]);
         if (ctx->ev_done[sl]) hipEventDestroy(ctx->ev_done[sl]);
         if (ctx->ev_cdone[sl]) hipEventDestroy(ctx->ev_cdone[sl]);
@@ -4975,10 +5266,63 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
 }
 
 int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
+    if (!ctx || ninst <= 0 || !tables) return PINT_E_INVALID;
+    return set_instances_impl(ctx, ninst, inst_psr, tables);
+}
+
+// A grid of npts points of one pulsar (gridutils.grid_chisq and friends): every point's table
+// is the base table with nvar entries replaced, formed on the device (k_grid_tables) from the
+// base table and the grid axes instead of npts host-built tables: variable j of point k takes
+// the value (hi, lo) = vals_j[((k0 + k) / stride[j]) % size[j]] (vals: the variables' value
+// pairs concatenated, size[j] pairs each) -- a meshgrid's axes, or every point's own value
+// (stride 1, size npts).
+int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar, const int32_t* var_toff,
+                  const int64_t* var_stride, const int64_t* var_size, const double* vals, int64_t k0) {
+    if (!ctx || npts <= 0 || !base || nvar < 0 || nvar > 16 || (nvar && (!var_toff || !var_stride || !var_size || !vals)))
+        return PINT_E_INVALID;
+    if (psr < 0 || psr >= (int)ctx->psrs.size()) { ctx->err = "bad pulsar id"; return PINT_E_INVALID; }
+    const int ts = ctx->psrs[psr].spec.tstride;
+    long nv = 0;
+    for (int j = 0; j < nvar; j++) {
+        if (var_toff[j] < 0 || var_toff[j] + 1 >= ts || var_stride[j] < 1 || var_size[j] < 1) {
+            ctx->err = "pint_set_grid: bad grid variable (table offset, stride or size)";
+            return PINT_E_INVALID;
+        }
+        nv += var_size[j];
+    }
+    std::vector<int32_t> ip(npts, psr);
+    if (int rc = set_instances_impl(ctx, npts, ip.data(), nullptr)) return rc;
+    // the spec: base table, then per variable (toff, stride, size, value offset) as doubles
+    // (exact: all < 2^53), then the value pairs
+    std::vector<double> spec((size_t)ts + 4 * nvar + 2 * nv);
+    for (int i = 0; i < ts; i++) spec[i] = base[i];
+    long vo = 0;
+    for (int j = 0; j < nvar; j++) {
+        double* h = spec.data() + ts + 4 * j;
+        h[0] = var_toff[j];
+        h[1] = (double)var_stride[j];
+        h[2] = (double)var_size[j];
+        h[3] = (double)vo;
+        vo += var_size[j];
+    }
+    for (long i = 0; i < 2 * nv; i++) spec[ts + 4 * nvar + i] = vals[i];
+    HIPCHK(cmalloc((void**)&ctx->d_gridspec, sizeof(double) * spec.size()));
+    HIPCHK(hipMemcpyAsync(ctx->d_gridspec, spec.data(), sizeof(double) * spec.size(), hipMemcpyHostToDevice, ctx->stream));
+    const long total = (long)npts * ts;
+    const int nb = (int)std::min<long>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_grid_tables, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_gridspec, ts, nvar, npts, (long)k0,
+                       ctx->d_tables);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));  // (spec is a host temporary)
+    return PINT_OK;
+}
+
+static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     if (ctx->psrs_dirty && refresh_psrs(ctx)) return PINT_E_HIP;
     if (flush_setup(ctx)) return PINT_E_HIP;  // the uploads' red-noise set-up, one batch
+    if (int rc = flush_cq_now(ctx)) return rc;  // (their buffers are freed below, after the streams drain)
     free_instances(ctx);
     ctx->inst.resize(ninst);
     long toff = 0, roff = 0, moff = 0, goff = 0, soff = 0, coff = 0, out = 0, cvoff = 0, eoff = 0, epoff = 0;
@@ -5170,7 +5514,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
             sdoff += (long)ph.dev.ndc * ph.dev.Kpd;
             ddoff += ph.dev.ndc;
             const long nbd = (ph.dev.Kd + 15) / 16, nbk = (ph.dev.ndc + 15) / 16;
-            xwoff += (nbd * (nbd + 1) / 2 + nbd * nbk) * 256 + (nbd + 3 * nbk) * 16;
+            xwoff += (nbd * (nbd + 1) / 2 + nbd * nbk) * 256 + (nbd + 3 * nbk) * 16 + schur_xw_extra(nbd, nbk);
             if (ph.dev.ndc > max_ndc) max_ndc = ph.dev.ndc;
         }
         I.self = k;
@@ -5268,7 +5612,8 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 // instances (first ncu workgroups) with the lightest (next ncu), then the rest
                 // heaviest first (PINT_GV_PAIR=0: plain heaviest-first order)
                 const int k1 = ncu / std::max(1, nsplit);
-                if (ctx->gv_pair && k1 > 0 && (int)b.size() > 2 * k1) {
+                const bool uniform = b.empty() || ck[b.front()] == ck[b.back()];  // (nothing to pair)
+                if (ctx->gv_pair && !uniform && k1 > 0 && (int)b.size() > 2 * k1) {
                     std::vector<int> o(b.begin(), b.begin() + k1);
                     o.insert(o.end(), b.rbegin(), b.rbegin() + k1);
                     o.insert(o.end(), b.begin() + k1, b.end() - k1);
@@ -5276,13 +5621,25 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
                 }
             }
         }
+        bool ident = true;  // the launch order is the instance order (e.g. a grid's points)
+        int nxt = 0;
         for (int T = 1; T <= maxT; T++) {
             if (bucket[T].empty()) continue;
             KpGroup g{T, (int)sorted.size(), (int)bucket[T].size(), bkp[T]};
-            for (int k : bucket[T]) sorted.push_back(ctx->inst[k]);
+            for (int k : bucket[T]) {
+                ident = ident && k == nxt++;
+                sorted.push_back(ctx->inst[k]);
+            }
             groups.push_back(g);
         }
         InstDev*& dst = lay == 0 ? ctx->d_inst_sorted : (lay == 1 ? ctx->d_inst_sorted_c : ctx->d_inst_sorted_v);
+        if (ident && (int)sorted.size() == ninst) {
+            // one upload of the instance array serves this launch order too (a 65,536-point
+            // grid batch moved ~10 MB of InstDev per order from pageable memory, ~1 ms each)
+            dst = ctx->d_inst;
+            ctx->sorted_alias[lay] = true;
+            continue;
+        }
         HIPCHK(cmalloc((void**)&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
         if (!sorted.empty())
             HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * sorted.size(), hipMemcpyHostToDevice));
@@ -5297,8 +5654,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_Sdp, sizeof(double) * std::max<long>(1, vgoff)));
     HIPCHK(cmalloc((void**)&ctx->d_BFp, sizeof(double) * std::max<long>(1, vboff)));
     if (xwoff > 0 && xwoff <= (1L << 28)) {
-        HIPCHK(cmalloc((void**)&ctx->d_xw_s[0], sizeof(double) * xwoff));
-        HIPCHK(cmalloc((void**)&ctx->d_xw_s[1], sizeof(double) * xwoff));
+        for (int sl = 0; sl < pint_ctx::NSLOT; sl++) HIPCHK(cmalloc((void**)&ctx->d_xw_s[sl], sizeof(double) * xwoff));
     }
     HIPCHK(cmalloc((void**)&ctx->d_TSp, sizeof(double) * std::max<long>(1, (long)ninst * nsplit * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
@@ -5336,7 +5692,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     }
 
     HIPCHK(cmalloc((void**)&ctx->d_tables, sizeof(double) * toff));
-    HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
+    if (tables) HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
     HIPCHK(cmalloc((void**)&ctx->d_phhi, sizeof(double) * roff));
     HIPCHK(cmalloc((void**)&ctx->d_phlo, sizeof(double) * roff));
     HIPCHK(cmalloc((void**)&ctx->d_ftay, sizeof(double) * roff));
@@ -5348,18 +5704,16 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
     HIPCHK(cmalloc((void**)&ctx->d_istatus, sizeof(int) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_rscr, sizeof(double) * RSCR * (size_t)ninst));
     HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ninst, ctx->stream));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2g_s[0], sizeof(double) * ninst));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2g_s[1], sizeof(double) * ninst));
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) HIPCHK(cmalloc((void**)&ctx->d_chi2g_s[sl], sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_lognorm, sizeof(double) * ninst));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2lin_s[0], sizeof(double) * ninst));
-    HIPCHK(cmalloc((void**)&ctx->d_chi2lin_s[1], sizeof(double) * ninst));
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) HIPCHK(cmalloc((void**)&ctx->d_chi2lin_s[sl], sizeof(double) * ninst));
     HIPCHK(cmalloc((void**)&ctx->d_G, sizeof(double) * goff));
     HIPCHK(cmalloc((void**)&ctx->d_colsq, sizeof(double) * coff * nsplit));
     HIPCHK(cmalloc((void**)&ctx->d_work, sizeof(double) * soff));
-    HIPCHK(cmalloc((void**)&ctx->d_cov_s[0], sizeof(double) * (cvoff > 0 ? cvoff : 1)));
-    HIPCHK(cmalloc((void**)&ctx->d_cov_s[1], sizeof(double) * (cvoff > 0 ? cvoff : 1)));
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++)
+        HIPCHK(cmalloc((void**)&ctx->d_cov_s[sl], sizeof(double) * (cvoff > 0 ? cvoff : 1)));
     HIPCHK(cmalloc((void**)&ctx->d_sigL, sizeof(double) * soff));
-    for (int sl = 0; sl < 2; sl++) {
+    for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
         HIPCHK(cmalloc((void**)&ctx->d_dpars_s[sl], sizeof(double) * coff));
         HIPCHK(cmalloc((void**)&ctx->d_errs_s[sl], sizeof(double) * coff));
         // the per-instance slot past the last column (K+1 stride) is never written by a solve
@@ -5449,9 +5803,10 @@ static int flush_chi2(pint_ctx* ctx);
 
 static int check_status(pint_ctx* ctx) {
     int st = 0;
+    if (int rc = flush_cq_now(ctx)) return rc;
     if (flush_chi2(ctx)) return PINT_E_HIP;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
-    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+    clear_copy_pend(ctx);
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -5482,6 +5837,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         ctx->red_valid[want_M == 2] = 1;
         ctx->red_valid[want_M != 2] = 0;  // the other layout's red columns get overwritten
         if (ctx->dm_noise_pend) {  // the evaluation with M rewrites the DM-noise scale d_dfac
+            if (int rc = flush_cq_now(ctx)) return rc;
             HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
             ctx->dm_noise_pend = false;
         }
@@ -5670,6 +6026,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     if (flush_restore(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
+    // deferred reads of this slot's outputs enqueued since the last step_end go first (this
+    // solve rewrites them)
+    if (int rc = flush_cq_now(ctx)) return rc;
     if (ctx->wbfit) {
         // k_wb_gram carries at most WB_MAXC free DM-type columns (DM Taylor terms + DMJUMPs):
         // refuse more instead of leaving the extra columns without their DM rows
@@ -5691,9 +6050,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     record(ctx, 6);
     if (mode == 1 && ctx->max_nep > 0) {
-        if (ctx->copy_pend[0] || ctx->copy_pend[1]) {  // the copy stream's noise realisations read esum / eD
+        if (any_copy_pend(ctx)) {  // the copy stream's noise realisations read esum / eD
             HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));
-            ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+            clear_copy_pend(ctx);
         }
         hipLaunchKernelGGL(k_ecorr, dim3((ctx->max_nep + 3) / 4, ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD, ctx->d_eW, ctx->m_compact,
@@ -5913,10 +6272,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         HIPCHK(hipEventRecord(ctx->ev_sigma, ctx->sstream));
         ctx->sigma_pending = true;
     }
-    hipEvent_t solved_ev = nullptr;  // ev_solved on the solve's dispatch packet (else a marker)
     if (ctx->copy_pend[ctx->slot]) {  // this slot's outputs may still be in flight to the host
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0));  // (the latest copies: covers them)
-        ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+        clear_copy_pend(ctx);
     }
     ctx->cov_pending = false;
     if (skip) {
@@ -5925,10 +6283,10 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         // beside the next kernels, so a small batch's solve does not carry it either)
         double* xw = (ctx->d_xw && (ctx->cov_defer == 2 || (ctx->cov_defer == 1 && (ctx->ninst >= 16 || ctx->lazy))))
                          ? ctx->d_xw : nullptr;
-        // when it is the last solve kernel, ev_solved rides on its dispatch packet (a separate
-        // event record is a marker packet between kernels: ~6-10 us of idle stream, measured)
-        // (in a graph capture: a plain event record, the cross-stream edge of the capture)
-        solved_ev = (Ks == 0 && !ctx->capturing) ? ctx->ev_solved : nullptr;
+        // (no event on the solve's dispatch: lazy copy-stream readers of the step are enqueued
+        // at its end (flush_cq); in a graph capture a plain ev_solved record after the solve is
+        // the capture's cross-stream edge.  Round 4 carried ev_solved on this packet: ~5 us of
+        // idle stream after the solve in every step.)
         // pint_fit_step_apply: the apply at the end of the solve when every instance is solved
         // here on the generated-Fourier path (whose Woodbury Sigma does not read F0 from the
         // table the apply rewrites)
@@ -5951,13 +6309,34 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 ctx->apply_done = true;
             }
         }
+        // the build phase (norms, S and U, S -= U U^T, b'_d) spread over the chip by k_schur
+        // when the solve exports to xw (deferred solves); PINT_SCHUR=0 keeps it in the solve
+        int pre = 0;
+        if (xw && ctx->schur) {
+            int mnb = 0, mnk = 0;
+            for (auto& I : ctx->inst) {
+                const PsrDev& pd = ctx->psrs[I.psr].dev;
+                if (!pd.dsplit) continue;
+                const int kd = mode == 0 ? pd.red0c : pd.Kd, nbd = (kd + 15) / 16;
+                mnb = std::max(mnb, nbd * (nbd + 1) / 2);
+                mnk = std::max(mnk, (pd.ndc + 15) / 16);
+            }
+            if (mnb > 0) {
+                hipLaunchKernelGGL(k_schur, dim3(mnb, ctx->ninst), dim3(SCHUR_T), schur_lds(mnk), ctx->stream,
+                                   (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_G,
+                                   (const double*)ctx->d_colsq, ctx->nsplit, mode, (const double*)ctx->d_Sd,
+                                   (const double*)ctx->d_DD, (const double*)ctx->d_DCS, xw);
+                HIPCHK(hipGetLastError());
+                pre = 1;
+            }
+        }
         hipExtLaunchKernelGGL((k_solve_dmx<16>), dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
-                              (uint32_t)lds_dyn, ctx->stream, nullptr, solved_ev, 0u,
+                              (uint32_t)lds_dyn, ctx->stream, nullptr, nullptr, 0u,
                               (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_tables,
                               (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
                               (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
                               ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam);
+                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam, pre);
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -5994,7 +6373,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     }
     HIPCHK(hipGetLastError());
     record(ctx, 8);
-    if (!solved_ev) HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
+    if (ctx->capturing) HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
     if (ctx->lazy) return PINT_OK;
     int rc = check_status(ctx);
     update_timings(ctx);
@@ -6008,6 +6387,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
 int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* ndeg, double* degvec, int degstride) {
     if (!ctx || ctx->ninst <= 0 || (mode != 0 && mode != 1) || !threshold) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc = flush_cq_now(ctx)) return rc;  // k_eig rewrites the step outputs
     int maxK = 0;
     for (auto& I : ctx->inst) maxK = std::max(maxK, mode == 0 ? ctx->psrs[I.psr].spec.ncol : I.K);
     if (degstride < maxK) { ctx->err = "degstride < columns"; return PINT_E_INVALID; }
@@ -6046,8 +6426,41 @@ int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* nd
 }
 
 int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, double* chi2lin) {
-    // lazy: copies run on the copy stream after the solve, overlapped with the kernels that
-    // follow; the caller's buffers (pinned: pint_host_alloc) are valid after pint_check().
+    if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
+    hipSetDevice(ctx->device);
+    if (ctx->lazy && !ctx->capturing) {
+        // lazy: k_cov_dmx and the copies go on the copy stream at the step's end (flush_cq),
+        // overlapped with the next step's kernels; the caller's buffers (pinned:
+        // pint_host_alloc) are valid after pint_check() / pint_check_step().  The slot's
+        // output buffers and the launch state are taken now.
+        const bool cov_run = (cov || errs) && ctx->cov_pending;
+        static const int cov_env = getenv("PINT_COV_WG") ? atoi(getenv("PINT_COV_WG")) : 0;
+        const int cov_wg = cov_env > 0 ? cov_env : COV_WG;
+        const int ninst = ctx->ninst, mode = ctx->cov_mode;
+        const size_t lds = ctx->cov_lds;
+        const long tc = ctx->tot_c, tcv = ctx->tot_cv;
+        double *d_dp = ctx->d_dpars, *d_er = ctx->d_errs, *d_cv = ctx->d_cov, *d_cl = ctx->d_chi2lin;
+        const double* d_xw = ctx->d_xw;
+        const PsrDev* psrs = ctx->d_psrs;
+        const InstDev* insts = ctx->d_inst;
+        ctx->cq.push_back([=]() -> int {
+            hipStream_t st = ctx->cstream;
+            if (cov_run) {
+                hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ninst, cov ? cov_wg : 1), dim3(1024), lds, st, psrs, insts, d_xw,
+                                   mode, cov ? d_cv : nullptr, d_er);
+                HIPCHK(hipGetLastError());
+            }
+            if (dpars) HIPCHK(hipMemcpyAsync(dpars, d_dp, sizeof(double) * tc, hipMemcpyDeviceToHost, st));
+            if (errs) HIPCHK(hipMemcpyAsync(errs, d_er, sizeof(double) * tc, hipMemcpyDeviceToHost, st));
+            if (cov) HIPCHK(hipMemcpyAsync(cov, d_cv, sizeof(double) * tcv, hipMemcpyDeviceToHost, st));
+            if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, d_cl, sizeof(double) * ninst, hipMemcpyDeviceToHost, st));
+            return PINT_OK;
+        });
+        if (cov_run) ctx->cov_pending = cov == nullptr;  // errors only: a later read of the covariance re-runs it
+        return PINT_OK;
+    }
+    // synchronous, or inside a graph capture: on the copy stream after ev_solved (capture: the
+    // cross-stream edge of the graph), or on the kernel stream
     hipStream_t st = ctx->lazy ? ctx->cstream : ctx->stream;
     if (ctx->lazy) HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_solved, 0));
     if ((cov || errs) && ctx->cov_pending) {  // the DMX-eliminated solve's W, DMX errors, covariance
@@ -6257,6 +6670,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
         return PINT_OK;
     }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_SCHUR) { ctx->schur = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_TIMING_EVERY) {
         if (value < 1) return PINT_E_INVALID;
         ctx->timing_every = value;
@@ -6266,7 +6680,8 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == 99) { ctx->gvdbg = value; return PINT_OK; }
     if (key == PINT_OPT_TIMING_MASK) {
         ctx->timing_mask = value & 0xff;
-        for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec_slot[0][k] = ctx->rec_slot[1][k] = false;
+        for (int sl = 0; sl < pint_ctx::NSLOT; sl++)
+            for (int k = 0; k < pint_ctx::NEV; k++) ctx->rec_slot[sl][k] = false;
         for (int k = 0; k < pint_ctx::NMS; k++) ctx->ms[k] = 0.0f;
         return PINT_OK;
     }
@@ -6281,20 +6696,21 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
 // frozen at capture: replays re-run the same batch on whatever the buffers hold.
 static void join_side_streams(pint_ctx* ctx) {
     if (ctx->sigma_pending) hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0);
-    if (ctx->copy_pend[0] || ctx->copy_pend[1]) hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0);
+    if (any_copy_pend(ctx)) hipStreamWaitEvent(ctx->stream, ctx->ev_copied, 0);
     ctx->sigma_pending = false;
-    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+    clear_copy_pend(ctx);
 }
 
 int pint_capture_begin(pint_ctx* ctx) {
     if (!ctx || ctx->ninst <= 0 || ctx->capturing) return PINT_E_INVALID;
     if (!ctx->lazy) { ctx->err = "graph capture needs lazy mode"; return PINT_E_INVALID; }
     hipSetDevice(ctx->device);
+    if (int rc = flush_cq_now(ctx)) return rc;
     HIPCHK(hipStreamSynchronize(ctx->cstream));
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->sigma_pending = false;
-    ctx->copy_pend[0] = ctx->copy_pend[1] = false;
+    clear_copy_pend(ctx);
     HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
     ctx->capturing = true;
     return PINT_OK;
@@ -6363,10 +6779,11 @@ int pint_check(pint_ctx* ctx) {
 }
 
 // Pipelined steps: pint_step_end closes the work enqueued since the previous step_end (the
-// side streams joined, the status word copied to its pinned mirror, an end event) and moves
-// the launches that follow to the other slot; pint_check_step(s) waits for step s only, so
-// the host enqueues step k+1 while the device still runs step k.  Two steps in flight at
-// most: the caller checks step s before ending the step after the next one.
+// side streams joined, the step's deferred copy-stream work enqueued behind its last kernel,
+// the status word copied to its pinned mirror, an end event) and moves the launches that
+// follow to the next slot; pint_check_step(s) waits for step s only, so the host enqueues
+// steps k+1 .. k+NSLOT-1 while the device still runs step k.  NSLOT steps in flight at most:
+// the caller checks step s before ending the step that reuses its slot.
 int pint_step_end(pint_ctx* ctx, int* slot) {
     if (!ctx || ctx->capturing || !slot) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
@@ -6379,7 +6796,11 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     // the step's kernels end at ev_done; its status word goes to the host on the copy stream
     // after them (off the kernel stream), and ev_cdone covers it and the step's output copies
     HIPCHK(hipEventRecord(ctx->ev_done[s], ctx->stream));
-    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_done[s], 0));
+    if (!ctx->cq.empty()) {  // the step's deferred copy-stream work, behind its last kernel
+        if (int rc = flush_cq(ctx, ctx->ev_done[s])) return rc;
+    } else {
+        HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_done[s], 0));
+    }
     if (ctx->chi2_dst) {  // the step's deferred chi2 copy (pint_chi2_gls, lazy)
         HIPCHK(hipMemcpyAsync(ctx->chi2_dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost,
                               ctx->cstream));
@@ -6388,7 +6809,7 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->cstream));
     HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
     ctx->cdone_rec[s] = true;
-    ctx->slot = s ^ 1;
+    ctx->slot = (s + 1) % pint_ctx::NSLOT;
     ctx->d_status = ctx->d_status_slots + ctx->slot;
     ctx->ev = ctx->ev_slot[ctx->slot];
     ctx->rec = ctx->rec_slot[ctx->slot];
@@ -6399,8 +6820,32 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     return PINT_OK;
 }
 
+// One GLSFitter.fit_toas(maxiter=1) step of every instance (fitter.py:2164-2289), enqueued by
+// one call: [the snapshot restored], the evaluation with the fit layout, the GLS step with the
+// full step applied (fused into the solve where possible), the step outputs and the noise
+// realisations on the copy stream, the post-fit evaluation and Woodbury chi2, then the step
+// closed (pint_step_end).  The same launches as the separate calls, without a host round trip
+// per call; lazy mode only (the outputs are complete after pint_check_step(*slot)).
+int pint_fit_step_enqueue(pint_ctx* ctx, int restore, int mode, double lambda_, double* dpars, double* errs,
+                          double* cov, double* chi2lin, double* noise_red, double* noise_ecorr, double* noise_dm,
+                          double* chi2, int* slot) {
+    if (!ctx || ctx->ninst <= 0 || !slot) return PINT_E_INVALID;
+    if (!ctx->lazy || ctx->capturing) { ctx->err = "pint_fit_step_enqueue needs lazy mode (no capture)"; return PINT_E_INVALID; }
+    if (mode != 1) { ctx->err = "pint_fit_step_enqueue: GLS steps (mode 1) only"; return PINT_E_INVALID; }
+    int rc = PINT_OK;
+    if (restore && (rc = pint_restore_tables(ctx))) return rc;
+    if ((rc = pint_eval(ctx, 2))) return rc;
+    if ((rc = pint_fit_step_apply(ctx, mode, lambda_))) return rc;
+    if ((dpars || errs || cov || chi2lin) && (rc = pint_read_step(ctx, dpars, errs, cov, chi2lin))) return rc;
+    if ((noise_red || noise_ecorr) && (rc = pint_noise_resids(ctx, noise_red, noise_ecorr))) return rc;
+    if (noise_dm && (rc = pint_noise_resids_dm(ctx, noise_dm))) return rc;
+    if ((rc = pint_eval(ctx, 0))) return rc;
+    if (chi2 && (rc = pint_chi2_gls(ctx, chi2))) return rc;
+    return pint_step_end(ctx, slot);
+}
+
 int pint_check_step(pint_ctx* ctx, int s) {
-    if (!ctx || s < 0 || s > 1) return PINT_E_INVALID;
+    if (!ctx || s < 0 || s >= pint_ctx::NSLOT) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     HIPCHK(hipEventSynchronize(ctx->ev_done[s]));
     if (ctx->cdone_rec[s]) HIPCHK(hipEventSynchronize(ctx->ev_cdone[s]));
@@ -6443,7 +6888,15 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
         unsigned long long ts[32];
         HIPCHK(hipStreamSynchronize(ctx->stream));
         HIPCHK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_ts), sizeof(ts)));
-        for (int i = 0; i < 32; i++) out[i] = (double)(ts[i] - ts[0]) * 0.01;
+        // (signed: a stamp this launch did not write -- zero after a reset (which 6), or stale --
+        // comes out negative or beyond the end stamp instead of as an unsigned wrap-around)
+        for (int i = 0; i < 32; i++) out[i] = (double)(long long)(ts[i] - ts[0]) * 0.01;
+        return 32;
+    }
+    if (which == 6) {  // reset the phase timestamps (before a probed launch)
+        unsigned long long z[32] = {0};
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_ts), z, sizeof(z)));
         return 32;
     }
     size_t n = which == 0 ? ctx->tot_g : which == 1 ? ctx->tot_c * ctx->nsplit : ctx->tot_s;
@@ -6486,9 +6939,34 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
     double* de = ctx->d_noise + std::max<long>(1, ctx->tot_out);
     int maxn = 1;
     for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
-    // lazy: the kernels and the copies run on the copy stream after the solve (ev_solved, no
-    // new event on the kernel stream): they read dpars and the ECORR epoch sums, which the
+    // lazy: the kernels and the copies run on the copy stream at the step's end (flush_cq; in
+    // a graph capture after ev_solved): they read dpars and the ECORR epoch sums, which the
     // next fit step overwrites only after waiting for ev_copied
+    if (ctx->lazy && !ctx->capturing) {
+        const int ninst = ctx->ninst, maxep = ctx->max_nep, cmp = ctx->m_compact;
+        const long tot = ctx->tot_out;
+        const double* d_dp = ctx->d_dpars;
+        const PsrDev* psrs = ctx->d_psrs;
+        const InstDev* insts = ctx->d_inst;
+        double *d_es = ctx->d_esum, *d_eD = ctx->d_eD, *d_eC = ctx->d_eC, *d_df = ctx->d_dfac;
+        ctx->cq.push_back([=]() -> int {
+            hipStream_t st = ctx->cstream;
+            if (red)
+                hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ninst), dim3(256), 0, st, psrs, insts, d_dp, dr, 0,
+                                   d_df);
+            if (ecorr) {
+                HIPCHK(hipMemsetAsync(de, 0, sizeof(double) * tot, st));
+                if (maxep > 0)
+                    hipLaunchKernelGGL(k_noise_ecorr, dim3(maxep, ninst), dim3(64), 0, st, psrs, insts, d_dp, d_es, d_eD,
+                                       de, cmp, d_eC);
+            }
+            HIPCHK(hipGetLastError());
+            if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
+            if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
+            return PINT_OK;
+        });
+        return PINT_OK;
+    }
     hipStream_t st = ctx->stream;
     if (ctx->lazy) {
         st = ctx->cstream;
@@ -6528,8 +7006,25 @@ int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
     double* d = ctx->d_noise + 2 * std::max<long>(1, ctx->tot_out);
     int maxn = 1;
     for (auto& I : ctx->inst) maxn = std::max(maxn, I.n);
-    // lazy: on the copy stream after the solve, like pint_noise_resids; the next evaluation
+    // lazy: on the copy stream at the step's end, like pint_noise_resids; the next evaluation
     // with M (which rewrites the per-TOA DM-noise scale d_dfac) waits for it
+    if (ctx->lazy && !ctx->capturing) {
+        const int ninst = ctx->ninst;
+        const long tot = ctx->tot_out;
+        const double* d_dp = ctx->d_dpars;
+        const PsrDev* psrs = ctx->d_psrs;
+        const InstDev* insts = ctx->d_inst;
+        double* d_df = ctx->d_dfac;
+        ctx->cq.push_back([=]() -> int {
+            hipStream_t st = ctx->cstream;
+            hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ninst), dim3(256), 0, st, psrs, insts, d_dp, d, 1, d_df);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(dm, d, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
+            return PINT_OK;
+        });
+        ctx->dm_noise_pend = true;
+        return PINT_OK;
+    }
     hipStream_t st = ctx->stream;
     if (ctx->lazy) {
         st = ctx->cstream;

@@ -478,7 +478,8 @@ class Session:
         self._inflight = set()  # pinned staging buffers with a copy still enqueued (lazy)
         self._keep = []         # host arrays of enqueued copies (lazy)
         self._slot = 0          # pipelined steps: the slot the next launches belong to
-        self._slot_state = {0: (self._inflight, self._keep), 1: (set(), [])}
+        self._slot_state = {0: (self._inflight, self._keep)}
+        self._slot_state.update({k: (set(), []) for k in range(1, L.NSLOT)})
         self._pending = set()   # slots of ended, not yet checked steps
 
     def close(self):
@@ -553,10 +554,39 @@ class Session:
         ids = np.full(tables.shape[0], lay.psr_id, dtype=np.int32)
         self._set(ids, tables.ravel(), [lay] * tables.shape[0], uniform=True)
 
+    def set_grid(self, lay: PulsarLayout, base_table: np.ndarray, variables, npts: int, k0: int = 0):
+        """npts grid points of one pulsar as instances (pint_set_grid): every point's table is
+        base_table with each variable's entry replaced, formed on the device.  variables:
+        [(parameter name, longdouble values, stride, size)] -- point k takes
+        values[((k0 + k) // stride) % size] (a meshgrid axis; stride 1, size npts for every
+        point's own value)."""
+        base = np.ascontiguousarray(base_table, dtype=np.float64)
+        if base.shape != (lay.tstride,):
+            raise ValueError(f"base table must have {lay.tstride} entries, got {base.shape}")
+        toff = np.array([lay.offsets[p] for p, _, _, _ in variables], dtype=np.int32)
+        stride = np.array([int(st) for _, _, st, _ in variables], dtype=np.int64)
+        size = np.array([int(sz) for _, _, _, sz in variables], dtype=np.int64)
+        pairs = []
+        for (_, v, _, sz) in variables:
+            v = np.asarray(v, dtype=np.longdouble).reshape(-1)
+            if v.size != sz:
+                raise ValueError("grid variable: values and size differ")
+            h = v.astype(np.float64)
+            lo = (v - h.astype(np.longdouble)).astype(np.float64)
+            pairs.append(np.stack([h, lo], axis=1).reshape(-1))
+        vals = np.ascontiguousarray(np.concatenate(pairs) if pairs else np.zeros(2))
+        self._check(self.L.pint_set_grid(self.ctx, lay.psr_id, int(npts), L.ptr(base), len(variables),
+                                         L.ptr(toff, C.c_int32), L.ptr(stride, C.c_int64), L.ptr(size, C.c_int64),
+                                         L.ptr(vals), int(k0)))
+        self._after_set([lay] * int(npts), int(npts) * lay.tstride, uniform=True)
+
     def _set(self, ids, tabs, lays, uniform=False):
         self._check(self.L.pint_set_instances(self.ctx, len(ids), L.ptr(ids, C.c_int32), L.ptr(tabs)))
+        self._after_set(lays, len(tabs), uniform)
+
+    def _after_set(self, lays, ntab, uniform=False):
         self.inst_layout = lays
-        self.ntab = len(tabs)
+        self.ntab = ntab
         # per-instance output offsets (read_step, noise_resids), formed once per batch (one
         # layout for every instance -- grid points -- without a Python loop over them: a
         # 256 x 256 grid's loops took ~15 ms of its ~25 ms)
@@ -762,6 +792,10 @@ class Session:
         never, 1 batches of >= 16 instances, 2 always)."""
         self._check(self.L.pint_set_option(self.ctx, 7, int(mode)))
 
+    def set_schur(self, on=True):
+        """The DMX-eliminated solve's build phase in k_schur (PINT_OPT_SCHUR, default on)."""
+        self._check(self.L.pint_set_option(self.ctx, 9, 1 if on else 0))
+
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))
@@ -784,15 +818,50 @@ class Session:
     # -- pipelined steps (lazy mode) ------------------------------------------------
     def step_end(self) -> int:
         """Close the step enqueued since the previous step_end; later launches, pinned
-        buffers and status go to the other slot.  Returns the closed step's slot for
-        check_step().  At most two steps in flight."""
+        buffers and status go to the next slot.  Returns the closed step's slot for
+        check_step().  At most L.NSLOT steps in flight."""
         sl = C.c_int(-1)
         self._check(self.L.pint_step_end(self.ctx, C.byref(sl)))
-        self._slot_state[sl.value] = (self._inflight, self._keep)
-        self._pending.add(sl.value)
-        self._slot = sl.value ^ 1
-        self._inflight, self._keep = self._slot_state[self._slot]
+        self._closed(sl.value)
         return sl.value
+
+    def _closed(self, sl):
+        self._slot_state[sl] = (self._inflight, self._keep)
+        self._pending.add(sl)
+        self._slot = (sl + 1) % L.NSLOT
+        self._inflight, self._keep = self._slot_state[self._slot]
+
+    def fit_step_enqueue(self, restore=True, lam=1.0, want_cov=True, noise=True):
+        """One GLSFitter.fit_toas(maxiter=1) step of every instance enqueued by one C call
+        (pint_fit_step_enqueue: [restore_tables], eval(FIT), fit_step_apply(1, lam),
+        read_step, noise_resids, eval, chi2_gls, step_end).  Lazy mode.  Returns (slot,
+        (steps, errors, covariances, linearised chi2), noise views or None, chi2); the
+        pinned arrays are complete after check_step(slot)."""
+        if not self.lazy:
+            raise RuntimeError("fit_step_enqueue needs lazy mode (set_lazy(True))")
+        lays = self.inst_layout
+        ok = self._off_k
+        dp, er = self._pin("dp", ok[-1]), self._pin("er", ok[-1])
+        cov = self._pin("cov", self._off_cov[-1]) if want_cov else None
+        cl = self._pin("cl", len(ok) - 1)
+        n = int(self._off_n[-1])
+        red = ec = dm = None
+        if noise:
+            if any(l.spec.dmn0 > 0 for l in lays):
+                red = self._pin("noise_red", n)
+            if any("EcorrNoise" in l.model.components for l in lays):
+                ec = self._pin("noise_ec", n)
+            if any(l.spec.dmn0 < l.nred for l in lays):
+                dm = self._pin("noise_dm", n)
+        c2 = self._pin("chi2g", len(lays))
+        sl = C.c_int(-1)
+        self._check(self.L.pint_fit_step_enqueue(self.ctx, 1 if restore else 0, 1, float(lam), L.ptr(dp), L.ptr(er),
+                                                 L.ptr(cov), L.ptr(cl), L.ptr(red), L.ptr(ec), L.ptr(dm), L.ptr(c2),
+                                                 C.byref(sl)))
+        self._closed(sl.value)
+        covs = SplitView(cov, self._off_cov, self._cov_shapes) if want_cov else []
+        nz = _NoiseViews(lays, self._off_n, red, ec, dm) if noise else None
+        return sl.value, (SplitView(dp, ok), SplitView(er, ok), covs, cl), nz, c2
 
     def check_step(self, slot: int):
         """Wait for the step closed as `slot`; its outputs (pinned buffers handed out while

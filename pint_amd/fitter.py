@@ -97,14 +97,16 @@ class BatchFit:
 
     def __init__(self, items: Optional[Sequence[tuple]], mode: str = "wls", session: Optional[Session] = None,
                  layouts=None, tables=None, threshold=None, degeneracy_style=None, track_mode=None,
-                 wideband=False, want_fac=False, fac_style=None, own_session=None):
+                 wideband=False, want_fac=False, fac_style=None, own_session=None, grid=None):
         """items: [(model, toas)], or None with `layouts` + `tables` given (instances that
         are bare parameter tables of already-uploaded pulsars, e.g. grid points).
 
         threshold: the SVD cut of the reference fitter (fitter.py:1314 WLS: None ->
         1e-14 max(N, P); GLS: 0); used when the normal equations are degenerate.
         degeneracy_style: the DegeneracyWarning text of "wls" (WLSState), "gls"
-        (GLSFitter) or "glsstate" (GLSState, the downhill GLS fitter)."""
+        (GLSFitter) or "glsstate" (GLSState, the downhill GLS fitter).
+        grid: (layout, base table, variables, npts, k0) -- grid points whose tables are formed
+        on the device (Session.set_grid) instead of `tables`."""
         self.items = list(items) if items is not None else None
         self.mode = mode
         self.want_fac = bool(want_fac)  # read the step's normalisation back (Fitter.fac)
@@ -116,6 +118,10 @@ class BatchFit:
         self.degenerate = None  # per instance: dropped directions of the last SVD-path step
         self.gls = mode == "gls"
         self.s = session or Session()
+        self.grid = grid
+        if grid is not None:
+            layouts = [grid[0]] * int(grid[3])
+            tables = None
         if layouts is None:
             layouts = []
             cache = {}
@@ -127,14 +133,14 @@ class BatchFit:
                 lay = self.s.add(build_layout(model, toas, track_mode=track_mode, use_gls_basis=self.gls))
                 cache[key] = lay
                 layouts.append(lay)
-        if tables is None:
+        if tables is None and grid is None:
             tables = [pack_table(l, m) for l, (m, _) in zip(layouts, self.items)]
         self.n0 = len(layouts)
         self.idx = np.arange(self.n0)                 # device instance -> original index
         self.failed = np.zeros(self.n0, dtype=bool)  # original instances taken out of the batch
         self.tables0 = tables
-        self.grid_like = (isinstance(tables, np.ndarray) and tables.ndim == 2 and len(layouts) > 0
-                          and len(set(map(id, layouts))) == 1)  # one layout object (C-level scan)
+        self.grid_like = grid is not None or (isinstance(tables, np.ndarray) and tables.ndim == 2 and len(layouts) > 0
+                                              and len(set(map(id, layouts))) == 1)  # one layout object (C-level scan)
         self.layouts0 = list(layouts)
         self._bind(list(layouts), tables)
         # wideband (WidebandTOAFitter / WidebandDownhillFitter): the DM rows join every fit
@@ -150,7 +156,10 @@ class BatchFit:
 
     def _bind(self, layouts, tables):
         self.layouts = layouts
-        if self.grid_like:
+        if self.grid is not None and tables is None:
+            lay, base, variables, npts, k0 = self.grid
+            self.s.set_grid(lay, base, variables, npts, k0)  # the points' tables formed on the device
+        elif self.grid_like:
             self.s.set_instances_of(layouts[0], np.asarray(tables).reshape(len(layouts), -1))  # grid points
         else:
             self.s.set_instances(list(zip(layouts, tables)))

@@ -36,6 +36,26 @@ def grid_points(parvalues):
     return out, [o.flatten() for o in out]
 
 
+def meshgrid_axes(parvalues):
+    """The flattened np.meshgrid(*parvalues) (indexing 'xy') as axes: for parameter j, its
+    axis values and (stride, size) such that flat point k takes values[(k // stride) % size]
+    -- what pint_set_grid forms on the device, without the flattened meshgrid."""
+    axes = [np.asarray(v, dtype=np.longdouble).reshape(-1) for v in parvalues]
+    n = [a.size for a in axes]
+    shape = list(n)
+    if len(n) >= 2:  # 'xy': the first two axes swap
+        shape[0], shape[1] = n[1], n[0]
+    ax_of = list(range(len(n)))
+    if len(n) >= 2:
+        ax_of[0], ax_of[1] = 1, 0
+    out = []
+    for j, a in enumerate(axes):
+        ax = ax_of[j]
+        stride = int(np.prod(shape[ax + 1:], dtype=np.int64)) if ax + 1 < len(shape) else 1
+        out.append((a, stride, shape[ax]))
+    return out, int(np.prod(shape, dtype=np.int64))
+
+
 def _dist():
     try:
         import torch.distributed as dist
@@ -105,14 +125,14 @@ def _drop_grid_session():
         cur[1].close()
 
 
-def _fit_block(s, lay, tabs, mode, down, fitargs, want_tables):
-    """Fit one batch of grid points of the uploaded pulsar `lay` (tables: (npts, tstride)),
-    every point its own instance.  Returns (chi2, final tables or None); a point that cannot
-    be evaluated is NaN (gridutils.py:101-106), and so is every point of a batch in which no
-    point can be."""
+def _fit_block(s, lay, grid, mode, down, fitargs, want_tables):
+    """Fit one batch of grid points of the uploaded pulsar `lay` (grid: (base table, variables,
+    npts, k0), the points' tables formed on the device), every point its own instance.
+    Returns (chi2, final tables or None); a point that cannot be evaluated is NaN
+    (gridutils.py:101-106), and so is every point of a batch in which no point can be."""
     from .fitter import InvalidModelParameters
-    npts = tabs.shape[0]
-    bf = BatchFit(None, mode=mode, session=s, layouts=[lay] * npts, tables=tabs)
+    base, variables, npts, k0 = grid
+    bf = BatchFit(None, mode=mode, session=s, grid=(lay, base, variables, npts, k0))
     try:
         if down:
             rq = fitargs.get("required_chi2_decrease", 1e-2)
@@ -124,7 +144,7 @@ def _fit_block(s, lay, tabs, mode, down, fitargs, want_tables):
             res = bf.fit_plain(maxiter=fitargs.get("maxiter", 1), outputs=False)
             chi2 = res.chi2
     except InvalidModelParameters:
-        return np.full(npts, np.nan), (np.full(tabs.shape, np.nan) if want_tables else None)
+        return np.full(npts, np.nan), (np.full((npts, lay.tstride), np.nan) if want_tables else None)
     ft = bf.final_tables_flat().reshape(npts, lay.tstride) if want_tables else None
     return chi2, ft
 
@@ -150,15 +170,19 @@ def _as_ld(v):
 
 
 def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
-                extraparnames: Sequence[str], fitargs):
+                extraparnames: Sequence[str], fitargs, axes=None):
     """Fit every point of `flat` (one longdouble array of values per parameter in
     `parnames`, all of one length) with `parnames` frozen; returns the flat chi2 array and a
     dict of flat extra-parameter arrays, every rank holding all points.  The shared body of
     the four grid entry points (gridutils.py:166/:392/:588/:773, parallel path: a cold
-    start from the input fitter's model at every point, gridutils.py:72)."""
+    start from the input fitter's model at every point, gridutils.py:72).  axes: instead of
+    `flat`, (meshgrid_axes output, npts) -- the points formed on the device from the axes."""
     from .engine import pack_table
     mode, down = _fit_kind(ftr)
-    npts = int(flat[0].size) if len(flat) else 0
+    if axes is not None:
+        axes, npts = axes
+    else:
+        npts = int(flat[0].size) if len(flat) else 0
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     per, lo, hi = shard_range(npts, rank, world)
@@ -177,8 +201,13 @@ def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
             chunk = int(max(1, min(hi - lo, GRID_BATCH_BYTES // per_pt, GRID_MAX_POINTS or hi - lo)))
             for c0 in range(lo, hi, chunk):
                 c1 = min(hi, c0 + chunk)
-                tabs = point_tables(lay, t0, parnames, flat, c0, c1)
-                c2, ft = _fit_block(s, lay, tabs, mode, down, fitargs, bool(extraparnames))
+                if axes is not None:   # meshgrid axes: point k of the chunk is flat point c0 + k
+                    var = [(p, a, st, sz) for p, (a, st, sz) in zip(parnames, axes)]
+                    grid = (t0, var, c1 - c0, c0)
+                else:                  # every point's own values
+                    var = [(p, np.asarray(v[c0:c1], dtype=np.longdouble), 1, c1 - c0) for p, v in zip(parnames, flat)]
+                    grid = (t0, var, c1 - c0, 0)
+                c2, ft = _fit_block(s, lay, grid, mode, down, fitargs, bool(extraparnames))
                 chi2[c0 - lo:c1 - lo] = c2
                 for e in extraparnames:
                     o = lay.offsets[e]
@@ -203,9 +232,8 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     GPU batch per rank instead of a process pool.  With torch.distributed initialised, rank
     r fits the r-th contiguous block of the flattened meshgrid and the blocks are
     all-gathered, so every rank returns the whole grid."""
-    out, flat = grid_points(parvalues)
-    shape = out[0].shape
-    chi2, extra = _chisq_flat(ftr, parnames, flat, extraparnames, fitargs)
+    shape = np.meshgrid(*[np.zeros(len(np.atleast_1d(v))) for v in parvalues])[0].shape
+    chi2, extra = _chisq_flat(ftr, parnames, None, extraparnames, fitargs, axes=meshgrid_axes(parvalues))
     return chi2.reshape(shape), {e: v.reshape(shape) for e, v in extra.items()}
 
 

@@ -47,7 +47,9 @@ def _stub_grid(gu):
     def session(base, toas, gls):
         return None, build_layout(base, toas, use_gls_basis=gls)
 
-    def fit_block(s, lay, tabs, mode, down, fitargs, want):
+    def fit_block(s, lay, grid, mode, down, fitargs, want):
+        from golden_util import grid_tables
+        tabs = grid_tables(lay, grid)  # (what pint_set_grid forms on the device)
         f0 = tabs[:, lay.offsets["F0"]] + tabs[:, lay.offsets["F0"] + 1]
         f1 = tabs[:, lay.offsets["F1"]] + tabs[:, lay.offsets["F1"] + 1]
         chi2 = (f0 - 61.4854765543) ** 2 * 1e18 + (f1 + 1.18e-15) ** 2 * 1e30 + 60.0

@@ -610,9 +610,10 @@ def test_graph_replay_matches_direct():
 def test_pipelined_graph_steps_match_enqueued():
     """The bench's step (restore the initial tables, evaluate with M, GLS fit, read the fit
     outputs and the noise realisations, apply, evaluate, GLS chi2) captured once per pipeline
-    slot and replayed two deep (pint_graph_launch + step_end / check_step) gives the same
+    slot and replayed pipelined (pint_graph_launch + step_end / check_step) gives the same
     outputs, bit for bit, as the same step enqueued launch by launch -- including the
     deferred W = XU / DMX errors / covariance of k_cov_dmx on the copy stream."""
+    from pint_amd import _lib as L
     from pint_amd.engine import Session, build_layout, pack_table
     items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
     s = Session()
@@ -643,26 +644,104 @@ def test_pipelined_graph_steps_match_enqueued():
         s.check_step(s.step_end())
         want.append(snap(r))
     caps = {}
-    for _ in range(2):
+    for _ in range(L.NSLOT):
         slot = s._slot
         caps[slot] = s.capture(step)
         s.check_step(s.step_end())
-    got, prev = [], None
-    for k in range(4):
+    got, pend = [], []
+    for k in range(2 * L.NSLOT):
+        if len(pend) >= L.NSLOT - 1:
+            cur, slot = pend.pop(0)
+            s.check_step(cur)
+            got.append(snap(caps[slot]))
         slot = s._slot
         s.replay()
-        cur = s.step_end()
-        if prev is not None:
-            s.check_step(prev[0])
-            got.append(snap(caps[prev[1]]))
-        prev = (cur, slot)
-    s.check_step(prev[0])
-    got.append(snap(caps[prev[1]]))
+        pend.append((s.step_end(), slot))
+    for cur, slot in pend:
+        s.check_step(cur)
+        got.append(snap(caps[slot]))
     for g in got:
         assert len(g) == len(want[0])
         for x, y in zip(want[0], g):
             assert np.array_equal(x, y)
     s.close()
+
+
+def test_fit_step_enqueue_matches_separate_calls():
+    """pint_fit_step_enqueue (the whole GLS step -- restore, evaluation with M, fused solve +
+    apply, fit outputs and noise realisations behind the step's last kernel, post-fit
+    evaluation, Woodbury chi2, step_end -- in one C call) gives, bit for bit, the outputs of
+    the same step as separate calls checked synchronously, with L.NSLOT steps in flight."""
+    from pint_amd import _lib as L
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso", "phoff_dmn")]
+    s = Session()
+    lays = [s.add(build_layout(m, t)) for m, t in items]
+    s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+    s.save_tables()
+    s.set_lazy(True)
+
+    def snap(out, nz, c2):
+        dp, er, cov, cl = out
+        return ([x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov]
+                + [np.array(cl, copy=True), np.array(c2, copy=True)]
+                + [np.asarray(v).copy() for k in range(len(lays)) for v in nz[k].values()])
+
+    s.restore_tables()
+    s.eval(want_M=Session.FIT)
+    s.fit_step_apply(1, 1.0)
+    out = s.read_step()
+    nz = s.noise_resids()
+    s.eval(want_M=False)
+    c2 = s.chi2_gls()
+    s.check()
+    want = snap(out, nz, c2)
+    tab_want = s.read_tables_flat()
+    pend, got = [], []
+    for k in range(2 * L.NSLOT + 1):
+        if len(pend) >= L.NSLOT:
+            sl, o, z, c = pend.pop(0)
+            s.check_step(sl)
+            got.append(snap(o, z, c))
+        sl, o, z, c = s.fit_step_enqueue(restore=True)
+        pend.append((sl, o, z, c))
+    for sl, o, z, c in pend:
+        s.check_step(sl)
+        got.append(snap(o, z, c))
+    assert len(got) == 2 * L.NSLOT + 1
+    for g in got:
+        assert len(g) == len(want)
+        for x, y in zip(want, g):
+            assert np.array_equal(x, y)
+    assert np.array_equal(s.read_tables_flat(), tab_want)
+    s.close()
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_schur_kernel_matches_in_solve_build(mode):
+    """k_schur (the DMX-eliminated solve's norms, S, U, S -= U U^T and b'_d over one workgroup
+    per block of S) gives the same step, errors, covariance and linearised chi2, bit for bit,
+    as the same build inside k_solve_dmx (PINT_OPT_SCHUR off), GLS and WLS."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso", "j0740_10k")]
+
+    def run(schur):
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.set_cov_defer(2)
+        s.set_schur(schur)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(mode)
+        dp, er, cov, cl = s.read_step()
+        out = [x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov] + [np.array(cl, copy=True)]
+        s.close()
+        return out
+
+    a, b = run(True), run(False)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
 
 
 def test_fit_step_apply_matches_separate_apply():

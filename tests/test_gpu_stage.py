@@ -392,6 +392,30 @@ def test_grid_m2_sini_j0740():
     print("reference serial vs parallel:", np.max(np.abs(st["grid_chi2_serial"] / ref - 1)))
 
 
+def test_device_grid_tables_match_host_tables():
+    """pint_set_grid's point tables (formed on the device from the base table and the grid
+    axes, k_grid_tables) equal the host restatement (golden_util.grid_tables) bit for bit:
+    a meshgrid block starting inside the grid (k0 > 0) and a list of per-point values."""
+    from golden_util import grid_tables
+    from pint_amd.engine import Session, build_layout, pack_table
+    from pint_amd.gridutils import meshgrid_axes
+    model, toas, _, _ = load("ngc6440e")
+    s = Session()
+    lay = s.add(build_layout(model, toas))
+    base = pack_table(lay, model)
+    F0, F1 = np.longdouble(model.F0.value), np.longdouble(model.F1.value)
+    g0 = F0 + np.linspace(-3, 3, 17, dtype=np.longdouble) * np.longdouble(1e-11)
+    g1 = F1 + np.linspace(-3, 3, 13, dtype=np.longdouble) * np.longdouble(1e-19)
+    axes, npts = meshgrid_axes((g0, g1))
+    var = [(p, a, st, sz) for p, (a, st, sz) in zip(("F0", "F1"), axes)]
+    for grid in ((base, var, npts - 40, 40),
+                 (base, [("DM", np.linspace(10, 11, 9, dtype=np.longdouble), 1, 9)], 9, 0)):
+        s.set_grid(lay, *grid)
+        got = s.read_tables_flat().reshape(grid[2], lay.tstride)
+        np.testing.assert_array_equal(got, grid_tables(lay, grid))
+    s.close()
+
+
 def test_invalid_grid_point_fails_alone():
     """A grid over the DD eccentricity that includes ECC >= 1: those points are NaN (the
     reference's doonefit returns NaN for the failed fit, gridutils.py:89-106) and every other

@@ -114,6 +114,28 @@ def test_library_exports_header_symbols():
     assert lib.pint_device_count() >= 0 or True  # callable without a GPU (returns 0 / error)
 
 
+@pytest.mark.parametrize("dims", [(7,), (5, 3), (4, 3, 2), (2, 3, 4, 5)])
+def test_meshgrid_axes_reproduce_the_flattened_meshgrid(dims):
+    """gridutils.meshgrid_axes (what pint_set_grid expands on the device) gives every flat
+    point of np.meshgrid(*parvalues) ('xy' indexing, C-order flatten) -- the reference's
+    point order (gridutils.py:331, :366) -- including a rank's block starting at k0."""
+    from golden_util import grid_tables
+    from pint_amd.gridutils import grid_points, meshgrid_axes
+
+    class Lay:
+        offsets = {f"P{j}": 2 * j for j in range(len(dims))}
+    vals = [np.longdouble(10 * j + 1) + np.arange(n, dtype=np.longdouble) / 3 for j, n in enumerate(dims)]
+    _, flat = grid_points(vals)
+    axes, npts = meshgrid_axes(vals)
+    assert npts == flat[0].size
+    var = [(f"P{j}", a, st, sz) for j, (a, st, sz) in enumerate(axes)]
+    for k0, cnt in ((0, npts), (npts // 3, npts - npts // 3)):
+        t = grid_tables(Lay, (np.zeros(2 * len(dims)), var, cnt, k0))
+        for j, f in enumerate(flat):
+            got = t[:, 2 * j].astype(np.longdouble) + t[:, 2 * j + 1]
+            np.testing.assert_array_equal(got, f[k0:k0 + cnt])
+
+
 def test_one_hip_runtime_whatever_loads_first():
     """libpint_hip.so loaded before `import torch` must not leave two HIP/HSA runtimes in the
     process (torch's would then see no device and the RCCL gathers could not start)."""
