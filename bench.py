@@ -64,6 +64,8 @@ def main():
                     help="N=1 only: upload + first fit of the PTA in a fresh session (cold_start)")
     args = ap.parse_args()
 
+    from pint_amd import _lib
+    _lib.lib()  # the process's HIP runtime (the system ROCm's), before torch is imported
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -313,7 +315,10 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
         step and returns its slot.  Returns the summed Gram-kernel event time of the
         sampled steps and their count."""
         kt, nk, pend = 0.0, 0, deque()
-        trace = [] if os.environ.get("PINT_BENCH_TRACE") else None
+        # PINT_BENCH_TRACE=1: the host clock after every launch and every check (2 floats per
+        # step into a preallocated array), reported on stderr
+        tr = np.zeros(2 * nsteps + 2) if os.environ.get("PINT_BENCH_TRACE") else None
+        clk = time.perf_counter
 
         def check_one():
             nonlocal kt, nk
@@ -321,21 +326,24 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
             t = s.timing()[SLOT_GRAM]
             kt, nk = kt + t, nk + (t > 0)
 
-        for _ in range(nsteps):
+        for i in range(nsteps):
             if len(pend) >= L.NSLOT:
-                if trace is not None:
-                    trace.append(("w", time.perf_counter()))
                 check_one()
-            if trace is not None:
-                trace.append(("l", time.perf_counter()))
+            if tr is not None:
+                tr[2 * i] = clk()
             pend.append(launch())
+            if tr is not None:
+                tr[2 * i + 1] = clk()
         while pend:
             check_one()
-        if trace is not None and len(trace) > 2:
-            d = [(trace[i + 1][1] - trace[i][1], i, trace[i][0]) for i in range(len(trace) - 1)]
-            big = sorted(d, reverse=True)[:4]
-            log(f"[trace] {nsteps} steps: largest host intervals (ms, index, after) "
-                f"{[(round(x * 1e3, 3), i, k) for x, i, k in big]}; median {np.median([x for x, _, _ in d]) * 1e3:.3f}")
+        if tr is not None:
+            tr[-1] = clk()
+            st = np.diff(tr[0:2 * nsteps:2]) * 1e3                   # launch to launch
+            ln = (tr[1:2 * nsteps:2] - tr[0:2 * nsteps:2]) * 1e3     # the launch call itself
+            big = np.argsort(st)[::-1][:4]
+            log(f"[trace] {nsteps} steps: launch-to-launch ms largest {[(int(k), round(float(st[k]), 3)) for k in big]} "
+                f"median {np.median(st):.3f}; launch call median {np.median(ln):.3f} max {ln.max():.3f} at {int(ln.argmax())}; "
+                f"drain {1e3 * (tr[-1] - tr[2 * nsteps - 1]):.3f}")
         return kt, nk
 
     run(warmup, step)

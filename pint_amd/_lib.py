@@ -50,38 +50,48 @@ class PintError(RuntimeError):
 
 
 _lib = None
-HIP_RUNTIME = None  # the libamdhip64 this process shares with torch (None: the system one)
+HIP_RUNTIME = None  # the libamdhip64 this process uses ("system", or torch's when torch came first)
 
 
-def _share_torch_hip_runtime():
-    """One HIP runtime per process, whatever is loaded first.
+def _one_hip_runtime():
+    """One HIP runtime per process -- the system ROCm's -- whatever is loaded first.
 
     libpint_hip.so needs libamdhip64.so.7 (RUNPATH /opt/rocm/lib).  The ROCm torch wheel
-    ships its own libamdhip64 + libhsa-runtime64 (soname libamdhip64.so.7 as well, loaded
-    through libtorch_hip's NEEDED "libamdhip64.so" and RPATH $ORIGIN).  If this library
-    loads first, the later `import torch` cannot match "libamdhip64.so" against the loaded
-    soname and maps the wheel's copy beside it: two HIP/HSA runtimes in one process, and
-    torch's sees no device (torch.cuda.is_available() False; the RCCL process group of
-    pta.gather_rows / gridutils.gather_blocks then cannot start).  Loading the wheel's
-    runtime first (by path, without importing torch) makes libpint_hip.so's NEEDED resolve
-    to it by soname, and torch's own later load to the same file (same inode): one runtime
-    either way.  PINT_HIP_RUNTIME=system keeps /opt/rocm's (for processes without torch)."""
+    ships its own libamdhip64 / libhsa-runtime64 / librocprofiler-register (ROCm 7.0), which
+    its libraries reach through NEEDED "libamdhip64.so" (bare name) and RPATH $ORIGIN.  If
+    this library loads first, a later `import torch` maps the wheel's runtimes beside the
+    system's: two HIP/HSA runtimes in one process, torch sees no device and the RCCL gathers
+    (pta.gather_rows, gridutils.gather_blocks) cannot start.  If torch's runtime is the one
+    shared, its asynchronous device->host copies blocked the host ~6-7 ms twice per process
+    (inside pint_step_end's copy-stream work, measured; the system runtime: none).  So the
+    system runtimes are loaded under the bare names the wheel's libraries ask for: their
+    NEEDED entries then match the loaded objects by name and torch runs on the system
+    runtime too.  (Loaded after torch, the names resolve to torch's runtime instead: still
+    one runtime.)  PINT_HIP_RUNTIME=torch loads the wheel's runtime first instead; =none does
+    nothing."""
     global HIP_RUNTIME
-    if os.environ.get("PINT_HIP_RUNTIME", "torch") == "system":
+    mode = os.environ.get("PINT_HIP_RUNTIME", "system")
+    if mode == "none":
         return
-    import importlib.util
-    try:
-        spec = importlib.util.find_spec("torch")
-    except (ImportError, ValueError):
-        spec = None
-    if spec is None or not spec.submodule_search_locations:
+    if mode == "torch":
+        import importlib.util
+        try:
+            spec = importlib.util.find_spec("torch")
+        except (ImportError, ValueError):
+            spec = None
+        for d in (spec.submodule_search_locations if spec and spec.submodule_search_locations else []):
+            p = os.path.join(d, "lib", "libamdhip64.so")
+            if os.path.exists(p):
+                C.CDLL(p, mode=C.RTLD_GLOBAL)
+                HIP_RUNTIME = p
+                return
         return
-    for d in spec.submodule_search_locations:
-        p = os.path.join(d, "lib", "libamdhip64.so")
-        if os.path.exists(p):
-            C.CDLL(p, mode=C.RTLD_GLOBAL)
-            HIP_RUNTIME = p
-            return
+    for name in ("librocprofiler-register.so", "libhsa-runtime64.so", "libamdhip64.so"):
+        try:
+            C.CDLL(name, mode=C.RTLD_GLOBAL)
+        except OSError:
+            return  # (not on the search path: libpint_hip.so's own RUNPATH decides)
+    HIP_RUNTIME = "system"
 
 
 def lib():
@@ -91,7 +101,7 @@ def lib():
         return _lib
     if not os.path.exists(LIBPATH):
         raise RuntimeError(f"HIP extension missing: {LIBPATH} (run __graft_entry__.build())")
-    _share_torch_hip_runtime()
+    _one_hip_runtime()
     L = C.CDLL(LIBPATH)
     vp = C.c_void_p
     L.pint_ctx_create.restype = vp

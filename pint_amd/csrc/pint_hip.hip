@@ -24,6 +24,7 @@
 #include <type_traits>
 #include <mutex>
 #include <functional>
+#include <chrono>
 #include "physics.hpp"
 
 using namespace pint;
@@ -4440,6 +4441,84 @@ __global__ __launch_bounds__(64) void k_norms(const PsrDev* __restrict__ psrs, c
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
+// k_export: a step's fit outputs written straight into the caller's pinned host buffers by
+// one kernel on the copy stream (lazy steps), instead of a runtime copy per output: the
+// runtime's async D2H copies launch a blit kernel each, and twice per process one of them
+// blocked the host ~7 ms (measured inside pint_step_end: with the driver's 5 warm-up steps
+// both landed in the timed steps, 0.38 -> 0.75-1.1 ms per step over 20 steps).
+constexpr int EXP_MAXSEG = 8;
+struct ExportSeg {
+    const double* src;
+    double* dst;  // device-visible address of the pinned host buffer
+    long n;
+};
+struct ExportArgs {
+    ExportSeg seg[EXP_MAXSEG];
+    int nseg;
+    const int* st_src;  // the slot's status word (nullptr: none)
+    int* st_dst;
+};
+__global__ __launch_bounds__(256) void k_export(ExportArgs a) {
+    if (a.st_src && blockIdx.x == 0 && threadIdx.x == 0) *a.st_dst = *a.st_src;
+    const long stride = (long)gridDim.x * 256;
+    for (int k = 0; k < a.nseg; k++) {
+        const double* __restrict__ s = a.seg[k].src;
+        double* __restrict__ d = a.seg[k].dst;
+        for (long i = blockIdx.x * 256L + threadIdx.x; i < a.seg[k].n; i += stride) d[i] = s[i];
+    }
+}
+
+// Pulsar uploads (pint_add_pulsar) staged in page-locked chunks and committed a chunk at a
+// time -- one device allocation and one asynchronous DMA per 16 MB chunk, the other chunk
+// filled meanwhile -- with the last chunk committed at the first call that needs the device
+// arrays (commit_uploads).  A PTA's 68 pulsars took 68 allocations and synchronous pageable
+// copies of ~1.4 MB each (17 ms of its cold start; one pageable 95 MB copy: 16 ms).  The two
+// staging chunks are a process-wide pool (StagePool), like the device allocation cache.
+constexpr size_t STAGE_CHUNK = (size_t)16 << 20;
+struct StagePool {
+    std::mutex mu;
+    char* buf[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    bool busy = false;  // held by a context's pending uploads
+};
+static StagePool g_stage;
+struct PendArena {
+    struct Fix {
+        size_t psr, field, off;  // pulsar, byte offset of the pointer field in its PsrDev, chunk offset
+    };
+    int cur = 0;               // the chunk being filled (g_stage.buf[cur])
+    char* host = nullptr;      // == g_stage.buf[cur] while held
+    size_t size = 0, cap = 0;
+    std::vector<Fix> fix;
+    hipEvent_t done[2] = {nullptr, nullptr};  // a chunk's DMA finished (reuse)
+    bool inflight[2] = {false, false};
+    long flushes = 0;
+    bool held = false;
+    size_t cur_idx = (size_t)-1;  // the pulsar being added (pint_add_pulsar) and its host record
+    PsrDev* cur_dev = nullptr;
+    std::vector<void*> bufs;      // the chunks' device allocations (freed with the context)
+    ~PendArena() { release(); }
+    void release() {
+        for (int k = 0; k < 2; k++) {
+            if (done[k]) {
+                if (inflight[k]) hipEventSynchronize(done[k]);
+                hipEventDestroy(done[k]);
+                done[k] = nullptr;
+            }
+            inflight[k] = false;
+        }
+        if (held) {
+            std::lock_guard<std::mutex> lk(g_stage.mu);
+            g_stage.busy = false;
+            held = false;
+        }
+        host = nullptr;
+        cap = 0;
+        size = 0;
+        fix.clear();
+    }
+};
+
 struct PsrHost {
     PsrDev dev;
     pint_spec_t spec;
@@ -4555,7 +4634,7 @@ struct pint_ctx {
     // pipelined steps (pint_step_end / pint_check_step): NSLOT slots, each with its own timing
     // events, status word and end-of-step event; non-pipelined use stays in slot 0
     int slot = 0;
-    hipEvent_t ev_slot[NSLOT][NEV];
+    hipEvent_t ev_slot[NSLOT][NEV] = {};  // (created at their first record: most runs time nothing)
     bool rec_slot[NSLOT][NEV] = {{false}};
     hipEvent_t* ev = ev_slot[0];  // the current slot's events
     bool* rec = rec_slot[0];
@@ -4593,7 +4672,11 @@ struct pint_ctx {
     // noise realisations): enqueued at the step's end (pint_step_end, after ev_done) or at
     // pint_check, behind the kernel stream's last kernel -- so no cross-stream event sits
     // inside the step (the solve's dispatch carried ev_solved: ~5 us of idle stream after it)
+    PendArena pend;              // pulsar uploads not committed to the device yet
     std::vector<std::function<int()>> cq;
+    std::vector<ExportSeg> exp;  // the deferred work's host-bound outputs (k_export at the flush)
+    const int* exp_st_src = nullptr;
+    int* exp_st_dst = nullptr;
     // (Tried: holding a closed step's cq back until the next step's solve starts -- an event
     // on k_schur's dispatch -- so its kernels and blit copies run beside the one-workgroup-
     // per-instance solve: the event cost a ~6 us gap and the copy-stream workgroups slowed the
@@ -4608,16 +4691,82 @@ static bool any_copy_pend(const pint_ctx* ctx) {
 static void clear_copy_pend(pint_ctx* ctx) {
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) ctx->copy_pend[sl] = false;
 }
+// a host-bound output of the deferred work: a k_export segment when it is small and the
+// destination pinned (device-visible), else a runtime copy on the copy stream now (the
+// runtime's blit copy streams large outputs over PCIe faster than a kernel's stores: k_export
+// for everything, 7.4 MB of covariances and 5.4 MB of noise realisations per 68-pulsar step,
+// took the step from 0.38 to 0.50-0.77 ms)
+constexpr long EXP_MAX_BYTES = 1L << 20;
+static int export_seg(pint_ctx* ctx, double* dst, const double* src, long n) {
+    if (!dst || n <= 0) return PINT_OK;
+    void* dd = nullptr;
+    static const long max_bytes = getenv("PINT_EXPORT_MAX") ? atol(getenv("PINT_EXPORT_MAX")) : EXP_MAX_BYTES;
+    if (n * (long)sizeof(double) <= max_bytes && (int)ctx->exp.size() < EXP_MAXSEG &&
+        hipHostGetDevicePointer(&dd, dst, 0) == hipSuccess && dd) {
+        ctx->exp.push_back(ExportSeg{src, static_cast<double*>(dd), n});
+        return PINT_OK;
+    }
+    (void)hipGetLastError();
+    HIPCHK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->cstream));
+    return PINT_OK;
+}
+static int launch_export(pint_ctx* ctx) {
+    if (ctx->exp.empty() && !ctx->exp_st_src) return PINT_OK;
+    ExportArgs a{};
+    a.nseg = (int)ctx->exp.size();
+    long tot = 0;
+    for (int k = 0; k < a.nseg; k++) {
+        a.seg[k] = ctx->exp[k];
+        tot += a.seg[k].n;
+    }
+    a.st_src = ctx->exp_st_src;
+    a.st_dst = ctx->exp_st_dst;
+    // a few workgroups: the writes are posted over PCIe (~50 GB/s), and workgroups on every
+    // CU waiting on them slowed the step's kernels beside them (256: 0.60 ms per step)
+    static const int wg = getenv("PINT_EXPORT_WG") ? std::max(1, atoi(getenv("PINT_EXPORT_WG"))) : 4;
+    const int nb = (int)std::max<long>(1, std::min<long>(wg, (tot + 4095) / 4096));
+    hipLaunchKernelGGL(k_export, dim3(nb), dim3(256), 0, ctx->cstream, a);
+    HIPCHK(hipGetLastError());
+    ctx->exp.clear();
+    ctx->exp_st_src = nullptr;
+    ctx->exp_st_dst = nullptr;
+    return PINT_OK;
+}
+
+// PINT_TRACE_ENQ=1: host-side stalls (> 1 ms) of single runtime calls on the step path
+struct HostLap {
+    const char* where;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    static bool on() {
+        static const bool v = getenv("PINT_TRACE_ENQ") && atoi(getenv("PINT_TRACE_ENQ"));
+        return v;
+    }
+    void operator()(const char* what) {
+        if (!on()) return;
+        const auto n = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(n - t).count();
+        if (ms > 1.0) fprintf(stderr, "[pint %s] %s took %.3f ms\n", where, what, ms);
+        t = n;
+    }
+};
+
 // enqueue the deferred copy-stream work behind `after` (an event just recorded on the kernel
 // stream); ev_copied then covers it, and copy_pend marks the current slot's outputs in flight
 static int flush_cq(pint_ctx* ctx, hipEvent_t after) {
-    if (ctx->cq.empty()) return PINT_OK;
+    if (ctx->cq.empty() && ctx->exp.empty() && !ctx->exp_st_src) return PINT_OK;
+    HostLap lap{"flush_cq"};
     HIPCHK(hipStreamWaitEvent(ctx->cstream, after, 0));
+    lap("wait event");
     std::vector<std::function<int()>> ops;
     ops.swap(ctx->cq);
-    for (auto& op : ops)
+    for (auto& op : ops) {
         if (int rc = op()) return rc;
+        lap("an op");
+    }
+    if (int rc = launch_export(ctx)) return rc;
+    lap("export");
     HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
+    lap("record ev_copied");
     ctx->copy_pend[ctx->slot] = true;
     return PINT_OK;
 }
@@ -4782,7 +4931,9 @@ static TrigJob trig_job(const PsrHost& ph, bool base) {
 
 // the red-noise set-up of every pulsar added since the last flush, batched: e^{i theta},
 // e^{i 8 theta} per TOA and the trig sums U_m, V_m, C_m, S_m (k_trig_setup + k_trig_sum)
+static int commit_uploads(pint_ctx* ctx);
 static int flush_setup(pint_ctx* ctx) {
+    if (commit_uploads(ctx)) return 1;
     if (ctx->setup_pending.empty()) return 0;
     std::vector<TrigJob> jobs;
     for (int p : ctx->setup_pending) jobs.push_back(trig_job(ctx->psrs[p], true));
@@ -4811,30 +4962,86 @@ static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const 
     return 0;
 }
 
-// A pulsar's upload staged on the host: every array at a 256-byte aligned offset of one
-// buffer, then one device allocation and one copy (instead of an allocation and a
-// synchronous copy per array); the recorded pointer fields are set at commit.
-struct Arena {
-    std::vector<char> host;
-    std::vector<std::pair<size_t, const void**>> fix;
-    template <typename T>
-    int add(const T* src, size_t count, const T*& dst) {
-        const size_t off = (host.size() + 255) & ~(size_t)255;
-        const size_t bytes = std::max(count * sizeof(T), sizeof(T));
-        host.resize(off + bytes, 0);
-        if (src && count) memcpy(host.data() + off, src, count * sizeof(T));
-        fix.push_back({off, reinterpret_cast<const void**>(&dst)});
-        return 0;
+// the current chunk to the device: its allocation, an asynchronous DMA, its pointers set
+static int flush_chunk(pint_ctx* ctx) {
+    PendArena& pa = ctx->pend;
+    if (pa.fix.empty()) return PINT_OK;
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, std::max<size_t>(pa.size, 256)));
+    HIPCHK(hipMemcpyAsync(p, pa.host, pa.size, hipMemcpyHostToDevice, ctx->stream));
+    if (!pa.done[pa.cur]) HIPCHK(hipEventCreateWithFlags(&pa.done[pa.cur], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(pa.done[pa.cur], ctx->stream));
+    pa.inflight[pa.cur] = true;
+    for (auto& f : pa.fix) {
+        PsrDev* tgt = f.psr < ctx->psrs.size() ? &ctx->psrs[f.psr].dev : (f.psr == pa.cur_idx ? pa.cur_dev : nullptr);
+        if (tgt)
+            *reinterpret_cast<const void**>(reinterpret_cast<char*>(tgt) + f.field) =
+                static_cast<const void*>(static_cast<char*>(p) + f.off);
     }
-    int commit(pint_ctx* ctx, PsrHost& ph) {
-        void* p = nullptr;
-        HIPCHK(hipMalloc(&p, std::max<size_t>(host.size(), 256)));
-        HIPCHK(hipMemcpy(p, host.data(), host.size(), hipMemcpyHostToDevice));
-        ph.bufs.push_back(p);
-        for (auto& f : fix) *f.second = static_cast<const void*>(static_cast<char*>(p) + f.first);
-        return 0;
+    pa.bufs.push_back(p);
+    pa.fix.clear();
+    pa.size = 0;
+    pa.flushes++;
+    // the other chunk next (once its own DMA has finished)
+    pa.cur ^= 1;
+    if (pa.inflight[pa.cur]) {
+        HIPCHK(hipEventSynchronize(pa.done[pa.cur]));
+        pa.inflight[pa.cur] = false;
     }
-};
+    pa.host = g_stage.buf[pa.cur];
+    pa.cap = g_stage.cap[pa.cur];
+    return PINT_OK;
+}
+// commit every staged pulsar upload; the device arrays are complete when the stream reaches
+// here (kernels on ctx->stream follow the DMAs), and the staging chunks go back to the pool
+static int commit_uploads(pint_ctx* ctx) {
+    PendArena& pa = ctx->pend;
+    if (!pa.held) return PINT_OK;
+    if (int rc = flush_chunk(ctx)) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    pa.release();
+    return PINT_OK;
+}
+// hold the process's staging chunks (page-locked, STAGE_CHUNK each) for this context
+static bool stage_hold(pint_ctx* ctx) {
+    PendArena& pa = ctx->pend;
+    if (pa.held) return true;
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    if (g_stage.busy) return false;  // (another context is staging: it uses the pageable path)
+    for (int k = 0; k < 2; k++)
+        if (!g_stage.buf[k]) {
+            if (hipHostMalloc((void**)&g_stage.buf[k], STAGE_CHUNK, hipHostMallocDefault) != hipSuccess) {
+                g_stage.buf[k] = nullptr;
+                return false;
+            }
+            g_stage.cap[k] = STAGE_CHUNK;
+        }
+    g_stage.busy = true;
+    pa.held = true;
+    pa.cur = 0;
+    pa.host = g_stage.buf[0];
+    pa.cap = g_stage.cap[0];
+    pa.size = 0;
+    return true;
+}
+// stage count elements (zeros when src is null) for the PsrDev pointer field dst of pulsar psr;
+// false: not staged (no pool chunk, or larger than a chunk) -- the caller uploads it itself
+template <typename T>
+static bool stage(pint_ctx* ctx, size_t psr, PsrDev& d, const T* src, size_t count, const T*& dst) {
+    PendArena& pa = ctx->pend;
+    const size_t bytes = std::max(count * sizeof(T), sizeof(T));
+    if (bytes > STAGE_CHUNK || !stage_hold(ctx)) return false;
+    size_t off = (pa.size + 255) & ~(size_t)255;
+    if (off + bytes > pa.cap) {
+        if (flush_chunk(ctx)) return false;
+        off = 0;
+    }
+    if (src && count) memcpy(pa.host + off, src, count * sizeof(T));
+    else memset(pa.host + off, 0, bytes);
+    pa.size = off + bytes;
+    pa.fix.push_back(PendArena::Fix{psr, (size_t)(reinterpret_cast<const char*>(&dst) - reinterpret_cast<const char*>(&d)), off});
+    return true;
+}
 
 extern "C" {
 static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables);
@@ -4862,6 +5069,7 @@ __global__ __launch_bounds__(256) void k_grid_tables(const double* __restrict__ 
 }
 
 static int refresh_psrs(pint_ctx* ctx) {
+    if (int rc = commit_uploads(ctx)) return rc;
     ctx->psrs_dirty = false;
     if (ctx->d_psrs) hipFree(ctx->d_psrs);
     ctx->d_psrs = nullptr;
@@ -4914,7 +5122,6 @@ pint_ctx* pint_ctx_create(int device) {
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
-        for (int i = 0; i < pint_ctx::NEV; i++) hipEventCreate(&ctx->ev_slot[sl][i]);
         hipEventCreateWithFlags(&ctx->ev_done[sl], evf);
         hipEventCreateWithFlags(&ctx->ev_cdone[sl], hipEventDisableTiming);
     }
@@ -4985,6 +5192,8 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     ctx->cq.clear();  // deferred reads never enqueued: their host buffers are not filled
     hipStreamSynchronize(ctx->stream);
     free_instances(ctx);
+    ctx->pend.release();
+    for (auto b : ctx->pend.bufs) hipFree(b);
     for (auto& p : ctx->psrs) {
         for (auto b : p.bufs) hipFree(b);
     }
@@ -4995,7 +5204,8 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->d_status_slots) hipFree(ctx->d_status_slots);
     if (ctx->h_status) hipHostFree(ctx->h_status);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
-        for (int i = 0; i < pint_ctx::NEV; i++) hipEventDestroy(ctx->ev_slot[sl][i]);
+        for (int i = 0; i < pint_ctx::NEV; i++)
+            if (ctx->ev_slot[sl][i]) hipEventDestroy(ctx->ev_slot[sl][i]);
         if (ctx->ev_done[sl]) hipEventDestroy(ctx->ev_done[sl]);
         if (ctx->ev_cdone[sl]) hipEventDestroy(ctx->ev_cdone[sl]);
     }
@@ -5032,43 +5242,67 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         return -PINT_E_INVALID;
     }
     PsrHost ph;
-    Arena ar;  // every array of the pulsar staged on the host, one allocation and one copy
+    // every array of the pulsar staged on the host (ctx->pend), committed with the other
+    // pulsars of the batch by commit_uploads
+    const size_t pidx = ctx->psrs.size();
+    PendArena& pa = ctx->pend;
+    const size_t mark_size = pa.size, mark_fix = pa.fix.size();
+    const long mark_flush = pa.flushes;
+    // staged (pool chunk) or, failing that, uploaded now into its own allocation
+    auto stg = [&](auto src, size_t count, auto& dst) {
+        if (stage(ctx, pidx, ph.dev, src, count, dst)) return 0;
+        return upload(ctx, ph, src, count, dst);
+    };
+    auto unstage = [&]() {  // (a rejected pulsar leaves nothing staged; what a flush already
+                            // committed of it stays allocated, unreferenced, until the context ends)
+        if (pa.flushes == mark_flush) {
+            pa.size = mark_size;
+            pa.fix.resize(mark_fix);
+        } else {
+            pa.size = 0;
+            pa.fix.clear();
+        }
+        pa.cur_idx = (size_t)-1;
+        pa.cur_dev = nullptr;
+    };
+    pa.cur_idx = pidx;
+    pa.cur_dev = &ph.dev;
     ph.spec = *spec;
     ph.n = n;
     ph.K = K;
     PsrDev& d = ph.dev;
     memset(&d, 0, sizeof(d));
     int rc = 0;
-    rc |= ar.add(t->tdb_hi, n + 1, d.tdb_hi);
-    rc |= ar.add(t->tdb_lo, n + 1, d.tdb_lo);
-    rc |= ar.add(t->freq_mhz, n + 1, d.freq);
-    rc |= ar.add(t->sigma_s, n, d.sigma);
+    rc |= stg(t->tdb_hi, n + 1, d.tdb_hi);
+    rc |= stg(t->tdb_lo, n + 1, d.tdb_lo);
+    rc |= stg(t->freq_mhz, n + 1, d.freq);
+    rc |= stg(t->sigma_s, n, d.sigma);
     {
         std::vector<double> is(n);
         double ls = 0.0, sw = 0.0;
         for (int i = 0; i < n; i++) {
-            if (!(t->sigma_s[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; return -PINT_E_INVALID; }
+            if (!(t->sigma_s[i] > 0.0)) { ctx->err = "TOA uncertainty must be > 0"; unstage(); return -PINT_E_INVALID; }
             is[i] = 1.0 / t->sigma_s[i];
             ls += std::log(t->sigma_s[i]);
             sw += is[i] * is[i];
         }
         d.logsig = ls;
         d.sumw = sw;
-        rc |= ar.add(is.data(), n, d.isig);
+        rc |= stg(is.data(), n, d.isig);
     }
-    rc |= ar.add(t->pos_km, 3 * (n + 1), d.pos);
-    rc |= ar.add(t->vel_kms, 3 * (n + 1), d.vel);
-    rc |= ar.add(t->sun_km, 3 * (n + 1), d.sun);
+    rc |= stg(t->pos_km, 3 * (n + 1), d.pos);
+    rc |= stg(t->vel_kms, 3 * (n + 1), d.vel);
+    rc |= stg(t->sun_km, 3 * (n + 1), d.sun);
     if (spec->shapiro == 2) {
-        if (!t->planet_km) { ctx->err = "PLANET_SHAPIRO needs the planet positions (planet_km)"; return -PINT_E_INVALID; }
-        rc |= ar.add(t->planet_km, (size_t)15 * (n + 1), d.planet);
+        if (!t->planet_km) { ctx->err = "PLANET_SHAPIRO needs the planet positions (planet_km)"; unstage(); return -PINT_E_INVALID; }
+        rc |= stg(t->planet_km, (size_t)15 * (n + 1), d.planet);
     }
-    rc |= ar.add(t->pulse_number, n, d.pn);
-    rc |= ar.add(t->delta_pn, n + 1, d.dpn);
-    rc |= ar.add(t->flags, n + 1, d.flags);
-    rc |= ar.add(t->jump_mask, n + 1, d.jmask);
-    rc |= ar.add(t->dmx_a, n + 1, d.dmx_a);
-    rc |= ar.add(t->dmx_b, n + 1, d.dmx_b);
+    rc |= stg(t->pulse_number, n, d.pn);
+    rc |= stg(t->delta_pn, n + 1, d.dpn);
+    rc |= stg(t->flags, n + 1, d.flags);
+    rc |= stg(t->jump_mask, n + 1, d.jmask);
+    rc |= stg(t->dmx_a, n + 1, d.dmx_a);
+    rc |= stg(t->dmx_b, n + 1, d.dmx_b);
     if (t->dmx_x) {
         // the CSR overflow of the DMX bin ids: n+2 non-decreasing offsets starting at n+2,
         // then bin indices in [0, ndmx) (the kernels index the table with them unchecked)
@@ -5076,14 +5310,14 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
         bool ok = x[0] == n + 2;
         for (int i = 0; ok && i <= n; i++) ok = x[i + 1] >= x[i];
         for (int k = ok ? n + 2 : 0; ok && k < x[n + 1]; k++) ok = x[k] >= 0 && x[k] < spec->ndmx;
-        if (!ok) { ctx->err = "dmx_x: malformed DMX overflow CSR (offsets or bin indices)"; return -PINT_E_INVALID; }
-        rc |= ar.add(t->dmx_x, (size_t)x[n + 1], d.dmx_x);
+        if (!ok) { ctx->err = "dmx_x: malformed DMX overflow CSR (offsets or bin indices)"; unstage(); return -PINT_E_INVALID; }
+        rc |= stg(t->dmx_x, (size_t)x[n + 1], d.dmx_x);
     }
-    rc |= ar.add(red_freq, (size_t)2 * spec->nred, d.red_freq);
-    rc |= ar.add(red_phi, (size_t)2 * spec->nred, d.red_phi);
-    rc |= ar.add((const double*)nullptr, (size_t)4 * n, d.red_cs);
-    rc |= ar.add((const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
-    rc |= ar.add((const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
+    rc |= stg(red_freq, (size_t)2 * spec->nred, d.red_freq);
+    rc |= stg(red_phi, (size_t)2 * spec->nred, d.red_phi);
+    rc |= stg((const double*)nullptr, (size_t)4 * n, d.red_cs);
+    rc |= stg((const double*)nullptr, (size_t)2 * VTRIG, d.trigU);
+    rc |= stg((const double*)nullptr, (size_t)2 * VTRIG, d.trigW);
     const bool trig_setup = spec->nred > 0;  // red_cs and the trig sums: flush_setup, batched
     if (trig_setup) {
         ph.f1 = red_freq[0];
@@ -5132,7 +5366,7 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
                 if (k > 0 && lists[a][k] != lists[a][k - 1] + 1) contig = false;
             }
         }
-        rc |= ar.add(drow.data(), drow.size(), d.drow);
+        rc |= stg(drow.data(), drow.size(), d.drow);
         ph.drow_host.assign(drow.begin(), drow.end());
         ph.dlo.assign(ndc, 0);
         ph.dhi.assign(ndc, 0);
@@ -5150,12 +5384,12 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
                 if (cmap[c] >= 0) dorig[cmap[c]] = c;
                 else xorig[-cmap[c] - 1] = c;
             }
-            rc |= ar.add(dorig.data(), dorig.size(), d.dorig);
-            rc |= ar.add(xorig.data(), xorig.size(), d.xorig);
+            rc |= stg(dorig.data(), dorig.size(), d.dorig);
+            rc |= stg(xorig.data(), xorig.size(), d.xorig);
         }
-        rc |= ar.add(cmap.data(), cmap.size(), d.cmap);
-        rc |= ar.add(dptr.data(), dptr.size(), d.dptr);
-        rc |= ar.add(didx.data(), didx.size(), d.didx);
+        rc |= stg(cmap.data(), cmap.size(), d.cmap);
+        rc |= stg(dptr.data(), dptr.size(), d.dptr);
+        rc |= stg(didx.data(), didx.size(), d.didx);
         // design-matrix column runs: same kind, consecutive indices (BIN: same kind only)
         std::vector<ColRun> runs;
         for (int c = 0; c < ncol; c++) {
@@ -5166,17 +5400,21 @@ int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec
             }
             runs.push_back(ColRun{k, c, 1, ix, k == PINT_COL_DMX ? -1 : cmap[c], {0, 0, 0}});
         }
-        rc |= ar.add(runs.data(), runs.size(), d.runs);
+        rc |= stg(runs.data(), runs.size(), d.runs);
         d.nrun = (int)runs.size();
     }
-    const pint_spec_t* sp = nullptr;
-    rc |= ar.add(spec, 1, sp);
-    if (rc || ar.commit(ctx, ph)) return -PINT_E_HIP;
-    d.spec = sp;
+    rc |= stg(spec, 1, d.spec);
+    if (rc) {
+        unstage();
+        ctx->err = "pint_add_pulsar: host staging allocation failed";
+        return -PINT_E_HIP;
+    }
     d.n = n;
     d.K = K;
     d.Kp = Kp;
     ctx->psrs.push_back(ph);
+    pa.cur_idx = (size_t)-1;
+    pa.cur_dev = nullptr;
     if (trig_setup) ctx->setup_pending.push_back((int)ctx->psrs.size() - 1);
     ctx->psrs_dirty = true;  // the device descriptor array is rebuilt once, at pint_set_instances
     return (int)ctx->psrs.size() - 1;
@@ -5206,6 +5444,7 @@ int pint_set_ecorr(pint_ctx* ctx, int psr, int nep, const int32_t* ep_ptr, const
                    const double* ep_phi) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || nep < 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc_ = commit_uploads(ctx)) return rc_;  // (staged pulsar uploads first)
     PsrHost& ph = ctx->psrs[psr];
     if (nep == 0) { ph.dev.nep = 0; return refresh_psrs(ctx) ? PINT_E_HIP : PINT_OK; }
     if (!ep_ptr || !ep_idx || !ep_phi || ep_ptr[0] != 0) { ctx->err = "bad ECORR epoch lists"; return PINT_E_INVALID; }
@@ -5423,7 +5662,12 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
                 if (slots_ok(ph, ntr)) { force_ntr = std::max(force_ntr, ntr); break; }
         }
     }
-    for (auto& ph : ctx->psrs) {
+    // the rows' DMX slot ids of every pulsar whose slot count changed, staged into one
+    // allocation and one copy after the loop (a PTA: 68 uploads of 40 KB each, ~0.1 ms apiece)
+    std::vector<std::pair<size_t, size_t>> slot_up;  // (pulsar, offset in slot_host)
+    std::vector<int32_t> slot_host;
+    for (size_t pi = 0; pi < ctx->psrs.size(); pi++) {
+        PsrHost& ph = ctx->psrs[pi];
         PsrDev& d = ph.dev;
         d.vg = 0;
         d.vb = 0;
@@ -5440,9 +5684,10 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
                 d.vns = ns;
                 d.vkp = kpv;
                 if (ph.dslot_ns != ns) {  // the rows' slots, so k_gram_v does no modulo
-                    std::vector<int32_t> sl(ph.n);
-                    for (int i = 0; i < ph.n; i++) sl[i] = ph.drow_host[i] >= 0 ? ph.drow_host[i] % ns : -1;
-                    if (upload(ctx, ph, sl.data(), sl.size(), d.dslot)) return PINT_E_HIP;
+                    const size_t o = (slot_host.size() + 63) & ~(size_t)63;
+                    slot_host.resize(o + ph.n);
+                    for (int i = 0; i < ph.n; i++) slot_host[o + i] = ph.drow_host[i] >= 0 ? ph.drow_host[i] % ns : -1;
+                    slot_up.push_back({pi, o});
                     ph.dslot_ns = ns;
                 }
                 break;
@@ -5473,6 +5718,13 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
             }
             d.vb = d.vg;
         }
+    }
+    if (!slot_up.empty()) {
+        void* p = nullptr;
+        HIPCHK(hipMalloc(&p, sizeof(int32_t) * slot_host.size()));
+        HIPCHK(hipMemcpy(p, slot_host.data(), sizeof(int32_t) * slot_host.size(), hipMemcpyHostToDevice));
+        ctx->psrs[slot_up[0].first].bufs.push_back(p);  // (freed with the first pulsar's buffers)
+        for (auto& u : slot_up) ctx->psrs[u.first].dev.dslot = static_cast<const int32_t*>(p) + u.second;
     }
     if (refresh_psrs(ctx)) return PINT_E_HIP;
     long vgoff = 0, vboff = 0, xwoff = 0;
@@ -5780,6 +6032,7 @@ static void record(pint_ctx* ctx, int i, hipStream_t st = nullptr) {
     for (int k = 0; k < pint_ctx::NMS; k++)
         if ((ctx->timing_mask >> k) & 1) on |= kTimingPairs[k][0] == i || kTimingPairs[k][1] == i;
     if (!on) return;
+    if (!ctx->ev[i] && hipEventCreate(&ctx->ev[i]) != hipSuccess) return;
     hipEventRecord(ctx->ev[i], st ? st : ctx->stream);
     ctx->rec[i] = true;
 }
@@ -5963,6 +6216,7 @@ int pint_set_wideband(pint_ctx* ctx, int psr, const double* pp_dm, const double*
                       const uint64_t* dmjump_mask) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !pp_dm || !pp_dme || !dm_sigma) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc_ = commit_uploads(ctx)) return rc_;  // (staged pulsar uploads first)
     PsrHost& ph = ctx->psrs[psr];
     if (ph.spec.ndmjump > 0 && !dmjump_mask) { ctx->err = "DMJUMPs without masks"; return PINT_E_INVALID; }
     for (int i = 0; i < ph.n; i++)
@@ -6140,6 +6394,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
             }
         }
     }
+    if (ext_t)  // (the timing events are created at first use)
+        for (int i : {12, 13})
+            if (!ctx->ev[i]) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (vgp) {
         for (size_t gi = 0; gi < ctx->kp_groups_v.size(); gi++) {
             const KpGroup& kg = ctx->kp_groups_v[gi];
@@ -6445,15 +6702,18 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
         const InstDev* insts = ctx->d_inst;
         ctx->cq.push_back([=]() -> int {
             hipStream_t st = ctx->cstream;
+            HostLap lap{"read_step op"};
             if (cov_run) {
                 hipLaunchKernelGGL(k_cov_dmx<16>, dim3(ninst, cov ? cov_wg : 1), dim3(1024), lds, st, psrs, insts, d_xw,
                                    mode, cov ? d_cv : nullptr, d_er);
                 HIPCHK(hipGetLastError());
+                lap("k_cov_dmx launch");
             }
-            if (dpars) HIPCHK(hipMemcpyAsync(dpars, d_dp, sizeof(double) * tc, hipMemcpyDeviceToHost, st));
-            if (errs) HIPCHK(hipMemcpyAsync(errs, d_er, sizeof(double) * tc, hipMemcpyDeviceToHost, st));
-            if (cov) HIPCHK(hipMemcpyAsync(cov, d_cv, sizeof(double) * tcv, hipMemcpyDeviceToHost, st));
-            if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, d_cl, sizeof(double) * ninst, hipMemcpyDeviceToHost, st));
+            if (int rc = export_seg(ctx, dpars, d_dp, tc)) return rc;
+            if (int rc = export_seg(ctx, errs, d_er, tc)) return rc;
+            if (int rc = export_seg(ctx, cov, d_cv, tcv)) return rc;
+            if (int rc = export_seg(ctx, chi2lin, d_cl, ninst)) return rc;
+            lap("segments");
             return PINT_OK;
         });
         if (cov_run) ctx->cov_pending = cov == nullptr;  // errors only: a later read of the covariance re-runs it
@@ -6795,19 +7055,32 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     const int s = ctx->slot;
     // the step's kernels end at ev_done; its status word goes to the host on the copy stream
     // after them (off the kernel stream), and ev_cdone covers it and the step's output copies
+    HostLap lap{"step_end"};
     HIPCHK(hipEventRecord(ctx->ev_done[s], ctx->stream));
-    if (!ctx->cq.empty()) {  // the step's deferred copy-stream work, behind its last kernel
-        if (int rc = flush_cq(ctx, ctx->ev_done[s])) return rc;
-    } else {
-        HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_done[s], 0));
-    }
-    if (ctx->chi2_dst) {  // the step's deferred chi2 copy (pint_chi2_gls, lazy)
-        HIPCHK(hipMemcpyAsync(ctx->chi2_dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost,
-                              ctx->cstream));
+    lap("record ev_done");
+    // the step's deferred copy-stream work behind its last kernel, its host-bound outputs --
+    // with the chi2 of pint_chi2_gls and the slot's status word -- in one k_export
+    if (ctx->chi2_dst) {
+        if (int rc = export_seg(ctx, ctx->chi2_dst, ctx->d_chi2g, ctx->ninst)) return rc;
         ctx->chi2_dst = nullptr;
     }
-    HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->cstream));
+    bool st_exp = false;
+    {
+        void* sd = nullptr;
+        if (hipHostGetDevicePointer(&sd, ctx->h_status + s, 0) == hipSuccess && sd) {
+            ctx->exp_st_src = ctx->d_status_slots + s;
+            ctx->exp_st_dst = static_cast<int*>(sd);
+            st_exp = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    if (int rc = flush_cq(ctx, ctx->ev_done[s])) return rc;
+    lap("flush");
+    if (!st_exp)  // (no device-visible address of the status mirror: a runtime copy)
+        HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->cstream));
     HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
+    lap("record ev_cdone");
     ctx->cdone_rec[s] = true;
     ctx->slot = (s + 1) % pint_ctx::NSLOT;
     ctx->d_status = ctx->d_status_slots + ctx->slot;
@@ -6833,15 +7106,36 @@ int pint_fit_step_enqueue(pint_ctx* ctx, int restore, int mode, double lambda_, 
     if (!ctx->lazy || ctx->capturing) { ctx->err = "pint_fit_step_enqueue needs lazy mode (no capture)"; return PINT_E_INVALID; }
     if (mode != 1) { ctx->err = "pint_fit_step_enqueue: GLS steps (mode 1) only"; return PINT_E_INVALID; }
     int rc = PINT_OK;
+    // PINT_TRACE_ENQ=1: the host time of each enqueue stage (a stall > 1 ms is printed)
+    static const bool tr = getenv("PINT_TRACE_ENQ") && atoi(getenv("PINT_TRACE_ENQ"));
+    static long ncall = 0;
+    ncall++;
+    auto t_prev = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!tr) return;
+        const auto t = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(t - t_prev).count();
+        if (ms > 1.0) fprintf(stderr, "[pint enqueue %ld] %s took %.3f ms\n", ncall, what, ms);
+        t_prev = t;
+    };
     if (restore && (rc = pint_restore_tables(ctx))) return rc;
+    lap("restore");
     if ((rc = pint_eval(ctx, 2))) return rc;
+    lap("eval(M)");
     if ((rc = pint_fit_step_apply(ctx, mode, lambda_))) return rc;
+    lap("fit_step_apply");
     if ((dpars || errs || cov || chi2lin) && (rc = pint_read_step(ctx, dpars, errs, cov, chi2lin))) return rc;
+    lap("read_step");
     if ((noise_red || noise_ecorr) && (rc = pint_noise_resids(ctx, noise_red, noise_ecorr))) return rc;
     if (noise_dm && (rc = pint_noise_resids_dm(ctx, noise_dm))) return rc;
+    lap("noise");
     if ((rc = pint_eval(ctx, 0))) return rc;
+    lap("eval");
     if (chi2 && (rc = pint_chi2_gls(ctx, chi2))) return rc;
-    return pint_step_end(ctx, slot);
+    lap("chi2_gls");
+    rc = pint_step_end(ctx, slot);
+    lap("step_end");
+    return rc;
 }
 
 int pint_check_step(pint_ctx* ctx, int s) {
@@ -6951,6 +7245,7 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
         double *d_es = ctx->d_esum, *d_eD = ctx->d_eD, *d_eC = ctx->d_eC, *d_df = ctx->d_dfac;
         ctx->cq.push_back([=]() -> int {
             hipStream_t st = ctx->cstream;
+            HostLap lap{"noise op"};
             if (red)
                 hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ninst), dim3(256), 0, st, psrs, insts, d_dp, dr, 0,
                                    d_df);
@@ -6961,8 +7256,11 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
                                        de, cmp, d_eC);
             }
             HIPCHK(hipGetLastError());
-            if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
-            if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
+            lap("kernels");
+            if (red)
+                if (int rc = export_seg(ctx, red, dr, tot)) return rc;
+            if (ecorr)
+                if (int rc = export_seg(ctx, ecorr, de, tot)) return rc;
             return PINT_OK;
         });
         return PINT_OK;
@@ -7019,8 +7317,7 @@ int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
             hipStream_t st = ctx->cstream;
             hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ninst), dim3(256), 0, st, psrs, insts, d_dp, d, 1, d_df);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(dm, d, sizeof(double) * tot, hipMemcpyDeviceToHost, st));
-            return PINT_OK;
+            return export_seg(ctx, dm, d, tot);
         });
         ctx->dm_noise_pend = true;
         return PINT_OK;
@@ -7105,6 +7402,7 @@ int pint_set_resids(pint_ctx* ctx, const double* time_resid) { return pint_debug
 int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || !sigma_s) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc_ = commit_uploads(ctx)) return rc_;  // (staged pulsar uploads first)
     ctx->wtile_valid = false;  // new weights: the fused Woodbury dots are stale
     PsrHost& ph = ctx->psrs[psr];
     const int n = ph.n;
@@ -7131,6 +7429,7 @@ int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
 int pint_set_noise_weights(pint_ctx* ctx, int psr, const double* red_phi, const double* ep_phi) {
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size()) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc_ = commit_uploads(ctx)) return rc_;  // (staged pulsar uploads first)
     PsrHost& ph = ctx->psrs[psr];
     const int nred = ph.spec.nred, nep = ph.dev.nep;
     if (red_phi)
@@ -7153,6 +7452,7 @@ int pint_set_noise_classes(pint_ctx* ctx, int psr, int ncls, const int32_t* cls_
     if (!ctx || psr < 0 || psr >= (int)ctx->psrs.size() || ncls <= 0 || !cls_ptr || !cls_idx || !sigma0_us)
         return PINT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (int rc_ = commit_uploads(ctx)) return rc_;  // (staged pulsar uploads first)
     PsrHost& ph = ctx->psrs[psr];
     const int n = ph.n;
     if (cls_ptr[0] != 0 || cls_ptr[ncls] != n) { ctx->err = "noise classes must cover every TOA once"; return PINT_E_INVALID; }

@@ -184,37 +184,28 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         tstride = pos
         spec.tstride = tstride
     noise_like = {"EFAC", "EQUAD", "ECORR", "TNEQ", "DMEFAC", "DMEQUAD"}
+    noise_amp = {"TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX", "TNDMAMP", "TNDMGAM", "TNDMC"}
+    # parameter -> (column kind, index), built once per layout (a PTA pulsar has ~115 free
+    # parameters, 100 of them DMX: list.index per parameter was a quadratic scan)
+    kind_of = {"PHOFF": (L.COL_OFFSET, 0), "PX": (L.COL_PX, 0)}  # (PHOFF: -d_offset_phase_d_PHOFF / F0 = 1/F0)
+    for names, kk in ((("RAJ", "ELONG"), L.COL_LON), (("DECJ", "ELAT"), L.COL_LAT), (("PMRA", "PMELONG"), L.COL_PMLON),
+                      (("PMDEC", "PMELAT"), L.COL_PMLAT)):
+        for nm in names:
+            kind_of[nm] = (kk, 0)
+    # (later groups first, so that an earlier group wins a shared name, as the if-chain did)
+    for group, kk in ((dmjumps, L.COL_ZERO), (jumps, L.COL_JUMP), (fds, L.COL_FD), (dmx, L.COL_DMX),
+                      (dms, L.COL_DM), (F, L.COL_F)):
+        for j, nm in enumerate(group):
+            kind_of[nm] = (kk, j)
     for n in model.free_params:
         p = model[n]
-        base = "".join(ch for ch in n if not ch.isdigit())
-        if p.kind == "mask" and base in noise_like:
+        if p.kind == "mask" and "".join(ch for ch in n if not ch.isdigit()) in noise_like:
             continue
-        if n in ("TNREDAMP", "TNREDGAM", "TNREDC", "RNAMP", "RNIDX", "TNDMAMP", "TNDMGAM", "TNDMC"):
+        if n in noise_amp:
             continue
-        if n == "PHOFF":  # -d_offset_phase_d_PHOFF / F0 = 1/F0, the Offset column's values
-            k, i = L.COL_OFFSET, 0
-        elif n in F:
-            k, i = L.COL_F, F.index(n)
-        elif n in ("RAJ", "ELONG"):
-            k, i = L.COL_LON, 0
-        elif n in ("DECJ", "ELAT"):
-            k, i = L.COL_LAT, 0
-        elif n in ("PMRA", "PMELONG"):
-            k, i = L.COL_PMLON, 0
-        elif n in ("PMDEC", "PMELAT"):
-            k, i = L.COL_PMLAT, 0
-        elif n == "PX":
-            k, i = L.COL_PX, 0
-        elif n in dms:
-            k, i = L.COL_DM, dms.index(n)
-        elif n in dmx:
-            k, i = L.COL_DMX, dmx.index(n)
-        elif n in fds:
-            k, i = L.COL_FD, fds.index(n)
-        elif n in jumps:
-            k, i = L.COL_JUMP, jumps.index(n)
-        elif n in dmjumps:  # DMJUMPs leave the delay alone: a zero column (dispersion_model.py:797)
-            k, i = L.COL_ZERO, dmjumps.index(n)
+        ki = kind_of.get(n)
+        if ki is not None:
+            k, i = ki
         elif model.binary and n in BIN_IDS and n in offs:
             k, i = L.COL_BIN, BIN_IDS[n]
         else:
@@ -877,14 +868,14 @@ class Session:
         """(steps, errors, covariances, linearised chi2) of the last fit_step: per-instance
         views (SplitView) of the K+1 step / error vectors and the timing covariance."""
         ok = self._off_k
-        dp = self._pin("dp", ok[-1])
-        er = self._pin("er", ok[-1])
-        cov = self._pin("cov", self._off_cov[-1]) if want_cov else None
-        cl = self._pin("cl", len(ok) - 1)
+        # lazy: pinned per-slot buffers the copy stream fills; synchronous: fresh pageable
+        # arrays (a first synchronous fit pays no page-locked allocation of its outputs)
+        get = self._pin if self.lazy else (lambda name, n: np.empty(max(1, int(n))))
+        dp = get("dp", ok[-1])
+        er = get("er", ok[-1])
+        cov = get("cov", self._off_cov[-1]) if want_cov else None
+        cl = get("cl", len(ok) - 1)
         self._check(self.L.pint_read_step(self.ctx, L.ptr(dp), L.ptr(er), L.ptr(cov), L.ptr(cl)))
-        if not self.lazy:  # synchronous call: hand out private copies of the pinned buffers
-            dp, er, cl = dp.copy(), er.copy(), cl.copy()
-            cov = cov.copy() if want_cov else None
         covs = SplitView(cov, self._off_cov, self._cov_shapes) if want_cov else []
         return SplitView(dp, ok), SplitView(er, ok), covs, cl
 
@@ -898,15 +889,15 @@ class Session:
         return t
 
     def chi2_gls(self):
-        c = self._pin("chi2g", len(self.inst_layout))
+        c = self._pin("chi2g", len(self.inst_layout)) if self.lazy else np.empty(len(self.inst_layout))
         self._check(self.L.pint_chi2_gls(self.ctx, L.ptr(c)))
-        return c if self.lazy else c.copy()
+        return c
 
     def chi2_wls(self):
         """WLS chi2 of the current residuals per instance (pint_chi2_wls)."""
-        c = self._pin("chi2w", len(self.inst_layout))
+        c = self._pin("chi2w", len(self.inst_layout)) if self.lazy else np.empty(len(self.inst_layout))
         self._check(self.L.pint_chi2_wls(self.ctx, L.ptr(c)))
-        return c if self.lazy else c.copy()
+        return c
 
     def solve_eig(self, mode, thresholds):
         """SVD path of the fitters on the last fit_step's Gram (k_eig): replaces the step

@@ -52,8 +52,8 @@ def red_noise_freqs_weights(model, toas):
     f_k stays longdouble, as the reference builds its basis sin(2 pi t f_k) with it
     (noise_model.py:861-880); the device receives it as a double-double pair."""
     amp, gam, nf = model.red_noise_params()
-    t = toas.tdbld * np.longdouble(86400)
-    T = t.max() - t.min()
+    lo, hi = toas.tdbld_extent()  # (== tdbld.min(), .max(): T as (tdbld * 86400).max() - .min())
+    T = hi * np.longdouble(86400) - lo * np.longdouble(86400)
     f = np.linspace(1 / T, nf / T, nf)
     ff = np.zeros(2 * nf)
     ff[::2] = f
@@ -68,8 +68,8 @@ def dm_noise_freqs_weights(model, toas):
     with TNDMAMP/TNDMGAM/TNDMC; its basis is the Fourier basis times (1400 MHz / f_bary)^2 per
     TOA, formed on the device (the barycentric frequency depends on the model)."""
     amp, gam, nf = model.dm_noise_params()
-    t = toas.tdbld * np.longdouble(86400)
-    T = t.max() - t.min()
+    lo, hi = toas.tdbld_extent()  # (== tdbld.min(), .max(): T as (tdbld * 86400).max() - .min())
+    T = hi * np.longdouble(86400) - lo * np.longdouble(86400)
     f = np.linspace(1 / T, nf / T, nf)
     ff = np.zeros(2 * nf)
     ff[::2] = f

@@ -68,6 +68,21 @@ class TOAs:
     def tdbld(self) -> np.ndarray:
         return self.arrays["tdb_hi"].astype(np.longdouble) + self.arrays["tdb_lo"].astype(np.longdouble)
 
+    def tdbld_extent(self):
+        """(min, max) of tdbld, equal to tdbld.min() / .max(), from the few TOAs whose hi part
+        is extreme (with lo within half an ulp of hi the order of hi decides but for ties):
+        the red-noise span T needs only these, not a longdouble pass over every TOA."""
+        hi, lo = self.arrays["tdb_hi"], self.arrays["tdb_lo"]
+        if len(hi) == 0 or not np.all(np.abs(lo) <= 0.5 * np.spacing(np.abs(hi))):
+            t = self.tdbld
+            return t.min(), t.max()
+        out = []
+        for ext in (hi.min(), hi.max()):
+            k = np.flatnonzero(hi == ext)
+            v = hi[k].astype(np.longdouble) + lo[k].astype(np.longdouble)
+            out.append(v.min() if ext == hi.min() and len(out) == 0 else v.max())
+        return out[0], out[1]
+
     def get_mjds(self) -> np.ndarray:
         return self.arrays["mjd_float"]
 

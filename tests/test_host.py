@@ -150,6 +150,10 @@ def test_one_hip_runtime_whatever_loads_first():
     env.pop("PINT_HIP_RUNTIME", None)
     out = subprocess.run([sys.executable, "-c", code], check=True, capture_output=True, text=True, env=env)
     assert out.stdout.split() == ["1", "1"], out.stdout
+    # ... and it is the system ROCm's (torch's copies never mapped)
+    code2 = code.replace("print(len(m), len(h))", "print(all('/torch/' not in x for x in m | h))")
+    out = subprocess.run([sys.executable, "-c", code2], check=True, capture_output=True, text=True, env=env)
+    assert out.stdout.split() == ["True"], out.stdout
 
 
 def test_struct_layout_matches_header():

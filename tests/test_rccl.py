@@ -28,15 +28,15 @@ def _free_port():
 
 @pytest.fixture
 def nccl_group():
+    from pint_amd import _lib
+    ndev = _lib.lib().pint_device_count()  # (before torch: the process's HIP runtime is chosen here)
     import torch
     import torch.distributed as dist
     from pint_amd import pta
-    from pint_amd import _lib
-    ndev = _lib.lib().pint_device_count()
     if ndev <= 0:
         pytest.skip("no GPU visible to libpint_hip")
     # the library sees a device, so torch must too: a False here is a second HIP runtime in
-    # the process (pint_amd._lib._share_torch_hip_runtime), never a reason to skip
+    # the process (pint_amd._lib._one_hip_runtime), never a reason to skip
     maps = sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln})
     assert torch.cuda.is_available(), (f"libpint_hip sees {ndev} device(s) but torch sees "
                                        f"{torch.cuda.device_count()}; HIP runtimes mapped: {maps}")
