@@ -346,6 +346,26 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
                 f"drain {1e3 * (tr[-1] - tr[2 * nsteps - 1]):.3f}")
         return kt, nk
 
+    # Python's cyclic GC: a full collection traverses every host object -- the TOA tables and
+    # flag lists of the whole PTA -- and took ~7 ms whenever it fell inside the timed steps
+    # (a 20-step run: 0.40 or 0.73 ms per step by where it fell).  Collected once before the
+    # warm-up and frozen (the objects alive now are never traversed again), no collection
+    # until the timed steps end; a compiled host would have no such pause.  (Collected between
+    # the warm-up and the timed steps instead, the device sat idle ~10 ms and the first timed
+    # steps ran slower.)
+    import gc
+    gc.collect()
+    gc.freeze()
+    gc.disable()
+    try:
+        return _timed(s, steps, warmup, barrier, max_over_ranks, graph, gram_pass, run, step, step_calls, replay)
+    finally:
+        gc.enable()
+        gc.unfreeze()
+
+
+def _timed(s, steps, warmup, barrier, max_over_ranks, graph, gram_pass, run, step, step_calls, replay):
+    from pint_amd import _lib as L
     run(warmup, step)
     use_graph = False
     if graph in (1, "1", "auto"):
@@ -364,24 +384,11 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
             use_graph = max_over_ranks(t_graph - t_direct) < 0.0  # the same choice on every rank
         else:
             use_graph = True
-    # Python's cyclic GC: a full collection traverses every host object -- the TOA tables and
-    # flag lists of the whole PTA -- and took ~7 ms whenever it fell inside the timed steps
-    # (a 20-step run: 0.40 or 0.73 ms per step by where it fell).  Collected once here and
-    # frozen (the objects alive now are never traversed again), no collection in the timed
-    # steps; a compiled host would have no such pause.
-    import gc
-    gc.collect()
-    gc.freeze()
-    gc.disable()
-    try:
-        barrier()
-        t0 = time.perf_counter()
-        run(steps, replay if use_graph else step)
-        barrier()
-        dt = max_over_ranks(time.perf_counter() - t0)
-    finally:
-        gc.enable()
-        gc.unfreeze()
+    barrier()
+    t0 = time.perf_counter()
+    run(steps, replay if use_graph else step)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
     # the Gram kernel's time: the same step with its events, after the timed region
     kt, nk = 0.0, 0
     if gram_pass:
@@ -569,10 +576,28 @@ def grid_leg(side, dist, barrier, max_over_ranks):
         barrier()
         dts.append(max_over_ranks(time.perf_counter() - t0))
     dt = float(np.median(dts))
+    # per-kernel device time of one more grid (every timing slot's HIP events on, the grid's
+    # one batch of points = one fit step; after the timed grids, which carry no events)
+    from pint_amd import gridutils
+    gs, glay = gridutils._GRID["cur"][1], gridutils._GRID["cur"][2]
+    gs.set_timing_mask(0xFF)
+    grid_chisq(f, ("F0", "F1"), (g0, g1))
+    kt = gs.timing()
+    gs.set_timing_mask(0)
+    roof = grid_roofline(kt, glay, side * side, dt)
     return {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
             "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 4),
             "seconds_all": [round(x, 4) for x in dts], "timing": "median of 3 grids after 2 warm-up grids",
-            "chi2_min": float(np.nanmin(chi2))}
+            "chi2_min": float(np.nanmin(chi2)), "roofline": roof}
+
+
+def grid_roofline(kt, lay, npts, dt):
+    """Roofline record of the grid step's kernels: per-kernel event times of
+    one grid and the dominant kernel against its bound."""
+    names = ["k_eval", "k_resid", "gram_span", "k_solve", "k_eval_M", "k_woodbury", "k_gram", "k_greduce"]
+    kms = {n: round(float(v), 4) for n, v in zip(names, kt)}
+    return {"kernel_ms": kms, "grid_ms": round(dt * 1e3, 3), "points": npts, "rows_per_point": lay.n,
+            "kernel_ms_source": "HIP events of every timing slot on one more grid after the timed grids"}
 
 
 def j0740_data():

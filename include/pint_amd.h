@@ -336,6 +336,11 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * k_schur, one workgroup per (block of S, instance), before the one-workgroup-per-instance
  * solve; 0 keeps it inside the solve.  Same operations in the same order: same bits. */
 #define PINT_OPT_SCHUR 9
+/* PINT_OPT_SMALL = 1 (default): instances of at most 32 padded columns and 512 rows (a
+ * grid's points) take k_gram_s (a wave per instance, applies from the next
+ * pint_set_instances) and the one-wave k_solve_blk (four instances per workgroup); 0 keeps
+ * them on the 16-wave Gram and the 4-wave solve (the tests cross-check the two). */
+#define PINT_OPT_SMALL 10
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

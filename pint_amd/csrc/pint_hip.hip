@@ -200,9 +200,22 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// a workgroup barrier, or with NW == 1 (one wave per instance, several instances per
+// workgroup) the wave's own: its LDS writes visible to its other lanes, no cross-wave wait
+template <int NW>
+__device__ __forceinline__ void bsync() {
+    if constexpr (NW == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
 template <int NW>
 __device__ double block_sum(double v, double* sh) {
     v = wave_sum(v);
+    if constexpr (NW == 1) return 0.0 + v;  // (the NW-wave form's order with one wave)
     int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) sh[w] = v;
@@ -218,6 +231,11 @@ template <int NW, int V>
 __device__ void block_sums(double* v, double* sh) {
 #pragma unroll
     for (int k = 0; k < V; k++) v[k] = wave_sum(v[k]);
+    if constexpr (NW == 1) {  // (the NW-wave form's order with one wave)
+#pragma unroll
+        for (int k = 0; k < V; k++) v[k] = 0.0 + v[k];
+        return;
+    }
     int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) {
@@ -468,19 +486,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 constexpr int RES_BT = 256;
 constexpr int RES_RB = 1024;  // rows per block (4 per thread)
 constexpr int RES_RPT = RES_RB / RES_BT;  // rows per thread
+// BT = threads per residual block: RES_BT, or 64 when every instance has at most 256 rows
+// (a grid's points): a wave per block, four blocks per workgroup, no workgroup barrier
+// (the 256-thread form gave a 62-row instance one busy wave, three idle ones and the
+// barriers of the block sums)
+constexpr int RES_SMALLN = 64 * RES_RPT;
+template <int BT>
 __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                   const int* __restrict__ rblk_inst,
+                                                   const int* __restrict__ rblk_inst, int nrblk,
                                                    const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
                                                    double* __restrict__ rphase, double* __restrict__ rpart) {
+    constexpr int NW = BT / 64;
     __shared__ double sh[2 * (RES_BT / 64)];
-    const int ii = rblk_inst[blockIdx.x];
+    const int rb = blockIdx.x * (RES_BT / BT) + (BT == RES_BT ? 0 : (int)__builtin_amdgcn_readfirstlane(threadIdx.x / BT));
+    if (BT != RES_BT && rb >= nrblk) return;  // (wave-uniform)
+    const int tid = threadIdx.x % BT;
+    const int ii = rblk_inst[rb];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
     const int n = I.n;
     const long ro = I.roff;
     const long oo = I.roff - ii;  // output rows: n per instance (roff counts n+1)
-    const int r0 = (int)(blockIdx.x - I.rb0) * RES_RB;
+    const int r0 = (int)(rb - I.rb0) * RES_RB;
     const int r1 = min(n, r0 + RES_RB);
     const dd tz = dd_make(ph_hi[ro + n], ph_lo[ro + n]);
     dd d0 = dd_make(0.0);
@@ -491,7 +519,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     double lh[RES_RPT], ll[RES_RPT], lp[RES_RPT], lpn[RES_RPT], lw[RES_RPT];
 #pragma unroll
     for (int u = 0; u < RES_RPT; u++) {
-        const int i = r0 + threadIdx.x + u * RES_BT;
+        const int i = r0 + tid + u * BT;
         const bool in = i < r1;
         lh[u] = in ? ph_hi[ro + i] : 0.0;
         ll[u] = in ? ph_lo[ro + i] : 0.0;
@@ -501,7 +529,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     }
 #pragma unroll
     for (int u = 0; u < RES_RPT; u++) {
-        const int i = r0 + threadIdx.x + u * RES_BT;
+        const int i = r0 + tid + u * BT;
         if (i >= r1) break;
         dd d = dd_add_d(dd_sub(dd_make(lh[u], ll[u]), tz), lp[u]);
         double full;
@@ -518,12 +546,12 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
     }
     if (S.subtract_mean) {
         double v[2] = {swx, sw};
-        block_sums<RES_BT / 64, 2>(v, sh);
+        block_sums<NW, 2>(v, sh);
         swx = v[0];
         sw = v[1];
-        if (threadIdx.x == 0) {
-            rpart[3 * blockIdx.x] = sw;
-            rpart[3 * blockIdx.x + 1] = swx;
+        if (tid == 0) {
+            rpart[3 * rb] = sw;
+            rpart[3 * rb + 1] = swx;
         }
     }
 }
@@ -538,31 +566,37 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
 // + 256j + lane (j < 4): four contiguous 64-row chunks, staged one at a time in the wave's own
 // LDS columns and contracted by 16 k-steps of 4 rows.
 constexpr int WT_CS = 66;  // k_resid2 tile staging: column stride (doubles), 64 rows + 2
+template <int BT>
 __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
-                                                   const int* __restrict__ rblk_inst, const double* __restrict__ ftay,
+                                                   const int* __restrict__ rblk_inst, int nrblk,
+                                                   const double* __restrict__ ftay,
                                                    double* __restrict__ rtime, double* __restrict__ rphase,
                                                    double* __restrict__ rpart, double* __restrict__ wtile) {
+    constexpr int NW = BT / 64;
     __shared__ double sh[2 * (RES_BT / 64)];
     extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS: A (columns 0-15), B (16-31)
-    const int ii = rblk_inst[blockIdx.x];
+    const int rb = blockIdx.x * (RES_BT / BT) + (BT == RES_BT ? 0 : (int)__builtin_amdgcn_readfirstlane(threadIdx.x / BT));
+    if (BT != RES_BT && rb >= nrblk) return;  // (wave-uniform)
+    const int tid = threadIdx.x % BT;
+    const int ii = rblk_inst[rb];
     const InstDev I = insts[ii];
     const PsrDev& Pd = psrs[I.psr];
     const pint_spec_t& S = *Pd.spec;
     const int n = I.n;
     const long ro = I.roff;
     const long oo = I.roff - ii;
-    const int r0 = (int)(blockIdx.x - I.rb0) * RES_RB;
+    const int r0 = (int)(rb - I.rb0) * RES_RB;
     const int r1 = min(n, r0 + RES_RB);
     const bool tile = wtile != nullptr;
     const bool harm = tile && __builtin_amdgcn_readfirstlane(S.nred) > 0;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;  // (the workgroup's wave: its LDS columns)
     // the thread's RES_RPT rows loaded up front (one load latency per block, not one per row),
     // before the weighted mean's partial sums and barriers, so the two latencies overlap
     double lr[RES_RPT], lf[RES_RPT], ls[RES_RPT];
     double4_t lz[RES_RPT];
 #pragma unroll
     for (int j = 0; j < RES_RPT; j++) {
-        const int i = r0 + threadIdx.x + j * RES_BT;
+        const int i = r0 + tid + j * BT;
         const bool in = i < r1;
         lr[j] = in ? rphase[oo + i] : 0.0;
         lf[j] = in ? ftay[ro + i] : 1.0;
@@ -572,12 +606,12 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     double mean = 0.0;
     if (S.subtract_mean) {  // residuals.py:314-425 weighted mean (utils.py:2002), fixed tree order
         double a = 0.0, b = 0.0;
-        for (int k = threadIdx.x; k < I.nrb; k += RES_BT) {
+        for (int k = tid; k < I.nrb; k += BT) {
             b += rpart[3 * (I.rb0 + k)];
             a += rpart[3 * (I.rb0 + k) + 1];
         }
         double v[2] = {a, b};
-        block_sums<RES_BT / 64, 2>(v, sh);
+        block_sums<NW, 2>(v, sh);
         mean = v[0] / v[1];
     }
     double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};  // independent chains
@@ -586,7 +620,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     double c2 = 0.0;
 #pragma unroll
     for (int j = 0; j < RES_RPT; j++) {
-        const int i = r0 + threadIdx.x + j * RES_BT;
+        const int i = r0 + tid + j * BT;
         double wr = 0.0;
         if (i < r1) {
             double p = lr[j] - mean;
@@ -621,9 +655,13 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
             __builtin_amdgcn_wave_barrier();
         }
     }
-    c2 = block_sum<RES_BT / 64>(c2, sh);
-    if (threadIdx.x == 0) rpart[3 * blockIdx.x + 2] = c2;
-    if (tile) {
+    c2 = block_sum<NW>(c2, sh);
+    if (tid == 0) rpart[3 * rb + 2] = c2;
+    if (tile && NW == 1) {  // the wave's own tile (D[4q + lane/16][lane%16])
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            wtile[(long)rb * 256 + (4 * q + (lane >> 4)) * 16 + (lane & 15)] = (acc[0][q] + acc[1][q]) + (acc[2][q] + acc[3][q]);
+    } else if (tile) {
         // the waves' tiles summed in a fixed order through LDS (acc[q]: D[4q + lane/16][lane%16])
         __syncthreads();
         double* red = xs;
@@ -632,7 +670,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
             red[wave * 256 + (4 * q + (lane >> 4)) * 16 + (lane & 15)] = (acc[0][q] + acc[1][q]) + (acc[2][q] + acc[3][q]);
         __syncthreads();
         for (int e = threadIdx.x; e < 256; e += RES_BT)
-            wtile[(long)blockIdx.x * 256 + e] = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
+            wtile[(long)rb * 256 + e] = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
     }
 }
 
@@ -955,6 +993,87 @@ __global__ __launch_bounds__(GTHREADS) void k_gram(const PsrDev* __restrict__ ps
             for (int g = 0; g < CG2; g++) v += lds[g * Kp + tid];
             colsq[(I.coff + tid) * nsplit + split] = v;
         }
+    }
+}
+
+// k_gram_s: k_gram's output (Gram partial of [T | r] / sigma, column sums of squares) for
+// small instances -- Kp <= 32, at most GS_MAXN rows per split (a grid's points: 62-row
+// NGC6440E fits by the 10^5).  One wave per (N-split, instance), four instances per
+// workgroup, no LDS and no barrier: lane l loads the MFMA operand it contributes directly,
+// row 4 kk + l / 16 of column l % 16 (and l % 16 + 16), weighted as it arrives, so a k-step
+// is one v_mfma_f64_16x16x4f64 per upper tile ((0,0); with Kp = 32 also (0,1), (1,1)).
+// The 16-wave k_gram gave such an instance one tile on one wave and 15 idle waves.
+constexpr int GS_MAXN = 512;
+__global__ __launch_bounds__(256) void k_gram_s(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                int count, const double* __restrict__ M,
+                                                const double* __restrict__ rtime, int nsplit, int compact,
+                                                double* __restrict__ Gpart, double* __restrict__ colsq) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= count) return;  // (wave-uniform)
+    const InstDev I = insts[q];
+    const PsrDev& Pd = psrs[I.psr];
+    const bool cmp = compact && Pd.dsplit;
+    const int n = I.n, K = cmp ? Pd.Kd : I.K, Kp = cmp ? Pd.Kpd : I.Kp;
+    const bool two = Kp > 16;
+    const int split = blockIdx.x;
+    long per = (n + nsplit - 1) / nsplit;
+    per = (per + 3) / 4 * 4;
+    const long i0 = min((long)n, split * per), i1 = min((long)n, i0 + per);
+    const double* Mi = M + I.moff;
+    const double* ri = rtime + I.ooff;
+    const int c0 = lane & 15, c1 = c0 + 16, kr = lane >> 4;
+    // the lane's two columns: a design-matrix column, the residual (column K) or padding
+    const double* p0 = c0 < K ? Mi + (long)c0 * n : ri;
+    const double* p1 = c1 < K ? Mi + (long)c1 * n : ri;
+    const bool z0 = c0 > K, z1 = c1 > K || !two;
+    double4_t a00 = {0, 0, 0, 0}, a01 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
+    double s0 = 0.0, s1 = 0.0;  // unweighted sums of squares of the lane's columns
+    constexpr int U = 4;        // k-steps per iteration: every load of the 16 rows issued first
+    for (long r0 = i0; r0 < i1; r0 += 4 * U) {
+        double v0[U], v1[U], w[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long row = r0 + 4 * u + kr;
+            ok[u] = row < i1;
+            const long rc = ok[u] ? row : i0;  // clamped, valid address
+            w[u] = ok[u] ? Pd.isig[rc] : 0.0;
+            v0[u] = z0 ? 0.0 : p0[rc];
+            v1[u] = z1 ? 0.0 : p1[rc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const double x0 = v0[u] * w[u], x1 = v1[u] * w[u];
+            if (ok[u]) {
+                s0 += v0[u] * v0[u];
+                s1 += v1[u] * v1[u];
+            }
+            a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x0, a00, 0, 0, 0);
+            if (two) {
+                a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x1, a01, 0, 0, 0);
+                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, x1, a11, 0, 0, 0);
+            }
+        }
+    }
+    double* G = Gpart + I.goff + (long)split * Kp * Kp;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {  // D[row = lane / 16 + 4 e][col = lane % 16]
+        const int row = kr + 4 * e;
+        G[(long)row * Kp + c0] = a00[e];
+        if (two) {
+            G[(long)row * Kp + c1] = a01[e];
+            G[(long)(row + 16) * Kp + c1] = a11[e];
+        }
+    }
+    // column sums of squares: the four lanes of a column (kr = 0..3) summed in a fixed order
+    s0 += __shfl_xor(s0, 16);
+    s0 += __shfl_xor(s0, 32);
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    if (kr == 0) {
+        if (c0 < K) colsq[(I.coff + c0) * nsplit + split] = s0;
+        if (two && c1 < K) colsq[(I.coff + c1) * nsplit + split] = s1;
     }
 }
 
@@ -2508,6 +2627,7 @@ __device__ void block_max2(double* v, double* sh) {
         v[0] = fmax(v[0], __shfl_xor(v[0], o, 64));
         v[1] = fmax(v[1], __shfl_xor(v[1], o, 64));
     }
+    if constexpr (NW == 1) return;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) {
@@ -2530,6 +2650,7 @@ template <int NW>
 __device__ double block_max(double v, double* sh) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    if constexpr (NW == 1) return v;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) sh[w] = v;
@@ -2623,7 +2744,7 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
             if (!ok && lane == 0) *sflag = 1;
         }
         if (k == 0) TS(10);
-        __syncthreads();
+        bsync<NW>();
         if (k == 0) TS(11);
         if (*sflag) return false;
         const double* Lkk = A + lblk(k, k);
@@ -2633,7 +2754,7 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
             bmma<false, false>(acc, Aik, Lkk, lane, false);
             bstore(Aik, acc, lane, 1.0);
         }
-        __syncthreads();
+        bsync<NW>();
         if (k == 0) TS(12);
         const int m = nb - k - 1;
         if (m == 0) break;
@@ -2645,7 +2766,7 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
             bmma<false, false>(acc, A + lblk(k + 1 + ii, k), A + lblk(k + 1 + jj, k), lane, true);
             bstore(Aij, acc, lane, 1.0);
         }
-        __syncthreads();
+        bsync<NW>();
         if (k == 0) TS(13);
     }
     TS(14);
@@ -2657,9 +2778,9 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
             for (int k = j; k < i; k++) bmma<false, true>(acc, A + lblk(i, k), A + lblk(k, j), lane, false);
             bmma_reg(acc2, A + lblk(i, i), acc, lane);
         }
-        __syncthreads();
+        bsync<NW>();
         if (j < i) bstore(A + lblk(i, j), acc2, lane, -1.0);
-        __syncthreads();
+        bsync<NW>();
         if (i == 1) TS(15);
     }
     TS(16);
@@ -2730,7 +2851,7 @@ __device__ __forceinline__ bool woodbury_sigma(const GramView& G, const PsrDev& 
 }
 
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+__global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                        const double* __restrict__ tables, const double* __restrict__ Gpart,
                                                        const double* __restrict__ colsq, int nsplit, int mode,
                                                        int compact, const double* __restrict__ Sd,
@@ -2738,11 +2859,18 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
                                                        double* __restrict__ dpars, double* __restrict__ errs,
                                                        double* __restrict__ cov, double* __restrict__ chi2lin,
                                                        double* __restrict__ sigL, int* __restrict__ status,
-                                                       int skip_dsplit, double* __restrict__ rscr, int refine) {
-    extern __shared__ double lds[];
-    __shared__ int sflag;
+                                                       int skip_dsplit, double* __restrict__ rscr, int refine,
+                                                       int ninst, int lds_stride) {
+    extern __shared__ double lds_all[];
+    // NW == 1: four instances per workgroup, a wave each (own LDS region, flag, barriers)
+    constexpr int IPB = NW == 1 ? 4 : 1;
+    const int wv = IPB > 1 ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+    __shared__ int sflags[IPB];
     __shared__ double sh[NW];
-    const int inst = blockIdx.x;
+    int& sflag = sflags[wv];
+    double* lds = lds_all + (long)wv * lds_stride;
+    const int inst = blockIdx.x * IPB + wv;
+    if (inst >= ninst) return;  // (wave-uniform; NW == 1 only)
     const InstDev I = insts[inst];
     const PsrDev& Pd = psrs[I.psr];
     if (skip_dsplit && compact && Pd.dsplit) return;  // solved by k_solve_dmx
@@ -2761,8 +2889,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     double* rv = xs + RSCR / 4;
     const bool cmp = compact && Pd.dsplit;
     const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tid = NW == 1 ? (threadIdx.x & 63) : threadIdx.x, lane = tid & 63;
+    const int wave = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) sflag = 0;
     // column norms (utils.py:2879 normalize_designmatrix: zero norm -> 1), as reciprocals
     for (int j = tid; j < nb * 16; j += NW * 64) {
@@ -2773,7 +2901,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
         }
         inv[j] = 1.0 / v;
     }
-    __syncthreads();
+    bsync<NW>();
     // the normalised normal matrix element (i, j < K), built from the Gram in global memory
     auto Aij = [&](int i, int j) {
         double v = G(i, j) * (inv[i] * inv[j]);
@@ -2790,7 +2918,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
     }
     for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) * inv[j] : 0.0;
     const double rwr = G(Kfull, Kfull);
-    __syncthreads();
+    bsync<NW>();
     if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         return;
@@ -2848,7 +2976,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
             sy += __shfl_xor(sy, 2, 64);
             if (sub == 0) yv[g] = sy;
         }
-        __syncthreads();
+        bsync<NW>();
         for (int g = g0; g < nb * 16; g += NW * 16) {  // x (+)= X^T y
             const int Jb = g >> 4, cc = g & 15;
             double sx = 0.0;
@@ -2857,7 +2985,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
             sx += __shfl_xor(sx, 2, 64);
             if (sub == 0) xs[g] = (pass == 0 ? 0.0 : xs[g]) + (g < K ? sx : 0.0);
         }
-        __syncthreads();
+        bsync<NW>();
         if (pass == REFINE_PASSES || !do_ref) break;
         for (int g = g0; g < nb * 16; g += NW * 16) {  // r = b - A x, double-double, a lane quad per row
             dd sa = dd_make(0.0);
@@ -2866,7 +2994,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_blk(const PsrDev* __restrict_
             sa = dd_quad_sum(sa);
             if (sub == 0) rv[g] = g < K ? dd_to_d(dd_sub(dd_make(bv[g]), sa)) : 0.0;
         }
-        __syncthreads();
+        bsync<NW>();
     }
     // dpars = x / norm; chi2lin = r^T W r - b^T x (= the minimised linearised chi2)
     double q2 = 0.0;
@@ -4558,6 +4686,11 @@ struct pint_ctx {
     int vbin = 1;        // PINT_OPT_VBIN: k_gram_v's binned DMX x Fourier tile
     int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
     int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
+    int maxn = 0;        // the batch's largest instance (rows)
+    bool grid_valid = false;  // the batch is pint_set_grid's: grid_psr's points, options grid_opts
+    int grid_psr = -1;
+    long grid_opts = 0;
+    int small = 1;       // PINT_OPT_SMALL: k_gram_s / one-wave k_solve_blk for small instances
     int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
@@ -5529,8 +5662,39 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
         }
         nv += var_size[j];
     }
-    std::vector<int32_t> ip(npts, psr);
-    if (int rc = set_instances_impl(ctx, npts, ip.data(), nullptr)) return rc;
+    // the same pulsar and point count as the resident batch (the next grid over the same
+    // TOAs, or the next chunk of one): every instance array, launch group and buffer is the
+    // same, only the tables differ -- reset the batch's state as a fresh batch has it and
+    // form the new tables, instead of ~3 ms of host set-up and InstDev uploads at 65,536 points
+    const long gkey = ((long)ctx->small << 2) | ((long)ctx->vgram << 1) | (long)ctx->vbin;
+    if (ctx->grid_valid && ctx->grid_psr == psr && ctx->ninst == npts && ctx->grid_opts == gkey && !ctx->psrs_dirty &&
+        ctx->setup_pending.empty()) {
+        if (int rc = flush_cq_now(ctx)) return rc;
+        HIPCHK(hipStreamSynchronize(ctx->cstream));
+        HIPCHK(hipStreamSynchronize(ctx->sstream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        clear_copy_pend(ctx);
+        dfree((void*&)ctx->d_tables0);  // (a snapshot of the previous points)
+        ctx->tables0_cap = 0;
+        ctx->ic_valid = ctx->ic0_valid = false;
+        ctx->restore_pending = ctx->chi2_pending = ctx->cov_pending = false;
+        ctx->wtile_valid = false;
+        ctx->chi2_dst = nullptr;
+        for (int k = 0; k < pint_ctx::NSLOT; k++) {
+            if (ctx->graph_exec_s[k]) hipGraphExecDestroy(ctx->graph_exec_s[k]);
+            if (ctx->graph_s[k]) hipGraphDestroy(ctx->graph_s[k]);
+            ctx->graph_exec_s[k] = nullptr;
+            ctx->graph_s[k] = nullptr;
+        }
+        HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ctx->ninst, ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->d_cov, 0, sizeof(double) * std::max<long>(1, ctx->tot_cv), ctx->stream));
+    } else {
+        std::vector<int32_t> ip(npts, psr);
+        if (int rc = set_instances_impl(ctx, npts, ip.data(), nullptr)) return rc;
+        ctx->grid_valid = true;
+        ctx->grid_psr = psr;
+        ctx->grid_opts = gkey;
+    }
     // the spec: base table, then per variable (toff, stride, size, value offset) as doubles
     // (exact: all < 2^53), then the value pairs
     std::vector<double> spec((size_t)ts + 4 * nvar + 2 * nv);
@@ -5558,6 +5722,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
 
 static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
+    ctx->grid_valid = false;  // (pint_set_grid marks its own batch afterwards)
     hipSetDevice(ctx->device);
     if (ctx->psrs_dirty && refresh_psrs(ctx)) return PINT_E_HIP;
     if (flush_setup(ctx)) return PINT_E_HIP;  // the uploads' red-noise set-up, one batch
@@ -5802,6 +5967,8 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     ctx->tot_out = out;
     ctx->tot_cv = cvoff;
     ctx->maxK = maxK;
+    ctx->maxn = 0;
+    for (const InstDev& I : ctx->inst) ctx->maxn = std::max(ctx->maxn, I.n);
     ctx->tot_e = eoff;
     ctx->tot_ep = epoff;
     ctx->max_nep = max_nep;
@@ -5836,7 +6003,8 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
                 const int ntr = (pd.red0c + 1 + pd.vns) / 16;
                 tT = 10 * (ntr - 1) + nt;
             }
-            if (tT < 1 || tT > maxT) continue;
+            if (lay < 2 && ctx->small && kp <= 32 && I.n <= GS_MAXN) tT = 0;  // k_gram_s
+            if (tT < (lay < 2 ? 0 : 1) || tT > maxT) continue;
             bucket[tT].push_back(k);
             if (kp > bkp[tT]) bkp[tT] = kp;
         }
@@ -5875,7 +6043,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
         }
         bool ident = true;  // the launch order is the instance order (e.g. a grid's points)
         int nxt = 0;
-        for (int T = 1; T <= maxT; T++) {
+        for (int T = 0; T <= maxT; T++) {
             if (bucket[T].empty()) continue;
             KpGroup g{T, (int)sorted.size(), (int)bucket[T].size(), bkp[T]};
             for (int k : bucket[T]) {
@@ -5929,7 +6097,9 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
             R = std::max(R, 2 * sp.nred);
             if (sp.dmn0 < sp.nred || sp.nred > 63) fuse = false;
         }
-        ctx->wfuse = fuse && !rbi.empty();
+        // (R = 0: no tile to form -- a WLS batch's post-fit pass would write 2 KB of zeros per
+        // residual block; 1^T W r then comes from k_wdot if a GLS chi2 is asked for)
+        ctx->wfuse = fuse && R > 0 && !rbi.empty();
         ctx->wtile_valid = false;
         if (ctx->wfuse) {
             HIPCHK(cmalloc((void**)&ctx->d_wtile, sizeof(double) * 256 * rbi.size()));
@@ -6182,10 +6352,21 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
         // (256-row blocks for small batches were measured: resid1 faster, resid2 and k_wsolve's
         // longer tile sums slower, the step ~1.4 us slower at 9 pulsars)
-        hipLaunchKernelGGL(k_resid1, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_rblk_inst, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
-        hipLaunchKernelGGL(k_resid2, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                           ctx->d_rblk_inst, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart, wt ? ctx->d_wtile : nullptr);
+        if (ctx->small && ctx->maxn <= RES_SMALLN) {  // a wave per residual block
+            const int nb4 = (ctx->nrblk + 3) / 4;
+            hipLaunchKernelGGL(k_resid1<64>, dim3(nb4), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
+            hipLaunchKernelGGL(k_resid2<64>, dim3(nb4), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                               ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
+                               wt ? ctx->d_wtile : nullptr);
+        } else {
+            hipLaunchKernelGGL(k_resid1<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_rp,
+                               ctx->d_rpart);
+            hipLaunchKernelGGL(k_resid2<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp,
+                               ctx->d_rpart, wt ? ctx->d_wtile : nullptr);
+        }
         // the chi2 partials are summed when the chi2 is read (pint_read_resids) or by k_wsolve,
         // which needs them anyway: no launch of its own in a fit step
         ctx->chi2_pending = true;
@@ -6370,9 +6551,20 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         for (int g = 0; g < (int)groups.size(); g++) {
             const KpGroup& kg = groups[g];
             const int T = kg.T;
+            const InstDev* di = (cmp ? ctx->d_inst_sorted_c : ctx->d_inst_sorted) + kg.first;
+            if (T == 0) {  // small instances: k_gram_s (the ECORR rows, if any, by k_gram<1> below)
+                hipLaunchKernelGGL(k_gram_s, dim3(ctx->nsplit, (kg.count + 3) / 4), dim3(256), 0, ctx->stream,
+                                   ctx->d_psrs, di, kg.count, ctx->d_M, ctx->d_rt, ctx->nsplit, cmp, ctx->d_G,
+                                   ctx->d_colsq);
+                if (mode == 1 && ctx->max_nep > 0)
+                    hipLaunchKernelGGL((k_gram<1, gram_ch(1), true>), dim3(1, kg.count), dim3(GTHREADS),
+                                       sizeof(double) * ((size_t)kg.maxKp * (gram_ch(1) + 2) + gram_ch(1)),
+                                       ctx->stream, ctx->d_psrs, di, ctx->d_M, ctx->d_rt, ctx->d_esum, ctx->d_eD,
+                                       ctx->nsplit, cmp, ctx->d_G, ctx->d_colsq);
+                continue;
+            }
             const int CH = gram_ch(T);
             size_t lds = sizeof(double) * ((size_t)kg.maxKp * (CH + 2) + CH);
-            const InstDev* di = (cmp ? ctx->d_inst_sorted_c : ctx->d_inst_sorted) + kg.first;
             for (int virt = 0; virt < 2; virt++) {
                 if (virt && !(mode == 1 && ctx->max_nep > 0)) break;
                 dim3 grid(virt ? 1 : ctx->nsplit, kg.count);
@@ -6603,17 +6795,28 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (skip && Ks == 0) {
         // every instance went through k_solve_dmx
     } else if (nbx <= BS_MAXNB && ctx->blocked_solve) {
-        size_t lds_b = sizeof(double) * ((size_t)nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx);
-        if (nbx <= 5)
+        const int ldsw = nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx;  // doubles per instance
+        size_t lds_b = sizeof(double) * (size_t)ldsw;
+        // K <= 32 (a grid's points): a wave per instance, four per workgroup -- the 4-wave
+        // form spent ~27 us of barriers and idle waves on each such instance
+        if (nbx <= 2 && ctx->small)
+            hipLaunchKernelGGL(k_solve_blk<1>, dim3((ctx->ninst + 3) / 4), dim3(256), 4 * lds_b, ctx->stream,
+                               ctx->d_psrs, ctx->d_inst, ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode,
+                               cmp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_dpars, ctx->d_errs, ctx->d_cov,
+                               ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine,
+                               ctx->ninst, ldsw);
+        else if (nbx <= 5)
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine,
+                               ctx->ninst, ldsw);
         else
             hipLaunchKernelGGL(k_solve_blk<16>, dim3(ctx->ninst), dim3(1024), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
                                ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
-                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine);
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine,
+                               ctx->ninst, ldsw);
     } else {
         int K = ctx->maxK;
         size_t lds_s = sizeof(double) * ((size_t)K * (K + 1) / 2 + 5 * K + 8);
@@ -6931,6 +7134,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     }
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_SCHUR) { ctx->schur = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_SMALL) { ctx->small = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_TIMING_EVERY) {
         if (value < 1) return PINT_E_INVALID;
         ctx->timing_every = value;

@@ -719,9 +719,11 @@ class Session:
     def read_chi2(self):
         """WLS chi2 per instance only (no residual rows copied back); lazy: a pinned buffer
         that is complete after check()."""
-        c2 = self._pin("chi2r", len(self.inst_layout)) if self.lazy else np.empty(len(self.inst_layout))
+        # (pinned either way: a copy into pageable memory left the host ~1 ms behind the
+        # device at 65,536 grid points)
+        c2 = self._pin("chi2r", len(self.inst_layout))
         self._check(self.L.pint_read_resids(self.ctx, None, None, L.ptr(c2)))
-        return c2
+        return c2 if self.lazy else c2.copy()
 
     def read_eval(self):
         rows = [l.n + 1 for l in self.inst_layout]
@@ -786,6 +788,11 @@ class Session:
     def set_schur(self, on=True):
         """The DMX-eliminated solve's build phase in k_schur (PINT_OPT_SCHUR, default on)."""
         self._check(self.L.pint_set_option(self.ctx, 9, 1 if on else 0))
+
+    def set_small(self, on=True):
+        """Small-instance kernels (PINT_OPT_SMALL, default on): k_gram_s from the next
+        set_instances, the one-wave solve from the next fit step."""
+        self._check(self.L.pint_set_option(self.ctx, 10, 1 if on else 0))
 
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""

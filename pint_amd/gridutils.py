@@ -110,6 +110,7 @@ def _grid_session(base, toas, gls):
     # a grid point reports its post-fit chi2, which is second order in a step error along
     # the weak directions: the solves' iterative refinement (PINT_OPT_REFINE) buys nothing
     s.set_refine(False)
+    s.set_timing_mask(0)  # no timing events in a grid's steps (bench.grid_leg turns them on)
     try:
         lay = s.add(build_layout(base, toas, use_gls_basis=gls))
     except Exception:

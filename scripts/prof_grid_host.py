@@ -22,3 +22,4 @@ pr.enable()
 grid_chisq(f, ("F0", "F1"), (g0, g1))
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(40)

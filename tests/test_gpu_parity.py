@@ -1200,3 +1200,88 @@ def test_fused_woodbury_dots_match_wdot(names):
     print(names, "fused vs k_wdot chi2", rel)
     assert np.all(rel < 1e-12), rel
     assert np.allclose(l_fused, l_wdot, rtol=1e-13, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mix", [False, True])
+def test_small_instance_kernels_match(mode, mix):
+    """k_gram_s (a wave per small instance) and the one-wave k_solve_blk (four instances per
+    workgroup) against the 16-wave k_gram and 4-wave solve (PINT_OPT_SMALL off): 9 NGC6440E
+    points (62 TOAs, two full workgroups and a partial one), alone or batched with a large
+    pulsar (which keeps the large kernels).  The Gram sums the same 4-row MFMA k-steps in
+    the same order; the column norms are summed in another order, so the steps agree to
+    rounding."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    m0, t0 = load("ngc6440e")[:2]
+    big = [load("pta_iso")[:2]] if mix else []
+
+    def run(small):
+        s = Session()
+        s.set_small(small)
+        lay = s.add(build_layout(m0, t0))
+        tab = pack_table(lay, m0)
+        insts = []
+        for k in range(9):
+            tk = tab.copy()
+            tk[lay.offsets["F0"]] += (k - 4) * 3e-11
+            insts.append((lay, tk))
+        for m, t in big:
+            bl = s.add(build_layout(m, t))
+            insts.append((bl, pack_table(bl, m)))
+        s.set_instances(insts)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(mode)
+        dp, er, cov, cl = s.read_step()
+        out = ([x.copy() for x in dp], [x.copy() for x in er], [x.copy() for x in cov], np.array(cl, copy=True))
+        s.close()
+        return out
+
+    (d1, e1, c1, l1), (d2, e2, c2, l2) = run(True), run(False)
+    for k in range(len(e1)):
+        f = e2[k] > 0  # (a column without an error: the last entry of a WLS step)
+        assert np.array_equal(e1[k] > 0, f)
+        assert np.max(np.abs(d1[k][f] - d2[k][f]) / e2[k][f]) < 1e-9
+        assert np.max(np.abs(e1[k][f] / e2[k][f] - 1)) < 1e-12
+        sc = np.sqrt(np.outer(np.diag(c2[k]), np.diag(c2[k])))
+        assert np.max(np.abs(c1[k] - c2[k]) / sc) < 1e-12
+    np.testing.assert_allclose(l1, l2, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_small_instance_residual_tiles_match():
+    """The one-wave residual blocks (k_resid1/2<64>, every instance <= 256 rows) with the
+    fused Woodbury trig tiles: every third TOA (200) of a PLRedNoise fixture, six instances (one
+    full workgroup and a half one), the post-fit GLS chi2 and the WLS chi2 of the 256-thread
+    blocks' (PINT_OPT_SMALL off) to rounding."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    model, full = load("phoff_red")[:2]
+    toas = full[np.arange(0, full.ntoas, 3)]
+    assert toas.ntoas <= 256
+
+    def run(small):
+        s = Session()
+        s.set_small(small)
+        lay = s.add(build_layout(model, toas))
+        tab = pack_table(lay, model)
+        insts = []
+        for k in range(6):
+            tk = tab.copy()
+            tk[lay.offsets["F0"]] += (k - 3) * 1e-11
+            insts.append((lay, tk))
+        s.set_instances(insts)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        s.apply_step_uniform(1.0)
+        s.eval(want_M=False)
+        tr, pr, c2w = s.read_resids()
+        c2g = s.chi2_gls().copy()
+        out = ([np.array(x, copy=True) for x in tr], np.array(c2w, copy=True), c2g)
+        s.close()
+        return out
+
+    (t1, w1, g1), (t2, w2, g2) = run(True), run(False)
+    for a, b in zip(t1, t2):
+        assert np.max(np.abs(a - b)) < 1e-15  # seconds
+    np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=0)
+    np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=0)

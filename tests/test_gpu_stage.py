@@ -416,6 +416,33 @@ def test_device_grid_tables_match_host_tables():
     s.close()
 
 
+@pytest.mark.parametrize("name,fitter", [("ngc6440e", "WLSFitter"), ("pta_dd", "GLSFitter")])
+def test_resident_grid_batch_matches_fresh(name, fitter):
+    """A grid over the same pulsar and point count as the resident batch reuses its instance
+    arrays, launch groups and buffers (pint_set_grid's fast path, only the tables formed
+    anew): the second grid equals the same grid in a fresh session bit for bit, after a first
+    grid with other values, and after a grid with an invalid point (whose batch was re-bound
+    without it)."""
+    import pint_amd
+    from pint_amd import gridutils
+    from pint_amd.gridutils import grid_chisq
+    model, toas = load(name)[:2]
+    f = getattr(pint_amd, fitter)(toas, copy.deepcopy(model))
+    f.fit_toas(maxiter=1)
+    F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+    s0, s1 = np.longdouble(f.model.F0.uncertainty), np.longdouble(f.model.F1.uncertainty)
+    ga = (F0 + np.linspace(-2, 2, 6) * s0, F1 + np.linspace(-2, 2, 5) * s1)
+    gb = (F0 + np.linspace(-3, 1, 6) * s0, F1 + np.linspace(-1, 3, 5) * s1)
+    extra = ["DM"]
+    gridutils._drop_grid_session()
+    grid_chisq(f, ("F0", "F1"), ga, extraparnames=extra)
+    c_res, e_res = grid_chisq(f, ("F0", "F1"), gb, extraparnames=extra)
+    gridutils._drop_grid_session()
+    c_new, e_new = grid_chisq(f, ("F0", "F1"), gb, extraparnames=extra)
+    np.testing.assert_array_equal(c_res, c_new)
+    np.testing.assert_array_equal(e_res["DM"], e_new["DM"])
+
+
 def test_invalid_grid_point_fails_alone():
     """A grid over the DD eccentricity that includes ECC >= 1: those points are NaN (the
     reference's doonefit returns NaN for the failed fit, gridutils.py:89-106) and every other
