@@ -2675,6 +2675,10 @@ __device__ __forceinline__ double rsq2(double d) {
     return __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
 }
 
+// N = 8: a block whose rows and columns 8..15 are identity padding (K <= 8 in a single-block
+// solve): only the leading 8 x 8 is factored -- the same operations on it as N = 16 does
+// (the padding's updates are exact no-ops), and the padding of L^-1 is identity as stored
+template <int N = 16>
 __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
     // Cholesky (lane r holds row r) and X = L^-1 (lane r its column r) in one pass: pivot j's
@@ -2682,30 +2686,30 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     // and the forward substitution, in axpy order (x[t] -= L[t][u] x[u], u ascending: the
     // same operations and rounding as a separate substitution after the factorisation, with
     // half the lane reads)
-    double a[16], x[16];
+    double a[N], x[N];
 #pragma unroll
-    for (int c = 0; c < 16; c++) {
+    for (int c = 0; c < N; c++) {
         a[c] = Akk[swz(r, c)];
         x[c] = (r == c) ? 1.0 : 0.0;
     }
     bool ok = true;
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
+    for (int j = 0; j < N; j++) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
         const double il = rsq2(djj);
         a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
         x[j] *= il;
 #pragma unroll
-        for (int c = j + 1; c < 16; c++) {
+        for (int c = j + 1; c < N; c++) {
             const double Lcj = rdlane(a[j], c);
             a[c] -= a[j] * Lcj;
             x[c] -= Lcj * x[j];
         }
     }
-    if (lane < 16) {
+    if (lane < N) {
 #pragma unroll
-        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+        for (int t = 0; t < N; t++) Akk[swz(t, r)] = x[t];
     }
     return ok;
 }
@@ -2736,11 +2740,13 @@ __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+
 // but either way the diagonal factor doubled (3.7 -> 6.9-7.2 us per block, also at k = 0
 // where no row is formed: the register allocation of the loop): dropped.)
 template <int NW>
-__device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag) {
+__device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag, int K = 1 << 30) {
     for (int k = 0; k < nb; k++) {
         if (k == 0) TS(9);
         if (wave == 0) {
-            bool ok = diag_factor(A + lblk(k, k), lane);
+            // (K: the matrix's order, its rows past K identity padding -- a last block of at
+            // most 8 rows takes the 8 x 8 factor)
+            bool ok = K - 16 * k <= 8 ? diag_factor<8>(A + lblk(k, k), lane) : diag_factor<16>(A + lblk(k, k), lane);
             if (!ok && lane == 0) *sflag = 1;
         }
         if (k == 0) TS(10);
@@ -2919,7 +2925,7 @@ __global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const Psr
     for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) * inv[j] : 0.0;
     const double rwr = G(Kfull, Kfull);
     bsync<NW>();
-    if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag)) {
+    if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag, K)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         return;
     }
@@ -4720,7 +4726,8 @@ struct pint_ctx {
     int* d_rblk_inst = nullptr;   // k_resid1/2 block -> instance
     double* d_rpart = nullptr;    // per residual block: sum w, sum w x, chi2 partial
     int nrblk = 0;
-    int eval_merge = 0;  // bit 0: one k_eval_mix launch without M, bit 1: with M (PINT_EVAL_MERGE)
+    int eval_merge = 0;  // bit 0: one k_eval_mix launch without M, bit 1: with M, bit 2: also for a
+                         // batch of one model (PINT_EVAL_MERGE)
     int nblk = 0;
     int blk_off[PINT_NBIN + 1] = {0};  // block ranges per binary model (PINT_BIN_*)
     long tot_table = 0, tot_rows = 0, tot_m = 0, tot_g = 0, tot_s = 0, tot_c = 0, tot_out = 0, tot_cv = 0;
@@ -6284,7 +6291,12 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         ctx->restore_pending = false;
         ctx->ic_valid = true;
     }
-    const bool mix = (ctx->eval_merge >> (want_M ? 1 : 0)) & 1;
+    // a batch of one model (a grid's points, an all-isolated PTA) takes that model's own
+    // build, whose register set the other models do not raise (k_eval<WM, 0>: 48 instead
+    // of 84 VGPRs + spills with M for an isolated pulsar); PINT_EVAL_MERGE bit 2 merges anyway
+    int ntyp = 0;
+    for (int t = 0; t < 3; t++) ntyp += ctx->blk_off[t + 1] > ctx->blk_off[t];
+    const bool mix = ((ctx->eval_merge >> (want_M ? 1 : 0)) & 1) && (ntyp > 1 || (ctx->eval_merge & 4));
     if (mix && ctx->nblk > 0) {
 #define PINT_EVAL_MIX(WM)                                                                                      \
         hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \

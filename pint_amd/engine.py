@@ -464,6 +464,7 @@ class Session:
         self.layouts: List[PulsarLayout] = []
         self.inst_psr: List[int] = []
         self.inst_layout: List[PulsarLayout] = []
+        self._uniform, self._offs = False, None
         self.lazy = False
         self._pinned: Dict[str, tuple] = {}
         self._inflight = set()  # pinned staging buffers with a copy still enqueued (lazy)
@@ -578,23 +579,45 @@ class Session:
     def _after_set(self, lays, ntab, uniform=False):
         self.inst_layout = lays
         self.ntab = ntab
-        # per-instance output offsets (read_step, noise_resids), formed once per batch (one
-        # layout for every instance -- grid points -- without a Python loop over them: a
-        # 256 x 256 grid's loops took ~15 ms of its ~25 ms)
-        if uniform and lays:
-            n = len(lays)
-            kk = np.full(n, lays[0].K + 1, dtype=np.int64)
-            nc = np.full(n, len(lays[0].columns), dtype=np.int64)
-            nn = np.full(n, lays[0].n, dtype=np.int64)
-            self._cov_shapes = [(int(nc[0]), int(nc[0]))] * n
-        else:
-            kk = np.array([l.K + 1 for l in lays], dtype=np.int64)
-            nc = np.array([len(l.columns) for l in lays], dtype=np.int64)
-            nn = np.array([l.n for l in lays], dtype=np.int64)
-            self._cov_shapes = [(int(c), int(c)) for c in nc]
-        self._off_k = np.concatenate([[0], np.cumsum(kk)])
-        self._off_cov = np.concatenate([[0], np.cumsum(nc * nc)])
-        self._off_n = np.concatenate([[0], np.cumsum(nn)])
+        self._uniform = uniform
+        self._offs = None  # (formed at the first read that needs them: a grid's points never do)
+
+    def _offsets(self):
+        """Per-instance output offsets (read_step, noise_resids), formed once per batch (one
+        layout for every instance -- grid points -- without a Python loop over them: a
+        256 x 256 grid's loops took ~15 ms of its ~25 ms)."""
+        if self._offs is None:
+            lays = self.inst_layout
+            if self._uniform and lays:
+                n = len(lays)
+                kk = np.full(n, lays[0].K + 1, dtype=np.int64)
+                nc = np.full(n, len(lays[0].columns), dtype=np.int64)
+                nn = np.full(n, lays[0].n, dtype=np.int64)
+                shapes = [(int(nc[0]), int(nc[0]))] * n
+            else:
+                kk = np.array([l.K + 1 for l in lays], dtype=np.int64)
+                nc = np.array([len(l.columns) for l in lays], dtype=np.int64)
+                nn = np.array([l.n for l in lays], dtype=np.int64)
+                shapes = [(int(c), int(c)) for c in nc]
+            self._offs = (np.concatenate([[0], np.cumsum(kk)]), np.concatenate([[0], np.cumsum(nc * nc)]),
+                          np.concatenate([[0], np.cumsum(nn)]), shapes)
+        return self._offs
+
+    @property
+    def _off_k(self):
+        return self._offsets()[0]
+
+    @property
+    def _off_cov(self):
+        return self._offsets()[1]
+
+    @property
+    def _off_n(self):
+        return self._offsets()[2]
+
+    @property
+    def _cov_shapes(self):
+        return self._offsets()[3]
 
     # -- launches -------------------------------------------------------------------
     FIT = 2  # want_M for a fit step: compact layout (DMX columns as bin sums, DESIGN.md)

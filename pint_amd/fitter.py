@@ -70,11 +70,12 @@ class BatchOutcome:
         self.maxiter_reached = ~converged & ~exc
 
 
-def model_key(model):
+def model_key(model, freeze=()):
     """Everything a pulsar upload (build_layout) depends on besides the TOAs: every
     parameter's name, value and frozen flag (noise values set sigma and the basis weights,
-    the frozen set the columns) and the component set."""
-    return (tuple((n, str(model[n].value), bool(model[n].frozen)) for n in model.params),
+    the frozen set the columns) and the component set.  freeze: parameters keyed as frozen
+    whatever their flag (the model a grid would copy and freeze them in)."""
+    return (tuple((n, str(model[n].value), bool(model[n].frozen) or n in freeze) for n in model.params),
             tuple(model.components), model.binary)
 
 

@@ -99,13 +99,19 @@ def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
 _GRID = {}
 
 
-def _grid_session(base, toas, gls):
+def _grid_session(model, parnames, toas, gls):
+    """The resident Session and layout for grids of `model` with `parnames` frozen (a copy
+    of the model is made and frozen only when a new upload is needed: the copy cost ~0.7 ms
+    per grid)."""
     from .engine import Session, build_layout
-    key = (id(toas), toas.ntoas, gls, model_key(base))
+    key = (id(toas), toas.ntoas, gls, model_key(model, freeze=tuple(parnames)))
     cur = _GRID.get("cur")
     if cur is not None and cur[0] == key and cur[3] is toas:
         return cur[1], cur[2]
     _drop_grid_session()
+    base = copy.deepcopy(model)
+    for p in parnames:
+        base[p].frozen = True
     s = Session()
     # a grid point reports its post-fit chi2, which is second order in a step error along
     # the weak directions: the solves' iterative refinement (PINT_OPT_REFINE) buys nothing
@@ -133,6 +139,10 @@ def _fit_block(s, lay, grid, mode, down, fitargs, want_tables):
     (gridutils.py:101-106), and so is every point of a batch in which no point can be."""
     from .fitter import InvalidModelParameters
     base, variables, npts, k0 = grid
+    if not down:
+        got = _fit_block_enqueued(s, lay, grid, mode, fitargs, want_tables)
+        if got is not None:
+            return got
     bf = BatchFit(None, mode=mode, session=s, grid=(lay, base, variables, npts, k0))
     try:
         if down:
@@ -146,6 +156,35 @@ def _fit_block(s, lay, grid, mode, down, fitargs, want_tables):
             chi2 = res.chi2
     except InvalidModelParameters:
         return np.full(npts, np.nan), (np.full((npts, lay.tstride), np.nan) if want_tables else None)
+    ft = bf.final_tables_flat().reshape(npts, lay.tstride) if want_tables else None
+    return chi2, ft
+
+
+def _fit_block_enqueued(s, lay, grid, mode, fitargs, want_tables):
+    """_fit_block's plain fit (maxiter steps, then the chi2) with every launch enqueued and
+    one synchronisation at the end (lazy Session): the synchronous form waited on the
+    device after each of its five calls (~40 us of idle device each at 65,536 points).
+    Returns None -- and the caller refits the block synchronously, which handles them -- if
+    any point raised a status (an invalid point, a degenerate normal matrix)."""
+    from . import _lib as L
+    base, variables, npts, k0 = grid
+    bf = BatchFit(None, mode=mode, session=s, grid=(lay, base, variables, npts, k0))
+    s.set_lazy(True)
+    try:
+        for _ in range(fitargs.get("maxiter", 1)):
+            s.eval(want_M=s.FIT)
+            s.fit_step(1 if bf.gls else 0)
+            s.apply_step_uniform(1.0)
+        s.eval(want_M=False)
+        get = bf._chi2_enqueue()
+        s.check()
+        chi2 = np.array(get()[0], dtype=np.float64)
+    except L.PintError as e:
+        if e.code not in BatchFit.EVAL_ERRORS + (L.PINT_E_NOT_PD,):
+            raise
+        return None
+    finally:
+        s.set_lazy(False)
     ft = bf.final_tables_flat().reshape(npts, lay.tstride) if want_tables else None
     return chi2, ft
 
@@ -187,15 +226,12 @@ def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     per, lo, hi = shard_range(npts, rank, world)
-    base = copy.deepcopy(ftr.model)
-    for p in parnames:
-        base[p].frozen = True
     chi2 = np.full(hi - lo, np.nan)
     extra = {e: np.full(hi - lo, np.nan) for e in extraparnames}
     if hi > lo:
-        s, lay = _grid_session(base, ftr.toas, mode == "gls")
+        s, lay = _grid_session(ftr.model, parnames, ftr.toas, mode == "gls")
         try:
-            t0 = pack_table(lay, base)
+            t0 = pack_table(lay, ftr.model)  # (the frozen flags do not enter the table)
             # points per batch: ~24 GB of per-instance device buffers (eval rows, design matrix,
             # Gram partials) per batch keeps any grid within HBM
             per_pt = 8.0 * (lay.n * (lay.K + 12) + 64 * (lay.K + 2) ** 2)

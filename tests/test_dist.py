@@ -44,7 +44,10 @@ def _stub_grid(gu):
     fit (chi2 a fixed function of each point's table; the 'fitted' table shifts DM)."""
     from pint_amd.engine import build_layout
 
-    def session(base, toas, gls):
+    def session(model, parnames, toas, gls):
+        base = copy.deepcopy(model)
+        for p in parnames:
+            base[p].frozen = True
         return None, build_layout(base, toas, use_gls_basis=gls)
 
     def fit_block(s, lay, grid, mode, down, fitargs, want):

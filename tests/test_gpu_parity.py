@@ -1285,3 +1285,32 @@ def test_small_instance_residual_tiles_match():
         assert np.max(np.abs(a - b)) < 1e-15  # seconds
     np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=0)
     np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_single_model_batch_eval_matches_merged(monkeypatch):
+    """A batch whose pulsars all share one model (isolated: NGC6440E points and the isolated
+    PTA pulsar) takes that model's own evaluation build (k_eval<WM, 0>) instead of the merged
+    k_eval_mix; PINT_EVAL_MERGE=7 forces the merged build.  Phases, delays, Taylor factors
+    and the design matrix agree to the last bit."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load("ngc6440e")[:2]] * 3 + [load("pta_iso")[:2]]
+
+    def run(merge):
+        monkeypatch.setenv("PINT_EVAL_MERGE", str(merge))
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.eval(want_M=True)
+        ev = [np.concatenate(x).copy() for x in s.read_eval()]
+        M = [x.copy() for x in s.read_designmatrix()]
+        s.eval(want_M=False)
+        ev0 = [np.concatenate(x).copy() for x in s.read_eval()]
+        s.close()
+        return ev, M, ev0
+
+    a, b = run(3), run(7)
+    for x, y in zip(a[0] + a[2], b[0] + b[2]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
