@@ -2739,14 +2739,17 @@ __device__ __forceinline__ void tri_decode(int p, int& i, int& j) {  // p = i(i+
 // the same operations, stored after a barrier -- removed the row loop below (3.3 -> 0.1 us)
 // but either way the diagonal factor doubled (3.7 -> 6.9-7.2 us per block, also at k = 0
 // where no row is formed: the register allocation of the loop): dropped.)
-template <int NW>
+template <int NW, bool SMALLK = false>
 __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lane, int* sflag, int K = 1 << 30) {
     for (int k = 0; k < nb; k++) {
         if (k == 0) TS(9);
         if (wave == 0) {
             // (K: the matrix's order, its rows past K identity padding -- a last block of at
             // most 8 rows takes the 8 x 8 factor)
-            bool ok = K - 16 * k <= 8 ? diag_factor<8>(A + lblk(k, k), lane) : diag_factor<16>(A + lblk(k, k), lane);
+            // (SMALLK: only k_solve_blk instantiates the 8 x 8 form -- compiled into the
+            // DMX-eliminated solve as a dead branch it slowed that solve's 16 x 16 factor)
+            bool ok = (SMALLK && K - 16 * k <= 8) ? diag_factor<8>(A + lblk(k, k), lane)
+                                                 : diag_factor<16>(A + lblk(k, k), lane);
             if (!ok && lane == 0) *sflag = 1;
         }
         if (k == 0) TS(10);
@@ -2925,7 +2928,7 @@ __global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const Psr
     for (int j = tid; j < nb * 16; j += NW * 64) bv[j] = j < K ? G(j, Kfull) * inv[j] : 0.0;
     const double rwr = G(Kfull, Kfull);
     bsync<NW>();
-    if (!blk_cholinv<NW>(A, nb, wave, lane, &sflag, K)) {
+    if (!blk_cholinv<NW, true>(A, nb, wave, lane, &sflag, K)) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         return;
     }
