@@ -393,7 +393,7 @@ def _timed(s, steps, warmup, barrier, max_over_ranks, graph, gram_pass, run, ste
     kt, nk = 0.0, 0
     if gram_pass:
         s.set_timing_mask(1 << SLOT_GRAM)
-        kt, nk = run(max(2 * GRAM_EVERY, steps // 2), step)
+        kt, nk = run(max(8 * GRAM_EVERY, steps // 2), step)  # (>= 8 sampled launches)
         s.set_timing_mask(0)
     return dt, kt, nk, step, ("hip-graph" if use_graph else "direct")
 
@@ -531,7 +531,7 @@ def load_json(name):
     return None
 
 
-PROFILE_ROUNDS = ("r04", "r03", "r02")  # newest first: the committed PMC summaries of this workload
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: the committed PMC summaries of this workload
 
 
 def pmc_value(stem, kernel, key, args):
@@ -592,12 +592,44 @@ def grid_leg(side, dist, barrier, max_over_ranks):
 
 
 def grid_roofline(kt, lay, npts, dt):
-    """Roofline record of the grid step's kernels: per-kernel event times of
-    one grid and the dominant kernel against its bound."""
+    """Roofline record of the grid step's dominant kernel.
+
+    The grid's points share one pulsar's TOAs, so a launch's algorithmic bytes are the TOA
+    inputs once ((n+1) x 116 B, then L2-resident) plus every point's own outputs: with M
+    (k_eval_M) (n+1) x 32 B (phase hi/lo, Taylor F, delay) + n x 8 K B (the design matrix);
+    without M the 32 B rows; the residual passes 80 B per point row; the Gram 8 (K+1) B per
+    row read.  None of them reaches HBM speed: the evaluation is bound by its FP64 VALU issue
+    (pmc_valu_busy from the committed PMC summary of this grid, profiles/pmc_grid_rNN.json)."""
     names = ["k_eval", "k_resid", "gram_span", "k_solve", "k_eval_M", "k_woodbury", "k_gram", "k_greduce"]
     kms = {n: round(float(v), 4) for n, v in zip(names, kt)}
-    return {"kernel_ms": kms, "grid_ms": round(dt * 1e3, 3), "points": npts, "rows_per_point": lay.n,
+    n, K = lay.n, lay.K
+    nbytes = {"k_eval_M": (n + 1) * 116.0 + npts * ((n + 1) * 32.0 + n * 8.0 * K),
+              "k_eval": (n + 1) * 116.0 + npts * (n + 1) * 32.0,
+              "k_resid": npts * n * 80.0,
+              "k_gram": npts * n * 8.0 * (K + 1)}
+    dom = max(nbytes, key=lambda k: kms.get(k, 0.0))
+    t = kms[dom] * 1e-3
+    ach = nbytes[dom] / t / 1e9 if t > 0 else None
+    traffic, src = pmc_grid(dom, "hbm_bytes")
+    valu, _ = pmc_grid(dom, "valu_busy_frac")
+    return {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": MI355X_HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / MI355X_HBM_PEAK_GBS, 4) if ach else None,
+            "traffic": traffic, "traffic_source": src, "alg_bytes_per_launch": nbytes[dom],
+            "pmc_valu_busy_frac": valu,
+            "per_kernel": {k: {"GB/s": round(b / (kms[k] * 1e-3) / 1e9, 1)} for k, b in nbytes.items() if kms.get(k, 0) > 0},
+            "kernel_ms": kms, "grid_ms": round(dt * 1e3, 3), "points": npts, "rows_per_point": n, "K": K,
             "kernel_ms_source": "HIP events of every timing slot on one more grid after the timed grids"}
+
+
+def pmc_grid(kernel, key):
+    """A per-launch PMC figure of the NGC6440E 256x256 grid's kernel from the newest
+    profiles/pmc_grid_rNN.json (scripts/gpu_prof.sh + scripts/pmc_grid_summary.py)."""
+    for r in PROFILE_ROUNDS:
+        d = load_json(f"pmc_grid_{r}.json")
+        k = (d or {}).get("kernels", {}).get(kernel)
+        if k is not None and k.get(key) is not None:
+            return k[key], f"pmc_grid_{r}.json"
+    return None, None
 
 
 def j0740_data():

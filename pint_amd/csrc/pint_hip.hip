@@ -1056,14 +1056,16 @@ __global__ __launch_bounds__(256) void k_gram_s(const PsrDev* __restrict__ psrs,
             }
         }
     }
+    // only the (K+1) x (K+1) entries the solves read (a 62-row grid point's 16 x 16 tile was
+    // 2 KB of writes, ~90 % padding)
     double* G = Gpart + I.goff + (long)split * Kp * Kp;
 #pragma unroll
     for (int e = 0; e < 4; e++) {  // D[row = lane / 16 + 4 e][col = lane % 16]
         const int row = kr + 4 * e;
-        G[(long)row * Kp + c0] = a00[e];
+        if (row <= K && c0 <= K) G[(long)row * Kp + c0] = a00[e];
         if (two) {
-            G[(long)row * Kp + c1] = a01[e];
-            G[(long)(row + 16) * Kp + c1] = a11[e];
+            if (row <= K && c1 <= K) G[(long)row * Kp + c1] = a01[e];
+            if (row + 16 <= K && c1 <= K) G[(long)(row + 16) * Kp + c1] = a11[e];
         }
     }
     // column sums of squares: the four lanes of a column (kr = 0..3) summed in a fixed order
