@@ -1404,13 +1404,25 @@ __device__ __forceinline__ void vb_flush(double4_t& acc, double* __restrict__ ds
         }                                                                                            \
     } while (0)
 
+// The pre-fit residual pass folded into the Gram (k_gram_v's staging forms r itself): with
+// `on`, the evaluation with the fit layout ran k_resid1 only, and wave 0 stages
+// r = (p - mean) / F from k_resid1's phase residual p, the Taylor factor F and the weighted
+// mean of the instance's block sums -- the same operations, in the same order, as k_resid2
+// (whose launch is deferred to the first reader of the time residuals, pint_* flush_r2).
+struct GvResid {
+    const double* rph;    // k_resid1's phase residuals (output rows)
+    const double* ftay;   // Taylor factors (n + 1 rows per instance)
+    const double* rpart;  // residual blocks' (sum w, sum w x, -)
+    int on;
+};
+
 template <int NTR, int NTC, int NSK, bool VB>
 __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restrict__ psrs,
                                             const InstDev* __restrict__ insts, const double* __restrict__ M,
                                             const double* __restrict__ rtime, const double* __restrict__ dmxv,
                                             int nsplit, double* __restrict__ Gpart, double* __restrict__ Sdp,
                                             double* __restrict__ colsq, double* __restrict__ TSp,
-                                            double* __restrict__ BFp, int dbg) {
+                                            double* __restrict__ BFp, int dbg, GvResid R) {
     constexpr int NTH = GW * 64;
     constexpr int CH = VCH;
     constexpr int CS = CH + 2;  // column stride (= 2 mod 32 doubles)
@@ -1447,6 +1459,22 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     const double* xv = dmxv + I.ooff;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // (R.on) the weighted mean of the phase residuals, summed as k_resid2 sums it: partial k
+    // of the instance's nrb <= 64 blocks on lane k of one wave, the same shuffle tree
+    const bool fr = R.on != 0;
+    const double* rpi = fr ? R.rph + I.ooff : ri;
+    const double* fti = R.ftay + I.roff;
+    double mean_r = 0.0;
+    if (fr && wave == 0) {
+        double a = 0.0, b = 0.0;
+        if (lane < I.nrb) {
+            b = R.rpart[3 * (I.rb0 + lane)];
+            a = R.rpart[3 * (I.rb0 + lane) + 1];
+        }
+        a = 0.0 + wave_sum(a);
+        b = 0.0 + wave_sum(b);
+        if (Pd.spec->subtract_mean) mean_r = a / b;
+    }
     double4_t acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = (double4_t){0, 0, 0, 0};
@@ -1454,7 +1482,7 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
 #pragma unroll
     for (int q = 0; q < QL; q++) csq[q] = 0.0;
     int sp0 = -1, sp1 = -1;  // per buffer: the slot column of this lane's row of two chunks ago
-    double w_n = 0.0, r_n = 0.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, c8_n = 1.0, s8_n = 0.0;
+    double w_n = 0.0, r_n = 0.0, f_n = 1.0, x_n = 0.0, c1_n = 1.0, s1_n = 0.0, c8_n = 1.0, s8_n = 0.0;
     double st[QL] = {};
     int d_n = -1;
     bool ok_n = false;
@@ -1485,7 +1513,8 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
         // which also count against lgkmcnt, so every LDS wait would wait for them too)
         w_n = ok_n ? ((gptr<double>)Pd.isig)[row] : 0.0;  // rows past the split weigh 0
         if (W == 0) {
-            r_n = ri[row];
+            r_n = rpi[row];  // (fr: the phase residual; its time residual is formed at the stage)
+            if (fr) f_n = fti[row];
             x_n = xv[row];
             sl_n = ((gptr<int>)Pd.dslot)[row];
         }
@@ -1521,7 +1550,8 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
         }
         if (W == 0) {  // residual and DMX slot entry (wave 0's share)
             const int sl = ok_n ? sl_n : -1;
-            put(Ts, r0, r_n * iw);
+            const double rr = fr ? (r_n - mean_r) / f_n : r_n;  // (k_resid2: p = lr - mean; rt = p / lf)
+            put(Ts, r0, rr * iw);
             put(Ts, vsel(sp >= 0, s0 + sp, DUM), 0.0);
             put(Ts, vsel(sl >= 0, s0 + sl, DUM), x_n * iw);
             sp = sl;
@@ -1745,12 +1775,12 @@ __device__ __forceinline__ void gram_v_nsk(double* lds, const PsrDev* __restrict
                                            const double* __restrict__ M, const double* __restrict__ rtime,
                                            const double* __restrict__ dmxv, int nsplit, double* __restrict__ Gpart,
                                            double* __restrict__ Sdp, double* __restrict__ colsq, double* __restrict__ TSp,
-                                           double* __restrict__ BFp, int dbg, int nsk) {
+                                           double* __restrict__ BFp, int dbg, int nsk, GvResid R) {
     if (nsk <= 0) {  // no all-slot row tile: VB would add a tile and remove none (PsrDev::vb = 0)
-        gram_v_body<NTR, NTC, 0, false>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
+        gram_v_body<NTR, NTC, 0, false>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, R);
     } else if constexpr (NTR >= 2) {
-        if (nsk == 1) gram_v_body<NTR, NTC, 1, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
-        else if constexpr (NTR >= 3) gram_v_body<NTR, NTC, 2, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg);
+        if (nsk == 1) gram_v_body<NTR, NTC, 1, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, R);
+        else if constexpr (NTR >= 3) gram_v_body<NTR, NTC, 2, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, R);
     }
 }
 
@@ -1760,12 +1790,12 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
                                                     const double* __restrict__ dmxv, int nsplit,
                                                     double* __restrict__ Gpart, double* __restrict__ Sdp,
                                                     double* __restrict__ colsq, double* __restrict__ TSp,
-                                                    double* __restrict__ BFp, int dbg) {
+                                                    double* __restrict__ BFp, int dbg, GvResid R) {
     extern __shared__ double lds[];
     const PsrDev& Pd = psrs[insts[blockIdx.y].psr];
     const int nsk = __builtin_amdgcn_readfirstlane(NTR - (Pd.red0c + 1 + 15) / 16);
     if constexpr (!VB || NTC <= 6)
-        gram_v_nsk<NTR, NTC, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, nsk);
+        gram_v_nsk<NTR, NTC, VB>(lds, psrs, insts, M, rtime, dmxv, nsplit, Gpart, Sdp, colsq, TSp, BFp, dbg, nsk, R);
 }
 
 // k_dm_resid: WidebandDMResiduals (residuals.py:1000-1031) of an instance, one workgroup per
@@ -4698,6 +4728,8 @@ struct pint_ctx {
     int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
     int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
     int maxn = 0;        // the batch's largest instance (rows)
+    int fuse_r2 = 1;     // PINT_FUSE_R2: the fit layout's k_resid2 folded into k_gram_v's staging
+    bool r2_pending = false;  // k_resid2 of the last pass deferred (the Gram formed its residuals)
     bool grid_valid = false;  // the batch is pint_set_grid's: grid_psr's points, options grid_opts
     int grid_psr = -1;
     long grid_opts = 0;
@@ -5264,6 +5296,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->eval_wpe = getenv("PINT_EVAL_WPE") ? atoi(getenv("PINT_EVAL_WPE")) : 3;
     ctx->gv_pair = getenv("PINT_GV_PAIR") ? atoi(getenv("PINT_GV_PAIR")) : 1;
     ctx->schur = getenv("PINT_SCHUR") ? atoi(getenv("PINT_SCHUR")) : 1;
+    ctx->fuse_r2 = getenv("PINT_FUSE_R2") ? atoi(getenv("PINT_FUSE_R2")) : 1;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
@@ -5735,6 +5768,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
 static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
     ctx->grid_valid = false;  // (pint_set_grid marks its own batch afterwards)
+    ctx->r2_pending = false;
     hipSetDevice(ctx->device);
     if (ctx->psrs_dirty && refresh_psrs(ctx)) return PINT_E_HIP;
     if (flush_setup(ctx)) return PINT_E_HIP;  // the uploads' red-noise set-up, one batch
@@ -6259,10 +6293,40 @@ static int decode_status(pint_ctx* ctx, int st) {
 }
 
 // Evaluate phases/delays (+ design matrix) and residuals for every instance.
+// k_resid2 of the last residual pass (with wt, the Woodbury trig tiles)
+static void launch_resid2(pint_ctx* ctx, bool wt) {
+    const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
+    if (ctx->small && ctx->maxn <= RES_SMALLN)
+        hipLaunchKernelGGL(k_resid2<64>, dim3((ctx->nrblk + 3) / 4), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
+                           wt ? ctx->d_wtile : nullptr);
+    else
+        hipLaunchKernelGGL(k_resid2<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
+                           wt ? ctx->d_wtile : nullptr);
+}
+
+// The fit layout's residual pass may leave k_resid2 to the Gram (GvResid) when every instance
+// takes k_gram_v and nothing else of the fit step reads the time residuals: no ECORR epochs
+// (k_ecorr), no wideband rows (k_wb_gram), and <= 64 residual blocks per instance (the mean
+// summed on one wave as k_resid2 sums it).  PINT_FUSE_R2=0 keeps k_resid2 in the pass.
+static bool can_defer_r2(const pint_ctx* ctx) {
+    return ctx->fuse_r2 && ctx->m_compact && ctx->n_vg == ctx->ninst && ctx->max_nep == 0 && !ctx->wbfit &&
+           ctx->maxn <= 64 * RES_RB;
+}
+
+// a reader of the time/phase residuals or their chi2 partials after a deferred pass
+static void flush_r2(pint_ctx* ctx) {
+    if (!ctx->r2_pending) return;
+    ctx->r2_pending = false;
+    launch_resid2(ctx, false);
+}
+
 int pint_eval(pint_ctx* ctx, int want_M) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     if (want_M < 0 || want_M > 2) return PINT_E_INVALID;
+    ctx->r2_pending = false;  // (this pass replaces the residuals a deferred k_resid2 would form)
     if (want_M) ctx->m_compact = (want_M == 2) ? 1 : 0;
     // the full and compact layouts place the red-noise columns differently; each is written
     // once after pint_set_instances (M is reallocated there)
@@ -6369,21 +6433,20 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
         // (256-row blocks for small batches were measured: resid1 faster, resid2 and k_wsolve's
         // longer tile sums slower, the step ~1.4 us slower at 9 pulsars)
+        // the fit layout's pass on the k_gram_v path: k_resid1 only, the Gram stages the time
+        // residuals itself and k_resid2 waits for a reader of them (flush_r2)
+        const bool defer2 = want_M == 2 && can_defer_r2(ctx);
         if (ctx->small && ctx->maxn <= RES_SMALLN) {  // a wave per residual block
             const int nb4 = (ctx->nrblk + 3) / 4;
             hipLaunchKernelGGL(k_resid1<64>, dim3(nb4), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
-            hipLaunchKernelGGL(k_resid2<64>, dim3(nb4), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
-                               wt ? ctx->d_wtile : nullptr);
         } else {
             hipLaunchKernelGGL(k_resid1<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs,
                                ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_rp,
                                ctx->d_rpart);
-            hipLaunchKernelGGL(k_resid2<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
-                               ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp,
-                               ctx->d_rpart, wt ? ctx->d_wtile : nullptr);
         }
+        if (defer2) ctx->r2_pending = true;
+        else launch_resid2(ctx, wt);
         // the chi2 partials are summed when the chi2 is read (pint_read_resids) or by k_wsolve,
         // which needs them anyway: no launch of its own in a fit step
         ctx->chi2_pending = true;
@@ -6398,6 +6461,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
 }
 
 int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, double* chi2) {
+    flush_r2(ctx);
     if (chi2 && ctx->chi2_pending) {
         hipLaunchKernelGGL(k_rsum, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_inst, ctx->d_rpart, ctx->d_chi2);
         HIPCHK(hipGetLastError());
@@ -6481,6 +6545,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     // deferred reads of this slot's outputs enqueued since the last step_end go first (this
     // solve rewrites them)
     if (int rc = flush_cq_now(ctx)) return rc;
+    if (ctx->r2_pending && !can_defer_r2(ctx)) flush_r2(ctx);  // (a kernel below reads d_rt)
+    const GvResid gvr{ctx->d_rp, ctx->d_ftay, ctx->d_rpart, ctx->r2_pending ? 1 : 0};
     if (ctx->wbfit) {
         // k_wb_gram carries at most WB_MAXC free DM-type columns (DM Taylor terms + DMJUMPs):
         // refuse more instead of leaving the extra columns without their DM rows
@@ -6620,12 +6686,12 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 hipExtLaunchKernelGGL((k_gram_v<R_, C_, true>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, \
                                       0u, (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M,                    \
                                       (const double*)ctx->d_rt, (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G,     \
-                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg);                   \
+                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg, gvr);              \
             else                                                                                                     \
                 hipExtLaunchKernelGGL((k_gram_v<R_, C_, false>), grid, dim3(GW * 64), (uint32_t)lds, ctx->stream, e0, e1, \
                                       0u, (const PsrDev*)ctx->d_psrs, di, (const double*)ctx->d_M,                    \
                                       (const double*)ctx->d_rt, (const double*)ctx->d_dmxv, ctx->nsplit, ctx->d_G,     \
-                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg)
+                                      ctx->d_Sdp, ctx->d_colsq, ctx->d_TSp, ctx->d_BFp, ctx->gvdbg, gvr)
             switch (kg.T) {
                 case 1: PINT_GRAMV(1, 1); break;
                 case 2: PINT_GRAMV(1, 2); break;
@@ -7074,6 +7140,7 @@ static int flush_restore(pint_ctx* ctx) {
 // Woodbury GLS chi2 of the current residuals; requires a previous pint_fit_step(mode=1)
 // (Sigma factor) and the red-noise columns of the last design matrix.
 int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
+    flush_r2(ctx);
     if (flush_chi2(ctx)) return PINT_E_HIP;
     int R = 0;
     for (auto& I : ctx->inst) R = 2 * ctx->psrs[I.psr].spec.nred > R ? 2 * ctx->psrs[I.psr].spec.nred : R;
@@ -7120,6 +7187,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
 // WLS chi2 of the current residuals, per instance (k_chi2w); the chi2 that pint_read_resids
 // reports comes from the residual pass itself, this one from whatever d_rt holds now.
 int pint_chi2_wls(pint_ctx* ctx, double* chi2) {
+    flush_r2(ctx);
     if (!ctx || ctx->ninst <= 0 || !chi2) return PINT_E_INVALID;
     if (flush_chi2(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
@@ -7607,6 +7675,7 @@ int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
 // caller's, e.g. the reference's own residual arrays, so that pint_fit_step / pint_chi2_gls
 // run on them (SURVEY.md 8(a) stage-wise parity).
 int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
+    flush_r2(ctx);  // (its rpart partials and phases first; the time residuals are replaced below)
     if (!ctx || ctx->ninst <= 0 || !time_resid) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
@@ -7700,6 +7769,7 @@ int pint_set_noise_classes(pint_ctx* ctx, int psr, int ncls, const int32_t* cls_
 
 int pint_noise_lnlike(pint_ctx* ctx, const int32_t* kind, const double* cls_qf, const double* ep_w, double* out3,
                       double* cls_g, double* ep_g) {
+    flush_r2(ctx);
     if (!ctx || ctx->ninst <= 0 || !kind || !cls_qf || !out3) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
     const int ni = ctx->ninst;

@@ -1314,3 +1314,33 @@ def test_single_model_batch_eval_matches_merged(monkeypatch):
         np.testing.assert_array_equal(x, y)
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_prefit_resid2_folded_into_gram(monkeypatch):
+    """The fit layout's k_resid2 left to k_gram_v's staging (r = (p - mean) / F formed there,
+    k_resid2 deferred to the first reader): the step, errors, covariance and linearised chi2
+    equal PINT_FUSE_R2=0's bit for bit, and so do the pre-fit residuals and chi2 read after
+    the step (the deferred k_resid2 runs at the read)."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+
+    def run(fuse):
+        monkeypatch.setenv("PINT_FUSE_R2", str(fuse))
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        assert s.n_vgram() == len(items)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(1)
+        dp, er, cov, cl = s.read_step()
+        out = [x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov] + [np.array(cl, copy=True)]
+        tr, pr, c2 = s.read_resids()
+        out += [np.concatenate(tr).copy(), np.concatenate(pr).copy(), np.array(c2, copy=True)]
+        s.close()
+        return out
+
+    a, b = run(1), run(0)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
