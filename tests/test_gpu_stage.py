@@ -443,6 +443,26 @@ def test_resident_grid_batch_matches_fresh(name, fitter):
     np.testing.assert_array_equal(e_res["DM"], e_new["DM"])
 
 
+def test_chunked_grid_matches_one_batch(monkeypatch):
+    """A grid fitted in equal chunks (the resident batch re-bound per chunk: pint_set_grid's
+    fast path) and a last smaller one (a fresh set-up) equals the same grid as one batch, bit
+    for bit (62-row points: one N-split whatever the batch size)."""
+    from pint_amd import WLSFitter, gridutils
+    from pint_amd.gridutils import grid_chisq
+    model, toas = load("ngc6440e")[:2]
+    f = WLSFitter(toas, copy.deepcopy(model))
+    f.fit_toas(maxiter=1)
+    F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+    g = (F0 + np.linspace(-2, 2, 6) * np.longdouble(f.model.F0.uncertainty),
+         F1 + np.linspace(-2, 2, 5) * np.longdouble(f.model.F1.uncertainty))
+    gridutils._drop_grid_session()
+    c_one, e_one = grid_chisq(f, ("F0", "F1"), g, extraparnames=["DM"])
+    monkeypatch.setattr(gridutils, "GRID_MAX_POINTS", 7)  # 30 points: 7, 7, 7, 7, 2
+    c_ch, e_ch = grid_chisq(f, ("F0", "F1"), g, extraparnames=["DM"])
+    np.testing.assert_array_equal(c_ch, c_one)
+    np.testing.assert_array_equal(e_ch["DM"], e_one["DM"])
+
+
 def test_invalid_grid_point_fails_alone():
     """A grid over the DD eccentricity that includes ECC >= 1: those points are NaN (the
     reference's doonefit returns NaN for the failed fit, gridutils.py:89-106) and every other
