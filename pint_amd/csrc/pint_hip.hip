@@ -413,8 +413,9 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
 
 // k_eval: one thread per TOA row; one launch per binary model (blocks of the isolated,
 // ELL1 or DD instances), so each instantiation carries only its own registers.
-template <int WANT_M, int BIN>
-__global__ __launch_bounds__(256) void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+template <int WANT_M, int BIN, int W = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1, W > 0 ? W : 10)))
+void k_eval(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                               const int* __restrict__ blk_inst, const int* __restrict__ blk_row0,
                                               const double* __restrict__ tables, const InstConst* __restrict__ ic,
                                               double* __restrict__ ph_hi, double* __restrict__ ph_lo,
@@ -4735,6 +4736,7 @@ struct pint_ctx {
     long grid_opts = 0;
     int small = 1;       // PINT_OPT_SMALL: k_gram_s / one-wave k_solve_blk for small instances
     int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
+    int eval0_wpe = 1;   // PINT_EVAL0_WPE: the isolated-model build at fixed register budgets (0: the compiler's)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
     int n_vg = 0;        // instances on the k_gram_v path
@@ -5297,6 +5299,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->gv_pair = getenv("PINT_GV_PAIR") ? atoi(getenv("PINT_GV_PAIR")) : 1;
     ctx->schur = getenv("PINT_SCHUR") ? atoi(getenv("PINT_SCHUR")) : 1;
     ctx->fuse_r2 = getenv("PINT_FUSE_R2") ? atoi(getenv("PINT_FUSE_R2")) : 1;
+    ctx->eval0_wpe = getenv("PINT_EVAL0_WPE") ? atoi(getenv("PINT_EVAL0_WPE")) : 1;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
@@ -6398,11 +6401,17 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         if (nb == 0) continue;
         const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
         const int* br = ctx->d_blk_row0 + ctx->blk_off[t];
-#define PINT_EVAL_LAUNCH(WM, BT)                                                                          \
-        hipLaunchKernelGGL((k_eval<WM, BT>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
+#define PINT_EVAL_LAUNCH(WM, BT, ...)                                                                     \
+        hipLaunchKernelGGL((k_eval<WM, BT, ##__VA_ARGS__>), dim3(nb), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, bi, br, \
                            tabs, icp, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay, ctx->d_M, \
                            ctx->d_dmxv, want_M == 2 ? 1 : 0, write_red, ctx->d_status, ctx->d_istatus, ctx->d_dfac, rs)
-        if (want_M) {
+        // the isolated build at a register budget of 6 waves/SIMD with M (80 VGPRs, no spills:
+        // 0.28 vs 0.31 ms on the 65,536-point NGC6440E grid) and 8 without (64 VGPRs, 36 B of
+        // spills: 0.143 vs 0.162 ms); 8 with M spilled 76 B and lost (0.35 ms).
+        // PINT_EVAL0_WPE=0: the compiler's own allocation (84 / 74 VGPRs, 5 / 6 waves)
+        if (t == 0 && ctx->eval0_wpe) {
+            if (want_M) PINT_EVAL_LAUNCH(1, 0, 6); else PINT_EVAL_LAUNCH(0, 0, 8);
+        } else if (want_M) {
             switch (t) {
                 case 0: PINT_EVAL_LAUNCH(1, 0); break;
                 case 1: PINT_EVAL_LAUNCH(1, 1); break;

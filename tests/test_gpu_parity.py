@@ -1344,3 +1344,28 @@ def test_prefit_resid2_folded_into_gram(monkeypatch):
     assert len(a) == len(b)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_isolated_eval_register_budgets_match(monkeypatch):
+    """The isolated model's evaluation at fixed register budgets (6 waves/SIMD with M, 8
+    without; PINT_EVAL0_WPE) against the compiler's own allocation: phases, delays, Taylor
+    factors and the design matrix bit for bit (the same code, other registers and spills)."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load("ngc6440e")[:2]] * 3 + [load("pta_iso")[:2]]
+
+    def run(w):
+        monkeypatch.setenv("PINT_EVAL0_WPE", str(w))
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.eval(want_M=True)
+        ev = [np.concatenate(x).copy() for x in s.read_eval()]
+        M = [x.copy() for x in s.read_designmatrix()]
+        s.eval(want_M=False)
+        ev0 = [np.concatenate(x).copy() for x in s.read_eval()]
+        s.close()
+        return ev + M + ev0
+
+    for x, y in zip(run(1), run(0)):
+        np.testing.assert_array_equal(x, y)
