@@ -4736,6 +4736,7 @@ struct pint_ctx {
     long grid_opts = 0;
     int small = 1;       // PINT_OPT_SMALL: k_gram_s / one-wave k_solve_blk for small instances
     int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
+    int evalb_wpe = 3;   // PINT_EVALB_WPE: one-model ELL1/DD batches with M at 3 waves/SIMD (0: the compiler's)
     int eval0_wpe = 1;   // PINT_EVAL0_WPE: the isolated-model build at fixed register budgets (0: the compiler's)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
@@ -5300,6 +5301,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->schur = getenv("PINT_SCHUR") ? atoi(getenv("PINT_SCHUR")) : 1;
     ctx->fuse_r2 = getenv("PINT_FUSE_R2") ? atoi(getenv("PINT_FUSE_R2")) : 1;
     ctx->eval0_wpe = getenv("PINT_EVAL0_WPE") ? atoi(getenv("PINT_EVAL0_WPE")) : 1;
+    ctx->evalb_wpe = getenv("PINT_EVALB_WPE") ? atoi(getenv("PINT_EVALB_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
@@ -6411,6 +6413,10 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         // PINT_EVAL0_WPE=0: the compiler's own allocation (84 / 74 VGPRs, 5 / 6 waves)
         if (t == 0 && ctx->eval0_wpe) {
             if (want_M) PINT_EVAL_LAUNCH(1, 0, 6); else PINT_EVAL_LAUNCH(0, 0, 8);
+        } else if (want_M && (t == 1 || t == 2) && ctx->evalb_wpe == 3 && nb > 2 * 256) {
+            // a large one-model ELL1 or DD batch (a J0740 grid) with M at the merged build's
+            // budget of 3 waves/SIMD (168 VGPRs + spills) instead of 2 (174 / 202 VGPRs)
+            if (t == 1) PINT_EVAL_LAUNCH(1, 1, 3); else PINT_EVAL_LAUNCH(1, 2, 3);
         } else if (want_M) {
             switch (t) {
                 case 0: PINT_EVAL_LAUNCH(1, 0); break;

@@ -1369,3 +1369,26 @@ def test_isolated_eval_register_budgets_match(monkeypatch):
 
     for x, y in zip(run(1), run(0)):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_large_one_model_batch_eval_budget_matches(monkeypatch):
+    """A large one-model ELL1 batch with M (14 x 10k J0740 rows: > 512 blocks) at the 3
+    waves/SIMD budget (PINT_EVALB_WPE=3, 168 VGPRs + spills) against the compiler's own 2-wave
+    allocation: phases, delays, Taylor factors and the design matrix bit for bit."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    m0, t0 = load("j0740_10k")[:2]
+
+    def run(w):
+        monkeypatch.setenv("PINT_EVALB_WPE", str(w))
+        s = Session()
+        lay = s.add(build_layout(m0, t0))
+        s.set_instances([(lay, pack_table(lay, m0))] * 14)
+        s.eval(want_M=True)
+        ev = [np.concatenate(x).copy() for x in s.read_eval()]
+        M = [x.copy() for x in s.read_designmatrix()]
+        s.close()
+        return ev + M
+
+    for x, y in zip(run(3), run(0)):
+        np.testing.assert_array_equal(x, y)
