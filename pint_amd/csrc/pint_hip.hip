@@ -2925,10 +2925,11 @@ __global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const Psr
     double* bv = A + nblk * 256;
     double* yv = bv + nb * 16;
     // per-instance vectors in global scratch (the LDS holds the factor and two vectors at
-    // nb = 12): reciprocal column norms, the normalised solution, the refinement residual
-    double* inv = rscr + (long)inst * RSCR;
-    double* xs = inv + RSCR / 4;
-    double* rv = xs + RSCR / 4;
+    // nb = 12): reciprocal column norms, the normalised solution, the refinement residual;
+    // the one-wave form (nb <= 2) keeps them in its LDS region too (no global round trips)
+    double* inv = NW == 1 ? yv + nb * 16 : rscr + (long)inst * RSCR;
+    double* xs = NW == 1 ? inv + nb * 16 : inv + RSCR / 4;
+    double* rv = NW == 1 ? xs + nb * 16 : xs + RSCR / 4;
     const bool cmp = compact && Pd.dsplit;
     const GramView G = gram_view(Pd, I, Gpart, cmp, Sd, DD);
     const int tid = NW == 1 ? (threadIdx.x & 63) : threadIdx.x, lane = tid & 63;
@@ -6894,15 +6895,16 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         // every instance went through k_solve_dmx
     } else if (nbx <= BS_MAXNB && ctx->blocked_solve) {
         const int ldsw = nbx * (nbx + 1) / 2 * 256 + 2 * 16 * nbx;  // doubles per instance
+        const int ldsw1 = ldsw + 3 * 16 * nbx;  // (+ the three scratch vectors: one-wave form)
         size_t lds_b = sizeof(double) * (size_t)ldsw;
         // K <= 32 (a grid's points): a wave per instance, four per workgroup -- the 4-wave
         // form spent ~27 us of barriers and idle waves on each such instance
         if (nbx <= 2 && ctx->small)
-            hipLaunchKernelGGL(k_solve_blk<1>, dim3((ctx->ninst + 3) / 4), dim3(256), 4 * lds_b, ctx->stream,
-                               ctx->d_psrs, ctx->d_inst, ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode,
-                               cmp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_dpars, ctx->d_errs, ctx->d_cov,
-                               ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine,
-                               ctx->ninst, ldsw);
+            hipLaunchKernelGGL(k_solve_blk<1>, dim3((ctx->ninst + 3) / 4), dim3(256), 4 * sizeof(double) * ldsw1,
+                               ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables, ctx->d_G, ctx->d_colsq,
+                               ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
+                               ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status, skip, ctx->d_rscr, ctx->refine,
+                               ctx->ninst, ldsw1);
         else if (nbx <= 5)
             hipLaunchKernelGGL(k_solve_blk<4>, dim3(ctx->ninst), dim3(256), lds_b, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_tables, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD,
