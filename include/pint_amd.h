@@ -281,7 +281,9 @@ int pint_check(pint_ctx *ctx);
  * be per slot.  In lazy mode pint_read_step / pint_noise_resids(_dm) put their copy-stream
  * work behind the step's last kernel (at pint_step_end or pint_check), not behind the
  * solve. */
-#define PINT_NSLOT 3
+#ifndef PINT_NSLOT
+#define PINT_NSLOT 4
+#endif
 int pint_step_end(pint_ctx *ctx, int *slot);
 /* One GLSFitter.fit_toas(maxiter=1) step of every instance (fitter.py:2164-2289: the GLS
  * step, full_cov=False noise realisations :2269-2282, the post-fit chi2 it returns) enqueued

@@ -15,7 +15,8 @@ LIBPATH = os.environ.get("PINT_LIB") or os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
 EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
-NSLOT = 3       # PINT_NSLOT: pipeline slots (pint_step_end / pint_check_step)
+NSLOT = int(os.environ.get("PINT_NSLOT", "4"))  # PINT_NSLOT: pipeline slots (pint_step_end / pint_check_step; a
+# library built with -DPINT_NSLOT=k needs the same k here)
 B_NPAR = 27
 BIN_NONE, BIN_ELL1, BIN_DD, BIN_ELL1H, BIN_BT, BIN_DDK = range(6)
 
