@@ -1,6 +1,6 @@
 #!/bin/bash
-# the chunked-grid test, then a two-rank rehearsal of the multi-rank bench on one GPU (gloo
-# collectives; not a scaling measurement)
+# the chunked-grid test, a two-rank rehearsal of the multi-rank bench on one GPU (gloo
+# collectives; not a scaling measurement), then 20-step runs after 5 and 100 warm-up steps
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
