@@ -4733,6 +4733,7 @@ struct pint_ctx {
     int fuse_r2 = 1;     // PINT_FUSE_R2: the fit layout's k_resid2 folded into k_gram_v's staging
     bool r2_pending = false;  // k_resid2 of the last pass deferred (the Gram formed its residuals)
     bool grid_valid = false;  // the batch is pint_set_grid's: grid_psr's points, options grid_opts
+    std::vector<double> grid_spec_host;  // pint_set_grid's spec, kept while its upload may run
     int grid_psr = -1;
     long grid_opts = 0;
     int small = 1;       // PINT_OPT_SMALL: k_gram_s / one-wave k_solve_blk for small instances
@@ -5748,7 +5749,10 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
     }
     // the spec: base table, then per variable (toff, stride, size, value offset) as doubles
     // (exact: all < 2^53), then the value pairs
-    std::vector<double> spec((size_t)ts + 4 * nvar + 2 * nv);
+    // (the spec stays in the context until the next pint_set_grid, which synchronises the
+    // streams before it is rewritten: no wait here for its upload)
+    std::vector<double>& spec = ctx->grid_spec_host;
+    spec.assign((size_t)ts + 4 * nvar + 2 * nv, 0.0);
     for (int i = 0; i < ts; i++) spec[i] = base[i];
     long vo = 0;
     for (int j = 0; j < nvar; j++) {
@@ -5760,6 +5764,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
         vo += var_size[j];
     }
     for (long i = 0; i < 2 * nv; i++) spec[ts + 4 * nvar + i] = vals[i];
+    dfree((void*&)ctx->d_gridspec);  // (the previous grid's: its tables were formed, the streams synchronised)
     HIPCHK(cmalloc((void**)&ctx->d_gridspec, sizeof(double) * spec.size()));
     HIPCHK(hipMemcpyAsync(ctx->d_gridspec, spec.data(), sizeof(double) * spec.size(), hipMemcpyHostToDevice, ctx->stream));
     const long total = (long)npts * ts;
@@ -5767,7 +5772,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
     hipLaunchKernelGGL(k_grid_tables, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_gridspec, ts, nvar, npts, (long)k0,
                        ctx->d_tables);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(ctx->stream));  // (spec is a host temporary)
+    if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 

@@ -168,9 +168,10 @@ def _fit_block_enqueued(s, lay, grid, mode, fitargs, want_tables):
     any point raised a status (an invalid point, a degenerate normal matrix)."""
     from . import _lib as L
     base, variables, npts, k0 = grid
-    bf = BatchFit(None, mode=mode, session=s, grid=(lay, base, variables, npts, k0))
     s.set_lazy(True)
     try:
+        # (lazy from the binding on: pint_set_grid then leaves its upload to the stream)
+        bf = BatchFit(None, mode=mode, session=s, grid=(lay, base, variables, npts, k0))
         for _ in range(fitargs.get("maxiter", 1)):
             s.eval(want_M=s.FIT)
             s.fit_step(1 if bf.gls else 0)
