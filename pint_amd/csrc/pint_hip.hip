@@ -2952,8 +2952,8 @@ __global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const Psr
         return v;
     };
     for (int e = tid; e < nblk * 256; e += NW * 64) {
-        int Ib, Jb;
-        tri_decode(e >> 8, Ib, Jb);
+        int Ib = 0, Jb = 0;
+        if (nblk > 1) tri_decode(e >> 8, Ib, Jb);  // (one block: no square root per element)
         const int r = e & 15, c = (e >> 4) & 15;
         const int gi = Ib * 16 + r, gj = Jb * 16 + c;
         const double v = (gi < K && gj < K) ? Aij(gi, gj) : (gi == gj ? 1.0 : 0.0);
