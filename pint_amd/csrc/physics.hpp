@@ -245,6 +245,74 @@ PD void inst_setup(const pint_spec_t& S, const double* P, InstConst& C) {
     C.has_pm = 1;
 }
 
+// inst_setup_wave's operations by one thread, in the same order (so the same values): the
+// lane-per-instance k_prep / k_apply of batches of small tables (grid points), where a wave
+// sets up 64 instances at once instead of one
+PD void inst_setup_seq(const pint_spec_t& S, const double* P, InstConst& C) {
+    if (S.astrometry != 1) {
+        inst_setup(S, P, C);
+        return;
+    }
+    double sx[12];
+    const double lon = pval(P, S.o_lon), lat = pval(P, S.o_lat);
+    const double pml = S.o_pmlon >= 0 ? pval(P, S.o_pmlon) : 0.0;
+    const double pmb = S.o_pmlat >= 0 ? pval(P, S.o_pmlat) : 0.0;
+    const double ra = lon * HA_RAD, dec = lat * DEG_RAD;
+    const bool pm = !(pml == 0.0 && pmb == 0.0);
+    const double pmd = pmb * MAS_RAD;
+    sx[0] = cos(ra);
+    sx[1] = sin(ra);
+    sx[2] = cos(dec);
+    sx[3] = sin(dec);
+    if (pm) {
+        sx[10] = cos(dec + pmd);
+        sx[11] = sin(dec + pmd);
+    }
+    if (S.binary && S.o_bin[PINT_B_PB] >= 0) {
+        dd ipb = dd_div(dd_make(1.0), dd_mul_d(pdd(P, S.o_bin[PINT_B_PB]), DAYSEC));
+        sx[4] = ipb.hi;
+        sx[5] = ipb.lo;
+    }
+    const double cd = sx[2];
+    const double pmr = pml * MAS_RAD / cd;
+    if (pm) {
+        const double ra2 = ra + pmr, d = ra2 - ra;
+        if (fabs(d) < 1e-2) {
+            const double d2 = d * d;
+            const double sd = d * (1.0 - d2 * (1.0 / 6.0 - d2 * (1.0 / 120.0 - d2 * (1.0 / 5040.0))));
+            const double cdl = 1.0 - d2 * (0.5 - d2 * (1.0 / 24.0 - d2 * (1.0 / 720.0 - d2 * (1.0 / 40320.0))));
+            sx[8] = sx[0] * cdl - sx[1] * sd;
+            sx[9] = sx[1] * cdl + sx[0] * sd;
+        } else {
+            sx[8] = cos(ra2);
+            sx[9] = sin(ra2);
+        }
+    }
+    C.F0 = pval(P, S.o_F);
+    C.iF0 = 1.0 / C.F0;
+    C.has_pm = 0;
+    C.posep = S.o_POSEPOCH >= 0 ? pval(P, S.o_POSEPOCH) : 0.0;
+    C.ipb_hi = C.ipb_lo = 0.0;
+    if (S.binary && S.o_bin[PINT_B_PB] >= 0) {
+        C.ipb_hi = sx[4];
+        C.ipb_lo = sx[5];
+    }
+    C.plon = ra;
+    C.plat = dec;
+    C.cplat = sx[2];
+    C.splat = sx[3];
+    C.cplon = sx[0];
+    C.splon = sx[1];
+    C.L0[0] = sx[0] * sx[2];
+    C.L0[1] = sx[1] * sx[2];
+    C.L0[2] = sx[3];
+    if (!pm) return;
+    const double px_as = (S.o_px >= 0 ? pval(P, S.o_px) : 0.0) * 1e-3;
+    const PmTrig T = {sx[0], sx[1], sx[2], sx[3], sx[8], sx[9], sx[10], sx[11]};
+    pm_setup_trig(pmr, pmd, px_as, T, C.pm);
+    C.has_pm = 1;
+}
+
 // inst_setup by the 64 lanes of one wave (k_prep, k_apply): the equatorial astrometry's
 // independent transcendental calls -- cos/sin of RA, DEC and the proper-motion-displaced DEC,
 // the double-double 1/PB -- on separate lanes, exchanged through

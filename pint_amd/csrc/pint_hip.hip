@@ -280,6 +280,52 @@ __device__ __forceinline__ void prep_one(const pint_spec_t* Sg, const double* Pg
     if (threadIdx.x == 0) *out = sC;
 }
 
+// k_prep / k_apply, lane per instance (PREP_LANES: batches whose tables all fit
+// PREP_LANE_TAB doubles, i.e. grid points of a small model): every thread sets up its own
+// instance with inst_setup_seq (inst_setup_wave's operations in one thread: the same values),
+// 64 instances per wave instead of one instance's serial code on one lane of a wave
+constexpr int PREP_LANE_TAB = 64;
+__global__ __launch_bounds__(64) void k_prep_lanes(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   int ninst, double* __restrict__ tables,
+                                                   const double* __restrict__ tables0, InstConst* __restrict__ ic) {
+    const int q = blockIdx.x * 64 + threadIdx.x;
+    if (q >= ninst) return;
+    const InstDev I = insts[q];
+    const pint_spec_t& S = *psrs[I.psr].spec;
+    const double* P = tables + I.toff;
+    if (tables0) {
+        const int ts = S.tstride;
+        for (int i = 0; i < ts; i++) tables[I.toff + i] = tables0[I.toff + i];
+        P = tables0 + I.toff;
+    }
+    InstConst C;
+    inst_setup_seq(S, P, C);
+    ic[q] = C;
+}
+__global__ __launch_bounds__(64) void k_apply_lanes(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    int ninst, double* __restrict__ tables,
+                                                    const double* __restrict__ dpars, const double* __restrict__ lam,
+                                                    InstConst* __restrict__ ic, double lam_u) {
+    const int q = blockIdx.x * 64 + threadIdx.x;
+    if (q >= ninst) return;
+    const InstDev I = insts[q];
+    const pint_spec_t& S = *psrs[I.psr].spec;
+    double* P = tables + I.toff;
+    const double li = lam ? lam[q] : lam_u;
+    if (li != 0.0) {  // (decided instances: a non-finite step must not touch them)
+        for (int c = 0; c < S.ncol; c++) {
+            const int o = S.col_toff[c];
+            if (o < 0) continue;
+            const dd v = dd_add_d(dd_make(P[o], P[o + 1]), li * dpars[I.coff + c]);
+            P[o] = v.hi;
+            P[o + 1] = v.lo;
+        }
+    }
+    InstConst C;
+    inst_setup_seq(S, P, C);
+    ic[q] = C;
+}
+
 // k_prep: the per-instance constants of the tables; with tables0 (pint_restore_tables
 // pending) the instance's table is first put back from the device snapshot, in the same
 // launch (the constants are formed from the snapshot, which is what the table then holds)
@@ -4730,6 +4776,8 @@ struct pint_ctx {
     int wbfit = 0;       // PINT_OPT_WBFIT: wideband DM rows in the fit step (k_wb_gram)
     int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
     int maxn = 0;        // the batch's largest instance (rows)
+    int max_ts = 0;      // the batch's largest parameter table (doubles)
+    int prep_lanes = 1;  // PINT_PREP_LANES: lane-per-instance k_prep / k_apply for small tables
     int fuse_r2 = 1;     // PINT_FUSE_R2: the fit layout's k_resid2 folded into k_gram_v's staging
     bool r2_pending = false;  // k_resid2 of the last pass deferred (the Gram formed its residuals)
     bool grid_valid = false;  // the batch is pint_set_grid's: grid_psr's points, options grid_opts
@@ -5303,6 +5351,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->schur = getenv("PINT_SCHUR") ? atoi(getenv("PINT_SCHUR")) : 1;
     ctx->fuse_r2 = getenv("PINT_FUSE_R2") ? atoi(getenv("PINT_FUSE_R2")) : 1;
     ctx->eval0_wpe = getenv("PINT_EVAL0_WPE") ? atoi(getenv("PINT_EVAL0_WPE")) : 1;
+    ctx->prep_lanes = getenv("PINT_PREP_LANES") ? atoi(getenv("PINT_PREP_LANES")) : 1;
     ctx->evalb_wpe = getenv("PINT_EVALB_WPE") ? atoi(getenv("PINT_EVALB_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
@@ -6025,7 +6074,11 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     ctx->tot_cv = cvoff;
     ctx->maxK = maxK;
     ctx->maxn = 0;
-    for (const InstDev& I : ctx->inst) ctx->maxn = std::max(ctx->maxn, I.n);
+    ctx->max_ts = 0;
+    for (const InstDev& I : ctx->inst) {
+        ctx->maxn = std::max(ctx->maxn, I.n);
+        ctx->max_ts = std::max(ctx->max_ts, ctx->psrs[I.psr].spec.tstride);
+    }
     ctx->tot_e = eoff;
     ctx->tot_ep = epoff;
     ctx->max_nep = max_nep;
@@ -6304,6 +6357,25 @@ static int decode_status(pint_ctx* ctx, int st) {
 }
 
 // Evaluate phases/delays (+ design matrix) and residuals for every instance.
+// k_prep / k_apply, or their lane-per-instance forms for a batch of small tables
+static bool prep_lanes(const pint_ctx* ctx) { return ctx->prep_lanes && ctx->max_ts <= PREP_LANE_TAB; }
+static void launch_prep(pint_ctx* ctx, double* tables, const double* tables0, InstConst* ic) {
+    if (prep_lanes(ctx))
+        hipLaunchKernelGGL(k_prep_lanes, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->ninst, tables, tables0, ic);
+    else
+        hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, tables,
+                           tables0, ic);
+}
+static void launch_apply(pint_ctx* ctx, const double* lam, double lam_u) {
+    if (prep_lanes(ctx))
+        hipLaunchKernelGGL(k_apply_lanes, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                           ctx->d_inst, ctx->ninst, ctx->d_tables, ctx->d_dpars, lam, ctx->d_ic, lam_u);
+    else
+        hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->d_tables, ctx->d_dpars, lam, ctx->d_ic, lam_u);
+}
+
 // k_resid2 of the last residual pass (with wt, the Woodbury trig tiles)
 static void launch_resid2(pint_ctx* ctx, bool wt) {
     const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
@@ -6364,8 +6436,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
             icp = ctx->d_ic0;
             rs = EvalRestore{ctx->d_tables, ctx->d_ic};
         } else {
-            hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                               ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
+            launch_prep(ctx, ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
             HIPCHK(hipGetLastError());
         }
         ctx->restore_pending = false;
@@ -7071,8 +7142,7 @@ int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
     if (flush_restore(ctx)) return PINT_E_HIP;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
-                       ctx->d_dpars, ctx->d_lam, ctx->d_ic, 0.0);
+    launch_apply(ctx, ctx->d_lam, 0.0);
     HIPCHK(hipGetLastError());
     ctx->ic_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -7085,8 +7155,7 @@ int pint_apply_step_uniform(pint_ctx* ctx, double lambda_) {
     if (!ctx || ctx->ninst <= 0) return PINT_E_INVALID;
     if (flush_restore(ctx)) return PINT_E_HIP;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
-    hipLaunchKernelGGL(k_apply, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables,
-                       ctx->d_dpars, (const double*)nullptr, ctx->d_ic, lambda_);
+    launch_apply(ctx, nullptr, lambda_);
     HIPCHK(hipGetLastError());
     ctx->ic_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -7130,8 +7199,7 @@ int pint_save_tables(pint_ctx* ctx) {
                           ctx->stream));
     // the snapshot's per-instance constants, so a restore needs no k_prep (pint_eval)
     if (!ctx->d_ic0) HIPCHK(cmalloc((void**)&ctx->d_ic0, sizeof(InstConst) * ctx->ninst));
-    hipLaunchKernelGGL(k_prep, dim3(ctx->ninst), dim3(PREP_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
-                       ctx->d_tables0, (const double*)nullptr, ctx->d_ic0);
+    launch_prep(ctx, ctx->d_tables0, nullptr, ctx->d_ic0);
     HIPCHK(hipGetLastError());
     ctx->ic0_valid = true;
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -1392,3 +1392,37 @@ def test_large_one_model_batch_eval_budget_matches(monkeypatch):
 
     for x, y in zip(run(3), run(0)):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ngc6440e", "white_mjd"])
+def test_lane_per_instance_setup_matches(monkeypatch, name):
+    """k_prep / k_apply with a lane per instance (PINT_PREP_LANES, tables of <= 64 doubles:
+    inst_setup_seq, inst_setup_wave's operations in one thread) against the one-wave-per-
+    instance kernels: the updated tables and the evaluations that read the constants, bit
+    for bit."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    m0, t0 = load(name)[:2]
+
+    def run(lanes):
+        monkeypatch.setenv("PINT_PREP_LANES", str(lanes))
+        s = Session()
+        lay = s.add(build_layout(m0, t0))
+        assert lay.tstride <= 64
+        tab = pack_table(lay, m0)
+        insts = []
+        for k in range(70):  # (two 64-instance waves)
+            tk = tab.copy()
+            tk[lay.offsets["F0"]] += (k - 35) * 1e-11
+            insts.append((lay, tk))
+        s.set_instances(insts)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(0)
+        s.apply_step_uniform(1.0)
+        s.eval(want_M=False)
+        out = [np.concatenate(x).copy() for x in s.read_eval()] + [s.read_tables_flat().copy()]
+        s.close()
+        return out
+
+    for x, y in zip(run(1), run(0)):
+        np.testing.assert_array_equal(x, y)
