@@ -721,6 +721,91 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     }
 }
 
+// k_resid12: k_resid1 and k_resid2 in one launch when every instance is one residual block
+// of <= 256 rows (a grid's points) and no trig tiles are formed: a wave per instance forms the
+// phase residuals, its weighted sums and -- from those sums, which are the instance's only
+// block partial, so k_resid2's read-back would give the same values -- the mean, the time
+// residuals and the chi2 partial, the phase residuals kept in registers in between.  The same
+// operations in the same order as the two kernels, so the same bits.
+__global__ __launch_bounds__(RES_BT) void k_resid12(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const int* __restrict__ rblk_inst, int nrblk,
+                                                    const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
+                                                    const double* __restrict__ ftay, double* __restrict__ rtime,
+                                                    double* __restrict__ rphase, double* __restrict__ rpart) {
+    const int rb = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (rb >= nrblk) return;  // (wave-uniform)
+    const int tid = threadIdx.x & 63;
+    const int ii = rblk_inst[rb];
+    const InstDev I = insts[ii];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int n = I.n;
+    const long ro = I.roff;
+    const long oo = I.roff - ii;
+    const int r0 = (int)(rb - I.rb0) * RES_RB;
+    const int r1 = min(n, r0 + RES_RB);
+    const dd tz = dd_make(ph_hi[ro + n], ph_lo[ro + n]);
+    dd d0 = dd_make(0.0);
+    if (!S.track_pn && S.subtract_mean) d0 = dd_add_d(dd_sub(dd_make(ph_hi[ro], ph_lo[ro]), tz), Pd.dpn[0]);
+    double sw = 0.0, swx = 0.0;
+    double lh[RES_RPT], ll[RES_RPT], lp[RES_RPT], lpn[RES_RPT], lw[RES_RPT], lf[RES_RPT], ls[RES_RPT], full[RES_RPT];
+#pragma unroll
+    for (int u = 0; u < RES_RPT; u++) {
+        const int i = r0 + tid + u * 64;
+        const bool in = i < r1;
+        lh[u] = in ? ph_hi[ro + i] : 0.0;
+        ll[u] = in ? ph_lo[ro + i] : 0.0;
+        lp[u] = in ? Pd.dpn[i] : 0.0;
+        lpn[u] = (in && S.track_pn) ? Pd.pn[i] : 0.0;
+        lw[u] = (in && S.weighted_mean) ? Pd.isig[i] : 1.0;
+        lf[u] = in ? ftay[ro + i] : 1.0;
+        ls[u] = in ? Pd.isig[i] : 0.0;
+        full[u] = 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RES_RPT; u++) {  // (k_resid1)
+        const int i = r0 + tid + u * 64;
+        if (i >= r1) break;
+        dd d = dd_add_d(dd_sub(dd_make(lh[u], ll[u]), tz), lp[u]);
+        if (S.track_pn) {
+            full[u] = dd_to_d(dd_add_d(d, -lpn[u]));
+        } else {
+            dd x = dd_sub(d, d0);
+            full[u] = dd_to_d(dd_sub(x, dd_round_half_up(x)));
+        }
+        double w = S.weighted_mean ? lw[u] * lw[u] : 1.0;
+        sw += w;
+        swx += w * full[u];
+    }
+    double mean = 0.0;
+    if (S.subtract_mean) {
+        double v[2] = {swx, sw};
+        block_sums<1, 2>(v, nullptr);
+        if (tid == 0) {
+            rpart[3 * rb] = v[1];
+            rpart[3 * rb + 1] = v[0];
+        }
+        // (k_resid2: 0.0 + each partial, the wave's sum of the one partial, 0.0 + that)
+        const double a = 0.0 + (0.0 + v[0]), b = 0.0 + (0.0 + v[1]);
+        mean = a / b;
+    }
+    double c2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < RES_RPT; u++) {  // (k_resid2)
+        const int i = r0 + tid + u * 64;
+        if (i < r1) {
+            double p = full[u] - mean;
+            rphase[oo + i] = p;
+            double rt = p / lf[u];
+            rtime[oo + i] = rt;
+            const double z = rt * ls[u];
+            c2 += z * z;
+        }
+    }
+    c2 = block_sum<1>(c2, nullptr);
+    if (tid == 0) rpart[3 * rb + 2] = c2;
+}
+
 // _calc_wls_chi2 (residuals.py:638-667): one wave per instance sums its blocks' chi2
 // partials in a fixed tree order (a kernel boundary, not a device-wide fence, orders them)
 __global__ __launch_bounds__(64) void k_rsum(const InstDev* __restrict__ insts, const double* __restrict__ rpart,
@@ -4777,6 +4862,7 @@ struct pint_ctx {
     int gv_pair = 1;     // PINT_GV_PAIR: k_gram_v launch order pairs heavy and light instances on a CU
     int maxn = 0;        // the batch's largest instance (rows)
     int max_ts = 0;      // the batch's largest parameter table (doubles)
+    int resid12 = 1;     // PINT_RESID12: k_resid12 for batches of one-block instances without tiles
     int prep_lanes = 1;  // PINT_PREP_LANES: lane-per-instance k_prep / k_apply for small tables
     int fuse_r2 = 1;     // PINT_FUSE_R2: the fit layout's k_resid2 folded into k_gram_v's staging
     bool r2_pending = false;  // k_resid2 of the last pass deferred (the Gram formed its residuals)
@@ -5352,6 +5438,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->fuse_r2 = getenv("PINT_FUSE_R2") ? atoi(getenv("PINT_FUSE_R2")) : 1;
     ctx->eval0_wpe = getenv("PINT_EVAL0_WPE") ? atoi(getenv("PINT_EVAL0_WPE")) : 1;
     ctx->prep_lanes = getenv("PINT_PREP_LANES") ? atoi(getenv("PINT_PREP_LANES")) : 1;
+    ctx->resid12 = getenv("PINT_RESID12") ? atoi(getenv("PINT_RESID12")) : 1;
     ctx->evalb_wpe = getenv("PINT_EVALB_WPE") ? atoi(getenv("PINT_EVALB_WPE")) : 3;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
@@ -6528,7 +6615,12 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         // the fit layout's pass on the k_gram_v path: k_resid1 only, the Gram stages the time
         // residuals itself and k_resid2 waits for a reader of them (flush_r2)
         const bool defer2 = want_M == 2 && can_defer_r2(ctx);
-        if (ctx->small && ctx->maxn <= RES_SMALLN) {  // a wave per residual block
+        const bool fused12 = ctx->small && ctx->maxn <= RES_SMALLN && !wt && !defer2 && ctx->resid12;
+        if (fused12) {  // one wave per instance does both passes
+            hipLaunchKernelGGL(k_resid12, dim3((ctx->nrblk + 3) / 4), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs,
+                               ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay,
+                               ctx->d_rt, ctx->d_rp, ctx->d_rpart);
+        } else if (ctx->small && ctx->maxn <= RES_SMALLN) {  // a wave per residual block
             const int nb4 = (ctx->nrblk + 3) / 4;
             hipLaunchKernelGGL(k_resid1<64>, dim3(nb4), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                                ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_rp, ctx->d_rpart);
@@ -6538,7 +6630,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
                                ctx->d_rpart);
         }
         if (defer2) ctx->r2_pending = true;
-        else launch_resid2(ctx, wt);
+        else if (!fused12) launch_resid2(ctx, wt);
         // the chi2 partials are summed when the chi2 is read (pint_read_resids) or by k_wsolve,
         // which needs them anyway: no launch of its own in a fit step
         ctx->chi2_pending = true;

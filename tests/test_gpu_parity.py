@@ -1426,3 +1426,35 @@ def test_lane_per_instance_setup_matches(monkeypatch, name):
 
     for x, y in zip(run(1), run(0)):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_fused_small_residual_pass_matches(monkeypatch):
+    """k_resid12 (both residual passes in one wave per one-block instance, PINT_RESID12)
+    against k_resid1<64> + k_resid2<64>: residuals, chi2 and a fit step bit for bit."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    m0, t0 = load("ngc6440e")[:2]
+
+    def run(f):
+        monkeypatch.setenv("PINT_RESID12", str(f))
+        s = Session()
+        lay = s.add(build_layout(m0, t0))
+        tab = pack_table(lay, m0)
+        insts = []
+        for k in range(9):
+            tk = tab.copy()
+            tk[lay.offsets["F0"]] += (k - 4) * 3e-11
+            insts.append((lay, tk))
+        s.set_instances(insts)
+        s.eval(want_M=False)
+        tr, pr, c2 = s.read_resids()
+        out = [np.concatenate(tr).copy(), np.concatenate(pr).copy(), np.array(c2, copy=True)]
+        s.eval(want_M=Session.FIT)
+        s.fit_step(0)
+        dp, er, cov, cl = s.read_step()
+        out += [x.copy() for x in dp] + [np.array(cl, copy=True)]
+        s.close()
+        return out
+
+    for x, y in zip(run(1), run(0)):
+        np.testing.assert_array_equal(x, y)
