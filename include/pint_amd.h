@@ -143,6 +143,9 @@ const char *pint_last_error(pint_ctx *ctx);
  * HIP runtime (no reference counterpart: device memory management). */
 void pint_release_cache(void);
 int pint_device_count(void);
+/* Pipeline slots of pint_step_end / pint_check_step, fixed when the library is built
+ * (-DPINT_NSLOT, default 4): the host's slot bookkeeping must use this value. */
+int pint_nslot(void);
 
 /* Upload one pulsar (packed TOAs + model structure); returns its id >= 0, or -status.
  * Replaces the TOAs.table hand-off of get_model_and_toas (model_builder.py:859) and the

@@ -15,8 +15,7 @@ LIBPATH = os.environ.get("PINT_LIB") or os.path.join(HERE, "libpint_hip.so")
 
 MAX_COLS = 320
 EIG_MAXDEG = 8  # PINT_EIG_MAXDEG
-NSLOT = int(os.environ.get("PINT_NSLOT", "4"))  # PINT_NSLOT: pipeline slots (pint_step_end / pint_check_step; a
-# library built with -DPINT_NSLOT=k needs the same k here)
+NSLOT = 4  # pipeline slots (pint_step_end / pint_check_step): set from the library's pint_nslot() by lib()
 B_NPAR = 27
 BIN_NONE, BIN_ELL1, BIN_DD, BIN_ELL1H, BIN_BT, BIN_DDK = range(6)
 
@@ -113,6 +112,10 @@ def lib():
     L.pint_release_cache.restype = None
     L.pint_release_cache.argtypes = []
     L.pint_device_count.restype = C.c_int
+    L.pint_nslot.restype = C.c_int
+    L.pint_nslot.argtypes = []
+    global NSLOT
+    NSLOT = int(L.pint_nslot())  # the library's compile-time slot count, not an environment guess
     L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
     L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
     L.pint_set_grid.argtypes = [vp, C.c_int, C.c_int, dptr, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
@@ -167,7 +170,7 @@ def lib():
     return L
 
 
-EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_release_cache", "pint_device_count", "pint_add_pulsar",
+EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_release_cache", "pint_device_count", "pint_nslot", "pint_add_pulsar",
             "pint_set_instances", "pint_get_tables", "pint_set_tables", "pint_eval", "pint_read_resids",
             "pint_read_eval", "pint_read_designmatrix", "pint_fit_step", "pint_read_step", "pint_apply_step",
             "pint_chi2_gls", "pint_set_ecorr", "pint_last_timing", "pint_sync", "pint_debug_read", "pint_set_lazy", "pint_check",

@@ -5398,6 +5398,8 @@ static int refresh_psrs(pint_ctx* ctx) {
 
 extern "C" {
 
+int pint_nslot(void) { return pint_ctx::NSLOT; }
+
 int pint_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -5836,6 +5838,7 @@ int pint_set_instances(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const 
 // the value (hi, lo) = vals_j[((k0 + k) / stride[j]) % size[j]] (vals: the variables' value
 // pairs concatenated, size[j] pairs each) -- a meshgrid's axes, or every point's own value
 // (stride 1, size npts).
+static int flush_chi2(pint_ctx* ctx);
 int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar, const int32_t* var_toff,
                   const int64_t* var_stride, const int64_t* var_size, const double* vals, int64_t k0) {
     if (!ctx || npts <= 0 || !base || nvar < 0 || nvar > 16 || (nvar && (!var_toff || !var_stride || !var_size || !vals)))
@@ -5857,6 +5860,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
     const long gkey = ((long)ctx->small << 2) | ((long)ctx->vgram << 1) | (long)ctx->vbin;
     if (ctx->grid_valid && ctx->grid_psr == psr && ctx->ninst == npts && ctx->grid_opts == gkey && !ctx->psrs_dirty &&
         ctx->setup_pending.empty()) {
+        if (flush_chi2(ctx)) return PINT_E_HIP;  // (a lazy pint_chi2_gls of the previous points is delivered)
         if (int rc = flush_cq_now(ctx)) return rc;
         HIPCHK(hipStreamSynchronize(ctx->cstream));
         HIPCHK(hipStreamSynchronize(ctx->sstream));
@@ -7369,8 +7373,8 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
 // WLS chi2 of the current residuals, per instance (k_chi2w); the chi2 that pint_read_resids
 // reports comes from the residual pass itself, this one from whatever d_rt holds now.
 int pint_chi2_wls(pint_ctx* ctx, double* chi2) {
-    flush_r2(ctx);
     if (!ctx || ctx->ninst <= 0 || !chi2) return PINT_E_INVALID;
+    flush_r2(ctx);
     if (flush_chi2(ctx)) return PINT_E_HIP;
     hipSetDevice(ctx->device);
     hipLaunchKernelGGL(k_chi2w, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt,
@@ -7857,8 +7861,8 @@ int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
 // caller's, e.g. the reference's own residual arrays, so that pint_fit_step / pint_chi2_gls
 // run on them (SURVEY.md 8(a) stage-wise parity).
 int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
-    flush_r2(ctx);  // (its rpart partials and phases first; the time residuals are replaced below)
     if (!ctx || ctx->ninst <= 0 || !time_resid) return PINT_E_INVALID;
+    flush_r2(ctx);  // (its rpart partials and phases first; the time residuals are replaced below)
     hipSetDevice(ctx->device);
     HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -7951,8 +7955,8 @@ int pint_set_noise_classes(pint_ctx* ctx, int psr, int ncls, const int32_t* cls_
 
 int pint_noise_lnlike(pint_ctx* ctx, const int32_t* kind, const double* cls_qf, const double* ep_w, double* out3,
                       double* cls_g, double* ep_g) {
-    flush_r2(ctx);
     if (!ctx || ctx->ninst <= 0 || !kind || !cls_qf || !out3) return PINT_E_INVALID;
+    flush_r2(ctx);
     hipSetDevice(ctx->device);
     const int ni = ctx->ninst;
     std::vector<long> meta(3 * (size_t)ni);

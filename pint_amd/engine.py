@@ -1128,31 +1128,28 @@ def _structure_sig(model, lay):
 
 
 def _toas_fingerprint(toas):
-    """A cheap content hash of the TOA columns the upload is built from (the arrays, the
-    flag columns, the observatories, the TZR TOA), so an in-place edit of the public
-    `toas.arrays` / `toas.flag_columns` re-uploads instead of reusing stale device data.
-    ~0.1 ms for 10k TOAs (xxh3 over the column bytes; flag columns by their tuple hash)."""
-    try:
-        import xxhash
-        h = xxhash.xxh3_64()
-    except ImportError:  # pragma: no cover - the image has xxhash
-        import hashlib
-        h = hashlib.blake2b(digest_size=8)
-    for k in sorted(toas.arrays):
-        a = np.ascontiguousarray(toas.arrays[k])
-        h.update(k.encode())
-        h.update(str(a.dtype).encode())
-        h.update(a.view(np.uint8).ravel() if a.dtype != object else repr(a.tolist()).encode())
-    for k in sorted(toas.flag_columns):
-        h.update(k.encode())
-        h.update(hash(tuple(toas.flag_columns[k])).to_bytes(8, "little", signed=True))
-    if getattr(toas, "obs", None) is not None:
-        h.update(hash(tuple(toas.obs)).to_bytes(8, "little", signed=True))
+    """What the upload of `toas` was built from, by object identity: every TOA column (numpy
+    arrays are read-only views and flag columns tuples, pint_amd.toa._Columns, so a column
+    changes only by being replaced), the observatory column and the TZR TOA's values.  The
+    objects themselves are held (not their ids), so a freed column's address cannot be
+    reused by a new one while the entry lives.  O(columns), not O(TOAs): hashing every
+    column's bytes per fit cost ~1.3-2.7 ms on C3's 50k TOAs."""
     tz = getattr(toas, "tzr", None) or {}
-    for k in sorted(tz):
-        h.update(k.encode())
-        h.update(repr(tz[k]).encode())
-    return h.hexdigest()
+
+    def val(v):  # the TZR row's values (an array's bytes: numpy's repr costs ~30 us each)
+        if isinstance(v, np.ndarray):
+            return (v.dtype.str, v.shape, v.tobytes() if v.dtype != object else repr(v.tolist()))
+        if isinstance(v, dict):
+            return tuple(sorted((k, repr(x)) for k, x in v.items()))
+        return repr(v)
+    return (tuple(sorted(toas.arrays.items())), tuple(sorted(toas.flag_columns.items())), getattr(toas, "obs", None),
+            tuple((k, val(tz[k])) for k in sorted(tz)))
+
+
+def _same_fingerprint(a, b):
+    def same_cols(x, y):
+        return len(x) == len(y) and all(kx == ky and vx is vy for (kx, vx), (ky, vy) in zip(x, y))
+    return same_cols(a[0], b[0]) and same_cols(a[1], b[1]) and a[2] is b[2] and a[3] == b[3]
 
 
 def resident(model, toas, tag=None, track_mode=None, subtract_mean=True, use_weighted_mean=True,
@@ -1165,7 +1162,7 @@ def resident(model, toas, tag=None, track_mode=None, subtract_mean=True, use_wei
     fp = _toas_fingerprint(toas)
     if ent is not None:
         s, lay, t0, sig, fp0 = ent
-        if t0 is toas and fp == fp0 and model.binary != "ELL1H" and _structure_sig(model, lay) == sig:
+        if t0 is toas and _same_fingerprint(fp, fp0) and model.binary != "ELL1H" and _structure_sig(model, lay) == sig:
             model.validate()
             _RESIDENT[key] = ent  # most recently used last
             return s, lay

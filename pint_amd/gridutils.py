@@ -56,6 +56,15 @@ def meshgrid_axes(parvalues):
     return out, int(np.prod(shape, dtype=np.int64))
 
 
+def meshgrid_shape(parvalues):
+    """np.meshgrid(*parvalues)[0].shape (indexing 'xy': the first two axes swap), from the
+    axis lengths alone."""
+    n = [np.atleast_1d(v).size for v in parvalues]
+    if len(n) >= 2:
+        n[0], n[1] = n[1], n[0]
+    return tuple(n)
+
+
 def _dist():
     try:
         import torch.distributed as dist
@@ -270,7 +279,7 @@ def grid_chisq(ftr, parnames: Sequence[str], parvalues: Sequence, extraparnames:
     GPU batch per rank instead of a process pool.  With torch.distributed initialised, rank
     r fits the r-th contiguous block of the flattened meshgrid and the blocks are
     all-gathered, so every rank returns the whole grid."""
-    shape = np.meshgrid(*[np.zeros(len(np.atleast_1d(v))) for v in parvalues])[0].shape
+    shape = meshgrid_shape(parvalues)
     chi2, extra = _chisq_flat(ftr, parnames, None, extraparnames, fitargs, axes=meshgrid_axes(parvalues))
     return chi2.reshape(shape), {e: v.reshape(shape) for e, v in extra.items()}
 

@@ -89,18 +89,25 @@ class TimingModel:
         return order
 
     def _params_order(self) -> List[str]:
-        top = [n for n, p in self._params.items() if p.component in ("", "TimingModel")]
-        astro = [n for n, p in self._params.items() if p.component.startswith("Astrometry")]
-        spin = [n for n, p in self._params.items() if p.component == "Spindown"]
-        rest = []
+        # one stable sort by group rank (dict order within a group): top level, astrometry,
+        # spindown, the delay/phase/noise components in order, the rest
         order = [("Binary" if c.startswith("Binary") else c) for c in DELAY_ORDER]
+        rest = {}
         for comp in dict.fromkeys(order + ["AbsPhase", "PhaseJump"] + NOISE):
-            if comp.startswith("Astrometry"):
-                continue
-            rest += [n for n, p in self._params.items() if p.component == comp]
-        seen = set(top + astro + spin + rest)
-        other = [n for n in self._params if n not in seen]
-        return top + astro + spin + rest + other
+            if not comp.startswith("Astrometry"):
+                rest.setdefault(comp, 3 + len(rest))
+        big = 3 + len(rest)
+
+        def rank(c):
+            if c in ("", "TimingModel"):
+                return 0
+            if c.startswith("Astrometry"):
+                return 1
+            if c == "Spindown":
+                return 2
+            return rest.get(c, big)
+        ranks = {c: rank(c) for c in {p.component for p in self._params.values()}}
+        return sorted(self._params, key=lambda n: ranks[self._params[n].component])
 
     def as_parfile(self, include_info: bool = True, comment: str = None) -> str:
         """The model as par-file text (timing_model.py:2747 as_parfile, format "pint")."""

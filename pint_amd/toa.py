@@ -26,12 +26,54 @@ FIELDS = ["tdb_hi", "tdb_lo", "freq_mhz", "err_us", "ssb_obs_pos_km", "ssb_obs_v
 PLANET_FIELDS = [f"obs_{p}_pos_km" for p in ("jupiter", "saturn", "venus", "uranus", "neptune", "earth")]
 
 
+def _ro_array(v):
+    """A read-only view of v (the caller's array keeps its own flags)."""
+    a = np.asarray(v).view()
+    a.setflags(write=False)
+    return a
+
+
+class _Columns(dict):
+    """TOA columns whose values cannot be edited in place: a column changes only by being
+    replaced (``toas.arrays[k] = new``), which the resident-upload cache
+    (engine.resident) sees by object identity instead of hashing every column per fit."""
+    @staticmethod
+    def _conv(v):
+        raise NotImplementedError
+
+    def __init__(self, items=()):
+        super().__init__()
+        self.update(items)
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, self._conv(v))
+
+    def update(self, items=(), **kw):
+        for k, v in (items.items() if hasattr(items, "items") else items):
+            self[k] = v
+        for k, v in kw.items():
+            self[k] = v
+
+    def setdefault(self, k, v=None):
+        if k not in self:
+            self[k] = v
+        return self[k]
+
+
+class _ArrayColumns(_Columns):
+    _conv = staticmethod(_ro_array)
+
+
+class _FlagColumns(_Columns):
+    _conv = staticmethod(tuple)
+
+
 class TOAs:
     def __init__(self, arrays: Dict[str, np.ndarray], flag_columns: Optional[Dict[str, List[str]]] = None,
                  tzr: Optional[Dict[str, np.ndarray]] = None, name: str = "", obs: Optional[List[str]] = None):
-        self.arrays = {k: np.asarray(v) for k, v in arrays.items()}
+        self.arrays = arrays
         n = len(self.arrays["tdb_hi"])
-        self.flag_columns = {k: list(v) for k, v in (flag_columns or {}).items()}
+        self.flag_columns = flag_columns or {}
         for k, v in self.flag_columns.items():
             if len(v) != n:
                 raise ValueError(f"flag column {k} has {len(v)} rows, expected {n}")
@@ -44,12 +86,39 @@ class TOAs:
         self.prepared = None  # tim-file TOAs: the preparation options (TZR TOAs are prepared alike)
         self.commands = []
         # observatory (canonical site name) of each TOA, when known: TEL masks select on it
-        self.obs = None if obs is None else np.asarray([str(o) for o in obs], dtype=object)
+        self.obs = obs
         if self.obs is not None and len(self.obs) != n:
             raise ValueError(f"obs has {len(self.obs)} rows, expected {n}")
         self.ephem = None   # the host preparation's ephemeris / clock chain, when known
         self.clock = None   # (update_model writes them into the model as EPHEM / CLOCK)
         self._uid = id(self)
+
+    # read-only columns (numpy arrays as read-only views, flag columns as tuples): assigning
+    # a new dict or a new column replaces objects, an in-place edit raises
+    @property
+    def arrays(self):
+        return self._arrays
+
+    @arrays.setter
+    def arrays(self, v):
+        self._arrays = _ArrayColumns(v)
+
+    @property
+    def flag_columns(self):
+        return self._flags
+
+    @flag_columns.setter
+    def flag_columns(self, v):
+        self._flags = _FlagColumns(v)
+
+    @property
+    def obs(self):
+        """Observatory (canonical site name) of each TOA, when known (TEL masks select on it)."""
+        return self._obs
+
+    @obs.setter
+    def obs(self, v):
+        self._obs = None if v is None else _ro_array(np.asarray([str(o) for o in v], dtype=object))
 
     # -- reference-like accessors ------------------------------------------------------
     @property
@@ -187,8 +256,7 @@ class TOAs:
         if len(key_value) == 2:
             raise NotImplementedError("range selection on a flag column")
         # each entry compared with == as the reference's selector does (an object array keeps
-        # None and non-string values as they are); built per call, so an in-place edit of
-        # the column is always seen
+        # None and non-string values as they are)
         arr = np.empty(len(col), dtype=object)
         arr[:] = col
         return np.where(arr == key_value[0])[0]
@@ -205,7 +273,8 @@ class TOAs:
             arr.update({"tzr_" + k: np.atleast_1d(v) for k, v in self.tzr.items() if k != "flags"})
         np.savez_compressed(base + ".npz", **arr)
         with open(base + ".json", "w") as f:
-            json.dump({"flag_columns": self.flag_columns, "name": self.name, "obs_names": names}, f)
+            json.dump({"flag_columns": {k: list(v) for k, v in self.flag_columns.items()}, "name": self.name,
+                       "obs_names": names}, f)
 
 
 def from_arrays_with_tzr(z: Dict[str, np.ndarray], flag_columns=None, name="", obs_names=None) -> TOAs:

@@ -38,6 +38,7 @@ def analyse(trace, log):
     for r in csv.DictReader(open(trace)):
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
     ks.sort()
+    agg = {}
     for line in open(log):
         if not line.startswith("fit "):
             continue
@@ -57,8 +58,18 @@ def analyse(trace, log):
                 cur_e = max(cur_e, e)
         if cur_e is not None:
             busy += cur_e - cur_s
+        if int(rep) >= 1:
+            for s, e, nm in ks:
+                if s >= t0 and e <= t1:
+                    agg.setdefault(nm, [0, 0])
+                    agg[nm][0] += 1
+                    agg[nm][1] += e - s
         print(f"fit {rep}: wall {(t1 - t0) / 1e6:.2f} ms, device busy {busy / 1e6:.2f} ms "
               f"({100.0 * busy / (t1 - t0):.0f} %), {n} kernels; host + gaps {(t1 - t0 - busy) / 1e6:.2f} ms")
+    print("per fit (fits 1..), by kernel: launches, device ms")
+    nf = 3
+    for nm, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {nm[:60]:60s} {c / nf:6.1f} {t / nf / 1e6:8.3f}")
 
 
 if __name__ == "__main__":
