@@ -585,10 +585,46 @@ def grid_leg(side, dist, barrier, max_over_ranks):
     kt = gs.timing()
     gs.set_timing_mask(0)
     roof = grid_roofline(kt, glay, side * side, dt)
-    return {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
-            "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 4),
-            "seconds_all": [round(x, 4) for x in dts], "timing": "median of 3 grids after 2 warm-up grids",
-            "chi2_min": float(np.nanmin(chi2)), "roofline": roof}
+    out = {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
+           "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 4),
+           "seconds_all": [round(x, 4) for x in dts], "timing": "median of 3 grids after 2 warm-up grids",
+           "chi2_min": float(np.nanmin(chi2)), "roofline": roof}
+    if dist is None:
+        out["predicted_strong"] = grid_emulate(f, g0, g1, side, dt)
+    return out
+
+
+def grid_emulate(f, g0, g1, side, dt1, worlds=(2, 4, 8)):
+    """Predicted strong scaling of the grid leg on this one GPU: for each world size N, the
+    contiguous blocks of the flattened meshgrid that ranks 0 and N-1 own in an N-rank run
+    (gridutils.shard_range; every other rank's block equals rank 0's) are fitted alone, the
+    median of 3 after a warm-up each; the predicted N-GPU grid time is the slower block's."""
+    from pint_amd import gridutils
+    from pint_amd.gridutils import grid_chisq
+    npts = side * side
+    out = {"method": ("ranks 0 and N-1's contiguous point blocks (gridutils.shard_range) each fitted alone on "
+                      "this GPU, median of 3 after a warm-up; predicted value = points / the slower block's time"),
+           "n1": {"value": round(npts / dt1, 1), "seconds": round(dt1, 6)}}
+    for nw in worlds:
+        per = []
+        for r in sorted({0, nw - 1}):
+            gridutils._EMULATE_SHARD = (r, nw)
+            try:
+                grid_chisq(f, ("F0", "F1"), (g0, g1))  # warm-up (the block's batch set up)
+                reps = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    grid_chisq(f, ("F0", "F1"), (g0, g1))
+                    reps.append(time.perf_counter() - t0)
+            finally:
+                gridutils._EMULATE_SHARD = None
+            per.append(float(np.median(reps)))
+        mx = max(per)
+        out[f"n{nw}"] = {"value": round(npts / mx, 1), "seconds": round(mx, 6),
+                         "points_per_rank": gridutils.shard_range(npts, 0, nw)[0],
+                         "speedup_vs_n1": round(dt1 / mx, 3)}
+        log(f"[grid emulate {nw}] blocks {[round(p * 1e3, 3) for p in per]} ms -> {npts / mx:.0f} points/s")
+    return out
 
 
 def grid_roofline(kt, lay, npts, dt):

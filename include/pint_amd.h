@@ -346,6 +346,26 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * pint_set_instances) and the one-wave k_solve_blk (four instances per workgroup); 0 keeps
  * them on the 16-wave Gram and the 4-wave solve (the tests cross-check the two). */
 #define PINT_OPT_SMALL 10
+/* PINT_OPT_LA_CHOL = 1 (default, env PINT_LA_CHOL): the DMX-eliminated solve factors its
+ * dense block with look-ahead (the next diagonal block factored beside the current trailing
+ * update, L^-1's block rows beside the panels); 0 runs the plain blocked order.  The same
+ * operations in the same order per block: the same bits. */
+#define PINT_OPT_LA_CHOL 11
+/* PINT_OPT_EFUSE = 1 (default, env PINT_EFUSE): batches off the small-instance path evaluate
+ * 254 rows per block plus row 0 and the TZR row, and form the phase residuals and their
+ * weighted sums there (the residual pass's first half, no k_resid1 launch); applies from the
+ * next pint_set_instances. */
+#define PINT_OPT_EFUSE 12
+/* PINT_OPT_LANE_SOLVE = 1 (default, env PINT_LANE_SOLVE): small-instance batches (the
+ * PINT_OPT_SMALL path) whose normal equations have at most 8 columns are solved with one
+ * lane per instance (64 instances per wave) instead of one wave per instance. */
+#define PINT_OPT_LANE_SOLVE 13
+/* PINT_OPT_SPIN_EVAL = 1 (default, env PINT_SPIN_EVAL): a pint_set_grid batch whose points
+ * differ in spin frequencies only (isolated model, no red-noise basis) evaluates its rows'
+ * delays and astrometric geometry once, on the first point, for the evaluation with the
+ * design matrix that precedes the first fit step; each point then runs the spin part only.
+ * The same bits as the full evaluation. */
+#define PINT_OPT_SPIN_EVAL 14
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

@@ -1096,9 +1096,130 @@ struct ColRun {
 // (timing_model.py:2164-2173).  compact: the fit layout, where the DMX columns (1 on the
 // bin's TOAs times one per-TOA value, o.dmc) are not stored and the other columns are
 // packed (ColRun.dcol0).
+// The parameter-side state eval_toa forms before the spin phase: everything but the spin
+// phase, the spin frequencies and the chain factor that scales the design-matrix row depends
+// on the TOA and the non-spin parameters only.  A grid whose points differ in spin
+// parameters alone shares it across its points (k_eval_head / k_eval_spin).
+struct EvalHead {
+    double delay;                          // total delay (s)
+    double gLON, gLAT, gPMLON, gPMLAT, gPX;  // astrometric geometry without the chain factor
+    double inv_f2, dt_yr_dm, logf;
+};
+constexpr int EVAL_HEAD_W = 9;  // doubles of an EvalHead row
+
+// eval_toa after the delay: the spin frequency at dt (dt0 - delay) and at dt0, the chain
+// factor of the design matrix
+struct EvalSpin {
+    dd dt;
+    double dtd, chain;
+};
+PD void eval_spin_a(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, double delay,
+                    EvalOut& o, EvalSpin& sp) {
+    o.delay = delay;
+    dd dt0 = dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_PEPOCH)), DAYSEC);
+    sp.dt = dd_add_d(dt0, -delay);
+    sp.dtd = dd_to_d(sp.dt);
+    o.fdt = spin_freq(S, P, sp.dtd);
+    o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
+    sp.chain = o.fdt * C.iF0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+}
+
+// eval_toa's spindown phase, jumps and PhaseOffset, then the design-matrix row but for the
+// binary columns (written by eval_toa while the binary state is live)
 template <int BIN>
-PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalOut& o,
-                 double* Mb, unsigned r, long ld, const ColRun* runs, int nrun, bool compact) {
+PD void eval_spin_b(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, const EvalHead& h,
+                    const EvalSpin& sp, EvalOut& o, double* Mb, unsigned r, long ld, const ColRun* runs, int nrun,
+                    bool compact) {
+    const double chain = sp.chain, dtd = sp.dtd;
+    // ---- spindown phase (spindown.py:124-155) + jumps (jump.py:119-136) ----
+    dd ph = spin_phase(S, P, sp.dt);
+    if (S.njump > 0 && t.jmask) {
+        dd F0 = pdd(P, S.o_F);
+        for (int k = 0; k < S.njump; k++)
+            if ((t.jmask >> k) & 1ull) ph = dd_add(ph, dd_mul(dd_make(pval(P, S.o_JUMP + 2 * k)), F0));
+    }
+    // PhaseOffset.offset_phase (phase_offset.py): -PHOFF on the TOAs, nothing on the TZR TOA
+    // (row ld = n)
+    if (S.o_PHOFF >= 0 && r < (unsigned)ld) ph = dd_sub(ph, pdd(P, S.o_PHOFF));
+    o.phase = ph;
+    if (!Mb) return;
+    // ---- design matrix row (timing_model.py:2073-2175) ----
+    const double iF0 = C.iF0;
+    const double dt_yr_dm = h.dt_yr_dm, logf = h.logf;
+    // the astrometric geometry formed above, times the chain factor
+    const double gLON = h.gLON * chain;
+    const double gLAT = h.gLAT * chain;
+    const double gPMLON = h.gPMLON * chain;
+    const double gPMLAT = h.gPMLAT * chain;
+    const double gPX = h.gPX * chain;
+    const double dmc = chain * DMCONST * h.inv_f2;
+    o.dmc = dmc;
+    for (int u = 0; u < nrun; u++) {
+        const ColRun R = runs[u];
+        if (compact && R.kind == PINT_COL_DMX) continue;
+        double* colp = Mb + (long)(compact ? R.dcol0 : R.col0) * ld;
+        switch (R.kind) {
+            case PINT_COL_OFFSET: colp[r] = iF0; break;
+            case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): -dt^(k+1)/(k+1)! / F0
+                double v = 1.0;
+                for (int j = 1; j <= R.idx0; j++) v = v * dtd * inv_int(j);
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    v = v * dtd * inv_int(R.idx0 + j + 1);
+                    colp[r] = -v * iF0;
+                }
+            } break;
+            case PINT_COL_JUMP:  // jump.py:138
+                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = ((t.jmask >> (R.idx0 + j)) & 1ull) ? -1.0 : 0.0;
+                break;
+            case PINT_COL_LON: colp[r] = gLON; break;
+            case PINT_COL_LAT: colp[r] = gLAT; break;
+            case PINT_COL_PMLON: colp[r] = gPMLON; break;
+            case PINT_COL_PMLAT: colp[r] = gPMLAT; break;
+            case PINT_COL_PX: colp[r] = gPX; break;
+            case PINT_COL_DM: {  // d_dm_d_DMs (dispersion_model.py:253) * DMconst / bfreq^2
+                double v = 1.0;
+                for (int j = 1; j <= R.idx0; j++) v = v * dt_yr_dm * inv_int(j);
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    if (j > 0) v = v * dt_yr_dm * inv_int(R.idx0 + j);
+                    colp[r] = dmc * v;
+                }
+            } break;
+            case PINT_COL_DMX:  // d_dm_d_DMX (:684): 1 on the bin's TOAs
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    const int idx = R.idx0 + j;
+                    bool in = t.dmx_a == idx || t.dmx_b == idx;
+                    for (int k = t.dmx_x0; k < t.dmx_x1; k++) in |= t.dmx_x[k] == idx;
+                    colp[r] = in ? dmc : 0.0;
+                }
+                break;
+            case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103): logf^(k+1)
+                double v = 1.0;
+                for (int j = 0; j <= R.idx0; j++) v *= logf;
+                for (int j = 0; j < R.cnt; j++, colp += ld) {
+                    if (j > 0) v *= logf;
+                    colp[r] = chain * v;
+                }
+            } break;
+            case PINT_COL_BIN:  // written with the binary state above
+                if (BIN == 0)
+                    for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
+                break;
+            default:
+                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
+        }
+    }
+}
+
+// eval_toa up to the binary model: the astrometric (Roemer, parallax), Solar-system Shapiro,
+// dispersion (DM Taylor series, DMX) delays, the barycentric frequency, FD (formed, added
+// after the binary delay), and the astrometric design-matrix geometry without the chain factor
+struct EvalPre {
+    EvalHead h;  // h.delay: the delay so far (without FD: acc_delay of the binary model)
+    double fd;
+    double L[3];
+};
+PD void eval_pre(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalOut& o, bool wantM,
+                 EvalPre& pre) {
     o.status = 0;
     o.dmc = 0.0;
     double delay = 0.0;
@@ -1185,7 +1306,7 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
     //      vectors and the pulsar direction die before the binary state is set up (the
     //      binary columns are written while that state is live: the register peak) ----
     double gLON = 0, gLAT = 0, gPMLON = 0, gPMLAT = 0, gPX = 0;
-    if (Mb && S.astrometry) {
+    if (wantM && S.astrometry) {
         // Earth direction angles (era, edec) of the SSB->observatory vector enter only as
         // cos(edec) sin(plon - era), cos(edec) cos(plon - era) and sin(edec): formed from
         // the vector itself, cos(edec) cos(era) = x/r etc. (no atan2/sin/cos per TOA)
@@ -1210,6 +1331,32 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         // d_delay_astrometry_d_PX (astrometry.py:219-249)
         gPX = 0.5 * ((rr - re_dot_L * re_dot_L) * INV_AUC) * MAS_RAD;
     }
+    pre.h = {delay, gLON, gLAT, gPMLON, gPMLAT, gPX, inv_f2, dt_yr_dm, logf};
+    pre.fd = fd;
+    pre.L[0] = L[0];
+    pre.L[1] = L[1];
+    pre.L[2] = L[2];
+}
+
+// the shared head of a spin-only grid (k_eval_head): eval_toa's operations up to the spin part
+PD void eval_head(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalHead& h) {
+    EvalOut o;
+    EvalPre pre;
+    eval_pre(S, P, C, t, o, true, pre);
+    h = pre.h;
+    if (S.nfd > 0) h.delay += pre.fd;
+}
+
+template <int BIN>
+PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, const ToaRow& t, EvalOut& o,
+                 double* Mb, unsigned r, long ld, const ColRun* runs, int nrun, bool compact) {
+    EvalPre pre;
+    eval_pre(S, P, C, t, o, Mb != nullptr, pre);
+    double delay = pre.h.delay;
+    const double* L = pre.L;
+    const double fd = pre.fd;
+    const double inv_f2 = pre.h.inv_f2, dt_yr_dm = pre.h.dt_yr_dm, logf = pre.h.logf;
+    const double gLON = pre.h.gLON, gLAT = pre.h.gLAT, gPMLON = pre.h.gPMLON, gPMLAT = pre.h.gPMLAT, gPX = pre.h.gPX;
     // ---- binary (pulsar_binary.py:457, acc_delay = delay so far) ----
     BinState B;
     B.status = 0;
@@ -1236,13 +1383,9 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
         if (B.status) o.status = B.status;
     }
     if (S.nfd > 0) delay += fd;
-    o.delay = delay;
-    dd dt0 = dd_mul_d(dd_sub(t.tdb, pdd(P, S.o_PEPOCH)), DAYSEC);
-    dd dt = dd_add_d(dt0, -delay);
-    double dtd = dd_to_d(dt);
-    o.fdt = spin_freq(S, P, dtd);
-    o.ftaylor = spin_freq(S, P, dd_to_d(dt0));
-    const double chain = o.fdt * C.iF0;  // M = -(d_phase_d_delay * d_delay_d_p)/F0, d_phase_d_delay = -F(dt)
+    EvalSpin sp;
+    eval_spin_a(S, P, C, t, delay, o, sp);
+    const double chain = sp.chain;
     // ---- the binary columns of the design-matrix row, while the binary state is live (it
     //      then dies: ~80 doubles fewer in registers through the phase and the other columns) ----
     if (Mb && BIN != 0) {
@@ -1263,82 +1406,8 @@ PD void eval_toa(const pint_spec_t& S, const double* P, const InstConst& C, cons
             }
         }
     }
-    // ---- spindown phase (spindown.py:124-155) + jumps (jump.py:119-136) ----
-    dd ph = spin_phase(S, P, dt);
-    if (S.njump > 0 && t.jmask) {
-        dd F0 = pdd(P, S.o_F);
-        for (int k = 0; k < S.njump; k++)
-            if ((t.jmask >> k) & 1ull) ph = dd_add(ph, dd_mul(dd_make(pval(P, S.o_JUMP + 2 * k)), F0));
-    }
-    // PhaseOffset.offset_phase (phase_offset.py): -PHOFF on the TOAs, nothing on the TZR TOA
-    // (row ld = n)
-    if (S.o_PHOFF >= 0 && r < (unsigned)ld) ph = dd_sub(ph, pdd(P, S.o_PHOFF));
-    o.phase = ph;
-    if (!Mb) return;
-    // ---- design matrix row (timing_model.py:2073-2175) ----
-    const double iF0 = C.iF0;
-    // the astrometric geometry formed above, times the chain factor
-    gLON *= chain;
-    gLAT *= chain;
-    gPMLON *= chain;
-    gPMLAT *= chain;
-    gPX *= chain;
-    const double dmc = chain * DMCONST * inv_f2;
-    o.dmc = dmc;
-    for (int u = 0; u < nrun; u++) {
-        const ColRun R = runs[u];
-        if (compact && R.kind == PINT_COL_DMX) continue;
-        double* colp = Mb + (long)(compact ? R.dcol0 : R.col0) * ld;
-        switch (R.kind) {
-            case PINT_COL_OFFSET: colp[r] = iF0; break;
-            case PINT_COL_F: {  // d_phase_d_F (spindown.py:207): -dt^(k+1)/(k+1)! / F0
-                double v = 1.0;
-                for (int j = 1; j <= R.idx0; j++) v = v * dtd * inv_int(j);
-                for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    v = v * dtd * inv_int(R.idx0 + j + 1);
-                    colp[r] = -v * iF0;
-                }
-            } break;
-            case PINT_COL_JUMP:  // jump.py:138
-                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = ((t.jmask >> (R.idx0 + j)) & 1ull) ? -1.0 : 0.0;
-                break;
-            case PINT_COL_LON: colp[r] = gLON; break;
-            case PINT_COL_LAT: colp[r] = gLAT; break;
-            case PINT_COL_PMLON: colp[r] = gPMLON; break;
-            case PINT_COL_PMLAT: colp[r] = gPMLAT; break;
-            case PINT_COL_PX: colp[r] = gPX; break;
-            case PINT_COL_DM: {  // d_dm_d_DMs (dispersion_model.py:253) * DMconst / bfreq^2
-                double v = 1.0;
-                for (int j = 1; j <= R.idx0; j++) v = v * dt_yr_dm * inv_int(j);
-                for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    if (j > 0) v = v * dt_yr_dm * inv_int(R.idx0 + j);
-                    colp[r] = dmc * v;
-                }
-            } break;
-            case PINT_COL_DMX:  // d_dm_d_DMX (:684): 1 on the bin's TOAs
-                for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    const int idx = R.idx0 + j;
-                    bool in = t.dmx_a == idx || t.dmx_b == idx;
-                    for (int k = t.dmx_x0; k < t.dmx_x1; k++) in |= t.dmx_x[k] == idx;
-                    colp[r] = in ? dmc : 0.0;
-                }
-                break;
-            case PINT_COL_FD: {  // d_delay_FD_d_FDX (frequency_dependent.py:103): logf^(k+1)
-                double v = 1.0;
-                for (int j = 0; j <= R.idx0; j++) v *= logf;
-                for (int j = 0; j < R.cnt; j++, colp += ld) {
-                    if (j > 0) v *= logf;
-                    colp[r] = chain * v;
-                }
-            } break;
-            case PINT_COL_BIN:  // written with the binary state above
-                if (BIN == 0)
-                    for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
-                break;
-            default:
-                for (int j = 0; j < R.cnt; j++, colp += ld) colp[r] = 0.0;
-        }
-    }
+    const EvalHead h = {delay, gLON, gLAT, gPMLON, gPMLAT, gPX, inv_f2, dt_yr_dm, logf};
+    eval_spin_b<BIN>(S, P, C, t, h, sp, o, Mb, r, ld, runs, nrun, compact);
 }
 
 }  // namespace pint

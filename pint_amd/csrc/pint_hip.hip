@@ -135,6 +135,8 @@ struct InstDev {
     int self;    // index of this instance in the batch
     int nrb;     // k_resid row blocks of this instance (RES_RB rows each)
     long rb0;    // first k_resid row block
+    int neb;     // evaluation blocks with the fused residual pass (EF_ROWS rows each; 0: not fused)
+    long eb0;    // their first weighted-sum partial (d_epart, 2 per block)
 };
 
 // Symmetric view of an instance's Gram [T|r]^T W [T|r] in the original column order:
@@ -193,6 +195,30 @@ struct KpGroup {  // instances sharing k_gram's tiles-per-wave T (launched toget
     } while (0)
 
 // ---------------------------------------------------------------------------------
+// Per-workgroup timeline of the fit step's kernels (diagnostic: pint_debug_read 7 reads it,
+// 8 switches it on or off and clears it; scripts/diag/wg_timeline.py): workgroup b of
+// kernel k stores its first stamp (s_memrealtime, 100 MHz) from thread 0, and every wave
+// raises its exit stamp with an atomic max when it leaves.  Off: one scalar flag load per
+// workgroup.
+// ---------------------------------------------------------------------------------
+constexpr int WGT_K = 12, WGT_B = 2048;
+enum { WGT_EVAL = 0, WGT_GRAMV, WGT_GRED, WGT_SCHUR, WGT_SOLVE, WGT_RES1, WGT_RES2, WGT_WSOLVE, WGT_COV, WGT_NOISE,
+       WGT_EXPORT, WGT_OTHER };
+__device__ int g_wgt_on;
+__device__ unsigned long long g_wgt[WGT_K * WGT_B * 2];
+struct WgTimer {
+    int slot;  // (k * WGT_B + b) * 2, or -1 when off / beyond WGT_B
+    __device__ __forceinline__ explicit WgTimer(int k) {
+        const int b = blockIdx.y * gridDim.x + blockIdx.x;
+        slot = (__builtin_amdgcn_readfirstlane(g_wgt_on) && b < WGT_B) ? (k * WGT_B + b) * 2 : -1;
+        if (slot >= 0 && threadIdx.x == 0) g_wgt[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ ~WgTimer() {
+        if (slot >= 0 && (threadIdx.x & 63) == 0) atomicMax(&g_wgt[slot + 1], __builtin_amdgcn_s_memrealtime());
+    }
+};
+
+// ---------------------------------------------------------------------------------
 // wave / block reductions (64-wide waves)
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
@@ -249,6 +275,26 @@ __device__ void block_sums(double* v, double* sh) {
 #pragma unroll
         for (int i = 0; i < NW; i++) t += sh[k * NW + i];
         v[k] = t;
+    }
+}
+
+// dst[e] = src[e], e < n, by NT threads, U loads per thread in flight before their stores:
+// a copy loop of one load per iteration waits on each load in turn (a 100 KB LDS stage of
+// the solve took ~5 us that way)
+template <int NT, int U, typename D>
+__device__ __forceinline__ void copy_in(D* __restrict__ dst, const double* __restrict__ src, int n, int tid) {
+    for (int base = 0; base < n; base += NT * U) {
+        double t[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = base + tid + u * NT;
+            t[u] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = base + tid + u * NT;
+            if (e < n) dst[e] = t[u];
+        }
     }
 }
 
@@ -350,7 +396,15 @@ struct EvalLds {
     InstConst C;
     ColRun R[EVAL_MAXRUN];
     double P[EVAL_MAXTAB];
+    double X[4];    // fused residual pass: the TZR row's and row 0's phase (hi, lo)
+    double red[8];  // fused residual pass: block_sums<4, 2>
 };
+// The residual pass's first half (k_resid1) fused into the evaluation (EvalRestore::epart):
+// each 256-thread block evaluates EF_ROWS rows of its instance plus, on its last two lanes,
+// row 0 and the TZR row (row n) -- 2 of 256 lanes of extra work -- so it forms its rows'
+// phase residuals and their weighted sums itself instead of a k_resid1 launch after the
+// evaluation (k_resid1's operations per row; the sums per block of EF_ROWS rows).
+constexpr int EF_ROWS = 254;
 
 // restore targets of an evaluation that reads the parameter snapshot (pint_restore_tables): the
 // first block of each instance writes the snapshot's table and constants back (k_prep's work
@@ -358,7 +412,77 @@ struct EvalLds {
 struct EvalRestore {
     double* tables;
     InstConst* ic;
+    double* rph;    // fused residual pass (null: k_resid1 follows): phase residuals (output rows)
+    double* epart;  // ... and the blocks' (sum w, sum w x) partials
 };
+
+// the TOA inputs of row r (row n: the TZR TOA)
+__device__ __forceinline__ void load_toa_row(const PsrDev& Pd, const pint_spec_t& S, unsigned r, ToaRow& t) {
+    t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
+    t.freq = Pd.freq[r];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        t.pos[k] = Pd.pos[3 * r + k];
+        t.vel[k] = Pd.vel[3 * r + k];
+        t.sun[k] = Pd.sun[3 * r + k];
+    }
+    t.planet = S.shapiro == 2 ? Pd.planet + 15 * r : nullptr;
+    t.flags = Pd.flags[r];
+    t.jmask = Pd.jmask[r];
+    t.dmx_a = Pd.dmx_a[r];
+    t.dmx_b = Pd.dmx_b[r];
+    t.dmx_x = Pd.dmx_x;
+    t.dmx_x0 = Pd.dmx_x ? Pd.dmx_x[r] : 0;
+    t.dmx_x1 = Pd.dmx_x ? Pd.dmx_x[r + 1] : 0;
+}
+
+// one row of eval_block: the row's evaluation and its outputs (own: this lane writes them)
+template <int WANT_M, int BIN>
+__device__ __forceinline__ void eval_row(const pint_spec_t& S, EvalLds& L, const PsrDev& Pd, const InstDev& I, bool stP,
+                                         bool stR, int nrun, const double* __restrict__ tables, unsigned r, int n,
+                                         bool own, double* __restrict__ Mout, double* __restrict__ dmxv, int compact,
+                                         int write_red, int* __restrict__ status, int* __restrict__ istatus, int ii,
+                                         double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                         double* __restrict__ ftay, double* __restrict__ delay_out,
+                                         double* __restrict__ dfac, EvalOut& o) {
+    const double* P = stP ? L.P : tables + I.toff;
+    ToaRow t;
+    load_toa_row(Pd, S, r, t);
+    double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
+    const bool rowM = WANT_M && own && r < (unsigned)n;
+    const bool cmp = WANT_M && compact && Pd.dsplit;
+    eval_toa<BIN>(S, P, L.C, t, o, rowM ? Mb : nullptr, r, n, stR ? L.R : Pd.runs, nrun, cmp);
+    if (!own) return;
+    if (rowM && cmp) dmxv[I.ooff + r] = o.dmc;
+    if (o.status) {  // the batch's status word and this instance's own (pint_inst_status)
+        atomicOr(status, 1 << o.status);
+        atomicOr(istatus + ii, 1 << o.status);
+    }
+    ph_hi[I.roff + r] = o.phase.hi;
+    ph_lo[I.roff + r] = o.phase.lo;
+    ftay[I.roff + r] = o.ftaylor;
+    delay_out[I.roff + r] = o.delay;
+    const bool dmn = S.dmn0 < S.nred;  // PLDMNoise modes: rescaled per TOA, rewritten every time
+    const double Dfac = 1400.0 * 1400.0 * o.inv_f2;
+    if (WANT_M && rowM && dmn) dfac[I.ooff + r] = Dfac;
+    if (WANT_M && rowM && S.nred > 0 && (write_red || dmn) && !(cmp && Pd.vg)) {  // vg: generated where used
+        // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
+        // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.  The basis
+        // does not depend on the timing parameters: it is written once per instance and
+        // layout (write_red) and stays resident in M across fit iterations.
+        dd ts = dd_mul_d(t.tdb, DAYSEC);
+        double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
+        for (int k = write_red ? 0 : S.dmn0; k < S.nred; k++) {
+            dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
+            double fr = dd_to_d(dd_sub(x, dd_floor(x)));
+            double sn, cs;
+            sincos(TWO_PI * fr, &sn, &cs);
+            const double sc = k >= S.dmn0 ? Dfac : 1.0;
+            colp[2L * k * n + r] = sn * sc;
+            colp[2L * k * n + r + n] = cs * sc;
+        }
+    }
+}
 
 template <int WANT_M, int BIN>
 __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
@@ -400,60 +524,134 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
         for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cs[k];
     }
     const pint_spec_t& S = L.S;
-    const unsigned r = (unsigned)(blk_row0[b] + threadIdx.x);
     const int n = I.n;
-    if (r > (unsigned)n) return;
-    const double* P = stP ? L.P : tables + I.toff;
-    ToaRow t;
-    t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
-    t.freq = Pd.freq[r];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        t.pos[k] = Pd.pos[3 * r + k];
-        t.vel[k] = Pd.vel[3 * r + k];
-        t.sun[k] = Pd.sun[3 * r + k];
+    const bool ef = rs.epart != nullptr;  // (launch-uniform) the fused residual pass
+    const int lt = threadIdx.x;
+    unsigned r;
+    bool own;  // the row's outputs are this lane's to write
+    if (ef) {
+        r = lt < EF_ROWS ? (unsigned)(blk_row0[b] + lt) : (lt == EF_ROWS ? 0u : (unsigned)n);
+        own = lt < EF_ROWS ? r < (unsigned)n : (lt == EF_ROWS + 1 && blk_row0[b] == 0);
+        if (lt < EF_ROWS && r >= (unsigned)n) r = 0;  // (an idle lane of the last block: evaluates row 0, writes nothing)
+    } else {
+        r = (unsigned)(blk_row0[b] + lt);
+        own = r <= (unsigned)n;
+        if (!own) return;
     }
-    t.planet = S.shapiro == 2 ? Pd.planet + 15 * r : nullptr;
-    t.flags = Pd.flags[r];
-    t.jmask = Pd.jmask[r];
-    t.dmx_a = Pd.dmx_a[r];
-    t.dmx_b = Pd.dmx_b[r];
-    t.dmx_x = Pd.dmx_x;
-    t.dmx_x0 = Pd.dmx_x ? Pd.dmx_x[r] : 0;
-    t.dmx_x1 = Pd.dmx_x ? Pd.dmx_x[r + 1] : 0;
     EvalOut o;
-    double* Mb = WANT_M ? (Mout + I.moff) : nullptr;  // wave-uniform column base
-    const bool rowM = WANT_M && r < (unsigned)n;
-    const bool cmp = WANT_M && compact && Pd.dsplit;
-    eval_toa<BIN>(S, P, L.C, t, o, rowM ? Mb : nullptr, r, n, stR ? L.R : Pd.runs, nrun, cmp);
-    if (rowM && cmp) dmxv[I.ooff + r] = o.dmc;
-    if (o.status) {  // the batch's status word and this instance's own (pint_inst_status)
-        atomicOr(status, 1 << o.status);
-        atomicOr(istatus + ii, 1 << o.status);
+    eval_row<WANT_M, BIN>(S, L, Pd, I, stP, stR, nrun, tables, r, n, own, Mout, dmxv, compact, write_red, status, istatus,
+                          ii, ph_hi, ph_lo, ftay, delay_out, dfac, o);
+    if (!ef) return;
+    // ---- the fused k_resid1 (residuals.py:314-425): tz and d0 from the block's own TZR and
+    //      row-0 lanes, then k_resid1's per-row operations and the block's weighted sums ----
+    if (lt == EF_ROWS) {
+        L.X[2] = o.phase.hi;
+        L.X[3] = o.phase.lo;
+    } else if (lt == EF_ROWS + 1) {
+        L.X[0] = o.phase.hi;
+        L.X[1] = o.phase.lo;
     }
-    ph_hi[I.roff + r] = o.phase.hi;
-    ph_lo[I.roff + r] = o.phase.lo;
-    ftay[I.roff + r] = o.ftaylor;
-    delay_out[I.roff + r] = o.delay;
-    const bool dmn = S.dmn0 < S.nred;  // PLDMNoise modes: rescaled per TOA, rewritten every time
-    const double Dfac = 1400.0 * 1400.0 * o.inv_f2;
-    if (WANT_M && rowM && dmn) dfac[I.ooff + r] = Dfac;
-    if (WANT_M && rowM && S.nred > 0 && (write_red || dmn) && !(cmp && Pd.vg)) {  // vg: generated where used
-        // PLRedNoise Fourier basis (noise_model.py:861-880): F[:,2k]=sin(2pi t f_k),
-        // F[:,2k+1]=cos(...), t = tdbld*86400 s.  Argument reduced exactly in dd.  The basis
-        // does not depend on the timing parameters: it is written once per instance and
-        // layout (write_red) and stays resident in M across fit iterations.
-        dd ts = dd_mul_d(t.tdb, DAYSEC);
-        double* colp = Mb + (long)(cmp ? Pd.red0c : S.ncol) * n;
-        for (int k = write_red ? 0 : S.dmn0; k < S.nred; k++) {
-            dd x = dd_mul(ts, dd_make(Pd.red_freq[k], Pd.red_freq[S.nred + k]));
-            double fr = dd_to_d(dd_sub(x, dd_floor(x)));
-            double sn, cs;
-            sincos(TWO_PI * fr, &sn, &cs);
-            const double sc = k >= S.dmn0 ? Dfac : 1.0;
-            colp[2L * k * n + r] = sn * sc;
-            colp[2L * k * n + r + n] = cs * sc;
+    __syncthreads();
+    const dd tz = dd_make(L.X[0], L.X[1]);
+    dd d0 = dd_make(0.0);
+    if (!S.track_pn && S.subtract_mean) d0 = dd_add_d(dd_sub(dd_make(L.X[2], L.X[3]), tz), Pd.dpn[0]);
+    double sw = 0.0, swx = 0.0;
+    if (lt < EF_ROWS && own) {
+        const dd d = dd_add_d(dd_sub(dd_make(o.phase.hi, o.phase.lo), tz), Pd.dpn[r]);
+        double full;
+        if (S.track_pn) {
+            full = dd_to_d(dd_add_d(d, -Pd.pn[r]));
+        } else {
+            const dd x = dd_sub(d, d0);
+            full = dd_to_d(dd_sub(x, dd_round_half_up(x)));
         }
+        rs.rph[I.roff - ii + r] = full;
+        const double lw = Pd.isig[r];
+        const double w = S.weighted_mean ? lw * lw : 1.0;
+        sw += w;
+        swx += w * full;
+    }
+    if (S.subtract_mean) {
+        double v[2] = {swx, sw};
+        block_sums<4, 2>(v, L.red);
+        if (lt == 0) {
+            const long eb = I.eb0 + blk_row0[b] / EF_ROWS;
+            rs.epart[2 * eb] = v[1];
+            rs.epart[2 * eb + 1] = v[0];
+        }
+    }
+}
+
+// Spin-only grids (pint_set_grid's variables all spin frequencies, isolated model, no
+// red-noise basis, the full layout): before the first fit step every point shares its
+// delays, astrometric geometry and dispersion factors (they depend on the TOAs and the
+// non-spin parameters only), so k_eval_head evaluates them once, on the batch's first
+// point, with eval_toa's own operations (eval_pre), and k_eval_spin gives each point only
+// eval_toa's spin part (eval_spin_a/b: spin phase and frequencies, the chain factor, the
+// design-matrix row).  The same operations on the same values as the full evaluation of
+// each point: the same bits (test_spin_grid_eval_matches_full).
+__global__ __launch_bounds__(256) void k_eval_head(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   const double* __restrict__ tables, const InstConst* __restrict__ ic,
+                                                   double* __restrict__ shr) {
+    const InstDev I = insts[0];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const unsigned r = blockIdx.x * 256 + threadIdx.x;
+    if (r > (unsigned)I.n) return;
+    ToaRow t;
+    load_toa_row(Pd, S, r, t);
+    EvalHead h;
+    eval_head(S, tables + I.toff, ic[0], t, h);
+    double* o = shr + (long)r * EVAL_HEAD_W;
+    o[0] = h.delay;
+    o[1] = h.gLON;
+    o[2] = h.gLAT;
+    o[3] = h.gPMLON;
+    o[4] = h.gPMLAT;
+    o[5] = h.gPX;
+    o[6] = h.inv_f2;
+    o[7] = h.dt_yr_dm;
+    o[8] = h.logf;
+}
+
+// a wave per point, lanes over its rows
+__global__ __launch_bounds__(256) void k_eval_spin(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                   int ninst, const double* __restrict__ tables,
+                                                   const InstConst* __restrict__ ic, const double* __restrict__ shr,
+                                                   double* __restrict__ ph_hi, double* __restrict__ ph_lo,
+                                                   double* __restrict__ ftay, double* __restrict__ delay_out,
+                                                   double* __restrict__ Mout) {
+    const int ii = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (ii >= ninst) return;  // (wave-uniform)
+    const InstDev I = insts[ii];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const InstConst C = ic[ii];
+    const double* P = tables + I.toff;
+    const int n = I.n;
+    double* Mb = Mout + I.moff;
+    for (int r = threadIdx.x & 63; r <= n; r += 64) {
+        ToaRow t;
+        t.tdb = dd_make(Pd.tdb_hi[r], Pd.tdb_lo[r]);
+        t.jmask = Pd.jmask[r];
+        t.dmx_a = Pd.dmx_a[r];
+        t.dmx_b = Pd.dmx_b[r];
+        t.dmx_x = Pd.dmx_x;
+        t.dmx_x0 = Pd.dmx_x ? Pd.dmx_x[r] : 0;
+        t.dmx_x1 = Pd.dmx_x ? Pd.dmx_x[r + 1] : 0;
+        const double* q = shr + (long)r * EVAL_HEAD_W;
+        const EvalHead h = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
+        EvalOut o;
+        o.status = 0;
+        o.dmc = 0.0;
+        o.inv_f2 = h.inv_f2;
+        EvalSpin sp;
+        eval_spin_a(S, P, C, t, h.delay, o, sp);
+        eval_spin_b<0>(S, P, C, t, h, sp, o, r < n ? Mb : nullptr, (unsigned)r, n, Pd.runs, Pd.nrun, false);
+        ph_hi[I.roff + r] = o.phase.hi;
+        ph_lo[I.roff + r] = o.phase.lo;
+        ftay[I.roff + r] = o.ftaylor;
+        delay_out[I.roff + r] = o.delay;
     }
 }
 
@@ -512,6 +710,7 @@ __device__ __forceinline__ void eval_mix_body(const PsrDev* __restrict__ psrs, c
         compact, write_red, status, istatus, dfac, rs
 template <int WANT_M>
 __global__ __launch_bounds__(256) void k_eval_mix(PINT_EVAL_MIX_ARGS) {
+    WgTimer wgt_(WGT_EVAL);
     eval_mix_body<WANT_M>(PINT_EVAL_MIX_PASS);
 }
 // the same with the register budget of W resident waves per SIMD: the evaluation with the
@@ -519,6 +718,7 @@ __global__ __launch_bounds__(256) void k_eval_mix(PINT_EVAL_MIX_ARGS) {
 // so a third wave per SIMD hides more than its 108 B of spills cost (PINT_EVAL_WPE)
 template <int WANT_M, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void k_eval_mix_w(PINT_EVAL_MIX_ARGS) {
+    WgTimer wgt_(WGT_EVAL);
     eval_mix_body<WANT_M>(PINT_EVAL_MIX_PASS);
 }
 
@@ -543,6 +743,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
                                                    const int* __restrict__ rblk_inst, int nrblk,
                                                    const double* __restrict__ ph_hi, const double* __restrict__ ph_lo,
                                                    double* __restrict__ rphase, double* __restrict__ rpart) {
+    WgTimer wgt_(WGT_RES1);
     constexpr int NW = BT / 64;
     __shared__ double sh[2 * (RES_BT / 64)];
     const int rb = blockIdx.x * (RES_BT / BT) + (BT == RES_BT ? 0 : (int)__builtin_amdgcn_readfirstlane(threadIdx.x / BT));
@@ -618,7 +819,9 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
                                                    const int* __restrict__ rblk_inst, int nrblk,
                                                    const double* __restrict__ ftay,
                                                    double* __restrict__ rtime, double* __restrict__ rphase,
-                                                   double* __restrict__ rpart, double* __restrict__ wtile) {
+                                                   double* __restrict__ rpart, double* __restrict__ wtile,
+                                                   const double* __restrict__ epart) {
+    WgTimer wgt_(WGT_RES2);
     constexpr int NW = BT / 64;
     __shared__ double sh[2 * (RES_BT / 64)];
     extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS: A (columns 0-15), B (16-31)
@@ -653,9 +856,16 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     double mean = 0.0;
     if (S.subtract_mean) {  // residuals.py:314-425 weighted mean (utils.py:2002), fixed tree order
         double a = 0.0, b = 0.0;
-        for (int k = tid; k < I.nrb; k += BT) {
-            b += rpart[3 * (I.rb0 + k)];
-            a += rpart[3 * (I.rb0 + k) + 1];
+        if (epart) {  // the evaluation's fused residual pass: its blocks' partials
+            for (int k = tid; k < I.neb; k += BT) {
+                b += epart[2 * (I.eb0 + k)];
+                a += epart[2 * (I.eb0 + k) + 1];
+            }
+        } else {
+            for (int k = tid; k < I.nrb; k += BT) {
+                b += rpart[3 * (I.rb0 + k)];
+                a += rpart[3 * (I.rb0 + k) + 1];
+            }
         }
         double v[2] = {a, b};
         block_sums<NW, 2>(v, sh);
@@ -1546,6 +1756,7 @@ struct GvResid {
     const double* ftay;   // Taylor factors (n + 1 rows per instance)
     const double* rpart;  // residual blocks' (sum w, sum w x, -)
     int on;
+    const double* epart;  // (non-null) the fused residual pass's partials instead, 2 per evaluation block
 };
 
 template <int NTR, int NTC, int NSK, bool VB>
@@ -1599,7 +1810,12 @@ __device__ __forceinline__ void gram_v_body(double* lds, const PsrDev* __restric
     double mean_r = 0.0;
     if (fr && wave == 0) {
         double a = 0.0, b = 0.0;
-        if (lane < I.nrb) {
+        if (R.epart) {
+            if (lane < I.neb) {
+                b = R.epart[2 * (I.eb0 + lane)];
+                a = R.epart[2 * (I.eb0 + lane) + 1];
+            }
+        } else if (lane < I.nrb) {
             b = R.rpart[3 * (I.rb0 + lane)];
             a = R.rpart[3 * (I.rb0 + lane) + 1];
         }
@@ -1923,6 +2139,7 @@ __global__ __launch_bounds__(GW * 64, GWG) void k_gram_v(const PsrDev* __restric
                                                     double* __restrict__ Gpart, double* __restrict__ Sdp,
                                                     double* __restrict__ colsq, double* __restrict__ TSp,
                                                     double* __restrict__ BFp, int dbg, GvResid R) {
+    WgTimer wgt_(WGT_GRAMV);
     extern __shared__ double lds[];
     const PsrDev& Pd = psrs[insts[blockIdx.y].psr];
     const int nsk = __builtin_amdgcn_readfirstlane(NTR - (Pd.red0c + 1 + 15) / 16);
@@ -2296,12 +2513,89 @@ __device__ __forceinline__ void gred_bin(const InstDev& I, const PsrDev& Pd, con
     per = (per + 3) / 4 * 4;
     const int q0 = (int)(lo / per), q1 = cnt > 0 ? (int)((hi - 1) / per) : q0 - 1;
     const double* part = g.Sdp + I.vgoff + (long)(a % Pd.vns) * SW;
-    for (int c = lane; c <= Kc; c += 64) {
+    // Every load of the bin is issued before its sums (a bin's rows fall in at most two
+    // N-splits but for bins longer than a split, GW wave quarters each): the partials of the
+    // lane's two columns for the first two splits and the bin's first GRB_R rows per lane,
+    // predicated, then summed in the loops' order (q, then w ascending; rows ascending) -- the
+    // same operations in the same order as one dependent load per term, so the same bits
+    // (that form waited on each load in turn: ~2 x GW dependent round trips per column).
+    constexpr int GRB_R = 4;
+    const bool vbp = g.vb && Pd.vb;
+    double dcs[2][2 * GW][2];
+    bool use[2 * GW];
+    long doff[2 * GW];
+#pragma unroll
+    for (int k = 0; k < 2 * GW; k++) {
+        const int q = q0 + k / GW, w = k % GW;
+        const long s0_ = (long)q * per, s1_ = min((long)I.n, s0_ + per), len = s1_ - s0_;
+        const long QV = (len + VCH - 1) / VCH * 16;
+        const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
+        use[k] = q <= q1 && !(w0 >= w1 || hi <= w0 || lo >= w1);  // (a row of the bin in quarter (q, w))
+        doff[k] = I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
+    }
+    double xr[GRB_R], sr[GRB_R];
+#pragma unroll
+    for (int u = 0; u < GRB_R; u++) {
+        const long i = lo + lane + 64 * u;
+        xr[u] = i < hi ? g.dmxv[I.ooff + i] : 0.0;
+        sr[u] = i < hi ? Pd.isig[i] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int c = lane + 64 * t;
+        const bool fc = vbp && c >= r0 && c < Kc;
+        int e0 = 0, e1 = 0;
+        if (fc) {
+            const int h = (c - r0) >> 1, k = h + 1, a_ = k & 7, cc = k >> 3;
+            const bool isin = ((c - r0) & 1) == 0;
+            e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
+            e1 = isin ? a_ * 8 + 4 + cc : (8 + a_) * 8 + 4 + cc;
+        }
+#pragma unroll
+        for (int k = 0; k < 2 * GW; k++) {
+            const bool ld = c <= Kc && (fc ? use[k] : (k % GW == 0 && q0 + k / GW <= q1));
+            dcs[t][k][0] = ld ? (fc ? g.BFp[doff[k] + e0] : part[(long)(q0 + k / GW) * Pd.vns * SW + c]) : 0.0;
+            dcs[t][k][1] = (ld && fc) ? g.BFp[doff[k] + e1] : 0.0;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int c = lane + 64 * t;
+        if (c > Kc) break;
         double v = 0.0;
-        if (g.vb && Pd.vb && c >= r0 && c < Kc) {
+        if (vbp && c >= r0 && c < Kc) {
             // binned DMX x F (k_gram_v VB): the 16x8 blocks D of the (split, wave) quarters
             // the bin's rows touch; harmonic k = a_ + 8 cc: cos = D[a_][cc] - D[8+a_][4+cc],
             // sin = D[8+a_][cc] + D[a_][4+cc]; column r0 + 2h is sin((h+1) theta), +1 cos
+            const bool isin = ((c - r0) & 1) == 0;
+            const double sg = isin ? 1.0 : -1.0;
+#pragma unroll
+            for (int k = 0; k < 2 * GW; k++)
+                if (use[k]) v += dcs[t][k][0] + sg * dcs[t][k][1];
+            for (int q = q0 + 2; q <= q1; q++) {  // (a bin longer than a split: the rest in place)
+                const int h = (c - r0) >> 1, kk = h + 1, a_ = kk & 7, cc = kk >> 3;
+                const int e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
+                const int e1 = isin ? a_ * 8 + 4 + cc : (8 + a_) * 8 + 4 + cc;
+                const long s0_ = (long)q * per, s1_ = min((long)I.n, s0_ + per), len = s1_ - s0_;
+                const long QV = (len + VCH - 1) / VCH * 16;
+                for (int w = 0; w < GW; w++) {
+                    const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
+                    if (w0 >= w1 || hi <= w0 || lo >= w1) continue;  // no row of the bin here
+                    const double* D = g.BFp + I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
+                    v += D[e0] + sg * D[e1];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                if (q0 + k <= q1) v += dcs[t][k * GW][0];
+            for (int q = q0 + 2; q <= q1; q++) v += part[(long)q * Pd.vns * SW + c];
+        }
+        g.Sd[I.sdoff + (long)a * Kp + c] = v;
+    }
+    for (int c = lane + 128; c <= Kc; c += 64) {  // (columns past 128: one load at a time)
+        double v = 0.0;
+        if (vbp && c >= r0 && c < Kc) {
             const int h = (c - r0) >> 1, k = h + 1, a_ = k & 7, cc = k >> 3;
             const bool isin = ((c - r0) & 1) == 0;
             const int e0 = isin ? (8 + a_) * 8 + cc : a_ * 8 + cc;
@@ -2312,7 +2606,7 @@ __device__ __forceinline__ void gred_bin(const InstDev& I, const PsrDev& Pd, con
                 const long QV = (len + VCH - 1) / VCH * 16;
                 for (int w = 0; w < GW; w++) {
                     const long w0 = s0_ + w * QV, w1 = min(s1_, w0 + QV);
-                    if (w0 >= w1 || hi <= w0 || lo >= w1) continue;  // no row of the bin here
+                    if (w0 >= w1 || hi <= w0 || lo >= w1) continue;
                     const double* D = g.BFp + I.vboff + (((long)q * GW + w) * Pd.vns + a % Pd.vns) * 128;
                     v += D[e0] + sg * D[e1];
                 }
@@ -2325,7 +2619,15 @@ __device__ __forceinline__ void gred_bin(const InstDev& I, const PsrDev& Pd, con
     // DD = sum (x/sigma)^2 and DCS = sum x^2 over the bin (the whitened DMX column's
     // square norm is the bin's only DMX x DMX entry: k_gram_v skips those tiles)
     double q2 = 0.0, qw = 0.0;
-    for (long i = lo + lane; i < hi; i += 64) {
+#pragma unroll
+    for (int u = 0; u < GRB_R; u++) {
+        if (lo + lane + 64 * u < hi) {
+            const double xx = xr[u], xw = xx * sr[u];
+            q2 += xx * xx;
+            qw += xw * xw;
+        }
+    }
+    for (long i = lo + lane + 64 * GRB_R; i < hi; i += 64) {
         const double xx = g.dmxv[I.ooff + i], xw = xx * Pd.isig[i];
         q2 += xx * xx;
         qw += xw * xw;
@@ -2381,11 +2683,23 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
 #pragma unroll
                     for (int u = 0; u < 32; u++) a[u & 7] += t[u];
                 }
-                for (; q + 8 <= g.nparts; q += 8) {
+                {
+                    // the < 32 remaining partials loaded at once (predicated), then summed in
+                    // rounds of eight and a tail into chain 0 as one load at a time would be
+                    const int rem = g.nparts - q;
+                    double t[31];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) a[u] += G[(long)(q + u) * KK + e];
+                    for (int u = 0; u < 31; u++) t[u] = u < rem ? G[(long)(q + u) * KK + e] : 0.0;
+#pragma unroll
+                    for (int r = 0; r < 3; r++)
+                        if (8 * r + 8 <= rem) {
+#pragma unroll
+                            for (int u = 0; u < 8; u++) a[u] += t[8 * r + u];
+                        }
+#pragma unroll
+                    for (int u = 0; u < 31; u++)
+                        if (u >= (rem & ~7) && u < rem) a[0] += t[u];
                 }
-                for (; q < g.nparts; q++) a[0] += G[(long)q * KK + e];
                 G[e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
             }
         }
@@ -2406,11 +2720,21 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
 #pragma unroll
                 for (int u = 0; u < 32; u++) a[u & 3] += t[u];
             }
-            for (; q + 4 <= g.nsplit; q += 4) {
+            {
+                const int rem = g.nsplit - q;
+                double t[31];
 #pragma unroll
-                for (int u = 0; u < 4; u++) a[u] += cs[q + u];
+                for (int u = 0; u < 31; u++) t[u] = u < rem ? cs[q + u] : 0.0;
+#pragma unroll
+                for (int r = 0; r < 7; r++)
+                    if (4 * r + 4 <= rem) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) a[u] += t[4 * r + u];
+                    }
+#pragma unroll
+                for (int u = 0; u < 31; u++)
+                    if (u >= (rem & ~3) && u < rem) a[0] += t[u];
             }
-            for (; q < g.nsplit; q++) a[0] += cs[q];
             cs[0] = (a[0] + a[1]) + (a[2] + a[3]);
         }
     }
@@ -2425,6 +2749,7 @@ __device__ __forceinline__ void gred_elem(const InstDev& I, const PsrDev& Pd, co
 //   sin a cos b = (S_a+b + S_a-b)/2     (S_-k = -S_k),
 __global__ __launch_bounds__(256) void k_greduce(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                  int nbg, GredArgs g) {
+    WgTimer wgt_(WGT_GRED);
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
     const bool vg = g.compact && Pd.dsplit && Pd.vg;
@@ -2960,6 +3285,76 @@ __device__ __forceinline__ bool blk_cholinv(double* A, int nb, int wave, int lan
     return true;
 }
 
+// blk_cholinv with look-ahead (k_solve_dmx): the same operations on the same blocks in the
+// same order -- each block's trailing updates T_0..T_k, its panel, its diagonal factor, X's
+// block rows -- so the same X, scheduled in two phases per block column k:
+//   A: the panels L_ik = A_ik L_kk^-T (i > k) and, on further waves, X's block row k
+//      (X_kj = -X_kk sum_{m=j..k-1} L_km X_mj, j < k) in registers;
+//   B: wave 0 applies T_k to block (k+1, k+1) and factors it at once while the other waves
+//      apply T_k to the rest; X's row k is stored over L's (no longer read).
+// Two barriers per block column instead of three, the diagonal factor k+1 beside the rest of
+// T_k, and no separate X loop after the factorisation (round 5: 27.6 us for five 16 x 16
+// blocks, 4.6 of them X's rows).  Needs NW >= nb - 1.
+template <int NW>
+__device__ __forceinline__ bool blk_cholinv_la(double* A, int nb, int wave, int lane, int* sflag) {
+    TS(9);
+    if (wave == 0) {
+        const bool ok = diag_factor<16>(A, lane);
+        if (!ok && lane == 0) *sflag = 1;
+    }
+    TS(10);
+    bsync<NW>();
+    TS(11);
+    for (int k = 0; k < nb; k++) {
+        if (*sflag) return false;  // (uniform: read after a barrier)
+        const int npan = nb - k - 1;
+        const bool xrow = wave >= npan && wave - npan < k;  // X_kj, j = wave - npan
+        double4_t xacc = {0, 0, 0, 0};
+        if (wave < npan) {
+            double* Aik = A + lblk(k + 1 + wave, k);
+            double4_t acc = {0, 0, 0, 0};
+            bmma<false, false>(acc, Aik, A + lblk(k, k), lane, false);
+            bstore(Aik, acc, lane, 1.0);
+        } else if (xrow) {
+            const int j = wave - npan;
+            double4_t acc = {0, 0, 0, 0};
+            for (int m = j; m < k; m++) bmma<false, true>(acc, A + lblk(k, m), A + lblk(m, j), lane, false);
+            bmma_reg(xacc, A + lblk(k, k), acc, lane);
+        }
+        bsync<NW>();
+        if (k == 0) TS(12);
+        if (xrow) bstore(A + lblk(k, wave - npan), xacc, lane, -1.0);
+        if (npan > 0) {
+            const int ntr = npan * (npan + 1) / 2;
+            if (wave == 0) {
+                double* Akk = A + lblk(k + 1, k + 1);
+                double4_t acc = bload(Akk, lane);
+                bmma<false, false>(acc, A + lblk(k + 1, k), A + lblk(k + 1, k), lane, true);
+                bstore(Akk, acc, lane, 1.0);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (its lanes' stores before its reads)
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const bool ok = diag_factor<16>(Akk, lane);
+                if (!ok && lane == 0) *sflag = 1;
+            } else {
+                for (int p = wave; p < ntr; p += NW - 1) {
+                    int ii, jj;
+                    tri_decode(p, ii, jj);
+                    double* Aij = A + lblk(k + 1 + ii, k + 1 + jj);
+                    double4_t acc = bload(Aij, lane);
+                    bmma<false, false>(acc, A + lblk(k + 1 + ii, k), A + lblk(k + 1 + jj, k), lane, true);
+                    bstore(Aij, acc, lane, 1.0);
+                }
+            }
+        }
+        bsync<NW>();
+        if (k == 0) TS(13);
+    }
+    TS(14);
+    TS(16);
+    return true;
+}
+
 // U^T W U entry (i, j) of U = [F, 1] (F: sin, cos of harmonics 1..R/2 at 2h, 2h + 1; the ones
 // column at R) from the weighted trig sums C_m = sum w cos m theta, S_m (trigW):
 //   sin a sin b = (C_|a-b| - C_a+b)/2,  cos a cos b = (C_|a-b| + C_a+b)/2,
@@ -3180,6 +3575,150 @@ __global__ __launch_bounds__(NW == 1 ? 256 : NW * 64) void k_solve_blk(const Psr
     if (tid == 0) chi2lin[inst] = rwr - q2;
 }
 
+// k_solve_lanes<KT>: k_solve_blk's solve for instances of at most KT <= 8 columns (a grid's
+// points) with one LANE per instance instead of one wave: 64 instances per wave.  The same
+// normalisation, factor and solve, in the same operations per element where the wave form
+// reduces over lanes in one order and this one in another (the errors' and covariance's
+// sums of squares, the MFMA covariance product, the dot products): the results agree to
+// rounding (test_lane_solve_matches_wave_solve).  A wave per 4-column instance ran ~1,240
+// wave instructions per point (round 5: 204 us of the 65,536-point NGC6440E grid).
+//   A = the normalised normal matrix (fitter.py:1282-1359 WLS / 2164-2202 GLS), L L^T = A by
+//   the diagonal factor's per-pivot operations (rsq2; x = L^-1 in axpy order), C = X^T X,
+//   x = X^T (X b) with one double-double refinement pass when max diag(A) max diag(A^-1)
+//   exceeds REFINE_KAPPA, chi2lin = r^T W r - b^T x.
+template <int KT>
+__global__ __launch_bounds__(64) void k_solve_lanes(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
+                                                    const double* __restrict__ Gpart, const double* __restrict__ colsq,
+                                                    int nsplit, int mode, double* __restrict__ dpars,
+                                                    double* __restrict__ errs, double* __restrict__ cov,
+                                                    double* __restrict__ chi2lin, int* __restrict__ status, int refine,
+                                                    int ninst) {
+    const int inst = blockIdx.x * 64 + threadIdx.x;
+    if (inst >= ninst) return;
+    const InstDev I = insts[inst];
+    const PsrDev& Pd = psrs[I.psr];
+    const pint_spec_t& S = *Pd.spec;
+    const int Kfull = I.K, ncol = S.ncol;
+    const int K = (mode == 0) ? ncol : Kfull;
+    const double* Gp = Gpart + I.goff;
+    const int Kp = I.Kp;
+    auto G = [&](int i, int j) { return i <= j ? Gp[(long)i * Kp + j] : Gp[(long)j * Kp + i]; };
+    double inv[KT], b[KT], a[KT][KT], x[KT][KT];
+#pragma unroll
+    for (int j = 0; j < KT; j++) {
+        double v = 1.0;
+        if (j < K) {
+            v = sqrt(mode == 0 ? G(j, j) : colsq[(I.coff + j) * nsplit]);
+            v = v == 0.0 ? 1.0 : v;
+        }
+        inv[j] = 1.0 / v;
+    }
+    auto Aij = [&](int i, int j) {
+        double v = G(i, j) * (inv[i] * inv[j]);
+        if (i == j && mode == 1 && i >= ncol) v += (inv[i] * inv[i]) / Pd.red_phi[i - ncol];
+        return v;
+    };
+#pragma unroll
+    for (int i = 0; i < KT; i++) {
+        b[i] = i < K ? G(i, Kfull) * inv[i] : 0.0;
+#pragma unroll
+        for (int j = 0; j < KT; j++) {
+            a[i][j] = (i < K && j < K) ? Aij(i, j) : (i == j ? 1.0 : 0.0);
+            x[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    }
+    const double rwr = G(Kfull, Kfull);
+    // Cholesky and X = L^-1 (diag_factor's per-pivot operations: row r of the wave form is a[r])
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < KT; j++) {
+        const double djj = a[j][j];
+        ok = ok && (djj > 0.0);
+        const double il = rsq2(djj);
+#pragma unroll
+        for (int r = 0; r < KT; r++) {
+            a[r][j] = (r == j) ? djj * il : (r > j ? a[r][j] * il : 0.0);
+            x[r][j] *= il;
+        }
+#pragma unroll
+        for (int c = j + 1; c < KT; c++) {
+            const double Lcj = a[c][j];
+#pragma unroll
+            for (int r = 0; r < KT; r++) {
+                a[r][c] -= a[r][j] * Lcj;
+                x[r][c] -= Lcj * x[r][j];
+            }
+        }
+    }
+    if (!ok) {
+        atomicOr(status, 1 << PINT_E_NOT_PD);
+        return;
+    }
+    // x[r][t] = (L^-1)[t][r] (lane r of the wave form held column r of X): X[t][r] = x[r][t]
+    // covariance of the timing block C = X^T X / (n n^T)
+    double* C = cov + (long)I.cvoff;
+    double amax = 0.0, vmax = 0.0;
+#pragma unroll
+    for (int r = 0; r < KT; r++) {
+#pragma unroll
+        for (int c = r; c < KT; c++) {
+            if (r < ncol && c < ncol) {
+                double acc = 0.0;
+#pragma unroll
+                for (int m = 0; m < KT; m++) acc += x[r][m] * x[c][m];
+                const double v = acc * (inv[r] * inv[c]);
+                C[(long)r * ncol + c] = v;
+                C[(long)c * ncol + r] = v;
+            }
+        }
+        if (r < K) {
+            double se = 0.0;
+#pragma unroll
+            for (int m = 0; m < KT; m++) se += x[r][m] * x[r][m];
+            errs[I.coff + r] = sqrt(se) * inv[r];
+            vmax = fmax(vmax, se);
+            amax = fmax(amax, Aij(r, r));
+        }
+    }
+    const bool do_ref = refine && amax * vmax > REFINE_KAPPA;
+    double xs[KT], rv[KT];
+#pragma unroll
+    for (int pass = 0; pass <= REFINE_PASSES; pass++) {
+        double yv[KT];
+#pragma unroll
+        for (int g = 0; g < KT; g++) {  // y = X rhs
+            double sy = 0.0;
+#pragma unroll
+            for (int c = 0; c <= g; c++) sy += x[c][g] * (pass == 0 ? b[c] : rv[c]);
+            yv[g] = sy;
+        }
+#pragma unroll
+        for (int g = 0; g < KT; g++) {  // x (+)= X^T y
+            double sx = 0.0;
+#pragma unroll
+            for (int rr = g; rr < KT; rr++) sx += x[g][rr] * yv[rr];
+            xs[g] = (pass == 0 ? 0.0 : xs[g]) + (g < K ? sx : 0.0);
+        }
+        if (pass == REFINE_PASSES || !do_ref) break;
+#pragma unroll
+        for (int g = 0; g < KT; g++) {  // r = b - A x in double-double
+            dd sa = dd_make(0.0);
+            if (g < K)
+                for (int j = 0; j < K; j++) dd_acc(sa, Aij(g, j), xs[j]);
+            rv[g] = g < K ? dd_to_d(dd_sub(dd_make(b[g]), sa)) : 0.0;
+        }
+    }
+    double q2 = 0.0;
+#pragma unroll
+    for (int g = 0; g < KT; g++) {
+        if (g < K) {
+            dpars[I.coff + g] = xs[g] * inv[g];
+            q2 += b[g] * xs[g];
+        }
+    }
+    chi2lin[inst] = rwr - q2;
+}
+
 // ---------------------------------------------------------------------------------
 // k_solve_dmx: the normal equations of the compact fit layout with the DMX block
 // eliminated.  In the normalised system A = [A_dd A_dx; A_xd D] the DMX-DMX block D is
@@ -3352,6 +3891,7 @@ __global__ __launch_bounds__(SCHUR_T) void k_schur(const PsrDev* __restrict__ ps
                                                    int nsplit, int mode, const double* __restrict__ Sd,
                                                    const double* __restrict__ DD, const double* __restrict__ DCS,
                                                    double* __restrict__ xw) {
+    WgTimer wgt_(WGT_SCHUR);
     extern __shared__ double lds[];
     const InstDev I = insts[blockIdx.y];
     const PsrDev& Pd = psrs[I.psr];
@@ -3532,7 +4072,8 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
                                                        int* __restrict__ status, int fuse_sigma, int refine,
                                                        double* __restrict__ xw, const double* __restrict__ ones,
                                                        double* __restrict__ apply_tables, InstConst* __restrict__ apply_ic,
-                                                       double apply_lam, int pre) {
+                                                       double apply_lam, int pre, int la_chol) {
+    WgTimer wgt_(WGT_SOLVE);
     extern __shared__ double lds[];
     __shared__ int sflag;
     __shared__ double sh[2 * NW];  // block_sum / block_max2
@@ -3603,7 +4144,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         // k_schur formed S' = S - U U^T, U, the norms and b'_d in xw (its layout): load them
         const double* o = xw + I.xwoff;
         const int na = (nblkS + nbd * nbk) * 256;
-        for (int e = tid; e < na; e += NW * 64) A[e] = o[e];
+        copy_in<NW * 64, 16>(A, o, na, tid);
         const double* v = o + na;
         for (int e = tid; e < nbd * 16; e += NW * 64) {
             ind[e] = v[e];
@@ -3747,7 +4288,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
     __syncthreads();
     }  // (build)
     TS(2);
-    if (!blk_cholinv<NW>(A, nbd, wave, lane, &sflag)) {
+    if (!(la_chol ? blk_cholinv_la<NW>(A, nbd, wave, lane, &sflag) : blk_cholinv<NW>(A, nbd, wave, lane, &sflag))) {
         if (tid == 0) atomicOr(status, 1 << PINT_E_NOT_PD);
         if (xw) {  // no X/W to export: the deferred covariance of this instance comes out NaN,
                    // not from the previous step's (or uninitialised) export
@@ -3989,6 +4530,7 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                      const double* __restrict__ xw, int mode, double* __restrict__ cov,
                                                      double* __restrict__ errs) {
+    WgTimer wgt_(WGT_COV);
     extern __shared__ double lds[];
     const InstDev I = insts[blockIdx.x];
     const PsrDev& Pd = psrs[I.psr];
@@ -3998,7 +4540,7 @@ __global__ __launch_bounds__(NW * 64) void k_cov_dmx(const PsrDev* __restrict__ 
     const int nbd = (Kd + 15) >> 4, nbk = (ndc + 15) >> 4, nblkS = nbd * (nbd + 1) / 2;
     const int na = (nblkS + nbd * nbk) * 256, nv = na + (nbd + 3 * nbk) * 16;
     const double* src = xw + I.xwoff;
-    for (int e = threadIdx.x; e < nv; e += NW * 64) lds[e] = src[e];
+    copy_in<NW * 64, 16>(lds, src, nv, threadIdx.x);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -4322,6 +4864,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
                                                 double* __restrict__ chi2, double* __restrict__ lognorm,
                                                 const double* __restrict__ wtile, const double* __restrict__ rpart,
                                                 double* __restrict__ chi2w, int compact) {
+    WgTimer wgt_(WGT_WSOLVE);
     extern __shared__ double lds[];
     __shared__ double sh[12];  // block_sums<4, 3>
     __shared__ double Dt[256], wloc[130];
@@ -4341,7 +4884,7 @@ __global__ __launch_bounds__(256) void k_wsolve(const PsrDev* __restrict__ psrs,
     {
         const double* X = sigL + I.soff;
         const int nX = nobasis ? 0 : Kn * (Kn + 1) / 2;
-        for (int e = threadIdx.x; e < nX; e += blockDim.x) Xs[e] = X[e];
+        copy_in<256, 8>(Xs, X, nX, threadIdx.x);
     }
     if (wtile) {
         // r^T W r: the residual pass's chi2 partials of the instance summed exactly as k_rsum
@@ -4519,6 +5062,7 @@ __global__ __launch_bounds__(256) void k_chi2w(const PsrDev* __restrict__ psrs, 
 __global__ __launch_bounds__(256) void k_noise_red(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const double* __restrict__ dpars, double* __restrict__ out,
                                                    int dm, const double* __restrict__ dfac) {
+    WgTimer wgt_(WGT_NOISE);
     __shared__ double sa[256];  // the component's amplitudes (a_k, b_k), staged once per block
     const int inst = blockIdx.y;
     const InstDev I = insts[inst];
@@ -4761,6 +5305,7 @@ struct ExportArgs {
     int* st_dst;
 };
 __global__ __launch_bounds__(256) void k_export(ExportArgs a) {
+    WgTimer wgt_(WGT_EXPORT);
     if (a.st_src && blockIdx.x == 0 && threadIdx.x == 0) *a.st_dst = *a.st_src;
     const long stride = (long)gridDim.x * 256;
     for (int k = 0; k < a.nseg; k++) {
@@ -4873,6 +5418,7 @@ struct pint_ctx {
     int small = 1;       // PINT_OPT_SMALL: k_gram_s / one-wave k_solve_blk for small instances
     int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
     int evalb_wpe = 3;   // PINT_EVALB_WPE: one-model ELL1/DD batches with M at 3 waves/SIMD (0: the compiler's)
+    int la_chol = 1;     // PINT_LA_CHOL: k_solve_dmx's look-ahead blocked Cholesky (0: blk_cholinv; the same bits)
     int eval0_wpe = 1;   // PINT_EVAL0_WPE: the isolated-model build at fixed register budgets (0: the compiler's)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
@@ -4901,6 +5447,16 @@ struct pint_ctx {
     int* d_blk_row0 = nullptr;
     int* d_rblk_inst = nullptr;   // k_resid1/2 block -> instance
     double* d_rpart = nullptr;    // per residual block: sum w, sum w x, chi2 partial
+    double* d_epart = nullptr;    // fused residual pass (efz): per evaluation block sum w, sum w x
+    int efz = 0;                  // the batch's evaluation blocks carry k_resid1 (EF_ROWS rows + row 0 + TZR)
+    int efuse = 1;                // PINT_EFUSE: fuse k_resid1 into the evaluation of large instances
+    int lane_solve = 1;           // PINT_LANE_SOLVE: k_solve_lanes for small-instance batches of K <= 8
+    std::vector<int> upsr;        // the batch's distinct pulsars (host plans loop over these, not instances)
+    int spin_grid = 0;            // the resident grid's points differ in spin parameters only (k_eval_head/_spin)
+    bool tables_fresh = false;    // ... and the tables are still pint_set_grid's (no step applied since)
+    int spin_eval = 1;            // PINT_SPIN_EVAL: use the shared head for such grids
+    double* d_shr = nullptr;      // its rows (EVAL_HEAD_W doubles each)
+    long shr_cap = 0;
     int nrblk = 0;
     int eval_merge = 0;  // bit 0: one k_eval_mix launch without M, bit 1: with M, bit 2: also for a
                          // batch of one model (PINT_EVAL_MERGE)
@@ -5442,6 +5998,10 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->prep_lanes = getenv("PINT_PREP_LANES") ? atoi(getenv("PINT_PREP_LANES")) : 1;
     ctx->resid12 = getenv("PINT_RESID12") ? atoi(getenv("PINT_RESID12")) : 1;
     ctx->evalb_wpe = getenv("PINT_EVALB_WPE") ? atoi(getenv("PINT_EVALB_WPE")) : 3;
+    ctx->la_chol = getenv("PINT_LA_CHOL") ? atoi(getenv("PINT_LA_CHOL")) : 1;
+    ctx->efuse = getenv("PINT_EFUSE") ? atoi(getenv("PINT_EFUSE")) : 1;
+    ctx->lane_solve = getenv("PINT_LANE_SOLVE") ? atoi(getenv("PINT_LANE_SOLVE")) : 1;
+    ctx->spin_eval = getenv("PINT_SPIN_EVAL") ? atoi(getenv("PINT_SPIN_EVAL")) : 1;
     hipEventCreateWithFlags(&ctx->ev_gram, evf);
     hipEventCreateWithFlags(&ctx->ev_sigma, evf);
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
@@ -5470,6 +6030,9 @@ static void free_instances(pint_ctx* ctx) {
         ctx->sorted_alias[l] = false;
     }
     dfree((void*&)ctx->d_gridspec);
+    dfree((void*&)ctx->d_shr);
+    ctx->shr_cap = 0;
+    ctx->spin_grid = 0;
     for (int sl = 0; sl < pint_ctx::NSLOT; sl++) {
         void** pss[] = {(void**)&ctx->d_chi2lin_s[sl], (void**)&ctx->d_dpars_s[sl], (void**)&ctx->d_errs_s[sl],
                         (void**)&ctx->d_cov_s[sl], (void**)&ctx->d_chi2g_s[sl], (void**)&ctx->d_xw_s[sl]};
@@ -5486,7 +6049,7 @@ static void free_instances(pint_ctx* ctx) {
                    (void**)&ctx->d_eW, (void**)&ctx->d_eC, (void**)&ctx->d_ecs, (void**)&ctx->d_wpart, (void**)&ctx->d_ic, (void**)&ctx->d_ic0,
                    (void**)&ctx->d_dmxv, (void**)&ctx->d_Sd, (void**)&ctx->d_DD, (void**)&ctx->d_DCS,
                    (void**)&ctx->d_dfac, (void**)&ctx->d_inst_sorted_c, (void**)&ctx->d_inst_sorted_v, (void**)&ctx->d_Sdp,
-                   (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart,
+                   (void**)&ctx->d_BFp, (void**)&ctx->d_TSp, (void**)&ctx->d_TS, (void**)&ctx->d_rblk_inst, (void**)&ctx->d_rpart, (void**)&ctx->d_epart,
                    (void**)&ctx->d_noise, (void**)&ctx->d_tables0,
                    (void**)&ctx->d_wtile, (void**)&ctx->d_norms, (void**)&ctx->d_ones};
     for (auto p : ps) dfree(*p);
@@ -5912,6 +6475,20 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
     hipLaunchKernelGGL(k_grid_tables, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_gridspec, ts, nvar, npts, (long)k0,
                        ctx->d_tables);
     HIPCHK(hipGetLastError());
+    // points that differ in spin frequencies only share the evaluation's head (k_eval_head)
+    {
+        const PsrHost& ph = ctx->psrs[psr];
+        const pint_spec_t& sp = ph.spec;
+        bool spin = nvar > 0 && sp.binary == 0 && sp.nred == 0 && !ph.dev.dsplit && !ctx->efz;
+        for (int j = 0; j < nvar; j++) spin = spin && var_toff[j] >= sp.o_F && var_toff[j] < sp.o_F + 2 * sp.nf;
+        ctx->spin_grid = spin;
+        if (spin && (long)(ph.n + 1) * EVAL_HEAD_W > ctx->shr_cap) {
+            dfree((void*&)ctx->d_shr);
+            ctx->shr_cap = (long)(ph.n + 1) * EVAL_HEAD_W;
+            HIPCHK(cmalloc((void**)&ctx->d_shr, sizeof(double) * ctx->shr_cap));
+        }
+        ctx->tables_fresh = true;
+    }
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -5919,6 +6496,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
 static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr, const double* tables) {
     if (!ctx || ninst <= 0) return PINT_E_INVALID;
     ctx->grid_valid = false;  // (pint_set_grid marks its own batch afterwards)
+    ctx->tables_fresh = false;
     ctx->r2_pending = false;
     hipSetDevice(ctx->device);
     if (ctx->psrs_dirty && refresh_psrs(ctx)) return PINT_E_HIP;
@@ -5937,6 +6515,10 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
         if (p < 0 || p >= (int)ctx->psrs.size()) { ctx->err = "bad pulsar id"; return PINT_E_INVALID; }
         if (ctx->psrs[p].n > maxN) maxN = ctx->psrs[p].n;
     }
+    // the fused residual pass for batches off the small-instance path (whose one-wave
+    // residual kernels serve instances of <= RES_SMALLN rows)
+    ctx->efz = ctx->efuse && !(ctx->small && maxN <= RES_SMALLN);
+    long ebn = 0;
     // N-split for the Gram so the launch fills the 256 CUs
     // choose the split count that minimises (workgroup rounds) / nsplit, i.e. the k_gram
     // makespan with one 1024-thread workgroup resident per CU, with >= 4 chunks per split
@@ -5978,6 +6560,10 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     }
     // (measured on the 68-pulsar PTA, round 4: 7 splits -- one round of workgroups, many CUs
     // with one -- 0.120 ms of k_gram_v, 8: 0.147, 11: 0.104, this model's 15: 0.089-0.093)
+    if (const char* e = getenv("PINT_NSPLIT")) {  // (diagnostic sweeps: a fixed split count)
+        const int v = atoi(e);
+        if (v >= 1) nsplit = std::min(v, std::max(1, (maxN + 63) / 64));
+    }
     ctx->nsplit = nsplit;
     ctx->red_valid[0] = ctx->red_valid[1] = 0;
     ctx->ic_valid = false;
@@ -6142,9 +6728,21 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
         toff += ph.spec.tstride;
         int bt = ph.spec.binary;
         if (bt < 0 || bt >= PINT_NBIN) { ctx->err = "bad binary model"; return PINT_E_INVALID; }
-        for (int r0 = 0; r0 <= ph.n; r0 += 256) {
-            bti[bt].push_back(k);
-            btr[bt].push_back(r0);
+        if (ctx->efz) {  // EF_ROWS rows per block (+ row 0 and the TZR row on its last lanes)
+            I.eb0 = ebn;
+            I.neb = std::max(1, (ph.n + EF_ROWS - 1) / EF_ROWS);
+            ebn += I.neb;
+            for (int r0 = 0; r0 < std::max(1, ph.n); r0 += EF_ROWS) {
+                bti[bt].push_back(k);
+                btr[bt].push_back(r0);
+            }
+        } else {
+            I.eb0 = 0;
+            I.neb = 0;
+            for (int r0 = 0; r0 <= ph.n; r0 += 256) {
+                bti[bt].push_back(k);
+                btr[bt].push_back(r0);
+            }
         }
         roff += ph.n + 1;
         moff += (long)ph.n * ph.K;
@@ -6169,6 +6767,15 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     for (const InstDev& I : ctx->inst) {
         ctx->maxn = std::max(ctx->maxn, I.n);
         ctx->max_ts = std::max(ctx->max_ts, ctx->psrs[I.psr].spec.tstride);
+    }
+    {
+        std::vector<char> seen(ctx->psrs.size(), 0);
+        ctx->upsr.clear();
+        for (int k = 0; k < ninst; k++)
+            if (!seen[inst_psr[k]]) {
+                seen[inst_psr[k]] = 1;
+                ctx->upsr.push_back(inst_psr[k]);
+            }
     }
     ctx->tot_e = eoff;
     ctx->tot_ep = epoff;
@@ -6288,6 +6895,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     if (!rbi.empty())
         HIPCHK(hipMemcpy(ctx->d_rblk_inst, rbi.data(), sizeof(int) * rbi.size(), hipMemcpyHostToDevice));
     HIPCHK(cmalloc((void**)&ctx->d_rpart, sizeof(double) * 3 * std::max<size_t>(1, rbi.size())));
+    HIPCHK(cmalloc((void**)&ctx->d_epart, sizeof(double) * 2 * std::max<long>(1, ebn)));
     // the post-fit Woodbury dots fused into the residual pass (k_resid2 tiles, k_rsum): every
     // instance's noise basis a PLRedNoise harmonic series of < 64 modes (no PLDMNoise)
     {
@@ -6388,6 +6996,7 @@ int pint_get_tables(pint_ctx* ctx, double* out) {
 
 int pint_set_tables(pint_ctx* ctx, const double* tables) {
     ctx->ic_valid = false;
+    ctx->tables_fresh = false;
     ctx->restore_pending = false;  // overwritten anyway
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
@@ -6459,6 +7068,7 @@ static void launch_prep(pint_ctx* ctx, double* tables, const double* tables0, In
                            tables0, ic);
 }
 static void launch_apply(pint_ctx* ctx, const double* lam, double lam_u) {
+    ctx->tables_fresh = false;
     if (prep_lanes(ctx))
         hipLaunchKernelGGL(k_apply_lanes, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->ninst, ctx->d_tables, ctx->d_dpars, lam, ctx->d_ic, lam_u);
@@ -6470,14 +7080,15 @@ static void launch_apply(pint_ctx* ctx, const double* lam, double lam_u) {
 // k_resid2 of the last residual pass (with wt, the Woodbury trig tiles)
 static void launch_resid2(pint_ctx* ctx, bool wt) {
     const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
-    if (ctx->small && ctx->maxn <= RES_SMALLN)
+    const double* ep = ctx->efz ? ctx->d_epart : nullptr;
+    if (!ctx->efz && ctx->small && ctx->maxn <= RES_SMALLN)
         hipLaunchKernelGGL(k_resid2<64>, dim3((ctx->nrblk + 3) / 4), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
-                           wt ? ctx->d_wtile : nullptr);
+                           wt ? ctx->d_wtile : nullptr, ep);
     else
         hipLaunchKernelGGL(k_resid2<RES_BT>, dim3(ctx->nrblk), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
                            ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_ftay, ctx->d_rt, ctx->d_rp, ctx->d_rpart,
-                           wt ? ctx->d_wtile : nullptr);
+                           wt ? ctx->d_wtile : nullptr, ep);
 }
 
 // The fit layout's residual pass may leave k_resid2 to the Gram (GvResid) when every instance
@@ -6486,7 +7097,7 @@ static void launch_resid2(pint_ctx* ctx, bool wt) {
 // summed on one wave as k_resid2 sums it).  PINT_FUSE_R2=0 keeps k_resid2 in the pass.
 static bool can_defer_r2(const pint_ctx* ctx) {
     return ctx->fuse_r2 && ctx->m_compact && ctx->n_vg == ctx->ninst && ctx->max_nep == 0 && !ctx->wbfit &&
-           ctx->maxn <= 64 * RES_RB;
+           ctx->maxn <= 64 * (ctx->efz ? EF_ROWS : RES_RB);
 }
 
 // a reader of the time/phase residuals or their chi2 partials after a deferred pass
@@ -6518,14 +7129,15 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     record(ctx, want_M ? 2 : 0);
     const double* tabs = ctx->d_tables;
     const InstConst* icp = ctx->d_ic;
-    EvalRestore rs{nullptr, nullptr};
+    EvalRestore rs{nullptr, nullptr, nullptr, nullptr};
     if (!ctx->ic_valid) {  // (k_apply refreshes them itself)
         if (ctx->restore_pending && ctx->ic0_valid) {
             // restore: the evaluation reads the snapshot and its constants (pint_save_tables) and
             // each instance's first block writes them back -- no k_prep launch in a refit step
             tabs = ctx->d_tables0;
             icp = ctx->d_ic0;
-            rs = EvalRestore{ctx->d_tables, ctx->d_ic};
+            rs.tables = ctx->d_tables;
+            rs.ic = ctx->d_ic;
         } else {
             launch_prep(ctx, ctx->d_tables, ctx->restore_pending ? (const double*)ctx->d_tables0 : nullptr, ctx->d_ic);
             HIPCHK(hipGetLastError());
@@ -6533,13 +7145,30 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         ctx->restore_pending = false;
         ctx->ic_valid = true;
     }
+    if (ctx->efz && ctx->nrblk > 0) {  // the residual pass's first half in the evaluation's blocks
+        rs.rph = ctx->d_rp;
+        rs.epart = ctx->d_epart;
+    }
+    // a spin-only grid's first evaluation with the design matrix: the shared head, then each
+    // point's spin part
+    const bool spin_pass = want_M && ctx->spin_grid && ctx->tables_fresh && ctx->spin_eval && rs.tables == nullptr &&
+                           !ctx->efz && ctx->d_shr && ctx->blk_off[PINT_NBIN] == ctx->blk_off[1];
+    if (spin_pass) {
+        const int n1 = ctx->inst[0].n + 1;
+        hipLaunchKernelGGL(k_eval_head, dim3((n1 + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           tabs, icp, ctx->d_shr);
+        hipLaunchKernelGGL(k_eval_spin, dim3((ctx->ninst + 3) / 4), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
+                           ctx->ninst, tabs, icp, ctx->d_shr, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay, ctx->d_delay,
+                           ctx->d_M);
+        HIPCHK(hipGetLastError());
+    }
     // a batch of one model (a grid's points, an all-isolated PTA) takes that model's own
     // build, whose register set the other models do not raise (k_eval<WM, 0>: 48 instead
     // of 84 VGPRs + spills with M for an isolated pulsar); PINT_EVAL_MERGE bit 2 merges anyway
     int ntyp = 0;
     for (int t = 0; t < 3; t++) ntyp += ctx->blk_off[t + 1] > ctx->blk_off[t];
     const bool mix = ((ctx->eval_merge >> (want_M ? 1 : 0)) & 1) && (ntyp > 1 || (ctx->eval_merge & 4));
-    if (mix && ctx->nblk > 0) {
+    if (!spin_pass && mix && ctx->nblk > 0) {
 #define PINT_EVAL_MIX(WM)                                                                                      \
         hipLaunchKernelGGL((k_eval_mix<WM>), dim3(ctx->nblk), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, \
                            ctx->d_blk_inst, ctx->d_blk_row0, ctx->blk_off[1], ctx->blk_off[2], ctx->blk_off[3],   \
@@ -6566,7 +7195,7 @@ int pint_eval(pint_ctx* ctx, int want_M) {
     // one launch per binary model, back to back on the stream: all models without the merged
     // launch; ELL1H/BT/DDK always (they stay out of k_eval_mix so its register set, which
     // every block of the merged launch carries, is not raised by the rarer models)
-    for (int t = mix ? 3 : 0; t < PINT_NBIN; t++) {
+    for (int t = spin_pass ? PINT_NBIN : (mix ? 3 : 0); t < PINT_NBIN; t++) {
         int nb = ctx->blk_off[t + 1] - ctx->blk_off[t];
         if (nb == 0) continue;
         const int* bi = ctx->d_blk_inst + ctx->blk_off[t];
@@ -6619,8 +7248,10 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         // the fit layout's pass on the k_gram_v path: k_resid1 only, the Gram stages the time
         // residuals itself and k_resid2 waits for a reader of them (flush_r2)
         const bool defer2 = want_M == 2 && can_defer_r2(ctx);
-        const bool fused12 = ctx->small && ctx->maxn <= RES_SMALLN && !wt && !defer2 && ctx->resid12;
-        if (fused12) {  // one wave per instance does both passes
+        const bool fused12 = !ctx->efz && ctx->small && ctx->maxn <= RES_SMALLN && !wt && !defer2 && ctx->resid12;
+        if (ctx->efz) {
+            // (k_resid1's work done by the evaluation's blocks)
+        } else if (fused12) {  // one wave per instance does both passes
             hipLaunchKernelGGL(k_resid12, dim3((ctx->nrblk + 3) / 4), dim3(RES_BT), 0, ctx->stream, ctx->d_psrs,
                                ctx->d_inst, ctx->d_rblk_inst, ctx->nrblk, ctx->d_phhi, ctx->d_phlo, ctx->d_ftay,
                                ctx->d_rt, ctx->d_rp, ctx->d_rpart);
@@ -6734,13 +7365,13 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     // solve rewrites them)
     if (int rc = flush_cq_now(ctx)) return rc;
     if (ctx->r2_pending && !can_defer_r2(ctx)) flush_r2(ctx);  // (a kernel below reads d_rt)
-    const GvResid gvr{ctx->d_rp, ctx->d_ftay, ctx->d_rpart, ctx->r2_pending ? 1 : 0};
+    const GvResid gvr{ctx->d_rp, ctx->d_ftay, ctx->d_rpart, ctx->r2_pending ? 1 : 0, ctx->efz ? ctx->d_epart : nullptr};
     if (ctx->wbfit) {
         // k_wb_gram carries at most WB_MAXC free DM-type columns (DM Taylor terms + DMJUMPs):
         // refuse more instead of leaving the extra columns without their DM rows
-        for (auto& I : ctx->inst) {
-            const pint_spec_t& sp = ctx->psrs[I.psr].spec;
-            if (!ctx->psrs[I.psr].dev.wb) continue;
+        for (int pi : ctx->upsr) {
+            const pint_spec_t& sp = ctx->psrs[pi].spec;
+            if (!ctx->psrs[pi].dev.wb) continue;
             int m = 0;
             for (int c = 0; c < sp.ncol; c++) m += (sp.col_kind[c] == PINT_COL_DM || sp.col_kind[c] == PINT_COL_ZERO);
             if (m > WB_MAXC) {
@@ -6770,8 +7401,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     // PhaseOffset with a frozen PHOFF and correlated noise: the Woodbury ones row (k_onesrow)
     const double* ones = nullptr;
     if (mode == 1) {
-        for (auto& I : ctx->inst) {
-            const PsrHost& ph = ctx->psrs[I.psr];
+        for (int pi : ctx->upsr) {
+            const PsrHost& ph = ctx->psrs[pi];
             if (ph.spec.o_PHOFF >= 0 && !ph.spec.wb_noones && (ph.spec.nred > 0 || ph.dev.nep > 0)) ones = ctx->d_ones;
         }
         if (ones) {
@@ -6783,8 +7414,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (cmp && ctx->max_ndc > 0 && ctx->any_dmx_rows) {
         int maxKd = 0;
         bool any_gather = false;
-        for (auto& I : ctx->inst) {
-            const PsrDev& pd = ctx->psrs[I.psr].dev;
+        for (int pi : ctx->upsr) {
+            const PsrDev& pd = ctx->psrs[pi].dev;
             if (pd.dsplit) maxKd = std::max(maxKd, pd.Kd);
             if (pd.dsplit && !pd.dcontig) any_gather = true;
         }
@@ -6915,8 +7546,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     int Ks = 0, Kn = 0, ndmx_inst = 0;
     bool dmx_ok = cmp && ctx->blocked_solve;
     size_t lds_x = 0;
-    for (auto& I : ctx->inst) {
-        const PsrHost& ph = ctx->psrs[I.psr];
+    for (int pi : ctx->upsr) {
+        const PsrHost& ph = ctx->psrs[pi];
         const pint_spec_t& sp = ph.spec;
         const int kn = mode == 1 ? 2 * sp.nred + 1 : 0;
         Kn = std::max(Kn, kn);
@@ -6930,11 +7561,11 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                                                       (size_t)(5 * nbd + 6 * nbk) * 16));
             if (lds_x > 160 * 1024 - 512) dmx_ok = false;  // (the kernel's static LDS beside it)
         } else {
-            Ks = std::max(Ks, mode == 0 ? sp.ncol : I.K);
+            Ks = std::max(Ks, mode == 0 ? sp.ncol : ph.K);
         }
     }
     if (!dmx_ok) {  // every instance through the general solve
-        for (auto& I : ctx->inst) Ks = std::max(Ks, mode == 0 ? ctx->psrs[I.psr].spec.ncol : I.K);
+        for (int pi : ctx->upsr) Ks = std::max(Ks, mode == 0 ? ctx->psrs[pi].spec.ncol : ctx->psrs[pi].K);
         ndmx_inst = 0;
     }
     const int skip = ndmx_inst > 0 ? 1 : 0;
@@ -6945,8 +7576,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
     if (mode == 1) {
         int kn = 0;
         bool any = false;
-        for (auto& I : ctx->inst) {
-            const PsrHost& ph = ctx->psrs[I.psr];
+        for (int pi : ctx->upsr) {
+            const PsrHost& ph = ctx->psrs[pi];
             if (ph.spec.nred > 0 || ph.dev.nep > 0) { any = true; kn = std::max(kn, 2 * ph.spec.nred + 1); }
         }
         nbs_sig = (kn + 15) / 16;
@@ -6959,9 +7590,9 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                  ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_BFp};
     if (nparts > 1 || vgp) {
         int maxKp = 16;
-        for (auto& I : ctx->inst) {
-            const PsrDev& pd = ctx->psrs[I.psr].dev;
-            maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : I.Kp);
+        for (int pi : ctx->upsr) {
+            const PsrDev& pd = ctx->psrs[pi].dev;
+            maxKp = std::max(maxKp, (cmp && pd.dsplit) ? pd.Kpd : pd.Kp);
         }
         // (round 4: the column sums of squares on threads of their own, beside the Gram's
         // chains, measured no faster -- 11.3-11.9 vs 10.5-10.9 us at 9 pulsars)
@@ -7016,8 +7647,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         if (ctx->apply_req && Ks == 0 && !side_sigma && !do_sigma) {
             bool ok = true;
             int maxts = 0;
-            for (auto& I : ctx->inst) {
-                const PsrHost& ph = ctx->psrs[I.psr];
+            for (int pi : ctx->upsr) {
+                const PsrHost& ph = ctx->psrs[pi];
                 ok = ok && cmp && ph.dev.dsplit && ph.dev.vg;
                 maxts = std::max(maxts, ph.spec.tstride);
             }
@@ -7027,6 +7658,7 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 apply_ic = ctx->d_ic;
                 lds_dyn = std::max(lds_dyn, lds_x + apply_tail_lds(maxts));
                 ctx->apply_done = true;
+                ctx->tables_fresh = false;
             }
         }
         // the build phase (norms, S and U, S -= U U^T, b'_d) spread over the chip by k_schur
@@ -7034,8 +7666,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         int pre = 0;
         if (xw && ctx->schur) {
             int mnb = 0, mnk = 0;
-            for (auto& I : ctx->inst) {
-                const PsrDev& pd = ctx->psrs[I.psr].dev;
+            for (int pi : ctx->upsr) {
+                const PsrDev& pd = ctx->psrs[pi].dev;
                 if (!pd.dsplit) continue;
                 const int kd = mode == 0 ? pd.red0c : pd.Kd, nbd = (kd + 15) / 16;
                 mnb = std::max(mnb, nbd * (nbd + 1) / 2);
@@ -7056,7 +7688,8 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                               (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
                               (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
                               ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam, pre);
+                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam, pre,
+                              ctx->la_chol);
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -7071,7 +7704,18 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
         size_t lds_b = sizeof(double) * (size_t)ldsw;
         // K <= 32 (a grid's points): a wave per instance, four per workgroup -- the 4-wave
         // form spent ~27 us of barriers and idle waves on each such instance
-        if (nbx <= 2 && ctx->small)
+        if (nbx <= 1 && ctx->small && ctx->lane_solve && !skip && Ks <= 8) {
+            // K <= 8 (a grid's points): a lane per instance
+            const int KT = Ks <= 4 ? 4 : 8;
+            if (KT == 4)
+                hipLaunchKernelGGL(k_solve_lanes<4>, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                                   ctx->d_inst, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                                   ctx->d_cov, ctx->d_chi2lin, ctx->d_status, ctx->refine, ctx->ninst);
+            else
+                hipLaunchKernelGGL(k_solve_lanes<8>, dim3((ctx->ninst + 63) / 64), dim3(64), 0, ctx->stream, ctx->d_psrs,
+                                   ctx->d_inst, ctx->d_G, ctx->d_colsq, ctx->nsplit, mode, ctx->d_dpars, ctx->d_errs,
+                                   ctx->d_cov, ctx->d_chi2lin, ctx->d_status, ctx->refine, ctx->ninst);
+        } else if (nbx <= 2 && ctx->small)
             hipLaunchKernelGGL(k_solve_blk<1>, dim3((ctx->ninst + 3) / 4), dim3(256), 4 * sizeof(double) * ldsw1,
                                ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_tables, ctx->d_G, ctx->d_colsq,
                                ctx->nsplit, mode, cmp, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_dpars, ctx->d_errs,
@@ -7308,6 +7952,7 @@ int pint_restore_tables(pint_ctx* ctx) {
         return PINT_E_INVALID;
     }
     ctx->ic_valid = false;
+    ctx->tables_fresh = false;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
     // deferred: the next pint_eval's k_prep copies the snapshot back as it forms the
     // per-instance constants (one launch less); every other reader of the tables flushes it
@@ -7329,7 +7974,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
     flush_r2(ctx);
     if (flush_chi2(ctx)) return PINT_E_HIP;
     int R = 0;
-    for (auto& I : ctx->inst) R = 2 * ctx->psrs[I.psr].spec.nred > R ? 2 * ctx->psrs[I.psr].spec.nred : R;
+    for (int pi : ctx->upsr) R = 2 * ctx->psrs[pi].spec.nred > R ? 2 * ctx->psrs[pi].spec.nred : R;
     int stride = R + 2;
     int nsw = ctx->nsplit;  // same N-split as the Gram (fills the CUs)
     if (ctx->wtile_valid) {  // the residual pass formed the dots (k_resid2 tiles -> k_rsum)
@@ -7406,6 +8051,10 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_REFINE) { ctx->refine = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_SCHUR) { ctx->schur = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_SMALL) { ctx->small = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_LA_CHOL) { ctx->la_chol = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_EFUSE) { ctx->efuse = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_LANE_SOLVE) { ctx->lane_solve = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_SPIN_EVAL) { ctx->spin_eval = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_TIMING_EVERY) {
         if (value < 1) return PINT_E_INVALID;
         ctx->timing_every = value;
@@ -7661,6 +8310,22 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
         // comes out negative or beyond the end stamp instead of as an unsigned wrap-around)
         for (int i = 0; i < 32; i++) out[i] = (double)(long long)(ts[i] - ts[0]) * 0.01;
         return 32;
+    }
+    if (which == 7) {  // the per-workgroup timeline (WgTimer), raw 100 MHz ticks
+        static unsigned long long t[WGT_K * WGT_B * 2];
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wgt), sizeof(t)));
+        for (int i = 0; i < WGT_K * WGT_B * 2; i++) out[i] = (double)t[i];
+        return WGT_K * WGT_B * 2;
+    }
+    if (which == 8) {  // the timeline on (out[0] != 0) or off, cleared
+        static unsigned long long z[WGT_K * WGT_B * 2];
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgt), z, sizeof(z)));
+        const int on = out && out[0] != 0.0 ? 1 : 0;
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgt_on), &on, sizeof(on)));
+        HIPCHK(hipDeviceSynchronize());
+        return on;
     }
     if (which == 6) {  // reset the phase timestamps (before a probed launch)
         unsigned long long z[32] = {0};

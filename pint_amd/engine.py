@@ -817,6 +817,23 @@ class Session:
         set_instances, the one-wave solve from the next fit step."""
         self._check(self.L.pint_set_option(self.ctx, 10, 1 if on else 0))
 
+    def set_la_chol(self, on=True):
+        """Look-ahead blocked Cholesky in the DMX-eliminated solve (PINT_OPT_LA_CHOL, default on)."""
+        self._check(self.L.pint_set_option(self.ctx, 11, 1 if on else 0))
+
+    def set_efuse(self, on=True):
+        """The residual pass's first half fused into the evaluation (PINT_OPT_EFUSE, default
+        on); applies from the next set_instances."""
+        self._check(self.L.pint_set_option(self.ctx, 12, 1 if on else 0))
+
+    def set_lane_solve(self, on=True):
+        """A lane per instance for small-instance solves of <= 8 columns (PINT_OPT_LANE_SOLVE, default on)."""
+        self._check(self.L.pint_set_option(self.ctx, 13, 1 if on else 0))
+
+    def set_spin_eval(self, on=True):
+        """Shared evaluation head for spin-only grids (PINT_OPT_SPIN_EVAL, default on)."""
+        self._check(self.L.pint_set_option(self.ctx, 14, 1 if on else 0))
+
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))

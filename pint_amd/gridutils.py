@@ -106,6 +106,9 @@ def gather_blocks(local: np.ndarray, per: int, npts: int, dist) -> np.ndarray:
 # name, value and frozen flag (noise parameters set the basis weights) -- so any change
 # re-uploads.
 _GRID = {}
+# (rank, world) whose contiguous block alone a grid call fits, without a process group: the
+# bench's per-rank prediction of an N-rank grid on one GPU (None: the real rank and world)
+_EMULATE_SHARD = None
 
 
 def _grid_session(model, parnames, toas, gls):
@@ -235,6 +238,9 @@ def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
         npts = int(flat[0].size) if len(flat) else 0
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    if _EMULATE_SHARD is not None:  # (bench.py's predicted_strong: one rank's block of an N-rank run, alone)
+        rank, world = _EMULATE_SHARD
+        dist = None
     per, lo, hi = shard_range(npts, rank, world)
     chi2 = np.full(hi - lo, np.nan)
     extra = {e: np.full(hi - lo, np.nan) for e in extraparnames}
@@ -266,6 +272,12 @@ def _chisq_flat(ftr, parnames: Sequence[str], flat: Sequence[np.ndarray],
     # extras are the point's parameter values after its fit, also for a MaxiterReached point
     # (gridutils.py:107-110 reads them outside the try); a point taken out of the batch as
     # invalid has none (NaN, final_tables_flat)
+    if _EMULATE_SHARD is not None:  # the block in place, NaN elsewhere
+        def place(v):
+            out = np.full(npts, np.nan)
+            out[lo:hi] = v
+            return out
+        return place(chi2), {e: place(extra[e]) for e in extraparnames}
     chi2_all = gather_blocks(chi2, per, npts, dist)
     extra_all = {e: gather_blocks(extra[e], per, npts, dist) for e in extraparnames}
     return chi2_all, extra_all

@@ -256,10 +256,26 @@ class TOAs:
         if len(key_value) == 2:
             raise NotImplementedError("range selection on a flag column")
         # each entry compared with == as the reference's selector does (an object array keeps
-        # None and non-string values as they are)
-        arr = np.empty(len(col), dtype=object)
-        arr[:] = col
-        return np.where(arr == key_value[0])[0]
+        # None and non-string values as they are); the column's object array and the
+        # selections are cached per column object (flag columns are tuples: an edit replaces
+        # the column, and the cache entry with it) -- EFAC, EQUAD and JUMP masks on one flag
+        # share them at upload
+        cache = self.__dict__.setdefault("_sel_cache", {})
+        ent = cache.get(k)
+        if ent is None or ent[0] is not col:
+            arr = np.empty(len(col), dtype=object)
+            arr[:] = col
+            ent = cache[k] = (col, arr, {})
+        sel = ent[2]
+        v = key_value[0]
+        key_ = (type(v), v) if isinstance(v, (str, int, float)) else None
+        hit = sel.get(key_) if key_ is not None else None
+        if hit is None:
+            hit = np.where(ent[1] == v)[0]
+            hit.setflags(write=False)
+            if key_ is not None:
+                sel[key_] = hit
+        return hit
 
     # -- persistence -----------------------------------------------------------------
     def save(self, path: str):

@@ -13,6 +13,7 @@ for k in ("n2", "n4", "n8"):
         print(k, ps[k]["ms_per_step"], "ms", ps[k]["speedup_vs_n1"], "x", ps[k]["ms_per_shard"])
 if d.get("grid"):
     print("grid", d["grid"]["value"], d["grid"].get("seconds_all"), d["grid"].get("roofline"))
+    print("grid predicted", json.dumps(d["grid"].get("predicted_strong")))
 print("cold", json.dumps(d.get("cold_start")))
 for k in ("j0740", "c2"):
     if d.get(k):

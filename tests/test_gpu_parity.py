@@ -744,6 +744,83 @@ def test_schur_kernel_matches_in_solve_build(mode):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("mode", [1, 0])
+def test_lookahead_cholesky_matches_blocked(mode):
+    """The DMX-eliminated solve's look-ahead factorisation (PINT_OPT_LA_CHOL: diagonal block
+    k+1 factored beside step k's trailing update, L^-1's block rows beside the panels) gives
+    the same step, errors, covariance and linearised chi2, bit for bit, as the plain blocked
+    order, GLS and WLS, with the build in the solve and in k_schur; j0740_10k (cond 7e12)
+    takes the refinement pass."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso", "j0740_10k")]
+
+    def run(la, schur):
+        s = Session()
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.set_cov_defer(2)
+        s.set_schur(schur)
+        s.set_la_chol(la)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(mode)
+        dp, er, cov, cl = s.read_step()
+        out = [x.copy() for x in dp] + [x.copy() for x in er] + [x.copy() for x in cov] + [np.array(cl, copy=True)]
+        s.close()
+        return out
+
+    for schur in (True, False):
+        a, b = run(True, schur), run(False, schur)
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+def test_fused_residual_pass_matches_separate():
+    """The residual pass's first half fused into the evaluation (PINT_OPT_EFUSE: 254 rows per
+    block plus row 0 and the TZR row, the phase residuals and weighted sums formed there)
+    against the k_resid1 launch: the phase residuals are the same operations on the same
+    values (bit for bit); the weighted mean is summed over other row groups, so the time
+    residuals, chi2 and the GLS/WLS steps agree to rounding.  Covers ECORR (B1855: k_resid2
+    in the pass), the deferred k_resid2 of the vg fit layout and WLS."""
+    from pint_amd.engine import Session, build_layout, pack_table
+
+    def run(fused, mode):
+        s = Session()
+        s.set_efuse(fused)
+        lays = [s.add(build_layout(m, t)) for m, t in items]  # (items: the loop's below)
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        s.eval(want_M=False)
+        tr, pr, c2 = s.read_resids()
+        out = {"tr": [x.copy() for x in tr], "pr": [x.copy() for x in pr], "c2": np.array(c2, copy=True)}
+        s.eval(want_M=Session.FIT)
+        s.fit_step(mode)
+        dp, er, _, cl = s.read_step()
+        out["dp"] = [x.copy() for x in dp]
+        out["er"] = [x.copy() for x in er]
+        out["cl"] = np.array(cl, copy=True)
+        tr2, _, c22 = s.read_resids()
+        out["tr2"] = [x.copy() for x in tr2]
+        out["c22"] = np.array(c22, copy=True)
+        s.close()
+        return out
+
+    for names, mode in ((("pta_dd", "pta_ell1", "pta_iso"), 1), (("pta_dd", "pta_ell1", "pta_iso"), 0),
+                        (("b1855",), 1)):
+        items = [load(n)[:2] for n in names]
+        a, b = run(True, mode), run(False, mode)
+        for x, y in zip(a["tr"] + a["tr2"], b["tr"] + b["tr2"]):
+            assert np.max(np.abs(x - y)) <= 1e-17 + 1e-12 * np.max(np.abs(y))
+        for x, y in zip(a["pr"], b["pr"]):
+            assert np.max(np.abs(x - y)) <= 1e-12 * max(1e-3, np.max(np.abs(y)))
+        np.testing.assert_allclose(a["c2"], b["c2"], rtol=1e-12)
+        np.testing.assert_allclose(a["c22"], b["c22"], rtol=1e-12)
+        np.testing.assert_allclose(a["cl"], b["cl"], rtol=1e-9)
+        for x, y, e in zip(a["dp"], b["dp"], b["er"]):
+            k = min(len(x), len(e))
+            ok = e[:k] > 0
+            assert np.max(np.abs(x[:k] - y[:k])[ok] / e[:k][ok]) <= 1e-9
+
+
 def test_fit_step_apply_matches_separate_apply():
     """pint_fit_step_apply (the full-step update and the new tables' constants formed at the
     end of the solve kernel) gives the same tables, step outputs, noise realisations and
@@ -1246,6 +1323,48 @@ def test_small_instance_kernels_match(mode, mix):
         sc = np.sqrt(np.outer(np.diag(c2[k]), np.diag(c2[k])))
         assert np.max(np.abs(c1[k] - c2[k]) / sc) < 1e-12
     np.testing.assert_allclose(l1, l2, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_lane_solve_matches_wave_solve(mode):
+    """k_solve_lanes (a lane per instance, K <= 8: 64 grid points per wave) against the
+    one-wave k_solve_blk (PINT_OPT_LANE_SOLVE off) on 130 NGC6440E points (two full waves
+    and a partial one): the same normalisation, factor and solve per element; the sums of
+    squares and dot products run in another order, so steps, errors, covariance and
+    linearised chi2 agree to rounding."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    m0, t0 = load("ngc6440e")[:2]
+
+    def run(lanes):
+        s = Session()
+        s.set_lane_solve(lanes)
+        lay = s.add(build_layout(m0, t0))
+        tab = pack_table(lay, m0)
+        insts = []
+        for k in range(130):
+            tk = tab.copy()
+            tk[lay.offsets["F0"]] += (k - 65) * 1e-11
+            insts.append((lay, tk))
+        s.set_instances(insts)
+        s.eval(want_M=Session.FIT)
+        s.fit_step(mode)
+        dp, er, cov, cl = s.read_step()
+        out = ([x.copy() for x in dp], [x.copy() for x in er], [x.copy() for x in cov], np.array(cl, copy=True))
+        s.close()
+        return out
+
+    (d1, e1, c1, l1), (d2, e2, c2, l2) = run(True), run(False)
+    for k in range(len(e1)):
+        f = e2[k] > 0
+        assert np.array_equal(e1[k] > 0, f)
+        assert np.max(np.abs(d1[k][f] - d2[k][f]) / e2[k][f]) < 1e-9
+        assert np.max(np.abs(e1[k][f] / e2[k][f] - 1)) < 1e-12
+        sc = np.sqrt(np.outer(np.diag(c2[k]), np.diag(c2[k])))
+        assert np.max(np.abs(c1[k] - c2[k]) / sc) < 1e-12
+    # chi2lin = r^T W r - b^T x cancels (~1e2 of the pre-fit chi2): the two solves' rounding of x
+    # shows at ~1e-12 of the result
+    np.testing.assert_allclose(l1, l2, rtol=1e-10, atol=0)
 
 
 @pytest.mark.gpu

@@ -443,6 +443,44 @@ def test_resident_grid_batch_matches_fresh(name, fitter):
     np.testing.assert_array_equal(e_res["DM"], e_new["DM"])
 
 
+@pytest.mark.parametrize("name", ["ngc6440e", "pta_iso"])
+def test_spin_grid_eval_matches_full(name):
+    """A grid whose points differ in F0 and F1 only (pint_set_grid, isolated model) evaluates
+    its first design matrix with the shared head (k_eval_head: every row's delay, astrometric
+    geometry and dispersion factors once) and each point's spin part (k_eval_spin): the
+    phases, Taylor frequencies, delays and design matrix equal the full per-point evaluation
+    (PINT_OPT_SPIN_EVAL off) bit for bit, and so do the fitted steps.  pta_iso (red noise) is
+    outside the shared path and must take the full evaluation either way."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    model, toas = load(name)[:2]
+
+    def run(spin):
+        s = Session()
+        s.set_spin_eval(spin)
+        lay = s.add(build_layout(model, toas))
+        base = pack_table(lay, model)
+        F0, F1 = np.longdouble(model.F0.value), np.longdouble(model.F1.value)
+        g0 = F0 + np.linspace(-2, 2, 7) * np.longdouble(1e-10)
+        g1 = F1 + np.linspace(-2, 2, 11) * np.longdouble(1e-18)
+        s.set_grid(lay, base, [("F0", g0, 11, 7), ("F1", g1, 1, 11)], 77)
+        s.eval(want_M=Session.FIT)
+        ev = s.read_eval()
+        # (the compact vg layout of pta_iso stores no Fourier columns: its M buffer is read
+        # only where written, through the fit below)
+        M = s.read_designmatrix() if name == "ngc6440e" else []
+        s.fit_step(0)
+        dp, er, _, cl = s.read_step()
+        out = [np.array(x, copy=True) for x in ev] + [np.array(M, copy=True)]
+        out += [np.array(x, copy=True) for x in dp] + [np.array(cl, copy=True)]
+        s.close()
+        return out
+
+    a, b = run(True), run(False)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_chunked_grid_matches_one_batch(monkeypatch):
     """A grid fitted in equal chunks (the resident batch re-bound per chunk: pint_set_grid's
     fast path) and a last smaller one (a fresh set-up) equals the same grid as one batch, bit
