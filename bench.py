@@ -472,15 +472,23 @@ def roofline(s, lays, kt_gram, step, args):
         exe += chunks * 16.0 * nt * 2048.0
     # bytes the evaluation kernels move per TOA: inputs tdb (16) + freq (8) +
     # pos/vel/sun (72) + flags (4) + jump mask (8) + DMX ids (8) = 116 B; outputs phase hi/lo,
-    # Taylor F, delay (32 B); with the fit layout also the compact timing columns (8 P B) and
-    # the row's DMX value (8 B)
+    # Taylor F, delay (32 B); the residual pass's first half fused into the evaluation (round
+    # 6) reads the pulse-number offset and 1/sigma and writes the phase residual (24 B); with
+    # the fit layout also the compact timing columns (8 P B) and the row's DMX value (8 B).
+    # The residual pass left (k_resid2, post-fit, with the Woodbury trig tiles) reads the phase
+    # residual, Taylor F, 1/sigma and the row's (cos, sin) of theta and 8 theta (56 B) and
+    # writes the phase and time residuals (16 B)
     nrow = float(sum(l.n + 1 for l in lays))
     pc = [s.vgram_layout(l)[3] for l in lays]
     nbytes = {
-        "k_eval": nrow * 148.0,
-        "k_eval_M": float(sum((l.n + 1) * 148.0 + l.n * (8.0 * p + 8.0) for l, p in zip(lays, pc))),
-        "k_resid": float(sum(l.n for l in lays)) * 80.0,       # two passes of 40 B
-        "k_woodbury": float(sum(l.n for l in lays)) * 32.0,    # r, 1/sigma, fundamental (cos, sin)
+        "k_eval": nrow * 172.0,
+        "k_eval_M": float(sum((l.n + 1) * 172.0 + l.n * (8.0 * p + 8.0) for l, p in zip(lays, pc))),
+        "k_resid": float(sum(l.n for l in lays)) * 72.0,
+        # k_wsolve on the fused path (the dots come from k_resid2's tiles): per instance its
+        # residual blocks' 16x16 tiles and chi2 partials, and the packed inverse factor of Sigma
+        # -- a latency-bound per-instance forward substitution, not a streaming kernel
+        "k_woodbury": float(sum(-(-l.n // 1024) * (256 + 3) * 8.0 + (2 * l.nred + 1) * (2 * l.nred + 2) / 2 * 8.0
+                                for l in lays)),
     }
     # per-kernel breakdown: a separate instrumented pass (every timing slot's events on)
     s.set_timing_mask(0xFF)

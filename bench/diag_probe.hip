@@ -9,8 +9,12 @@
 //   3  the pivot column broadcast through LDS (VGPR operands), 4: that with one Newton step,
 //   5  variant 3 with a scheduling barrier after each pivot,
 //   6  two waves: the factorisation (readlane) and the inverse (LDS columns) one pivot apart,
-//   7  variant 0 with the lane index opaque per pivot (no hoisted lane-mask SGPR pairs).
-// The kernel is compiled with the 1024-thread register budget of the solves (128 VGPRs).
+//   7  variant 0 with the lane index opaque per pivot (no hoisted lane-mask SGPR pairs),
+//   8  readlane broadcasts, every lane scaling its entry (a[j] *= il: no lane masks; the rows
+//      above the pivot hold values no later pivot reads), a scheduling barrier per pivot,
+//   9  variant 8 with the pivot column through LDS, 10: that without the barrier.
+// The kernel is compiled with the register budget of -DLB threads per workgroup (default
+// 1024, the 16-wave solves' 128 VGPRs; 512: the 8-wave solve's 256).
 // Prints the max error of L^-1 against a long-double Cholesky inverse on the host (relative
 // to max |L^-1|) and the cycles per factor (s_memtime, 64 dependent factors in one wave).
 // Build: hipcc --offload-arch=gfx950 -O3 bench/diag_probe.hip -o build/diag_probe
@@ -94,6 +98,60 @@ __device__ __forceinline__ bool diag_factor_c4(double* Akk, int lane) {
             a[c] -= a[j] * Lcj;
             x[c] -= Lcj * x[j];
         }
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Akk[swz(t, r)] = x[t];
+    }
+    return ok;
+}
+
+// variants 8-10: no lane masks (every lane scales its own entry), readlane or LDS columns
+template <bool LDSC, bool SB>
+__device__ __forceinline__ bool diag_factor_nm(double* Akk, double* colbuf, int lane) {
+    const int r = lane & 15;
+    double a[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        a[c] = Akk[swz(r, c)];
+        x[c] = (r == c) ? 1.0 : 0.0;
+    }
+    bool ok = true;
+    typedef __attribute__((address_space(3))) double ldsd;
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) dv2 ldsd2;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const double djj = rdlane(a[j], j);
+        ok = ok && (djj > 0.0);
+        const double il = rsqn<2>(djj);
+        a[j] *= il;
+        x[j] *= il;
+        if constexpr (LDSC) {
+            if (lane < 16) ((ldsd*)colbuf)[lane] = a[j];
+            __builtin_amdgcn_wave_barrier();
+            double Lc[16];
+#pragma unroll
+            for (int c2 = (j + 1) / 2; c2 < 8; c2++) {
+                const dv2 v = ((ldsd2*)colbuf)[c2];
+                Lc[2 * c2] = v.x;
+                Lc[2 * c2 + 1] = v.y;
+            }
+#pragma unroll
+            for (int c = j + 1; c < 16; c++) {
+                a[c] -= a[j] * Lc[c];
+                x[c] -= Lc[c] * x[j];
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int c = j + 1; c < 16; c++) {
+                const double Lcj = rdlane(a[j], c);
+                a[c] -= a[j] * Lcj;
+                x[c] -= Lcj * x[j];
+            }
+        }
+        if (SB) __builtin_amdgcn_sched_barrier(0);
     }
     if (lane < 16) {
 #pragma unroll
@@ -210,14 +268,20 @@ __device__ __forceinline__ bool diag_factor2(double* Akk, double* colbuf, volati
 
 template <int V>
 __device__ __forceinline__ bool factor_v(double* Akk, double* colbuf, int lane) {
-    if constexpr (V == 7) return diag_factor_c4(Akk, lane);
+    if constexpr (V == 8) return diag_factor_nm<false, true>(Akk, colbuf, lane);
+    else if constexpr (V == 9) return diag_factor_nm<true, true>(Akk, colbuf, lane);
+    else if constexpr (V == 10) return diag_factor_nm<true, false>(Akk, colbuf, lane);
+    else if constexpr (V == 7) return diag_factor_c4(Akk, lane);
     else if constexpr (V >= 5) return diag_factor_lds<2, true>(Akk, colbuf, lane);
     else if constexpr (V >= 3) return diag_factor_lds<V == 3 ? 2 : 1>(Akk, colbuf, lane);
     else return diag_factor<V>(Akk, lane);
 }
 
+#ifndef LB
+#define LB 1024
+#endif
 template <int V>
-__global__ __launch_bounds__(1024) void k_diag(const double* __restrict__ in, double* __restrict__ out,
+__global__ __launch_bounds__(LB) void k_diag(const double* __restrict__ in, double* __restrict__ out,
                                              long long* __restrict__ cyc, int reps) {
     __shared__ double blk[256];
     __shared__ double colbuf[16 * 16 + 16];
@@ -307,7 +371,8 @@ int main() {
     hipMalloc(&dout, 256 * 8);
     hipMalloc(&dc, 8);
     hipMemcpy(din, A.data(), 256 * 8, hipMemcpyHostToDevice);
-    for (int v = 0; v < 8; v++) {
+    printf("register budget of %d-thread workgroups\n", LB);
+    for (int v = 0; v < 11; v++) {
         if (v == 0) hipLaunchKernelGGL(k_diag<0>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 1) hipLaunchKernelGGL(k_diag<1>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 2) hipLaunchKernelGGL(k_diag<2>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
@@ -316,6 +381,9 @@ int main() {
         if (v == 5) hipLaunchKernelGGL(k_diag<5>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         if (v == 6) hipLaunchKernelGGL(k_diag<6>, dim3(1), dim3(128), 0, 0, din, dout, dc, 64);
         if (v == 7) hipLaunchKernelGGL(k_diag<7>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 8) hipLaunchKernelGGL(k_diag<8>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 9) hipLaunchKernelGGL(k_diag<9>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
+        if (v == 10) hipLaunchKernelGGL(k_diag<10>, dim3(1), dim3(64), 0, 0, din, dout, dc, 64);
         std::vector<double> o(256);
         long long c;
         hipMemcpy(o.data(), dout, 256 * 8, hipMemcpyDeviceToHost);

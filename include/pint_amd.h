@@ -366,6 +366,10 @@ int pint_check_step(pint_ctx *ctx, int slot);
  * design matrix that precedes the first fit step; each point then runs the spin part only.
  * The same bits as the full evaluation. */
 #define PINT_OPT_SPIN_EVAL 14
+/* PINT_OPT_SOLVE_W8 = 1 (default, env PINT_SOLVE_W8): the DMX-eliminated solve runs 8 waves
+ * per instance (256 VGPRs per lane) when its dense block has at most 8 16-column blocks,
+ * else 16.  The same operations per element: the same bits. */
+#define PINT_OPT_SOLVE_W8 15
 int pint_set_option(pint_ctx *ctx, int key, int value);
 /* The SVD path of the fitters for degenerate normal equations (WLSState.step,
  * fitter.py:1282-1359: singular values of the whitened normalised M below threshold * s_max

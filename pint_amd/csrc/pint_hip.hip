@@ -813,7 +813,8 @@ __global__ __launch_bounds__(RES_BT) void k_resid1(const PsrDev* __restrict__ ps
 // sin k = D[8+a][b] + D[a][8+b]; 1^T W r = D[0][0]).  Wave w of the block holds rows r0 + 64w
 // + 256j + lane (j < 4): four contiguous 64-row chunks, staged one at a time in the wave's own
 // LDS columns and contracted by 16 k-steps of 4 rows.
-constexpr int WT_CS = 66;  // k_resid2 tile staging: column stride (doubles), 64 rows + 2
+constexpr int WT_CS = 66;  // k_wdot tile staging: column stride (doubles), 64 rows + 2
+constexpr int WT_CS2 = 34;  // k_resid2 tile staging: 32-row halves of the wave's 64 rows, stride 32 + 2
 template <int BT>
 __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ psrs, const InstDev* __restrict__ insts,
                                                    const int* __restrict__ rblk_inst, int nrblk,
@@ -824,7 +825,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     WgTimer wgt_(WGT_RES2);
     constexpr int NW = BT / 64;
     __shared__ double sh[2 * (RES_BT / 64)];
-    extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS: A (columns 0-15), B (16-31)
+    extern __shared__ double xs[];  // with wtile, per wave 32 * WT_CS2: A (columns 0-15), B (16-31)
     const int rb = blockIdx.x * (RES_BT / BT) + (BT == RES_BT ? 0 : (int)__builtin_amdgcn_readfirstlane(threadIdx.x / BT));
     if (BT != RES_BT && rb >= nrblk) return;  // (wave-uniform)
     const int tid = threadIdx.x % BT;
@@ -873,7 +874,7 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
     }
     double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};  // independent chains
     typedef double __attribute__((address_space(3))) ldsd;
-    ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS);
+    ldsd* X = (ldsd*)(xs + wave * 32 * WT_CS2);
     double c2 = 0.0;
 #pragma unroll
     for (int j = 0; j < RES_RPT; j++) {
@@ -890,26 +891,43 @@ __global__ __launch_bounds__(RES_BT) void k_resid2(const PsrDev* __restrict__ ps
             wr = z * is;
         }
         if (tile) {  // (block-uniform)
+            // the row's 32 tile values, then two 32-row halves staged and contracted in turn
+            // (half the LDS of one 64-row stage: 4 workgroups per CU instead of 2; the k-steps
+            // keep their chains and order -- k-step ks of half h is the 64-row form's 8h + ks)
             const double c1 = lz[j][0], s1 = lz[j][1], c8 = lz[j][2], s8 = lz[j][3];
             double ca = wr, sa = 0.0, cb = 1.0, sb = 0.0;
+            double va[8], vs[8], vc[8], vd[8];
 #pragma unroll
             for (int a = 0; a < 8; a++) {
-                X[a * WT_CS + lane] = ca;
-                X[(8 + a) * WT_CS + lane] = sa;
-                X[(16 + a) * WT_CS + lane] = cb;
-                X[(24 + a) * WT_CS + lane] = sb;
+                va[a] = ca;
+                vs[a] = sa;
+                vc[a] = cb;
+                vd[a] = sb;
                 rot(ca, sa, c1, s1);
                 rot(cb, sb, c8, s8);
             }
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's stores before its reads
-            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int ks = 0; ks < 16; ks++) {
-                const int row = 4 * ks + (lane >> 4);
-                const double av = X[(lane & 15) * WT_CS + row], bv = X[(16 + (lane & 15)) * WT_CS + row];
-                acc[ks & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ks & 3], 0, 0, 0);
+            for (int h = 0; h < 2; h++) {
+                if ((lane >> 5) == h) {
+                    const int lr_ = lane & 31;
+#pragma unroll
+                    for (int a = 0; a < 8; a++) {
+                        X[a * WT_CS2 + lr_] = va[a];
+                        X[(8 + a) * WT_CS2 + lr_] = vs[a];
+                        X[(16 + a) * WT_CS2 + lr_] = vc[a];
+                        X[(24 + a) * WT_CS2 + lr_] = vd[a];
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's stores before its reads
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int ks = 0; ks < 8; ks++) {
+                    const int row = 4 * ks + (lane >> 4);
+                    const double av = X[(lane & 15) * WT_CS2 + row], bv = X[(16 + (lane & 15)) * WT_CS2 + row];
+                    acc[ks & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ks & 3], 0, 0, 0);
+                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
         }
     }
     c2 = block_sum<NW>(c2, sh);
@@ -3167,7 +3185,7 @@ __device__ __forceinline__ double rsq2(double d) {
 // N = 8: a block whose rows and columns 8..15 are identity padding (K <= 8 in a single-block
 // solve): only the leading 8 x 8 is factored -- the same operations on it as N = 16 does
 // (the padding's updates are exact no-ops), and the padding of L^-1 is identity as stored
-template <int N = 16>
+template <int N = 16, bool SB = false>
 __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
     const int r = lane & 15;
     // Cholesky (lane r holds row r) and X = L^-1 (lane r its column r) in one pass: pivot j's
@@ -3187,7 +3205,11 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
         const double djj = rdlane(a[j], j);
         ok = ok && (djj > 0.0);
         const double il = rsq2(djj);
-        a[j] = (r == j) ? djj * il : (r > j ? a[j] * il : 0.0);
+        // every lane scales its entry: rows r >= j get L[r][j] (row j: djj il, the same
+        // product), rows r < j an upper-triangle value no later pivot reads -- no per-pivot
+        // lane masks (the selects' 32 loop-invariant masks were hoisted into SGPRs and
+        // spilled to VGPR lanes, ~half the pivot loop's instructions)
+        a[j] *= il;
         x[j] *= il;
 #pragma unroll
         for (int c = j + 1; c < N; c++) {
@@ -3195,6 +3217,10 @@ __device__ __forceinline__ bool diag_factor(double* Akk, int lane) {
             a[c] -= a[j] * Lcj;
             x[c] -= Lcj * x[j];
         }
+        // right-looking order kept: without the barrier the scheduler sank every column's
+        // updates to just before its own pivot (left-looking), a dependent chain of j FMAs
+        // ahead of pivot j (and the pivot columns parked in SGPRs spilled to VGPR lanes)
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
     }
     if (lane < N) {
 #pragma unroll
@@ -3299,7 +3325,7 @@ template <int NW>
 __device__ __forceinline__ bool blk_cholinv_la(double* A, int nb, int wave, int lane, int* sflag) {
     TS(9);
     if (wave == 0) {
-        const bool ok = diag_factor<16>(A, lane);
+        const bool ok = diag_factor<16, true>(A, lane);
         if (!ok && lane == 0) *sflag = 1;
     }
     TS(10);
@@ -3334,7 +3360,7 @@ __device__ __forceinline__ bool blk_cholinv_la(double* A, int nb, int wave, int 
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (its lanes' stores before its reads)
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const bool ok = diag_factor<16>(Akk, lane);
+                const bool ok = diag_factor<16, true>(Akk, lane);
                 if (!ok && lane == 0) *sflag = 1;
             } else {
                 for (int p = wave; p < ntr; p += NW - 1) {
@@ -4343,7 +4369,7 @@ __global__ __launch_bounds__(NW * 64) void k_solve_dmx(const PsrDev* __restrict_
         }
         if (hs == 0) {
             xd[g] = s1;
-            errs[I.coff + od_h] = sqrt(se) * ind[g];  // (g = h0: one round of groups)
+            errs[I.coff + (g == h0 ? od_h : Pd.dorig[g])] = sqrt(se) * ind[g];  // (g = h0: the first round of groups)
             vmax = fmax(vmax, se);
             amax = fmax(amax, rd[g]);
         }
@@ -5419,6 +5445,7 @@ struct pint_ctx {
     int schur = 1;       // PINT_SCHUR: k_schur forms the DMX-eliminated solve's S', U, b'_d (deferred solves)
     int evalb_wpe = 3;   // PINT_EVALB_WPE: one-model ELL1/DD batches with M at 3 waves/SIMD (0: the compiler's)
     int la_chol = 1;     // PINT_LA_CHOL: k_solve_dmx's look-ahead blocked Cholesky (0: blk_cholinv; the same bits)
+    int solve_w8 = 1;    // PINT_SOLVE_W8: k_solve_dmx with 8 waves when the dense block fits (0: 16 waves)
     int eval0_wpe = 1;   // PINT_EVAL0_WPE: the isolated-model build at fixed register budgets (0: the compiler's)
     int eval_wpe = 3;    // PINT_EVAL_WPE: k_eval_mix<1>'s register budget in waves/SIMD (3: 168 VGPRs,
                          // 108 B of spills, 0.124 -> 0.105 ms; 4: 276 B of spills, slower; 0: none, 204)
@@ -5999,6 +6026,7 @@ pint_ctx* pint_ctx_create(int device) {
     ctx->resid12 = getenv("PINT_RESID12") ? atoi(getenv("PINT_RESID12")) : 1;
     ctx->evalb_wpe = getenv("PINT_EVALB_WPE") ? atoi(getenv("PINT_EVALB_WPE")) : 3;
     ctx->la_chol = getenv("PINT_LA_CHOL") ? atoi(getenv("PINT_LA_CHOL")) : 1;
+    ctx->solve_w8 = getenv("PINT_SOLVE_W8") ? atoi(getenv("PINT_SOLVE_W8")) : 1;
     ctx->efuse = getenv("PINT_EFUSE") ? atoi(getenv("PINT_EFUSE")) : 1;
     ctx->lane_solve = getenv("PINT_LANE_SOLVE") ? atoi(getenv("PINT_LANE_SOLVE")) : 1;
     ctx->spin_eval = getenv("PINT_SPIN_EVAL") ? atoi(getenv("PINT_SPIN_EVAL")) : 1;
@@ -7079,7 +7107,7 @@ static void launch_apply(pint_ctx* ctx, const double* lam, double lam_u) {
 
 // k_resid2 of the last residual pass (with wt, the Woodbury trig tiles)
 static void launch_resid2(pint_ctx* ctx, bool wt) {
-    const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
+    const size_t wlds = wt ? sizeof(double) * std::max((RES_BT / 64) * 32 * WT_CS2, 4 * 256) : 0;
     const double* ep = ctx->efz ? ctx->d_epart : nullptr;
     if (!ctx->efz && ctx->small && ctx->maxn <= RES_SMALLN)
         hipLaunchKernelGGL(k_resid2<64>, dim3((ctx->nrblk + 3) / 4), dim3(RES_BT), wlds, ctx->stream, ctx->d_psrs,
@@ -7242,7 +7270,6 @@ int pint_eval(pint_ctx* ctx, int want_M) {
         // without the design matrix (the post-fit evaluation a GLS chi2 follows): the Woodbury
         // dot products come with the residual pass (k_resid2 tiles, k_rsum)
         const bool wt = ctx->wfuse && want_M == 0;
-        const size_t wlds = wt ? sizeof(double) * (RES_BT / 64) * 32 * WT_CS : 0;
         // (256-row blocks for small batches were measured: resid1 faster, resid2 and k_wsolve's
         // longer tile sums slower, the step ~1.4 us slower at 9 pulsars)
         // the fit layout's pass on the k_gram_v path: k_resid1 only, the Gram stages the time
@@ -7682,14 +7709,27 @@ int pint_fit_step(pint_ctx* ctx, int mode) {
                 pre = 1;
             }
         }
-        hipExtLaunchKernelGGL((k_solve_dmx<16>), dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(1024),
-                              (uint32_t)lds_dyn, ctx->stream, nullptr, nullptr, 0u,
-                              (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_tables,
-                              (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,
-                              (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,
-                              ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,
-                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam, pre,
-                              ctx->la_chol);
+        // 8 waves (256 VGPRs per lane) when the dense block fits them (nbd <= 8 and, for the
+        // fused Woodbury Sigma, nbs <= 9): the 16-wave form's 128-VGPR budget made the
+        // diagonal factor spill its pivot columns to SGPRs and sink each column's updates to
+        // its pivot, serialising them (a chain of j FMAs before pivot j)
+        int mnbd = 0;
+        for (int pi : ctx->upsr) {
+            const PsrDev& pd = ctx->psrs[pi].dev;
+            if (pd.dsplit) mnbd = std::max(mnbd, ((mode == 0 ? pd.red0c : pd.Kd) + 15) / 16);
+        }
+        const bool w8 = ctx->solve_w8 && mnbd <= 8 && (!fuse_sigma || nbs_sig <= 9);
+#define PINT_SOLVE_DMX(NWS)                                                                                          \
+        hipExtLaunchKernelGGL((k_solve_dmx<NWS>), dim3(ctx->ninst * (fuse_sigma ? 2 : 1)), dim3(NWS * 64),           \
+                              (uint32_t)lds_dyn, ctx->stream, nullptr, nullptr, 0u,                                  \
+                              (const PsrDev*)ctx->d_psrs, (const InstDev*)ctx->d_inst, (const double*)ctx->d_tables, \
+                              (const double*)ctx->d_G, (const double*)ctx->d_colsq, ctx->nsplit, mode,               \
+                              (const double*)ctx->d_Sd, (const double*)ctx->d_DD, (const double*)ctx->d_DCS,         \
+                              ctx->d_dpars, ctx->d_errs, ctx->d_cov, ctx->d_chi2lin, ctx->d_sigL, ctx->d_status,     \
+                              fuse_sigma, ctx->refine, xw, ones, apply_tab, apply_ic, ctx->apply_lam, pre,           \
+                              ctx->la_chol)
+        if (w8) PINT_SOLVE_DMX(8); else PINT_SOLVE_DMX(16);
+#undef PINT_SOLVE_DMX
         HIPCHK(hipGetLastError());
         ctx->cov_pending = xw != nullptr;
         ctx->cov_mode = mode;
@@ -8052,6 +8092,7 @@ int pint_set_option(pint_ctx* ctx, int key, int value) {
     if (key == PINT_OPT_SCHUR) { ctx->schur = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_SMALL) { ctx->small = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_LA_CHOL) { ctx->la_chol = value ? 1 : 0; return PINT_OK; }
+    if (key == PINT_OPT_SOLVE_W8) { ctx->solve_w8 = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_EFUSE) { ctx->efuse = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_LANE_SOLVE) { ctx->lane_solve = value ? 1 : 0; return PINT_OK; }
     if (key == PINT_OPT_SPIN_EVAL) { ctx->spin_eval = value ? 1 : 0; return PINT_OK; }

@@ -834,6 +834,10 @@ class Session:
         """Shared evaluation head for spin-only grids (PINT_OPT_SPIN_EVAL, default on)."""
         self._check(self.L.pint_set_option(self.ctx, 14, 1 if on else 0))
 
+    def set_solve_w8(self, on=True):
+        """8 waves per instance in the DMX-eliminated solve when its dense block fits (PINT_OPT_SOLVE_W8)."""
+        self._check(self.L.pint_set_option(self.ctx, 15, 1 if on else 0))
+
     def set_vbin(self, on=True):
         """k_gram_v's binned DMX x Fourier tile (PINT_OPT_VBIN); applies from the next set_instances."""
         self._check(self.L.pint_set_option(self.ctx, 5, 1 if on else 0))

@@ -750,17 +750,19 @@ def test_lookahead_cholesky_matches_blocked(mode):
     k+1 factored beside step k's trailing update, L^-1's block rows beside the panels) gives
     the same step, errors, covariance and linearised chi2, bit for bit, as the plain blocked
     order, GLS and WLS, with the build in the solve and in k_schur; j0740_10k (cond 7e12)
-    takes the refinement pass."""
+    takes the refinement pass.  So does the 8-wave solve (PINT_OPT_SOLVE_W8) against the
+    16-wave one."""
     from pint_amd.engine import Session, build_layout, pack_table
     items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso", "j0740_10k")]
 
-    def run(la, schur):
+    def run(la, schur, w8=True):
         s = Session()
         lays = [s.add(build_layout(m, t)) for m, t in items]
         s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
         s.set_cov_defer(2)
         s.set_schur(schur)
         s.set_la_chol(la)
+        s.set_solve_w8(w8)
         s.eval(want_M=Session.FIT)
         s.fit_step(mode)
         dp, er, cov, cl = s.read_step()
@@ -773,6 +775,10 @@ def test_lookahead_cholesky_matches_blocked(mode):
         assert len(a) == len(b)
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+    # the 8-wave solve (PINT_OPT_SOLVE_W8) against the 16-wave one: the same bits
+    a, b = run(True, True, True), run(True, True, False)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
 
 
 def test_fused_residual_pass_matches_separate():
