@@ -60,10 +60,17 @@ def main():
     ap.add_argument("--graph", default="0", choices=["0", "1", "auto"],
                     help="step launches: 0 enqueued from the host, 1 one HIP-graph replay per step, auto the "
                          "faster of the two on a short trial (every rank makes the same choice)")
+    ap.add_argument("--pipes", default="auto",
+                    help="independent step pipelines per GPU (sessions with their own streams and buffers, fed "
+                         "round-robin): a count, or auto = the fastest of 1..--max-pipes on a short trial")
+    ap.add_argument("--max-pipes", type=int, default=2)
     ap.add_argument("--cold-start", type=int, default=1,
                     help="N=1 only: upload + first fit of the PTA in a fresh session (cold_start)")
     args = ap.parse_args()
 
+    # (several pipelines share the process's GPU_MAX_HW_QUEUES hardware queues, default 4:
+    # measured, 2 x 9-pulsar pipelines 0.105 ms per step with 4 queues, 0.237 with 12, where
+    # the hardware scheduler time-slices the queues; the variable is left as it is)
     from pint_amd import _lib
     _lib.lib()  # the process's HIP runtime (the system ROCm's), before torch is imported
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,7 +152,7 @@ def main():
                                       f"realisations (the {args.npsr}-pulsar PTA, LPT-sharded over {world} rank(s))",
                           "npsr": args.npsr, "ntoas": args.ntoas,
                           "pulsars_per_rank": [len(s) for s in shards], "K_cols_max": leg["kmax"],
-                          "launch": leg["launch"],
+                          "launch": leg["launch"], "pipelines": leg["pipes"],
                           "parallelism": f"pulsar shards x{world} (LPT, no data-path collective)"},
                "roofline": roof, "pta_weak": weak, "predicted_strong": emu, "cold_start": cold,
                "grid": grid, "j0740": j0740, "c2": c2,
@@ -163,18 +170,34 @@ def pta_leg(mine, models, args, rank, barrier, max_over_ranks, profile):
     t0 = time.time()
     items = sim.make_pta(ntoas=args.ntoas, indices=mine, models=[models[i] for i in mine])
     log(f"[rank {rank}] generated {len(items)} pulsars x {args.ntoas} TOAs in {time.time() - t0:.1f}s")
-    s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
-    lays = [s.add(build_layout(m, t)) for m, t in items]
-    tabs0 = [pack_table(l, m) for l, (m, _) in zip(lays, items)]
-    s.set_instances(list(zip(lays, tabs0)))
-    dt, kt_gram, n_gram, step, launch = timed_steps(s, args.steps, args.warmup, barrier, max_over_ranks,
-                                                    graph=args.graph)
-    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays)), "launch": launch}
+    ss, lays = pipelines(items, npipes(args))
+    dt, kt_gram, n_gram, step, launch, p = timed_steps(ss, args.steps, args.warmup, barrier, max_over_ranks,
+                                                       graph=args.graph, pipes=args.pipes)
+    out = {"dt": dt, "items": items, "kmax": int(max(l.K for l in lays)), "launch": launch, "pipes": p}
     if profile:
-        out["roofline"] = roofline(s, lays, kt_gram / max(1, n_gram), step, args)
+        out["roofline"] = roofline(ss[0], lays, kt_gram / max(1, n_gram), step, args)
         out["roofline"]["gram_event_launches"] = int(n_gram)
-    s.close()
+    for s in ss:
+        s.close()
     return out
+
+
+def npipes(args):
+    return args.max_pipes if args.pipes == "auto" else max(1, int(args.pipes))
+
+
+def pipelines(items, n):
+    """n sessions (independent pipelines: streams, device buffers) holding the same batch;
+    returns them and the first one's layouts."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    ss, lays0 = [], None
+    for _ in range(n):
+        s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
+        lays = [s.add(build_layout(m, t)) for m, t in items]
+        s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+        ss.append(s)
+        lays0 = lays0 or lays
+    return ss, lays0
 
 
 def emulate_world(items, costs, worlds, args, value1, step1):
@@ -203,20 +226,18 @@ def emulate_world(items, costs, worlds, args, value1, step1):
                 per.append(0.0)
                 modes.append(None)
                 continue
-            s = Session(device=int(os.environ.get("LOCAL_RANK", "0")))
-            sub = [items[i] for i in sh]
-            lays = [s.add(build_layout(m, t)) for m, t in sub]
-            s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, sub)])
+            ss, _ = pipelines([items[i] for i in sh], npipes(args))
             # the median of three timed runs: one host hiccup in a short run would otherwise
             # stand for the shard (a 4x outlier seen once in ~20 runs)
             reps = []
             for _ in range(3):
-                dt, _, _, _, launch = timed_steps(s, steps, warm, nobarrier, lambda v: v, graph=args.graph,
-                                                  gram_pass=False)
+                dt, _, _, _, launch, p = timed_steps(ss, steps, warm, nobarrier, lambda v: v, graph=args.graph,
+                                                     gram_pass=False, pipes=args.pipes)
                 reps.append(dt / steps)
-            s.close()
+            for s in ss:
+                s.close()
             per.append(float(np.median(reps)))
-            modes.append(launch)
+            modes.append(f"{launch} x{p}")
         mx = max(per)
         out[f"n{nw}"] = {"value": round(len(items) / mx, 3), "ms_per_step": round(mx * 1e3, 4),
                          "ms_per_shard": [round(p * 1e3, 4) for p in per],
@@ -264,23 +285,38 @@ def cold_start(items, rank):
     return out
 
 
-def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pass=True):
-    """Time `steps` fit steps of the Session's batch (warm-up first), pipelined L.NSLOT deep;
-    one step is GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.
+def timed_steps(sessions, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pass=True, pipes=1):
+    """Time `steps` fit steps of the batch (warm-up first); one step is
+    GLSFitter.fit_toas(maxiter=1) of every instance from its initial model.
 
+    sessions: one Session, or several holding the same batch -- independent pipelines
+    (each its own streams and device buffers) fed round-robin, step i on pipeline i mod P,
+    each pipelined L.NSLOT deep: a small batch's step is a chain of latency-bound kernels
+    that leaves most of the chip idle, and a second or third pipeline's kernels run in those
+    gaps.  pipes: how many of the sessions to use, or "auto": the fastest P on a short trial
+    after the warm-up (every rank makes the same choice).
     graph: 0 enqueue every launch of every step from the host; 1 capture the step once per
     pipeline slot into a HIP graph and replay it (the same kernels, copies and outputs, one
-    host launch per step); "auto" times a short run of each after the warm-up and keeps the
-    faster (a small batch's step is shorter than its ~20 host launches take to enqueue).
+    host launch per step); "auto" the faster of the two on the trial.
     Returns (max-over-ranks seconds, summed Gram event time of the sampled steps, their
-    count, step, launch mode)."""
+    count, step, launch mode, pipelines)."""
     from collections import deque
     from pint_amd import _lib as L
     from pint_amd.engine import Session
-    s.save_tables()        # the initial models, resident in HBM like the TOAs
-    s.set_lazy(True)
+    if isinstance(sessions, Session):
+        sessions = [sessions]
+    for s in sessions:
+        s.save_tables()        # the initial models, resident in HBM like the TOAs
+        s.set_lazy(True)
+        # Gram timing: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop
+        # on its first/last dispatch packet, or marker packets on the other Gram paths), on
+        # every GRAM_EVERY-th step of a pass of enqueued steps run after the timed region (the
+        # first pipeline alone): an event pair still idles the stream ~5-10 us (a 9-pulsar
+        # step's trace shows it), so the timed steps carry none.
+        s.set_timing_mask(0)
+        s.set_timing_every(GRAM_EVERY)
 
-    def step_calls():
+    def step_calls(s):
         """The step as separate library calls (the graph capture records these)."""
         s.restore_tables()     # every step fits from the initial models (device->device copy)
         s.eval(want_M=Session.FIT)
@@ -291,51 +327,47 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
         c2 = s.chi2_gls()      # post-fit GLS chi2 (GLSFitter returns calc_chi2())
         return out, nz, c2
 
-    def step():
+    def step(s):
         """The same step enqueued by one call (pint_fit_step_enqueue, closes the step);
         returns its slot."""
         return s.fit_step_enqueue(restore=True, lam=1.0)[0]
 
-    def replay():
+    def replay(s):
         s.replay()
         return s.step_end()
 
-    # Gram timing: HIP events on the Gram dispatches only (hipExtLaunchKernel start/stop on
-    # its first/last dispatch packet, or marker packets on the other Gram paths), on every
-    # GRAM_EVERY-th step of a pass of enqueued steps run after the timed region: an event pair
-    # still idles the stream ~5-10 us (a 9-pulsar step's trace shows it), so the timed steps
-    # carry none.
-    s.set_timing_mask(0)
-    s.set_timing_every(GRAM_EVERY)
-
-    def run(nsteps, launch):
-        """nsteps steps pipelined L.NSLOT deep: before a step is enqueued, the step that last
-        used its slot is checked (Session.check_step), so the device holds up to NSLOT - 1
-        queued steps while the host enqueues the next; launch() enqueues and closes one
-        step and returns its slot.  Returns the summed Gram-kernel event time of the
-        sampled steps and their count."""
-        kt, nk, pend = 0.0, 0, deque()
+    def run(nsteps, launch, sess):
+        """nsteps steps over the pipelines `sess`, round-robin, each pipelined L.NSLOT deep:
+        before a step is enqueued on a pipeline, the step that last used that pipeline's
+        slot is checked (Session.check_step), so every device queue holds up to NSLOT - 1
+        steps while the host enqueues the next; launch(s) enqueues and closes one step on s
+        and returns its slot.  Returns the summed Gram-kernel event time of the sampled
+        steps and their count."""
+        kt, nk = 0.0, 0
+        pend = [deque() for _ in sess]
         # PINT_BENCH_TRACE=1: the host clock after every launch and every check (2 floats per
         # step into a preallocated array), reported on stderr
         tr = np.zeros(2 * nsteps + 2) if os.environ.get("PINT_BENCH_TRACE") else None
         clk = time.perf_counter
 
-        def check_one():
+        def check_one(k):
             nonlocal kt, nk
-            s.check_step(pend.popleft())
-            t = s.timing()[SLOT_GRAM]
+            sess[k].check_step(pend[k].popleft())
+            t = sess[k].timing()[SLOT_GRAM]
             kt, nk = kt + t, nk + (t > 0)
 
         for i in range(nsteps):
-            if len(pend) >= L.NSLOT:
-                check_one()
+            k = i % len(sess)
+            if len(pend[k]) >= L.NSLOT:
+                check_one(k)
             if tr is not None:
                 tr[2 * i] = clk()
-            pend.append(launch())
+            pend[k].append(launch(sess[k]))
             if tr is not None:
                 tr[2 * i + 1] = clk()
-        while pend:
-            check_one()
+        for k in range(len(sess)):
+            while pend[k]:
+                check_one(k)
         if tr is not None:
             tr[-1] = clk()
             st = np.diff(tr[0:2 * nsteps:2]) * 1e3                   # launch to launch
@@ -358,44 +390,52 @@ def timed_steps(s, steps, warmup, barrier, max_over_ranks, graph="auto", gram_pa
     gc.freeze()
     gc.disable()
     try:
-        return _timed(s, steps, warmup, barrier, max_over_ranks, graph, gram_pass, run, step, step_calls, replay)
+        return _timed(sessions, steps, warmup, barrier, max_over_ranks, graph, gram_pass, pipes, run, step,
+                      step_calls, replay)
     finally:
         gc.enable()
         gc.unfreeze()
 
 
-def _timed(s, steps, warmup, barrier, max_over_ranks, graph, gram_pass, run, step, step_calls, replay):
+def _timed(sessions, steps, warmup, barrier, max_over_ranks, graph, gram_pass, pipes, run, step, step_calls, replay):
     from pint_amd import _lib as L
-    run(warmup, step)
-    use_graph = False
+    run(warmup * len(sessions), step, sessions)  # every pipeline warmed up
     if graph in (1, "1", "auto"):
-        s.set_timing_mask(0)
-        for _ in range(L.NSLOT):  # one graph per pipeline slot
-            s.capture(step_calls)
-            s.check_step(s.step_end())
-        if graph == "auto":
-            ntry = max(10, min(50, steps // 2))
+        for s in sessions:
+            s.set_timing_mask(0)
+            for _ in range(L.NSLOT):  # one graph per pipeline slot
+                s.capture(lambda: step_calls(s))
+                s.check_step(s.step_end())
+    # the candidates (launch mode, pipelines): fixed by the arguments, or timed on a short
+    # trial each and the fastest kept
+    modes = {"0": ["direct"], "1": ["hip-graph"], "auto": ["direct", "hip-graph"]}[str(graph)]
+    npipe = list(range(1, len(sessions) + 1)) if pipes == "auto" else [min(int(pipes), len(sessions))]
+    cands = [(m, p) for p in npipe for m in modes]
+    if len(cands) > 1:
+        ntry = max(20, min(50, steps // 2))
+        best = None
+        for m, p in cands:
             t0 = time.perf_counter()
-            run(ntry, step)
-            t_direct = time.perf_counter() - t0
-            t0 = time.perf_counter()
-            run(ntry, replay)
-            t_graph = time.perf_counter() - t0
-            use_graph = max_over_ranks(t_graph - t_direct) < 0.0  # the same choice on every rank
-        else:
-            use_graph = True
+            run(ntry, replay if m == "hip-graph" else step, sessions[:p])
+            t = max_over_ranks(time.perf_counter() - t0)  # the same choice on every rank
+            if best is None or t < best[0]:
+                best = (t, m, p)
+        _, mode, p = best
+    else:
+        mode, p = cands[0]
     barrier()
     t0 = time.perf_counter()
-    run(steps, replay if use_graph else step)
+    run(steps, replay if mode == "hip-graph" else step, sessions[:p])
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
     # the Gram kernel's time: the same step with its events, after the timed region
     kt, nk = 0.0, 0
+    s0 = sessions[0]
     if gram_pass:
-        s.set_timing_mask(1 << SLOT_GRAM)
-        kt, nk = run(max(8 * GRAM_EVERY, steps // 2), step)  # (>= 8 sampled launches)
-        s.set_timing_mask(0)
-    return dt, kt, nk, step, ("hip-graph" if use_graph else "direct")
+        s0.set_timing_mask(1 << SLOT_GRAM)
+        kt, nk = run(max(8 * GRAM_EVERY, steps // 2), step, [s0])  # (>= 8 sampled launches)
+        s0.set_timing_mask(0)
+    return dt, kt, nk, (lambda: step(s0)), mode, p
 
 
 def c2_leg(batch, steps, warmup, world, barrier, max_over_ranks):
@@ -425,7 +465,7 @@ def c2_leg(batch, steps, warmup, world, barrier, max_over_ranks):
     lay = s.add(build_layout(model, toas))
     s.set_instances([(lay, pack_table(lay, model))] * batch)
     layout = s.fit_layout(lay)
-    dtb, kt, nk, _, launch = timed_steps(s, steps, warmup, barrier, max_over_ranks)
+    dtb, kt, nk, _, launch, _ = timed_steps(s, steps, warmup, barrier, max_over_ranks)
     s.close()
     out["batched"] = {"metric": f"GLS fits/sec, {batch} B1855 fits per batched step on each of {world} rank(s)",
                       "unit": "fits/s", "value": round(batch * world * steps / dtb, 1), "ms_per_step": round(dtb / steps * 1e3, 4),

@@ -206,6 +206,15 @@ enum { WGT_EVAL = 0, WGT_GRAMV, WGT_GRED, WGT_SCHUR, WGT_SOLVE, WGT_RES1, WGT_RE
        WGT_EXPORT, WGT_OTHER };
 __device__ int g_wgt_on;
 __device__ unsigned long long g_wgt[WGT_K * WGT_B * 2];
+// evaluation blocks' phase stamps (pint_debug_read 9): end of the LDS staging prologue
+// (thread 0), end of the rows' evaluation (atomic max over the waves)
+__device__ unsigned long long g_wgp[WGT_B * 2];
+__device__ __forceinline__ void wgp_stamp(int which, bool first_only) {
+    const int b = blockIdx.x;
+    if (!__builtin_amdgcn_readfirstlane(g_wgt_on) || b >= WGT_B) return;
+    if (first_only ? threadIdx.x == 0 : (threadIdx.x & 63) == 0)
+        atomicMax(&g_wgp[2 * b + which], __builtin_amdgcn_s_memrealtime());
+}
 struct WgTimer {
     int slot;  // (k * WGT_B + b) * 2, or -1 when off / beyond WGT_B
     __device__ __forceinline__ explicit WgTimer(int k) {
@@ -517,6 +526,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
         }
     }
     __syncthreads();
+    wgp_stamp(0, true);
     if (rs.tables && blk_row0[b] == 0) {  // the instance's first block puts the snapshot back
         for (int k = threadIdx.x; k < ts; k += blockDim.x) rs.tables[I.toff + k] = stP ? L.P[k] : tables[I.toff + k];
         const int* cs = reinterpret_cast<const int*>(&L.C);
@@ -541,6 +551,7 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     EvalOut o;
     eval_row<WANT_M, BIN>(S, L, Pd, I, stP, stR, nrun, tables, r, n, own, Mout, dmxv, compact, write_red, status, istatus,
                           ii, ph_hi, ph_lo, ftay, delay_out, dfac, o);
+    wgp_stamp(1, false);
     if (!ef) return;
     // ---- the fused k_resid1 (residuals.py:314-425): tz and d0 from the block's own TZR and
     //      row-0 lanes, then k_resid1's per-row operations and the block's weighted sums ----
@@ -5989,6 +6000,39 @@ int pint_device_count(void) {
     return n;
 }
 
+// Streams outlive their contexts: a destroyed context's streams go back to per-device pools,
+// one per role (kernel, copy, side stream), and a later context takes the oldest (first
+// created) of each role, so the k-th context alive on a device always runs on the streams the k-th context
+// ever created had -- on the same hardware queues.  HIP maps each new stream onto one of
+// GPU_MAX_HW_QUEUES hardware queues as it is created; with streams destroyed and recreated
+// the mapping of a later context's streams changed from context to context, and so did the
+// speed of several contexts' steps run concurrently (bench.py --pipes: 2 x 9-pulsar
+// pipelines 0.105 or 0.138 ms per step by which streams a shard's sessions had got).
+static std::mutex g_stream_mu;
+static std::map<int, std::map<long, hipStream_t>> g_stream_pool[3];  // per role: creation rank -> idle stream
+static std::map<hipStream_t, long> g_stream_rank;
+static long g_stream_made = 0;
+enum { STREAM_KERNEL = 0, STREAM_COPY = 1, STREAM_SIDE = 2 };
+static hipStream_t stream_get(int device, int role) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto& v = g_stream_pool[role][device];
+    if (!v.empty()) {  // the oldest idle stream of the role
+        hipStream_t s = v.begin()->second;
+        v.erase(v.begin());
+        return s;
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    g_stream_rank[s] = g_stream_made++;
+    return s;
+}
+static void stream_put(int device, int role, hipStream_t s) {
+    if (!s) return;
+    hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    g_stream_pool[role][device][g_stream_rank[s]] = s;
+}
+
 pint_ctx* pint_ctx_create(int device) {
     pint_ctx* ctx = new pint_ctx();
     ctx->device = device;
@@ -5998,8 +6042,8 @@ pint_ctx* pint_ctx_create(int device) {
     }
     // (stream priorities -- the kernel stream highest, the copy stream lowest -- measured no
     // different in round 4: 0.376-0.384 vs 0.380-0.387 ms per 68-pulsar step)
-    hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
+    ctx->stream = stream_get(device, STREAM_KERNEL);
+    ctx->cstream = stream_get(device, STREAM_COPY);
     // the cross-stream events are waited on by the device (and ev_done by the host only for
     // completion: everything the host reads comes through copies covered by ev_cdone), so they
     // release to device scope: the default system-scope release writes back the caches and
@@ -6012,7 +6056,7 @@ pint_ctx* pint_ctx_create(int device) {
     // PINT_SERIAL=1 (profiling aid): side-stream kernels run on the main stream, so
     // rocprof's per-kernel durations are not inflated by concurrent kernels
     if (getenv("PINT_SERIAL") && atoi(getenv("PINT_SERIAL"))) ctx->sstream = ctx->stream;
-    else hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking);
+    else ctx->sstream = stream_get(device, STREAM_SIDE);
     ctx->no_events = getenv("PINT_NO_EVENTS") && atoi(getenv("PINT_NO_EVENTS"));
     ctx->eval_merge = getenv("PINT_EVAL_MERGE") ? atoi(getenv("PINT_EVAL_MERGE")) : 3;
     ctx->vbin = getenv("PINT_VBIN") ? (atoi(getenv("PINT_VBIN")) ? 1 : 0) : 1;  // PINT_OPT_VBIN default
@@ -6130,9 +6174,9 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     if (ctx->sstream) hipStreamSynchronize(ctx->sstream);
     if (ctx->ev_gram) hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_sigma) hipEventDestroy(ctx->ev_sigma);
-    if (ctx->sstream && ctx->sstream != ctx->stream) hipStreamDestroy(ctx->sstream);
-    if (ctx->cstream) hipStreamDestroy(ctx->cstream);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->sstream && ctx->sstream != ctx->stream) stream_put(ctx->device, STREAM_SIDE, ctx->sstream);
+    stream_put(ctx->device, STREAM_COPY, ctx->cstream);
+    stream_put(ctx->device, STREAM_KERNEL, ctx->stream);
     delete ctx;
 }
 
@@ -8359,10 +8403,18 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
         for (int i = 0; i < WGT_K * WGT_B * 2; i++) out[i] = (double)t[i];
         return WGT_K * WGT_B * 2;
     }
+    if (which == 9) {  // the evaluation blocks' phase stamps (g_wgp), raw 100 MHz ticks
+        static unsigned long long t[WGT_B * 2];
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wgp), sizeof(t)));
+        for (int i = 0; i < WGT_B * 2; i++) out[i] = (double)t[i];
+        return WGT_B * 2;
+    }
     if (which == 8) {  // the timeline on (out[0] != 0) or off, cleared
         static unsigned long long z[WGT_K * WGT_B * 2];
         HIPCHK(hipStreamSynchronize(ctx->stream));
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgt), z, sizeof(z)));
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgp), z, sizeof(unsigned long long) * WGT_B * 2));
         const int on = out && out[0] != 0.0 ? 1 : 0;
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wgt_on), &on, sizeof(on)));
         HIPCHK(hipDeviceSynchronize());
