@@ -625,17 +625,24 @@ def grid_leg(side, dist, barrier, max_over_ranks):
         dts.append(max_over_ranks(time.perf_counter() - t0))
     dt = float(np.median(dts))
     # per-kernel device time of one more grid (every timing slot's HIP events on, the grid's
-    # one batch of points = one fit step; after the timed grids, which carry no events)
+    # points as one batch on one session = one fit step; after the timed grids, which carry
+    # no events and run on gridutils.GRID_PIPES concurrent sessions)
     from pint_amd import gridutils
-    gs, glay = gridutils._GRID["cur"][1], gridutils._GRID["cur"][2]
-    gs.set_timing_mask(0xFF)
-    grid_chisq(f, ("F0", "F1"), (g0, g1))
-    kt = gs.timing()
-    gs.set_timing_mask(0)
+    npipe = gridutils.GRID_PIPES
+    gridutils.GRID_PIPES = 1
+    try:
+        gs, glay = gridutils._GRID["cur"][1][0]
+        gs.set_timing_mask(0xFF)
+        grid_chisq(f, ("F0", "F1"), (g0, g1))
+        kt = gs.timing()
+        gs.set_timing_mask(0)
+    finally:
+        gridutils.GRID_PIPES = npipe
     roof = grid_roofline(kt, glay, side * side, dt)
     out = {"metric": "chi2-grid points/sec", "value": round(side * side / dt, 1), "unit": "points/s",
            "workload": f"NGC6440E (62 TOAs) {side}x{side} (F0,F1) WLSFitter", "seconds": round(dt, 4),
            "seconds_all": [round(x, 4) for x in dts], "timing": "median of 3 grids after 2 warm-up grids",
+           "pipelines": gridutils.GRID_PIPES if side * side >= 2 * gridutils.GRID_PIPE_MIN else 1,
            "chi2_min": float(np.nanmin(chi2)), "roofline": roof}
     if dist is None:
         out["predicted_strong"] = grid_emulate(f, g0, g1, side, dt)

@@ -44,11 +44,11 @@ def _stub_grid(gu):
     fit (chi2 a fixed function of each point's table; the 'fitted' table shifts DM)."""
     from pint_amd.engine import build_layout
 
-    def session(model, parnames, toas, gls):
+    def session(model, parnames, toas, gls, npipe=1):
         base = copy.deepcopy(model)
         for p in parnames:
             base[p].frozen = True
-        return None, build_layout(base, toas, use_gls_basis=gls)
+        return [(None, build_layout(base, toas, use_gls_basis=gls))] * npipe
 
     def fit_block(s, lay, grid, mode, down, fitargs, want):
         from golden_util import grid_tables

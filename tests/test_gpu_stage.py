@@ -501,6 +501,31 @@ def test_chunked_grid_matches_one_batch(monkeypatch):
     np.testing.assert_array_equal(e_ch["DM"], e_one["DM"])
 
 
+@pytest.mark.parametrize("npipe", [2, 3])
+def test_grid_pipelines_match_one_session(monkeypatch, npipe):
+    """A grid split over concurrent sessions (gridutils.GRID_PIPES: contiguous blocks, each
+    enqueued on its own session before any is waited on) equals the grid on one session, bit
+    for bit, chi2 and extra parameters (62-row points: one N-split whatever the block)."""
+    from pint_amd import WLSFitter, gridutils
+    from pint_amd.gridutils import grid_chisq
+    model, toas = load("ngc6440e")[:2]
+    f = WLSFitter(toas, copy.deepcopy(model))
+    f.fit_toas(maxiter=1)
+    F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+    g = (F0 + np.linspace(-2, 2, 7) * np.longdouble(f.model.F0.uncertainty),
+         F1 + np.linspace(-2, 2, 5) * np.longdouble(f.model.F1.uncertainty))
+    gridutils._drop_grid_session()
+    monkeypatch.setattr(gridutils, "GRID_PIPES", 1)
+    c_one, e_one = grid_chisq(f, ("F0", "F1"), g, extraparnames=["DM"])
+    monkeypatch.setattr(gridutils, "GRID_PIPES", npipe)
+    monkeypatch.setattr(gridutils, "GRID_PIPE_MIN", 4)  # 35 points over npipe sessions
+    c_p, e_p = grid_chisq(f, ("F0", "F1"), g, extraparnames=["DM"])
+    assert len(gridutils._GRID["cur"][1]) == npipe
+    np.testing.assert_array_equal(c_p, c_one)
+    np.testing.assert_array_equal(e_p["DM"], e_one["DM"])
+    gridutils._drop_grid_session()
+
+
 def test_invalid_grid_point_fails_alone():
     """A grid over the DD eccentricity that includes ECC >= 1: those points are NaN (the
     reference's doonefit returns NaN for the failed fit, gridutils.py:89-106) and every other
