@@ -142,7 +142,7 @@ class BatchFit:
         self.tables0 = tables
         self.grid_like = grid is not None or (isinstance(tables, np.ndarray) and tables.ndim == 2 and len(layouts) > 0
                                               and len(set(map(id, layouts))) == 1)  # one layout object (C-level scan)
-        self.layouts0 = list(layouts)
+        self.layouts0 = layouts if grid is not None else list(layouts)  # (a grid's list is its own)
         self._bind(list(layouts), tables)
         # wideband (WidebandTOAFitter / WidebandDownhillFitter): the DM rows join every fit
         # step (k_wb_gram) and every chi2 (the DM chi2 of WidebandTOAResiduals)
@@ -165,10 +165,11 @@ class BatchFit:
         else:
             self.s.set_instances(list(zip(layouts, tables)))
         self.ninst = len(layouts)
+        # (an array: a grid's 65,536-point Python list took ~0.1 ms per any() / np.where)
         if self.grid_like and layouts:
-            self.use_gls_chi2 = [self.gls and (layouts[0].nred > 0 or layouts[0].nep > 0)] * len(layouts)
+            self.use_gls_chi2 = np.full(len(layouts), self.gls and (layouts[0].nred > 0 or layouts[0].nep > 0))
         else:
-            self.use_gls_chi2 = [self.gls and (l.nred > 0 or l.nep > 0) for l in layouts]
+            self.use_gls_chi2 = np.array([self.gls and (l.nred > 0 or l.nep > 0) for l in layouts], dtype=bool)
 
     def _drop(self, bad):
         """Take the device instances flagged in `bad` out of the batch (their current tables
@@ -213,11 +214,11 @@ class BatchFit:
         """Enqueue the chi2 reads of the current residuals; returns a function giving the
         per-instance chi2 (after check() in lazy mode, where the reads land in pinned
         buffers)."""
-        if all(self.use_gls_chi2):
+        if self.use_gls_chi2.all():
             cg = self.s.chi2_gls()
             return lambda: (np.array(cg, dtype=np.float64), None)
         cw = self.s.read_chi2()
-        cg = self.s.chi2_gls() if any(self.use_gls_chi2) else None
+        cg = self.s.chi2_gls() if self.use_gls_chi2.any() else None
         if cg is None:
             return lambda: (np.array(cw, dtype=np.float64), None)
         return lambda: (np.where(self.use_gls_chi2, cg, cw), None)

@@ -1,0 +1,61 @@
+"""Host time of each call of a grid block's enqueue (gridutils._fit_block_start) on the
+256 x 256 NGC6440E (F0, F1) grid: BatchFit set-up (pint_set_grid), the evaluations, the
+step, the update, the chi2 reads, and the wait (us, median of 20 grids)."""
+import copy
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from golden_util import load
+from pint_amd import WLSFitter, gridutils
+from pint_amd.fitter import BatchFit
+from pint_amd.engine import pack_table
+from pint_amd.gridutils import meshgrid_axes
+
+model, toas, _, _ = load("ngc6440e")
+f = WLSFitter(toas, copy.deepcopy(model))
+f.fit_toas(maxiter=1)
+F0, F1 = np.longdouble(f.model.F0.value), np.longdouble(f.model.F1.value)
+side = 256
+g0 = F0 + np.linspace(-3, 3, side) * np.longdouble(f.model.F0.uncertainty)
+g1 = F1 + np.linspace(-3, 3, side) * np.longdouble(f.model.F1.uncertainty)
+gridutils.GRID_PIPES = 1
+pipes = gridutils._grid_session(f.model, ("F0", "F1"), f.toas, False, 1)
+s, lay = pipes[0]
+axes = meshgrid_axes((g0, g1))[0]
+npts = side * side
+rows = []
+for it in range(25):
+    T = [time.perf_counter()]
+    t0 = pack_table(lay, f.model)
+    var = [(p, a, st, sz) for p, (a, st, sz) in zip(("F0", "F1"), axes)]
+    T.append(time.perf_counter())
+    s.set_lazy(True)
+    bf = BatchFit(None, mode="wls", session=s, grid=(lay, t0, var, npts, 0))
+    T.append(time.perf_counter())
+    s.eval(want_M=s.FIT)
+    T.append(time.perf_counter())
+    s.fit_step(0)
+    T.append(time.perf_counter())
+    s.apply_step_uniform(1.0)
+    T.append(time.perf_counter())
+    s.eval(want_M=False)
+    T.append(time.perf_counter())
+    get = bf._chi2_enqueue()
+    T.append(time.perf_counter())
+    s.check()
+    T.append(time.perf_counter())
+    c = get()[0]
+    s.set_lazy(False)
+    T.append(time.perf_counter())
+    rows.append(np.diff(T) * 1e6)
+r = np.median(np.array(rows[5:]), axis=0)
+names = ["pack_table", "BatchFit+set_grid", "eval(FIT)", "fit_step", "apply", "eval", "chi2 enqueue", "check (wait)", "read"]
+for n, v in zip(names, r):
+    print(f"{n:18s} {v:8.1f} us")
+print(f"total {r.sum():.1f} us")
+gridutils._drop_grid_session()
