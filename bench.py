@@ -583,7 +583,7 @@ def load_json(name):
     return None
 
 
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: the committed PMC summaries of this workload
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest first: the committed PMC summaries of this workload
 
 
 def pmc_value(stem, kernel, key, args):

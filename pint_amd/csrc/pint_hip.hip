@@ -6013,10 +6013,15 @@ static std::map<int, std::map<long, hipStream_t>> g_stream_pool[3];  // per role
 static std::map<hipStream_t, long> g_stream_rank;
 static long g_stream_made = 0;
 enum { STREAM_KERNEL = 0, STREAM_COPY = 1, STREAM_SIDE = 2 };
+static int g_stream_pool_on = -1;  // PINT_STREAM_POOL=0: every context creates and destroys its own
+static bool stream_pool_on() {
+    if (g_stream_pool_on < 0) g_stream_pool_on = getenv("PINT_STREAM_POOL") ? (atoi(getenv("PINT_STREAM_POOL")) != 0) : 1;
+    return g_stream_pool_on != 0;
+}
 static hipStream_t stream_get(int device, int role) {
     std::lock_guard<std::mutex> lk(g_stream_mu);
     auto& v = g_stream_pool[role][device];
-    if (!v.empty()) {  // the oldest idle stream of the role
+    if (stream_pool_on() && !v.empty()) {  // the oldest idle stream of the role
         hipStream_t s = v.begin()->second;
         v.erase(v.begin());
         return s;
@@ -6029,6 +6034,10 @@ static hipStream_t stream_get(int device, int role) {
 static void stream_put(int device, int role, hipStream_t s) {
     if (!s) return;
     hipStreamSynchronize(s);
+    if (!stream_pool_on()) {
+        hipStreamDestroy(s);
+        return;
+    }
     std::lock_guard<std::mutex> lk(g_stream_mu);
     g_stream_pool[role][device][g_stream_rank[s]] = s;
 }

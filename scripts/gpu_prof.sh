@@ -8,16 +8,17 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export PINT_GRID_PIPES=1  # (per-kernel figures of one session: no concurrent grid blocks)
 # the 68-pulsar PTA step only: no emulated shards, no cold start (their launches would mix
 # other batch sizes into the per-kernel figures)
-B="python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0"
+B="python3 bench.py --steps 2 --warmup 1 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 --pipes 1"
 # kernel stats at the bench's own length (100 timed steps, steady clocks), its line beside
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-    python3 bench.py --steps 100 --warmup 10 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 \
+    python3 bench.py --steps 100 --warmup 10 --grid 0 --j0740 0 --c2 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 --pipes 1 \
     > gpurun_out/prof.json 2> gpurun_out/prof.log || exit $?
 # C2 (B1855 x 256 batched fits) on its own trace: its kernels share names with the PTA's
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c2 -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --npsr 4 --grid 0 --j0740 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 \
+    python3 bench.py --steps 2 --warmup 1 --npsr 4 --grid 0 --j0740 0 --cpu-baseline 0 --emulate-world 0 --cold-start 0 --pipes 1 \
     > gpurun_out/prof_c2.log 2>&1 || exit $?
 # the (F0, F1) grid alone
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_grid -o run -- \
