@@ -1,4 +1,4 @@
-"""profiles/pmc_gram_rNN.json from scripts/pmc_gram.sh's rocprofv3 --pmc passes: per-kernel
+"""profiles/pmc_gram_rNN.json from scripts/gpu_prof.sh's rocprofv3 --pmc passes: per-kernel
 counters per *step*, where a kernel's step value is the sum over its template
 instantiations of the per-dispatch mean (a fit step launches k_gram_v once per layout
 group), plus derived MFMA figures:
