@@ -137,6 +137,12 @@ struct InstDev {
     long rb0;    // first k_resid row block
     int neb;     // evaluation blocks with the fused residual pass (EF_ROWS rows each; 0: not fused)
     long eb0;    // their first weighted-sum partial (d_epart, 2 per block)
+    // the pulsar's model structure and column runs (copies of its PsrDev fields: the evaluation
+    // blocks' LDS staging starts from the instance record, two dependent loads sooner)
+    const pint_spec_t* spec;
+    const ColRun* runs;
+    int ts;            // spec->tstride
+    int nrun;
 };
 
 // Symmetric view of an instance's Gram [T|r]^T W [T|r] in the original column order:
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(PREP_T) void k_prep(const PsrDev* __restrict__ psrs
 
 constexpr int EVAL_MAXTAB = 512;  // doubles of a parameter table staged in LDS (larger ones read in place)
 constexpr int EVAL_MAXRUN = 64;   // column runs staged in LDS
-struct EvalLds {
+struct alignas(16) EvalLds {  // (16-byte aligned: the staging stores 16-byte words)
     pint_spec_t S;
     InstConst C;
     ColRun R[EVAL_MAXRUN];
@@ -508,22 +514,40 @@ __device__ __forceinline__ void eval_block(int b, const PsrDev* __restrict__ psr
     // the block's instance -- model structure, parameter table, per-instance constants and
     // column runs -- staged in LDS: every row reads them, and an LDS read returns in a
     // fraction of a global (cache) load's latency and needs no address registers
-    const int ts = Pd.spec->tstride, nrun = Pd.nrun;
+    const int ts = I.ts, nrun = I.nrun;
     const bool stP = ts <= EVAL_MAXTAB, stR = nrun <= EVAL_MAXRUN;
     {
-        const int* sg = reinterpret_cast<const int*>(Pd.spec);
-        int* sd = reinterpret_cast<int*>(&L.S);
-        for (int k = threadIdx.x; k < (int)(sizeof(pint_spec_t) / 4); k += blockDim.x) sd[k] = sg[k];
-        const int* cg = reinterpret_cast<const int*>(ic + ii);
-        int* cd = reinterpret_cast<int*>(&L.C);
-        for (int k = threadIdx.x; k < (int)(sizeof(InstConst) / 4); k += blockDim.x) cd[k] = cg[k];
-        if (stP)
-            for (int k = threadIdx.x; k < ts; k += blockDim.x) L.P[k] = tables[I.toff + k];
-        if (stR) {
-            const int* rg = reinterpret_cast<const int*>(Pd.runs);
-            int* rd = reinterpret_cast<int*>(L.R);
-            for (int k = threadIdx.x; k < nrun * (int)(sizeof(ColRun) / 4); k += blockDim.x) rd[k] = rg[k];
-        }
+        // every load of the staging issued before any LDS store, in 16-byte words: one load
+        // latency per block instead of one per strided round (the 4 KB spec alone took five
+        // dependent rounds of 4-byte loads and stores, ~2 us of a block's 14-23 us)
+        static_assert(sizeof(pint_spec_t) % 16 == 0 && sizeof(InstConst) % 16 == 0 && sizeof(ColRun) % 16 == 0,
+                      "eval staging: 16-byte words");
+        constexpr int NS = (int)(sizeof(pint_spec_t) / 16), NC = (int)(sizeof(InstConst) / 16);
+        constexpr int RW = (int)(sizeof(ColRun) / 16);
+        static_assert(NS <= 512 && NC + EVAL_MAXRUN * RW <= 256 && EVAL_MAXTAB <= 512, "eval staging: two rounds of 256");
+        const int t = threadIdx.x;  // (256 threads: every eval_block launch)
+        const int NR = stR ? nrun * RW : 0;
+        const uint4* sg = reinterpret_cast<const uint4*>(I.spec);
+        const uint4* cg = reinterpret_cast<const uint4*>(ic + ii);
+        const uint4* rg = reinterpret_cast<const uint4*>(I.runs);
+        const double* pg = tables + I.toff;
+        const bool hs0 = t < NS, hs1 = t + 256 < NS, hc = t < NC, hr = !hc && t < NC + NR;
+        const bool hp0 = stP && t < ts, hp1 = stP && t + 256 < ts;
+        uint4 s0 = {}, s1 = {}, cr = {};
+        double p0 = 0.0, p1 = 0.0;
+        if (hs0) s0 = sg[t];
+        if (hs1) s1 = sg[t + 256];
+        if (hc) cr = cg[t];
+        else if (hr) cr = rg[t - NC];
+        if (hp0) p0 = pg[t];
+        if (hp1) p1 = pg[t + 256];
+        uint4* sd = reinterpret_cast<uint4*>(&L.S);
+        if (hs0) sd[t] = s0;
+        if (hs1) sd[t + 256] = s1;
+        if (hc) reinterpret_cast<uint4*>(&L.C)[t] = cr;
+        else if (hr) reinterpret_cast<uint4*>(L.R)[t - NC] = cr;
+        if (hp0) L.P[t] = p0;
+        if (hp1) L.P[t + 256] = p1;
     }
     __syncthreads();
     wgp_stamp(0, true);
@@ -6767,6 +6791,10 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
         InstDev& I = ctx->inst[k];
         I.psr = p;
         I.n = ph.n;
+        I.spec = ph.dev.spec;
+        I.runs = ph.dev.runs;
+        I.ts = ph.spec.tstride;
+        I.nrun = ph.dev.nrun;
         I.K = ph.K;
         I.Kp = ph.dev.Kp;
         I.toff = toff;
