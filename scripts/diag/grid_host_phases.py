@@ -28,6 +28,19 @@ pipes = gridutils._grid_session(f.model, ("F0", "F1"), f.toas, False, 1)
 s, lay = pipes[0]
 axes = meshgrid_axes((g0, g1))[0]
 npts = side * side
+from pint_amd.engine import Session
+_sg = Session.set_grid
+tsg = []
+
+
+def timed_set_grid(self, *a, **k):
+    t = time.perf_counter()
+    r = _sg(self, *a, **k)
+    tsg.append(time.perf_counter() - t)
+    return r
+
+
+Session.set_grid = timed_set_grid
 rows = []
 for it in range(25):
     T = [time.perf_counter()]
@@ -57,5 +70,5 @@ r = np.median(np.array(rows[5:]), axis=0)
 names = ["pack_table", "BatchFit+set_grid", "eval(FIT)", "fit_step", "apply", "eval", "chi2 enqueue", "check (wait)", "read"]
 for n, v in zip(names, r):
     print(f"{n:18s} {v:8.1f} us")
-print(f"total {r.sum():.1f} us")
+print(f"total {r.sum():.1f} us; of BatchFit+set_grid, Session.set_grid {np.median(tsg[5:]) * 1e6:.1f} us")
 gridutils._drop_grid_session()
