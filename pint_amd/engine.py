@@ -260,13 +260,20 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
 
 
 def pack_table(lay: PulsarLayout, model: Optional[TimingModel] = None) -> np.ndarray:
+    """The device parameter table of `model` in `lay`'s layout: every parameter as its
+    (hi, lo) double-double split (split_ld's operations, on all parameters at once)."""
     model = model or lay.model
     tab = np.zeros(lay.tstride)
-    for n, o in lay.offsets.items():
-        v = model[n].value
-        if v is None:
-            v = 0.0
-        tab[o], tab[o + 1] = split_ld(v)
+    offs = lay.__dict__.get("_offs_np")
+    if offs is None or offs[0] is not lay.offsets or len(offs[1]) != len(lay.offsets):
+        offs = (lay.offsets, list(lay.offsets), np.fromiter(lay.offsets.values(), dtype=np.int64, count=len(lay.offsets)))
+        lay.__dict__["_offs_np"] = offs
+    names, o = offs[1], offs[2]
+    p = model._params
+    v = np.array([0.0 if p[n].value is None else p[n].value for n in names], dtype=np.longdouble)
+    hi = v.astype(np.float64)
+    tab[o] = hi
+    tab[o + 1] = (v - hi.astype(np.longdouble)).astype(np.float64)
     return tab
 
 

@@ -238,3 +238,18 @@ def test_shard_range_covers():
                 per, lo, hi = shard_range(npts, r, world)
                 got += list(range(lo, max(lo, hi)))
             assert got == list(range(npts))
+
+
+@pytest.mark.parametrize("name", ["ngc6440e", "b1855", "j0740", "pta_dd", "pta_ell1", "pta_iso", "pta_ddk", "wb_dd"])
+def test_pack_table_matches_per_parameter_split(name):
+    """engine.pack_table (all parameters converted at once) equals split_ld parameter by
+    parameter: the same (hi, lo) double-double split, bit for bit."""
+    from pint_amd.engine import build_layout, pack_table, split_ld
+    model, toas = load(name)[:2]
+    lay = build_layout(model, toas)
+    ref = np.zeros(lay.tstride)
+    for n, o in lay.offsets.items():
+        v = model[n].value
+        ref[o], ref[o + 1] = split_ld(0.0 if v is None else v)
+    np.testing.assert_array_equal(pack_table(lay, model), ref)
+    np.testing.assert_array_equal(pack_table(lay, model), ref)  # (the cached offset arrays)
