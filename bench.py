@@ -564,8 +564,12 @@ def roofline(s, lays, kt_gram, step, args):
                                  f"{GRAM_EVERY}th step of a pass after the timed region (averaged over those "
                                  f"launches; the timed steps carry no events); others: a separate "
                                  f"instrumented pass of {nprof} steps (gram_span = Gram + reduction)")}
+    # what sets each one's time (the SQ counters of pmc_r06): the
+    # evaluations' dependent FP64 chains at their occupancy, the residual pass's stream, the
+    # Woodbury solve's per-instance substitution (its bytes are a few KB per pulsar)
+    bound = {"k_eval": "fp64-latency", "k_eval_M": "fp64-latency", "k_resid": "hbm", "k_woodbury": "latency"}
     roof["per_kernel"] = {n: {"GB/s": round(b / (kms[n] * 1e-3) / 1e9, 1), "frac_hbm":
-                              round(b / (kms[n] * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4)}
+                              round(b / (kms[n] * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4), "bound": bound.get(n)}
                           for n, b in nbytes.items() if kms.get(n, 0) > 0}
     gram_equiv = float(sum(2.0 * l.n * (l.K + 1.0) ** 2 for l in lays))
     roof["gram_full_equiv_tflops"] = round(gram_equiv / (kt_gram * 1e-3) / 1e12, 2) if kt_gram > 0 else None
