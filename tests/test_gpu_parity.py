@@ -1583,3 +1583,29 @@ def test_fused_small_residual_pass_matches(monkeypatch):
 
     for x, y in zip(run(1), run(0)):
         np.testing.assert_array_equal(x, y)
+
+
+def test_step_pipelines_match_one_session():
+    """pipelines.StepPipelines: steps enqueued round-robin on two concurrent sessions give
+    every step the same bits as one session's steps (steps, errors, linearised and post-fit
+    chi2): the pipelines share no state."""
+    from pint_amd.pipelines import StepPipelines
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+    got = {}
+
+    def keep(step, out):
+        dp, er, cov, cl, nz, c2 = out
+        got[step] = ([x.copy() for x in dp], [x.copy() for x in er], np.array(cl, copy=True), np.array(c2, copy=True))
+
+    with StepPipelines(items, n=1, on_done=keep) as one:
+        one.enqueue()
+    ref = got.pop(0)
+    with StepPipelines(items, n=2, on_done=keep) as p:
+        for _ in range(10):
+            p.enqueue()
+    assert sorted(got) == list(range(10))
+    for k, (dp, er, cl, c2) in got.items():
+        for x, y in zip(dp + er, ref[0] + ref[1]):
+            np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(cl, ref[2])
+        np.testing.assert_array_equal(c2, ref[3])
