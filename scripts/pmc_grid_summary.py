@@ -6,7 +6,7 @@ WRITE_SIZE, MI355X_MICROARCH.md) and VALU issue utilisation of each grid kernel.
                   (1024 SIMDs x kernel cycles), kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs
 
 Kernel names follow bench.grid_roofline: k_eval_M / k_eval (k_eval<1|0, model> and the
-merged k_eval_mix), k_resid (k_resid1 + k_resid2: one residual pass), k_gram (k_gram_s or
+merged k_eval_mix; for a spin-only grid k_eval_M is k_eval_head + k_eval_spin), k_resid (k_resid1 + k_resid2: one residual pass), k_gram (k_gram_s or
 k_gram), k_solve (k_solve_blk).  A launch's value is the mean over its dispatches.
 
 usage: pmc_grid_summary.py OUT FETCH_DIR WRITE_DIR VALU_DIR
@@ -22,6 +22,8 @@ SIMDS, XCDS = 1024, 8
 
 def key(name):
     n = name.split("(")[0].replace("void ", "").strip()
+    if n.startswith("k_eval_spin") or n.startswith("k_eval_head"):
+        return "k_eval_M"  # a spin-only grid's evaluation with M: the shared head, then each point's spin part
     m = re.match(r"k_eval(_mix)?(_w)?<(\d)", n)
     if m:
         return "k_eval_M" if m.group(3) == "1" else "k_eval"
@@ -41,6 +43,12 @@ def load(d):
         if full.startswith("__amd"):
             continue
         per[key(full)][full][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    # a spin-only grid's evaluation with M is k_eval_head + k_eval_spin; a full k_eval<1, ..>
+    # dispatch beside them is the one-pulsar fit before the grid, not a grid launch
+    em = per.get("k_eval_M", {})
+    if any(f.startswith("k_eval_spin") for f in em):
+        for f in [f for f in em if not (f.startswith("k_eval_spin") or f.startswith("k_eval_head"))]:
+            del em[f]
     # a launch: the sum over the group's kernels of their per-dispatch means
     out = collections.defaultdict(dict)
     for k, byname in per.items():
