@@ -40,6 +40,12 @@ steps = steps[len(steps) // 3:]  # steady state
 dur = [s[-1][1] - s[0][0] for s in steps]
 med = steps[int(np.argsort(dur)[len(dur) // 2])]
 print(f"{len(steps)} steady steps; span median {np.median(dur) / 1e3:.1f} us (min {min(dur) / 1e3:.1f})")
+# the device's step interval: consecutive steps' first dispatches (with several pipelines
+# the steps of the sessions interleave, and a step's span is its latency, not the interval)
+st0 = np.array(sorted(s[0][0] for s in steps), dtype=np.float64)
+if len(st0) > 2:
+    print(f"step interval (start to start): median {np.median(np.diff(st0)) / 1e3:.1f} us, "
+          f"mean {(st0[-1] - st0[0]) / (len(st0) - 1) / 1e3:.1f} us over {len(st0)} steps")
 t0 = med[0][0]
 prev_end = defaultdict(lambda: t0)
 tot = defaultdict(float)
