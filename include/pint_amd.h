@@ -65,6 +65,36 @@ typedef struct {
                                        then the bin indices; NULL when no TOA has more than two */
 } pint_toas_t;
 
+/* The same per-TOA input as the TOA table's own columns (n rows each, no TZR row) plus the TZR
+ * TOA's values and the DMX ranges: the library forms the n+1-row pint_toas_t itself (the TZR
+ * row appended, flags, DMX bins) -- the host packing of engine.pack_toas in native code. */
+typedef struct {
+    int32_t n;
+    const double *tdb_hi, *tdb_lo;  /* n                                                  */
+    const double *freq_mhz;         /* n                                                  */
+    const double *pos_km;           /* n*3 ssb_obs_pos; vel_kms, sun_km likewise          */
+    const double *vel_kms;
+    const double *sun_km;
+    const double *delta_pn;         /* n, or NULL (zeros)                                 */
+    const double *mjd;              /* n float MJDs: the DMX ranges select on them (toa_select.py:101) */
+    const uint8_t *is_bary;         /* n: barycentric observatory                         */
+    const double *sigma_us;         /* n: scaled TOA uncertainty (us), noise_model.py:159  */
+    const double *pulse_number;     /* n, or NULL (zeros)                                 */
+    const uint64_t *jump_mask;      /* n+1, or NULL (no JUMPs)                            */
+    const double *planet_km;        /* (n+1)*15 as in pint_toas_t, or NULL               */
+    double tzr[15];                 /* the TZR TOA: tdb_hi, tdb_lo, freq_mhz, pos[3], vel[3], sun[3],
+                                       delta_pn, mjd, is_bary (0/1)                      */
+    int32_t ndmx;                   /* DMX ranges in parameter order (DMXR1_k, DMXR2_k)   */
+    const double *dmx_r1, *dmx_r2;
+} pint_toa_cols_t;
+
+/* Form the pint_toas_t of `cols` into caller buffers (host only, no device): out->n and every
+ * n+1 (n for sigma_s, pulse_number) array pointer must be set; dmx_x receives the overflow CSR
+ * of TOAs in three or more bins when dmx_x_cap holds it.  Returns that CSR's length (0: none,
+ * out->dmx_x set to NULL; larger than dmx_x_cap: nothing written to dmx_x, call again), or a
+ * negative status.  Bit-identical to engine.pack_toas. */
+int64_t pint_pack_toas(const pint_toa_cols_t *cols, pint_toas_t *out, int32_t *dmx_x, int64_t dmx_x_cap);
+
 /* ---- model structure ------------------------------------------------------------ */
 /* column kinds for the design matrix (timing_model.py:2073 designmatrix)              */
 enum {
@@ -155,6 +185,9 @@ int pint_nslot(void);
  * (noise_model.py:780 get_noise_weights).  The library copies everything it needs. */
 int pint_add_pulsar(pint_ctx *ctx, const pint_toas_t *toas, const pint_spec_t *spec,
                     const double *red_freq, const double *red_phi);
+/* pint_add_pulsar from the TOA table's columns (pint_pack_toas into the context's scratch). */
+int pint_add_pulsar_cols(pint_ctx *ctx, const pint_toa_cols_t *cols, const pint_spec_t *spec,
+                         const double *red_freq, const double *red_phi);
 
 /* Bind `ninst` instances (grid points, PTA pulsars, trial states): inst_psr[k] is a
  * pulsar id; `tables` concatenates each instance's parameter table (spec.tstride doubles,

@@ -34,6 +34,14 @@ class ToasT(C.Structure):
                 ("dmx_x", C.POINTER(C.c_int32))]
 
 
+class ToaColsT(C.Structure):
+    _fields_ = [("n", C.c_int32), ("tdb_hi", dptr), ("tdb_lo", dptr), ("freq_mhz", dptr), ("pos_km", dptr),
+                ("vel_kms", dptr), ("sun_km", dptr), ("delta_pn", dptr), ("mjd", dptr),
+                ("is_bary", C.POINTER(C.c_uint8)), ("sigma_us", dptr), ("pulse_number", dptr),
+                ("jump_mask", C.POINTER(C.c_uint64)), ("planet_km", dptr), ("tzr", C.c_double * 15),
+                ("ndmx", C.c_int32), ("dmx_r1", dptr), ("dmx_r2", dptr)]
+
+
 class SpecT(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("nf", "astrometry", "shapiro", "ndm", "ndmx", "binary", "nfd", "njump",
                                           "track_pn", "subtract_mean", "weighted_mean", "ncol", "nred", "tstride",
@@ -117,6 +125,9 @@ def lib():
     global NSLOT
     NSLOT = int(L.pint_nslot())  # the library's compile-time slot count, not an environment guess
     L.pint_add_pulsar.argtypes = [vp, C.POINTER(ToasT), C.POINTER(SpecT), dptr, dptr]
+    L.pint_add_pulsar_cols.argtypes = [vp, C.POINTER(ToaColsT), C.POINTER(SpecT), dptr, dptr]
+    L.pint_pack_toas.restype = C.c_int64
+    L.pint_pack_toas.argtypes = [C.POINTER(ToaColsT), C.POINTER(ToasT), C.POINTER(C.c_int32), C.c_int64]
     L.pint_set_instances.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), dptr]
     L.pint_set_grid.argtypes = [vp, C.c_int, C.c_int, dptr, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                 C.POINTER(C.c_int64), dptr, C.c_int64]
@@ -181,7 +192,7 @@ EXPORTED = ["pint_ctx_create", "pint_ctx_destroy", "pint_last_error", "pint_rele
             "pint_set_resids", "pint_set_sigma", "pint_set_noise_weights", "pint_set_noise_classes",
             "pint_noise_lnlike", "pint_noise_resids_dm", "pint_set_wideband", "pint_dm_resids", "pint_chi2_wls",
             "pint_apply_step_uniform", "pint_fit_step_apply", "pint_save_tables", "pint_restore_tables", "pint_read_norms",
-            "pint_fit_step_enqueue", "pint_set_grid"]
+            "pint_fit_step_enqueue", "pint_set_grid", "pint_add_pulsar_cols", "pint_pack_toas"]
 
 
 def ptr(a: np.ndarray, ct=C.c_double):

@@ -5607,6 +5607,12 @@ struct pint_ctx {
     // pint_check, behind the kernel stream's last kernel -- so no cross-stream event sits
     // inside the step (the solve's dispatch carried ev_solved: ~5 us of idle stream after it)
     PendArena pend;              // pulsar uploads not committed to the device yet
+    // pint_add_pulsar_cols: the packed columns of the pulsar being added (reused: the pages of
+    // a 10k-TOA pulsar's 1.4 MB are touched once per context, not once per pulsar)
+    std::vector<double> pk_d;
+    std::vector<uint64_t> pk_j;
+    std::vector<uint32_t> pk_f;
+    std::vector<int32_t> pk_i, pk_x;
     std::vector<std::function<int()>> cq;
     std::vector<ExportSeg> exp;  // the deferred work's host-bound outputs (k_export at the flush)
     const int* exp_st_src = nullptr;
@@ -6211,6 +6217,170 @@ void pint_ctx_destroy(pint_ctx* ctx) {
     stream_put(ctx->device, STREAM_COPY, ctx->cstream);
     stream_put(ctx->device, STREAM_KERNEL, ctx->stream);
     delete ctx;
+}
+
+// engine.pack_toas in native code, bit-identical to it: every column with the TZR row appended,
+// flags = is_bary | all(ssb_obs_pos != 0) << 1, sigma_s = sigma_us * 1e-6, and each TOA's DMX
+// bins in parameter order (toa_select.py:101, inclusive ranges; dispersion_model.py:659-678 sums
+// every selecting bin): the first two in dmx_a/dmx_b, any further ones in the dmx_x CSR.  Ranges
+// that sorted by start have non-decreasing ends hold MJD t in the sorted positions lo..hi
+// (lo = #(ends < t), hi = #(starts <= t) - 1): a two-pointer sweep over time-ordered TOAs, a
+// binary search otherwise; other ranges are tested one by one.
+int64_t pint_pack_toas(const pint_toa_cols_t* c, pint_toas_t* o, int32_t* dmx_x, int64_t cap) {
+    if (!c || !o || c->n <= 0 || o->n != c->n) return -PINT_E_INVALID;
+    if (!c->tdb_hi || !c->tdb_lo || !c->freq_mhz || !c->pos_km || !c->vel_kms || !c->sun_km || !c->mjd ||
+        !c->is_bary || !c->sigma_us || (c->ndmx > 0 && (!c->dmx_r1 || !c->dmx_r2)))
+        return -PINT_E_INVALID;
+    if (!o->tdb_hi || !o->tdb_lo || !o->freq_mhz || !o->sigma_s || !o->pos_km || !o->vel_kms || !o->sun_km ||
+        !o->pulse_number || !o->delta_pn || !o->flags || !o->jump_mask || !o->dmx_a || !o->dmx_b)
+        return -PINT_E_INVALID;
+    const int n = c->n;
+    const double* tz = c->tzr;
+    auto col = [&](const double* src, int w, const double* tail, const double* dst_c) {
+        double* dst = const_cast<double*>(dst_c);
+        if (src) memcpy(dst, src, sizeof(double) * w * n);
+        else memset(dst, 0, sizeof(double) * w * n);
+        memcpy(dst + (size_t)w * n, tail, sizeof(double) * w);
+    };
+    col(c->tdb_hi, 1, tz + 0, o->tdb_hi);
+    col(c->tdb_lo, 1, tz + 1, o->tdb_lo);
+    col(c->freq_mhz, 1, tz + 2, o->freq_mhz);
+    col(c->pos_km, 3, tz + 3, o->pos_km);
+    col(c->vel_kms, 3, tz + 6, o->vel_kms);
+    col(c->sun_km, 3, tz + 9, o->sun_km);
+    col(c->delta_pn, 1, tz + 12, o->delta_pn);
+    double* sg = const_cast<double*>(o->sigma_s);
+    for (int i = 0; i < n; i++) sg[i] = c->sigma_us[i] * 1e-6;
+    double* pn = const_cast<double*>(o->pulse_number);
+    if (c->pulse_number) memcpy(pn, c->pulse_number, sizeof(double) * n);
+    else memset(pn, 0, sizeof(double) * n);
+    uint64_t* jm = const_cast<uint64_t*>(o->jump_mask);
+    if (c->jump_mask) memcpy(jm, c->jump_mask, sizeof(uint64_t) * (n + 1));
+    else memset(jm, 0, sizeof(uint64_t) * (n + 1));
+    uint32_t* fl = const_cast<uint32_t*>(o->flags);
+    auto allpos = [](const double* p) { return (uint32_t)(p[0] != 0.0 && p[1] != 0.0 && p[2] != 0.0); };
+    for (int i = 0; i < n; i++) fl[i] = (uint32_t)(c->is_bary[i] != 0) | (allpos(c->pos_km + 3 * i) << 1);
+    fl[n] = (uint32_t)(tz[14] != 0.0) | (allpos(tz + 3) << 1);
+    o->planet_km = c->planet_km;
+
+    int32_t* da = const_cast<int32_t*>(o->dmx_a);
+    int32_t* db = const_cast<int32_t*>(o->dmx_b);
+    const int m = c->ndmx > 0 ? c->ndmx : 0;
+    auto tmjd = [&](int i) { return i < n ? c->mjd[i] : tz[13]; };
+    std::vector<int> order(m);
+    std::vector<double> s1(m), s2(m);
+    bool vec = m > 0;
+    for (int j = 0; j < m; j++) {
+        order[j] = j;
+        vec = vec && !std::isnan(c->dmx_r1[j]) && !std::isnan(c->dmx_r2[j]);
+    }
+    if (vec) {
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->dmx_r1[a] < c->dmx_r1[b]; });
+        for (int k = 0; k < m; k++) {
+            s1[k] = c->dmx_r1[order[k]];
+            s2[k] = c->dmx_r2[order[k]];
+            vec = vec && s1[k] <= s2[k] && (k == 0 || s2[k] >= s2[k - 1]);
+        }
+    }
+    auto search = [&](double t, int& lo, int& hi) {  // lo = #(s2 < t), hi = #(s1 <= t) - 1
+        lo = (int)(std::lower_bound(s2.begin(), s2.end(), t) - s2.begin());
+        hi = (int)(std::upper_bound(s1.begin(), s1.end(), t) - s1.begin()) - 1;
+        if (std::isnan(t)) { lo = m; hi = m - 1; }  // (numpy orders NaN last: no bin)
+    };
+    // the bins of TOA i in parameter order
+    std::vector<int> tmp;
+    auto bins_of = [&](int i, int lo, int hi) -> const std::vector<int>& {
+        tmp.clear();
+        if (vec) {
+            for (int k = lo; k <= hi; k++) tmp.push_back(order[k]);
+            std::sort(tmp.begin(), tmp.end());
+        } else {
+            const double t = tmjd(i);
+            for (int j = 0; j < m; j++)
+                if (t >= c->dmx_r1[j] && t <= c->dmx_r2[j]) tmp.push_back(j);
+        }
+        return tmp;
+    };
+    bool tord = vec;
+    for (int i = 1; i < n && tord; i++) tord = c->mjd[i] >= c->mjd[i - 1];
+    int64_t extra = 0;
+    int lo = 0, hi = -1;
+    for (int i = 0; i <= n; i++) {
+        da[i] = db[i] = -1;
+        if (m == 0) continue;
+        if (vec) {
+            if (tord && i < n) {  // a sweep: both counts only grow with t
+                const double t = c->mjd[i];
+                while (lo < m && s2[lo] < t) lo++;
+                while (hi + 1 < m && s1[hi + 1] <= t) hi++;
+            } else {
+                search(tmjd(i), lo, hi);
+            }
+            const int cnt = hi - lo + 1;
+            if (cnt == 1) {
+                da[i] = order[lo];
+                continue;
+            }
+            if (cnt == 2) {
+                da[i] = std::min(order[lo], order[hi]);
+                db[i] = std::max(order[lo], order[hi]);
+                continue;
+            }
+            if (cnt <= 0) continue;
+        }
+        const std::vector<int>& b = bins_of(i, lo, hi);
+        if (b.size() > 0) da[i] = b[0];
+        if (b.size() > 1) db[i] = b[1];
+        if (b.size() > 2) extra += (int64_t)b.size() - 2;
+    }
+    o->dmx_x = nullptr;
+    if (extra == 0) return 0;
+    const int64_t need = (int64_t)(n + 2) + extra;
+    if (!dmx_x || need > cap) return need;
+    int64_t off = n + 2;
+    for (int i = 0; i <= n; i++) {
+        dmx_x[i] = (int32_t)off;
+        if (vec) search(tmjd(i), lo, hi);
+        const std::vector<int>& b = bins_of(i, lo, hi);
+        for (size_t k = 2; k < b.size(); k++) dmx_x[off++] = b[k];
+    }
+    dmx_x[n + 1] = (int32_t)off;
+    o->dmx_x = dmx_x;
+    return need;
+}
+
+int pint_add_pulsar_cols(pint_ctx* ctx, const pint_toa_cols_t* c, const pint_spec_t* spec, const double* red_freq,
+                         const double* red_phi) {
+    if (!ctx || !c || !spec || c->n <= 0) return -PINT_E_INVALID;
+    const size_t n = (size_t)c->n;
+    ctx->pk_d.resize(15 * (n + 1));  // tdb_hi, tdb_lo, freq, delta_pn, sigma, pulse_number: n+1 each; pos, vel, sun: 3(n+1)
+    ctx->pk_j.resize(n + 1);
+    ctx->pk_f.resize(n + 1);
+    ctx->pk_i.resize(2 * (n + 1));
+    double* D = ctx->pk_d.data();
+    pint_toas_t t;
+    memset(&t, 0, sizeof(t));
+    t.n = c->n;
+    t.tdb_hi = D;
+    t.tdb_lo = D + (n + 1);
+    t.freq_mhz = D + 2 * (n + 1);
+    t.delta_pn = D + 3 * (n + 1);
+    t.sigma_s = D + 4 * (n + 1);
+    t.pulse_number = D + 5 * (n + 1);
+    t.pos_km = D + 6 * (n + 1);
+    t.vel_kms = D + 9 * (n + 1);
+    t.sun_km = D + 12 * (n + 1);
+    t.flags = ctx->pk_f.data();
+    t.jump_mask = ctx->pk_j.data();
+    t.dmx_a = ctx->pk_i.data();
+    t.dmx_b = ctx->pk_i.data() + (n + 1);
+    int64_t need = pint_pack_toas(c, &t, ctx->pk_x.data(), (int64_t)ctx->pk_x.size());
+    if (need > (int64_t)ctx->pk_x.size()) {
+        ctx->pk_x.resize((size_t)need);
+        need = pint_pack_toas(c, &t, ctx->pk_x.data(), need);
+    }
+    if (need < 0) { ctx->err = "pint_add_pulsar_cols: missing TOA column"; return (int)need; }
+    return pint_add_pulsar(ctx, &t, spec, red_freq, red_phi);
 }
 
 int pint_add_pulsar(pint_ctx* ctx, const pint_toas_t* t, const pint_spec_t* spec, const double* red_freq,

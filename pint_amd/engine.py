@@ -390,6 +390,57 @@ def pack_toas(lay: PulsarLayout):
     return t, keep
 
 
+def pack_cols(lay: PulsarLayout):
+    """The TOA table's own columns for pint_add_pulsar_cols / pint_pack_toas: the library
+    forms the n+1-row boundary arrays (pack_toas) itself.  Returns (ToaColsT, keep)."""
+    model, toas = lay.model, lay.toas
+    n = toas.ntoas
+    A = toas.arrays
+    tz = (toas.tzr_for(model) if hasattr(toas, "tzr_for") else toas.tzr) if "AbsPhase" in model.components else None
+    if tz is None:
+        tz = make_tzr_row(model, toas)
+
+    def col(name, w=1):
+        a = np.ascontiguousarray(A[name], dtype=np.float64)
+        if a.size != w * n:
+            raise ValueError(f"TOA column {name}: {a.shape}, expected {n} x {w}")
+        return a
+
+    def tzv(name, default, w=1):
+        return np.asarray(tz[name], dtype=np.float64).reshape(w) if name in tz else np.full(w, default)
+
+    cols = [col("tdb_hi"), col("tdb_lo"), col("freq_mhz"), col("ssb_obs_pos_km", 3), col("ssb_obs_vel_kms", 3),
+            col("obs_sun_pos_km", 3), col("delta_pulse_number"), col("mjd_float")]
+    is_bary = np.ascontiguousarray(np.asarray(A["is_bary"]).astype(bool).astype(np.uint8))
+    tzr = np.concatenate([tzv("tdb_hi", 0.0), tzv("tdb_lo", 0.0), tzv("freq_mhz", np.inf),
+                          tzv("ssb_obs_pos_km", 0.0, 3), tzv("ssb_obs_vel_kms", 0.0, 3), tzv("obs_sun_pos_km", 0.0, 3),
+                          tzv("delta_pulse_number", 0.0), tzv("mjd_float", 0.0),
+                          [float(bool(np.asarray(tz.get("is_bary", [0])).reshape(1)[0]))]])
+    sigma = scaled_sigma_us(model, toas)
+    lay.sigma_us = sigma
+    sigma = np.ascontiguousarray(sigma, dtype=np.float64)
+    pn = toas.get_pulse_numbers()
+    pn = np.ascontiguousarray(pn, dtype=np.float64) if pn is not None else None
+    jm = None
+    jumps = model.mask_params("JUMP")
+    if jumps:
+        jm = np.zeros(n + 1, dtype=np.uint64)
+        for k, name in enumerate(jumps):
+            p = model[name]
+            jm[toas.select_mask(p.key, p.key_value)] |= np.uint64(1) << np.uint64(k)
+            if len(toas.select_mask(p.key, p.key_value, tzr=True)) if toas.tzr else False:
+                jm[n] |= np.uint64(1) << np.uint64(k)
+    tags = [name.split("_")[1] for name in model.dmx_params()]
+    r = (np.array([float(model["DMXR1_" + t].value) for t in tags], dtype=np.float64),
+         np.array([float(model["DMXR2_" + t].value) for t in tags], dtype=np.float64))
+    planet = planet_rows(toas, tz, np.concatenate([is_bary, [int(tzr[14])]]).astype(bool)) \
+        if lay.spec.shapiro == 2 else None
+    c = L.ToaColsT(n, *[L.ptr(a) for a in cols[:7]], L.ptr(cols[7]), L.ptr(is_bary, C.c_uint8), L.ptr(sigma),
+                   L.ptr(pn), L.ptr(jm, C.c_uint64), L.ptr(planet), (C.c_double * 15)(*tzr), len(r[0]),
+                   L.ptr(r[0]), L.ptr(r[1]))
+    return c, [cols, is_bary, sigma, pn, jm, r, planet]
+
+
 SHAPIRO_PLANETS = ("jupiter", "saturn", "venus", "uranus", "neptune")   # solar_system_shapiro.py:112
 
 
@@ -520,8 +571,13 @@ class Session:
             raise L.PintError(rc, self.L.pint_last_error(self.ctx).decode())
 
     def add(self, lay: PulsarLayout, packed=None) -> PulsarLayout:
-        """Upload a pulsar (pint_add_pulsar); packed: its pack_toas(lay) when already formed."""
-        t, keep = packed if packed is not None else pack_toas(lay)
+        """Upload a pulsar: pint_add_pulsar_cols (the library packs the TOA table's columns;
+        packed: pack_cols(lay) when already formed), or pint_add_pulsar when packed is
+        pack_toas(lay) (the numpy packing)."""
+        if packed is None:  # the table's columns, packed by the library (pint_add_pulsar_cols)
+            packed = pack_cols(lay)
+        native = isinstance(packed[0], L.ToaColsT)
+        t, keep = packed
         if lay.red_freq is not None:  # double-double frequencies: hi[nred] then lo[nred]
             f = np.asarray(lay.red_freq, dtype=np.longdouble)
             fh = f.astype(np.float64)
@@ -529,7 +585,10 @@ class Session:
         else:
             rf = np.zeros(2)
         rp = np.ascontiguousarray(lay.red_phi if lay.red_phi is not None else np.zeros(1))
-        pid = self.L.pint_add_pulsar(self.ctx, C.byref(t), C.byref(lay.spec), L.ptr(rf), L.ptr(rp))
+        if native:
+            pid = self.L.pint_add_pulsar_cols(self.ctx, C.byref(t), C.byref(lay.spec), L.ptr(rf), L.ptr(rp))
+        else:
+            pid = self.L.pint_add_pulsar(self.ctx, C.byref(t), C.byref(lay.spec), L.ptr(rf), L.ptr(rp))
         if pid < 0:
             self._check(-pid)
         lay.psr_id = pid

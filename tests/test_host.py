@@ -159,7 +159,7 @@ def test_one_hip_runtime_whatever_loads_first():
 def test_struct_layout_matches_header():
     """ctypes mirrors (pint_amd/_lib.py) == the C header layout (compiled with gcc)."""
     from pint_amd import _lib
-    fields = {"pint_toas_t": _lib.ToasT, "pint_spec_t": _lib.SpecT}
+    fields = {"pint_toas_t": _lib.ToasT, "pint_spec_t": _lib.SpecT, "pint_toa_cols_t": _lib.ToaColsT}
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "pint_amd.h"', 'int main(void){']
     for st, cls in fields.items():
         src.append(f'printf("{st} %zu\\n", sizeof({st}));')
