@@ -430,9 +430,10 @@ def pack_cols(lay: PulsarLayout):
             jm[toas.select_mask(p.key, p.key_value)] |= np.uint64(1) << np.uint64(k)
             if len(toas.select_mask(p.key, p.key_value, tzr=True)) if toas.tzr else False:
                 jm[n] |= np.uint64(1) << np.uint64(k)
-    tags = [name.split("_")[1] for name in model.dmx_params()]
-    r = (np.array([float(model["DMXR1_" + t].value) for t in tags], dtype=np.float64),
-         np.array([float(model["DMXR2_" + t].value) for t in tags], dtype=np.float64))
+    P = model._params
+    tags = [name[4:] for name in model.dmx_params()]  # DMX_<tag>
+    r = tuple(np.array([P[k + t].value for t in tags], dtype=np.longdouble).astype(np.float64)
+              for k in ("DMXR1_", "DMXR2_"))
     planet = planet_rows(toas, tz, np.concatenate([is_bary, [int(tzr[14])]]).astype(bool)) \
         if lay.spec.shapiro == 2 else None
     c = L.ToaColsT(n, *[L.ptr(a) for a in cols[:7]], L.ptr(cols[7]), L.ptr(is_bary, C.c_uint8), L.ptr(sigma),
