@@ -98,7 +98,8 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         if model.PHOFF.value is None:
             model.PHOFF.value = 0.0
         spec.o_PHOFF = place("PHOFF")
-    phoff_free = has_phoff and "PHOFF" in model.free_params
+    free = model.free_params
+    phoff_free = has_phoff and "PHOFF" in free
     spec.wb_noones = 1 if phoff_free else 0
     # (a frozen PHOFF with correlated noise: the Woodbury chi2 appends a column of ones the fit
     # layout does not carry; k_onesrow forms its row of Sigma -- PLRedNoise from the weighted
@@ -197,7 +198,7 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
                       (dms, L.COL_DM), (F, L.COL_F)):
         for j, nm in enumerate(group):
             kind_of[nm] = (kk, j)
-    for n in model.free_params:
+    for n in free:
         p = model[n]
         if p.kind == "mask" and "".join(ch for ch in n if not ch.isdigit()) in noise_like:
             continue

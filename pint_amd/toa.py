@@ -142,14 +142,21 @@ class TOAs:
         is extreme (with lo within half an ulp of hi the order of hi decides but for ties):
         the red-noise span T needs only these, not a longdouble pass over every TOA."""
         hi, lo = self.arrays["tdb_hi"], self.arrays["tdb_lo"]
-        if len(hi) == 0 or not np.all(np.abs(lo) <= 0.5 * np.spacing(np.abs(hi))):
+        if len(hi) == 0:
+            t = self.tdbld
+            return t.min(), t.max()
+        hmin, hmax = hi.min(), hi.max()
+        # every |lo| within half an ulp of its hi: at once when the largest |lo| is within half
+        # an ulp of the smallest positive hi (the ulp only grows with |hi|), else row by row
+        if not (hmin > 0 and max(lo.max(), -lo.min()) <= 0.5 * np.spacing(hmin)) and \
+                not np.all(np.abs(lo) <= 0.5 * np.spacing(np.abs(hi))):
             t = self.tdbld
             return t.min(), t.max()
         out = []
-        for ext in (hi.min(), hi.max()):
+        for ext in (hmin, hmax):
             k = np.flatnonzero(hi == ext)
             v = hi[k].astype(np.longdouble) + lo[k].astype(np.longdouble)
-            out.append(v.min() if ext == hi.min() and len(out) == 0 else v.max())
+            out.append(v.min() if ext == hmin and len(out) == 0 else v.max())
         return out[0], out[1]
 
     def get_mjds(self) -> np.ndarray:

@@ -128,3 +128,20 @@ def test_native_pack_rejects_missing_columns():
     t = L.ToasT()
     t.n = 4
     assert lib.pint_pack_toas(C.byref(c), C.byref(t), None, 0) < 0
+
+
+@pytest.mark.parametrize("case", ["fixture", "unnormalised_lo", "negative"])
+def test_tdbld_extent_equals_longdouble_min_max(case):
+    """TOAs.tdbld_extent (the red-noise span's ends, from the extreme hi parts) equals
+    tdbld.min() / .max(), whichever form of the half-ulp guard it takes."""
+    model, toas = load("b1855")[:2]
+    if case == "unnormalised_lo":  # a lo beyond half an ulp of its hi: the longdouble pass
+        lo = np.array(toas.arrays["tdb_lo"])
+        lo[5] = 3.0
+        toas.arrays["tdb_lo"] = lo
+    elif case == "negative":
+        toas.arrays["tdb_hi"] = -toas.arrays["tdb_hi"]
+        toas.arrays["tdb_lo"] = -toas.arrays["tdb_lo"]
+    lo, hi = toas.tdbld_extent()
+    t = toas.tdbld
+    assert lo == t.min() and hi == t.max()
