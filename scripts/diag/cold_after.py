@@ -1,5 +1,6 @@
 """The first synchronous fit of a fresh 68-pulsar session, call by call (ms), in three
-sessions made one after another in one process (bench.cold_start's sequence)."""
+sessions made one after another in one process (bench.cold_start's sequence).
+    python3 scripts/diag/cold_after.py [nogc] [nohuge]   (nohuge: numpy's hugepage madvise off)"""
 import os
 import sys
 import time
@@ -9,7 +10,11 @@ from pint_amd import simulation as sim
 from pint_amd.engine import Session, build_layout, pack_table
 
 items = sim.make_pta(ntoas=10000, indices=list(range(68)))
-if len(sys.argv) > 1 and sys.argv[1] == "nogc":
+if "nohuge" in sys.argv[1:]:
+    import numpy as np
+    np._core.multiarray._set_madvise_hugepage(False)
+    print("numpy hugepage madvise off")
+if "nogc" in sys.argv[1:]:
     import gc
     gc.collect()
     gc.disable()
