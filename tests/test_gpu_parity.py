@@ -1609,3 +1609,31 @@ def test_step_pipelines_match_one_session():
             np.testing.assert_array_equal(x, y)
         np.testing.assert_array_equal(cl, ref[2])
         np.testing.assert_array_equal(c2, ref[3])
+
+
+@pytest.mark.gpu
+def test_native_packer_uploads_the_same_pulsar():
+    """Session.add's default upload (the library packs the TOA columns, pint_add_pulsar_cols)
+    and the numpy packing (pack_toas -> pint_add_pulsar) give bit-identical residuals and
+    design matrices, DMX overlap (the dmx_x CSR) and PLANET_SHAPIRO included."""
+    from pint_amd.engine import Session, build_layout, pack_table, pack_toas
+    items = [load(n)[:2] for n in ("pta_dd", "dmx_overlap", "planet_ngc", "b1855")]
+    outs = []
+    for native in (True, False):
+        s = Session(0)
+        try:
+            lays = []
+            for m, t in items:
+                lay = build_layout(m, t)
+                lays.append(s.add(lay) if native else s.add(lay, pack_toas(lay)))
+            s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+            s.eval(want_M=True)
+            tr, pr, _ = s.read_resids()
+            M = s.read_designmatrix()
+            outs.append(([np.array(x, copy=True) for x in tr], [np.array(x, copy=True) for x in pr],
+                         [np.array(x, copy=True) for x in M]))
+        finally:
+            s.close()
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
