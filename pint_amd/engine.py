@@ -600,6 +600,44 @@ class Session:
         self.layouts.append(lay)
         return lay
 
+    def add_all(self, items, **layout_kw) -> List[PulsarLayout]:
+        """Add many pulsars ((model, toas) pairs), in order: each pulsar's host layout and
+        TOA columns (build_layout, pack_cols) are formed on this thread while one worker thread
+        uploads the previous ones (pint_add_pulsar_cols runs without the GIL), so the Python
+        host work and the library's packing and staging overlap.  self.add_timing: the
+        caller thread's host ms and the ms it then waited for the uploads."""
+        from concurrent.futures import ThreadPoolExecutor
+        import time
+        t0 = time.perf_counter()
+        futs, lays, failed = [], [], []
+
+        def upload(lay, packed):
+            if failed:  # (nothing after a rejected pulsar, as a loop of add() would stop there)
+                return None
+            try:
+                return self.add(lay, packed)
+            except BaseException as e:
+                failed.append(e)
+                raise
+
+        with ThreadPoolExecutor(1, thread_name_prefix="pint-upload") as ex:
+            try:
+                for m, t in items:
+                    if failed:
+                        break
+                    lay = build_layout(m, t, **layout_kw)
+                    futs.append(ex.submit(upload, lay, pack_cols(lay)))
+                    lays.append(lay)
+            finally:
+                t1 = time.perf_counter()
+                for f in futs:  # in order; the first failure raises (after every upload ended)
+                    f.exception()
+        t2 = time.perf_counter()
+        for f in futs:
+            f.result()
+        self.add_timing = {"host_ms": (t1 - t0) * 1e3, "upload_wait_ms": (t2 - t1) * 1e3}
+        return lays
+
     def set_instances(self, insts: Sequence[tuple]):
         """insts: sequence of (layout, table ndarray)."""
         ids = np.array([lay.psr_id for lay, _ in insts], dtype=np.int32)

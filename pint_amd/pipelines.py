@@ -20,7 +20,7 @@ from typing import Callable, Optional, Sequence
 import numpy as np
 
 from . import _lib as L
-from .engine import Session, build_layout, pack_table
+from .engine import Session, pack_table
 
 
 class StepPipelines:
@@ -40,7 +40,7 @@ class StepPipelines:
         try:
             for _ in range(n):
                 s = Session(device)
-                lays = [s.add(build_layout(m, t)) for m, t in items]
+                lays = s.add_all(items)
                 s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
                 s.save_tables()  # every step fits from these initial models
                 s.set_lazy(True)

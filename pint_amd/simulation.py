@@ -112,7 +112,7 @@ def make_fake_toas_batch(specs: Sequence[dict], seed: Optional[int] = None, maxi
     specs: dicts with model, start, end, ntoas, freq, obs, error_us, add_noise,
     add_correlated_noise, multi_freqs_in_epoch, flags, seed.
     """
-    from .engine import Session, build_layout, pack_table
+    from .engine import Session, pack_table
     from .noise import fourier_basis, red_noise_freqs_weights, scaled_sigma_us
 
     toas_list = []
@@ -129,8 +129,8 @@ def make_fake_toas_batch(specs: Sequence[dict], seed: Optional[int] = None, maxi
     def residuals(track_pn):
         s = Session()
         try:
-            lays = [s.add(build_layout(m, t, track_mode="use_pulse_numbers" if track_pn else "nearest",
-                                       use_gls_basis=False)) for m, t in zip(models, toas_list)]
+            lays = s.add_all(zip(models, toas_list), track_mode="use_pulse_numbers" if track_pn else "nearest",
+                             use_gls_basis=False)
             s.set_instances([(l, pack_table(l)) for l in lays])
             s.eval(False)
             tr, pr, _ = s.read_resids()

@@ -1637,3 +1637,37 @@ def test_native_packer_uploads_the_same_pulsar():
     for a, b in zip(outs[0], outs[1]):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_add_all_matches_sequential_adds_and_stops_at_a_rejected_pulsar():
+    """Session.add_all (host work overlapped with the uploads on a worker thread) adds the
+    pulsars in order with the same bits as add() one by one; a pulsar the library rejects
+    raises its error and nothing after it is added."""
+    from pint_amd._lib import PintError
+    from pint_amd.engine import Session, build_layout, pack_table
+    items = [load(n)[:2] for n in ("pta_dd", "pta_ell1", "pta_iso")]
+    outs = []
+    for batched in (True, False):
+        s = Session(0)
+        try:
+            lays = s.add_all(items) if batched else [s.add(build_layout(m, t)) for m, t in items]
+            assert [l.psr_id for l in lays] == [0, 1, 2] and s.layouts == lays
+            s.set_instances([(l, pack_table(l, m)) for l, (m, _) in zip(lays, items)])
+            s.eval(want_M=False)
+            outs.append([np.array(x, copy=True) for x in s.read_resids()[0]])
+        finally:
+            s.close()
+    for x, y in zip(*outs):
+        np.testing.assert_array_equal(x, y)
+    bad_m, bad_t = load("pta_iso")[:2]
+    err = np.array(bad_t.arrays["err_us"])
+    err[3] = np.nan
+    bad_t.arrays["err_us"] = err
+    s = Session(0)
+    try:
+        with pytest.raises(PintError, match="uncertainty"):
+            s.add_all([items[0], (bad_m, bad_t), items[1]])
+        assert len(s.layouts) == 1
+    finally:
+        s.close()
