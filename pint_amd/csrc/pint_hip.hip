@@ -5390,6 +5390,70 @@ struct StagePool {
     bool busy = false;  // held by a context's pending uploads
 };
 static StagePool g_stage;
+// page-locked host buffers of pint_host_alloc (start -> bytes): copies into them stay direct
+static std::mutex g_pinned_mu;
+static std::map<uintptr_t, size_t> g_pinned;
+static bool host_pinned(const void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a + bytes <= it->first + it->second;
+}
+// device -> host copy.  Into pageable memory a large copy goes through the staging chunk (a
+// page-locked buffer the uploads already made), synchronously, chunk by chunk: left to the
+// runtime, it page-locks the caller's buffer for the copy, and registering or releasing
+// such pages makes the driver evict and restore the process's queues -- a 12-33 ms stall of
+// whichever synchronous call comes next (a fresh session's first fit, DESIGN §3 Round 6;
+// none in 6 sessions with the runtime's own pinning turned off).  Small copies, copies into
+// pint_host_alloc buffers, and a staging chunk in use by a context's uploads: direct.
+constexpr size_t BOUNCE_MIN = (size_t)64 << 10;
+static hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes < BOUNCE_MIN || host_pinned(dst, bytes)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    {
+        std::lock_guard<std::mutex> lk(g_stage.mu);
+        if (g_stage.busy || !g_stage.buf[0]) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+        g_stage.busy = true;
+    }
+    hipError_t e = hipSuccess;
+    for (size_t off = 0; off < bytes && e == hipSuccess; off += g_stage.cap[0]) {
+        const size_t n = std::min(g_stage.cap[0], bytes - off);
+        e = hipMemcpyAsync(g_stage.buf[0], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) memcpy(static_cast<char*>(dst) + off, g_stage.buf[0], n);
+    }
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    g_stage.busy = false;
+    return e;
+}
+// host -> device, the same way round (blocking: hipMemcpy's semantics, else stream-ordered)
+static hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st, bool blocking) {
+    auto direct = [&]() {
+        return blocking ? hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)
+                        : hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    };
+    if (bytes < BOUNCE_MIN || host_pinned(src, bytes)) return direct();
+    {
+        std::lock_guard<std::mutex> lk(g_stage.mu);
+        if (g_stage.busy || !g_stage.buf[0]) return direct();
+        g_stage.busy = true;
+    }
+    hipError_t e = hipSuccess;
+    for (size_t off = 0; off < bytes && e == hipSuccess; off += g_stage.cap[0]) {
+        const size_t n = std::min(g_stage.cap[0], bytes - off);
+        memcpy(g_stage.buf[0], static_cast<const char*>(src) + off, n);
+        if (blocking) {
+            e = hipMemcpy(static_cast<char*>(dst) + off, g_stage.buf[0], n, hipMemcpyHostToDevice);
+        } else {
+            e = hipMemcpyAsync(static_cast<char*>(dst) + off, g_stage.buf[0], n, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    g_stage.busy = false;
+    return e;
+}
 struct PendArena {
     struct Fix {
         size_t psr, field, off;  // pulsar, byte offset of the pointer field in its PsrDev, chunk offset
@@ -5647,7 +5711,7 @@ static int export_seg(pint_ctx* ctx, double* dst, const double* src, long n) {
         return PINT_OK;
     }
     (void)hipGetLastError();
-    HIPCHK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->cstream));
+    HIPCHK(d2h(dst, src, sizeof(double) * n, ctx->cstream));
     return PINT_OK;
 }
 static int launch_export(pint_ctx* ctx) {
@@ -5841,7 +5905,7 @@ static int run_trig_jobs(pint_ctx* ctx, std::vector<TrigJob>& jobs) {
     void *part = nullptr, *dj = nullptr;
     HIPCHK(cmalloc(&part, sizeof(double) * 512 * (size_t)std::max(1, nb)));
     HIPCHK(cmalloc(&dj, sizeof(TrigJob) * jobs.size()));
-    HIPCHK(hipMemcpyAsync(dj, jobs.data(), sizeof(TrigJob) * jobs.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(dj, jobs.data(), sizeof(TrigJob) * jobs.size(), ctx->stream, false));
     hipLaunchKernelGGL(k_trig_setup, dim3(nb), dim3(256), sizeof(double) * 4 * 48 * WT_CS, ctx->stream,
                        (const TrigJob*)dj, (int)jobs.size(), (double*)part);
     hipLaunchKernelGGL(k_trig_sum, dim3((unsigned)jobs.size()), dim3(256), 0, ctx->stream, (const TrigJob*)dj,
@@ -5895,7 +5959,7 @@ static int upload(pint_ctx* ctx, PsrHost& ph, const T* src, size_t count, const 
     size_t bytes = count * sizeof(T);
     if (bytes == 0) bytes = sizeof(T);
     HIPCHK(hipMalloc(&p, bytes));
-    if (src && count) HIPCHK(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    if (src && count) HIPCHK(h2d(p, src, count * sizeof(T), nullptr, true));
     else HIPCHK(hipMemset(p, 0, bytes));
     ph.bufs.push_back(p);
     dst = (const T*)p;
@@ -5908,7 +5972,7 @@ static int flush_chunk(pint_ctx* ctx) {
     if (pa.fix.empty()) return PINT_OK;
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, std::max<size_t>(pa.size, 256)));
-    HIPCHK(hipMemcpyAsync(p, pa.host, pa.size, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(p, pa.host, pa.size, ctx->stream, false));
     if (!pa.done[pa.cur]) HIPCHK(hipEventCreateWithFlags(&pa.done[pa.cur], hipEventDisableTiming));
     HIPCHK(hipEventRecord(pa.done[pa.cur], ctx->stream));
     pa.inflight[pa.cur] = true;
@@ -5953,6 +6017,10 @@ static bool stage_hold(pint_ctx* ctx) {
             if (hipHostMalloc((void**)&g_stage.buf[k], STAGE_CHUNK, hipHostMallocDefault) != hipSuccess) {
                 g_stage.buf[k] = nullptr;
                 return false;
+            }
+            {
+                std::lock_guard<std::mutex> pk(g_pinned_mu);
+                g_pinned[reinterpret_cast<uintptr_t>(g_stage.buf[k])] = STAGE_CHUNK;
             }
             g_stage.cap[k] = STAGE_CHUNK;
         }
@@ -6016,7 +6084,7 @@ static int refresh_psrs(pint_ctx* ctx) {
     std::vector<PsrDev> all;
     for (auto& p : ctx->psrs) all.push_back(p.dev);
     HIPCHK(hipMalloc(&ctx->d_psrs, sizeof(PsrDev) * all.size()));
-    HIPCHK(hipMemcpy(ctx->d_psrs, all.data(), sizeof(PsrDev) * all.size(), hipMemcpyHostToDevice));
+    HIPCHK(h2d(ctx->d_psrs, all.data(), sizeof(PsrDev) * all.size(), nullptr, true));
     return 0;
 }
 
@@ -6744,7 +6812,7 @@ int pint_set_grid(pint_ctx* ctx, int psr, int npts, const double* base, int nvar
     for (long i = 0; i < 2 * nv; i++) spec[ts + 4 * nvar + i] = vals[i];
     dfree((void*&)ctx->d_gridspec);  // (the previous grid's: its tables were formed, the streams synchronised)
     HIPCHK(cmalloc((void**)&ctx->d_gridspec, sizeof(double) * spec.size()));
-    HIPCHK(hipMemcpyAsync(ctx->d_gridspec, spec.data(), sizeof(double) * spec.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(ctx->d_gridspec, spec.data(), sizeof(double) * spec.size(), ctx->stream, false));
     const long total = (long)npts * ts;
     const int nb = (int)std::min<long>((total + 255) / 256, 65536);
     hipLaunchKernelGGL(k_grid_tables, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_gridspec, ts, nvar, npts, (long)k0,
@@ -6945,7 +7013,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     if (!slot_up.empty()) {
         void* p = nullptr;
         HIPCHK(hipMalloc(&p, sizeof(int32_t) * slot_host.size()));
-        HIPCHK(hipMemcpy(p, slot_host.data(), sizeof(int32_t) * slot_host.size(), hipMemcpyHostToDevice));
+        HIPCHK(h2d(p, slot_host.data(), sizeof(int32_t) * slot_host.size(), nullptr, true));
         ctx->psrs[slot_up[0].first].bufs.push_back(p);  // (freed with the first pulsar's buffers)
         for (auto& u : slot_up) ctx->psrs[u.first].dev.dslot = static_cast<const int32_t*>(p) + u.second;
     }
@@ -7069,7 +7137,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     ctx->blk_off[PINT_NBIN] = (int)bi.size();
     ctx->nblk = ctx->blk_off[3];  // k_eval_mix covers the isolated, ELL1 and DD blocks
     HIPCHK(cmalloc((void**)&ctx->d_inst, sizeof(InstDev) * ninst));
-    HIPCHK(hipMemcpy(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, hipMemcpyHostToDevice));
+    HIPCHK(h2d(ctx->d_inst, ctx->inst.data(), sizeof(InstDev) * ninst, nullptr, true));
     for (int lay = 0; lay < 3; lay++) {  // k_gram launch groups: full, compact, compact + vg
         std::vector<InstDev> sorted;
         std::vector<KpGroup>& groups = lay == 0 ? ctx->kp_groups : (lay == 1 ? ctx->kp_groups_c : ctx->kp_groups_v);
@@ -7149,7 +7217,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
         }
         HIPCHK(cmalloc((void**)&dst, sizeof(InstDev) * std::max<size_t>(1, sorted.size())));
         if (!sorted.empty())
-            HIPCHK(hipMemcpy(dst, sorted.data(), sizeof(InstDev) * sorted.size(), hipMemcpyHostToDevice));
+            HIPCHK(h2d(dst, sorted.data(), sizeof(InstDev) * sorted.size(), nullptr, true));
     }
     if (getenv("PINT_VERBOSE")) {
         for (auto& g : ctx->kp_groups_v) fprintf(stderr, "[pint] k_gram_v group key %d: %d instances, max width %d\n", g.T, g.count, g.maxKp);
@@ -7167,12 +7235,12 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     HIPCHK(cmalloc((void**)&ctx->d_TS, sizeof(double) * std::max<long>(1, (long)ninst * 4 * VTRIG)));
     HIPCHK(cmalloc((void**)&ctx->d_blk_inst, sizeof(int) * bi.size()));
     HIPCHK(cmalloc((void**)&ctx->d_blk_row0, sizeof(int) * br.size()));
-    HIPCHK(hipMemcpy(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ctx->d_blk_row0, br.data(), sizeof(int) * br.size(), hipMemcpyHostToDevice));
+    HIPCHK(h2d(ctx->d_blk_inst, bi.data(), sizeof(int) * bi.size(), nullptr, true));
+    HIPCHK(h2d(ctx->d_blk_row0, br.data(), sizeof(int) * br.size(), nullptr, true));
     ctx->nrblk = (int)rbi.size();
     HIPCHK(cmalloc((void**)&ctx->d_rblk_inst, sizeof(int) * std::max<size_t>(1, rbi.size())));
     if (!rbi.empty())
-        HIPCHK(hipMemcpy(ctx->d_rblk_inst, rbi.data(), sizeof(int) * rbi.size(), hipMemcpyHostToDevice));
+        HIPCHK(h2d(ctx->d_rblk_inst, rbi.data(), sizeof(int) * rbi.size(), nullptr, true));
     HIPCHK(cmalloc((void**)&ctx->d_rpart, sizeof(double) * 3 * std::max<size_t>(1, rbi.size())));
     HIPCHK(cmalloc((void**)&ctx->d_epart, sizeof(double) * 2 * std::max<long>(1, ebn)));
     // the post-fit Woodbury dots fused into the residual pass (k_resid2 tiles, k_rsum): every
@@ -7202,7 +7270,7 @@ static int set_instances_impl(pint_ctx* ctx, int ninst, const int32_t* inst_psr,
     }
 
     HIPCHK(cmalloc((void**)&ctx->d_tables, sizeof(double) * toff));
-    if (tables) HIPCHK(hipMemcpy(ctx->d_tables, tables, sizeof(double) * toff, hipMemcpyHostToDevice));
+    if (tables) HIPCHK(h2d(ctx->d_tables, tables, sizeof(double) * toff, nullptr, true));
     HIPCHK(cmalloc((void**)&ctx->d_phhi, sizeof(double) * roff));
     HIPCHK(cmalloc((void**)&ctx->d_phlo, sizeof(double) * roff));
     HIPCHK(cmalloc((void**)&ctx->d_ftay, sizeof(double) * roff));
@@ -7262,13 +7330,13 @@ static int flush_chi2(pint_ctx* ctx) {
     if (!ctx->chi2_dst) return PINT_OK;
     double* dst = ctx->chi2_dst;
     ctx->chi2_dst = nullptr;
-    HIPCHK(hipMemcpyAsync(dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(dst, ctx->d_chi2g, sizeof(double) * ctx->ninst, ctx->stream));
     return PINT_OK;
 }
 
 int pint_get_tables(pint_ctx* ctx, double* out) {
     if (flush_restore(ctx)) return PINT_E_HIP;
-    HIPCHK(hipMemcpyAsync(out, ctx->d_tables, sizeof(double) * ctx->tot_table, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out, ctx->d_tables, sizeof(double) * ctx->tot_table, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -7278,7 +7346,7 @@ int pint_set_tables(pint_ctx* ctx, const double* tables) {
     ctx->tables_fresh = false;
     ctx->restore_pending = false;  // overwritten anyway
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
-    HIPCHK(hipMemcpyAsync(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(ctx->d_tables, tables, sizeof(double) * ctx->tot_table, ctx->stream, false));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -7320,7 +7388,7 @@ static int check_status(pint_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->cstream));
     clear_copy_pend(ctx);
     HIPCHK(hipStreamSynchronize(ctx->sstream));
-    HIPCHK(hipMemcpyAsync(&st, ctx->d_status, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(&st, ctx->d_status, sizeof(int), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     // the status word accumulates error bits of everything enqueued since the last check
     if (st) HIPCHK(hipMemsetAsync(ctx->d_status, 0, sizeof(int), ctx->stream));
@@ -7564,9 +7632,9 @@ int pint_read_resids(pint_ctx* ctx, double* time_resid, double* phase_resid, dou
         HIPCHK(hipGetLastError());
         ctx->chi2_pending = false;
     }
-    if (time_resid) HIPCHK(hipMemcpyAsync(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
-    if (phase_resid) HIPCHK(hipMemcpyAsync(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
-    if (chi2) HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    if (time_resid) HIPCHK(d2h(time_resid, ctx->d_rt, sizeof(double) * ctx->tot_out, ctx->stream));
+    if (phase_resid) HIPCHK(d2h(phase_resid, ctx->d_rp, sizeof(double) * ctx->tot_out, ctx->stream));
+    if (chi2) HIPCHK(d2h(chi2, ctx->d_chi2, sizeof(double) * ctx->ninst, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));  // lazy: valid after pint_check
     return PINT_OK;
 }
@@ -7612,24 +7680,24 @@ int pint_dm_resids(pint_ctx* ctx, int subtract_mean, int use_weighted_mean, doub
     hipLaunchKernelGGL(k_dm_resid, dim3(ctx->ninst), dim3(DMR_T), 0, ctx->stream, ctx->d_psrs, ctx->d_inst,
                        ctx->d_tables, subtract_mean, use_weighted_mean, ctx->d_dmr, ctx->d_dmc2);
     HIPCHK(hipGetLastError());
-    if (resid_out) HIPCHK(hipMemcpyAsync(resid_out, ctx->d_dmr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, ctx->stream));
-    if (chi2_out) HIPCHK(hipMemcpyAsync(chi2_out, ctx->d_dmc2, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    if (resid_out) HIPCHK(d2h(resid_out, ctx->d_dmr, sizeof(double) * ctx->tot_out, ctx->stream));
+    if (chi2_out) HIPCHK(d2h(chi2_out, ctx->d_dmc2, sizeof(double) * ctx->ninst, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
 int pint_read_eval(pint_ctx* ctx, double* ph_hi, double* ph_lo, double* ftaylor, double* delay) {
     size_t b = sizeof(double) * ctx->tot_rows;
-    if (ph_hi) HIPCHK(hipMemcpyAsync(ph_hi, ctx->d_phhi, b, hipMemcpyDeviceToHost, ctx->stream));
-    if (ph_lo) HIPCHK(hipMemcpyAsync(ph_lo, ctx->d_phlo, b, hipMemcpyDeviceToHost, ctx->stream));
-    if (ftaylor) HIPCHK(hipMemcpyAsync(ftaylor, ctx->d_ftay, b, hipMemcpyDeviceToHost, ctx->stream));
-    if (delay) HIPCHK(hipMemcpyAsync(delay, ctx->d_delay, b, hipMemcpyDeviceToHost, ctx->stream));
+    if (ph_hi) HIPCHK(d2h(ph_hi, ctx->d_phhi, b, ctx->stream));
+    if (ph_lo) HIPCHK(d2h(ph_lo, ctx->d_phlo, b, ctx->stream));
+    if (ftaylor) HIPCHK(d2h(ftaylor, ctx->d_ftay, b, ctx->stream));
+    if (delay) HIPCHK(d2h(delay, ctx->d_delay, b, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
 
 int pint_read_designmatrix(pint_ctx* ctx, double* M) {
-    HIPCHK(hipMemcpyAsync(M, ctx->d_M, sizeof(double) * ctx->tot_m, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(M, ctx->d_M, sizeof(double) * ctx->tot_m, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -8072,7 +8140,7 @@ int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* nd
     if (ctx->degv_cap < maxK) { ctx->err = "eig scratch too small"; return PINT_E_INVALID; }
     const size_t lds = sizeof(double) * (4 * (size_t)maxK + maxK + 2);
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));
-    HIPCHK(hipMemcpyAsync(ctx->d_lam, threshold, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(ctx->d_lam, threshold, sizeof(double) * ctx->ninst, ctx->stream, false));
     ctx->cov_pending = false;  // k_eig writes every instance's covariance
     hipLaunchKernelGGL(k_eig, dim3(ctx->ninst), dim3(EIG_T), lds, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
                        ctx->d_colsq, ctx->nsplit, mode, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_lam,
@@ -8080,9 +8148,9 @@ int pint_solve_eig(pint_ctx* ctx, int mode, const double* threshold, int32_t* nd
                        ctx->d_degv, ctx->degv_cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->ev_solved, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ndeg, ctx->d_ndeg, sizeof(int) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(ndeg, ctx->d_ndeg, sizeof(int) * ctx->ninst, ctx->stream));
     std::vector<double> tmp((size_t)ctx->ninst * PINT_EIG_MAXDEG * ctx->degv_cap);
-    HIPCHK(hipMemcpyAsync(tmp.data(), ctx->d_degv, sizeof(double) * tmp.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(tmp.data(), ctx->d_degv, sizeof(double) * tmp.size(), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < ctx->ninst; i++)
         for (int d = 0; d < PINT_EIG_MAXDEG; d++)
@@ -8145,10 +8213,10 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
         HIPCHK(hipGetLastError());
         ctx->cov_pending = cov == nullptr;  // errors only: a later read of the covariance re-runs it
     }
-    if (dpars) HIPCHK(hipMemcpyAsync(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
-    if (errs) HIPCHK(hipMemcpyAsync(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, st));
-    if (cov) HIPCHK(hipMemcpyAsync(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, hipMemcpyDeviceToHost, st));
-    if (chi2lin) HIPCHK(hipMemcpyAsync(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, st));
+    if (dpars) HIPCHK(d2h(dpars, ctx->d_dpars, sizeof(double) * ctx->tot_c, st));
+    if (errs) HIPCHK(d2h(errs, ctx->d_errs, sizeof(double) * ctx->tot_c, st));
+    if (cov) HIPCHK(d2h(cov, ctx->d_cov, sizeof(double) * ctx->tot_cv, st));
+    if (chi2lin) HIPCHK(d2h(chi2lin, ctx->d_chi2lin, sizeof(double) * ctx->ninst, st));
     if (ctx->lazy) {
         HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
         ctx->copy_pend[ctx->slot] = true;
@@ -8161,18 +8229,25 @@ int pint_read_step(pint_ctx* ctx, double* dpars, double* errs, double* cov, doub
 void* pint_host_alloc(size_t bytes) {
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes ? bytes : 8, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes ? bytes : 8;
     return p;
 }
 
 void pint_host_free(void* p) {
-    if (p) hipHostFree(p);
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+    }
+    hipHostFree(p);
 }
 
 int pint_apply_step(pint_ctx* ctx, const double* lambda_) {
     if (!ctx || ctx->ninst <= 0 || !lambda_) return PINT_E_INVALID;
     if (flush_restore(ctx)) return PINT_E_HIP;
     if (ctx->sigma_pending) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_sigma, 0));  // k_sigma reads F0
-    HIPCHK(hipMemcpyAsync(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(ctx->d_lam, lambda_, sizeof(double) * ctx->ninst, ctx->stream, false));
     launch_apply(ctx, ctx->d_lam, 0.0);
     HIPCHK(hipGetLastError());
     ctx->ic_valid = true;
@@ -8301,7 +8376,7 @@ int pint_chi2_gls(pint_ctx* ctx, double* chi2) {
         ctx->chi2_dst = chi2;
         return PINT_OK;
     }
-    HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -8316,7 +8391,7 @@ int pint_chi2_wls(pint_ctx* ctx, double* chi2) {
     hipLaunchKernelGGL(k_chi2w, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt,
                        ctx->d_chi2g);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(chi2, ctx->d_chi2g, sizeof(double) * ctx->ninst, ctx->stream));
     if (!ctx->lazy) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -8432,7 +8507,7 @@ int pint_lognorm(pint_ctx* ctx, int gls, double* out) {
                          : 0.5 * (2.0 * d.logsig + std::log(1e40) + std::log(1e-40 + d.sumw));
         }
     } else if (gls) {
-        HIPCHK(hipMemcpyAsync(out, ctx->d_lognorm, sizeof(double) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(d2h(out, ctx->d_lognorm, sizeof(double) * ctx->ninst, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
     } else {
         for (int k = 0; k < ctx->ninst; k++) out[k] = ctx->psrs[ctx->inst[k].psr].dev.logsig;
@@ -8494,7 +8569,7 @@ int pint_step_end(pint_ctx* ctx, int* slot) {
     if (int rc = flush_cq(ctx, ctx->ev_done[s])) return rc;
     lap("flush");
     if (!st_exp)  // (no device-visible address of the status mirror: a runtime copy)
-        HIPCHK(hipMemcpyAsync(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), hipMemcpyDeviceToHost, ctx->cstream));
+        HIPCHK(d2h(ctx->h_status + s, ctx->d_status_slots + s, sizeof(int), ctx->cstream));
     HIPCHK(hipEventRecord(ctx->ev_cdone[s], ctx->cstream));
     lap("record ev_cdone");
     ctx->cdone_rec[s] = true;
@@ -8635,7 +8710,7 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
     }
     size_t n = which == 0 ? ctx->tot_g : which == 1 ? ctx->tot_c * ctx->nsplit : ctx->tot_s;
     double* src = which == 0 ? ctx->d_G : which == 1 ? ctx->d_colsq : which == 2 ? ctx->d_sigL : ctx->d_work;
-    HIPCHK(hipMemcpyAsync(out, src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out, src, sizeof(double) * n, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return ctx->nsplit;
 }
@@ -8647,7 +8722,7 @@ int pint_debug_read(pint_ctx* ctx, int which, double* out) {
 int pint_inst_status(pint_ctx* ctx, int32_t* out) {
     if (!ctx || ctx->ninst <= 0 || !out) return PINT_E_INVALID;
     hipSetDevice(ctx->device);
-    HIPCHK(hipMemcpyAsync(out, ctx->d_istatus, sizeof(int) * ctx->ninst, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out, ctx->d_istatus, sizeof(int) * ctx->ninst, ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_istatus, 0, sizeof(int) * ctx->ninst, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
@@ -8720,8 +8795,8 @@ int pint_noise_resids(pint_ctx* ctx, double* red, double* ecorr) {
                                ctx->d_inst, ctx->d_dpars, ctx->d_esum, ctx->d_eD, de, ctx->m_compact, ctx->d_eC);
     }
     if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids: launch failed"; return PINT_E_HIP; }
-    if (red) HIPCHK(hipMemcpyAsync(red, dr, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
-    if (ecorr) HIPCHK(hipMemcpyAsync(ecorr, de, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
+    if (red) HIPCHK(d2h(red, dr, sizeof(double) * ctx->tot_out, st));
+    if (ecorr) HIPCHK(d2h(ecorr, de, sizeof(double) * ctx->tot_out, st));
     if (ctx->lazy) {
         HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
         ctx->copy_pend[ctx->slot] = true;
@@ -8770,7 +8845,7 @@ int pint_noise_resids_dm(pint_ctx* ctx, double* dm) {
     hipLaunchKernelGGL(k_noise_red, dim3((maxn + 255) / 256, ctx->ninst), dim3(256), 0, st, ctx->d_psrs,
                        ctx->d_inst, ctx->d_dpars, d, 1, ctx->d_dfac);
     if (hipGetLastError() != hipSuccess) { ctx->err = "pint_noise_resids_dm: launch failed"; return PINT_E_HIP; }
-    HIPCHK(hipMemcpyAsync(dm, d, sizeof(double) * ctx->tot_out, hipMemcpyDeviceToHost, st));
+    HIPCHK(d2h(dm, d, sizeof(double) * ctx->tot_out, st));
     if (ctx->lazy) {
         HIPCHK(hipEventRecord(ctx->ev_copied, ctx->cstream));
         ctx->copy_pend[ctx->slot] = true;
@@ -8792,7 +8867,7 @@ int pint_read_norms(pint_ctx* ctx, int mode, double* out) {
     hipLaunchKernelGGL(k_norms, dim3(ctx->ninst), dim3(64), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
                        ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, mode, ctx->d_norms);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, ctx->d_norms, sizeof(double) * ctx->tot_c, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out, ctx->d_norms, sizeof(double) * ctx->tot_c, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -8810,12 +8885,12 @@ int pint_debug_gram(pint_ctx* ctx, int pre_ecorr, double* out) {
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     HIPCHK(hipMalloc(&d, sizeof(double) * off[ctx->ninst]));
     HIPCHK(hipMalloc(&doff, sizeof(long) * ctx->ninst));
-    HIPCHK(hipMemcpy(doff, off.data(), sizeof(long) * ctx->ninst, hipMemcpyHostToDevice));
+    HIPCHK(h2d(doff, off.data(), sizeof(long) * ctx->ninst, nullptr, true));
     hipLaunchKernelGGL(k_debug_gram, dim3(ctx->ninst), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_G,
                        ctx->d_colsq, ctx->nsplit, ctx->m_compact, ctx->d_Sd, ctx->d_DD, ctx->d_DCS, ctx->d_esum,
                        ctx->d_eD, pre_ecorr && ctx->max_nep > 0, doff, d, ctx->d_eC);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, d, sizeof(double) * off[ctx->ninst], hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out, d, sizeof(double) * off[ctx->ninst], ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     hipFree(d);
     hipFree(doff);
@@ -8829,7 +8904,7 @@ int pint_debug_set_resids(pint_ctx* ctx, const double* time_resid) {
     if (!ctx || ctx->ninst <= 0 || !time_resid) return PINT_E_INVALID;
     flush_r2(ctx);  // (its rpart partials and phases first; the time residuals are replaced below)
     hipSetDevice(ctx->device);
-    HIPCHK(hipMemcpyAsync(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(ctx->d_rt, time_resid, sizeof(double) * ctx->tot_out, ctx->stream, false));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->wtile_valid = false;  // the fused Woodbury dots were those of the replaced residuals
     return PINT_OK;
@@ -8856,8 +8931,8 @@ int pint_set_sigma(pint_ctx* ctx, int psr, const double* sigma_s) {
         sw += is[i] * is[i];
     }
     HIPCHK(hipStreamSynchronize(ctx->sstream));
-    HIPCHK(hipMemcpyAsync((void*)ph.dev.sigma, sigma_s, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync((void*)ph.dev.isig, is.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d((void*)ph.dev.sigma, sigma_s, sizeof(double) * n, ctx->stream, false));
+    HIPCHK(h2d((void*)ph.dev.isig, is.data(), sizeof(double) * n, ctx->stream, false));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (ph.spec.nred > 0 && form_trigw(ctx, ph)) return PINT_E_HIP;  // the F^T W F sums of the new weights
     ph.dev.logsig = ls;
@@ -8881,9 +8956,9 @@ int pint_set_noise_weights(pint_ctx* ctx, int psr, const double* red_phi, const 
             if (!(ep_phi[e] > 0.0)) { ctx->err = "ECORR weight must be > 0"; return PINT_E_INVALID; }
     HIPCHK(hipStreamSynchronize(ctx->sstream));
     if (red_phi && nred > 0)
-        HIPCHK(hipMemcpyAsync((void*)ph.dev.red_phi, red_phi, sizeof(double) * 2 * nred, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(h2d((void*)ph.dev.red_phi, red_phi, sizeof(double) * 2 * nred, ctx->stream, false));
     if (ep_phi && nep > 0)
-        HIPCHK(hipMemcpyAsync((void*)ph.dev.ep_phi, ep_phi, sizeof(double) * nep, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(h2d((void*)ph.dev.ep_phi, ep_phi, sizeof(double) * nep, ctx->stream, false));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }
@@ -8959,16 +9034,16 @@ int pint_noise_lnlike(pint_ctx* ctx, const int32_t* kind, const double* cls_qf, 
     double* d_eg = d_sv + 2 * nep;
     double* d_out = d_eg + nep;
     static_assert(sizeof(long) == sizeof(double), "meta packing");
-    HIPCHK(hipMemcpyAsync(d_meta, meta.data(), sizeof(long) * meta.size(), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(d_q, cls_qf, sizeof(double) * 2 * nq, hipMemcpyHostToDevice, ctx->stream));
-    if (any_ep) HIPCHK(hipMemcpyAsync(d_w, ep_w, sizeof(double) * ctx->tot_ep, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(h2d(d_meta, meta.data(), sizeof(long) * meta.size(), ctx->stream, false));
+    HIPCHK(h2d(d_q, cls_qf, sizeof(double) * 2 * nq, ctx->stream, false));
+    if (any_ep) HIPCHK(h2d(d_w, ep_w, sizeof(double) * ctx->tot_ep, ctx->stream, false));
     hipLaunchKernelGGL(k_noise_lnl, dim3(ni), dim3(256), 0, ctx->stream, ctx->d_psrs, ctx->d_inst, ctx->d_rt, d_meta,
                        d_q, d_w, d_sv, d_out, d_g, d_eg);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out3, d_out, sizeof(double) * 3 * ni, hipMemcpyDeviceToHost, ctx->stream));
-    if (cls_g) HIPCHK(hipMemcpyAsync(cls_g, d_g, sizeof(double) * 2 * nq, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(d2h(out3, d_out, sizeof(double) * 3 * ni, ctx->stream));
+    if (cls_g) HIPCHK(d2h(cls_g, d_g, sizeof(double) * 2 * nq, ctx->stream));
     if (ep_g && ctx->tot_ep > 0)
-        HIPCHK(hipMemcpyAsync(ep_g, d_eg, sizeof(double) * ctx->tot_ep, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(d2h(ep_g, d_eg, sizeof(double) * ctx->tot_ep, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PINT_OK;
 }

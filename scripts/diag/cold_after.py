@@ -1,6 +1,8 @@
 """The first synchronous fit of a fresh 68-pulsar session, call by call (ms), in three
 sessions made one after another in one process (bench.cold_start's sequence).
-    python3 scripts/diag/cold_after.py [nogc] [nohuge]   (nohuge: numpy's hugepage madvise off)"""
+    python3 scripts/diag/cold_after.py [nogc] [nohuge] [pinout]
+(nohuge: numpy's hugepage madvise off; pinout: read_step into page-locked buffers, not fresh
+pageable arrays)"""
 import os
 import sys
 import time
@@ -27,7 +29,13 @@ for rep in range(3):
     T = [time.perf_counter()]
     s.eval(want_M=Session.FIT); T.append(time.perf_counter())
     s.fit_step_apply(1, 1.0); T.append(time.perf_counter())
-    s.read_step(); T.append(time.perf_counter())
+    if "pinout" in sys.argv[1:]:
+        s.lazy = True  # (Python side only: read_step's outputs from the pinned per-name pool)
+        s.read_step()
+        s.lazy = False
+    else:
+        s.read_step()
+    T.append(time.perf_counter())
     s.noise_resids(); T.append(time.perf_counter())
     s.eval(want_M=False); T.append(time.perf_counter())
     s.chi2_gls(); T.append(time.perf_counter())
