@@ -220,11 +220,10 @@ def build_layout(model: TimingModel, toas, track_mode=None, subtract_mean=True, 
         toffs.append(offs[n])
     if len(cols) > L.MAX_COLS:
         raise NotImplementedError("too many design-matrix columns")
-    spec.ncol = len(cols)
-    for j in range(len(cols)):
-        spec.col_kind[j] = kinds[j]
-        spec.col_index[j] = idxs[j]
-        spec.col_toff[j] = toffs[j]
+    spec.ncol = nc = len(cols)
+    spec.col_kind[:nc] = kinds
+    spec.col_index[:nc] = idxs
+    spec.col_toff[:nc] = toffs
     tm = _track_mode(model, toas, track_mode)
     spec.track_pn = 1 if tm == "use_pulse_numbers" else 0
     spec.subtract_mean = 1 if (subtract_mean and not has_phoff) else 0
