@@ -5416,13 +5416,29 @@ static hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) 
         if (g_stage.busy || !g_stage.buf[0]) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
         g_stage.busy = true;
     }
+    // the two chunks alternate: chunk k's DMA runs while chunk k-1 is copied out on the host
+    static hipEvent_t ev[2] = {nullptr, nullptr};  // (used under the busy flag only)
     hipError_t e = hipSuccess;
-    for (size_t off = 0; off < bytes && e == hipSuccess; off += g_stage.cap[0]) {
-        const size_t n = std::min(g_stage.cap[0], bytes - off);
-        e = hipMemcpyAsync(g_stage.buf[0], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e == hipSuccess) memcpy(static_cast<char*>(dst) + off, g_stage.buf[0], n);
+    const int nb = g_stage.buf[1] ? 2 : 1;
+    const size_t cap = nb == 2 ? std::min(g_stage.cap[0], g_stage.cap[1]) : g_stage.cap[0];
+    for (int b = 0; b < nb && e == hipSuccess; b++)
+        if (!ev[b]) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+    const size_t nch = (bytes + cap - 1) / cap;
+    auto out = [&](size_t k) {  // chunk k (its DMA recorded) -> the caller's buffer
+        const size_t off = k * cap, n = std::min(cap, bytes - off);
+        hipError_t r = hipEventSynchronize(ev[k % nb]);
+        if (r == hipSuccess) memcpy(static_cast<char*>(dst) + off, g_stage.buf[k % nb], n);
+        return r;
+    };
+    for (size_t k = 0; k < nch && e == hipSuccess; k++) {
+        const size_t off = k * cap, n = std::min(cap, bytes - off);
+        if (nb == 1 && k > 0) e = out(k - 1);  // (one chunk: drained before it is refilled)
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(g_stage.buf[k % nb], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(ev[k % nb], st);
+        if (e == hipSuccess && nb == 2 && k > 0) e = out(k - 1);
     }
+    if (e == hipSuccess && nch > 0) e = out(nch - 1);
     std::lock_guard<std::mutex> lk(g_stage.mu);
     g_stage.busy = false;
     return e;

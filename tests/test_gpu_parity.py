@@ -1671,3 +1671,30 @@ def test_add_all_matches_sequential_adds_and_stops_at_a_rejected_pulsar():
         assert len(s.layouts) == 1
     finally:
         s.close()
+
+
+@pytest.mark.gpu
+def test_large_reads_through_the_staging_chunks():
+    """A design-matrix read of several 16 MB staging chunks into pageable memory (the chunks
+    alternate, the last one partial) returns every instance's matrix bit for bit as a
+    one-instance read does."""
+    from pint_amd.engine import Session, build_layout, pack_table
+    model, toas = load("b1855")[:2]
+    outs = []
+    for ninst in (1, None):
+        s = Session(0)
+        try:
+            lay = s.add(build_layout(model, toas))
+            tab = pack_table(lay, model)
+            if ninst is None:  # enough instances for > 3 chunks
+                ninst = int(np.ceil(3.5 * (16 << 20) / (8 * lay.n * lay.K)))
+            s.set_instances_of(lay, np.tile(tab, (ninst, 1)))
+            s.eval(want_M=True)
+            M = s.read_designmatrix()
+            assert len(M) == ninst
+            outs.append(M)
+        finally:
+            s.close()
+    assert sum(m.nbytes for m in outs[1]) > 3 * (16 << 20)
+    for m in outs[1]:
+        np.testing.assert_array_equal(m, outs[0][0])
